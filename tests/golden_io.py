@@ -1,0 +1,105 @@
+"""Loader for the committed JM 18.5 golden fixtures (tests/golden/*.npz).
+
+A fixture holds the luma planes JM searched and, per integer-pel search, the
+inputs JM's IntPelME received and the (mv, cost) it returned.  See
+tests/golden/make_golden.py for how they were produced.
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLDEN = os.path.join(HERE, "golden")
+REPO = os.path.dirname(HERE)
+sys.path.insert(0, os.path.join(REPO, "--h.264-by-zhaodongyu_amd"))
+
+B_SLICE = 1  # JM lcommon/inc/types.h SliceType: P_SLICE 0, B_SLICE 1, I_SLICE 2
+
+
+def manifest() -> dict:
+    return json.load(open(os.path.join(GOLDEN, "manifest.json")))
+
+
+def cases() -> list[str]:
+    return sorted(manifest())
+
+
+class Case:
+    def __init__(self, name: str):
+        from jmme import synth
+        self.name = name
+        self.meta = manifest()[name]
+        z = np.load(os.path.join(GOLDEN, f"{name}.npz"))
+        self.r = {k[2:]: z[k] for k in z.files if k.startswith("r_")}
+        self.n = len(self.r["mode"])
+        cur_fn = z["cur_frame_no"]
+        ref_key = z["ref_key"]
+        if "cur" in z.files:
+            cur = z["cur"]
+            ref = z["ref"]
+        else:
+            m = self.meta
+            luma = synth.luma_sequence(m["w"], m["h"], m["frames"], seed=m["seed"], gmv=tuple(m["gmv"]),
+                                       adversarial=m["adversarial"])
+            hc, wc = (m["h"] + 15) // 16 * 16, (m["w"] + 15) // 16 * 16
+            orig = np.pad(luma, ((0, 0), (0, hc - m["h"]), (0, wc - m["w"])), mode="edge")
+            cur = orig[cur_fn]
+            ref = (orig[ref_key[:, 0] - 1 - ref_key[:, 2]].astype(np.int16)
+                   + z["ref_residual"].astype(np.int16)).astype(np.uint8)
+        for c, h in zip(cur, z["cur_md5"]):
+            if hashlib.md5(c.tobytes()).hexdigest() != str(h):
+                raise AssertionError(f"{name}: regenerated current frame does not match the fixture md5")
+        self.cur = {int(f): cur[i] for i, f in enumerate(cur_fn)}
+        self.ref = {(int(k[0]), int(k[1]), int(k[2])): ref[i] for i, k in enumerate(ref_key)}
+
+    def groups(self):
+        """Yield (frame_no, list, ref, index array) for each searched picture pair."""
+        r = self.r
+        keys = np.stack([r["frame_no"], r["list"], r["ref"]], 1)
+        uk = np.unique(keys, axis=0)
+        for f, l, rf in uk:
+            idx = np.nonzero((keys[:, 0] == f) & (keys[:, 1] == l) & (keys[:, 2] == rf))[0]
+            yield int(f), int(l), int(rf), idx
+
+    # ---- full search (SearchMode -1) ------------------------------------
+    def fs_check_for_00(self, idx):
+        r = self.r
+        return ((r["blocktype"][idx] == 1) & (r["rdopt"][idx] == 0) &
+                (r["slice_type"][idx] != B_SLICE) & (r["ref"][idx] == 0)).astype(np.int32)
+
+    def fs_search_range(self, idx):
+        # me_fullsearch.c:49  imin(max_x, max_y) >> 2
+        return (np.minimum(self.r["sr_max_x"][idx], self.r["sr_max_y"][idx]) >> 2).astype(np.int32)
+
+    def ffs_block_range(self, idx):
+        # me_fullfast.c:627  imax(max_x, max_y) >> 2
+        return (np.maximum(self.r["sr_max_x"][idx], self.r["sr_max_y"][idx]) >> 2).astype(np.int32)
+
+    def oracle_fs_req(self, idx):
+        r = self.r
+        cols = [r["pos_x"][idx], r["pos_y"][idx], r["bsx"][idx], r["bsy"][idx],
+                r["pred_x"][idx], r["pred_y"][idx], r["center_x"][idx], r["center_y"][idx],
+                self.fs_search_range(idx), r["lambda"][idx], self.fs_check_for_00(idx)]
+        return np.stack([np.asarray(c, np.int32) for c in cols], 1)
+
+    # ---- fast full search (SearchMode 0) ---------------------------------
+    def oracle_ffs_args(self, idx):
+        """Per-MB setup rows + per-block rows for oracle_lib.ffs_batch (one picture pair)."""
+        r = self.r
+        mbkey = np.stack([r["mb_addr"][idx], r["ffs_center_x"][idx], r["ffs_center_y"][idx]], 1)
+        # consecutive runs of the same MB (JM searches one MB at a time)
+        starts = np.r_[0, np.nonzero(np.any(mbkey[1:] != mbkey[:-1], axis=1))[0] + 1]
+        mb_index = np.cumsum(np.isin(np.arange(len(idx)), starts)) - 1
+        mbs = np.stack([r["pix_x"][idx][starts], r["pix_y"][idx][starts],
+                        r["ffs_center_x"][idx][starts], r["ffs_center_y"][idx][starts]], 1).astype(np.int32)
+        blk = np.stack([mb_index, r["blocktype"][idx], r["block_x"][idx], r["block_y"][idx],
+                        r["pred_x"][idx], r["pred_y"][idx], self.ffs_block_range(idx),
+                        r["lambda"][idx], r["ffs_pos00"][idx]], 1).astype(np.int32)
+        surf = int(r["ffs_max_range"][idx][0])
+        assert np.all(r["ffs_max_range"][idx] == surf)
+        return surf, int(r["max_mvd"][idx][0]), int(r["rdopt"][idx][0]), mbs, blk

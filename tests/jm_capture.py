@@ -1,0 +1,59 @@
+"""Reader for the binary log written by oracle/capture/jm_me_capture.c.
+
+Test infrastructure only: used by tests/golden/make_golden.py to turn a real
+JM 18.5 run into committed fixtures.  The record layout mirrors
+`struct cap_search` in jm_me_capture.c (packed, little endian).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+SEARCH_DTYPE = np.dtype([
+    ("mode", "<i4"), ("frame_no", "<i4"), ("mb_addr", "<i4"),
+    ("pix_x", "<i2"), ("pix_y", "<i2"),
+    ("blocktype", "<i2"), ("block_x", "<i2"), ("block_y", "<i2"),
+    ("pos_x", "<i2"), ("pos_y", "<i2"), ("bsx", "<i2"), ("bsy", "<i2"),
+    ("list", "<i2"), ("ref", "<i2"),
+    ("pred_x", "<i2"), ("pred_y", "<i2"), ("center_x", "<i2"), ("center_y", "<i2"),
+    ("sr_min_x", "<i4"), ("sr_max_x", "<i4"), ("sr_min_y", "<i4"), ("sr_max_y", "<i4"),
+    ("lambda", "<i4"), ("rdopt", "<i4"), ("slice_type", "<i4"),
+    ("min_mcost_in", "<i8"),
+    ("ffs_center_x", "<i2"), ("ffs_center_y", "<i2"),
+    ("ffs_max_range", "<i4"), ("ffs_pos00", "<i4"), ("max_mvd", "<i4"),
+    ("img_w", "<i4"), ("img_h", "<i4"),
+    ("out_mv_x", "<i2"), ("out_mv_y", "<i2"), ("out_cost", "<i8"),
+])
+TAG_PLANE = 0x304E4C50
+TAG_SEARCH = 0x30435253
+
+
+def read_capture(path: str):
+    """Return (planes, records).
+
+    planes: dict {(frame_no, kind, list, ref): uint16 [H, W]} (kind 0 = current
+    original, 1 = reference reconstruction as JM's imgY);
+    records: structured array of SEARCH_DTYPE in call order.
+    """
+    buf = open(path, "rb").read()
+    mv = memoryview(buf)
+    off = 0
+    planes = {}
+    recs = []
+    n = len(buf)
+    rsz = SEARCH_DTYPE.itemsize
+    while off < n:
+        tag = int.from_bytes(mv[off:off + 4], "little")
+        off += 4
+        if tag == TAG_PLANE:
+            hdr = np.frombuffer(mv[off:off + 24], dtype="<i4")
+            off += 24
+            frame_no, kind, lst, ref, w, h = (int(v) for v in hdr)
+            a = np.frombuffer(mv[off:off + 2 * w * h], dtype="<u2").reshape(h, w).copy()
+            off += 2 * w * h
+            planes[(frame_no, kind, lst, ref)] = a
+        elif tag == TAG_SEARCH:
+            recs.append(np.frombuffer(mv[off:off + rsz], dtype=SEARCH_DTYPE)[0])
+            off += rsz
+        else:
+            raise ValueError(f"bad tag {tag:#x} at {off - 4}")
+    return planes, np.array(recs, dtype=SEARCH_DTYPE)
