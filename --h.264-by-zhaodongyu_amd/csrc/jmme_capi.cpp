@@ -1,0 +1,490 @@
+// jmme_capi.cpp -- host side of libjmme.so: configuration (JM .cfg keys),
+// frame-buffer upload from JM's get_mem2Dpel layout, request validation and
+// kernel launch.  See include/jmme.h for the reference interfaces replaced.
+#include <hip/hip_runtime.h>
+
+#include <cctype>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "jmme.h"
+#include "jmme_common.h"
+#include "jmme_internal.h"
+
+using namespace jmme;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(const char *fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return -1;
+}
+
+#define HIPCHK(x)                                                                 \
+  do {                                                                            \
+    hipError_t e_ = (x);                                                          \
+    if (e_ != hipSuccess) return fail("%s: %s", #x, hipGetErrorString(e_));      \
+  } while (0)
+
+}  // namespace
+
+struct jmme_ctx {
+  jmme_config cfg;
+  int device = 0;
+  int max_mvd = 0;
+  int width = 0, height = 0, pitch = 0;
+  uint8_t *d_cur = nullptr;
+  uint8_t *d_refs[kMaxLists * kMaxRefs] = {};
+  const uint8_t **d_ref_table = nullptr;     // device copy of d_refs
+  bool ref_table_dirty = true;
+  std::vector<uint8_t> h_stage;              // u16 -> u8 conversion buffer
+  jmme_mb_req *d_req = nullptr;
+  jmme_block_res *d_out = nullptr;
+  size_t cap_units = 0;
+  unsigned *d_defer_count = nullptr;         // [0] defer count, [1] status
+  int *d_defer_list = nullptr;
+  size_t cap_defer = 0;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool timed = false;
+};
+
+// ----------------------------------------------------------------- config --
+extern "C" int jmme_config_default(jmme_config *c) {
+  if (!c) return fail("null config");
+  // defaults of JM's Map[] (JM/lencod/inc/configfile.h, column 4)
+  c->SourceWidth = 176;
+  c->SourceHeight = 144;
+  c->SearchMode = 0;
+  c->SearchRange = 16;
+  c->NumberReferenceFrames = 1;
+  c->DisableSubpelME = 0;
+  c->RDOptimization = 0;
+  c->MEDistortionFPel = 0;
+  c->MDDistortion = 2;
+  c->EPZSSubPelGrid = 0;
+  c->RestrictSearchRange = 2;
+  c->UseMVLimits = 0;
+  c->SetMVXLimit = 0;
+  c->SetMVYLimit = 0;
+  c->ChromaMEEnable = 0;
+  c->SourceBitDepthLuma = 8;
+  return 0;
+}
+
+namespace {
+
+int *cfg_field(jmme_config *c, const std::string &k) {
+  struct { const char *name; size_t off; } tab[] = {
+#define F(n) {#n, offsetof(jmme_config, n)}
+      F(SourceWidth), F(SourceHeight), F(SearchMode), F(SearchRange), F(NumberReferenceFrames),
+      F(DisableSubpelME), F(RDOptimization), F(MEDistortionFPel), F(MDDistortion), F(EPZSSubPelGrid),
+      F(RestrictSearchRange), F(UseMVLimits), F(SetMVXLimit), F(SetMVYLimit), F(ChromaMEEnable),
+      F(SourceBitDepthLuma),
+#undef F
+  };
+  for (auto &t : tab)
+    if (k == t.name) return reinterpret_cast<int *>(reinterpret_cast<char *>(c) + t.off);
+  return nullptr;
+}
+
+// One "Key = Value" assignment, JM syntax (ParseContent, configfile.c):
+// '#' starts a comment; values are numbers (ints, or doubles truncated by JM
+// for int params) or quoted strings (ignored here).
+int apply_assign(jmme_config *c, const std::string &key, const std::string &val) {
+  int *f = cfg_field(c, key);
+  if (!f) return 0;  // not an ME key: JM's Map has it, we do not need it
+  const char *s = val.c_str();
+  char *end = nullptr;
+  double d = strtod(s, &end);
+  if (end == s) return fail("config: bad value '%s' for %s", s, key.c_str());
+  *f = (int)d;
+  return 0;
+}
+
+int parse_text(jmme_config *c, const std::string &text) {
+  size_t i = 0, n = text.size();
+  std::vector<std::string> tok;
+  while (i < n) {
+    char ch = text[i];
+    if (ch == '#') {
+      while (i < n && text[i] != '\n') ++i;
+    } else if (isspace((unsigned char)ch)) {
+      ++i;
+    } else if (ch == '=') {
+      tok.push_back("=");
+      ++i;
+    } else if (ch == '"') {
+      size_t j = text.find('"', i + 1);
+      if (j == std::string::npos) return fail("config: unterminated string");
+      tok.push_back(text.substr(i, j - i + 1));
+      i = j + 1;
+    } else {
+      size_t j = i;
+      while (j < n && !isspace((unsigned char)text[j]) && text[j] != '=' && text[j] != '#') ++j;
+      tok.push_back(text.substr(i, j - i));
+      i = j;
+    }
+  }
+  for (size_t k = 0; k < tok.size();) {
+    if (k + 2 < tok.size() + 0 && tok[k + 1] == "=") {
+      if (apply_assign(c, tok[k], tok[k + 2])) return -1;
+      k += 3;
+    } else if (k + 1 < tok.size() && tok[k + 1] == "=") {
+      return fail("config: missing value for %s", tok[k].c_str());
+    } else {
+      ++k;
+    }
+  }
+  return 0;
+}
+
+}  // namespace
+
+extern "C" int jmme_config_parse(jmme_config *c, const char *path, int argc, const char *const *argv) {
+  if (!c) return fail("null config");
+  if (path) {
+    FILE *fp = fopen(path, "rb");
+    if (!fp) return fail("config: cannot open %s", path);
+    std::string text;
+    char buf[4096];
+    size_t r;
+    while ((r = fread(buf, 1, sizeof buf, fp)) > 0) text.append(buf, r);
+    fclose(fp);
+    if (parse_text(c, text)) return -1;
+  }
+  for (int i = 0; i < argc; ++i)
+    if (argv[i] && parse_text(c, argv[i])) return -1;
+  return 0;
+}
+
+extern "C" int jmme_max_mvd(const jmme_config *c) {
+  // init_motion_search_module, JM/lencod/src/mv_search.c:321-328
+  int sr = c->SearchRange;
+  int nsp = 4 * (2 * sr + 3);
+  int max_mv_bits = 3 + 2 * (int)ceil(log((double)(nsp + 1)) / log(2.0) + 1e-10);
+  int base = (1 << (max_mv_bits >> 1)) - 1;
+  if (c->UseMVLimits) {
+    int lim = 4 * (c->SetMVXLimit > c->SetMVYLimit ? c->SetMVXLimit : c->SetMVYLimit);
+    return lim > base ? lim : base;
+  }
+  return base;
+}
+
+// ---------------------------------------------------------------- context --
+extern "C" const char *jmme_last_error(void) { return g_err.c_str(); }
+extern "C" const char *jmme_version(void) { return "jmme 0.1 (gfx950)"; }
+
+extern "C" jmme_ctx *jmme_create(const jmme_config *cfg, int device) {
+  if (!cfg) { fail("null config"); return nullptr; }
+  if (cfg->ChromaMEEnable) { fail("ChromaMEEnable != 0 is not supported"); return nullptr; }
+  if (cfg->SourceBitDepthLuma != 8) { fail("only 8-bit luma is supported"); return nullptr; }
+  if (cfg->SearchRange < 0 || cfg->SearchRange > JMME_MAX_RANGE) {
+    fail("SearchRange %d outside [0,%d]", cfg->SearchRange, JMME_MAX_RANGE);
+    return nullptr;
+  }
+  auto *ctx = new jmme_ctx;
+  ctx->cfg = *cfg;
+  ctx->max_mvd = jmme_max_mvd(cfg);
+  hipError_t e;
+  if (device >= 0) {
+    e = hipSetDevice(device);
+    if (e != hipSuccess) { fail("hipSetDevice(%d): %s", device, hipGetErrorString(e)); delete ctx; return nullptr; }
+  }
+  (void)hipGetDevice(&ctx->device);
+  if ((e = hipMalloc(&ctx->d_ref_table, sizeof(uint8_t *) * kMaxLists * kMaxRefs)) != hipSuccess ||
+      (e = hipMalloc(&ctx->d_defer_count, 16)) != hipSuccess ||
+      (e = hipEventCreate(&ctx->ev0)) != hipSuccess || (e = hipEventCreate(&ctx->ev1)) != hipSuccess) {
+    fail("jmme_create: %s", hipGetErrorString(e));
+    jmme_destroy(ctx);
+    return nullptr;
+  }
+  return ctx;
+}
+
+extern "C" void jmme_destroy(jmme_ctx *ctx) {
+  if (!ctx) return;
+  (void)hipFree(ctx->d_cur);
+  for (auto *p : ctx->d_refs) (void)hipFree(p);
+  (void)hipFree(ctx->d_ref_table);
+  (void)hipFree(ctx->d_req);
+  (void)hipFree(ctx->d_out);
+  (void)hipFree(ctx->d_defer_count);
+  (void)hipFree(ctx->d_defer_list);
+  if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
+  if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+  delete ctx;
+}
+
+namespace {
+
+int set_geometry(jmme_ctx *ctx, int w, int h) {
+  if (w <= 0 || h <= 0 || (w & 15) || (h & 15))
+    return fail("picture %dx%d: width and height must be positive multiples of 16 (JM's coded size)", w, h);
+  if (ctx->width == w && ctx->height == h) return 0;
+  if (ctx->width) return fail("picture size changed from %dx%d to %dx%d", ctx->width, ctx->height, w, h);
+  ctx->width = w;
+  ctx->height = h;
+  ctx->pitch = (w + 63) & ~63;
+  return 0;
+}
+
+// JM get_mem2Dpel(_pad) planes: rows[y] equally spaced.  Converted to 8-bit.
+int upload_plane(jmme_ctx *ctx, uint8_t **dst, const jmme_imgpel *const *rows, int w, int h) {
+  if (!rows || !rows[0]) return fail("null plane");
+  if (set_geometry(ctx, w, h)) return -1;
+  ptrdiff_t stride = h > 1 ? rows[1] - rows[0] : w;
+  ctx->h_stage.resize((size_t)ctx->pitch * h);
+  for (int y = 0; y < h; ++y) {
+    const jmme_imgpel *src = rows[0] + (ptrdiff_t)y * stride;
+    if (rows[y] != src) return fail("plane rows are not equally spaced (row %d)", y);
+    uint8_t *d = &ctx->h_stage[(size_t)y * ctx->pitch];
+    unsigned m = 0;
+    for (int x = 0; x < w; ++x) { m |= src[x]; d[x] = (uint8_t)src[x]; }
+    if (m > 255) return fail("sample > 255 in row %d: only 8-bit luma is supported", y);
+  }
+  if (!*dst) HIPCHK(hipMalloc(dst, (size_t)ctx->pitch * h));
+  HIPCHK(hipMemcpy(*dst, ctx->h_stage.data(), (size_t)ctx->pitch * h, hipMemcpyHostToDevice));
+  return 0;
+}
+
+}  // namespace
+
+extern "C" int jmme_upload_cur(jmme_ctx *ctx, const jmme_imgpel *const *rows, int w, int h) {
+  if (!ctx) return fail("null ctx");
+  return upload_plane(ctx, &ctx->d_cur, rows, w, h);
+}
+
+extern "C" int jmme_upload_ref(jmme_ctx *ctx, int list, int ref_idx, const jmme_imgpel *const *rows, int w, int h) {
+  if (!ctx) return fail("null ctx");
+  if (list < 0 || list >= kMaxLists || ref_idx < 0 || ref_idx >= kMaxRefs)
+    return fail("list/ref_idx (%d,%d) out of range", list, ref_idx);
+  uint8_t **slot = &ctx->d_refs[list * kMaxRefs + ref_idx];
+  bool fresh = *slot == nullptr;
+  if (upload_plane(ctx, slot, rows, w, h)) return -1;
+  if (fresh) ctx->ref_table_dirty = true;
+  return 0;
+}
+
+// ----------------------------------------------------------------- search --
+extern "C" int jmme_slot(int bt, int bx, int by) { return slot_of(bt, bx, by); }
+extern "C" int jmme_spiral_index(int ox, int oy) { return spiral_index(ox, oy); }
+extern "C" void jmme_spiral_offset(int idx, int *ox, int *oy) { spiral_offset(idx, ox, oy); }
+extern "C" int jmme_mvbits(int v) { return mvbits(v); }
+
+namespace {
+
+int ensure_units(jmme_ctx *ctx, size_t n) {
+  if (n <= ctx->cap_units) return 0;
+  (void)hipFree(ctx->d_req);
+  (void)hipFree(ctx->d_out);
+  ctx->d_req = nullptr;
+  ctx->d_out = nullptr;
+  size_t cap = n < 1024 ? 1024 : n;
+  HIPCHK(hipMalloc(&ctx->d_req, cap * sizeof(jmme_mb_req)));
+  HIPCHK(hipMalloc(&ctx->d_out, cap * JMME_NSLOT * sizeof(jmme_block_res)));
+  ctx->cap_units = cap;
+  return 0;
+}
+
+int ensure_defer(jmme_ctx *ctx, size_t n) {
+  if (n <= ctx->cap_defer) return 0;
+  (void)hipFree(ctx->d_defer_list);
+  ctx->d_defer_list = nullptr;
+  size_t cap = n < 1024 ? 1024 : n;
+  HIPCHK(hipMalloc(&ctx->d_defer_list, cap * sizeof(int)));
+  ctx->cap_defer = cap;
+  return 0;
+}
+
+int sync_ref_table(jmme_ctx *ctx, hipStream_t s) {
+  if (!ctx->ref_table_dirty) return 0;
+  HIPCHK(hipMemcpyAsync(ctx->d_ref_table, ctx->d_refs, sizeof(ctx->d_refs), hipMemcpyHostToDevice, s));
+  HIPCHK(hipStreamSynchronize(s));
+  ctx->ref_table_dirty = false;
+  return 0;
+}
+
+int launch(jmme_ctx *ctx, int mode, const uint8_t *d_cur, const uint8_t *const *d_ref_table, int pitch,
+           int w, int h, const jmme_mb_req *d_req, int n, jmme_block_res *d_out, hipStream_t s) {
+  if (mode != JMME_FULL_SEARCH && mode != JMME_FAST_FULL_SEARCH)
+    return fail("search mode %d not supported by the batched engine (FS=-1, FFS=0)", mode);
+  if (n < 0) return fail("negative unit count");
+  if (n == 0) return 0;
+  if (ensure_defer(ctx, (size_t)n)) return -1;
+  KParams p{};
+  p.cur = d_cur;
+  p.refs = d_ref_table;
+  p.pitch = pitch;
+  p.width = w;
+  p.height = h;
+  p.req = d_req;
+  p.out = d_out;
+  p.n = n;
+  p.mode = mode;
+  p.max_mvd = ctx->max_mvd;
+  p.lds_range = ctx->cfg.SearchRange;
+  p.defer_count = ctx->d_defer_count;
+  p.defer_list = ctx->d_defer_list;
+  p.status = ctx->d_defer_count + 1;
+  const bool key32 = p.lds_range <= kKey32MaxRange;
+  HIPCHK(hipMemsetAsync(ctx->d_defer_count, 0, 16, s));
+  HIPCHK(hipEventRecord(ctx->ev0, s));
+  HIPCHK(launch_units(p, key32, n, s));
+  if (key32) {
+    // units whose every candidate saturated the 32-bit cost field (none in
+    // practice): redo with 64-bit keys; the grid drains the device list.
+    KParams q = p;
+    q.unit_list = ctx->d_defer_list;
+    q.unit_count = ctx->d_defer_count;
+    q.defer_count = nullptr;
+    HIPCHK(launch_units(q, false, 64, s));
+  }
+  HIPCHK(hipEventRecord(ctx->ev1, s));
+  ctx->timed = true;
+  return 0;
+}
+
+int check_status(jmme_ctx *ctx) {
+  unsigned st[2] = {0, 0};
+  HIPCHK(hipMemcpy(st, ctx->d_defer_count, sizeof st, hipMemcpyDeviceToHost));
+  if (st[1] & 1u) return fail("a request's search range exceeds the configured SearchRange %d", ctx->cfg.SearchRange);
+  if (st[1] & 2u) return fail("a full-search centre is not on the integer grid (EPZSSubPelGrid sub-pel centres are not supported)");
+  return 0;
+}
+
+int validate(const jmme_ctx *ctx, int mode, const jmme_mb_req *req, int n) {
+  for (int i = 0; i < n; ++i) {
+    const jmme_mb_req &r = req[i];
+    if (r.mb_x < 0 || r.mb_y < 0 || (r.mb_x & 15) || (r.mb_y & 15) || r.mb_x + 16 > ctx->width ||
+        r.mb_y + 16 > ctx->height)
+      return fail("unit %d: macroblock (%d,%d) outside the %dx%d picture", i, r.mb_x, r.mb_y, ctx->width, ctx->height);
+    if (r.list < 0 || r.list >= kMaxLists || r.ref_idx < 0 || r.ref_idx >= kMaxRefs ||
+        !ctx->d_refs[r.list * kMaxRefs + r.ref_idx])
+      return fail("unit %d: reference (%d,%d) not uploaded", i, r.list, r.ref_idx);
+    if (r.slot_mask >> JMME_NSLOT) return fail("unit %d: slot mask has bits above %d", i, JMME_NSLOT - 1);
+    if (mode == JMME_FAST_FULL_SEARCH) {
+      if (r.ffs_range < 0 || r.ffs_range > ctx->cfg.SearchRange)
+        return fail("unit %d: FFS range %d outside [0,%d]", i, r.ffs_range, ctx->cfg.SearchRange);
+      if ((r.ffs_center_x | r.ffs_center_y) & 3) return fail("unit %d: FFS centre not integer", i);
+    }
+    for (int s = 0; s < JMME_NSLOT; ++s) {
+      if (!((r.slot_mask >> s) & 1)) continue;
+      const jmme_block_req &b = r.blk[s];
+      if (b.lambda < 0) return fail("unit %d slot %d: negative lambda", i, s);
+      if (mode == JMME_FULL_SEARCH) {
+        if (b.search_range < 0 || b.search_range > ctx->cfg.SearchRange)
+          return fail("unit %d slot %d: range %d outside [0,%d]", i, s, b.search_range, ctx->cfg.SearchRange);
+        if ((b.center_x | b.center_y) & 3)
+          return fail("unit %d slot %d: sub-pel search centre (EPZSSubPelGrid) not supported", i, s);
+      } else if (b.search_range < 0 || b.search_range > r.ffs_range) {
+        return fail("unit %d slot %d: block range %d outside the FFS surface range %d", i, s, b.search_range, r.ffs_range);
+      }
+    }
+  }
+  return 0;
+}
+
+}  // namespace
+
+extern "C" int jmme_search_mbs(jmme_ctx *ctx, int mode, const jmme_mb_req *req, int n, jmme_block_res *out) {
+  if (!ctx) return fail("null ctx");
+  if (!ctx->d_cur) return fail("current picture not uploaded");
+  if (n == 0) return 0;
+  if (!req || !out) return fail("null request/result array");
+  if (validate(ctx, mode, req, n)) return -1;
+  if (ensure_units(ctx, (size_t)n)) return -1;
+  hipStream_t s = nullptr;
+  if (sync_ref_table(ctx, s)) return -1;
+  HIPCHK(hipMemcpyAsync(ctx->d_req, req, (size_t)n * sizeof(jmme_mb_req), hipMemcpyHostToDevice, s));
+  if (launch(ctx, mode, ctx->d_cur, ctx->d_ref_table, ctx->pitch, ctx->width, ctx->height, ctx->d_req, n,
+             ctx->d_out, s))
+    return -1;
+  // results for searched slots only: copy the whole block, then merge
+  std::vector<jmme_block_res> tmp((size_t)n * JMME_NSLOT);
+  HIPCHK(hipMemcpyAsync(tmp.data(), ctx->d_out, tmp.size() * sizeof(jmme_block_res), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (check_status(ctx)) return -1;
+  for (int i = 0; i < n; ++i)
+    for (int sl = 0; sl < JMME_NSLOT; ++sl)
+      if ((req[i].slot_mask >> sl) & 1) out[(size_t)i * JMME_NSLOT + sl] = tmp[(size_t)i * JMME_NSLOT + sl];
+  return 0;
+}
+
+extern "C" int jmme_search_mbs_async(jmme_ctx *ctx, int mode, const jmme_mb_req *d_req, int n,
+                                     jmme_block_res *d_out, void *stream) {
+  if (!ctx) return fail("null ctx");
+  if (!ctx->d_cur) return fail("current picture not uploaded");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (sync_ref_table(ctx, s)) return -1;
+  return launch(ctx, mode, ctx->d_cur, ctx->d_ref_table, ctx->pitch, ctx->width, ctx->height, d_req, n, d_out, s);
+}
+
+extern "C" int jmme_search_mbs_planes_async(jmme_ctx *ctx, int mode, const uint8_t *d_cur, const uint8_t *d_ref,
+                                            int pitch, int w, int h, const jmme_mb_req *d_req, int n,
+                                            jmme_block_res *d_out, void *stream) {
+  if (!ctx) return fail("null ctx");
+  if (!d_cur || !d_ref) return fail("null plane");
+  if (pitch < w || (pitch & 3) || (w & 15) || (h & 15)) return fail("bad plane geometry %dx%d pitch %d", w, h, pitch);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  // every (list, ref) of this call reads the one given plane
+  std::vector<const uint8_t *> tab(kMaxLists * kMaxRefs, d_ref);
+  HIPCHK(hipMemcpyAsync(ctx->d_ref_table, tab.data(), tab.size() * sizeof(void *), hipMemcpyHostToDevice, s));
+  ctx->ref_table_dirty = true;
+  return launch(ctx, mode, d_cur, ctx->d_ref_table, pitch, w, h, d_req, n, d_out, s);
+}
+
+extern "C" float jmme_last_kernel_ms(jmme_ctx *ctx) {
+  if (!ctx || !ctx->timed) return -1.0f;
+  float ms = -1.0f;
+  if (hipEventSynchronize(ctx->ev1) != hipSuccess) return -1.0f;
+  if (hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1) != hipSuccess) return -1.0f;
+  return ms;
+}
+
+extern "C" jmme_distblk jmme_full_search_block(jmme_ctx *ctx, int list, int ref_idx, int pos_x, int pos_y,
+                                               int blocktype, const jmme_mv *pred_mv, jmme_mv *mv_inout,
+                                               jmme_distblk min_mcost, int lambda_factor, int search_range,
+                                               int check_for_00) {
+  // IntPelME-signature drop-in: one partition as a one-slot unit.  JM's
+  // error() semantics on failure (print, exit 500).
+  int mb_x = pos_x & ~15, mb_y = pos_y & ~15;
+  int s = slot_of(blocktype, (pos_x - mb_x) >> 2, (pos_y - mb_y) >> 2);
+  jmme_mb_req r;
+  memset(&r, 0, sizeof r);
+  r.mb_x = (int16_t)mb_x;
+  r.mb_y = (int16_t)mb_y;
+  r.list = (int16_t)list;
+  r.ref_idx = (int16_t)ref_idx;
+  if (s < 0) { fprintf(stderr, "jmme_full_search_block: bad block\n"); exit(500); }
+  r.slot_mask = 1ull << s;
+  r.blk[s].pred_x = pred_mv->mv_x;
+  r.blk[s].pred_y = pred_mv->mv_y;
+  r.blk[s].center_x = mv_inout->mv_x;
+  r.blk[s].center_y = mv_inout->mv_y;
+  r.blk[s].search_range = (int16_t)search_range;
+  r.blk[s].flags = (int16_t)(check_for_00 ? JMME_BLK_CHECK00 : 0);
+  r.blk[s].lambda = lambda_factor;
+  jmme_block_res out[JMME_NSLOT];
+  if (jmme_search_mbs(ctx, JMME_FULL_SEARCH, &r, 1, out)) {
+    fprintf(stderr, "jmme_full_search_block: %s\n", jmme_last_error());
+    exit(500);
+  }
+  // JM's min_mcost argument is DISTBLK_MAX from BlockMotionSearch (mv_search.c:878);
+  // a smaller incoming bound only matters when nothing beats it.
+  if (out[s].cost >= min_mcost) return min_mcost;
+  mv_inout->mv_x = out[s].mv_x;
+  mv_inout->mv_y = out[s].mv_y;
+  return out[s].cost;
+}

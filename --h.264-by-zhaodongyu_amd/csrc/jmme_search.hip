@@ -1,0 +1,422 @@
+// jmme_search.hip -- gfx950 kernels for JM 18.5 integer-pel full search (FS)
+// and fast full search (FFS), one workgroup per macroblock x reference unit.
+//
+// Semantics restated from JM 18.5 (JM = /root/reference/4.对比程序/jm18.5/JM):
+//   FS   full_search_motion_estimation   JM/lencod/src/me_fullsearch.c:39-103
+//        computeSAD (luma)               JM/lencod/src/me_distortion.c:349-426
+//   FFS  setup_fast_full_search          JM/lencod/src/me_fullfast.c:269-608
+//        update_full_search_large_blocks JM/lencod/src/me_fullfast.c:196-260
+//        fast_full_search_motion_est.    JM/lencod/src/me_fullfast.c:618-689
+//   mv_cost (JCOST_CALC_SCALEUP)         JM/lencod/inc/mv_search.h:100-104
+//   UMVLine4X reference clamp            JM/lencod/inc/refbuf.h:22-26
+//
+// Exactness argument.  JM walks the spiral with strict '<' and an early-exit
+// SAD that returns the threshold when it exits (me_distortion.c:384-385), so
+// the result is the lexicographic minimum of (cost, spiral index) over all
+// eligible candidates.  We evaluate every candidate exhaustively and reduce
+// that key; no early exit, same answer.
+//
+// Work mapping (one workgroup = one MB x ref unit, 256 threads):
+//   * partitions are grouped by identical search window (FS: centre + range;
+//     FFS: the MB's single surface); each group stages its reference window
+//     (2R+16)^2 pels from HBM into LDS once, as "word[y][x] = pels x..x+3" so
+//     every SAD row read is an aligned ds_read_b32;
+//   * each thread takes search positions; for one position it forms the 16
+//     4x4 SADs with v_sad_u8 (4 abs-diffs per lane-op; the current MB row is a
+//     broadcast ds_read_b128), sums them to the 41 partition SADs and updates
+//     a running (cost, rank) minimum per partition in registers;
+//   * partitions that share a predictor share the mv-cost arithmetic;
+//   * at the end a wave shuffle + LDS reduction produces the 41 results.
+#include <hip/hip_runtime.h>
+#include "jmme.h"
+#include "jmme_common.h"
+#include "jmme_internal.h"
+
+namespace jmme {
+
+namespace {
+
+constexpr int kNS = JMME_NSLOT;
+constexpr int kWaves = kWG / 64;
+constexpr uint32_t kSat32 = (1u << 19) - 1;   // saturated cost field of a 32-bit key
+constexpr int kKey32First = 9;
+#ifndef JMME_WAVES_PER_EU
+#define JMME_WAVES_PER_EU 2
+#endif                 // slots 9..40 (8x4, 4x8, 4x4) use 32-bit keys
+
+struct Lds {
+  int wp;        // words per window row
+  int rawp;      // bytes per raw row
+  int rows;      // window rows
+  uint32_t *words;
+  uint8_t *raw;
+  uint32_t *cur;          // 64 words: row r, column group c at [r*4+c]
+  int4 *slot;             // 41 x jmme_block_req
+  unsigned long long *grp;  // per slot: mask of slots sharing its window
+  unsigned long long *cls;  // per slot: mask of slots sharing its predictor/lambda
+  unsigned long long *red;  // kWaves x 41 reduction scratch
+  int *flag;                // unit must be redone with 64-bit keys
+};
+
+__device__ __forceinline__ Lds carve(unsigned char *smem, int R) {
+  Lds L;
+  L.rows = 2 * R + 16;
+  L.wp = (2 * R + 13) | 1;
+  L.rawp = ((2 * R + 16 + 4) + 3) & ~3;
+  size_t off = 0;
+  L.words = reinterpret_cast<uint32_t *>(smem + off); off += (size_t)L.rows * L.wp * 4;
+  off = (off + 15) & ~(size_t)15;
+  L.raw = smem + off;                                    off += (size_t)L.rows * L.rawp;
+  off = (off + 15) & ~(size_t)15;
+  L.cur = reinterpret_cast<uint32_t *>(smem + off);      off += 64 * 4;
+  L.slot = reinterpret_cast<int4 *>(smem + off);         off += kNS * 16;
+  L.grp = reinterpret_cast<unsigned long long *>(smem + off); off += kNS * 8;
+  L.cls = reinterpret_cast<unsigned long long *>(smem + off); off += kNS * 8;
+  L.red = reinterpret_cast<unsigned long long *>(smem + off); off += kWaves * kNS * 8;
+  L.flag = reinterpret_cast<int *>(smem + off);            off += 16;
+  return L;
+}
+
+__device__ __forceinline__ int ufl(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ unsigned long long ufl64(unsigned long long v) {
+  unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
+  unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+  return ((unsigned long long)hi << 32) | lo;
+}
+
+__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+// slot request fields from the int4 image of jmme_block_req
+__device__ __forceinline__ int rq_pred_x(int4 q) { return (int)(short)(q.x & 0xffff); }
+__device__ __forceinline__ int rq_pred_y(int4 q) { return (int)(short)((unsigned)q.x >> 16); }
+__device__ __forceinline__ int rq_cen_x(int4 q) { return (int)(short)(q.y & 0xffff); }
+__device__ __forceinline__ int rq_cen_y(int4 q) { return (int)(short)((unsigned)q.y >> 16); }
+__device__ __forceinline__ int rq_range(int4 q) { return (int)(short)(q.z & 0xffff); }
+__device__ __forceinline__ int rq_flags(int4 q) { return (int)(short)((unsigned)q.z >> 16); }
+__device__ __forceinline__ int rq_lambda(int4 q) { return q.w; }
+
+// bijective XCD-aware remap: blocks are dealt round-robin to the 8 XCDs, so
+// give each XCD a contiguous run of units (neighbouring macroblocks read
+// overlapping reference windows, which then hit that XCD's L2).
+__device__ __forceinline__ int xcd_unit(int b, int nb) {
+  const int nx = 8;
+  int q = nb / nx, r = nb % nx, x = b % nx;
+  return x * q + (x < r ? x : r) + b / nx;
+}
+
+template <bool KEY32, bool FFS>
+__device__ __forceinline__ void unit_body(const KParams &p, int u, unsigned char *smem) {
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  constexpr bool ffs = FFS;
+
+  const jmme_mb_req *rq = p.req + u;
+  const int mb_x = ufl(rq->mb_x);
+  const int mb_y = ufl(rq->mb_y);
+  const int list = ufl(rq->list);
+  const int ref_idx = ufl(rq->ref_idx);
+  const unsigned long long slot_mask = ufl64(rq->slot_mask) & ((1ull << kNS) - 1);
+  const int ffs_cx = ufl(rq->ffs_center_x);
+  const int ffs_cy = ufl(rq->ffs_center_y);
+  const int ffs_range = ufl(rq->ffs_range);
+  const bool preseed = ffs && ufl(rq->ffs_pos00_valid) != 0;
+  const uint8_t *ref = p.refs[list * kMaxRefs + ref_idx];
+
+  Lds L = carve(smem, p.lds_range);
+
+  // ---- unit setup: slot requests, window groups, predictor classes, current MB
+  if (tid < kNS) {
+    const int4 *src = reinterpret_cast<const int4 *>(&rq->blk[0]);
+    L.slot[tid] = src[tid];
+  }
+  if (tid >= 64 && tid < 128) {
+    int t = tid - 64, r = t >> 2, c = t & 3;
+    L.cur[t] = *reinterpret_cast<const uint32_t *>(p.cur + (size_t)(mb_y + r) * p.pitch + mb_x + 4 * c);
+  }
+  __syncthreads();
+  if (tid < kNS) {
+    int4 me = L.slot[tid];
+    unsigned long long g = 0, c = 0;
+    if ((slot_mask >> tid) & 1) {
+      for (int t = 0; t < kNS; ++t) {
+        if (!((slot_mask >> t) & 1)) continue;
+        int4 o = L.slot[t];
+        bool same_win = ffs || (o.y == me.y && rq_range(o) == rq_range(me));
+        bool same_cls = same_win && o.x == me.x && o.w == me.w;
+        g |= (unsigned long long)same_win << t;
+        c |= (unsigned long long)same_cls << t;
+      }
+    }
+    L.grp[tid] = g;
+    L.cls[tid] = c;
+  }
+  if (tid == 0) L.flag[0] = 0;
+  __syncthreads();
+
+  // per-thread running minima of the (cost, rank) keys
+  unsigned long long best64[KEY32 ? kKey32First : kNS];
+  uint32_t best32[KEY32 ? kNS - kKey32First : 1];
+#pragma unroll
+  for (int s = 0; s < (KEY32 ? kKey32First : kNS); ++s) best64[s] = ~0ull;
+#pragma unroll
+  for (int s = 0; s < (KEY32 ? kNS - kKey32First : 1); ++s) best32[s] = ~0u;
+
+  unsigned long long remaining = slot_mask;
+  while (remaining) {
+    const int lead = __builtin_ctzll(remaining);
+    const unsigned long long gmask = ufl64(L.grp[lead]) & remaining;
+    remaining &= ~gmask;
+    const int4 lq = L.slot[lead];
+    const int cqx = ufl(ffs ? ffs_cx : rq_cen_x(lq));   // window centre, qpel (multiple of 4)
+    const int cqy = ufl(ffs ? ffs_cy : rq_cen_y(lq));
+    const int R = ufl(ffs ? ffs_range : rq_range(lq));
+    if (R < 0 || R > p.lds_range || ((cqx | cqy) & 3)) {
+      // outside what this launch was sized for (or a sub-pel-grid centre):
+      // refuse loudly instead of overrunning LDS; the host reports it
+      if (tid == 0) atomicOr(p.status, (R < 0 || R > p.lds_range) ? 1u : 2u);
+      continue;
+    }
+    // FFS: partitions searched over a smaller range than the surface (me_fullfast.c:627)
+    unsigned long long rlim = 0;
+    if (ffs) {
+      for (int t = 0; t < kNS; ++t)
+        if ((gmask >> t) & 1) rlim |= (unsigned long long)(rq_range(L.slot[t]) < R) << t;
+      rlim = ufl64(rlim);
+    }
+    const int chk00 = ufl((!ffs && (gmask & 1)) ? (rq_flags(L.slot[0]) & JMME_BLK_CHECK00) : 0);
+
+    // ---- stage the (2R+16)^2 reference window, clamped like UMVLine4X
+    const int x0 = mb_x + (cqx >> 2) - R;
+    const int y0 = mb_y + (cqy >> 2) - R;
+    const int wcols = 2 * R + 16;
+    const int wrows = 2 * R + 16;
+    __syncthreads();   // previous group's readers are done with the window
+    for (int i = tid; i < wrows * L.rawp; i += kWG) {
+      int r = i / L.rawp, c = i - r * L.rawp;
+      int gy = clampi(y0 + r, 0, p.height - 1);
+      int gx = clampi(x0 + (c < wcols ? c : wcols - 1), 0, p.width - 1);
+      L.raw[i] = ref[(size_t)gy * p.pitch + gx];
+    }
+    __syncthreads();
+    const int wpr = 2 * R + 13;
+    for (int i = tid; i < wrows * wpr; i += kWG) {
+      int r = i / wpr, c = i - r * wpr;
+      const uint32_t *rw = reinterpret_cast<const uint32_t *>(L.raw + (size_t)r * L.rawp);
+      uint32_t lo = rw[c >> 2], hi = rw[(c >> 2) + 1];
+      L.words[r * L.wp + c] = __builtin_amdgcn_alignbyte(hi, lo, c & 3);
+    }
+    __syncthreads();
+
+    // ---- sweep all (2R+1)^2 positions of the window
+    const int D = 2 * R + 1;
+    const int NP = D * D;
+    for (int pos = tid; pos < NP; pos += kWG) {
+      // opaque zero: keeps the 16 broadcast reads of the current MB inside the
+      // loop instead of letting LICM pin 64 VGPRs for them
+      int zero;
+      asm volatile("v_mov_b32 %0, 0" : "=v"(zero));
+      const uint4 *cur4 = reinterpret_cast<const uint4 *>(L.cur) + zero;
+      const int oyw = pos / D;
+      const int oxw = pos - oyw * D;
+      uint32_t a[16];
+      const uint32_t *wrow = L.words + oyw * L.wp + oxw;
+#pragma unroll
+      for (int by = 0; by < 4; ++by) {
+        uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+        // rows are not unrolled: bounds the loads in flight (VGPR budget)
+#pragma unroll 1
+        for (int r = 0; r < 4; ++r) {
+          const int i = by * 4 + r;
+          const uint4 c = cur4[i];
+          const uint32_t *w = wrow + i * L.wp;
+          s0 = __builtin_amdgcn_sad_u8(w[0], c.x, s0);
+          s1 = __builtin_amdgcn_sad_u8(w[4], c.y, s1);
+          s2 = __builtin_amdgcn_sad_u8(w[8], c.z, s2);
+          s3 = __builtin_amdgcn_sad_u8(w[12], c.w, s3);
+        }
+        // costs are SAD<<5 (dist_scale, JCOST_CALC_SCALEUP): scale once here
+        a[by * 4 + 0] = s0 << 5;
+        a[by * 4 + 1] = s1 << 5;
+        a[by * 4 + 2] = s2 << 5;
+        a[by * 4 + 3] = s3 << 5;
+      }
+      // partition SADs (update_full_search_large_blocks order does not
+      // matter: integer sums)
+      uint32_t ps[kNS];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) ps[25 + k] = a[k];                       // 4x4
+#pragma unroll
+      for (int by = 0; by < 4; ++by)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) ps[9 + by * 2 + h] = a[by * 4 + 2 * h] + a[by * 4 + 2 * h + 1];  // 8x4
+#pragma unroll
+      for (int v = 0; v < 2; ++v)
+#pragma unroll
+        for (int bx = 0; bx < 4; ++bx) ps[17 + v * 4 + bx] = a[(2 * v) * 4 + bx] + a[(2 * v + 1) * 4 + bx];  // 4x8
+#pragma unroll
+      for (int v = 0; v < 2; ++v)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) ps[5 + v * 2 + h] = ps[9 + (2 * v) * 2 + h] + ps[9 + (2 * v + 1) * 2 + h];  // 8x8
+      ps[3] = ps[5] + ps[7];
+      ps[4] = ps[6] + ps[8];   // 8x16
+      ps[1] = ps[5] + ps[6];
+      ps[2] = ps[7] + ps[8];   // 16x8
+      ps[0] = ps[1] + ps[2];   // 16x16
+
+      const int ox = oxw - R, oy = oyw - R;
+      const int lring = max(abs(ox), abs(oy));
+      const int sidx = spiral_index(ox, oy);
+      const int candx = cqx + 4 * ox;   // candidate MV (qpel, relative to the block)
+      const int candy = cqy + 4 * oy;
+      const bool is00 = (candx == 0) && (candy == 0);
+      const uint32_t rank = ffs ? ((preseed && is00) ? 0u : (uint32_t)sidx + 1u) : (uint32_t)sidx;
+
+      unsigned long long cm = gmask;
+      while (cm) {
+        const int cl = __builtin_ctzll(cm);
+        const unsigned long long cmask = ufl64(L.cls[cl]) & cm;
+        cm &= ~cmask;
+        const int4 cq = L.slot[cl];
+        const int px = ufl(rq_pred_x(cq));
+        const int py = ufl(rq_pred_y(cq));
+        const int lam = ufl(rq_lambda(cq));
+        const int dx = candx - px, dy = candy - py;
+        const uint32_t mvc = (uint32_t)lam * (uint32_t)(mvbits(dx) + mvbits(dy));
+        bool ok = true;
+        if (ffs) ok = max(abs(dx), abs(dy)) < p.max_mvd - 1;   // GetMaxMVD gate, me_fullfast.c:663
+#pragma unroll
+        for (int s = 0; s < kNS; ++s) {
+          if (!((cmask >> s) & 1)) continue;
+          uint32_t m = mvc;
+          if (s == 0 && chk00) {
+            const uint32_t t = 16u * (uint32_t)lam;           // weighted_cost(lambda,16)
+            if (is00) m = m > t ? m - t : 0u;
+          }
+          bool oks = ok;
+          if (ffs && ((rlim >> s) & 1)) {
+            const int rs = ufl(rq_range(L.slot[s]));
+            oks = oks && (lring <= rs || (preseed && is00));
+          }
+          const uint32_t cost = ps[s] + m;
+          if (KEY32 && s >= kKey32First) {
+            const uint32_t k = oks ? ((min(cost, kSat32) << 13) | rank) : ~0u;
+            best32[s - kKey32First] = min(best32[s - kKey32First], k);
+          } else {
+            const unsigned long long k = oks ? (((unsigned long long)cost << 32) | rank) : ~0ull;
+            best64[s] = best64[s] < k ? best64[s] : k;
+          }
+        }
+      }
+    }
+  }
+
+  // ---- workgroup reduction of the per-thread minima
+#pragma unroll
+  for (int s = 0; s < kNS; ++s) {
+    if (!((slot_mask >> s) & 1)) continue;
+    unsigned long long k;
+    if (KEY32 && s >= kKey32First) {
+      uint32_t v = best32[s - kKey32First];
+      k = (v == ~0u) ? ~0ull : ((((unsigned long long)(v >> 13)) << 32) | (v & 8191u) |
+                                 (((v >> 13) == kSat32) ? (1ull << 31) : 0ull));
+    } else {
+      k = best64[s];
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      unsigned lo = __shfl_xor((unsigned)k, off, 64);
+      unsigned hi = __shfl_xor((unsigned)(k >> 32), off, 64);
+      unsigned long long o = ((unsigned long long)hi << 32) | lo;
+      k = o < k ? o : k;
+    }
+    if (lane == 0) L.red[wave * kNS + s] = k;
+  }
+  __syncthreads();
+  if (tid < kNS && ((slot_mask >> tid) & 1)) {
+    unsigned long long k = L.red[tid];
+#pragma unroll
+    for (int w = 1; w < kWaves; ++w) { unsigned long long o = L.red[w * kNS + tid]; k = o < k ? o : k; }
+    const int4 q = L.slot[tid];
+    const int cx = ffs ? ffs_cx : rq_cen_x(q);
+    const int cy = ffs ? ffs_cy : rq_cen_y(q);
+    jmme_block_res res;
+    res.reserved = 0;
+    if (k == ~0ull) {
+      // nothing eligible: JM leaves best_pos = 0 and returns the incoming min_mcost
+      res.mv_x = (int16_t)cx; res.mv_y = (int16_t)cy; res.cost = JMME_DISTBLK_MAX;
+    } else {
+      if (KEY32 && tid >= kKey32First && (k & (1ull << 31))) {
+        // every candidate saturated the 32-bit cost field: this unit is redone
+        // with 64-bit keys by the deferred pass (which overwrites all slots)
+        L.flag[0] = 1;
+      }
+      const uint32_t rank = (uint32_t)(k & 0x7fffffffu);
+      int sidx = ffs ? (int)rank - 1 : (int)rank;
+      int ox, oy;
+      if (ffs && rank == 0) { ox = -(cx >> 2); oy = -(cy >> 2); }   // the pre-seeded (0,0)
+      else spiral_offset(sidx, &ox, &oy);
+      res.mv_x = (int16_t)(cx + 4 * ox);
+      res.mv_y = (int16_t)(cy + 4 * oy);
+      res.cost = (int64_t)(k >> 32);
+    }
+    p.out[(size_t)u * kNS + tid] = res;
+  }
+  if (KEY32) {
+    __syncthreads();
+    if (tid == 0 && L.flag[0]) p.defer_list[atomicAdd(p.defer_count, 1u)] = u;
+  }
+}
+
+// direct pass: one workgroup per unit (XCD-aware order)
+template <bool KEY32, bool FFS>
+__global__ __launch_bounds__(kWG, JMME_WAVES_PER_EU) void me_units_kernel(KParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int u = xcd_unit(blockIdx.x, gridDim.x);
+  if (u >= p.n) return;
+  unit_body<KEY32, FFS>(p, u, smem);
+}
+
+// deferred pass (64-bit keys): a small grid drains the device-side list of
+// units whose 32-bit keys saturated; every workgroup exits when the list ends
+template <bool FFS>
+__global__ __launch_bounds__(kWG, 1) void me_units_deferred_kernel(KParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const unsigned cnt = *p.unit_count;
+  for (unsigned i = blockIdx.x; i < cnt; i += gridDim.x) {
+    unit_body<false, FFS>(p, p.unit_list[i], smem);
+    __syncthreads();
+  }
+}
+
+}  // namespace
+
+size_t units_lds_bytes(int R) {
+  const int rows = 2 * R + 16;
+  const int wp = (2 * R + 13) | 1;
+  const int rawp = ((2 * R + 16 + 4) + 3) & ~3;
+  size_t off = (size_t)rows * wp * 4;
+  off = (off + 15) & ~(size_t)15;
+  off += (size_t)rows * rawp;
+  off = (off + 15) & ~(size_t)15;
+  off += 64 * 4 + kNS * 16 + 2 * kNS * 8 + kWaves * kNS * 8 + 16;
+  return off;
+}
+
+hipError_t launch_units(const KParams &p, bool key32, int grid, hipStream_t s) {
+  const size_t lds = units_lds_bytes(p.lds_range);
+  const bool ffs = p.mode == JMME_FAST_FULL_SEARCH;
+  if (p.unit_list) {
+    if (ffs) hipLaunchKernelGGL(me_units_deferred_kernel<true>, dim3(grid), dim3(kWG), lds, s, p);
+    else hipLaunchKernelGGL(me_units_deferred_kernel<false>, dim3(grid), dim3(kWG), lds, s, p);
+  } else if (key32) {
+    if (ffs) hipLaunchKernelGGL((me_units_kernel<true, true>), dim3(grid), dim3(kWG), lds, s, p);
+    else hipLaunchKernelGGL((me_units_kernel<true, false>), dim3(grid), dim3(kWG), lds, s, p);
+  } else {
+    if (ffs) hipLaunchKernelGGL((me_units_kernel<false, true>), dim3(grid), dim3(kWG), lds, s, p);
+    else hipLaunchKernelGGL((me_units_kernel<false, false>), dim3(grid), dim3(kWG), lds, s, p);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace jmme

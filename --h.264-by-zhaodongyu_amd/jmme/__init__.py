@@ -1,0 +1,9 @@
+"""jmme -- MI355X-native JM 18.5 integer-pel motion estimation (host side).
+
+Mirrors the JM 18.5 lencod ME interface (encoder.cfg keys, get_mem2Dpel frame
+buffers, the IntPelME search contract) over the C ABI of libjmme.so
+(include/jmme.h).  See DESIGN.md.
+"""
+from ._lib import (BLK_CHECK00, BLOCK_REQ, BLOCK_RES, DISTBLK_MAX, FAST_FULL_SEARCH,  # noqa: F401
+                   FULL_SEARCH, MB_REQ, NSLOT, JmmeError)
+from .engine import MotionEstimator, config_from_cfg, slot_of, spiral  # noqa: F401

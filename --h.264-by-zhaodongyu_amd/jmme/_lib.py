@@ -1,0 +1,98 @@
+"""ctypes binding of libjmme.so (the C ABI declared in include/jmme.h).
+
+The product path: every search call below runs the HIP kernels in libjmme.so.
+There is no CPU fallback -- if the library is missing this module raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libjmme.so")
+
+NSLOT = 41
+DISTBLK_MAX = 0x7FFFFFFF << 5
+FULL_SEARCH = -1
+FAST_FULL_SEARCH = 0
+BLK_CHECK00 = 1
+
+BLOCK_REQ = np.dtype([("pred_x", "<i2"), ("pred_y", "<i2"), ("center_x", "<i2"), ("center_y", "<i2"),
+                      ("search_range", "<i2"), ("flags", "<i2"), ("lambda", "<i4")])
+MB_REQ = np.dtype([("mb_x", "<i2"), ("mb_y", "<i2"), ("list", "<i2"), ("ref_idx", "<i2"),
+                   ("slot_mask", "<u8"),
+                   ("ffs_center_x", "<i2"), ("ffs_center_y", "<i2"), ("ffs_range", "<i2"),
+                   ("ffs_pos00_valid", "<i2"), ("reserved", "<i2", (4,)),
+                   ("blk", BLOCK_REQ, (NSLOT,))])
+BLOCK_RES = np.dtype([("mv_x", "<i2"), ("mv_y", "<i2"), ("reserved", "<i4"), ("cost", "<i8")])
+assert BLOCK_REQ.itemsize == 16 and MB_REQ.itemsize == 688 and BLOCK_RES.itemsize == 16
+
+CONFIG_FIELDS = ["SourceWidth", "SourceHeight", "SearchMode", "SearchRange", "NumberReferenceFrames",
+                 "DisableSubpelME", "RDOptimization", "MEDistortionFPel", "MDDistortion", "EPZSSubPelGrid",
+                 "RestrictSearchRange", "UseMVLimits", "SetMVXLimit", "SetMVYLimit", "ChromaMEEnable",
+                 "SourceBitDepthLuma"]
+
+
+class JmmeConfig(ctypes.Structure):
+    _fields_ = [(f, ctypes.c_int) for f in CONFIG_FIELDS]
+
+    def as_dict(self) -> dict:
+        return {f: getattr(self, f) for f in CONFIG_FIELDS}
+
+
+class JmmeMv(ctypes.Structure):
+    _fields_ = [("mv_x", ctypes.c_int16), ("mv_y", ctypes.c_int16)]
+
+
+class JmmeError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise JmmeError(f"{LIB_PATH} not built: run __graft_entry__.build() (make -C <pkg>)")
+    L = ctypes.CDLL(LIB_PATH)
+    P, I, V = ctypes.c_void_p, ctypes.c_int, None
+    sig = {
+        "jmme_config_default": (I, [P]),
+        "jmme_config_parse": (I, [P, ctypes.c_char_p, I, P]),
+        "jmme_max_mvd": (I, [P]),
+        "jmme_create": (P, [P, I]),
+        "jmme_destroy": (V, [P]),
+        "jmme_last_error": (ctypes.c_char_p, []),
+        "jmme_version": (ctypes.c_char_p, []),
+        "jmme_upload_cur": (I, [P, P, I, I]),
+        "jmme_upload_ref": (I, [P, I, I, P, I, I]),
+        "jmme_slot": (I, [I, I, I]),
+        "jmme_search_mbs": (I, [P, I, P, I, P]),
+        "jmme_search_mbs_async": (I, [P, I, P, I, P, P]),
+        "jmme_search_mbs_planes_async": (I, [P, I, P, P, I, I, I, P, I, P, P]),
+        "jmme_full_search_block": (ctypes.c_int64, [P, I, I, I, I, I, P, P, ctypes.c_int64, I, I, I]),
+        "jmme_last_kernel_ms": (ctypes.c_float, [P]),
+        "jmme_spiral_index": (I, [I, I]),
+        "jmme_spiral_offset": (V, [I, P, P]),
+        "jmme_mvbits": (I, [I]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def check(status: int) -> None:
+    if status != 0:
+        raise JmmeError(lib().jmme_last_error().decode())
+
+
+def ptr(a: np.ndarray) -> ctypes.c_void_p:
+    return a.ctypes.data_as(ctypes.c_void_p)

@@ -1,0 +1,127 @@
+"""Host mirror of JM 18.5's integer-pel ME entry points over libjmme.so.
+
+JM 18.5 (JM = /root/reference/4.对比程序/jm18.5/JM) reference points:
+  * config keys / -d file -p k=v   JM/lencod/src/configfile.c:314 (Configure)
+  * frame buffers                  get_mem2Dpel JM/lcommon/src/memalloc.c:864
+  * IntPelME contract              JM/lencod/inc/global.h:459,
+                                   me_fullsearch.c:39 / me_fullfast.c:618
+  * per-MB partition searches      PartitionMotionSearch mv_search.c:1564,
+                                   SubPartitionMotionSearch mv_search.c:1686
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Mapping
+
+import numpy as np
+
+from . import _lib
+from ._lib import BLOCK_RES, MB_REQ, NSLOT, JmmeConfig, JmmeMv, check, lib, ptr
+
+
+def config_from_cfg(cfg_path: str | None = None, overrides: Mapping[str, object] | None = None) -> JmmeConfig:
+    """JM's `lencod -d cfg_path -p Key=Value ...` for the ME keys."""
+    c = JmmeConfig()
+    check(lib().jmme_config_default(ctypes.byref(c)))
+    args = [f"{k}={v}".encode() for k, v in (overrides or {}).items()]
+    argv = (ctypes.c_char_p * max(1, len(args)))(*args)
+    check(lib().jmme_config_parse(ctypes.byref(c), cfg_path.encode() if cfg_path else None, len(args),
+                                  ctypes.cast(argv, ctypes.c_void_p)))
+    return c
+
+
+def slot_of(blocktype: int, block_x: int, block_y: int) -> int:
+    return int(lib().jmme_slot(int(blocktype), int(block_x), int(block_y)))
+
+
+def spiral(R: int) -> np.ndarray:
+    """JM's spiral_search order (integer pels), from the library's own formula."""
+    n = (2 * R + 1) ** 2
+    out = np.zeros((n, 2), dtype=np.int32)
+    ox, oy = ctypes.c_int(), ctypes.c_int()
+    for i in range(n):
+        lib().jmme_spiral_offset(i, ctypes.byref(ox), ctypes.byref(oy))
+        out[i] = (ox.value, oy.value)
+    return out
+
+
+def _rows(plane: np.ndarray):
+    """get_mem2Dpel layout: one uint16 allocation + a row-pointer array."""
+    p = np.ascontiguousarray(plane, dtype=np.uint16)
+    h, w = p.shape
+    base = p.ctypes.data
+    rows = (ctypes.c_void_p * h)(*[base + 2 * w * y for y in range(h)])
+    return p, rows
+
+
+class MotionEstimator:
+    """One libjmme context: a device, the current picture and the DPB references."""
+
+    def __init__(self, cfg: JmmeConfig | Mapping[str, object] | None = None, device: int = -1):
+        if cfg is None or isinstance(cfg, Mapping):
+            cfg = config_from_cfg(None, cfg or {})
+        self.cfg = cfg
+        self._ctx = lib().jmme_create(ctypes.byref(cfg), int(device))
+        if not self._ctx:
+            raise _lib.JmmeError(lib().jmme_last_error().decode())
+        self.max_mvd = int(lib().jmme_max_mvd(ctypes.byref(cfg)))
+
+    def close(self) -> None:
+        if self._ctx:
+            lib().jmme_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # ---- frame buffers -------------------------------------------------
+    def upload_cur(self, plane: np.ndarray) -> None:
+        keep, rows = _rows(plane)
+        check(lib().jmme_upload_cur(self._ctx, ctypes.cast(rows, ctypes.c_void_p), keep.shape[1], keep.shape[0]))
+
+    def upload_ref(self, list_idx: int, ref_idx: int, plane: np.ndarray) -> None:
+        keep, rows = _rows(plane)
+        check(lib().jmme_upload_ref(self._ctx, int(list_idx), int(ref_idx), ctypes.cast(rows, ctypes.c_void_p),
+                                    keep.shape[1], keep.shape[0]))
+
+    # ---- searches ------------------------------------------------------
+    def search(self, mode: int, req: np.ndarray) -> np.ndarray:
+        """Batched per-MB search; returns BLOCK_RES [n, 41] (unsearched slots zero)."""
+        req = np.ascontiguousarray(req, dtype=MB_REQ)
+        out = np.zeros((req.shape[0], NSLOT), dtype=BLOCK_RES)
+        check(lib().jmme_search_mbs(self._ctx, int(mode), ptr(req), req.shape[0], ptr(out)))
+        return out
+
+    def search_async(self, mode: int, d_req: int, n: int, d_out: int, stream: int = 0) -> None:
+        """Device-resident variant: d_req/d_out are device addresses (e.g. torch data_ptr())."""
+        check(lib().jmme_search_mbs_async(self._ctx, int(mode), ctypes.c_void_p(d_req), int(n),
+                                          ctypes.c_void_p(d_out), ctypes.c_void_p(stream)))
+
+    def search_planes_async(self, mode: int, d_cur: int, d_ref: int, pitch: int, width: int, height: int,
+                            d_req: int, n: int, d_out: int, stream: int = 0) -> None:
+        check(lib().jmme_search_mbs_planes_async(self._ctx, int(mode), ctypes.c_void_p(d_cur),
+                                                 ctypes.c_void_p(d_ref), int(pitch), int(width), int(height),
+                                                 ctypes.c_void_p(d_req), int(n), ctypes.c_void_p(d_out),
+                                                 ctypes.c_void_p(stream)))
+
+    def last_kernel_ms(self) -> float:
+        return float(lib().jmme_last_kernel_ms(self._ctx))
+
+    def full_search_block(self, list_idx, ref_idx, pos_x, pos_y, blocktype, pred, center,
+                          lambda_factor, search_range, check_for_00, min_mcost=_lib.DISTBLK_MAX):
+        """full_search_motion_estimation's contract for one partition (JM global.h:459)."""
+        p = JmmeMv(int(pred[0]), int(pred[1]))
+        mv = JmmeMv(int(center[0]), int(center[1]))
+        cost = lib().jmme_full_search_block(self._ctx, int(list_idx), int(ref_idx), int(pos_x), int(pos_y),
+                                            int(blocktype), ctypes.byref(p), ctypes.byref(mv), int(min_mcost),
+                                            int(lambda_factor), int(search_range), int(check_for_00))
+        return (mv.mv_x, mv.mv_y), int(cost)

@@ -1,0 +1,181 @@
+/*
+ * jmme.h -- C ABI of the MI355X-native (gfx950) JM 18.5 integer-pel motion
+ * estimation engine (libjmme.so).  Plain C types only; no HIP/torch types.
+ *
+ * What it replaces in JM 18.5 lencod (JM = /root/reference/4.对比程序/jm18.5/JM):
+ *
+ *   jmme_full_search_block()      <- currMB->IntPelME = full_search_motion_estimation
+ *                                    signature JM/lencod/inc/global.h:459,
+ *                                    body JM/lencod/src/me_fullsearch.c:39-103,
+ *                                    assigned JM/lencod/src/mv_search.c:139-175
+ *   jmme_fast_full_search_block() <- currMB->IntPelME = fast_full_search_motion_estimation
+ *                                    (JM/lencod/src/me_fullfast.c:618-689) together with
+ *                                    currMB->p_SetupFastFullPelSearch = setup_fast_full_search
+ *                                    (global.h:469, me_fullfast.c:269-608)
+ *   jmme_search_mbs()             <- the same two searches batched per macroblock x
+ *                                    reference: one unit = the 41 partitions
+ *                                    PartitionMotionSearch / SubPartitionMotionSearch
+ *                                    issue for one MB (mv_search.c:1564,1686)
+ *   jmme_upload_cur/_ref()        <- the frame buffers JM's searches read:
+ *                                    p_Vid->pCurImg (image.c:2868, get_mem2Dpel layout,
+ *                                    JM/lcommon/src/memalloc.c:864) and the reference
+ *                                    StorablePicture::imgY (get_mem2Dpel_pad,
+ *                                    memalloc.c:881; filled at store_picture_in_dpb,
+ *                                    mbuffer.c:2116-2122)
+ *   jmme_config_parse()           <- Configure()/ParseContent for the ME keys of
+ *                                    encoder.cfg (JM/lencod/src/configfile.c:314,
+ *                                    Map[] JM/lencod/inc/configfile.h:32-615)
+ *
+ * Error behaviour: every call returns a status (0 = OK, <0 = error) and
+ * jmme_last_error() describes the last failure of the calling thread.  The
+ * JM-signature wrappers mirror JM's error(): they print and exit(500) on
+ * failure, because JM has no error return on that path.
+ *
+ * Numerics: bit-exact with JM 18.5 (JCOST_CALC_SCALEUP=1, imgpel=uint16,
+ * distblk=int64).  8-bit content only in this version (BitDepthLuma 8):
+ * uploads with a sample > 255 are rejected.
+ */
+#ifndef JMME_H
+#define JMME_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef uint16_t jmme_imgpel;   /* JM imgpel, IMGTYPE 1 (JM/lcommon/inc/typedefs.h:35) */
+typedef int64_t  jmme_distblk;  /* JM distblk (typedefs.h:37) */
+
+#define JMME_DISTBLK_MAX (((int64_t)0x7fffffff) << 5)  /* JM/lencod/inc/defines.h:135 */
+#define JMME_NSLOT 41           /* partitions per macroblock (7 block types) */
+#define JMME_MAX_RANGE 64       /* largest integer-pel search range supported */
+
+typedef struct jmme_mv { int16_t mv_x, mv_y; } jmme_mv;  /* JM MotionVector, quarter-pel */
+
+/* SearchMode values, JM/lcommon/inc/types.h:126-133 */
+enum { JMME_FULL_SEARCH = -1, JMME_FAST_FULL_SEARCH = 0, JMME_UM_HEX = 1,
+       JMME_UM_HEX_SIMPLE = 2, JMME_EPZS = 3 };
+
+/* The motion-estimation subset of JM's InputParameters, with encoder.cfg key
+ * names (JM/lencod/inc/configfile.h line of each Map entry in brackets). */
+typedef struct jmme_config {
+  int SourceWidth;            /* [76]  */
+  int SourceHeight;           /* [77]  */
+  int SearchMode;             /* [407] -1 FS, 0 FFS, 1 UMHEX, 2 sUMHEX, 3 EPZS */
+  int SearchRange;            /* [62]  integer pels */
+  int NumberReferenceFrames;  /* [63]  */
+  int DisableSubpelME;        /* [61]  */
+  int RDOptimization;         /* [153] rdopt */
+  int MEDistortionFPel;       /* [278] 0 SAD, 1 SSE, 2 SATD */
+  int MDDistortion;           /* [281] */
+  int EPZSSubPelGrid;         /* [435] */
+  int RestrictSearchRange;    /* [401] full_search */
+  int UseMVLimits;            /* [403] */
+  int SetMVXLimit;            /* [404] */
+  int SetMVYLimit;            /* [405] */
+  int ChromaMEEnable;         /* [275] must be 0 in this version */
+  int SourceBitDepthLuma;     /* [332] must be 8 in this version */
+} jmme_config;
+
+/* ---- configuration ------------------------------------------------------ */
+/* JM defaults (InitParams, JM/lcommon/src/config_common.c:297, for these keys). */
+int jmme_config_default(jmme_config *cfg);
+/* Parse a JM encoder.cfg (may be NULL) then `-p Key=Value` overrides
+ * (argv holds "Key=Value" strings), as lencod -d file -p k=v does.
+ * Unknown keys are ignored (JM warns); malformed values fail. */
+int jmme_config_parse(jmme_config *cfg, const char *cfg_path, int argc, const char *const *argv);
+/* p_Vid->max_mvd for this config (JM/lencod/src/mv_search.c:321-328). */
+int jmme_max_mvd(const jmme_config *cfg);
+
+/* ---- context ------------------------------------------------------------ */
+typedef struct jmme_ctx jmme_ctx;
+/* device < 0: current HIP device.  Returns NULL on error. */
+jmme_ctx *jmme_create(const jmme_config *cfg, int device);
+void jmme_destroy(jmme_ctx *ctx);
+const char *jmme_last_error(void);
+const char *jmme_version(void);
+
+/* ---- frame buffers (JM get_mem2Dpel / get_mem2Dpel_pad layout) ----------
+ * rows[y] points at sample (0, y) of the UNPADDED picture; rows are equally
+ * spaced (one allocation), so a single strided copy moves the plane.
+ * The reference must be the reconstructed picture JM stores in the DPB. */
+int jmme_upload_cur(jmme_ctx *ctx, const jmme_imgpel *const *rows, int width, int height);
+int jmme_upload_ref(jmme_ctx *ctx, int list, int ref_idx,
+                    const jmme_imgpel *const *rows, int width, int height);
+
+/* ---- batched search: one unit = one macroblock x one reference ----------
+ * Slot order of the 41 partitions (jmme_slot()):
+ *   0 16x16 | 1-2 16x8 | 3-4 8x16 | 5-8 8x8 | 9-16 8x4 | 17-24 4x8 | 25-40 4x4
+ * Per-slot inputs are exactly what JM hands the IntPelME call for that
+ * partition (BlockMotionSearch, mv_search.c:916-960). */
+typedef struct jmme_block_req {
+  int16_t pred_x, pred_y;     /* MV predictor (qpel)                           */
+  int16_t center_x, center_y; /* FS: search centre mv_block->mv[list] (qpel)   */
+  int16_t search_range;       /* FS: imin(max_x,max_y)>>2; FFS: imax(...)>>2    */
+  int16_t flags;              /* JMME_BLK_* */
+  int32_t lambda;             /* lambda_factor[F_PEL] */
+} jmme_block_req;             /* 16 bytes */
+
+#define JMME_BLK_CHECK00 1    /* FS: (0,0) bonus, me_fullsearch.c:61,78-82 */
+
+typedef struct jmme_mb_req {
+  int16_t mb_x, mb_y;         /* macroblock origin (luma pels)                 */
+  int16_t list, ref_idx;      /* which uploaded reference                      */
+  uint64_t slot_mask;         /* bit s set = slot s is searched                */
+  int16_t ffs_center_x;       /* FFS: search_center[list][ref] (qpel)          */
+  int16_t ffs_center_y;
+  int16_t ffs_range;          /* FFS: max_search_range[list][ref] (pels)       */
+  int16_t ffs_pos00_valid;    /* FFS: !rdopt pre-seed of (0,0) enabled          */
+  int16_t reserved[4];        /* zero; keeps blk[] 16-byte aligned              */
+  jmme_block_req blk[JMME_NSLOT];
+} jmme_mb_req;                /* 32 + 41*16 = 688 bytes */
+
+typedef struct jmme_block_res {
+  int16_t mv_x, mv_y;         /* best mv (qpel), mv_block->mv[list] on return  */
+  int32_t reserved;
+  int64_t cost;               /* min_mcost JM returns (distblk)                 */
+} jmme_block_res;             /* 16 bytes */
+
+/* slot of (blocktype 1..7, block_x, block_y in 4x4 units), -1 if invalid */
+int jmme_slot(int blocktype, int block_x, int block_y);
+
+/* mode = JMME_FULL_SEARCH or JMME_FAST_FULL_SEARCH.  Host arrays, synchronous.
+ * out has n * JMME_NSLOT entries (unsearched slots are left untouched). */
+int jmme_search_mbs(jmme_ctx *ctx, int mode, const jmme_mb_req *req, int n, jmme_block_res *out);
+
+/* Device-resident variant for pipelines and the benchmark: d_req/d_out are
+ * device pointers, planes are those already uploaded; enqueued on `stream`
+ * (a hipStream_t, NULL = default stream); no host synchronisation. */
+int jmme_search_mbs_async(jmme_ctx *ctx, int mode, const jmme_mb_req *d_req, int n,
+                          jmme_block_res *d_out, void *stream);
+
+/* Device-plane variant: d_cur/d_ref are 8-bit planes (pitch bytes per row)
+ * already in device memory (e.g. from torch), for multi-frame pipelines. */
+int jmme_search_mbs_planes_async(jmme_ctx *ctx, int mode,
+                                 const uint8_t *d_cur, const uint8_t *d_ref, int pitch,
+                                 int width, int height,
+                                 const jmme_mb_req *d_req, int n, jmme_block_res *d_out,
+                                 void *stream);
+
+/* ---- JM IntPelME-signature drop-ins (one partition per call) ------------
+ * Same inputs/outputs as full_search_motion_estimation / the FFS pair, in C
+ * types: mv_inout is mv_block->mv[list] (centre in, best out). */
+jmme_distblk jmme_full_search_block(jmme_ctx *ctx, int list, int ref_idx,
+                                    int pos_x, int pos_y, int blocktype,
+                                    const jmme_mv *pred_mv, jmme_mv *mv_inout,
+                                    jmme_distblk min_mcost, int lambda_factor,
+                                    int search_range, int check_for_00);
+
+/* ---- timing of the last jmme_search_mbs* launch (HIP events on its stream) */
+float jmme_last_kernel_ms(jmme_ctx *ctx);
+
+/* ---- exposed for host-side tests (no GPU needed) ------------------------ */
+int jmme_spiral_index(int ox, int oy);                /* position in spiral_search order */
+void jmme_spiral_offset(int index, int *ox, int *oy); /* inverse */
+int jmme_mvbits(int v);                                /* mvbits[v], mv_search.c:366-374 */
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* JMME_H */

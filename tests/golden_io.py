@@ -103,3 +103,45 @@ class Case:
         surf = int(r["ffs_max_range"][idx][0])
         assert np.all(r["ffs_max_range"][idx] == surf)
         return surf, int(r["max_mvd"][idx][0]), int(r["rdopt"][idx][0]), mbs, blk
+
+    # ---- HIP engine requests ----------------------------------------------
+    def units(self, idx, mode):
+        """Group the searches `idx` (one picture pair) into per-MB units.
+
+        Returns (req MB_REQ[n], unit_of[len(idx)], slot_of[len(idx)]).
+        """
+        from jmme import MB_REQ, BLK_CHECK00, FAST_FULL_SEARCH, slot_of
+        r = self.r
+        mb = r["mb_addr"][idx]
+        umb, unit_of = np.unique(mb, return_inverse=True)
+        req = np.zeros(len(umb), dtype=MB_REQ)
+        slots = np.array([slot_of(b, x, y) for b, x, y in
+                          zip(r["blocktype"][idx], r["block_x"][idx], r["block_y"][idx])], np.int64)
+        assert np.all(slots >= 0)
+        first = np.zeros(len(umb), np.int64)
+        first[unit_of[::-1]] = np.arange(len(idx))[::-1]
+        fi = idx[first]
+        req["mb_x"] = r["pix_x"][fi]
+        req["mb_y"] = r["pix_y"][fi]
+        req["list"] = r["list"][fi]
+        req["ref_idx"] = r["ref"][fi]
+        if mode == FAST_FULL_SEARCH:
+            req["ffs_center_x"] = r["ffs_center_x"][fi]
+            req["ffs_center_y"] = r["ffs_center_y"][fi]
+            req["ffs_range"] = r["ffs_max_range"][fi]
+            req["ffs_pos00_valid"] = (r["rdopt"][fi] == 0)
+            rng = self.ffs_block_range(idx)
+            flags = np.zeros(len(idx), np.int16)
+        else:
+            rng = self.fs_search_range(idx)
+            flags = np.where(self.fs_check_for_00(idx) != 0, BLK_CHECK00, 0).astype(np.int16)
+        for k, (u, s) in enumerate(zip(unit_of, slots)):
+            assert not (int(req["slot_mask"][u]) >> int(s)) & 1, "one search per partition per unit"
+            req["slot_mask"][u] |= np.uint64(1) << np.uint64(s)
+            b = req["blk"][u, s]
+            j = idx[k]
+            b["pred_x"], b["pred_y"] = r["pred_x"][j], r["pred_y"][j]
+            b["center_x"], b["center_y"] = r["center_x"][j], r["center_y"][j]
+            b["search_range"], b["flags"], b["lambda"] = rng[k], flags[k], r["lambda"][j]
+            req["blk"][u, s] = b
+        return req, unit_of, slots

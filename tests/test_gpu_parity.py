@@ -1,0 +1,225 @@
+"""HIP path (libjmme.so on gfx950) against JM 18.5: bit-exact MVs and costs.
+
+Every call goes through the C ABI (include/jmme.h).  The expected values are
+the (mv, cost) JM 18.5 itself returned (tests/golden/, captured from the
+unmodified encoder), or -- for inputs no JM run produced -- the CPU oracle,
+which test_oracle_golden.py pins against those same JM captures.
+"""
+import numpy as np
+import pytest
+
+import golden_io as g
+import oracle_lib as ol
+
+pytestmark = pytest.mark.gpu
+
+CASES = g.cases()
+
+
+def _engine(case, gpu):
+    from jmme import MotionEstimator
+    ov = g.manifest()[case.name]["cfg_overrides"]
+    return MotionEstimator({"SearchRange": ov["SearchRange"], "SearchMode": ov["SearchMode"]})
+
+
+def _run_case(c, me, mode):
+    n_ok = n = 0
+    for f, lst, rf, idx in c.groups():
+        me.upload_cur(c.cur[f])
+        me.upload_ref(lst, rf, c.ref[(f, lst, rf)])
+        req, unit_of, slots = c.units(idx, mode)
+        out = me.search(mode, req)
+        res = out[unit_of, slots]
+        ok = ((res["mv_x"] == c.r["out_mv_x"][idx]) & (res["mv_y"] == c.r["out_mv_y"][idx]) &
+              (res["cost"] == c.r["out_cost"][idx]))
+        if not ok.all():
+            k = np.nonzero(~ok)[0][:5]
+            detail = [(int(idx[i]), int(unit_of[i]), int(slots[i]), (int(res["mv_x"][i]), int(res["mv_y"][i]),
+                       int(res["cost"][i])), (int(c.r["out_mv_x"][idx[i]]), int(c.r["out_mv_y"][idx[i]]),
+                       int(c.r["out_cost"][idx[i]]))) for i in k]
+            raise AssertionError(f"{c.name} frame {f} ref {rf}: {(~ok).sum()}/{len(idx)} differ: {detail}")
+        n_ok += int(ok.sum())
+        n += len(idx)
+    return n_ok, n
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_hip_matches_jm_golden(name, gpu):
+    c = g.Case(name)
+    mode = g.manifest()[name]["cfg_overrides"]["SearchMode"]
+    with _engine(c, gpu) as me:
+        n_ok, n = _run_case(c, me, mode)
+    assert n_ok == n == c.n
+
+
+def test_partial_slot_masks_and_shuffled_units(gpu):
+    """Units carrying any subset of partitions, in any order, give the same
+    per-partition answers (the grouping by window / predictor is exact)."""
+    from jmme import FULL_SEARCH
+    c = g.Case("syn_cif_adv_fs32")
+    rng = np.random.default_rng(3)
+    with _engine(c, gpu) as me:
+        for f, lst, rf, idx in c.groups():
+            me.upload_cur(c.cur[f])
+            me.upload_ref(lst, rf, c.ref[(f, lst, rf)])
+            req, unit_of, slots = c.units(idx, FULL_SEARCH)
+            keep = rng.random(len(idx)) < 0.35
+            for u in range(len(req)):
+                m = 0
+                for k in np.nonzero((unit_of == u) & keep)[0]:
+                    m |= 1 << int(slots[k])
+                req["slot_mask"][u] = m
+            perm = rng.permutation(len(req))
+            out = me.search(FULL_SEARCH, req[perm])
+            inv = np.argsort(perm)
+            res = out[inv[unit_of], slots]
+            sel = keep
+            assert np.array_equal(res["mv_x"][sel], c.r["out_mv_x"][idx][sel])
+            assert np.array_equal(res["mv_y"][sel], c.r["out_mv_y"][idx][sel])
+            assert np.array_equal(res["cost"][sel], c.r["out_cost"][idx][sel])
+
+
+def test_several_references_in_one_launch(gpu):
+    """All refs of a frame are uploaded once and their units searched in one call."""
+    from jmme import FULL_SEARCH, MB_REQ
+    c = g.Case("syn_cif_fs32_rdo0_3ref")
+    with _engine(c, gpu) as me:
+        frames = sorted({f for f, _, _, _ in c.groups()})
+        f = frames[-1]
+        groups = [(lst, rf, idx) for ff, lst, rf, idx in c.groups() if ff == f]
+        assert len(groups) >= 3
+        me.upload_cur(c.cur[f])
+        reqs, maps = [], []
+        for lst, rf, idx in groups:
+            me.upload_ref(lst, rf, c.ref[(f, lst, rf)])
+            req, unit_of, slots = c.units(idx, FULL_SEARCH)
+            maps.append((idx, unit_of + sum(len(x) for x in reqs), slots))
+            reqs.append(req)
+        out = me.search(FULL_SEARCH, np.concatenate(reqs).astype(MB_REQ))
+        for idx, unit_of, slots in maps:
+            res = out[unit_of, slots]
+            assert np.array_equal(res["cost"], c.r["out_cost"][idx])
+            assert np.array_equal(res["mv_x"], c.r["out_mv_x"][idx])
+            assert np.array_equal(res["mv_y"], c.r["out_mv_y"][idx])
+
+
+def test_intpelme_signature_dropin(gpu):
+    """jmme_full_search_block = full_search_motion_estimation's contract."""
+    c = g.Case("c1_foreman_qcif_fs16_rdo0")
+    r = c.r
+    with _engine(c, gpu) as me:
+        f, lst, rf, idx = next(iter(c.groups()))
+        me.upload_cur(c.cur[f])
+        me.upload_ref(lst, rf, c.ref[(f, lst, rf)])
+        rng = np.random.default_rng(0)
+        for j in rng.choice(idx, 60, replace=False):
+            mv, cost = me.full_search_block(lst, rf, r["pos_x"][j], r["pos_y"][j], r["blocktype"][j],
+                                            (r["pred_x"][j], r["pred_y"][j]), (r["center_x"][j], r["center_y"][j]),
+                                            r["lambda"][j], c.fs_search_range(np.array([j]))[0],
+                                            c.fs_check_for_00(np.array([j]))[0])
+            assert mv == (r["out_mv_x"][j], r["out_mv_y"][j]) and cost == r["out_cost"][j]
+
+
+def _random_units(rng, w, h, n, R, lam_max=400, mode=-1):
+    from jmme import MB_REQ, BLK_CHECK00
+    req = np.zeros(n, dtype=MB_REQ)
+    req["mb_x"] = rng.integers(0, w // 16, n) * 16
+    req["mb_y"] = rng.integers(0, h // 16, n) * 16
+    req["slot_mask"] = (1 << 41) - 1
+    for u in range(n):
+        base = rng.integers(-3 * R, 3 * R + 1, size=2) * 4
+        for s in range(41):
+            b = req["blk"][u, s]
+            cen = base + rng.integers(-2, 3, size=2) * 4 * (rng.random() < 0.3)
+            b["center_x"], b["center_y"] = cen
+            b["pred_x"], b["pred_y"] = cen + rng.integers(-9, 10, size=2)
+            b["search_range"] = R
+            b["lambda"] = rng.integers(0, lam_max)
+            b["flags"] = BLK_CHECK00 if s == 0 and rng.random() < 0.5 else 0
+            req["blk"][u, s] = b
+    return req
+
+
+def _oracle_units(cur, ref, req):
+    """Oracle answers for every slot of every unit (FS)."""
+    from jmme import slot_of
+    rows, keys = [], []
+    geo = {}
+    for bt, (bw, bh) in {1: (16, 16), 2: (16, 8), 3: (8, 16), 4: (8, 8), 5: (8, 4), 6: (4, 8), 7: (4, 4)}.items():
+        for by in range(0, 16, bh):
+            for bx in range(0, 16, bw):
+                geo[slot_of(bt, bx // 4, by // 4)] = (bx, by, bw, bh)
+    for u, q in enumerate(req):
+        for s in range(41):
+            if not (int(q["slot_mask"]) >> s) & 1:
+                continue
+            b = q["blk"][s]
+            bx, by, bw, bh = geo[s]
+            rows.append([q["mb_x"] + bx, q["mb_y"] + by, bw, bh, b["pred_x"], b["pred_y"], b["center_x"],
+                         b["center_y"], b["search_range"], b["lambda"], int(b["flags"] & 1)])
+            keys.append((u, s))
+    mv, cost = ol.full_search_batch(cur, ref, np.array(rows, np.int32))
+    return keys, mv, cost
+
+
+@pytest.mark.parametrize("size,R", [((3840, 2160), 32), ((1920, 1088), 16), ((352, 288), 44), ((176, 144), 0)])
+def test_random_requests_vs_oracle(size, R, gpu):
+    """Inputs no JM run produced (4K, unusual ranges, centres far outside the
+    picture, mixed windows per MB): HIP == oracle on every partition."""
+    from jmme import FULL_SEARCH, MotionEstimator
+    from jmme import synth
+    w, h = size
+    rng = np.random.default_rng(R + w)
+    luma = synth.luma_sequence(w, h, 2, seed=w + R, gmv=(3, -2))
+    cur, ref = luma[1], luma[0]
+    req = _random_units(rng, w, h, 24, R)
+    with MotionEstimator({"SearchRange": max(R, 1), "SearchMode": -1}) as me:
+        me.upload_cur(cur)
+        me.upload_ref(0, 0, ref)
+        out = me.search(FULL_SEARCH, req)
+    keys, mv, cost = _oracle_units(cur, ref, req)
+    got = np.array([(out[u, s]["mv_x"], out[u, s]["mv_y"], out[u, s]["cost"]) for u, s in keys])
+    exp = np.column_stack([mv[:, 0], mv[:, 1], cost])
+    bad = np.nonzero(np.any(got != exp, axis=1))[0]
+    assert len(bad) == 0, [(keys[i], got[i].tolist(), exp[i].tolist()) for i in bad[:5]]
+
+
+def test_saturated_32bit_keys_take_the_64bit_path(gpu):
+    """Huge lambdas push every candidate of the small partitions past the
+    32-bit key's cost field; the deferred 64-bit pass must keep results exact."""
+    from jmme import FULL_SEARCH, MotionEstimator, synth
+    w, h, R = 352, 288, 16
+    rng = np.random.default_rng(9)
+    luma = synth.luma_sequence(w, h, 2, seed=4)
+    req = _random_units(rng, w, h, 6, R)
+    req["blk"]["lambda"] = 400000
+    with MotionEstimator({"SearchRange": R, "SearchMode": -1}) as me:
+        me.upload_cur(luma[1])
+        me.upload_ref(0, 0, luma[0])
+        out = me.search(FULL_SEARCH, req)
+    keys, mv, cost = _oracle_units(luma[1], luma[0], req)
+    for i, (u, s) in enumerate(keys):
+        assert (out[u, s]["mv_x"], out[u, s]["mv_y"], out[u, s]["cost"]) == (mv[i, 0], mv[i, 1], cost[i])
+
+
+def test_requests_outside_contract_are_rejected(gpu):
+    from jmme import FULL_SEARCH, JmmeError, MotionEstimator, MB_REQ, synth
+    luma = synth.luma_sequence(176, 144, 2, seed=1)
+    with MotionEstimator({"SearchRange": 8, "SearchMode": -1}) as me:
+        me.upload_cur(luma[1])
+        me.upload_ref(0, 0, luma[0])
+        req = np.zeros(1, dtype=MB_REQ)
+        req["slot_mask"] = 1
+        req["blk"][0, 0]["search_range"] = 9           # > SearchRange
+        with pytest.raises(JmmeError):
+            me.search(FULL_SEARCH, req)
+        req["blk"][0, 0]["search_range"] = 8
+        req["blk"][0, 0]["center_x"] = 2                # sub-pel centre (EPZSSubPelGrid)
+        with pytest.raises(JmmeError):
+            me.search(FULL_SEARCH, req)
+        req["blk"][0, 0]["center_x"] = 0
+        req["ref_idx"] = 3                              # never uploaded
+        with pytest.raises(JmmeError):
+            me.search(FULL_SEARCH, req)
+        with pytest.raises(JmmeError):
+            me.upload_ref(0, 1, np.full((144, 176), 300, np.uint16))  # not 8-bit
