@@ -342,6 +342,7 @@ int launch(jmme_ctx *ctx, int mode, const uint8_t *d_cur, const uint8_t *const *
   HIPCHK(hipMemsetAsync(ctx->d_defer_count, 0, 16, s));
   HIPCHK(hipEventRecord(ctx->ev0, s));
   HIPCHK(launch_units(p, key32, n, s));
+  HIPCHK(hipEventRecord(ctx->ev1, s));   // jmme_last_kernel_ms: the unit kernel alone
   if (key32) {
     // units whose every candidate saturated the 32-bit cost field (none in
     // practice): redo with 64-bit keys; the grid drains the device list.
@@ -351,7 +352,6 @@ int launch(jmme_ctx *ctx, int mode, const uint8_t *d_cur, const uint8_t *const *
     q.defer_count = nullptr;
     HIPCHK(launch_units(q, false, 64, s));
   }
-  HIPCHK(hipEventRecord(ctx->ev1, s));
   ctx->timed = true;
   return 0;
 }
