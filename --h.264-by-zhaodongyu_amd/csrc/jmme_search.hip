@@ -28,6 +28,7 @@
 //   * partitions that share a predictor share the mv-cost arithmetic;
 //   * at the end a wave shuffle + LDS reduction produces the 41 results.
 #include <hip/hip_runtime.h>
+#include <type_traits>
 #include "jmme.h"
 #include "jmme_common.h"
 #include "jmme_internal.h"
@@ -38,7 +39,6 @@ namespace {
 
 constexpr int kNS = JMME_NSLOT;
 constexpr int kWaves = kWG / 64;
-constexpr uint32_t kSat32 = (1u << 19) - 1;   // saturated cost field of a 32-bit key
 constexpr int kKey32First = 9;
 #ifndef JMME_WAVES_PER_EU
 #define JMME_WAVES_PER_EU 2
@@ -104,6 +104,115 @@ __device__ __forceinline__ int xcd_unit(int b, int nb) {
   return x * q + (x < r ? x : r) + b / nx;
 }
 
+constexpr unsigned long long kAll = (1ull << kNS) - 1;
+constexpr uint32_t kKey32MaxLambda = 3556;   // lambda*74 + 8x4 SAD<<5 < 2^19: 32-bit keys exact
+
+// the 41 partition SADs (already <<5) from the 16 4x4 SADs; JM sums them in
+// update_full_search_large_blocks (me_fullfast.c:196-260) -- integer sums, any order
+__device__ __forceinline__ void partition_sads(const uint32_t *a, uint32_t *ps) {
+#pragma unroll
+  for (int k = 0; k < 16; ++k) ps[25 + k] = a[k];                                           // 4x4
+#pragma unroll
+  for (int by = 0; by < 4; ++by)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) ps[9 + by * 2 + h] = a[by * 4 + 2 * h] + a[by * 4 + 2 * h + 1];   // 8x4
+#pragma unroll
+  for (int v = 0; v < 2; ++v)
+#pragma unroll
+    for (int bx = 0; bx < 4; ++bx) ps[17 + v * 4 + bx] = a[(2 * v) * 4 + bx] + a[(2 * v + 1) * 4 + bx];  // 4x8
+#pragma unroll
+  for (int v = 0; v < 2; ++v)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) ps[5 + v * 2 + h] = ps[9 + (2 * v) * 2 + h] + ps[9 + (2 * v + 1) * 2 + h];  // 8x8
+  ps[3] = ps[5] + ps[7];
+  ps[4] = ps[6] + ps[8];   // 8x16
+  ps[1] = ps[5] + ps[6];
+  ps[2] = ps[7] + ps[8];   // 16x8
+  ps[0] = ps[1] + ps[2];   // 16x16
+}
+
+// branch-free spiral_index (jmme_common.h) for the sweep
+__device__ __forceinline__ int spiral_index_bl(int ox, int oy) {
+  const int ax = abs(ox), ay = abs(oy);
+  const int l = max(ax, ay);
+  const int base = (2 * l - 1) * (2 * l - 1);
+  const int top = base + 2 * (ox + l - 1) + (oy > 0);
+  const int side = base + 2 * (2 * l - 1) + 2 * (oy + l) + (ox > 0);
+  const int v = (ay == l && ax < l) ? top : side;
+  return l == 0 ? 0 : v;
+}
+
+struct SlotCtx {
+  uint32_t mvc, rank;
+  int lring;
+  bool is00, ok;
+  int chk00, lam;
+  bool preseed;
+  unsigned long long rlim;
+  const int4 *slot;
+  int candx, candy, max_mvd;
+};
+
+// mv cost lambda*(mvbits[dx]+mvbits[dy]) of candidate (candx, candy) against
+// predictor (px, py), mv_search.h:100-104; GetMaxMVD gate for FFS.
+struct MvCost { uint32_t mvc; bool ok; };
+template <bool FFS>
+__device__ __forceinline__ MvCost mv_cost(int candx, int candy, int px, int py, int lam, int max_mvd) {
+  const int dx = candx - px, dy = candy - py;
+  MvCost r;
+  r.mvc = (uint32_t)lam * (uint32_t)(mvbits(dx) + mvbits(dy));
+  r.ok = FFS ? (max(abs(dx), abs(dy)) < max_mvd - 1) : true;   // me_fullfast.c:663
+  return r;
+}
+
+// PERSLOT: partitions of this window have different predictors; each slot's
+// predictor/lambda is read (LDS broadcast) and its mv cost computed here.
+template <bool KEY32, bool FFS, bool ALL, bool PERSLOT, int NB64, int NB32>
+__device__ __forceinline__ void update_slots_impl(const uint32_t (&ps)[kNS], unsigned long long cmask,
+                                                  const SlotCtx &c, unsigned long long (&best64)[NB64],
+                                                  uint32_t (&best32)[NB32]) {
+#pragma unroll
+  for (int s = 0; s < kNS; ++s) {
+    if (!ALL && !((cmask >> s) & 1)) continue;
+    uint32_t m = c.mvc;
+    int lam = c.lam;
+    bool oks = c.ok;
+    if (PERSLOT) {
+      const int4 q = c.slot[s];
+      lam = ufl(rq_lambda(q));
+      const MvCost mc = mv_cost<FFS>(c.candx, c.candy, ufl(rq_pred_x(q)), ufl(rq_pred_y(q)), lam, c.max_mvd);
+      m = mc.mvc;
+      oks = mc.ok;
+    }
+    if (!FFS && s == 0 && c.chk00) {
+      const uint32_t t = 16u * (uint32_t)lam;             // weighted_cost(lambda,16), me_fullsearch.c:80
+      if (c.is00) m = m > t ? m - t : 0u;
+    }
+    if (FFS && ((c.rlim >> s) & 1)) {
+      const int rs = ufl(rq_range(c.slot[s]));
+      oks = oks && (c.lring <= rs || (c.preseed && c.is00));
+    }
+    const uint32_t cost = ps[s] + m;
+    if (KEY32 && s >= kKey32First) {
+      const uint32_t k = (cost << 13) | c.rank;
+      if (FFS)
+        best32[s - kKey32First] = min(best32[s - kKey32First], oks ? k : ~0u);
+      else
+        best32[s - kKey32First] = min(best32[s - kKey32First], k);
+    } else {
+      const unsigned long long k = ((unsigned long long)cost << 32) | c.rank;
+      const unsigned long long kk = FFS ? (oks ? k : ~0ull) : k;
+      best64[s] = best64[s] < kk ? best64[s] : kk;
+    }
+  }
+}
+
+template <bool KEY32, bool FFS, bool ALL, bool PERSLOT, int NB64, int NB32>
+__device__ __forceinline__ void update_slots(const uint32_t (&ps)[kNS], unsigned long long cmask, const SlotCtx &c,
+                                             unsigned long long (&best64)[NB64], uint32_t (&best32)[NB32]) {
+  update_slots_impl<KEY32, FFS, ALL, PERSLOT>(ps, cmask, c, best64, best32);
+}
+
 template <bool KEY32, bool FFS>
 __device__ __forceinline__ void unit_body(const KParams &p, int u, unsigned char *smem) {
   const int tid = threadIdx.x;
@@ -130,6 +239,7 @@ __device__ __forceinline__ void unit_body(const KParams &p, int u, unsigned char
     const int4 *src = reinterpret_cast<const int4 *>(&rq->blk[0]);
     L.slot[tid] = src[tid];
   }
+  if (tid == 255) L.flag[0] = 0;
   if (tid >= 64 && tid < 128) {
     int t = tid - 64, r = t >> 2, c = t & 3;
     L.cur[t] = *reinterpret_cast<const uint32_t *>(p.cur + (size_t)(mb_y + r) * p.pitch + mb_x + 4 * c);
@@ -142,31 +252,43 @@ __device__ __forceinline__ void unit_body(const KParams &p, int u, unsigned char
       for (int t = 0; t < kNS; ++t) {
         if (!((slot_mask >> t) & 1)) continue;
         int4 o = L.slot[t];
+        // a group = partitions with the same search window AND the same
+        // predictor/lambda: one SAD sweep and one mv-cost per position serve
+        // the whole group (a window with several predictors is swept once per
+        // predictor -- straight-line code, no per-partition predictor loads)
         bool same_win = ffs || (o.y == me.y && rq_range(o) == rq_range(me));
         bool same_cls = same_win && o.x == me.x && o.w == me.w;
-        g |= (unsigned long long)same_win << t;
-        c |= (unsigned long long)same_cls << t;
+        g |= (unsigned long long)same_cls << t;
+        c |= (unsigned long long)same_win << t;
       }
     }
     L.grp[tid] = g;
     L.cls[tid] = c;
+    // 32-bit keys are exact only while lambda*74 + SAD<<5 < 2^19 (kKey32MaxLambda)
+    if (KEY32 && ((slot_mask >> tid) & 1) && (uint32_t)rq_lambda(me) > kKey32MaxLambda) L.flag[0] = 1;
   }
-  if (tid == 0) L.flag[0] = 0;
   __syncthreads();
+  if (KEY32 && ufl(L.flag[0])) {
+    // redo the whole unit with 64-bit keys in the deferred pass
+    if (tid == 0) p.defer_list[atomicAdd(p.defer_count, 1u)] = u;
+    return;
+  }
 
-  // per-thread running minima of the (cost, rank) keys
-  unsigned long long best64[KEY32 ? kKey32First : kNS];
-  uint32_t best32[KEY32 ? kNS - kKey32First : 1];
-#pragma unroll
-  for (int s = 0; s < (KEY32 ? kKey32First : kNS); ++s) best64[s] = ~0ull;
-#pragma unroll
-  for (int s = 0; s < (KEY32 ? kNS - kKey32First : 1); ++s) best32[s] = ~0u;
-
+  // One pass per search window (group of partitions sharing it): stage the
+  // window, sweep it, reduce and write that group's results.  Nothing is
+  // carried from one group to the next.
   unsigned long long remaining = slot_mask;
   while (remaining) {
     const int lead = __builtin_ctzll(remaining);
     const unsigned long long gmask = ufl64(L.grp[lead]) & remaining;
     remaining &= ~gmask;
+    // per-thread running minima of the (cost, rank) keys
+    unsigned long long best64[KEY32 ? kKey32First : kNS];
+    uint32_t best32[KEY32 ? kNS - kKey32First : 1];
+#pragma unroll
+    for (int s = 0; s < (KEY32 ? kKey32First : kNS); ++s) best64[s] = ~0ull;
+#pragma unroll
+    for (int s = 0; s < (KEY32 ? kNS - kKey32First : 1); ++s) best32[s] = ~0u;
     const int4 lq = L.slot[lead];
     const int cqx = ufl(ffs ? ffs_cx : rq_cen_x(lq));   // window centre, qpel (multiple of 4)
     const int cqy = ufl(ffs ? ffs_cy : rq_cen_y(lq));
@@ -185,6 +307,9 @@ __device__ __forceinline__ void unit_body(const KParams &p, int u, unsigned char
       rlim = ufl64(rlim);
     }
     const int chk00 = ufl((!ffs && (gmask & 1)) ? (rq_flags(L.slot[0]) & JMME_BLK_CHECK00) : 0);
+    const int cls_px = ufl(rq_pred_x(lq));
+    const int cls_py = ufl(rq_pred_y(lq));
+    const int cls_lam = ufl(rq_lambda(lq));
 
     // ---- stage the (2R+16)^2 reference window, clamped like UMVLine4X
     const int x0 = mb_x + (cqx >> 2) - R;
@@ -208,163 +333,126 @@ __device__ __forceinline__ void unit_body(const KParams &p, int u, unsigned char
     }
     __syncthreads();
 
-    // ---- sweep all (2R+1)^2 positions of the window
-    const int D = 2 * R + 1;
-    const int NP = D * D;
-    for (int pos = tid; pos < NP; pos += kWG) {
-      // opaque zero: keeps the 16 broadcast reads of the current MB inside the
-      // loop instead of letting LICM pin 64 VGPRs for them
-      int zero;
-      asm volatile("v_mov_b32 %0, 0" : "=v"(zero));
-      const uint4 *cur4 = reinterpret_cast<const uint4 *>(L.cur) + zero;
-      const int oyw = pos / D;
-      const int oxw = pos - oyw * D;
-      uint32_t a[16];
-      const uint32_t *wrow = L.words + oyw * L.wp + oxw;
-#pragma unroll
-      for (int by = 0; by < 4; ++by) {
-        uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-        // rows are not unrolled: bounds the loads in flight (VGPR budget)
-#pragma unroll 1
-        for (int r = 0; r < 4; ++r) {
-          const int i = by * 4 + r;
-          const uint4 c = cur4[i];
-          const uint32_t *w = wrow + i * L.wp;
-          s0 = __builtin_amdgcn_sad_u8(w[0], c.x, s0);
-          s1 = __builtin_amdgcn_sad_u8(w[4], c.y, s1);
-          s2 = __builtin_amdgcn_sad_u8(w[8], c.z, s2);
-          s3 = __builtin_amdgcn_sad_u8(w[12], c.w, s3);
+    // ---- sweep all (2R+1)^2 positions of the window.  A task is a vertical
+    // pair of positions (x, y), (x, y+1): the 17 reference rows they need are
+    // read from LDS once and feed both (halves the LDS traffic per position).
+    // the sweep, specialised for a window that serves all 41 partitions (no
+    // per-partition mask tests) or a subset
+    auto sweep = [&](auto all_tag) {
+      const int D = 2 * R + 1;
+      const int DP = (D + 1) >> 1;          // position pairs per column
+      const int ntask = D * DP;
+      const int qstep = kWG / D, rstep = kWG - (kWG / D) * D;
+      int tx = tid % D, ty = tid / D;       // task column, pair row
+      for (int t = tid; t < ntask; t += kWG) {
+        uint32_t a0[16], a1[16];
+  #pragma unroll
+        for (int k = 0; k < 16; ++k) { a0[k] = 0; a1[k] = 0; }
+        {
+          // opaque zero: keeps the broadcast reads of the current MB inside the
+          // loop instead of letting LICM pin 64 VGPRs for them
+          int zero;
+          asm volatile("v_mov_b32 %0, 0" : "=v"(zero));
+          const uint4 *cur4 = reinterpret_cast<const uint4 *>(L.cur) + zero;
+          const uint32_t *wrow = L.words + (2 * ty) * L.wp + tx;
+          uint4 cprev = make_uint4(0, 0, 0, 0);
+  #pragma unroll
+          for (int r = 0; r < 17; ++r) {
+            const uint32_t *w = wrow + r * L.wp;
+            const uint32_t w0 = w[0], w1 = w[4], w2 = w[8], w3 = w[12];
+            if (r < 16) {   // row r of the MB against position y
+              const uint4 c = cur4[r];
+              const int b = (r >> 2) * 4;
+              a0[b + 0] = __builtin_amdgcn_sad_u8(w0, c.x, a0[b + 0]);
+              a0[b + 1] = __builtin_amdgcn_sad_u8(w1, c.y, a0[b + 1]);
+              a0[b + 2] = __builtin_amdgcn_sad_u8(w2, c.z, a0[b + 2]);
+              a0[b + 3] = __builtin_amdgcn_sad_u8(w3, c.w, a0[b + 3]);
+            }
+            if (r > 0) {    // row r-1 of the MB against position y+1
+              const int b = ((r - 1) >> 2) * 4;
+              a1[b + 0] = __builtin_amdgcn_sad_u8(w0, cprev.x, a1[b + 0]);
+              a1[b + 1] = __builtin_amdgcn_sad_u8(w1, cprev.y, a1[b + 1]);
+              a1[b + 2] = __builtin_amdgcn_sad_u8(w2, cprev.z, a1[b + 2]);
+              a1[b + 3] = __builtin_amdgcn_sad_u8(w3, cprev.w, a1[b + 3]);
+            }
+            if (r < 16) cprev = cur4[r];
+            // bound the scheduler's look-ahead: a few rows of loads in flight,
+            // not all 17 (which would pin ~140 VGPRs)
+            if ((r & 1) == 1) __builtin_amdgcn_sched_barrier(0);
+          }
+          // pin the accumulators here: otherwise the SADs are sunk into the
+          // (branchy) cost code and all 17 rows of loads stay live
+  #pragma unroll
+          for (int k = 0; k < 16; ++k) asm volatile("" : "+v"(a0[k]), "+v"(a1[k]));
         }
-        // costs are SAD<<5 (dist_scale, JCOST_CALC_SCALEUP): scale once here
-        a[by * 4 + 0] = s0 << 5;
-        a[by * 4 + 1] = s1 << 5;
-        a[by * 4 + 2] = s2 << 5;
-        a[by * 4 + 3] = s3 << 5;
+        const int ox = tx - R;
+        const int candx = cqx + 4 * ox;     // candidate MV (qpel, relative to the block)
+        auto eval_position = [&](const uint32_t (&acc)[16], int oyw) {
+          const int oy = oyw - R;
+          uint32_t ps[kNS];
+          partition_sads(acc, ps);
+          const int lring = max(abs(ox), abs(oy));
+          const int sidx = spiral_index_bl(ox, oy);
+          const int candy = cqy + 4 * oy;
+          const bool is00 = (candx == 0) && (candy == 0);
+          const uint32_t rank = ffs ? ((preseed && is00) ? 0u : (uint32_t)sidx + 1u) : (uint32_t)sidx;
+          const MvCost mc = mv_cost<FFS>(candx, candy, cls_px, cls_py, cls_lam, p.max_mvd);
+          SlotCtx c{mc.mvc, rank, lring, is00, mc.ok, chk00, cls_lam, preseed, rlim, L.slot, candx, candy, p.max_mvd};
+          update_slots<KEY32, FFS, decltype(all_tag)::value, false>(ps, gmask, c, best64, best32);
+        };
+        eval_position(a0, 2 * ty);
+        if (2 * ty + 1 < D) eval_position(a1, 2 * ty + 1);   // odd D: last pair has one position
+        tx += rstep;
+        ty += qstep;
+        if (tx >= D) { tx -= D; ++ty; }
       }
-      // partition SADs (update_full_search_large_blocks order does not
-      // matter: integer sums)
-      uint32_t ps[kNS];
-#pragma unroll
-      for (int k = 0; k < 16; ++k) ps[25 + k] = a[k];                       // 4x4
-#pragma unroll
-      for (int by = 0; by < 4; ++by)
-#pragma unroll
-        for (int h = 0; h < 2; ++h) ps[9 + by * 2 + h] = a[by * 4 + 2 * h] + a[by * 4 + 2 * h + 1];  // 8x4
-#pragma unroll
-      for (int v = 0; v < 2; ++v)
-#pragma unroll
-        for (int bx = 0; bx < 4; ++bx) ps[17 + v * 4 + bx] = a[(2 * v) * 4 + bx] + a[(2 * v + 1) * 4 + bx];  // 4x8
-#pragma unroll
-      for (int v = 0; v < 2; ++v)
-#pragma unroll
-        for (int h = 0; h < 2; ++h) ps[5 + v * 2 + h] = ps[9 + (2 * v) * 2 + h] + ps[9 + (2 * v + 1) * 2 + h];  // 8x8
-      ps[3] = ps[5] + ps[7];
-      ps[4] = ps[6] + ps[8];   // 8x16
-      ps[1] = ps[5] + ps[6];
-      ps[2] = ps[7] + ps[8];   // 16x8
-      ps[0] = ps[1] + ps[2];   // 16x16
+    };
+    if (gmask == kAll) sweep(std::integral_constant<bool, true>{});
+    else sweep(std::integral_constant<bool, false>{});
 
-      const int ox = oxw - R, oy = oyw - R;
-      const int lring = max(abs(ox), abs(oy));
-      const int sidx = spiral_index(ox, oy);
-      const int candx = cqx + 4 * ox;   // candidate MV (qpel, relative to the block)
-      const int candy = cqy + 4 * oy;
-      const bool is00 = (candx == 0) && (candy == 0);
-      const uint32_t rank = ffs ? ((preseed && is00) ? 0u : (uint32_t)sidx + 1u) : (uint32_t)sidx;
-
-      unsigned long long cm = gmask;
-      while (cm) {
-        const int cl = __builtin_ctzll(cm);
-        const unsigned long long cmask = ufl64(L.cls[cl]) & cm;
-        cm &= ~cmask;
-        const int4 cq = L.slot[cl];
-        const int px = ufl(rq_pred_x(cq));
-        const int py = ufl(rq_pred_y(cq));
-        const int lam = ufl(rq_lambda(cq));
-        const int dx = candx - px, dy = candy - py;
-        const uint32_t mvc = (uint32_t)lam * (uint32_t)(mvbits(dx) + mvbits(dy));
-        bool ok = true;
-        if (ffs) ok = max(abs(dx), abs(dy)) < p.max_mvd - 1;   // GetMaxMVD gate, me_fullfast.c:663
+    // ---- workgroup reduction of this group's per-thread minima
 #pragma unroll
-        for (int s = 0; s < kNS; ++s) {
-          if (!((cmask >> s) & 1)) continue;
-          uint32_t m = mvc;
-          if (s == 0 && chk00) {
-            const uint32_t t = 16u * (uint32_t)lam;           // weighted_cost(lambda,16)
-            if (is00) m = m > t ? m - t : 0u;
-          }
-          bool oks = ok;
-          if (ffs && ((rlim >> s) & 1)) {
-            const int rs = ufl(rq_range(L.slot[s]));
-            oks = oks && (lring <= rs || (preseed && is00));
-          }
-          const uint32_t cost = ps[s] + m;
-          if (KEY32 && s >= kKey32First) {
-            const uint32_t k = oks ? ((min(cost, kSat32) << 13) | rank) : ~0u;
-            best32[s - kKey32First] = min(best32[s - kKey32First], k);
-          } else {
-            const unsigned long long k = oks ? (((unsigned long long)cost << 32) | rank) : ~0ull;
-            best64[s] = best64[s] < k ? best64[s] : k;
-          }
-        }
+    for (int s = 0; s < kNS; ++s) {
+      if (!((gmask >> s) & 1)) continue;
+      unsigned long long k;
+      if (KEY32 && s >= kKey32First) {
+        const uint32_t v = best32[s - kKey32First];
+        k = (v == ~0u) ? ~0ull : ((((unsigned long long)(v >> 13)) << 32) | (v & 8191u));
+      } else {
+        k = best64[s];
       }
-    }
-  }
-
-  // ---- workgroup reduction of the per-thread minima
 #pragma unroll
-  for (int s = 0; s < kNS; ++s) {
-    if (!((slot_mask >> s) & 1)) continue;
-    unsigned long long k;
-    if (KEY32 && s >= kKey32First) {
-      uint32_t v = best32[s - kKey32First];
-      k = (v == ~0u) ? ~0ull : ((((unsigned long long)(v >> 13)) << 32) | (v & 8191u) |
-                                 (((v >> 13) == kSat32) ? (1ull << 31) : 0ull));
-    } else {
-      k = best64[s];
-    }
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-      unsigned lo = __shfl_xor((unsigned)k, off, 64);
-      unsigned hi = __shfl_xor((unsigned)(k >> 32), off, 64);
-      unsigned long long o = ((unsigned long long)hi << 32) | lo;
-      k = o < k ? o : k;
-    }
-    if (lane == 0) L.red[wave * kNS + s] = k;
-  }
-  __syncthreads();
-  if (tid < kNS && ((slot_mask >> tid) & 1)) {
-    unsigned long long k = L.red[tid];
-#pragma unroll
-    for (int w = 1; w < kWaves; ++w) { unsigned long long o = L.red[w * kNS + tid]; k = o < k ? o : k; }
-    const int4 q = L.slot[tid];
-    const int cx = ffs ? ffs_cx : rq_cen_x(q);
-    const int cy = ffs ? ffs_cy : rq_cen_y(q);
-    jmme_block_res res;
-    res.reserved = 0;
-    if (k == ~0ull) {
-      // nothing eligible: JM leaves best_pos = 0 and returns the incoming min_mcost
-      res.mv_x = (int16_t)cx; res.mv_y = (int16_t)cy; res.cost = JMME_DISTBLK_MAX;
-    } else {
-      if (KEY32 && tid >= kKey32First && (k & (1ull << 31))) {
-        // every candidate saturated the 32-bit cost field: this unit is redone
-        // with 64-bit keys by the deferred pass (which overwrites all slots)
-        L.flag[0] = 1;
+      for (int off = 32; off >= 1; off >>= 1) {
+        const unsigned lo = __shfl_xor((unsigned)k, off, 64);
+        const unsigned hi = __shfl_xor((unsigned)(k >> 32), off, 64);
+        const unsigned long long o = ((unsigned long long)hi << 32) | lo;
+        k = o < k ? o : k;
       }
-      const uint32_t rank = (uint32_t)(k & 0x7fffffffu);
-      int sidx = ffs ? (int)rank - 1 : (int)rank;
-      int ox, oy;
-      if (ffs && rank == 0) { ox = -(cx >> 2); oy = -(cy >> 2); }   // the pre-seeded (0,0)
-      else spiral_offset(sidx, &ox, &oy);
-      res.mv_x = (int16_t)(cx + 4 * ox);
-      res.mv_y = (int16_t)(cy + 4 * oy);
-      res.cost = (int64_t)(k >> 32);
+      if (lane == 0) L.red[wave * kNS + s] = k;
     }
-    p.out[(size_t)u * kNS + tid] = res;
-  }
-  if (KEY32) {
     __syncthreads();
-    if (tid == 0 && L.flag[0]) p.defer_list[atomicAdd(p.defer_count, 1u)] = u;
+    if (tid < kNS && ((gmask >> tid) & 1)) {
+      unsigned long long k = L.red[tid];
+#pragma unroll
+      for (int w = 1; w < kWaves; ++w) { const unsigned long long o = L.red[w * kNS + tid]; k = o < k ? o : k; }
+      const int cx = cqx, cy = cqy;
+      jmme_block_res res;
+      res.reserved = 0;
+      if (k == ~0ull) {
+        // nothing eligible: JM leaves best_pos = 0 and returns the incoming min_mcost
+        res.mv_x = (int16_t)cx; res.mv_y = (int16_t)cy; res.cost = JMME_DISTBLK_MAX;
+      } else {
+        const uint32_t rank = (uint32_t)(k & 0x7fffffffu);
+        const int sidx = ffs ? (int)rank - 1 : (int)rank;
+        int ox, oy;
+        if (ffs && rank == 0) { ox = -(cx >> 2); oy = -(cy >> 2); }   // the pre-seeded (0,0)
+        else spiral_offset(sidx, &ox, &oy);
+        res.mv_x = (int16_t)(cx + 4 * ox);
+        res.mv_y = (int16_t)(cy + 4 * oy);
+        res.cost = (int64_t)(k >> 32);
+      }
+      p.out[(size_t)u * kNS + tid] = res;
+    }
   }
 }
 
