@@ -62,7 +62,7 @@ __device__ __forceinline__ Lds carve(unsigned char *smem, int R) {
   Lds L;
   L.rows = 2 * R + 16;
   L.wp = (2 * R + 13) | 1;
-  L.rawp = ((2 * R + 16 + 4) + 3) & ~3;
+  L.rawp = 4 * ((3 + 2 * R + 13 + 2) / 4 + 2);
   size_t off = 0;
   L.words = reinterpret_cast<uint32_t *>(smem + off); off += (size_t)L.rows * L.wp * 4;
   off = (off + 15) & ~(size_t)15;
@@ -311,25 +311,45 @@ __device__ __forceinline__ void unit_body(const KParams &p, int u, unsigned char
     const int cls_py = ufl(rq_pred_y(lq));
     const int cls_lam = ufl(rq_lambda(lq));
 
-    // ---- stage the (2R+16)^2 reference window, clamped like UMVLine4X
+    // ---- stage the (2R+16)^2 reference window, clamped like UMVLine4X.
+    // Rows are clamped into the picture; when the window's columns lie
+    // inside the picture each row is fetched as aligned dwords (one round
+    // trip, all loads in flight), else byte by byte with column clamping.
     const int x0 = mb_x + (cqx >> 2) - R;
     const int y0 = mb_y + (cqy >> 2) - R;
     const int wcols = 2 * R + 16;
     const int wrows = 2 * R + 16;
+    const int wpr = 2 * R + 13;                 // words per window row
+    const int xa = x0 & ~3;                     // dword-aligned start (floor)
+    const int sh = x0 - xa;                     // 0..3
+    const int nd = (sh + wpr + 2) / 4 + 1;      // dwords per row that the words need
+    const int rdw = L.rawp >> 2;
+    uint32_t *raw32 = reinterpret_cast<uint32_t *>(L.raw);
     __syncthreads();   // previous group's readers are done with the window
-    for (int i = tid; i < wrows * L.rawp; i += kWG) {
-      int r = i / L.rawp, c = i - r * L.rawp;
-      int gy = clampi(y0 + r, 0, p.height - 1);
-      int gx = clampi(x0 + (c < wcols ? c : wcols - 1), 0, p.width - 1);
-      L.raw[i] = ref[(size_t)gy * p.pitch + gx];
+    if (xa >= 0 && xa + 4 * nd <= p.width) {
+      const int total = wrows * nd;
+#pragma unroll 4
+      for (int i = tid; i < total; i += kWG) {
+        const int r = i / nd, d = i - r * nd;
+        const int gy = clampi(y0 + r, 0, p.height - 1);
+        raw32[r * rdw + d] = *reinterpret_cast<const uint32_t *>(ref + (size_t)gy * p.pitch + xa + 4 * d);
+      }
+    } else {
+      const int rb = 4 * nd;
+      const int total = wrows * rb;
+#pragma unroll 8
+      for (int i = tid; i < total; i += kWG) {
+        const int r = i / rb, c = i - r * rb;
+        const int gy = clampi(y0 + r, 0, p.height - 1);
+        const int gx = clampi(xa + c, 0, p.width - 1);
+        L.raw[r * L.rawp + c] = ref[(size_t)gy * p.pitch + gx];
+      }
     }
     __syncthreads();
-    const int wpr = 2 * R + 13;
     for (int i = tid; i < wrows * wpr; i += kWG) {
-      int r = i / wpr, c = i - r * wpr;
-      const uint32_t *rw = reinterpret_cast<const uint32_t *>(L.raw + (size_t)r * L.rawp);
-      uint32_t lo = rw[c >> 2], hi = rw[(c >> 2) + 1];
-      L.words[r * L.wp + c] = __builtin_amdgcn_alignbyte(hi, lo, c & 3);
+      const int r = i / wpr, c = i - r * wpr + sh;
+      const uint32_t *rw = raw32 + r * rdw;
+      L.words[r * L.wp + (c - sh)] = __builtin_amdgcn_alignbyte(rw[(c >> 2) + 1], rw[c >> 2], c & 3);
     }
     __syncthreads();
 
@@ -482,7 +502,7 @@ __global__ __launch_bounds__(kWG, 1) void me_units_deferred_kernel(KParams p) {
 size_t units_lds_bytes(int R) {
   const int rows = 2 * R + 16;
   const int wp = (2 * R + 13) | 1;
-  const int rawp = ((2 * R + 16 + 4) + 3) & ~3;
+  const int rawp = 4 * ((3 + 2 * R + 13 + 2) / 4 + 2);
   size_t off = (size_t)rows * wp * 4;
   off = (off + 15) & ~(size_t)15;
   off += (size_t)rows * rawp;
