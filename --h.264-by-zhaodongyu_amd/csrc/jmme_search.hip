@@ -322,7 +322,7 @@ __device__ __forceinline__ void unit_body(const KParams &p, int u, unsigned char
     const int wpr = 2 * R + 13;                 // words per window row
     const int xa = x0 & ~3;                     // dword-aligned start (floor)
     const int sh = x0 - xa;                     // 0..3
-    const int nd = (sh + wpr + 2) / 4 + 1;      // dwords per row that the words need
+    const int nd = (sh + wpr + 2) / 4 + 2;      // dwords per row the words read (incl. alignbyte hi)
     const int rdw = L.rawp >> 2;
     uint32_t *raw32 = reinterpret_cast<uint32_t *>(L.raw);
     __syncthreads();   // previous group's readers are done with the window
