@@ -317,7 +317,8 @@ int sync_ref_table(jmme_ctx *ctx, hipStream_t s) {
 }
 
 int launch(jmme_ctx *ctx, int mode, const uint8_t *d_cur, const uint8_t *const *d_ref_table, int pitch,
-           int w, int h, const jmme_mb_req *d_req, int n, jmme_block_res *d_out, hipStream_t s) {
+           int w, int h, const jmme_mb_req *d_req, int n, jmme_block_res *d_out, hipStream_t s,
+           uint32_t *debug_words = nullptr) {
   if (mode != JMME_FULL_SEARCH && mode != JMME_FAST_FULL_SEARCH)
     return fail("search mode %d not supported by the batched engine (FS=-1, FFS=0)", mode);
   if (n < 0) return fail("negative unit count");
@@ -338,6 +339,7 @@ int launch(jmme_ctx *ctx, int mode, const uint8_t *d_cur, const uint8_t *const *
   p.defer_count = ctx->d_defer_count;
   p.defer_list = ctx->d_defer_list;
   p.status = ctx->d_defer_count + 1;
+  p.debug_words = debug_words;
   const bool key32 = p.lds_range <= kKey32MaxRange;
   HIPCHK(hipMemsetAsync(ctx->d_defer_count, 0, 16, s));
   HIPCHK(hipEventRecord(ctx->ev0, s));
@@ -487,4 +489,25 @@ extern "C" jmme_distblk jmme_full_search_block(jmme_ctx *ctx, int list, int ref_
   mv_inout->mv_x = out[s].mv_x;
   mv_inout->mv_y = out[s].mv_y;
   return out[s].cost;
+}
+
+extern "C" int jmme_debug_window(jmme_ctx *ctx, int mode, const jmme_mb_req *req, uint32_t *out, int max_words) {
+  // Test hook: run unit `req` (one unit) and return the first reference
+  // window it staged in LDS (rows x pitch words, word[y][x] = pels x..x+3).
+  if (!ctx) return fail("null ctx");
+  if (validate(ctx, mode, req, 1)) return -1;
+  if (ensure_units(ctx, 1)) return -1;
+  const int R = ctx->cfg.SearchRange;
+  const int words = (2 * R + 16) * ((2 * R + 13) | 1);
+  if (max_words < words) return fail("debug buffer needs %d words", words);
+  uint32_t *d = nullptr;
+  HIPCHK(hipMalloc(&d, (size_t)words * 4));
+  hipStream_t s = nullptr;
+  if (sync_ref_table(ctx, s)) return -1;
+  HIPCHK(hipMemcpy(ctx->d_req, req, sizeof(jmme_mb_req), hipMemcpyHostToDevice));
+  int rc = launch(ctx, mode, ctx->d_cur, ctx->d_ref_table, ctx->pitch, ctx->width, ctx->height, ctx->d_req, 1,
+                  ctx->d_out, s, d);
+  if (rc == 0) HIPCHK(hipMemcpy(out, d, (size_t)words * 4, hipMemcpyDeviceToHost));
+  (void)hipFree(d);
+  return rc;
 }

@@ -352,6 +352,9 @@ __device__ __forceinline__ void unit_body(const KParams &p, int u, unsigned char
       L.words[r * L.wp + (c - sh)] = __builtin_amdgcn_alignbyte(rw[(c >> 2) + 1], rw[c >> 2], c & 3);
     }
     __syncthreads();
+    if (p.debug_words && u == 0 && gmask == (slot_mask & ufl64(L.grp[__builtin_ctzll(slot_mask)]))) {
+      for (int i = tid; i < wrows * L.wp; i += kWG) p.debug_words[i] = L.words[i];
+    }
 
     // ---- sweep all (2R+1)^2 positions of the window.  A task is a vertical
     // pair of positions (x, y), (x, y+1): the 17 reference rows they need are

@@ -223,3 +223,35 @@ def test_requests_outside_contract_are_rejected(gpu):
             me.search(FULL_SEARCH, req)
         with pytest.raises(JmmeError):
             me.upload_ref(0, 1, np.full((144, 176), 300, np.uint16))  # not 8-bit
+
+
+@pytest.mark.parametrize("mb,cen", [((0, 0), (0, 0)), ((16, 0), (0, 0)), ((48, 32), (-12, 8)),
+                                    ((160, 128), (20, 16)), ((80, 64), (400, -400))])
+def test_staged_window_is_the_clamped_reference(mb, cen, gpu):
+    """The LDS window the kernel searches equals the reference clamped into the
+    picture (UMVLine4X over JM's edge-replicated padding, refbuf.h:22-26)."""
+    import ctypes
+    from jmme import FULL_SEARCH, MB_REQ, MotionEstimator, synth, _lib
+    W, H, R = 176, 144, 16
+    luma = synth.luma_sequence(W, H, 2, seed=8)
+    req = np.zeros(1, dtype=MB_REQ)
+    req["mb_x"], req["mb_y"] = mb
+    req["slot_mask"] = 1
+    req["blk"][0, 0]["center_x"], req["blk"][0, 0]["center_y"] = cen
+    req["blk"][0, 0]["search_range"] = R
+    with MotionEstimator({"SearchRange": R, "SearchMode": -1}) as me:
+        me.upload_cur(luma[1])
+        me.upload_ref(0, 0, luma[0])
+        wp = (2 * R + 13) | 1
+        out = np.zeros((2 * R + 16) * wp, np.uint32)
+        _lib.check(_lib.lib().jmme_debug_window(me._ctx, FULL_SEARCH, _lib.ptr(req), _lib.ptr(out), out.size))
+    out = out.reshape(2 * R + 16, wp)
+    x0 = mb[0] + cen[0] // 4 - R
+    y0 = mb[1] + cen[1] // 4 - R
+    ys = np.clip(np.arange(y0, y0 + 2 * R + 16), 0, H - 1)
+    exp = np.zeros((2 * R + 16, 2 * R + 13), np.uint32)
+    for b in range(4):
+        xs = np.clip(np.arange(x0 + b, x0 + b + 2 * R + 13), 0, W - 1)
+        exp |= luma[0][np.ix_(ys, xs)].astype(np.uint32) << np.uint32(8 * b)
+    bad = np.argwhere(out[:, :2 * R + 13] != exp)
+    assert len(bad) == 0, (len(bad), bad[:5].tolist())
