@@ -369,7 +369,7 @@ __device__ __forceinline__ void unit_body(const KParams &p, int u, unsigned char
       int tx = tid % D, ty = tid / D;       // task column, pair row
       for (int t = tid; t < ntask; t += kWG) {
         uint32_t a0[16], a1[16];
-  #pragma unroll
+#pragma unroll
         for (int k = 0; k < 16; ++k) { a0[k] = 0; a1[k] = 0; }
         {
           // opaque zero: keeps the broadcast reads of the current MB inside the
@@ -379,7 +379,7 @@ __device__ __forceinline__ void unit_body(const KParams &p, int u, unsigned char
           const uint4 *cur4 = reinterpret_cast<const uint4 *>(L.cur) + zero;
           const uint32_t *wrow = L.words + (2 * ty) * L.wp + tx;
           uint4 cprev = make_uint4(0, 0, 0, 0);
-  #pragma unroll
+#pragma unroll
           for (int r = 0; r < 17; ++r) {
             const uint32_t *w = wrow + r * L.wp;
             const uint32_t w0 = w[0], w1 = w[4], w2 = w[8], w3 = w[12];
@@ -405,8 +405,11 @@ __device__ __forceinline__ void unit_body(const KParams &p, int u, unsigned char
           }
           // pin the accumulators here: otherwise the SADs are sunk into the
           // (branchy) cost code and all 17 rows of loads stay live
-  #pragma unroll
+#pragma unroll
           for (int k = 0; k < 16; ++k) asm volatile("" : "+v"(a0[k]), "+v"(a1[k]));
+          // costs are SAD<<5 (dist_scale, JCOST_CALC_SCALEUP): scale once here
+#pragma unroll
+          for (int k = 0; k < 16; ++k) { a0[k] <<= 5; a1[k] <<= 5; }
         }
         const int ox = tx - R;
         const int candx = cqx + 4 * ox;     // candidate MV (qpel, relative to the block)
