@@ -107,7 +107,7 @@ __device__ __forceinline__ int xcd_unit(int b, int nb) {
 constexpr unsigned long long kAll = (1ull << kNS) - 1;
 constexpr uint32_t kKey32MaxLambda = 3556;   // lambda*74 + 8x4 SAD<<5 < 2^19: 32-bit keys exact
 
-// the 41 partition SADs (already <<5) from the 16 4x4 SADs; JM sums them in
+// the 41 partition SADs from the 16 4x4 SADs; JM sums them in
 // update_full_search_large_blocks (me_fullfast.c:196-260) -- integer sums, any order
 __device__ __forceinline__ void partition_sads(const uint32_t *a, uint32_t *ps) {
 #pragma unroll
@@ -165,52 +165,41 @@ __device__ __forceinline__ MvCost mv_cost(int candx, int candy, int px, int py, 
   return r;
 }
 
-// PERSLOT: partitions of this window have different predictors; each slot's
-// predictor/lambda is read (LDS broadcast) and its mv cost computed here.
-template <bool KEY32, bool FFS, bool ALL, bool PERSLOT, int NB64, int NB32>
-__device__ __forceinline__ void update_slots_impl(const uint32_t (&ps)[kNS], unsigned long long cmask,
-                                                  const SlotCtx &c, unsigned long long (&best64)[NB64],
-                                                  uint32_t (&best32)[NB32]) {
+// Per-slot minimum update.  ps[] holds UNSCALED partition SADs.
+//  * 32-bit key (slots 9..40 when KEY32): (cost << 13) | rank with
+//    cost = SAD<<5 + mvc  ==  (SAD << 18) + K32,  K32 = (mvc << 13) | rank
+//    (exact: the lambda guard keeps cost < 2^19), i.e. ONE v_lshl_add_u32
+//    and one v_min_u32 per partition;
+//  * 64-bit key otherwise: hi = SAD<<5 + mvc (one v_lshl_add_u32), lo = rank.
+template <bool KEY32, bool FFS, bool ALL, int NB64, int NB32>
+__device__ __forceinline__ void update_slots(const uint32_t (&ps)[kNS], unsigned long long cmask,
+                                             const SlotCtx &c, unsigned long long (&best64)[NB64],
+                                             uint32_t (&best32)[NB32]) {
+  const uint32_t k32 = (c.mvc << 13) | c.rank;
 #pragma unroll
   for (int s = 0; s < kNS; ++s) {
     if (!ALL && !((cmask >> s) & 1)) continue;
-    uint32_t m = c.mvc;
-    int lam = c.lam;
     bool oks = c.ok;
-    if (PERSLOT) {
-      const int4 q = c.slot[s];
-      lam = ufl(rq_lambda(q));
-      const MvCost mc = mv_cost<FFS>(c.candx, c.candy, ufl(rq_pred_x(q)), ufl(rq_pred_y(q)), lam, c.max_mvd);
-      m = mc.mvc;
-      oks = mc.ok;
-    }
-    if (!FFS && s == 0 && c.chk00) {
-      const uint32_t t = 16u * (uint32_t)lam;             // weighted_cost(lambda,16), me_fullsearch.c:80
-      if (c.is00) m = m > t ? m - t : 0u;
-    }
     if (FFS && ((c.rlim >> s) & 1)) {
+      // FFS partition searched over a smaller range than the surface (me_fullfast.c:627)
       const int rs = ufl(rq_range(c.slot[s]));
       oks = oks && (c.lring <= rs || (c.preseed && c.is00));
     }
-    const uint32_t cost = ps[s] + m;
     if (KEY32 && s >= kKey32First) {
-      const uint32_t k = (cost << 13) | c.rank;
-      if (FFS)
-        best32[s - kKey32First] = min(best32[s - kKey32First], oks ? k : ~0u);
-      else
-        best32[s - kKey32First] = min(best32[s - kKey32First], k);
+      const uint32_t k = (ps[s] << 18) + k32;
+      best32[s - kKey32First] = min(best32[s - kKey32First], FFS ? (oks ? k : ~0u) : k);
     } else {
-      const unsigned long long k = ((unsigned long long)cost << 32) | c.rank;
+      uint32_t m = c.mvc;
+      if (!FFS && s == 0 && c.chk00) {
+        const uint32_t t = 16u * (uint32_t)c.lam;           // weighted_cost(lambda,16), me_fullsearch.c:80
+        if (c.is00) m = m > t ? m - t : 0u;
+      }
+      const uint32_t hi = (ps[s] << 5) + m;
+      const unsigned long long k = ((unsigned long long)hi << 32) | c.rank;
       const unsigned long long kk = FFS ? (oks ? k : ~0ull) : k;
       best64[s] = best64[s] < kk ? best64[s] : kk;
     }
   }
-}
-
-template <bool KEY32, bool FFS, bool ALL, bool PERSLOT, int NB64, int NB32>
-__device__ __forceinline__ void update_slots(const uint32_t (&ps)[kNS], unsigned long long cmask, const SlotCtx &c,
-                                             unsigned long long (&best64)[NB64], uint32_t (&best32)[NB32]) {
-  update_slots_impl<KEY32, FFS, ALL, PERSLOT>(ps, cmask, c, best64, best32);
 }
 
 template <bool KEY32, bool FFS>
@@ -317,7 +306,6 @@ __device__ __forceinline__ void unit_body(const KParams &p, int u, unsigned char
     // trip, all loads in flight), else byte by byte with column clamping.
     const int x0 = mb_x + (cqx >> 2) - R;
     const int y0 = mb_y + (cqy >> 2) - R;
-    const int wcols = 2 * R + 16;
     const int wrows = 2 * R + 16;
     const int wpr = 2 * R + 13;                 // words per window row
     const int xa = x0 & ~3;                     // dword-aligned start (floor)
@@ -407,9 +395,6 @@ __device__ __forceinline__ void unit_body(const KParams &p, int u, unsigned char
           // (branchy) cost code and all 17 rows of loads stay live
 #pragma unroll
           for (int k = 0; k < 16; ++k) asm volatile("" : "+v"(a0[k]), "+v"(a1[k]));
-          // costs are SAD<<5 (dist_scale, JCOST_CALC_SCALEUP): scale once here
-#pragma unroll
-          for (int k = 0; k < 16; ++k) { a0[k] <<= 5; a1[k] <<= 5; }
         }
         const int ox = tx - R;
         const int candx = cqx + 4 * ox;     // candidate MV (qpel, relative to the block)
@@ -424,7 +409,7 @@ __device__ __forceinline__ void unit_body(const KParams &p, int u, unsigned char
           const uint32_t rank = ffs ? ((preseed && is00) ? 0u : (uint32_t)sidx + 1u) : (uint32_t)sidx;
           const MvCost mc = mv_cost<FFS>(candx, candy, cls_px, cls_py, cls_lam, p.max_mvd);
           SlotCtx c{mc.mvc, rank, lring, is00, mc.ok, chk00, cls_lam, preseed, rlim, L.slot, candx, candy, p.max_mvd};
-          update_slots<KEY32, FFS, decltype(all_tag)::value, false>(ps, gmask, c, best64, best32);
+          update_slots<KEY32, FFS, decltype(all_tag)::value>(ps, gmask, c, best64, best32);
         };
         eval_position(a0, 2 * ty);
         if (2 * ty + 1 < D) eval_position(a1, 2 * ty + 1);   // odd D: last pair has one position

@@ -11,7 +11,8 @@ import os
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libjmme.so")
+# JMME_LIB: A/B experiments with an alternative in-tree build (lib/variants/...)
+LIB_PATH = os.environ.get("JMME_LIB") or os.path.join(PKG_DIR, "lib", "libjmme.so")
 
 NSLOT = 41
 DISTBLK_MAX = 0x7FFFFFFF << 5
