@@ -314,7 +314,13 @@ __device__ __forceinline__ void unit_body(const KParams &p, int u, unsigned char
     const int rdw = L.rawp >> 2;
     uint32_t *raw32 = reinterpret_cast<uint32_t *>(L.raw);
     __syncthreads();   // previous group's readers are done with the window
-    if (xa >= 0 && xa + 4 * nd <= p.width) {
+#ifdef JMME_ABL_NOSTAGE  // timing ablation only: skip fetching the window
+    constexpr bool kFetch = false;
+#else
+    constexpr bool kFetch = true;
+#endif
+    if (!kFetch) {
+    } else if (xa >= 0 && xa + 4 * nd <= p.width) {
       const int total = wrows * nd;
 #pragma unroll 4
       for (int i = tid; i < total; i += kWG) {
@@ -370,7 +376,12 @@ __device__ __forceinline__ void unit_body(const KParams &p, int u, unsigned char
 #pragma unroll
           for (int r = 0; r < 17; ++r) {
             const uint32_t *w = wrow + r * L.wp;
+#ifdef JMME_ABL_NOLDS    // timing ablation only: no window reads
+            const uint32_t w0 = r * 0x01010101u + tx, w1 = w0 ^ 1, w2 = w0 ^ 2, w3 = w0 ^ 3;
+            (void)w;
+#else
             const uint32_t w0 = w[0], w1 = w[4], w2 = w[8], w3 = w[12];
+#endif
             if (r < 16) {   // row r of the MB against position y
               const uint4 c = cur4[r];
               const int b = (r >> 2) * 4;
@@ -411,8 +422,13 @@ __device__ __forceinline__ void unit_body(const KParams &p, int u, unsigned char
           SlotCtx c{mc.mvc, rank, lring, is00, mc.ok, chk00, cls_lam, preseed, rlim, L.slot, candx, candy, p.max_mvd};
           update_slots<KEY32, FFS, decltype(all_tag)::value>(ps, gmask, c, best64, best32);
         };
+#ifdef JMME_ABL_NOCOST   // timing ablation only: keep the SADs live, skip the cost/minimum work
+#pragma unroll
+        for (int k = 0; k < 16; ++k) asm volatile("" :: "v"(a0[k]), "v"(a1[k]));
+#else
         eval_position(a0, 2 * ty);
         if (2 * ty + 1 < D) eval_position(a1, 2 * ty + 1);   // odd D: last pair has one position
+#endif
         tx += rstep;
         ty += qstep;
         if (tx >= D) { tx -= D; ++ty; }

@@ -1,17 +1,19 @@
 #!/bin/bash
 # PMC counter passes over a short bench run (one rocprofv3 pass per group).
-# Usage (GPU box, repo root): tools/pmc.sh OUTDIR
+# Usage (GPU box, repo root): [JMME_LIB=...] tools/pmc.sh OUTDIR [groups...]
 set -e
-OUT=${1:-gpurun_out/pmc}
+OUT=${1:-gpurun_out/pmc}; shift || true
+GROUPS_=${@:-sq1 sq2 sq3 tcc1 tcc2}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-run() {  # name counters...
-  local name=$1; shift
-  timeout -k 10 240 rocprofv3 --kernel-trace --pmc "$@" --output-format csv -d "$OUT/$name" -o p -- \
-    python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > "$OUT/$name.log" 2>&1
-}
-run sq1 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE
-run sq2 SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD
-run tcc1 FETCH_SIZE
-run tcc2 WRITE_SIZE
+declare -A G
+G[sq1]="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"
+G[sq2]="SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD"
+G[sq3]="SQ_IFETCH SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_INSTS_BRANCH SQ_INST_CYCLES_SALU SQ_ACTIVE_INST_FLAT SQ_INSTS_FLAT SQ_WAVES"
+G[tcc1]="FETCH_SIZE"
+G[tcc2]="WRITE_SIZE"
+for g in $GROUPS_; do
+  timeout -k 10 240 rocprofv3 --kernel-trace --pmc ${G[$g]} --output-format csv -d "$OUT/$g" -o p -- \
+    python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > "$OUT/$g.log" 2>&1 || echo "group $g failed"
+done
 echo pmc done
