@@ -12,21 +12,27 @@
 //
 // Exactness argument.  JM walks the spiral with strict '<' and an early-exit
 // SAD that returns the threshold when it exits (me_distortion.c:384-385), so
-// the result is the lexicographic minimum of (cost, spiral index) over all
+// the result is the lexicographic minimum of (cost, spiral rank) over all
 // eligible candidates.  We evaluate every candidate exhaustively and reduce
 // that key; no early exit, same answer.
 //
-// Work mapping (one workgroup = one MB x ref unit, 256 threads):
-//   * partitions are grouped by identical search window (FS: centre + range;
-//     FFS: the MB's single surface); each group stages its reference window
-//     (2R+16)^2 pels from HBM into LDS once, as "word[y][x] = pels x..x+3" so
-//     every SAD row read is an aligned ds_read_b32;
-//   * each thread takes search positions; for one position it forms the 16
-//     4x4 SADs with v_sad_u8 (4 abs-diffs per lane-op; the current MB row is a
-//     broadcast ds_read_b128), sums them to the 41 partition SADs and updates
-//     a running (cost, rank) minimum per partition in registers;
-//   * partitions that share a predictor share the mv-cost arithmetic;
-//   * at the end a wave shuffle + LDS reduction produces the 41 results.
+// Work mapping (one workgroup = one MB x ref unit, 256 threads = 4 waves):
+//   * partitions are grouped by identical search window and predictor (FS:
+//     centre + range + predictor; FFS: the MB's surface + predictor); each
+//     group stages its reference window (2R+16)^2 pels from HBM into LDS once,
+//     as "word[y][x] = pels x..x+3" so every SAD row read is an aligned
+//     ds_read_b32;
+//   * a thread takes a vertical PAIR of search positions: the 17 reference
+//     rows they need are read once, the 2 x 16 4x4 SADs formed with v_sad_u8
+//     (the current MB row is a broadcast ds_read_b128), summed to the 41
+//     partition SADs, and a running minimum per partition kept in registers;
+//   * key (fast path): 32 bits = cost << 10 | rank >> 3.  cost < 2^22 holds for
+//     every partition while lambda <= kMaxLambda32, so one v_lshl_add_u32 and
+//     one v_min_u32 update a partition.  The 3 dropped rank bits are recovered
+//     exactly afterwards: the winner's rank lies in [8c, 8c+8), and those <= 8
+//     positions are re-evaluated per partition (refine pass);
+//   * key (exact fallback): 64 bits = cost << 32 | rank, for ranges > 44 or
+//     huge lambdas (deferred pass).
 #include <hip/hip_runtime.h>
 #include <type_traits>
 #include "jmme.h"
@@ -39,41 +45,46 @@ namespace {
 
 constexpr int kNS = JMME_NSLOT;
 constexpr int kWaves = kWG / 64;
-constexpr int kKey32First = 9;
+constexpr unsigned long long kAll = (1ull << kNS) - 1;
+constexpr uint32_t kMaxLambda32 = 28450;   // 32*65280 + lambda*74 < 2^22: 22-bit cost field exact
+constexpr int kCostShift = 10;             // key32 = cost << 10 | rank >> 3
+constexpr int kRankDrop = 3;
+constexpr int kCand = 1 << kRankDrop;      // refine candidates per partition
 #ifndef JMME_WAVES_PER_EU
-#define JMME_WAVES_PER_EU 2
-#endif                 // slots 9..40 (8x4, 4x8, 4x4) use 32-bit keys
+#define JMME_WAVES_PER_EU 4
+#endif
 
 struct Lds {
   int wp;        // words per window row
   int rawp;      // bytes per raw row
-  int rows;      // window rows
   uint32_t *words;
   uint8_t *raw;
-  uint32_t *cur;          // 64 words: row r, column group c at [r*4+c]
-  int4 *slot;             // 41 x jmme_block_req
-  unsigned long long *grp;  // per slot: mask of slots sharing its window
-  unsigned long long *cls;  // per slot: mask of slots sharing its predictor/lambda
+  uint32_t *cur;            // 64 words: MB row r, column group c at [r*4+c]
+  int4 *slot;               // 41 x jmme_block_req
+  unsigned long long *grp;  // per slot: mask of slots sharing window AND predictor
   unsigned long long *red;  // kWaves x 41 reduction scratch
+  uint32_t *match;          // 41 x kCand refine flags
   int *flag;                // unit must be redone with 64-bit keys
 };
 
+__host__ __device__ inline int lds_rawp(int R) { return 4 * ((3 + 2 * R + 13 + 2) / 4 + 2); }
+
 __device__ __forceinline__ Lds carve(unsigned char *smem, int R) {
   Lds L;
-  L.rows = 2 * R + 16;
+  const int rows = 2 * R + 16;
   L.wp = (2 * R + 13) | 1;
-  L.rawp = 4 * ((3 + 2 * R + 13 + 2) / 4 + 2);
+  L.rawp = lds_rawp(R);
   size_t off = 0;
-  L.words = reinterpret_cast<uint32_t *>(smem + off); off += (size_t)L.rows * L.wp * 4;
+  L.words = reinterpret_cast<uint32_t *>(smem + off); off += (size_t)rows * L.wp * 4;
   off = (off + 15) & ~(size_t)15;
-  L.raw = smem + off;                                    off += (size_t)L.rows * L.rawp;
+  L.raw = smem + off;                                    off += (size_t)rows * L.rawp;
   off = (off + 15) & ~(size_t)15;
   L.cur = reinterpret_cast<uint32_t *>(smem + off);      off += 64 * 4;
   L.slot = reinterpret_cast<int4 *>(smem + off);         off += kNS * 16;
   L.grp = reinterpret_cast<unsigned long long *>(smem + off); off += kNS * 8;
-  L.cls = reinterpret_cast<unsigned long long *>(smem + off); off += kNS * 8;
   L.red = reinterpret_cast<unsigned long long *>(smem + off); off += kWaves * kNS * 8;
-  L.flag = reinterpret_cast<int *>(smem + off);            off += 16;
+  L.match = reinterpret_cast<uint32_t *>(smem + off);    off += kNS * kCand * 4;
+  L.flag = reinterpret_cast<int *>(smem + off);          off += 16;
   return L;
 }
 
@@ -104,11 +115,8 @@ __device__ __forceinline__ int xcd_unit(int b, int nb) {
   return x * q + (x < r ? x : r) + b / nx;
 }
 
-constexpr unsigned long long kAll = (1ull << kNS) - 1;
-constexpr uint32_t kKey32MaxLambda = 3556;   // lambda*74 + 8x4 SAD<<5 < 2^19: 32-bit keys exact
-
-// the 41 partition SADs from the 16 4x4 SADs; JM sums them in
-// update_full_search_large_blocks (me_fullfast.c:196-260) -- integer sums, any order
+// the 41 partition SADs from the 16 4x4 SADs (JM sums them in
+// update_full_search_large_blocks, me_fullfast.c:196-260 -- integer sums)
 __device__ __forceinline__ void partition_sads(const uint32_t *a, uint32_t *ps) {
 #pragma unroll
   for (int k = 0; k < 16; ++k) ps[25 + k] = a[k];                                           // 4x4
@@ -142,17 +150,6 @@ __device__ __forceinline__ int spiral_index_bl(int ox, int oy) {
   return l == 0 ? 0 : v;
 }
 
-struct SlotCtx {
-  uint32_t mvc, rank;
-  int lring;
-  bool is00, ok;
-  int chk00, lam;
-  bool preseed;
-  unsigned long long rlim;
-  const int4 *slot;
-  int candx, candy, max_mvd;
-};
-
 // mv cost lambda*(mvbits[dx]+mvbits[dy]) of candidate (candx, candy) against
 // predictor (px, py), mv_search.h:100-104; GetMaxMVD gate for FFS.
 struct MvCost { uint32_t mvc; bool ok; };
@@ -165,65 +162,99 @@ __device__ __forceinline__ MvCost mv_cost(int candx, int candy, int px, int py, 
   return r;
 }
 
-// Per-slot minimum update.  ps[] holds UNSCALED partition SADs.
-//  * 32-bit key (slots 9..40 when KEY32): (cost << 13) | rank with
-//    cost = SAD<<5 + mvc  ==  (SAD << 18) + K32,  K32 = (mvc << 13) | rank
-//    (exact: the lambda guard keeps cost < 2^19), i.e. ONE v_lshl_add_u32
-//    and one v_min_u32 per partition;
-//  * 64-bit key otherwise: hi = SAD<<5 + mvc (one v_lshl_add_u32), lo = rank.
-template <bool KEY32, bool FFS, bool ALL, int NB64, int NB32>
-__device__ __forceinline__ void update_slots(const uint32_t (&ps)[kNS], unsigned long long cmask,
-                                             const SlotCtx &c, unsigned long long (&best64)[NB64],
-                                             uint32_t (&best32)[NB32]) {
-  const uint32_t k32 = (c.mvc << 13) | c.rank;
+// check_for_00 (me_fullsearch.c:61,78-82): at the (0,0) vector subtract
+// weighted_cost(lambda,16), floored at 0.
+__device__ __forceinline__ uint32_t check00_adjust(uint32_t mvc, int lam, bool is00) {
+  const uint32_t t = 16u * (uint32_t)lam;
+  return is00 ? (mvc > t ? mvc - t : 0u) : mvc;
+}
+
+// what a position contributes, shared by all partitions of the group
+struct PosCtx {
+  uint32_t mvc, mvc0, rank;   // mvc0: slot 0's cost after check_for_00
+  int lring;
+  bool is00, ok;
+};
+
+struct GroupCtx {
+  int R, cqx, cqy, px, py, lam, chk00, max_mvd;
+  bool preseed;
+  unsigned long long gmask, rlim;
+  const int4 *slot;
+};
+
+// FFS partition searched over a smaller range than the surface (me_fullfast.c:627)
+template <bool FFS>
+__device__ __forceinline__ bool slot_eligible(const GroupCtx &g, const PosCtx &c, int s) {
+  if (!FFS) return true;
+  bool oks = c.ok;
+  if ((g.rlim >> s) & 1) {
+    const int rs = ufl(rq_range(g.slot[s]));
+    oks = oks && (c.lring <= rs || (g.preseed && c.is00));
+  }
+  return oks;
+}
+
+template <bool KEY32, bool FFS, bool ALL, typename Best>
+__device__ __forceinline__ void update_slots(const uint32_t (&ps)[kNS], const GroupCtx &g, const PosCtx &c,
+                                             Best (&best)[kNS]) {
+  if (KEY32) {
+    const uint32_t k32 = (c.mvc << kCostShift) | (c.rank >> kRankDrop);
+    const uint32_t k32_0 = (c.mvc0 << kCostShift) | (c.rank >> kRankDrop);
 #pragma unroll
-  for (int s = 0; s < kNS; ++s) {
-    if (!ALL && !((cmask >> s) & 1)) continue;
-    bool oks = c.ok;
-    if (FFS && ((c.rlim >> s) & 1)) {
-      // FFS partition searched over a smaller range than the surface (me_fullfast.c:627)
-      const int rs = ufl(rq_range(c.slot[s]));
-      oks = oks && (c.lring <= rs || (c.preseed && c.is00));
+    for (int s = 0; s < kNS; ++s) {
+      if (!ALL && !((g.gmask >> s) & 1)) continue;
+      // cost<<10 | rank>>3  ==  (SAD << 15) + ((mvc << 10) | rank >> 3)
+      const uint32_t k = (ps[s] << (5 + kCostShift)) + (s == 0 ? k32_0 : k32);
+      const uint32_t kk = FFS ? (slot_eligible<FFS>(g, c, s) ? k : ~0u) : k;
+      best[s] = min((uint32_t)best[s], kk);
     }
-    if (KEY32 && s >= kKey32First) {
-      const uint32_t k = (ps[s] << 18) + k32;
-      best32[s - kKey32First] = min(best32[s - kKey32First], FFS ? (oks ? k : ~0u) : k);
-    } else {
-      uint32_t m = c.mvc;
-      if (!FFS && s == 0 && c.chk00) {
-        const uint32_t t = 16u * (uint32_t)c.lam;           // weighted_cost(lambda,16), me_fullsearch.c:80
-        if (c.is00) m = m > t ? m - t : 0u;
-      }
-      const uint32_t hi = (ps[s] << 5) + m;
+  } else {
+#pragma unroll
+    for (int s = 0; s < kNS; ++s) {
+      if (!ALL && !((g.gmask >> s) & 1)) continue;
+      const uint32_t hi = (ps[s] << 5) + (s == 0 ? c.mvc0 : c.mvc);
       const unsigned long long k = ((unsigned long long)hi << 32) | c.rank;
-      const unsigned long long kk = FFS ? (oks ? k : ~0ull) : k;
-      best64[s] = best64[s] < kk ? best64[s] : kk;
+      const unsigned long long kk = FFS ? (slot_eligible<FFS>(g, c, s) ? k : ~0ull) : k;
+      best[s] = best[s] < kk ? best[s] : kk;
     }
   }
 }
 
+// exact SAD of partition s at window offset (oxw, oyw), for the refine pass
+__device__ __forceinline__ uint32_t partition_sad_at(const Lds &L, int s, int oxw, int oyw) {
+  const SlotGeom gm = slot_geom(s);
+  uint32_t sad = 0;
+  for (int r = 0; r < 4 * gm.h; ++r) {
+    const int row = gm.by * 4 + r;
+    const uint32_t *w = L.words + (oyw + row) * L.wp + oxw + gm.bx * 4;
+    for (int c = 0; c < gm.w; ++c) sad = __builtin_amdgcn_sad_u8(w[4 * c], L.cur[row * 4 + gm.bx + c], sad);
+  }
+  return sad;
+}
+
 template <bool KEY32, bool FFS>
 __device__ __forceinline__ void unit_body(const KParams &p, int u, unsigned char *smem) {
+  using Best = typename std::conditional<KEY32, uint32_t, unsigned long long>::type;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  constexpr bool ffs = FFS;
 
   const jmme_mb_req *rq = p.req + u;
   const int mb_x = ufl(rq->mb_x);
   const int mb_y = ufl(rq->mb_y);
   const int list = ufl(rq->list);
   const int ref_idx = ufl(rq->ref_idx);
-  const unsigned long long slot_mask = ufl64(rq->slot_mask) & ((1ull << kNS) - 1);
+  const unsigned long long slot_mask = ufl64(rq->slot_mask) & kAll;
   const int ffs_cx = ufl(rq->ffs_center_x);
   const int ffs_cy = ufl(rq->ffs_center_y);
   const int ffs_range = ufl(rq->ffs_range);
-  const bool preseed = ffs && ufl(rq->ffs_pos00_valid) != 0;
+  const bool preseed = FFS && ufl(rq->ffs_pos00_valid) != 0;
   const uint8_t *ref = p.refs[list * kMaxRefs + ref_idx];
 
   Lds L = carve(smem, p.lds_range);
 
-  // ---- unit setup: slot requests, window groups, predictor classes, current MB
+  // ---- unit setup: slot requests, groups, current MB
   if (tid < kNS) {
     const int4 *src = reinterpret_cast<const int4 *>(&rq->blk[0]);
     L.slot[tid] = src[tid];
@@ -235,77 +266,70 @@ __device__ __forceinline__ void unit_body(const KParams &p, int u, unsigned char
   }
   __syncthreads();
   if (tid < kNS) {
-    int4 me = L.slot[tid];
-    unsigned long long g = 0, c = 0;
+    const int4 me = L.slot[tid];
+    unsigned long long g = 0;
     if ((slot_mask >> tid) & 1) {
       for (int t = 0; t < kNS; ++t) {
         if (!((slot_mask >> t) & 1)) continue;
-        int4 o = L.slot[t];
+        const int4 o = L.slot[t];
         // a group = partitions with the same search window AND the same
         // predictor/lambda: one SAD sweep and one mv-cost per position serve
         // the whole group (a window with several predictors is swept once per
         // predictor -- straight-line code, no per-partition predictor loads)
-        bool same_win = ffs || (o.y == me.y && rq_range(o) == rq_range(me));
-        bool same_cls = same_win && o.x == me.x && o.w == me.w;
-        g |= (unsigned long long)same_cls << t;
-        c |= (unsigned long long)same_win << t;
+        const bool same_win = FFS || (o.y == me.y && rq_range(o) == rq_range(me));
+        g |= (unsigned long long)(same_win && o.x == me.x && o.w == me.w) << t;
       }
+      if (KEY32 && (uint32_t)rq_lambda(me) > kMaxLambda32) L.flag[0] = 1;
     }
     L.grp[tid] = g;
-    L.cls[tid] = c;
-    // 32-bit keys are exact only while lambda*74 + SAD<<5 < 2^19 (kKey32MaxLambda)
-    if (KEY32 && ((slot_mask >> tid) & 1) && (uint32_t)rq_lambda(me) > kKey32MaxLambda) L.flag[0] = 1;
   }
   __syncthreads();
   if (KEY32 && ufl(L.flag[0])) {
-    // redo the whole unit with 64-bit keys in the deferred pass
+    // the 22-bit cost field could overflow: redo the whole unit with 64-bit keys
     if (tid == 0) p.defer_list[atomicAdd(p.defer_count, 1u)] = u;
     return;
   }
 
-  // One pass per search window (group of partitions sharing it): stage the
-  // window, sweep it, reduce and write that group's results.  Nothing is
-  // carried from one group to the next.
+  // One pass per group: stage the window, sweep it, reduce, (refine), write.
+  // Nothing is carried from one group to the next.
   unsigned long long remaining = slot_mask;
   while (remaining) {
     const int lead = __builtin_ctzll(remaining);
     const unsigned long long gmask = ufl64(L.grp[lead]) & remaining;
     remaining &= ~gmask;
-    // per-thread running minima of the (cost, rank) keys
-    unsigned long long best64[KEY32 ? kKey32First : kNS];
-    uint32_t best32[KEY32 ? kNS - kKey32First : 1];
-#pragma unroll
-    for (int s = 0; s < (KEY32 ? kKey32First : kNS); ++s) best64[s] = ~0ull;
-#pragma unroll
-    for (int s = 0; s < (KEY32 ? kNS - kKey32First : 1); ++s) best32[s] = ~0u;
     const int4 lq = L.slot[lead];
-    const int cqx = ufl(ffs ? ffs_cx : rq_cen_x(lq));   // window centre, qpel (multiple of 4)
-    const int cqy = ufl(ffs ? ffs_cy : rq_cen_y(lq));
-    const int R = ufl(ffs ? ffs_range : rq_range(lq));
-    if (R < 0 || R > p.lds_range || ((cqx | cqy) & 3)) {
+    GroupCtx g;
+    g.cqx = ufl(FFS ? ffs_cx : rq_cen_x(lq));   // window centre, qpel (multiple of 4)
+    g.cqy = ufl(FFS ? ffs_cy : rq_cen_y(lq));
+    g.R = ufl(FFS ? ffs_range : rq_range(lq));
+    g.px = ufl(rq_pred_x(lq));
+    g.py = ufl(rq_pred_y(lq));
+    g.lam = ufl(rq_lambda(lq));
+    g.max_mvd = p.max_mvd;
+    g.preseed = preseed;
+    g.gmask = gmask;
+    g.slot = L.slot;
+    const int R = g.R;
+    if (R < 0 || R > p.lds_range || ((g.cqx | g.cqy) & 3)) {
       // outside what this launch was sized for (or a sub-pel-grid centre):
       // refuse loudly instead of overrunning LDS; the host reports it
       if (tid == 0) atomicOr(p.status, (R < 0 || R > p.lds_range) ? 1u : 2u);
       continue;
     }
-    // FFS: partitions searched over a smaller range than the surface (me_fullfast.c:627)
-    unsigned long long rlim = 0;
-    if (ffs) {
+    g.rlim = 0;
+    if (FFS) {
       for (int t = 0; t < kNS; ++t)
-        if ((gmask >> t) & 1) rlim |= (unsigned long long)(rq_range(L.slot[t]) < R) << t;
-      rlim = ufl64(rlim);
+        if ((gmask >> t) & 1) g.rlim |= (unsigned long long)(rq_range(L.slot[t]) < R) << t;
+      g.rlim = ufl64(g.rlim);
     }
-    const int chk00 = ufl((!ffs && (gmask & 1)) ? (rq_flags(L.slot[0]) & JMME_BLK_CHECK00) : 0);
-    const int cls_px = ufl(rq_pred_x(lq));
-    const int cls_py = ufl(rq_pred_y(lq));
-    const int cls_lam = ufl(rq_lambda(lq));
+    g.chk00 = ufl((!FFS && (gmask & 1)) ? (rq_flags(L.slot[0]) & JMME_BLK_CHECK00) : 0);
 
     // ---- stage the (2R+16)^2 reference window, clamped like UMVLine4X.
-    // Rows are clamped into the picture; when the window's columns lie
-    // inside the picture each row is fetched as aligned dwords (one round
-    // trip, all loads in flight), else byte by byte with column clamping.
-    const int x0 = mb_x + (cqx >> 2) - R;
-    const int y0 = mb_y + (cqy >> 2) - R;
+    // Rows are clamped into the picture; when the window's columns lie inside
+    // the picture each row is fetched as aligned dwords (one round trip, all
+    // loads in flight), else byte by byte with column clamping.
+    const int x0 = mb_x + (g.cqx >> 2) - R;
+    const int y0 = mb_y + (g.cqy >> 2) - R;
     const int wrows = 2 * R + 16;
     const int wpr = 2 * R + 13;                 // words per window row
     const int xa = x0 & ~3;                     // dword-aligned start (floor)
@@ -350,11 +374,15 @@ __device__ __forceinline__ void unit_body(const KParams &p, int u, unsigned char
       for (int i = tid; i < wrows * L.wp; i += kWG) p.debug_words[i] = L.words[i];
     }
 
+    // per-thread running minima of the keys
+    Best best[kNS];
+#pragma unroll
+    for (int s = 0; s < kNS; ++s) best[s] = (Best)~0ull;
+
     // ---- sweep all (2R+1)^2 positions of the window.  A task is a vertical
     // pair of positions (x, y), (x, y+1): the 17 reference rows they need are
-    // read from LDS once and feed both (halves the LDS traffic per position).
-    // the sweep, specialised for a window that serves all 41 partitions (no
-    // per-partition mask tests) or a subset
+    // read from LDS once and feed both.  Specialised for a group that is all
+    // 41 partitions (no per-partition mask tests) or a subset.
     auto sweep = [&](auto all_tag) {
       const int D = 2 * R + 1;
       const int DP = (D + 1) >> 1;          // position pairs per column
@@ -398,9 +426,9 @@ __device__ __forceinline__ void unit_body(const KParams &p, int u, unsigned char
               a1[b + 3] = __builtin_amdgcn_sad_u8(w3, cprev.w, a1[b + 3]);
             }
             if (r < 16) cprev = cur4[r];
-            // bound the scheduler's look-ahead: a few rows of loads in flight,
-            // not all 17 (which would pin ~140 VGPRs)
+#ifdef JMME_SAD_SCHED_BARRIER
             if ((r & 1) == 1) __builtin_amdgcn_sched_barrier(0);
+#endif
           }
           // pin the accumulators here: otherwise the SADs are sunk into the
           // (branchy) cost code and all 17 rows of loads stay live
@@ -408,23 +436,27 @@ __device__ __forceinline__ void unit_body(const KParams &p, int u, unsigned char
           for (int k = 0; k < 16; ++k) asm volatile("" : "+v"(a0[k]), "+v"(a1[k]));
         }
         const int ox = tx - R;
-        const int candx = cqx + 4 * ox;     // candidate MV (qpel, relative to the block)
+        const int candx = g.cqx + 4 * ox;     // candidate MV (qpel, relative to the block)
         auto eval_position = [&](const uint32_t (&acc)[16], int oyw) {
           const int oy = oyw - R;
           uint32_t ps[kNS];
           partition_sads(acc, ps);
-          const int lring = max(abs(ox), abs(oy));
+          PosCtx c;
+          c.lring = max(abs(ox), abs(oy));
           const int sidx = spiral_index_bl(ox, oy);
-          const int candy = cqy + 4 * oy;
-          const bool is00 = (candx == 0) && (candy == 0);
-          const uint32_t rank = ffs ? ((preseed && is00) ? 0u : (uint32_t)sidx + 1u) : (uint32_t)sidx;
-          const MvCost mc = mv_cost<FFS>(candx, candy, cls_px, cls_py, cls_lam, p.max_mvd);
-          SlotCtx c{mc.mvc, rank, lring, is00, mc.ok, chk00, cls_lam, preseed, rlim, L.slot, candx, candy, p.max_mvd};
-          update_slots<KEY32, FFS, decltype(all_tag)::value>(ps, gmask, c, best64, best32);
+          const int candy = g.cqy + 4 * oy;
+          c.is00 = (candx == 0) && (candy == 0);
+          c.rank = FFS ? ((g.preseed && c.is00) ? 0u : (uint32_t)sidx + 1u) : (uint32_t)sidx;
+          const MvCost mc = mv_cost<FFS>(candx, candy, g.px, g.py, g.lam, g.max_mvd);
+          c.mvc = mc.mvc;
+          c.ok = mc.ok;
+          c.mvc0 = g.chk00 ? check00_adjust(mc.mvc, g.lam, c.is00) : mc.mvc;
+          update_slots<KEY32, FFS, decltype(all_tag)::value>(ps, g, c, best);
         };
 #ifdef JMME_ABL_NOCOST   // timing ablation only: keep the SADs live, skip the cost/minimum work
 #pragma unroll
         for (int k = 0; k < 16; ++k) asm volatile("" :: "v"(a0[k]), "v"(a1[k]));
+        (void)eval_position;
 #else
         eval_position(a0, 2 * ty);
         if (2 * ty + 1 < D) eval_position(a1, 2 * ty + 1);   // odd D: last pair has one position
@@ -441,42 +473,104 @@ __device__ __forceinline__ void unit_body(const KParams &p, int u, unsigned char
 #pragma unroll
     for (int s = 0; s < kNS; ++s) {
       if (!((gmask >> s) & 1)) continue;
-      unsigned long long k;
-      if (KEY32 && s >= kKey32First) {
-        const uint32_t v = best32[s - kKey32First];
-        k = (v == ~0u) ? ~0ull : ((((unsigned long long)(v >> 13)) << 32) | (v & 8191u));
-      } else {
-        k = best64[s];
-      }
+      Best k = best[s];
 #pragma unroll
       for (int off = 32; off >= 1; off >>= 1) {
-        const unsigned lo = __shfl_xor((unsigned)k, off, 64);
-        const unsigned hi = __shfl_xor((unsigned)(k >> 32), off, 64);
-        const unsigned long long o = ((unsigned long long)hi << 32) | lo;
-        k = o < k ? o : k;
+        if (KEY32) {
+          const uint32_t o = __shfl_xor((uint32_t)k, off, 64);
+          k = min((uint32_t)k, o);
+        } else {
+          const unsigned lo = __shfl_xor((unsigned)k, off, 64);
+          const unsigned hi = __shfl_xor((unsigned)((unsigned long long)k >> 32), off, 64);
+          const unsigned long long o = ((unsigned long long)hi << 32) | lo;
+          k = o < (unsigned long long)k ? o : k;
+        }
       }
-      if (lane == 0) L.red[wave * kNS + s] = k;
+      if (lane == 0) L.red[wave * kNS + s] = (unsigned long long)k;
     }
     __syncthreads();
-    if (tid < kNS && ((gmask >> tid) & 1)) {
+    if (tid < kNS) {
       unsigned long long k = L.red[tid];
 #pragma unroll
       for (int w = 1; w < kWaves; ++w) { const unsigned long long o = L.red[w * kNS + tid]; k = o < k ? o : k; }
-      const int cx = cqx, cy = cqy;
+      L.red[tid] = k;   // wave 0's row now holds the group result
+    }
+    __syncthreads();
+
+    // ---- refine (32-bit keys): recover the 3 rank bits the key dropped.
+    // The winner has cost == key>>10 and rank in [8c, 8c+8), c = key & 1023;
+    // re-evaluate those positions exactly and take the smallest matching rank.
+    if (KEY32) {
+      const int D = 2 * R + 1;
+      for (int item = tid; item < kNS * kCand; item += kWG) {
+        const int s = item / kCand, j = item - s * kCand;
+        uint32_t m = 0;
+        const uint32_t key = (uint32_t)L.red[s];
+        if (((gmask >> s) & 1) && key != ~0u) {
+          const uint32_t mincost = key >> kCostShift;
+          const int rk = (int)(((key & ((1u << kCostShift) - 1)) << kRankDrop) + j);
+          int ox = 0, oy = 0;
+          bool valid;
+          if (FFS && rk == 0) {          // the pre-seeded (0,0) vector
+            ox = -(g.cqx >> 2); oy = -(g.cqy >> 2);
+            valid = g.preseed && abs(ox) <= R && abs(oy) <= R;
+          } else {
+            const int sidx = FFS ? rk - 1 : rk;
+            valid = sidx < D * D;
+            if (valid) spiral_offset(sidx, &ox, &oy);
+          }
+          if (valid) {
+            const int candx = g.cqx + 4 * ox, candy = g.cqy + 4 * oy;
+            PosCtx c;
+            c.is00 = (candx == 0) && (candy == 0);
+            c.lring = max(abs(ox), abs(oy));
+            const int sidx = spiral_index(ox, oy);
+            c.rank = FFS ? ((g.preseed && c.is00) ? 0u : (uint32_t)sidx + 1u) : (uint32_t)sidx;
+            const MvCost mc = mv_cost<FFS>(candx, candy, g.px, g.py, g.lam, g.max_mvd);
+            c.ok = mc.ok;
+            const uint32_t mv = (s == 0 && g.chk00) ? check00_adjust(mc.mvc, g.lam, c.is00) : mc.mvc;
+            const uint32_t cost = (partition_sad_at(L, s, ox + R, oy + R) << 5) + mv;
+            m = (c.rank == (uint32_t)rk) && cost == mincost && slot_eligible<FFS>(g, c, s);
+          }
+        }
+        L.match[item] = m;
+      }
+      __syncthreads();
+    }
+
+    // ---- results of this group
+    if (tid < kNS && ((gmask >> tid) & 1)) {
+      const unsigned long long k = L.red[tid];
       jmme_block_res res;
       res.reserved = 0;
-      if (k == ~0ull) {
+      uint32_t rank = 0, cost = 0;
+      bool found = false;
+      if (KEY32) {
+        const uint32_t key = (uint32_t)k;
+        if (key != ~0u) {
+          for (int j = 0; j < kCand && !found; ++j)
+            if (L.match[tid * kCand + j]) {
+              found = true;
+              rank = ((key & ((1u << kCostShift) - 1)) << kRankDrop) + j;
+            }
+          cost = key >> kCostShift;
+          if (!found) atomicOr(p.status, 4u);   // cannot happen: refine lost the winner
+        }
+      } else if (k != ~0ull) {
+        found = true;
+        rank = (uint32_t)(k & 0x7fffffffu);
+        cost = (uint32_t)(k >> 32);
+      }
+      if (!found) {
         // nothing eligible: JM leaves best_pos = 0 and returns the incoming min_mcost
-        res.mv_x = (int16_t)cx; res.mv_y = (int16_t)cy; res.cost = JMME_DISTBLK_MAX;
+        res.mv_x = (int16_t)g.cqx; res.mv_y = (int16_t)g.cqy; res.cost = JMME_DISTBLK_MAX;
       } else {
-        const uint32_t rank = (uint32_t)(k & 0x7fffffffu);
-        const int sidx = ffs ? (int)rank - 1 : (int)rank;
         int ox, oy;
-        if (ffs && rank == 0) { ox = -(cx >> 2); oy = -(cy >> 2); }   // the pre-seeded (0,0)
-        else spiral_offset(sidx, &ox, &oy);
-        res.mv_x = (int16_t)(cx + 4 * ox);
-        res.mv_y = (int16_t)(cy + 4 * oy);
-        res.cost = (int64_t)(k >> 32);
+        if (FFS && rank == 0) { ox = -(g.cqx >> 2); oy = -(g.cqy >> 2); }   // the pre-seeded (0,0)
+        else spiral_offset(FFS ? (int)rank - 1 : (int)rank, &ox, &oy);
+        res.mv_x = (int16_t)(g.cqx + 4 * ox);
+        res.mv_y = (int16_t)(g.cqy + 4 * oy);
+        res.cost = (int64_t)cost;
       }
       p.out[(size_t)u * kNS + tid] = res;
     }
@@ -485,7 +579,7 @@ __device__ __forceinline__ void unit_body(const KParams &p, int u, unsigned char
 
 // direct pass: one workgroup per unit (XCD-aware order)
 template <bool KEY32, bool FFS>
-__global__ __launch_bounds__(kWG, JMME_WAVES_PER_EU) void me_units_kernel(KParams p) {
+__global__ __launch_bounds__(kWG, KEY32 ? JMME_WAVES_PER_EU : 2) void me_units_kernel(KParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int u = xcd_unit(blockIdx.x, gridDim.x);
   if (u >= p.n) return;
@@ -493,7 +587,7 @@ __global__ __launch_bounds__(kWG, JMME_WAVES_PER_EU) void me_units_kernel(KParam
 }
 
 // deferred pass (64-bit keys): a small grid drains the device-side list of
-// units whose 32-bit keys saturated; every workgroup exits when the list ends
+// units the 32-bit pass could not take; every workgroup exits when the list ends
 template <bool FFS>
 __global__ __launch_bounds__(kWG, 1) void me_units_deferred_kernel(KParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -509,12 +603,11 @@ __global__ __launch_bounds__(kWG, 1) void me_units_deferred_kernel(KParams p) {
 size_t units_lds_bytes(int R) {
   const int rows = 2 * R + 16;
   const int wp = (2 * R + 13) | 1;
-  const int rawp = 4 * ((3 + 2 * R + 13 + 2) / 4 + 2);
   size_t off = (size_t)rows * wp * 4;
   off = (off + 15) & ~(size_t)15;
-  off += (size_t)rows * rawp;
+  off += (size_t)rows * lds_rawp(R);
   off = (off + 15) & ~(size_t)15;
-  off += 64 * 4 + kNS * 16 + 2 * kNS * 8 + kWaves * kNS * 8 + 16;
+  off += 64 * 4 + kNS * 16 + kNS * 8 + kWaves * kNS * 8 + kNS * kCand * 4 + 16;
   return off;
 }
 
