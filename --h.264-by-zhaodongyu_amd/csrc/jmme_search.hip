@@ -400,18 +400,34 @@ __device__ __forceinline__ void unit_body(const KParams &p, int u, unsigned char
           asm volatile("v_mov_b32 %0, 0" : "=v"(zero));
           const uint4 *cur4 = reinterpret_cast<const uint4 *>(L.cur) + zero;
           const uint32_t *wrow = L.words + (2 * ty) * L.wp + tx;
+          // software pipeline, one row ahead: row r+1's reference words and MB
+          // row are requested before row r's v_sad_u8s, so each LDS round trip
+          // hides behind a row of arithmetic (and the other waves of the SIMD)
+          uint32_t n0, n1, n2, n3;
+          uint4 cn;
+#ifdef JMME_ABL_NOLDS    // timing ablation only: no window reads
+          n0 = tx; n1 = n0 ^ 1; n2 = n0 ^ 2; n3 = n0 ^ 3;
+#else
+          n0 = wrow[0]; n1 = wrow[4]; n2 = wrow[8]; n3 = wrow[12];
+#endif
+          cn = cur4[0];
           uint4 cprev = make_uint4(0, 0, 0, 0);
 #pragma unroll
           for (int r = 0; r < 17; ++r) {
-            const uint32_t *w = wrow + r * L.wp;
-#ifdef JMME_ABL_NOLDS    // timing ablation only: no window reads
-            const uint32_t w0 = r * 0x01010101u + tx, w1 = w0 ^ 1, w2 = w0 ^ 2, w3 = w0 ^ 3;
-            (void)w;
+            const uint32_t w0 = n0, w1 = n1, w2 = n2, w3 = n3;
+            const uint4 c = cn;
+            if (r < 16) {
+              const uint32_t *w = wrow + (r + 1) * L.wp;
+#ifdef JMME_ABL_NOLDS
+              n0 = (r + 1) * 0x01010101u + tx; n1 = n0 ^ 1; n2 = n0 ^ 2; n3 = n0 ^ 3;
+              (void)w;
 #else
-            const uint32_t w0 = w[0], w1 = w[4], w2 = w[8], w3 = w[12];
+              n0 = w[0]; n1 = w[4]; n2 = w[8]; n3 = w[12];
 #endif
+              if (r < 15) cn = cur4[r + 1];
+            }
+            __builtin_amdgcn_sched_barrier(0);
             if (r < 16) {   // row r of the MB against position y
-              const uint4 c = cur4[r];
               const int b = (r >> 2) * 4;
               a0[b + 0] = __builtin_amdgcn_sad_u8(w0, c.x, a0[b + 0]);
               a0[b + 1] = __builtin_amdgcn_sad_u8(w1, c.y, a0[b + 1]);
@@ -425,10 +441,8 @@ __device__ __forceinline__ void unit_body(const KParams &p, int u, unsigned char
               a1[b + 2] = __builtin_amdgcn_sad_u8(w2, cprev.z, a1[b + 2]);
               a1[b + 3] = __builtin_amdgcn_sad_u8(w3, cprev.w, a1[b + 3]);
             }
-            if (r < 16) cprev = cur4[r];
-#ifdef JMME_SAD_SCHED_BARRIER
-            if ((r & 1) == 1) __builtin_amdgcn_sched_barrier(0);
-#endif
+            cprev = c;
+            __builtin_amdgcn_sched_barrier(0);
           }
           // pin the accumulators here: otherwise the SADs are sunk into the
           // (branchy) cost code and all 17 rows of loads stay live
