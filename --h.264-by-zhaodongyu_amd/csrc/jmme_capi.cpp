@@ -53,6 +53,8 @@ struct jmme_ctx {
   jmme_mb_req *d_req = nullptr;
   jmme_block_res *d_out = nullptr;
   size_t cap_units = 0;
+  unsigned long long *d_stamps = nullptr;    // diagnostic builds only
+  size_t cap_stamps = 0;
   unsigned *d_defer_count = nullptr;         // [0] defer count, [1] status
   int *d_defer_list = nullptr;
   size_t cap_defer = 0;
@@ -340,6 +342,14 @@ int launch(jmme_ctx *ctx, int mode, const uint8_t *d_cur, const uint8_t *const *
   p.defer_list = ctx->d_defer_list;
   p.status = ctx->d_defer_count + 1;
   p.debug_words = debug_words;
+#ifdef JMME_STAMPS
+  if ((size_t)n > ctx->cap_stamps) {
+    (void)hipFree(ctx->d_stamps);
+    HIPCHK(hipMalloc(&ctx->d_stamps, (size_t)n * 8 * sizeof(unsigned long long)));
+    ctx->cap_stamps = (size_t)n;
+  }
+  p.stamps = ctx->d_stamps;
+#endif
   const bool key32 = p.lds_range <= kKey32MaxRange;
   HIPCHK(hipMemsetAsync(ctx->d_defer_count, 0, 16, s));
   HIPCHK(hipEventRecord(ctx->ev0, s));
@@ -510,4 +520,15 @@ extern "C" int jmme_debug_window(jmme_ctx *ctx, int mode, const jmme_mb_req *req
   if (rc == 0) HIPCHK(hipMemcpy(out, d, (size_t)words * 4, hipMemcpyDeviceToHost));
   (void)hipFree(d);
   return rc;
+}
+
+extern "C" int jmme_debug_stamps(jmme_ctx *ctx, uint64_t *out, int max_units) {
+  // Diagnostic builds (-DJMME_STAMPS): per-unit s_memtime phase sums of the
+  // last launch: [setup, stage, sweep, reduce, refine, output, nslots, valid].
+  if (!ctx) return fail("null ctx");
+  if (!ctx->d_stamps) return fail("library built without JMME_STAMPS");
+  size_t n = (size_t)max_units < ctx->cap_stamps ? (size_t)max_units : ctx->cap_stamps;
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(out, ctx->d_stamps, n * 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  return (int)n;
 }

@@ -28,6 +28,7 @@ struct KParams {
   const unsigned *unit_count;         // device count for the indirection
   unsigned *status;                   // bit 0: unit with range > lds_range; bit 1: sub-pel FS centre
   uint32_t *debug_words;              // debug: unit 0's first staged window (rows x wp words)
+  unsigned long long *stamps;         // diagnostic builds (JMME_STAMPS): per-unit phase clocks
 };
 
 size_t units_lds_bytes(int lds_range);

@@ -88,6 +88,15 @@ __device__ __forceinline__ Lds carve(unsigned char *smem, int R) {
   return L;
 }
 
+// Diagnostic phase clocks (build with -DJMME_STAMPS; never in the shipped
+// library): s_memtime at phase boundaries, summed per unit, written by lane 0.
+#ifdef JMME_STAMPS
+#define STAMP(acc) do { __builtin_amdgcn_sched_barrier(0); unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+                        acc += t_ - t_last; t_last = t_; __builtin_amdgcn_sched_barrier(0); } while (0)
+#else
+#define STAMP(acc) do { } while (0)
+#endif
+
 __device__ __forceinline__ int ufl(int v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ unsigned long long ufl64(unsigned long long v) {
   unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
@@ -253,6 +262,10 @@ __device__ __forceinline__ void unit_body(const KParams &p, int u, unsigned char
   const uint8_t *ref = p.refs[list * kMaxRefs + ref_idx];
 
   Lds L = carve(smem, p.lds_range);
+#ifdef JMME_STAMPS
+  unsigned long long t_last = __builtin_amdgcn_s_memtime();
+  unsigned long long st_setup = 0, st_stage = 0, st_sweep = 0, st_reduce = 0, st_refine = 0, st_out = 0;
+#endif
 
   // ---- unit setup: slot requests, groups, current MB
   if (tid < kNS) {
@@ -290,6 +303,7 @@ __device__ __forceinline__ void unit_body(const KParams &p, int u, unsigned char
     return;
   }
 
+  STAMP(st_setup);
   // One pass per group: stage the window, sweep it, reduce, (refine), write.
   // Nothing is carried from one group to the next.
   unsigned long long remaining = slot_mask;
@@ -374,6 +388,7 @@ __device__ __forceinline__ void unit_body(const KParams &p, int u, unsigned char
       for (int i = tid; i < wrows * L.wp; i += kWG) p.debug_words[i] = L.words[i];
     }
 
+    STAMP(st_stage);
     // per-thread running minima of the keys
     Best best[kNS];
 #pragma unroll
@@ -482,6 +497,7 @@ __device__ __forceinline__ void unit_body(const KParams &p, int u, unsigned char
     };
     if (gmask == kAll) sweep(std::integral_constant<bool, true>{});
     else sweep(std::integral_constant<bool, false>{});
+    STAMP(st_sweep);
 
     // ---- workgroup reduction of this group's per-thread minima
 #pragma unroll
@@ -510,6 +526,7 @@ __device__ __forceinline__ void unit_body(const KParams &p, int u, unsigned char
       L.red[tid] = k;   // wave 0's row now holds the group result
     }
     __syncthreads();
+    STAMP(st_reduce);
 
     // ---- refine (32-bit keys): recover the 3 rank bits the key dropped.
     // The winner has cost == key>>10 and rank in [8c, 8c+8), c = key & 1023;
@@ -551,6 +568,7 @@ __device__ __forceinline__ void unit_body(const KParams &p, int u, unsigned char
       }
       __syncthreads();
     }
+    STAMP(st_refine);
 
     // ---- results of this group
     if (tid < kNS && ((gmask >> tid) & 1)) {
@@ -588,7 +606,15 @@ __device__ __forceinline__ void unit_body(const KParams &p, int u, unsigned char
       }
       p.out[(size_t)u * kNS + tid] = res;
     }
+    STAMP(st_out);
   }
+#ifdef JMME_STAMPS
+  if (p.stamps && tid == 0) {
+    unsigned long long *o = p.stamps + (size_t)u * 8;
+    o[0] = st_setup; o[1] = st_stage; o[2] = st_sweep; o[3] = st_reduce; o[4] = st_refine; o[5] = st_out;
+    o[6] = __builtin_popcountll(slot_mask); o[7] = 1;
+  }
+#endif
 }
 
 // direct pass: one workgroup per unit (XCD-aware order)

@@ -82,6 +82,7 @@ def lib() -> ctypes.CDLL:
         "jmme_spiral_offset": (V, [I, P, P]),
         "jmme_mvbits": (I, [I]),
         "jmme_debug_window": (I, [P, I, P, P, I]),
+        "jmme_debug_stamps": (I, [P, P, I]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

@@ -180,6 +180,10 @@ int jmme_mvbits(int v);                                /* mvbits[v], mv_search.c
  * of the clamped reference; R = the context's SearchRange. */
 int jmme_debug_window(jmme_ctx *ctx, int mode, const jmme_mb_req *req, uint32_t *out, int max_words);
 
+/* Diagnostic builds only (-DJMME_STAMPS): per-unit phase clock sums of the
+ * last launch, 8 x uint64 per unit; returns units copied or -1. */
+int jmme_debug_stamps(jmme_ctx *ctx, uint64_t *out, int max_units);
+
 #ifdef __cplusplus
 }
 #endif
