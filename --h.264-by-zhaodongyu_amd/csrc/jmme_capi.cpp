@@ -55,9 +55,9 @@ struct jmme_ctx {
   size_t cap_units = 0;
   unsigned long long *d_stamps = nullptr;    // diagnostic builds only
   size_t cap_stamps = 0;
-  unsigned *d_defer_count = nullptr;         // [0] defer count, [1] status
-  int *d_defer_list = nullptr;
-  size_t cap_defer = 0;
+  unsigned *d_counts = nullptr;              // [0] 32-bit items, [1] 64-bit items, [2] status
+  Item *d_items = nullptr;                   // work items (one per unit x partition group)
+  size_t cap_items = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
 };
@@ -206,7 +206,7 @@ extern "C" jmme_ctx *jmme_create(const jmme_config *cfg, int device) {
   }
   (void)hipGetDevice(&ctx->device);
   if ((e = hipMalloc(&ctx->d_ref_table, sizeof(uint8_t *) * kMaxLists * kMaxRefs)) != hipSuccess ||
-      (e = hipMalloc(&ctx->d_defer_count, 16)) != hipSuccess ||
+      (e = hipMalloc(&ctx->d_counts, 16)) != hipSuccess ||
       (e = hipEventCreate(&ctx->ev0)) != hipSuccess || (e = hipEventCreate(&ctx->ev1)) != hipSuccess) {
     fail("jmme_create: %s", hipGetErrorString(e));
     jmme_destroy(ctx);
@@ -222,8 +222,9 @@ extern "C" void jmme_destroy(jmme_ctx *ctx) {
   (void)hipFree(ctx->d_ref_table);
   (void)hipFree(ctx->d_req);
   (void)hipFree(ctx->d_out);
-  (void)hipFree(ctx->d_defer_count);
-  (void)hipFree(ctx->d_defer_list);
+  (void)hipFree(ctx->d_counts);
+  (void)hipFree(ctx->d_items);
+  (void)hipFree(ctx->d_stamps);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
   delete ctx;
@@ -300,13 +301,14 @@ int ensure_units(jmme_ctx *ctx, size_t n) {
   return 0;
 }
 
-int ensure_defer(jmme_ctx *ctx, size_t n) {
-  if (n <= ctx->cap_defer) return 0;
-  (void)hipFree(ctx->d_defer_list);
-  ctx->d_defer_list = nullptr;
-  size_t cap = n < 1024 ? 1024 : n;
-  HIPCHK(hipMalloc(&ctx->d_defer_list, cap * sizeof(int)));
-  ctx->cap_defer = cap;
+// every unit yields at most one item per searched partition
+int ensure_items(jmme_ctx *ctx, size_t n) {
+  if (n <= ctx->cap_items) return 0;
+  (void)hipFree(ctx->d_items);
+  ctx->d_items = nullptr;
+  size_t cap = n < 4096 ? 4096 : n;
+  HIPCHK(hipMalloc(&ctx->d_items, cap * sizeof(Item)));
+  ctx->cap_items = cap;
   return 0;
 }
 
@@ -325,7 +327,7 @@ int launch(jmme_ctx *ctx, int mode, const uint8_t *d_cur, const uint8_t *const *
     return fail("search mode %d not supported by the batched engine (FS=-1, FFS=0)", mode);
   if (n < 0) return fail("negative unit count");
   if (n == 0) return 0;
-  if (ensure_defer(ctx, (size_t)n)) return -1;
+  if (ensure_items(ctx, (size_t)n * JMME_NSLOT)) return -1;
   KParams p{};
   p.cur = d_cur;
   p.refs = d_ref_table;
@@ -338,9 +340,10 @@ int launch(jmme_ctx *ctx, int mode, const uint8_t *d_cur, const uint8_t *const *
   p.mode = mode;
   p.max_mvd = ctx->max_mvd;
   p.lds_range = ctx->cfg.SearchRange;
-  p.defer_count = ctx->d_defer_count;
-  p.defer_list = ctx->d_defer_list;
-  p.status = ctx->d_defer_count + 1;
+  p.key32 = p.lds_range <= kKey32MaxRange;
+  p.items = ctx->d_items;
+  p.item_cap = (unsigned)ctx->cap_items;
+  p.counts = ctx->d_counts;
   p.debug_words = debug_words;
 #ifdef JMME_STAMPS
   if ((size_t)n > ctx->cap_stamps) {
@@ -349,30 +352,21 @@ int launch(jmme_ctx *ctx, int mode, const uint8_t *d_cur, const uint8_t *const *
     ctx->cap_stamps = (size_t)n;
   }
   p.stamps = ctx->d_stamps;
+  HIPCHK(hipMemsetAsync(ctx->d_stamps, 0, (size_t)n * 8 * sizeof(unsigned long long), s));
 #endif
-  const bool key32 = p.lds_range <= kKey32MaxRange;
-  HIPCHK(hipMemsetAsync(ctx->d_defer_count, 0, 16, s));
-  HIPCHK(hipEventRecord(ctx->ev0, s));
-  HIPCHK(launch_units(p, key32, n, s));
-  HIPCHK(hipEventRecord(ctx->ev1, s));   // jmme_last_kernel_ms: the unit kernel alone
-  if (key32) {
-    // units whose every candidate saturated the 32-bit cost field (none in
-    // practice): redo with 64-bit keys; the grid drains the device list.
-    KParams q = p;
-    q.unit_list = ctx->d_defer_list;
-    q.unit_count = ctx->d_defer_count;
-    q.defer_count = nullptr;
-    HIPCHK(launch_units(q, false, 64, s));
-  }
+  HIPCHK(hipMemsetAsync(ctx->d_counts, 0, 16, s));
+  // jmme_last_kernel_ms: the main item kernel alone (ev0 .. ev1)
+  HIPCHK(launch_search(p, s, ctx->ev0, ctx->ev1));
   ctx->timed = true;
   return 0;
 }
 
 int check_status(jmme_ctx *ctx) {
-  unsigned st[2] = {0, 0};
-  HIPCHK(hipMemcpy(st, ctx->d_defer_count, sizeof st, hipMemcpyDeviceToHost));
-  if (st[1] & 1u) return fail("a request's search range exceeds the configured SearchRange %d", ctx->cfg.SearchRange);
-  if (st[1] & 2u) return fail("a full-search centre is not on the integer grid (EPZSSubPelGrid sub-pel centres are not supported)");
+  unsigned st[3] = {0, 0, 0};
+  HIPCHK(hipMemcpy(st, ctx->d_counts, sizeof st, hipMemcpyDeviceToHost));
+  if (st[2] & 4u) return fail("internal: the refine pass lost a winner");
+  if (st[2] & 1u) return fail("a request's search range exceeds the configured SearchRange %d", ctx->cfg.SearchRange);
+  if (st[2] & 2u) return fail("a full-search centre is not on the integer grid (EPZSSubPelGrid sub-pel centres are not supported)");
   return 0;
 }
 
@@ -524,7 +518,7 @@ extern "C" int jmme_debug_window(jmme_ctx *ctx, int mode, const jmme_mb_req *req
 
 extern "C" int jmme_debug_stamps(jmme_ctx *ctx, uint64_t *out, int max_units) {
   // Diagnostic builds (-DJMME_STAMPS): per-unit s_memtime phase sums of the
-  // last launch: [setup, stage, sweep, reduce, refine, output, nslots, valid].
+  // last launch: [wait, expand, sweep, reduce, refine, output, nslots, items].
   if (!ctx) return fail("null ctx");
   if (!ctx->d_stamps) return fail("library built without JMME_STAMPS");
   size_t n = (size_t)max_units < ctx->cap_stamps ? (size_t)max_units : ctx->cap_stamps;

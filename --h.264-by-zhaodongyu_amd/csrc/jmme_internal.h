@@ -11,6 +11,25 @@ constexpr int kMaxRefs = 32;
 constexpr int kKey32MaxRange = 44;   // (2R+1)^2 < 2^13 spiral ranks fit the 32-bit key
 constexpr int kWG = 256;             // 4 waves of 64
 
+// One work item of the search kernels: the partitions of one MB x ref unit
+// that share a search window AND a predictor/lambda (one SAD sweep serves all
+// of them).  Built on the device by the plan kernel from the unit requests.
+struct Item {
+  unsigned long long gmask;   // partitions (slots) served; 0 = refused item (status set)
+  unsigned long long rlim;    // FFS: members whose own range is below the window's
+  int u;                      // unit index
+  int16_t mb_x, mb_y;
+  int16_t cqx, cqy;           // window centre (qpel, on the integer grid)
+  int16_t R, flags;           // window range; flags: kItemChk00 | kItemPreseed
+  int16_t px, py;             // predictor (qpel)
+  int lam;                    // lambda_factor
+  int ref;                    // list * kMaxRefs + ref_idx
+  int pad;
+};
+static_assert(sizeof(Item) == 48, "Item layout");
+constexpr int kItemChk00 = 1;     // slot 0 takes check_for_00 (me_fullsearch.c:61)
+constexpr int kItemPreseed = 2;   // FFS pos00 pre-seed (me_fullfast.c:640-648)
+
 struct KParams {
   const uint8_t *cur;                 // 8-bit current picture
   const uint8_t *const *refs;         // device table [kMaxLists*kMaxRefs] of 8-bit reference planes
@@ -22,16 +41,18 @@ struct KParams {
   int mode;                           // JMME_FULL_SEARCH / JMME_FAST_FULL_SEARCH
   int max_mvd;                        // p_Vid->max_mvd (FFS gate)
   int lds_range;                      // largest search range in the launch (LDS sizing)
-  unsigned *defer_count;              // units whose 32-bit keys saturated
-  int *defer_list;
-  const int *unit_list;               // optional indirection (deferred pass)
-  const unsigned *unit_count;         // device count for the indirection
-  unsigned *status;                   // bit 0: unit with range > lds_range; bit 1: sub-pel FS centre
+  int key32;                          // plan: route items to the 32-bit list (else all to the 64-bit list)
+  Item *items;                        // [item_cap]: 32-bit list grows up from 0, 64-bit list down from the top
+  unsigned item_cap;
+  unsigned *counts;                   // [0] 32-bit items, [1] 64-bit items, [2] status
   uint32_t *debug_words;              // debug: unit 0's first staged window (rows x wp words)
   unsigned long long *stamps;         // diagnostic builds (JMME_STAMPS): per-unit phase clocks
 };
+// status bits (counts[2]): bit 0 range > lds_range, bit 1 sub-pel centre, bit 2 refine lost a winner
 
-size_t units_lds_bytes(int lds_range);
-hipError_t launch_units(const KParams &p, bool key32, int grid, hipStream_t s);
+size_t items_lds_bytes(int lds_range);
+// plan (unit requests -> items), then the persistent 32-bit and 64-bit item
+// kernels; ev0/ev1 (optional) bracket the main search kernel
+hipError_t launch_search(const KParams &p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1);
 
 }  // namespace jmme

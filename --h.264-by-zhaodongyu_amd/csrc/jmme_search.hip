@@ -1,5 +1,5 @@
 // jmme_search.hip -- gfx950 kernels for JM 18.5 integer-pel full search (FS)
-// and fast full search (FFS), one workgroup per macroblock x reference unit.
+// and fast full search (FFS).
 //
 // Semantics restated from JM 18.5 (JM = /root/reference/4.对比程序/jm18.5/JM):
 //   FS   full_search_motion_estimation   JM/lencod/src/me_fullsearch.c:39-103
@@ -16,12 +16,19 @@
 // eligible candidates.  We evaluate every candidate exhaustively and reduce
 // that key; no early exit, same answer.
 //
-// Work mapping (one workgroup = one MB x ref unit, 256 threads = 4 waves):
-//   * partitions are grouped by identical search window and predictor (FS:
-//     centre + range + predictor; FFS: the MB's surface + predictor); each
-//     group stages its reference window (2R+16)^2 pels from HBM into LDS once,
-//     as "word[y][x] = pels x..x+3" so every SAD row read is an aligned
-//     ds_read_b32;
+// Work decomposition:
+//   * plan kernel (one wave per MB x ref unit): the unit's partitions are
+//     grouped by identical search window AND predictor/lambda (FS: centre +
+//     range + predictor; FFS: the MB's surface + predictor).  Each group is a
+//     work Item; one SAD sweep serves every partition of the group.  Units
+//     whose lambda could overflow the 32-bit key go to the 64-bit item list.
+//   * item kernels (persistent, one 256-thread workgroup per CU slot, items
+//     statically dealt in contiguous runs per XCD so neighbouring macroblocks'
+//     overlapping windows hit the same L2): while item k is swept, item k+1's
+//     reference window, current MB and slot requests stream HBM -> LDS with
+//     global_load_lds (no VGPRs held), so the sweep hides the fetch latency;
+//   * window in LDS as "word[y][x] = pels x..x+3": every SAD row read is an
+//     aligned ds_read_b32;
 //   * a thread takes a vertical PAIR of search positions: the 17 reference
 //     rows they need are read once, the 2 x 16 4x4 SADs formed with v_sad_u8
 //     (the current MB row is a broadcast ds_read_b128), summed to the 41
@@ -32,7 +39,7 @@
 //     exactly afterwards: the winner's rank lies in [8c, 8c+8), and those <= 8
 //     positions are re-evaluated per partition (refine pass);
 //   * key (exact fallback): 64 bits = cost << 32 | rank, for ranges > 44 or
-//     huge lambdas (deferred pass).
+//     huge lambdas.
 #include <hip/hip_runtime.h>
 #include <type_traits>
 #include "jmme.h"
@@ -50,46 +57,46 @@ constexpr uint32_t kMaxLambda32 = 28450;   // 32*65280 + lambda*74 < 2^22: 22-bi
 constexpr int kCostShift = 10;             // key32 = cost << 10 | rank >> 3
 constexpr int kRankDrop = 3;
 constexpr int kCand = 1 << kRankDrop;      // refine candidates per partition
+constexpr int kPlanWaves = 16;             // plan kernel: units per workgroup
 #ifndef JMME_WAVES_PER_EU
 #define JMME_WAVES_PER_EU 4
 #endif
 
+// dwords per staged raw row: the words of a row read pels x0 .. x0+2R+15,
+// fetched as aligned dwords from floor4(x0) (+1 dword for alignbyte's high half)
+__host__ __device__ inline int raw_row_dwords(int R) { return (3 + 2 * R + 13 + 2) / 4 + 2; }
+// the fetch also carries the item's current MB and slot requests behind the
+// window (LDS DMA only ever targets the raw area: the sweep's LDS reads never
+// alias an in-flight fetch, so the compiler inserts no vmcnt waits there)
+constexpr int kRawExtra = 64 + 4 * JMME_NSLOT + 64;   // + one wave of slack: fetch chunks are 64-aligned
+
 struct Lds {
-  int wp;        // words per window row
-  int rawp;      // bytes per raw row
-  uint32_t *words;
-  uint8_t *raw;
-  uint32_t *cur;            // 64 words: MB row r, column group c at [r*4+c]
-  int4 *slot;               // 41 x jmme_block_req
-  unsigned long long *grp;  // per slot: mask of slots sharing window AND predictor
+  int wp;                   // words per window row
+  uint32_t *words;          // current item's window, rows x wp
+  uint32_t *raw;            // next item as fetched: window rows x nd dwords (dense),
+                            // then its current MB (64) and slot requests (164)
+  uint32_t *cur;            // 64 words: MB row r, column group c at [r*4+c]  (static LDS:
+  int4 *slot;               // 41 x jmme_block_req                            provably not the DMA target)
   unsigned long long *red;  // kWaves x 41 reduction scratch
   uint32_t *match;          // 41 x kCand refine flags
-  int *flag;                // unit must be redone with 64-bit keys
 };
-
-__host__ __device__ inline int lds_rawp(int R) { return 4 * ((3 + 2 * R + 13 + 2) / 4 + 2); }
 
 __device__ __forceinline__ Lds carve(unsigned char *smem, int R) {
   Lds L;
   const int rows = 2 * R + 16;
   L.wp = (2 * R + 13) | 1;
-  L.rawp = lds_rawp(R);
   size_t off = 0;
   L.words = reinterpret_cast<uint32_t *>(smem + off); off += (size_t)rows * L.wp * 4;
   off = (off + 15) & ~(size_t)15;
-  L.raw = smem + off;                                    off += (size_t)rows * L.rawp;
+  L.raw = reinterpret_cast<uint32_t *>(smem + off);   off += ((size_t)rows * raw_row_dwords(R) + kRawExtra) * 4;
   off = (off + 15) & ~(size_t)15;
-  L.cur = reinterpret_cast<uint32_t *>(smem + off);      off += 64 * 4;
-  L.slot = reinterpret_cast<int4 *>(smem + off);         off += kNS * 16;
-  L.grp = reinterpret_cast<unsigned long long *>(smem + off); off += kNS * 8;
   L.red = reinterpret_cast<unsigned long long *>(smem + off); off += kWaves * kNS * 8;
   L.match = reinterpret_cast<uint32_t *>(smem + off);    off += kNS * kCand * 4;
-  L.flag = reinterpret_cast<int *>(smem + off);          off += 16;
   return L;
 }
 
 // Diagnostic phase clocks (build with -DJMME_STAMPS; never in the shipped
-// library): s_memtime at phase boundaries, summed per unit, written by lane 0.
+// library): s_memtime at phase boundaries, summed per unit by lane 0.
 #ifdef JMME_STAMPS
 #define STAMP(acc) do { __builtin_amdgcn_sched_barrier(0); unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
                         acc += t_ - t_last; t_last = t_; __builtin_amdgcn_sched_barrier(0); } while (0)
@@ -106,6 +113,18 @@ __device__ __forceinline__ unsigned long long ufl64(unsigned long long v) {
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
+// LDS reads of the sweep.  Plain loads: the compiler tracks them (an inline-asm
+// load would let it copy the destination before the data lands).
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) const uint32_t lds_u32;
+__device__ __forceinline__ uint32_t lds_addr(const void *p) { return (uint32_t)(uintptr_t)p; }
+__device__ __forceinline__ u32x2 ds_read2_0_4(uint32_t a) { const lds_u32 *q = (const lds_u32 *)(uintptr_t)a; return u32x2{q[0], q[4]}; }
+__device__ __forceinline__ u32x2 ds_read2_8_12(uint32_t a) { const lds_u32 *q = (const lds_u32 *)(uintptr_t)a; return u32x2{q[8], q[12]}; }
+__device__ __forceinline__ u32x4 ds_read_b128(uint32_t a) {
+  return *reinterpret_cast<const __attribute__((address_space(3))) u32x4 *>((const lds_u32 *)(uintptr_t)a);
+}
+
 // slot request fields from the int4 image of jmme_block_req
 __device__ __forceinline__ int rq_pred_x(int4 q) { return (int)(short)(q.x & 0xffff); }
 __device__ __forceinline__ int rq_pred_y(int4 q) { return (int)(short)((unsigned)q.x >> 16); }
@@ -114,15 +133,6 @@ __device__ __forceinline__ int rq_cen_y(int4 q) { return (int)(short)((unsigned)
 __device__ __forceinline__ int rq_range(int4 q) { return (int)(short)(q.z & 0xffff); }
 __device__ __forceinline__ int rq_flags(int4 q) { return (int)(short)((unsigned)q.z >> 16); }
 __device__ __forceinline__ int rq_lambda(int4 q) { return q.w; }
-
-// bijective XCD-aware remap: blocks are dealt round-robin to the 8 XCDs, so
-// give each XCD a contiguous run of units (neighbouring macroblocks read
-// overlapping reference windows, which then hit that XCD's L2).
-__device__ __forceinline__ int xcd_unit(int b, int nb) {
-  const int nx = 8;
-  int q = nb / nx, r = nb % nx, x = b % nx;
-  return x * q + (x < r ? x : r) + b / nx;
-}
 
 // the 41 partition SADs from the 16 4x4 SADs (JM sums them in
 // update_full_search_large_blocks, me_fullfast.c:196-260 -- integer sums)
@@ -157,6 +167,24 @@ __device__ __forceinline__ int spiral_index_bl(int ox, int oy) {
   const int side = base + 2 * (2 * l - 1) + 2 * (oy + l) + (ox > 0);
   const int v = (ay == l && ax < l) ? top : side;
   return l == 0 ? 0 : v;
+}
+
+// spiral_offset (jmme_common.h) without the ring loop: ring l = (isqrt(idx)+1)/2
+__device__ __forceinline__ void spiral_offset_fast(int idx, int *ox, int *oy) {
+  int q = (int)sqrtf((float)idx);
+  q -= q * q > idx;
+  q += (q + 1) * (q + 1) <= idx;
+  const int l = (q + 1) >> 1;
+  int r = idx - (2 * l - 1) * (2 * l - 1);
+  if (idx <= 0) { *ox = 0; *oy = 0; return; }
+  if (r < 2 * (2 * l - 1)) {
+    *ox = r / 2 - l + 1;
+    *oy = (r & 1) ? l : -l;
+  } else {
+    r -= 2 * (2 * l - 1);
+    *oy = r / 2 - l;
+    *ox = (r & 1) ? l : -l;
+  }
 }
 
 // mv cost lambda*(mvbits[dx]+mvbits[dy]) of candidate (candx, candy) against
@@ -231,438 +259,599 @@ __device__ __forceinline__ void update_slots(const uint32_t (&ps)[kNS], const Gr
 }
 
 // exact SAD of partition s at window offset (oxw, oyw), for the refine pass
-__device__ __forceinline__ uint32_t partition_sad_at(const Lds &L, int s, int oxw, int oyw) {
+__device__ __forceinline__ uint32_t partition_sad_at(const Lds &L, const uint32_t *cur, int s, int oxw, int oyw) {
   const SlotGeom gm = slot_geom(s);
   uint32_t sad = 0;
   for (int r = 0; r < 4 * gm.h; ++r) {
     const int row = gm.by * 4 + r;
     const uint32_t *w = L.words + (oyw + row) * L.wp + oxw + gm.bx * 4;
-    for (int c = 0; c < gm.w; ++c) sad = __builtin_amdgcn_sad_u8(w[4 * c], L.cur[row * 4 + gm.bx + c], sad);
+    for (int c = 0; c < gm.w; ++c) sad = __builtin_amdgcn_sad_u8(w[4 * c], cur[row * 4 + gm.bx + c], sad);
   }
   return sad;
 }
 
+// minimum over the wave with DPP (row_shr 1,2,4,8 then row_bcast 15/31): lane 63
+// ends with the wave minimum.  No LDS traffic, 6 VALU ops per value.
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+#define JMME_DPP_MIN(ctrl, rmask) \
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, ctrl, rmask, 0xf, false))
+  JMME_DPP_MIN(0x111, 0xf);   // row_shr:1
+  JMME_DPP_MIN(0x112, 0xf);   // row_shr:2
+  JMME_DPP_MIN(0x114, 0xf);   // row_shr:4
+  JMME_DPP_MIN(0x118, 0xf);   // row_shr:8
+  JMME_DPP_MIN(0x142, 0xa);   // row_bcast:15
+  JMME_DPP_MIN(0x143, 0xc);   // row_bcast:31
+#undef JMME_DPP_MIN
+  return v;
+}
+
+// ------------------------------------------------------------ plan kernel --
+// One wave per unit: lane s holds slot s's request; groups found with
+// readlane + ballot; items appended with one atomic per workgroup per list.
+template <bool FFS>
+__global__ __launch_bounds__(64 * kPlanWaves) void me_plan_kernel(KParams p) {
+  __shared__ unsigned s_n[kPlanWaves], s_64[kPlanWaves], s_off[kPlanWaves];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int u = blockIdx.x * kPlanWaves + wave;
+  int ng = 0;
+  bool to64 = !p.key32;
+  unsigned long long my_gm = 0, my_rl = 0;
+  int my_lead = 0;
+  if (u < p.n) {
+    const jmme_mb_req *rq = p.req + u;
+    const unsigned long long mask = ufl64(rq->slot_mask) & kAll;
+    const int fR = ufl(rq->ffs_range);
+    const int4 me = lane < kNS ? reinterpret_cast<const int4 *>(&rq->blk[0])[lane] : make_int4(0, 0, 0, 0);
+    const bool valid = lane < kNS && ((mask >> lane) & 1);
+    if (__builtin_amdgcn_ballot_w64(valid && (uint32_t)rq_lambda(me) > kMaxLambda32)) to64 = true;
+    unsigned long long rem = mask;
+    while (rem) {
+      const int lead = __builtin_ctzll(rem);
+      const int ox = __builtin_amdgcn_readlane(me.x, lead);
+      const int oy = __builtin_amdgcn_readlane(me.y, lead);
+      const int oz = __builtin_amdgcn_readlane(me.z, lead);
+      const int ow = __builtin_amdgcn_readlane(me.w, lead);
+      // same predictor and lambda; FS also the same window (centre, range)
+      const bool eq = valid && me.x == ox && me.w == ow &&
+                      (FFS || (me.y == oy && rq_range(me) == (int)(short)(oz & 0xffff)));
+      const unsigned long long gm = __builtin_amdgcn_ballot_w64(eq) & rem;
+      const unsigned long long rl = FFS ? (__builtin_amdgcn_ballot_w64(eq && rq_range(me) < fR) & rem) : 0ull;
+      if (lane == ng) { my_gm = gm; my_rl = rl; my_lead = lead; }
+      ++ng;
+      rem &= ~gm;
+    }
+  }
+  if (lane == 0) { s_n[wave] = ng; s_64[wave] = to64; }
+  __syncthreads();
+  if (tid == 0) {
+    unsigned na = 0, nb = 0;
+    for (int w = 0; w < kPlanWaves; ++w) {
+      unsigned &c = s_64[w] ? nb : na;
+      s_off[w] = c;
+      c += s_n[w];
+    }
+    const unsigned ba = na ? atomicAdd(&p.counts[0], na) : 0u;
+    const unsigned bb = nb ? atomicAdd(&p.counts[1], nb) : 0u;
+    for (int w = 0; w < kPlanWaves; ++w) s_off[w] += s_64[w] ? bb : ba;
+  }
+  __syncthreads();
+  if (u < p.n && lane < ng) {
+    const jmme_mb_req *rq = p.req + u;
+    const int4 lq = reinterpret_cast<const int4 *>(&rq->blk[0])[my_lead];
+    Item it;
+    it.gmask = my_gm;
+    it.rlim = my_rl;
+    it.u = u;
+    it.mb_x = rq->mb_x;
+    it.mb_y = rq->mb_y;
+    const int cqx = FFS ? rq->ffs_center_x : rq_cen_x(lq);
+    const int cqy = FFS ? rq->ffs_center_y : rq_cen_y(lq);
+    const int R = FFS ? rq->ffs_range : rq_range(lq);
+    it.cqx = (int16_t)cqx;
+    it.cqy = (int16_t)cqy;
+    it.R = (int16_t)R;
+    it.flags = (int16_t)(((!FFS && my_lead == 0 && (rq_flags(lq) & JMME_BLK_CHECK00)) ? kItemChk00 : 0) |
+                         ((FFS && rq->ffs_pos00_valid) ? kItemPreseed : 0));
+    it.px = (int16_t)rq_pred_x(lq);
+    it.py = (int16_t)rq_pred_y(lq);
+    it.lam = rq_lambda(lq);
+    it.ref = rq->list * kMaxRefs + rq->ref_idx;
+    it.pad = 0;
+    if (R < 0 || R > p.lds_range || ((cqx | cqy) & 3)) {
+      // outside what this launch was sized for (or a sub-pel-grid centre):
+      // refuse loudly instead of overrunning LDS; the host reports it
+      atomicOr(&p.counts[2], (R < 0 || R > p.lds_range) ? 1u : 2u);
+      it.gmask = 0;
+    }
+    const unsigned idx = s_off[wave] + lane;
+    p.items[to64 ? p.item_cap - 1 - idx : idx] = it;
+  }
+}
+
+// ------------------------------------------------------------ item kernels --
+struct Win { int R, x0, y0, wrows, wpr, xa, sh, nd; bool inner; };
+
+__device__ __forceinline__ Win win_of(const KParams &p, const Item &it) {
+  Win w;
+  w.R = it.R;
+  w.x0 = it.mb_x + (it.cqx >> 2) - w.R;
+  w.y0 = it.mb_y + (it.cqy >> 2) - w.R;
+  w.wrows = 2 * w.R + 16;
+  w.wpr = 2 * w.R + 13;                    // words per window row
+  w.xa = w.x0 & ~3;                        // dword-aligned start (floor)
+  w.sh = w.x0 - w.xa;                      // 0..3
+  w.nd = (w.sh + w.wpr + 2) / 4 + 2;       // dwords per row the words read (incl. alignbyte hi)
+  w.inner = w.xa >= 0 && w.xa + 4 * w.nd <= p.width;
+  return w;
+}
+
+// Issue the HBM -> LDS fetch of item `it` (window rows clamped into the
+// picture, dword columns clamped into it -- UMVLine4X), its current MB and its
+// slot requests.  global_load_lds: per-lane global address, LDS destination
+// contiguous per wave instruction; completion is awaited (vmcnt) only at the
+// top of the next item.
+__device__ __forceinline__ void prefetch(const KParams &p, const Item &it, const Lds &L, int wave, int lane) {
+  if (!it.gmask) return;
+  const Win w = win_of(p, it);
+  const uint8_t *ref = p.refs[it.ref];
+  const int total = w.wrows * w.nd;
+  const int w4 = p.width >> 2, xq = w.xa >> 2;
+  for (int base = wave * 64; base < total; base += kWG) {
+    const int i = base + lane;
+    if (i < total) {
+      const int r = i / w.nd, d = i - r * w.nd;
+      const int gy = clampi(w.y0 + r, 0, p.height - 1);
+      const int pd = clampi(xq + d, 0, w4 - 1);
+      __builtin_amdgcn_global_load_lds(ref + (size_t)gy * p.pitch + 4 * pd, L.raw + base, 4, 0, 0);
+    }
+  }
+  // behind the window: current MB (wave 0), slot requests (waves 1..3)
+  uint32_t *tail = L.raw + total;
+  if (wave == 0) {
+    const int r = lane >> 2, c = lane & 3;
+    __builtin_amdgcn_global_load_lds(p.cur + (size_t)(it.mb_y + r) * p.pitch + it.mb_x + 4 * c, tail, 4, 0, 0);
+  } else {
+    const int i = (wave - 1) * 64 + lane;
+    if (i < kNS * 4)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint32_t *>(&p.req[it.u].blk[0]) + i,
+                                       tail + 64 + (wave - 1) * 64, 4, 0, 0);
+  }
+}
+
+// raw dwords -> words (word[y][x] = pels x..x+3 of the window)
+__device__ __forceinline__ void expand(const KParams &p, const Item &it, const Lds &L, int tid) {
+  const Win w = win_of(p, it);
+  const int n = w.wrows * w.wpr;
+  const uint32_t *tail = L.raw + w.wrows * w.nd;
+  if (tid < 64) L.cur[tid] = tail[tid];
+  else if (tid < 64 + 4 * kNS) reinterpret_cast<uint32_t *>(L.slot)[tid - 64] = tail[tid];
+  if (w.inner) {
+    for (int i = tid; i < n; i += kWG) {
+      const int r = i / w.wpr, c = i - r * w.wpr + w.sh;
+      const uint32_t *rw = L.raw + r * w.nd;
+      L.words[r * L.wp + (c - w.sh)] = __builtin_amdgcn_alignbyte(rw[(c >> 2) + 1], rw[c >> 2], c & 3);
+    }
+  } else {
+    // window crosses (or lies beyond) the left/right picture edge: pel x of
+    // the window is picture column gx = clamp(x, 0, W-1); fetched dword d holds
+    // picture dword clamp(xa/4 + d, 0, W/4-1), so gx sits in dword
+    // clamp(gx/4 - xa/4, 0, nd-1), byte gx & 3
+    const uint8_t *raw8 = reinterpret_cast<const uint8_t *>(L.raw);
+    const int xq = w.xa >> 2;
+    for (int i = tid; i < n; i += kWG) {
+      const int r = i / w.wpr, c = i - r * w.wpr;
+      const uint8_t *rb = raw8 + r * 4 * w.nd;
+      uint32_t v = 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const int gx = clampi(w.x0 + c + b, 0, p.width - 1);
+        v |= (uint32_t)rb[4 * clampi((gx >> 2) - xq, 0, w.nd - 1) + (gx & 3)] << (8 * b);
+      }
+      L.words[r * L.wp + c] = v;
+    }
+  }
+}
+
 template <bool KEY32, bool FFS>
-__device__ __forceinline__ void unit_body(const KParams &p, int u, unsigned char *smem) {
+struct ItemStamps {
+  unsigned long long wait = 0, expand = 0, sweep = 0, reduce = 0, refine = 0, out = 0;
+};
+
+// sweep + reduce + refine + output of one item whose window is in L.words
+template <bool KEY32, bool FFS>
+__device__ __forceinline__ void search_item(const KParams &p, const Item &it, const Lds &L
+#ifdef JMME_STAMPS
+                                            , unsigned long long &t_last, ItemStamps<KEY32, FFS> &st
+#endif
+) {
   using Best = typename std::conditional<KEY32, uint32_t, unsigned long long>::type;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
+  const uint32_t *curw = L.cur;
 
-  const jmme_mb_req *rq = p.req + u;
-  const int mb_x = ufl(rq->mb_x);
-  const int mb_y = ufl(rq->mb_y);
-  const int list = ufl(rq->list);
-  const int ref_idx = ufl(rq->ref_idx);
-  const unsigned long long slot_mask = ufl64(rq->slot_mask) & kAll;
-  const int ffs_cx = ufl(rq->ffs_center_x);
-  const int ffs_cy = ufl(rq->ffs_center_y);
-  const int ffs_range = ufl(rq->ffs_range);
-  const bool preseed = FFS && ufl(rq->ffs_pos00_valid) != 0;
-  const uint8_t *ref = p.refs[list * kMaxRefs + ref_idx];
+  GroupCtx g;
+  g.cqx = it.cqx;
+  g.cqy = it.cqy;
+  g.R = it.R;
+  g.px = it.px;
+  g.py = it.py;
+  g.lam = it.lam;
+  g.max_mvd = p.max_mvd;
+  g.preseed = FFS && (it.flags & kItemPreseed);
+  g.gmask = it.gmask;
+  g.rlim = it.rlim;
+  g.chk00 = !FFS && (it.flags & kItemChk00);
+  g.slot = L.slot;
+  const int R = g.R;
+  const unsigned long long gmask = g.gmask;
+  const int u = it.u;
 
-  Lds L = carve(smem, p.lds_range);
-#ifdef JMME_STAMPS
-  unsigned long long t_last = __builtin_amdgcn_s_memtime();
-  unsigned long long st_setup = 0, st_stage = 0, st_sweep = 0, st_reduce = 0, st_refine = 0, st_out = 0;
-#endif
-
-  // ---- unit setup: slot requests, groups, current MB
-  if (tid < kNS) {
-    const int4 *src = reinterpret_cast<const int4 *>(&rq->blk[0]);
-    L.slot[tid] = src[tid];
-  }
-  if (tid == 255) L.flag[0] = 0;
-  if (tid >= 64 && tid < 128) {
-    int t = tid - 64, r = t >> 2, c = t & 3;
-    L.cur[t] = *reinterpret_cast<const uint32_t *>(p.cur + (size_t)(mb_y + r) * p.pitch + mb_x + 4 * c);
-  }
-  __syncthreads();
-  if (tid < kNS) {
-    const int4 me = L.slot[tid];
-    unsigned long long g = 0;
-    if ((slot_mask >> tid) & 1) {
-      for (int t = 0; t < kNS; ++t) {
-        if (!((slot_mask >> t) & 1)) continue;
-        const int4 o = L.slot[t];
-        // a group = partitions with the same search window AND the same
-        // predictor/lambda: one SAD sweep and one mv-cost per position serve
-        // the whole group (a window with several predictors is swept once per
-        // predictor -- straight-line code, no per-partition predictor loads)
-        const bool same_win = FFS || (o.y == me.y && rq_range(o) == rq_range(me));
-        g |= (unsigned long long)(same_win && o.x == me.x && o.w == me.w) << t;
-      }
-      if (KEY32 && (uint32_t)rq_lambda(me) > kMaxLambda32) L.flag[0] = 1;
-    }
-    L.grp[tid] = g;
-  }
-  __syncthreads();
-  if (KEY32 && ufl(L.flag[0])) {
-    // the 22-bit cost field could overflow: redo the whole unit with 64-bit keys
-    if (tid == 0) p.defer_list[atomicAdd(p.defer_count, 1u)] = u;
-    return;
-  }
-
-  STAMP(st_setup);
-  // One pass per group: stage the window, sweep it, reduce, (refine), write.
-  // Nothing is carried from one group to the next.
-  unsigned long long remaining = slot_mask;
-  while (remaining) {
-    const int lead = __builtin_ctzll(remaining);
-    const unsigned long long gmask = ufl64(L.grp[lead]) & remaining;
-    remaining &= ~gmask;
-    const int4 lq = L.slot[lead];
-    GroupCtx g;
-    g.cqx = ufl(FFS ? ffs_cx : rq_cen_x(lq));   // window centre, qpel (multiple of 4)
-    g.cqy = ufl(FFS ? ffs_cy : rq_cen_y(lq));
-    g.R = ufl(FFS ? ffs_range : rq_range(lq));
-    g.px = ufl(rq_pred_x(lq));
-    g.py = ufl(rq_pred_y(lq));
-    g.lam = ufl(rq_lambda(lq));
-    g.max_mvd = p.max_mvd;
-    g.preseed = preseed;
-    g.gmask = gmask;
-    g.slot = L.slot;
-    const int R = g.R;
-    if (R < 0 || R > p.lds_range || ((g.cqx | g.cqy) & 3)) {
-      // outside what this launch was sized for (or a sub-pel-grid centre):
-      // refuse loudly instead of overrunning LDS; the host reports it
-      if (tid == 0) atomicOr(p.status, (R < 0 || R > p.lds_range) ? 1u : 2u);
-      continue;
-    }
-    g.rlim = 0;
-    if (FFS) {
-      for (int t = 0; t < kNS; ++t)
-        if ((gmask >> t) & 1) g.rlim |= (unsigned long long)(rq_range(L.slot[t]) < R) << t;
-      g.rlim = ufl64(g.rlim);
-    }
-    g.chk00 = ufl((!FFS && (gmask & 1)) ? (rq_flags(L.slot[0]) & JMME_BLK_CHECK00) : 0);
-
-    // ---- stage the (2R+16)^2 reference window, clamped like UMVLine4X.
-    // Rows are clamped into the picture; when the window's columns lie inside
-    // the picture each row is fetched as aligned dwords (one round trip, all
-    // loads in flight), else byte by byte with column clamping.
-    const int x0 = mb_x + (g.cqx >> 2) - R;
-    const int y0 = mb_y + (g.cqy >> 2) - R;
-    const int wrows = 2 * R + 16;
-    const int wpr = 2 * R + 13;                 // words per window row
-    const int xa = x0 & ~3;                     // dword-aligned start (floor)
-    const int sh = x0 - xa;                     // 0..3
-    const int nd = (sh + wpr + 2) / 4 + 2;      // dwords per row the words read (incl. alignbyte hi)
-    const int rdw = L.rawp >> 2;
-    uint32_t *raw32 = reinterpret_cast<uint32_t *>(L.raw);
-    __syncthreads();   // previous group's readers are done with the window
-#ifdef JMME_ABL_NOSTAGE  // timing ablation only: skip fetching the window
-    constexpr bool kFetch = false;
-#else
-    constexpr bool kFetch = true;
-#endif
-    if (!kFetch) {
-    } else if (xa >= 0 && xa + 4 * nd <= p.width) {
-      const int total = wrows * nd;
-#pragma unroll 4
-      for (int i = tid; i < total; i += kWG) {
-        const int r = i / nd, d = i - r * nd;
-        const int gy = clampi(y0 + r, 0, p.height - 1);
-        raw32[r * rdw + d] = *reinterpret_cast<const uint32_t *>(ref + (size_t)gy * p.pitch + xa + 4 * d);
-      }
-    } else {
-      const int rb = 4 * nd;
-      const int total = wrows * rb;
-#pragma unroll 8
-      for (int i = tid; i < total; i += kWG) {
-        const int r = i / rb, c = i - r * rb;
-        const int gy = clampi(y0 + r, 0, p.height - 1);
-        const int gx = clampi(xa + c, 0, p.width - 1);
-        L.raw[r * L.rawp + c] = ref[(size_t)gy * p.pitch + gx];
-      }
-    }
-    __syncthreads();
-    for (int i = tid; i < wrows * wpr; i += kWG) {
-      const int r = i / wpr, c = i - r * wpr + sh;
-      const uint32_t *rw = raw32 + r * rdw;
-      L.words[r * L.wp + (c - sh)] = __builtin_amdgcn_alignbyte(rw[(c >> 2) + 1], rw[c >> 2], c & 3);
-    }
-    __syncthreads();
-    if (p.debug_words && u == 0 && gmask == (slot_mask & ufl64(L.grp[__builtin_ctzll(slot_mask)]))) {
-      for (int i = tid; i < wrows * L.wp; i += kWG) p.debug_words[i] = L.words[i];
-    }
-
-    STAMP(st_stage);
-    // per-thread running minima of the keys
-    Best best[kNS];
+  // per-thread running minima of the keys
+  Best best[kNS];
 #pragma unroll
-    for (int s = 0; s < kNS; ++s) best[s] = (Best)~0ull;
+  for (int s = 0; s < kNS; ++s) best[s] = (Best)~0ull;
 
-    // ---- sweep all (2R+1)^2 positions of the window.  A task is a vertical
-    // pair of positions (x, y), (x, y+1): the 17 reference rows they need are
-    // read from LDS once and feed both.  Specialised for a group that is all
-    // 41 partitions (no per-partition mask tests) or a subset.
-    auto sweep = [&](auto all_tag) {
-      const int D = 2 * R + 1;
-      const int DP = (D + 1) >> 1;          // position pairs per column
-      const int ntask = D * DP;
-      const int qstep = kWG / D, rstep = kWG - (kWG / D) * D;
-      int tx = tid % D, ty = tid / D;       // task column, pair row
-      for (int t = tid; t < ntask; t += kWG) {
-        uint32_t a0[16], a1[16];
+  // ---- sweep all (2R+1)^2 positions of the window.  A task is a vertical
+  // pair of positions (x, y), (x, y+1): the 17 reference rows they need are
+  // read from LDS once and feed both.  Specialised for a group that is all
+  // 41 partitions (no per-partition mask tests) or a subset.
+  auto sweep = [&](auto all_tag) {
+    const int D = 2 * R + 1;
+    const int DP = (D + 1) >> 1;          // position pairs per column
+    const int ntask = D * DP;
+    const int qstep = kWG / D, rstep = kWG - (kWG / D) * D;
+    int tx = tid % D, ty = tid / D;       // task column, pair row
+    for (int t = tid; t < ntask; t += kWG) {
+      uint32_t a0[16], a1[16];
 #pragma unroll
-        for (int k = 0; k < 16; ++k) { a0[k] = 0; a1[k] = 0; }
-        {
-          // opaque zero: keeps the broadcast reads of the current MB inside the
-          // loop instead of letting LICM pin 64 VGPRs for them
-          int zero;
-          asm volatile("v_mov_b32 %0, 0" : "=v"(zero));
-          const uint4 *cur4 = reinterpret_cast<const uint4 *>(L.cur) + zero;
-          const uint32_t *wrow = L.words + (2 * ty) * L.wp + tx;
-          // software pipeline, one row ahead: row r+1's reference words and MB
-          // row are requested before row r's v_sad_u8s, so each LDS round trip
-          // hides behind a row of arithmetic (and the other waves of the SIMD)
-          uint32_t n0, n1, n2, n3;
-          uint4 cn;
+      for (int k = 0; k < 16; ++k) { a0[k] = 0; a1[k] = 0; }
+      {
+        // opaque zero: keeps the broadcast reads of the current MB inside the
+        // loop instead of letting LICM pin 64 VGPRs for them
+        uint32_t zero;
+        asm volatile("v_mov_b32 %0, 0" : "=v"(zero));
+        const uint32_t wrow = lds_addr(L.words) + 4u * (uint32_t)((2 * ty) * L.wp + tx);
+        const uint32_t rowb = 4u * (uint32_t)L.wp;
+        const uint32_t cb = lds_addr(curw) + zero;
+        // software pipeline, one row ahead: row r+1's reference words and MB
+        // row are requested before row r's v_sad_u8s, so each LDS round trip
+        // hides behind a row of arithmetic (and the other waves of the SIMD)
+        u32x2 n01, n23;
+        u32x4 cn;
 #ifdef JMME_ABL_NOLDS    // timing ablation only: no window reads
-          n0 = tx; n1 = n0 ^ 1; n2 = n0 ^ 2; n3 = n0 ^ 3;
+        n01 = u32x2{(uint32_t)tx, (uint32_t)tx ^ 1u}; n23 = u32x2{(uint32_t)tx ^ 2u, (uint32_t)tx ^ 3u};
 #else
-          n0 = wrow[0]; n1 = wrow[4]; n2 = wrow[8]; n3 = wrow[12];
+        n01 = ds_read2_0_4(wrow); n23 = ds_read2_8_12(wrow);
 #endif
-          cn = cur4[0];
-          uint4 cprev = make_uint4(0, 0, 0, 0);
+        cn = ds_read_b128(cb);
+        u32x4 cprev = u32x4{0u, 0u, 0u, 0u};
 #pragma unroll
-          for (int r = 0; r < 17; ++r) {
-            const uint32_t w0 = n0, w1 = n1, w2 = n2, w3 = n3;
-            const uint4 c = cn;
-            if (r < 16) {
-              const uint32_t *w = wrow + (r + 1) * L.wp;
+        for (int r = 0; r < 17; ++r) {
+          const u32x2 w01 = n01, w23 = n23;
+          const u32x4 c = cn;
+          if (r < 16) {
+            const uint32_t a = wrow + (uint32_t)(r + 1) * rowb;
 #ifdef JMME_ABL_NOLDS
-              n0 = (r + 1) * 0x01010101u + tx; n1 = n0 ^ 1; n2 = n0 ^ 2; n3 = n0 ^ 3;
-              (void)w;
+            n01 = u32x2{(r + 1) * 0x01010101u + tx, a}; n23 = u32x2{a ^ 2u, a ^ 3u};
 #else
-              n0 = w[0]; n1 = w[4]; n2 = w[8]; n3 = w[12];
+            n01 = ds_read2_0_4(a); n23 = ds_read2_8_12(a);
 #endif
-              if (r < 15) cn = cur4[r + 1];
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            if (r < 16) {   // row r of the MB against position y
-              const int b = (r >> 2) * 4;
-              a0[b + 0] = __builtin_amdgcn_sad_u8(w0, c.x, a0[b + 0]);
-              a0[b + 1] = __builtin_amdgcn_sad_u8(w1, c.y, a0[b + 1]);
-              a0[b + 2] = __builtin_amdgcn_sad_u8(w2, c.z, a0[b + 2]);
-              a0[b + 3] = __builtin_amdgcn_sad_u8(w3, c.w, a0[b + 3]);
-            }
-            if (r > 0) {    // row r-1 of the MB against position y+1
-              const int b = ((r - 1) >> 2) * 4;
-              a1[b + 0] = __builtin_amdgcn_sad_u8(w0, cprev.x, a1[b + 0]);
-              a1[b + 1] = __builtin_amdgcn_sad_u8(w1, cprev.y, a1[b + 1]);
-              a1[b + 2] = __builtin_amdgcn_sad_u8(w2, cprev.z, a1[b + 2]);
-              a1[b + 3] = __builtin_amdgcn_sad_u8(w3, cprev.w, a1[b + 3]);
-            }
-            cprev = c;
-            __builtin_amdgcn_sched_barrier(0);
+            if (r < 15) cn = ds_read_b128(cb + 16u * (uint32_t)(r + 1));
           }
-          // pin the accumulators here: otherwise the SADs are sunk into the
-          // (branchy) cost code and all 17 rows of loads stay live
-#pragma unroll
-          for (int k = 0; k < 16; ++k) asm volatile("" : "+v"(a0[k]), "+v"(a1[k]));
+          __builtin_amdgcn_sched_barrier(0);
+          if (r < 16) {   // row r of the MB against position y
+            const int b = (r >> 2) * 4;
+            a0[b + 0] = __builtin_amdgcn_sad_u8(w01.x, c.x, a0[b + 0]);
+            a0[b + 1] = __builtin_amdgcn_sad_u8(w01.y, c.y, a0[b + 1]);
+            a0[b + 2] = __builtin_amdgcn_sad_u8(w23.x, c.z, a0[b + 2]);
+            a0[b + 3] = __builtin_amdgcn_sad_u8(w23.y, c.w, a0[b + 3]);
+          }
+          if (r > 0) {    // row r-1 of the MB against position y+1
+            const int b = ((r - 1) >> 2) * 4;
+            a1[b + 0] = __builtin_amdgcn_sad_u8(w01.x, cprev.x, a1[b + 0]);
+            a1[b + 1] = __builtin_amdgcn_sad_u8(w01.y, cprev.y, a1[b + 1]);
+            a1[b + 2] = __builtin_amdgcn_sad_u8(w23.x, cprev.z, a1[b + 2]);
+            a1[b + 3] = __builtin_amdgcn_sad_u8(w23.y, cprev.w, a1[b + 3]);
+          }
+          cprev = c;
+          __builtin_amdgcn_sched_barrier(0);
         }
-        const int ox = tx - R;
-        const int candx = g.cqx + 4 * ox;     // candidate MV (qpel, relative to the block)
-        auto eval_position = [&](const uint32_t (&acc)[16], int oyw) {
-          const int oy = oyw - R;
-          uint32_t ps[kNS];
-          partition_sads(acc, ps);
-          PosCtx c;
-          c.lring = max(abs(ox), abs(oy));
-          const int sidx = spiral_index_bl(ox, oy);
-          const int candy = g.cqy + 4 * oy;
-          c.is00 = (candx == 0) && (candy == 0);
-          c.rank = FFS ? ((g.preseed && c.is00) ? 0u : (uint32_t)sidx + 1u) : (uint32_t)sidx;
-          const MvCost mc = mv_cost<FFS>(candx, candy, g.px, g.py, g.lam, g.max_mvd);
-          c.mvc = mc.mvc;
-          c.ok = mc.ok;
-          c.mvc0 = g.chk00 ? check00_adjust(mc.mvc, g.lam, c.is00) : mc.mvc;
-          update_slots<KEY32, FFS, decltype(all_tag)::value>(ps, g, c, best);
-        };
+        // pin the accumulators here: otherwise the SADs are sunk into the
+        // (branchy) cost code and all 17 rows of loads stay live
+#pragma unroll
+        for (int k = 0; k < 16; ++k) asm volatile("" : "+v"(a0[k]), "+v"(a1[k]));
+      }
+      const int ox = tx - R;
+      const int candx = g.cqx + 4 * ox;     // candidate MV (qpel, relative to the block)
+      auto eval_position = [&](const uint32_t (&acc)[16], int oyw) {
+        const int oy = oyw - R;
+        uint32_t ps[kNS];
+        partition_sads(acc, ps);
+        PosCtx c;
+        c.lring = max(abs(ox), abs(oy));
+        const int sidx = spiral_index_bl(ox, oy);
+        const int candy = g.cqy + 4 * oy;
+        c.is00 = (candx == 0) && (candy == 0);
+        c.rank = FFS ? ((g.preseed && c.is00) ? 0u : (uint32_t)sidx + 1u) : (uint32_t)sidx;
+        const MvCost mc = mv_cost<FFS>(candx, candy, g.px, g.py, g.lam, g.max_mvd);
+        c.mvc = mc.mvc;
+        c.ok = mc.ok;
+        c.mvc0 = g.chk00 ? check00_adjust(mc.mvc, g.lam, c.is00) : mc.mvc;
+        update_slots<KEY32, FFS, decltype(all_tag)::value>(ps, g, c, best);
+      };
 #ifdef JMME_ABL_NOCOST   // timing ablation only: keep the SADs live, skip the cost/minimum work
 #pragma unroll
-        for (int k = 0; k < 16; ++k) asm volatile("" :: "v"(a0[k]), "v"(a1[k]));
-        (void)eval_position;
+      for (int k = 0; k < 16; ++k) asm volatile("" :: "v"(a0[k]), "v"(a1[k]));
+      (void)eval_position;
 #else
-        eval_position(a0, 2 * ty);
-        if (2 * ty + 1 < D) eval_position(a1, 2 * ty + 1);   // odd D: last pair has one position
+      eval_position(a0, 2 * ty);
+      if (2 * ty + 1 < D) eval_position(a1, 2 * ty + 1);   // odd D: last pair has one position
 #endif
-        tx += rstep;
-        ty += qstep;
-        if (tx >= D) { tx -= D; ++ty; }
-      }
-    };
-    if (gmask == kAll) sweep(std::integral_constant<bool, true>{});
-    else sweep(std::integral_constant<bool, false>{});
-    STAMP(st_sweep);
+      tx += rstep;
+      ty += qstep;
+      if (tx >= D) { tx -= D; ++ty; }
+    }
+  };
+  // every partition's minimum is tracked even when the group is a subset: the
+  // slots outside gmask are simply never read back (one code path, no
+  // per-partition masks in the loop)
+  sweep(std::integral_constant<bool, true>{});
+  STAMP(st.sweep);
 
-    // ---- workgroup reduction of this group's per-thread minima
+  // ---- workgroup reduction of this group's per-thread minima
 #pragma unroll
-    for (int s = 0; s < kNS; ++s) {
-      if (!((gmask >> s) & 1)) continue;
-      Best k = best[s];
+  for (int s = 0; s < kNS; ++s) {
+    if (!((gmask >> s) & 1)) continue;
+#ifndef JMME_NO_DPP
+    if (KEY32) {
+      const uint32_t k = wave_min_u32((uint32_t)best[s]);
+      if (lane == 63) L.red[wave * kNS + s] = k;
+    } else
+#endif
+    {
+      unsigned long long k = best[s];
 #pragma unroll
       for (int off = 32; off >= 1; off >>= 1) {
-        if (KEY32) {
-          const uint32_t o = __shfl_xor((uint32_t)k, off, 64);
-          k = min((uint32_t)k, o);
-        } else {
-          const unsigned lo = __shfl_xor((unsigned)k, off, 64);
-          const unsigned hi = __shfl_xor((unsigned)((unsigned long long)k >> 32), off, 64);
-          const unsigned long long o = ((unsigned long long)hi << 32) | lo;
-          k = o < (unsigned long long)k ? o : k;
-        }
+        const unsigned lo = __shfl_xor((unsigned)k, off, 64);
+        const unsigned hi = __shfl_xor((unsigned)(k >> 32), off, 64);
+        const unsigned long long o = ((unsigned long long)hi << 32) | lo;
+        k = o < k ? o : k;
       }
-      if (lane == 0) L.red[wave * kNS + s] = (unsigned long long)k;
+      if (lane == 0) L.red[wave * kNS + s] = k;
     }
-    __syncthreads();
-    if (tid < kNS) {
-      unsigned long long k = L.red[tid];
+  }
+  __syncthreads();
+  if (tid < kNS) {
+    unsigned long long k = L.red[tid];
 #pragma unroll
-      for (int w = 1; w < kWaves; ++w) { const unsigned long long o = L.red[w * kNS + tid]; k = o < k ? o : k; }
-      L.red[tid] = k;   // wave 0's row now holds the group result
+    for (int w = 1; w < kWaves; ++w) { const unsigned long long o = L.red[w * kNS + tid]; k = o < k ? o : k; }
+    L.red[tid] = k;   // wave 0's row now holds the group result
+  }
+  __syncthreads();
+  STAMP(st.reduce);
+
+  // ---- refine (32-bit keys): recover the 3 rank bits the key dropped.
+  // The winner has cost == key>>10 and rank in [8c, 8c+8), c = key & 1023;
+  // re-evaluate those positions exactly and take the smallest matching rank.
+  if (KEY32) {
+    const int D = 2 * R + 1;
+    for (int item = tid; item < kNS * kCand; item += kWG) {
+      const int s = item / kCand, j = item - s * kCand;
+      uint32_t m = 0;
+      const uint32_t key = (uint32_t)L.red[s];
+      if (((gmask >> s) & 1) && key != ~0u) {
+        const uint32_t mincost = key >> kCostShift;
+        const int rk = (int)(((key & ((1u << kCostShift) - 1)) << kRankDrop) + j);
+        int ox = 0, oy = 0;
+        bool valid;
+        if (FFS && rk == 0) {          // the pre-seeded (0,0) vector
+          ox = -(g.cqx >> 2); oy = -(g.cqy >> 2);
+          valid = g.preseed && abs(ox) <= R && abs(oy) <= R;
+        } else {
+          const int sidx = FFS ? rk - 1 : rk;
+          valid = sidx < D * D;
+          if (valid) spiral_offset_fast(sidx, &ox, &oy);
+        }
+        if (valid) {
+          const int candx = g.cqx + 4 * ox, candy = g.cqy + 4 * oy;
+          PosCtx c;
+          c.is00 = (candx == 0) && (candy == 0);
+          c.lring = max(abs(ox), abs(oy));
+          const int sidx = spiral_index_bl(ox, oy);
+          c.rank = FFS ? ((g.preseed && c.is00) ? 0u : (uint32_t)sidx + 1u) : (uint32_t)sidx;
+          const MvCost mc = mv_cost<FFS>(candx, candy, g.px, g.py, g.lam, g.max_mvd);
+          c.ok = mc.ok;
+          const uint32_t mv = (s == 0 && g.chk00) ? check00_adjust(mc.mvc, g.lam, c.is00) : mc.mvc;
+          const uint32_t cost = (partition_sad_at(L, curw, s, ox + R, oy + R) << 5) + mv;
+          m = (c.rank == (uint32_t)rk) && cost == mincost && slot_eligible<FFS>(g, c, s);
+        }
+      }
+      L.match[item] = m;
     }
     __syncthreads();
-    STAMP(st_reduce);
+  }
+  STAMP(st.refine);
 
-    // ---- refine (32-bit keys): recover the 3 rank bits the key dropped.
-    // The winner has cost == key>>10 and rank in [8c, 8c+8), c = key & 1023;
-    // re-evaluate those positions exactly and take the smallest matching rank.
+  // ---- results of this group
+  if (tid < kNS && ((gmask >> tid) & 1)) {
+    const unsigned long long k = L.red[tid];
+    jmme_block_res res;
+    res.reserved = 0;
+    uint32_t rank = 0, cost = 0;
+    bool found = false;
     if (KEY32) {
-      const int D = 2 * R + 1;
-      for (int item = tid; item < kNS * kCand; item += kWG) {
-        const int s = item / kCand, j = item - s * kCand;
-        uint32_t m = 0;
-        const uint32_t key = (uint32_t)L.red[s];
-        if (((gmask >> s) & 1) && key != ~0u) {
-          const uint32_t mincost = key >> kCostShift;
-          const int rk = (int)(((key & ((1u << kCostShift) - 1)) << kRankDrop) + j);
-          int ox = 0, oy = 0;
-          bool valid;
-          if (FFS && rk == 0) {          // the pre-seeded (0,0) vector
-            ox = -(g.cqx >> 2); oy = -(g.cqy >> 2);
-            valid = g.preseed && abs(ox) <= R && abs(oy) <= R;
-          } else {
-            const int sidx = FFS ? rk - 1 : rk;
-            valid = sidx < D * D;
-            if (valid) spiral_offset(sidx, &ox, &oy);
+      const uint32_t key = (uint32_t)k;
+      if (key != ~0u) {
+        for (int j = 0; j < kCand && !found; ++j)
+          if (L.match[tid * kCand + j]) {
+            found = true;
+            rank = ((key & ((1u << kCostShift) - 1)) << kRankDrop) + j;
           }
-          if (valid) {
-            const int candx = g.cqx + 4 * ox, candy = g.cqy + 4 * oy;
-            PosCtx c;
-            c.is00 = (candx == 0) && (candy == 0);
-            c.lring = max(abs(ox), abs(oy));
-            const int sidx = spiral_index(ox, oy);
-            c.rank = FFS ? ((g.preseed && c.is00) ? 0u : (uint32_t)sidx + 1u) : (uint32_t)sidx;
-            const MvCost mc = mv_cost<FFS>(candx, candy, g.px, g.py, g.lam, g.max_mvd);
-            c.ok = mc.ok;
-            const uint32_t mv = (s == 0 && g.chk00) ? check00_adjust(mc.mvc, g.lam, c.is00) : mc.mvc;
-            const uint32_t cost = (partition_sad_at(L, s, ox + R, oy + R) << 5) + mv;
-            m = (c.rank == (uint32_t)rk) && cost == mincost && slot_eligible<FFS>(g, c, s);
-          }
-        }
-        L.match[item] = m;
+        cost = key >> kCostShift;
+        if (!found) atomicOr(&p.counts[2], 4u);   // cannot happen: refine lost the winner
       }
-      __syncthreads();
+    } else if (k != ~0ull) {
+      found = true;
+      rank = (uint32_t)(k & 0x7fffffffu);
+      cost = (uint32_t)(k >> 32);
     }
-    STAMP(st_refine);
-
-    // ---- results of this group
-    if (tid < kNS && ((gmask >> tid) & 1)) {
-      const unsigned long long k = L.red[tid];
-      jmme_block_res res;
-      res.reserved = 0;
-      uint32_t rank = 0, cost = 0;
-      bool found = false;
-      if (KEY32) {
-        const uint32_t key = (uint32_t)k;
-        if (key != ~0u) {
-          for (int j = 0; j < kCand && !found; ++j)
-            if (L.match[tid * kCand + j]) {
-              found = true;
-              rank = ((key & ((1u << kCostShift) - 1)) << kRankDrop) + j;
-            }
-          cost = key >> kCostShift;
-          if (!found) atomicOr(p.status, 4u);   // cannot happen: refine lost the winner
-        }
-      } else if (k != ~0ull) {
-        found = true;
-        rank = (uint32_t)(k & 0x7fffffffu);
-        cost = (uint32_t)(k >> 32);
-      }
-      if (!found) {
-        // nothing eligible: JM leaves best_pos = 0 and returns the incoming min_mcost
-        res.mv_x = (int16_t)g.cqx; res.mv_y = (int16_t)g.cqy; res.cost = JMME_DISTBLK_MAX;
-      } else {
-        int ox, oy;
-        if (FFS && rank == 0) { ox = -(g.cqx >> 2); oy = -(g.cqy >> 2); }   // the pre-seeded (0,0)
-        else spiral_offset(FFS ? (int)rank - 1 : (int)rank, &ox, &oy);
-        res.mv_x = (int16_t)(g.cqx + 4 * ox);
-        res.mv_y = (int16_t)(g.cqy + 4 * oy);
-        res.cost = (int64_t)cost;
-      }
-      p.out[(size_t)u * kNS + tid] = res;
+    if (!found) {
+      // nothing eligible: JM leaves best_pos = 0 and returns the incoming min_mcost
+      res.mv_x = (int16_t)g.cqx; res.mv_y = (int16_t)g.cqy; res.cost = JMME_DISTBLK_MAX;
+    } else {
+      int ox, oy;
+      if (FFS && rank == 0) { ox = -(g.cqx >> 2); oy = -(g.cqy >> 2); }   // the pre-seeded (0,0)
+      else spiral_offset_fast(FFS ? (int)rank - 1 : (int)rank, &ox, &oy);
+      res.mv_x = (int16_t)(g.cqx + 4 * ox);
+      res.mv_y = (int16_t)(g.cqy + 4 * oy);
+      res.cost = (int64_t)cost;
     }
-    STAMP(st_out);
+    p.out[(size_t)u * kNS + tid] = res;
   }
-#ifdef JMME_STAMPS
-  if (p.stamps && tid == 0) {
-    unsigned long long *o = p.stamps + (size_t)u * 8;
-    o[0] = st_setup; o[1] = st_stage; o[2] = st_sweep; o[3] = st_reduce; o[4] = st_refine; o[5] = st_out;
-    o[6] = __builtin_popcountll(slot_mask); o[7] = 1;
-  }
-#endif
+  STAMP(st.out);
 }
 
-// direct pass: one workgroup per unit (XCD-aware order)
+// item descriptors are wave-uniform: keep every field in SGPRs
+__device__ __forceinline__ Item load_item(const Item *items, unsigned j) {
+  const int *src = reinterpret_cast<const int *>(items + j);
+  Item it;
+  int *dst = reinterpret_cast<int *>(&it);
+#pragma unroll
+  for (int k = 0; k < (int)(sizeof(Item) / 4); ++k) dst[k] = ufl(src[k]);
+  return it;
+}
+
+// Persistent item kernel.  The KEY32 instance drains the 32-bit list, the
+// other the 64-bit list.  Items are dealt to XCD x (= blockIdx % 8) as the
+// contiguous run [x*cnt/8, (x+1)*cnt/8), strided over that XCD's workgroups.
 template <bool KEY32, bool FFS>
-__global__ __launch_bounds__(kWG, KEY32 ? JMME_WAVES_PER_EU : 2) void me_units_kernel(KParams p) {
+__global__ __launch_bounds__(kWG, KEY32 ? JMME_WAVES_PER_EU : 2) void me_items_kernel(KParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int u = xcd_unit(blockIdx.x, gridDim.x);
-  if (u >= p.n) return;
-  unit_body<KEY32, FFS>(p, u, smem);
+  __shared__ __attribute__((aligned(16))) uint32_t s_cur[64];
+  __shared__ int4 s_slot[kNS];
+  const unsigned cnt = p.counts[KEY32 ? 0 : 1];
+  const Item *items = KEY32 ? p.items : p.items + (p.item_cap - cnt);
+  const int x = blockIdx.x & 7, lb = blockIdx.x >> 3, nbx = (gridDim.x - x + 7) >> 3;
+  const unsigned start = (unsigned)(((unsigned long long)cnt * x) >> 3);
+  const unsigned end = (unsigned)(((unsigned long long)cnt * (x + 1)) >> 3);
+  unsigned j = start + lb;
+  if (j >= end) return;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = ufl(tid >> 6);
+  Lds L = carve(smem, p.lds_range);
+  L.cur = s_cur;
+  L.slot = s_slot;
+  const unsigned long long dbg_slot =
+      p.debug_words ? (1ull << __builtin_ctzll((ufl64(p.req[0].slot_mask) & kAll) | (1ull << 63))) : 0ull;
+#ifdef JMME_STAMPS
+  unsigned long long t_last = __builtin_amdgcn_s_memtime();
+#endif
+
+  Item it = load_item(items, j);
+  prefetch(p, it, L, wave, lane);
+  for (;;) {
+#ifdef JMME_STAMPS
+    ItemStamps<KEY32, FFS> st;
+#endif
+    const unsigned jn = j + nbx;
+    const bool more = jn < end;
+    Item nx;
+    if (more) nx = load_item(items, jn);
+    // this item's fetch has landed (every wave waits for its own loads, the
+    // barrier for everyone's); the previous item is completely done with LDS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    STAMP(st.wait);
+    if (it.gmask) expand(p, it, L, tid);
+    __syncthreads();
+    if (p.debug_words && it.u == 0 && (it.gmask & dbg_slot)) {
+      const Win w = win_of(p, it);
+      for (int i = tid; i < w.wrows * L.wp; i += kWG) p.debug_words[i] = L.words[i];
+    }
+    STAMP(st.expand);
+    // the raw buffer is free: start fetching the next item behind this sweep
+    if (more) prefetch(p, nx, L, wave, lane);
+    if (it.gmask) {
+#ifdef JMME_STAMPS
+      search_item<KEY32, FFS>(p, it, L, t_last, st);
+#else
+      search_item<KEY32, FFS>(p, it, L);
+#endif
+    }
+#ifdef JMME_STAMPS
+    if (p.stamps && tid == 0) {
+      unsigned long long *o = p.stamps + (size_t)it.u * 8;
+      atomicAdd(o + 0, st.wait); atomicAdd(o + 1, st.expand); atomicAdd(o + 2, st.sweep);
+      atomicAdd(o + 3, st.reduce); atomicAdd(o + 4, st.refine); atomicAdd(o + 5, st.out);
+      atomicAdd(o + 6, (unsigned long long)__builtin_popcountll(it.gmask)); atomicAdd(o + 7, 1ull);
+    }
+#endif
+    if (!more) break;
+    it = nx;
+    j = jn;
+  }
 }
 
-// deferred pass (64-bit keys): a small grid drains the device-side list of
-// units the 32-bit pass could not take; every workgroup exits when the list ends
-template <bool FFS>
-__global__ __launch_bounds__(kWG, 1) void me_units_deferred_kernel(KParams p) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const unsigned cnt = *p.unit_count;
-  for (unsigned i = blockIdx.x; i < cnt; i += gridDim.x) {
-    unit_body<false, FFS>(p, p.unit_list[i], smem);
-    __syncthreads();
+struct Occupancy {
+  int cus = 0;
+  int wg[4][JMME_MAX_RANGE + 1] = {};   // resident workgroups per CU, by kernel variant and lds range
+};
+
+template <typename K>
+int resident_grid(Occupancy &o, int variant, K kernel, int lds_range, size_t lds) {
+  if (!o.cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&o.cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || o.cus <= 0)
+      o.cus = 256;
   }
+  int &nb = o.wg[variant][lds_range];
+  if (!nb) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, kWG, lds) != hipSuccess || nb <= 0) nb = 1;
+  }
+  return nb * o.cus;
 }
 
 }  // namespace
 
-size_t units_lds_bytes(int R) {
+size_t items_lds_bytes(int R) {
   const int rows = 2 * R + 16;
   const int wp = (2 * R + 13) | 1;
   size_t off = (size_t)rows * wp * 4;
   off = (off + 15) & ~(size_t)15;
-  off += (size_t)rows * lds_rawp(R);
+  off += ((size_t)rows * raw_row_dwords(R) + kRawExtra) * 4;
   off = (off + 15) & ~(size_t)15;
-  off += 64 * 4 + kNS * 16 + kNS * 8 + kWaves * kNS * 8 + kNS * kCand * 4 + 16;
+  off += kWaves * kNS * 8 + kNS * kCand * 4;
   return off;
 }
 
-hipError_t launch_units(const KParams &p, bool key32, int grid, hipStream_t s) {
-  const size_t lds = units_lds_bytes(p.lds_range);
+hipError_t launch_search(const KParams &p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
+  static thread_local Occupancy occ;
+  const size_t lds = items_lds_bytes(p.lds_range);
   const bool ffs = p.mode == JMME_FAST_FULL_SEARCH;
-  if (p.unit_list) {
-    if (ffs) hipLaunchKernelGGL(me_units_deferred_kernel<true>, dim3(grid), dim3(kWG), lds, s, p);
-    else hipLaunchKernelGGL(me_units_deferred_kernel<false>, dim3(grid), dim3(kWG), lds, s, p);
-  } else if (key32) {
-    if (ffs) hipLaunchKernelGGL((me_units_kernel<true, true>), dim3(grid), dim3(kWG), lds, s, p);
-    else hipLaunchKernelGGL((me_units_kernel<true, false>), dim3(grid), dim3(kWG), lds, s, p);
+  const int plan_grid = (p.n + kPlanWaves - 1) / kPlanWaves;
+  if (ffs) hipLaunchKernelGGL(me_plan_kernel<true>, dim3(plan_grid), dim3(64 * kPlanWaves), 0, s, p);
+  else hipLaunchKernelGGL(me_plan_kernel<false>, dim3(plan_grid), dim3(64 * kPlanWaves), 0, s, p);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  auto k32 = ffs ? me_items_kernel<true, true> : me_items_kernel<true, false>;
+  auto k64 = ffs ? me_items_kernel<false, true> : me_items_kernel<false, false>;
+  const int v = ffs ? 2 : 0;
+  if (ev0) (void)hipEventRecord(ev0, s);
+  if (p.key32) {
+    hipLaunchKernelGGL(k32, dim3(resident_grid(occ, v, k32, p.lds_range, lds)), dim3(kWG), lds, s, p);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (ev1) (void)hipEventRecord(ev1, s);
+    // units whose lambda could saturate the 32-bit cost field (none in
+    // practice) were planned into the 64-bit list: a small grid drains it
+    hipLaunchKernelGGL(k64, dim3(64), dim3(kWG), lds, s, p);
   } else {
-    if (ffs) hipLaunchKernelGGL((me_units_kernel<false, true>), dim3(grid), dim3(kWG), lds, s, p);
-    else hipLaunchKernelGGL((me_units_kernel<false, false>), dim3(grid), dim3(kWG), lds, s, p);
+    hipLaunchKernelGGL(k64, dim3(resident_grid(occ, v + 1, k64, p.lds_range, lds)), dim3(kWG), lds, s, p);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (ev1) (void)hipEventRecord(ev1, s);
   }
   return hipGetLastError();
 }

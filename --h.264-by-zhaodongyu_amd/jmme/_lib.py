@@ -84,7 +84,10 @@ def lib() -> ctypes.CDLL:
         "jmme_debug_window": (I, [P, I, P, P, I]),
         "jmme_debug_stamps": (I, [P, P, I]),
     }
+    optional = {"jmme_debug_stamps"}   # absent from older builds (A/B baselines)
     for name, (res, args) in sig.items():
+        if name in optional and not hasattr(L, name):
+            continue
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args

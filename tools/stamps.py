@@ -16,8 +16,8 @@ out = me.search(FULL_SEARCH, req)
 st = np.zeros((len(req), 8), np.uint64)
 n = _lib.lib().jmme_debug_stamps(me._ctx, _lib.ptr(st), len(req))
 st = st[:n].astype(np.float64)
-names = ["setup", "stage", "sweep", "reduce", "refine", "output"]
+names = ["wait", "expand", "sweep", "reduce", "refine", "output"]
 tot = st[:, :6].sum(1)
-print("units", n, "mean cycles per unit", tot.mean())
+print("units", n, "items", int(st[:, 7].sum()), "mean cycles per unit", tot.mean())
 for i, nm in enumerate(names):
     print(f"{nm:8s} mean {st[:, i].mean():12.0f} cyc  {100 * st[:, i].sum() / tot.sum():5.1f}%")
