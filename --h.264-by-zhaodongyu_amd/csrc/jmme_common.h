@@ -69,8 +69,8 @@ JMME_HD int slot_of(int bt, int bx, int by) {
   }
 }
 
-JMME_HD SlotGeom slot_geom(int s) {
-  SlotGeom g;
+JMME_HD constexpr SlotGeom slot_geom(int s) {
+  SlotGeom g{};
   if (s == 0) { g.bt = 1; g.bx = 0; g.by = 0; g.w = 4; g.h = 4; }
   else if (s <= 2) { g.bt = 2; g.bx = 0; g.by = (int8_t)(2 * (s - 1)); g.w = 4; g.h = 2; }
   else if (s <= 4) { g.bt = 3; g.bx = (int8_t)(2 * (s - 3)); g.by = 0; g.w = 2; g.h = 4; }

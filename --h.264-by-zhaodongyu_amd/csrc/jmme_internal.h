@@ -16,7 +16,9 @@ constexpr int kWG = 256;             // 4 waves of 64
 // of them).  Built on the device by the plan kernel from the unit requests.
 struct Item {
   unsigned long long gmask;   // partitions (slots) served; 0 = refused item (status set)
-  unsigned long long rlim;    // FFS: members whose own range is below the window's
+  int rs;                     // FFS: the members' own search range (<= R; positions beyond ring rs
+                              // are not theirs, except a pre-seeded (0,0))
+  int pad0;
   int u;                      // unit index
   int16_t mb_x, mb_y;
   int16_t cqx, cqy;           // window centre (qpel, on the integer grid)

@@ -25,7 +25,7 @@
 //   * item kernels (persistent, one 256-thread workgroup per CU slot, items
 //     statically dealt in contiguous runs per XCD so neighbouring macroblocks'
 //     overlapping windows hit the same L2): while item k is swept, item k+1's
-//     reference window, current MB and slot requests stream HBM -> LDS with
+//     reference window and current MB stream HBM -> LDS with
 //     global_load_lds (no VGPRs held), so the sweep hides the fetch latency;
 //   * window in LDS as "word[y][x] = pels x..x+3": every SAD row read is an
 //     aligned ds_read_b32;
@@ -58,6 +58,23 @@ constexpr int kCostShift = 10;             // key32 = cost << 10 | rank >> 3
 constexpr int kRankDrop = 3;
 constexpr int kCand = 1 << kRankDrop;      // refine candidates per partition
 constexpr int kPlanWaves = 16;             // plan kernel: units per workgroup
+constexpr int kRed1 = (kNS + 3) / 4 * 2;      // reduce: registers after the permlane32 level (22)
+constexpr int kRed2 = kRed1 / 2;              //         ... after the permlane16 level (11)
+
+// refine work list: every 4x4 block of every partition, (slot << 4) | (by*4 + bx)
+constexpr int kBlkItems = 112;
+struct BlkTab { uint16_t v[kBlkItems]; };
+constexpr BlkTab make_blk_tab() {
+  BlkTab t{};
+  int n = 0;
+  for (int s = 0; s < kNS; ++s) {
+    const SlotGeom gm = slot_geom(s);
+    for (int j = 0; j < gm.h; ++j)
+      for (int i = 0; i < gm.w; ++i) t.v[n++] = (uint16_t)((s << 4) | ((gm.by + j) * 4 + gm.bx + i));
+  }
+  return t;
+}
+__constant__ BlkTab kBlkTab = make_blk_tab();
 #ifndef JMME_WAVES_PER_EU
 #define JMME_WAVES_PER_EU 4
 #endif
@@ -65,18 +82,16 @@ constexpr int kPlanWaves = 16;             // plan kernel: units per workgroup
 // dwords per staged raw row: the words of a row read pels x0 .. x0+2R+15,
 // fetched as aligned dwords from floor4(x0) (+1 dword for alignbyte's high half)
 __host__ __device__ inline int raw_row_dwords(int R) { return (3 + 2 * R + 13 + 2) / 4 + 2; }
-// the fetch also carries the item's current MB and slot requests behind the
-// window (LDS DMA only ever targets the raw area: the sweep's LDS reads never
-// alias an in-flight fetch, so the compiler inserts no vmcnt waits there)
-constexpr int kRawExtra = 64 + 4 * JMME_NSLOT + 64;   // + one wave of slack: fetch chunks are 64-aligned
+// the fetch also carries the item's current MB behind the window (LDS DMA only
+// ever targets the raw area, never what the sweep reads)
+constexpr int kRawExtra = 64;
 
 struct Lds {
   int wp;                   // words per window row
   uint32_t *words;          // current item's window, rows x wp
   uint32_t *raw;            // next item as fetched: window rows x nd dwords (dense),
-                            // then its current MB (64) and slot requests (164)
-  uint32_t *cur;            // 64 words: MB row r, column group c at [r*4+c]  (static LDS:
-  int4 *slot;               // 41 x jmme_block_req                            provably not the DMA target)
+                            // then its current MB (64 dwords)
+  uint32_t *cur;            // 64 words: MB row r, column group c at [r*4+c] (static LDS)
   unsigned long long *red;  // kWaves x 41 reduction scratch
   uint32_t *match;          // 41 x kCand refine flags
 };
@@ -109,6 +124,15 @@ __device__ __forceinline__ unsigned long long ufl64(unsigned long long v) {
   unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
   unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
   return ((unsigned long long)hi << 32) | lo;
+}
+
+// threadIdx.x through an opaque copy: values derived from it are recomputed in
+// the phase that uses them instead of being hoisted out of the item loop (and
+// kept live -- spilled -- across the sweep)
+__device__ __forceinline__ int opaque_tid() {
+  int t = threadIdx.x;
+  asm volatile("" : "+v"(t));
+  return t;
 }
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
@@ -216,20 +240,18 @@ struct PosCtx {
 struct GroupCtx {
   int R, cqx, cqy, px, py, lam, chk00, max_mvd;
   bool preseed;
-  unsigned long long gmask, rlim;
-  const int4 *slot;
+  unsigned long long gmask;
+  int rs;
 };
 
-// FFS partition searched over a smaller range than the surface (me_fullfast.c:627)
+// FFS eligibility of a position for the item's partitions: the GetMaxMVD gate
+// (me_fullfast.c:663) and the partition's own range when it is below the
+// surface's (me_fullfast.c:627) -- the pre-seeded (0,0) is always a candidate.
+// Uniform over the item: partitions are grouped by their range too.
 template <bool FFS>
-__device__ __forceinline__ bool slot_eligible(const GroupCtx &g, const PosCtx &c, int s) {
+__device__ __forceinline__ bool pos_eligible(const GroupCtx &g, bool gate_ok, int lring, bool is00) {
   if (!FFS) return true;
-  bool oks = c.ok;
-  if ((g.rlim >> s) & 1) {
-    const int rs = ufl(rq_range(g.slot[s]));
-    oks = oks && (c.lring <= rs || (g.preseed && c.is00));
-  }
-  return oks;
+  return gate_ok && (lring <= g.rs || (g.preseed && is00));
 }
 
 template <bool KEY32, bool FFS, bool ALL, typename Best>
@@ -243,7 +265,7 @@ __device__ __forceinline__ void update_slots(const uint32_t (&ps)[kNS], const Gr
       if (!ALL && !((g.gmask >> s) & 1)) continue;
       // cost<<10 | rank>>3  ==  (SAD << 15) + ((mvc << 10) | rank >> 3)
       const uint32_t k = (ps[s] << (5 + kCostShift)) + (s == 0 ? k32_0 : k32);
-      const uint32_t kk = FFS ? (slot_eligible<FFS>(g, c, s) ? k : ~0u) : k;
+      const uint32_t kk = FFS ? (c.ok ? k : ~0u) : k;
       best[s] = min((uint32_t)best[s], kk);
     }
   } else {
@@ -252,7 +274,7 @@ __device__ __forceinline__ void update_slots(const uint32_t (&ps)[kNS], const Gr
       if (!ALL && !((g.gmask >> s) & 1)) continue;
       const uint32_t hi = (ps[s] << 5) + (s == 0 ? c.mvc0 : c.mvc);
       const unsigned long long k = ((unsigned long long)hi << 32) | c.rank;
-      const unsigned long long kk = FFS ? (slot_eligible<FFS>(g, c, s) ? k : ~0ull) : k;
+      const unsigned long long kk = FFS ? (c.ok ? k : ~0ull) : k;
       best[s] = best[s] < kk ? best[s] : kk;
     }
   }
@@ -270,19 +292,9 @@ __device__ __forceinline__ uint32_t partition_sad_at(const Lds &L, const uint32_
   return sad;
 }
 
-// minimum over the wave with DPP (row_shr 1,2,4,8 then row_bcast 15/31): lane 63
-// ends with the wave minimum.  No LDS traffic, 6 VALU ops per value.
-__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
-#define JMME_DPP_MIN(ctrl, rmask) \
-  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, ctrl, rmask, 0xf, false))
-  JMME_DPP_MIN(0x111, 0xf);   // row_shr:1
-  JMME_DPP_MIN(0x112, 0xf);   // row_shr:2
-  JMME_DPP_MIN(0x114, 0xf);   // row_shr:4
-  JMME_DPP_MIN(0x118, 0xf);   // row_shr:8
-  JMME_DPP_MIN(0x142, 0xa);   // row_bcast:15
-  JMME_DPP_MIN(0x143, 0xc);   // row_bcast:31
-#undef JMME_DPP_MIN
-  return v;
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_min(uint32_t v) {
+  return min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, 0xf, 0xf, false));
 }
 
 // ------------------------------------------------------------ plan kernel --
@@ -295,12 +307,11 @@ __global__ __launch_bounds__(64 * kPlanWaves) void me_plan_kernel(KParams p) {
   const int u = blockIdx.x * kPlanWaves + wave;
   int ng = 0;
   bool to64 = !p.key32;
-  unsigned long long my_gm = 0, my_rl = 0;
+  unsigned long long my_gm = 0;
   int my_lead = 0;
   if (u < p.n) {
     const jmme_mb_req *rq = p.req + u;
     const unsigned long long mask = ufl64(rq->slot_mask) & kAll;
-    const int fR = ufl(rq->ffs_range);
     const int4 me = lane < kNS ? reinterpret_cast<const int4 *>(&rq->blk[0])[lane] : make_int4(0, 0, 0, 0);
     const bool valid = lane < kNS && ((mask >> lane) & 1);
     if (__builtin_amdgcn_ballot_w64(valid && (uint32_t)rq_lambda(me) > kMaxLambda32)) to64 = true;
@@ -312,11 +323,11 @@ __global__ __launch_bounds__(64 * kPlanWaves) void me_plan_kernel(KParams p) {
       const int oz = __builtin_amdgcn_readlane(me.z, lead);
       const int ow = __builtin_amdgcn_readlane(me.w, lead);
       // same predictor and lambda; FS also the same window (centre, range)
-      const bool eq = valid && me.x == ox && me.w == ow &&
-                      (FFS || (me.y == oy && rq_range(me) == (int)(short)(oz & 0xffff)));
+      // FFS: also the same own range (the eligibility test is then per item)
+      const bool eq = valid && me.x == ox && me.w == ow && rq_range(me) == (int)(short)(oz & 0xffff) &&
+                      (FFS || me.y == oy);
       const unsigned long long gm = __builtin_amdgcn_ballot_w64(eq) & rem;
-      const unsigned long long rl = FFS ? (__builtin_amdgcn_ballot_w64(eq && rq_range(me) < fR) & rem) : 0ull;
-      if (lane == ng) { my_gm = gm; my_rl = rl; my_lead = lead; }
+      if (lane == ng) { my_gm = gm; my_lead = lead; }
       ++ng;
       rem &= ~gm;
     }
@@ -340,7 +351,8 @@ __global__ __launch_bounds__(64 * kPlanWaves) void me_plan_kernel(KParams p) {
     const int4 lq = reinterpret_cast<const int4 *>(&rq->blk[0])[my_lead];
     Item it;
     it.gmask = my_gm;
-    it.rlim = my_rl;
+    it.rs = rq_range(lq);
+    it.pad0 = 0;
     it.u = u;
     it.mb_x = rq->mb_x;
     it.mb_y = rq->mb_y;
@@ -386,12 +398,12 @@ __device__ __forceinline__ Win win_of(const KParams &p, const Item &it) {
 }
 
 // Issue the HBM -> LDS fetch of item `it` (window rows clamped into the
-// picture, dword columns clamped into it -- UMVLine4X), its current MB and its
-// slot requests.  global_load_lds: per-lane global address, LDS destination
+// picture, dword columns clamped into it -- UMVLine4X) and its current MB.  global_load_lds: per-lane global address, LDS destination
 // contiguous per wave instruction; completion is awaited (vmcnt) only at the
 // top of the next item.
-__device__ __forceinline__ void prefetch(const KParams &p, const Item &it, const Lds &L, int wave, int lane) {
+__device__ __forceinline__ void prefetch(const KParams &p, const Item &it, const Lds &L) {
   if (!it.gmask) return;
+  const int tid = opaque_tid(), lane = tid & 63, wave = ufl(tid >> 6);
   const Win w = win_of(p, it);
   const uint8_t *ref = p.refs[it.ref];
   const int total = w.wrows * w.nd;
@@ -405,31 +417,38 @@ __device__ __forceinline__ void prefetch(const KParams &p, const Item &it, const
       __builtin_amdgcn_global_load_lds(ref + (size_t)gy * p.pitch + 4 * pd, L.raw + base, 4, 0, 0);
     }
   }
-  // behind the window: current MB (wave 0), slot requests (waves 1..3)
-  uint32_t *tail = L.raw + total;
+  // behind the window: the current MB (wave 0)
   if (wave == 0) {
     const int r = lane >> 2, c = lane & 3;
-    __builtin_amdgcn_global_load_lds(p.cur + (size_t)(it.mb_y + r) * p.pitch + it.mb_x + 4 * c, tail, 4, 0, 0);
-  } else {
-    const int i = (wave - 1) * 64 + lane;
-    if (i < kNS * 4)
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint32_t *>(&p.req[it.u].blk[0]) + i,
-                                       tail + 64 + (wave - 1) * 64, 4, 0, 0);
+    __builtin_amdgcn_global_load_lds(p.cur + (size_t)(it.mb_y + r) * p.pitch + it.mb_x + 4 * c, L.raw + total, 4, 0,
+                                     0);
   }
 }
 
 // raw dwords -> words (word[y][x] = pels x..x+3 of the window)
-__device__ __forceinline__ void expand(const KParams &p, const Item &it, const Lds &L, int tid) {
+__device__ __forceinline__ void expand(const KParams &p, const Item &it, const Lds &L) {
+  const int tid = opaque_tid();
   const Win w = win_of(p, it);
   const int n = w.wrows * w.wpr;
   const uint32_t *tail = L.raw + w.wrows * w.nd;
   if (tid < 64) L.cur[tid] = tail[tid];
-  else if (tid < 64 + 4 * kNS) reinterpret_cast<uint32_t *>(L.slot)[tid - 64] = tail[tid];
   if (w.inner) {
-    for (int i = tid; i < n; i += kWG) {
-      const int r = i / w.wpr, c = i - r * w.wpr + w.sh;
-      const uint32_t *rw = L.raw + r * w.nd;
-      L.words[r * L.wp + (c - w.sh)] = __builtin_amdgcn_alignbyte(rw[(c >> 2) + 1], rw[c >> 2], c & 3);
+    // a thread makes 4 consecutive words of a row from 3 fetched dwords
+    const int ng = (w.wpr + 3) >> 2;          // word groups per row
+    const int rstep = kWG / ng;               // rows per pass
+    const int r0 = tid / ng, g = tid - r0 * ng;
+    if (r0 < rstep) {
+      for (int r = r0; r < w.wrows; r += rstep) {
+        const uint32_t *rw = L.raw + r * w.nd + g;
+        const uint32_t d0 = rw[0], d1 = rw[1], d2 = rw[2];
+        uint32_t *dst = L.words + r * L.wp + 4 * g;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int o = k + w.sh;   // byte offset of word 4g+k from dword g (0..6)
+          if (4 * g + k < w.wpr)
+            dst[k] = o < 4 ? __builtin_amdgcn_alignbyte(d1, d0, o) : __builtin_amdgcn_alignbyte(d2, d1, o - 4);
+        }
+      }
     }
   } else {
     // window crosses (or lies beyond) the left/right picture edge: pel x of
@@ -465,9 +484,9 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
 #endif
 ) {
   using Best = typename std::conditional<KEY32, uint32_t, unsigned long long>::type;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
+  int tid = opaque_tid();
+  int lane = tid & 63;
+  int wave = tid >> 6;
   const uint32_t *curw = L.cur;
 
   GroupCtx g;
@@ -480,9 +499,8 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
   g.max_mvd = p.max_mvd;
   g.preseed = FFS && (it.flags & kItemPreseed);
   g.gmask = it.gmask;
-  g.rlim = it.rlim;
+  g.rs = it.rs;
   g.chk00 = !FFS && (it.flags & kItemChk00);
-  g.slot = L.slot;
   const int R = g.R;
   const unsigned long long gmask = g.gmask;
   const int u = it.u;
@@ -576,7 +594,7 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
         c.rank = FFS ? ((g.preseed && c.is00) ? 0u : (uint32_t)sidx + 1u) : (uint32_t)sidx;
         const MvCost mc = mv_cost<FFS>(candx, candy, g.px, g.py, g.lam, g.max_mvd);
         c.mvc = mc.mvc;
-        c.ok = mc.ok;
+        c.ok = pos_eligible<FFS>(g, mc.ok, c.lring, c.is00);
         c.mvc0 = g.chk00 ? check00_adjust(mc.mvc, g.lam, c.is00) : mc.mvc;
         update_slots<KEY32, FFS, decltype(all_tag)::value>(ps, g, c, best);
       };
@@ -600,16 +618,39 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
   STAMP(st.sweep);
 
   // ---- workgroup reduction of this group's per-thread minima
+  tid = opaque_tid();
+  lane = tid & 63;
+  wave = tid >> 6;
+  if (KEY32) {
+    // reduce-scatter through the wave: permlane32_swap pairs slots (lanes
+    // 0-31 keep one, 32-63 the other), permlane16_swap pairs again (one slot
+    // per row of 16), four DPP steps finish each row -- 11 registers carry
+    // the 41 slots (padded to 44) instead of 41 full-wave reductions.
+    uint32_t k1[kRed1];
 #pragma unroll
-  for (int s = 0; s < kNS; ++s) {
-    if (!((gmask >> s) & 1)) continue;
-#ifndef JMME_NO_DPP
-    if (KEY32) {
-      const uint32_t k = wave_min_u32((uint32_t)best[s]);
-      if (lane == 63) L.red[wave * kNS + s] = k;
-    } else
-#endif
-    {
+    for (int m = 0; m < kRed1; ++m) {
+      const uint32_t a = 2 * m < kNS ? (uint32_t)best[2 * m] : ~0u;
+      const uint32_t b = 2 * m + 1 < kNS ? (uint32_t)best[2 * m + 1] : ~0u;
+      const auto sw = __builtin_amdgcn_permlane32_swap(a, b, false, false);
+      k1[m] = min((uint32_t)sw[0], (uint32_t)sw[1]);
+    }
+    const int row = lane >> 4;
+#pragma unroll
+    for (int q = 0; q < kRed2; ++q) {
+      const auto sw = __builtin_amdgcn_permlane16_swap(k1[2 * q], k1[2 * q + 1], false, false);
+      uint32_t v = min((uint32_t)sw[0], (uint32_t)sw[1]);
+      v = dpp_min<0xB1>(v);    // quad_perm [1,0,3,2]
+      v = dpp_min<0x4E>(v);    // quad_perm [2,3,0,1]
+      v = dpp_min<0x141>(v);   // row_half_mirror
+      v = dpp_min<0x140>(v);   // row_mirror: every lane of the row holds its minimum
+      // row 0: slot 4q, row 1: 4q+2, row 2: 4q+1, row 3: 4q+3
+      const int s = 4 * q + (((row & 1) << 1) | (row >> 1));
+      if ((lane & 15) == 0 && s < kNS) L.red[wave * kNS + s] = v;
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < kNS; ++s) {
+      if (!((gmask >> s) & 1)) continue;
       unsigned long long k = best[s];
 #pragma unroll
       for (int off = 32; off >= 1; off >>= 1) {
@@ -621,6 +662,8 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
       if (lane == 0) L.red[wave * kNS + s] = k;
     }
   }
+  if (KEY32)
+    for (int i = tid; i < kNS * kCand; i += kWG) L.match[i] = 0;   // refine SAD accumulators
   __syncthreads();
   if (tid < kNS) {
     unsigned long long k = L.red[tid];
@@ -634,38 +677,57 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
   // ---- refine (32-bit keys): recover the 3 rank bits the key dropped.
   // The winner has cost == key>>10 and rank in [8c, 8c+8), c = key & 1023;
   // re-evaluate those positions exactly and take the smallest matching rank.
+  tid = opaque_tid();
   if (KEY32) {
     const int D = 2 * R + 1;
+    // candidate j of slot s: its window offset, or false if it does not exist
+    auto candidate = [&](int s, int j, int &ox, int &oy, int &rk) -> bool {
+      const uint32_t key = (uint32_t)L.red[s];
+      if (!((gmask >> s) & 1) || key == ~0u) return false;
+      rk = (int)(((key & ((1u << kCostShift) - 1)) << kRankDrop) + j);
+      if (FFS && rk == 0) {          // the pre-seeded (0,0) vector
+        ox = -(g.cqx >> 2); oy = -(g.cqy >> 2);
+        return g.preseed && abs(ox) <= R && abs(oy) <= R;
+      }
+      const int sidx = FFS ? rk - 1 : rk;
+      if (sidx >= D * D) return false;
+      spiral_offset_fast(sidx, &ox, &oy);
+      return true;
+    };
+    // (a) the partition SADs at the candidates, one 4x4 block per work item
+    //     (896 items: a 16x16 candidate is 16 of them), summed in LDS
+    for (int e = tid; e < kBlkItems * kCand; e += kWG) {
+      const int j = e & (kCand - 1);
+      const int sb = kBlkTab.v[e >> kRankDrop];
+      const int s = sb >> 4, bx = sb & 3, by = (sb >> 2) & 3;
+      int ox, oy, rk;
+      if (candidate(s, j, ox, oy, rk)) {
+        const uint32_t *w = L.words + (oy + R + 4 * by) * L.wp + ox + R + 4 * bx;
+        uint32_t sad = 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sad = __builtin_amdgcn_sad_u8(w[r * L.wp], curw[(4 * by + r) * 4 + bx], sad);
+        atomicAdd(&L.match[s * kCand + j], sad);
+      }
+    }
+    __syncthreads();
+    // (b) exact cost and eligibility of each candidate
     for (int item = tid; item < kNS * kCand; item += kWG) {
       const int s = item / kCand, j = item - s * kCand;
       uint32_t m = 0;
-      const uint32_t key = (uint32_t)L.red[s];
-      if (((gmask >> s) & 1) && key != ~0u) {
-        const uint32_t mincost = key >> kCostShift;
-        const int rk = (int)(((key & ((1u << kCostShift) - 1)) << kRankDrop) + j);
-        int ox = 0, oy = 0;
-        bool valid;
-        if (FFS && rk == 0) {          // the pre-seeded (0,0) vector
-          ox = -(g.cqx >> 2); oy = -(g.cqy >> 2);
-          valid = g.preseed && abs(ox) <= R && abs(oy) <= R;
-        } else {
-          const int sidx = FFS ? rk - 1 : rk;
-          valid = sidx < D * D;
-          if (valid) spiral_offset_fast(sidx, &ox, &oy);
-        }
-        if (valid) {
-          const int candx = g.cqx + 4 * ox, candy = g.cqy + 4 * oy;
-          PosCtx c;
-          c.is00 = (candx == 0) && (candy == 0);
-          c.lring = max(abs(ox), abs(oy));
-          const int sidx = spiral_index_bl(ox, oy);
-          c.rank = FFS ? ((g.preseed && c.is00) ? 0u : (uint32_t)sidx + 1u) : (uint32_t)sidx;
-          const MvCost mc = mv_cost<FFS>(candx, candy, g.px, g.py, g.lam, g.max_mvd);
-          c.ok = mc.ok;
-          const uint32_t mv = (s == 0 && g.chk00) ? check00_adjust(mc.mvc, g.lam, c.is00) : mc.mvc;
-          const uint32_t cost = (partition_sad_at(L, curw, s, ox + R, oy + R) << 5) + mv;
-          m = (c.rank == (uint32_t)rk) && cost == mincost && slot_eligible<FFS>(g, c, s);
-        }
+      int ox, oy, rk;
+      if (candidate(s, j, ox, oy, rk)) {
+        const uint32_t mincost = (uint32_t)L.red[s] >> kCostShift;
+        const int candx = g.cqx + 4 * ox, candy = g.cqy + 4 * oy;
+        PosCtx c;
+        c.is00 = (candx == 0) && (candy == 0);
+        c.lring = max(abs(ox), abs(oy));
+        const int sidx = spiral_index_bl(ox, oy);
+        c.rank = FFS ? ((g.preseed && c.is00) ? 0u : (uint32_t)sidx + 1u) : (uint32_t)sidx;
+        const MvCost mc = mv_cost<FFS>(candx, candy, g.px, g.py, g.lam, g.max_mvd);
+        c.ok = pos_eligible<FFS>(g, mc.ok, c.lring, c.is00);
+        const uint32_t mv = (s == 0 && g.chk00) ? check00_adjust(mc.mvc, g.lam, c.is00) : mc.mvc;
+        const uint32_t cost = (L.match[item] << 5) + mv;
+        m = (c.rank == (uint32_t)rk) && cost == mincost && c.ok;
       }
       L.match[item] = m;
     }
@@ -674,6 +736,7 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
   STAMP(st.refine);
 
   // ---- results of this group
+  tid = opaque_tid();
   if (tid < kNS && ((gmask >> tid) & 1)) {
     const unsigned long long k = L.red[tid];
     jmme_block_res res;
@@ -729,7 +792,6 @@ template <bool KEY32, bool FFS>
 __global__ __launch_bounds__(kWG, KEY32 ? JMME_WAVES_PER_EU : 2) void me_items_kernel(KParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ __attribute__((aligned(16))) uint32_t s_cur[64];
-  __shared__ int4 s_slot[kNS];
   const unsigned cnt = p.counts[KEY32 ? 0 : 1];
   const Item *items = KEY32 ? p.items : p.items + (p.item_cap - cnt);
   const int x = blockIdx.x & 7, lb = blockIdx.x >> 3, nbx = (gridDim.x - x + 7) >> 3;
@@ -738,12 +800,8 @@ __global__ __launch_bounds__(kWG, KEY32 ? JMME_WAVES_PER_EU : 2) void me_items_k
   unsigned j = start + lb;
   if (j >= end) return;
 
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = ufl(tid >> 6);
   Lds L = carve(smem, p.lds_range);
   L.cur = s_cur;
-  L.slot = s_slot;
   const unsigned long long dbg_slot =
       p.debug_words ? (1ull << __builtin_ctzll((ufl64(p.req[0].slot_mask) & kAll) | (1ull << 63))) : 0ull;
 #ifdef JMME_STAMPS
@@ -751,7 +809,7 @@ __global__ __launch_bounds__(kWG, KEY32 ? JMME_WAVES_PER_EU : 2) void me_items_k
 #endif
 
   Item it = load_item(items, j);
-  prefetch(p, it, L, wave, lane);
+  prefetch(p, it, L);
   for (;;) {
 #ifdef JMME_STAMPS
     ItemStamps<KEY32, FFS> st;
@@ -765,15 +823,15 @@ __global__ __launch_bounds__(kWG, KEY32 ? JMME_WAVES_PER_EU : 2) void me_items_k
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     STAMP(st.wait);
-    if (it.gmask) expand(p, it, L, tid);
+    if (it.gmask) expand(p, it, L);
     __syncthreads();
     if (p.debug_words && it.u == 0 && (it.gmask & dbg_slot)) {
       const Win w = win_of(p, it);
-      for (int i = tid; i < w.wrows * L.wp; i += kWG) p.debug_words[i] = L.words[i];
+      for (int i = opaque_tid(); i < w.wrows * L.wp; i += kWG) p.debug_words[i] = L.words[i];
     }
     STAMP(st.expand);
     // the raw buffer is free: start fetching the next item behind this sweep
-    if (more) prefetch(p, nx, L, wave, lane);
+    if (more) prefetch(p, nx, L);
     if (it.gmask) {
 #ifdef JMME_STAMPS
       search_item<KEY32, FFS>(p, it, L, t_last, st);
@@ -782,7 +840,7 @@ __global__ __launch_bounds__(kWG, KEY32 ? JMME_WAVES_PER_EU : 2) void me_items_k
 #endif
     }
 #ifdef JMME_STAMPS
-    if (p.stamps && tid == 0) {
+    if (p.stamps && threadIdx.x == 0) {
       unsigned long long *o = p.stamps + (size_t)it.u * 8;
       atomicAdd(o + 0, st.wait); atomicAdd(o + 1, st.expand); atomicAdd(o + 2, st.sweep);
       atomicAdd(o + 3, st.reduce); atomicAdd(o + 4, st.refine); atomicAdd(o + 5, st.out);
