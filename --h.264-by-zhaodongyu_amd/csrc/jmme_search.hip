@@ -521,6 +521,9 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
     const int qstep = kWG / D, rstep = kWG - (kWG / D) * D;
     int tx = tid % D, ty = tid / D;       // task column, pair row
     for (int t = tid; t < ntask; t += kWG) {
+      // the pair (yb, yb+1); D odd: the last pair is shifted up one row and
+      // re-evaluates position D-2 (same key twice: harmless for a minimum)
+      const int yb = D > 1 ? min(2 * ty, D - 2) : 0;
       uint32_t a0[16], a1[16];
 #pragma unroll
       for (int k = 0; k < 16; ++k) { a0[k] = 0; a1[k] = 0; }
@@ -529,7 +532,7 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
         // loop instead of letting LICM pin 64 VGPRs for them
         uint32_t zero;
         asm volatile("v_mov_b32 %0, 0" : "=v"(zero));
-        const uint32_t wrow = lds_addr(L.words) + 4u * (uint32_t)((2 * ty) * L.wp + tx);
+        const uint32_t wrow = lds_addr(L.words) + 4u * (uint32_t)(yb * L.wp + tx);
         const uint32_t rowb = 4u * (uint32_t)L.wp;
         const uint32_t cb = lds_addr(curw) + zero;
         // software pipeline, one row ahead: row r+1's reference words and MB
@@ -582,10 +585,8 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
       }
       const int ox = tx - R;
       const int candx = g.cqx + 4 * ox;     // candidate MV (qpel, relative to the block)
-      auto eval_position = [&](const uint32_t (&acc)[16], int oyw) {
+      auto pos_ctx = [&](int oyw) {
         const int oy = oyw - R;
-        uint32_t ps[kNS];
-        partition_sads(acc, ps);
         PosCtx c;
         c.lring = max(abs(ox), abs(oy));
         const int sidx = spiral_index_bl(ox, oy);
@@ -596,15 +597,28 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
         c.mvc = mc.mvc;
         c.ok = pos_eligible<FFS>(g, mc.ok, c.lring, c.is00);
         c.mvc0 = g.chk00 ? check00_adjust(mc.mvc, g.lam, c.is00) : mc.mvc;
-        update_slots<KEY32, FFS, decltype(all_tag)::value>(ps, g, c, best);
+        return c;
       };
+      auto eval_position = [&](const uint32_t (&acc)[16], int oyw) {
+        uint32_t ps[kNS];
+        partition_sads(acc, ps);
+        update_slots<KEY32, FFS, decltype(all_tag)::value>(ps, g, pos_ctx(oyw), best);
+      };
+
 #ifdef JMME_ABL_NOCOST   // timing ablation only: keep the SADs live, skip the cost/minimum work
 #pragma unroll
       for (int k = 0; k < 16; ++k) asm volatile("" :: "v"(a0[k]), "v"(a1[k]));
       (void)eval_position;
 #else
-      eval_position(a0, 2 * ty);
-      if (2 * ty + 1 < D) eval_position(a1, 2 * ty + 1);   // odd D: last pair has one position
+      // range 0 (D == 1): one position -- the second is made a copy of it
+      if (D == 1) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) a1[k] = a0[k];
+      }
+      // both positions unconditionally (one basic block): the two minima per
+      // partition fold into one v_min3_u32
+      eval_position(a0, yb);
+      eval_position(a1, min(yb + 1, D - 1));
 #endif
       tx += rstep;
       ty += qstep;
