@@ -495,6 +495,50 @@ extern "C" jmme_distblk jmme_full_search_block(jmme_ctx *ctx, int list, int ref_
   return out[s].cost;
 }
 
+extern "C" jmme_distblk jmme_fast_full_search_block(jmme_ctx *ctx, int list, int ref_idx, int pos_x, int pos_y,
+                                                    int blocktype, const jmme_mv *pred_mv,
+                                                    const jmme_mv *search_center, int surface_range,
+                                                    int block_range, int rdopt, jmme_mv *mv_out,
+                                                    jmme_distblk min_mcost, int lambda_factor) {
+  // fast_full_search_motion_estimation's contract for one partition, as a
+  // one-slot FFS unit (the surface of setup_fast_full_search is the unit's
+  // window).  JM's error() semantics on failure (print, exit 500).
+  int mb_x = pos_x & ~15, mb_y = pos_y & ~15;
+  int s = slot_of(blocktype, (pos_x - mb_x) >> 2, (pos_y - mb_y) >> 2);
+  if (s < 0 || !pred_mv || !search_center || !mv_out) {
+    fprintf(stderr, "jmme_fast_full_search_block: bad block or null argument\n");
+    exit(500);
+  }
+  jmme_mb_req r;
+  memset(&r, 0, sizeof r);
+  r.mb_x = (int16_t)mb_x;
+  r.mb_y = (int16_t)mb_y;
+  r.list = (int16_t)list;
+  r.ref_idx = (int16_t)ref_idx;
+  r.slot_mask = 1ull << s;
+  r.ffs_center_x = search_center->mv_x;
+  r.ffs_center_y = search_center->mv_y;
+  r.ffs_range = (int16_t)surface_range;
+  r.ffs_pos00_valid = (int16_t)(rdopt == 0);
+  r.blk[s].pred_x = pred_mv->mv_x;
+  r.blk[s].pred_y = pred_mv->mv_y;
+  r.blk[s].search_range = (int16_t)block_range;
+  r.blk[s].lambda = lambda_factor;
+  jmme_block_res out[JMME_NSLOT];
+  if (jmme_search_mbs(ctx, JMME_FAST_FULL_SEARCH, &r, 1, out)) {
+    fprintf(stderr, "jmme_fast_full_search_block: %s\n", jmme_last_error());
+    exit(500);
+  }
+  // nothing beat the incoming bound: JM keeps best_pos = 0, i.e. the centre
+  if (out[s].cost >= min_mcost) {
+    *mv_out = *search_center;
+    return min_mcost;
+  }
+  mv_out->mv_x = out[s].mv_x;
+  mv_out->mv_y = out[s].mv_y;
+  return out[s].cost;
+}
+
 extern "C" int jmme_debug_window(jmme_ctx *ctx, int mode, const jmme_mb_req *req, uint32_t *out, int max_words) {
   // Test hook: run unit `req` (one unit) and return the first reference
   // window it staged in LDS (rows x pitch words, word[y][x] = pels x..x+3).

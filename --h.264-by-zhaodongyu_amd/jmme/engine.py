@@ -125,3 +125,15 @@ class MotionEstimator:
                                             int(blocktype), ctypes.byref(p), ctypes.byref(mv), int(min_mcost),
                                             int(lambda_factor), int(search_range), int(check_for_00))
         return (mv.mv_x, mv.mv_y), int(cost)
+
+    def fast_full_search_block(self, list_idx, ref_idx, pos_x, pos_y, blocktype, pred, search_center,
+                               surface_range, block_range, rdopt, lambda_factor, min_mcost=_lib.DISTBLK_MAX):
+        """fast_full_search_motion_estimation's contract for one partition (JM me_fullfast.c:618-689)."""
+        p = JmmeMv(int(pred[0]), int(pred[1]))
+        c = JmmeMv(int(search_center[0]), int(search_center[1]))
+        mv = JmmeMv(0, 0)
+        cost = lib().jmme_fast_full_search_block(self._ctx, int(list_idx), int(ref_idx), int(pos_x), int(pos_y),
+                                                 int(blocktype), ctypes.byref(p), ctypes.byref(c),
+                                                 int(surface_range), int(block_range), int(rdopt),
+                                                 ctypes.byref(mv), int(min_mcost), int(lambda_factor))
+        return (mv.mv_x, mv.mv_y), int(cost)

@@ -42,8 +42,10 @@ CASE = "c2_syn_1080p_fs32"
 ALG_BYTES_PER_UNIT = 1516          # per MB x ref
 ABSDIFF_PER_UNIT = 65 * 65 * 256   # (2R+1)^2 * 256 at R=32, SURVEY.md §8(d)
 HBM_PEAK_GBS = 8000.0              # MI355X_MICROARCH.md (spec)
-CU, SIMD, LANES, CLK = 256, 4, 32, 2.4e9
-VSAD_PEAK = CU * SIMD * LANES * 4 * CLK   # abs-diffs/s if every VALU lane-op were a v_sad_u8
+# VALU ceiling for the SAD: v_sad_u8 lane-ops/s measured on MI355X by
+# tools/ubench_valu.hip (profiles/round1/ubench_valu.jsonl), 4 abs-diffs each
+VSAD_LANE_OPS = 35.5e12
+VSAD_PEAK = VSAD_LANE_OPS * 4
 
 JM_CFG = """# minimal JM 18.5 lencod configuration written by bench.py (unlisted keys: JM defaults)
 ProfileIDC            = 66
@@ -146,6 +148,24 @@ def pmc_traffic():
     return None
 
 
+def reduce_over_ranks(wall: float, exact: int, ws: int, dev) -> tuple[float, int]:
+    """Job time = the slowest rank's time; parity = the worst rank's count.
+    The only collectives of the run (no data-path exchange: ranks own whole GOPs)."""
+    if ws == 1:
+        return wall, exact
+    import torch.distributed as dist
+    t = torch.tensor([wall], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    e = torch.tensor([exact], dtype=torch.int64, device=dev)
+    dist.all_reduce(e, op=dist.ReduceOp.MIN)
+    return float(t.item()), int(e.item())
+
+
+def job_value(units_per_rank_step: int, steps: int, ws: int, wall: float) -> float:
+    """Whole-job throughput: every rank's units over the max-over-ranks time."""
+    return units_per_rank_step * steps * ws / wall
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -204,17 +224,10 @@ def main():
         torch.distributed.barrier()
     wall = time.perf_counter() - t0
     ev_ms = ev0.elapsed_time(ev1)
-    t = torch.tensor([wall], dtype=torch.float64, device=dev)
-    if ws > 1:
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        tot = torch.tensor([exact], dtype=torch.int64, device=dev)
-        torch.distributed.all_reduce(tot, op=torch.distributed.ReduceOp.MIN)
-        exact = int(tot.item())   # worst rank
-    wall = float(t.item())
+    wall, exact = reduce_over_ranks(wall, exact, ws, dev)
 
     if rank == 0:
-        units_total = n * args.steps * ws
-        value = units_total / wall
+        value = job_value(n, args.steps, ws, wall)
         ms_per_step = wall * 1e3 / args.steps
         ach = ALG_BYTES_PER_UNIT * n / (kernel_ms * 1e-3) / 1e9
         cpu = None
@@ -245,6 +258,7 @@ def main():
                          "note": "integer SAD search is VALU-bound, see valu"},
             "valu": {"achieved_absdiff_per_s": round(ABSDIFF_PER_UNIT * n / (kernel_ms * 1e-3), 1),
                      "peak_absdiff_per_s": VSAD_PEAK,
+                     "peak_source": "measured v_sad_u8 rate (tools/ubench_valu.hip) x 4 abs-diffs",
                      "frac": round(ABSDIFF_PER_UNIT * n / (kernel_ms * 1e-3) / VSAD_PEAK, 4)},
             "event_ms_per_step": round(ev_ms / args.steps, 4),
             "cpu_baseline": cpu,

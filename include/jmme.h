@@ -9,7 +9,7 @@
  *                                    body JM/lencod/src/me_fullsearch.c:39-103,
  *                                    assigned JM/lencod/src/mv_search.c:139-175
  *   jmme_fast_full_search_block() <- currMB->IntPelME = fast_full_search_motion_estimation
- *                                    (JM/lencod/src/me_fullfast.c:618-689) together with
+ *                                    (global.h:459, JM/lencod/src/me_fullfast.c:618-689) with
  *                                    currMB->p_SetupFastFullPelSearch = setup_fast_full_search
  *                                    (global.h:469, me_fullfast.c:269-608)
  *   jmme_search_mbs()             <- the same two searches batched per macroblock x
@@ -166,6 +166,19 @@ jmme_distblk jmme_full_search_block(jmme_ctx *ctx, int list, int ref_idx,
                                     const jmme_mv *pred_mv, jmme_mv *mv_inout,
                                     jmme_distblk min_mcost, int lambda_factor,
                                     int search_range, int check_for_00);
+
+/* fast_full_search_motion_estimation (me_fullfast.c:618-689) with the state
+ * setup_fast_full_search leaves in p_Vid->p_ffast_me (me_fullfast.c:269-608):
+ * search_center = p_ffast_me->search_center[list][ref] (qpel, integer grid),
+ * surface_range = the SAD surface's range (p_ffast_me->max_search_range),
+ * block_range   = imax(searchRange.max_x, max_y) >> 2 for this partition,
+ * rdopt         = p_Inp->rdopt (0: the (0,0) vector is pre-seeded, :650-657).
+ * mv_out = mv_block->mv[list]; returns the minimum motion cost. */
+jmme_distblk jmme_fast_full_search_block(jmme_ctx *ctx, int list, int ref_idx,
+                                         int pos_x, int pos_y, int blocktype,
+                                         const jmme_mv *pred_mv, const jmme_mv *search_center,
+                                         int surface_range, int block_range, int rdopt,
+                                         jmme_mv *mv_out, jmme_distblk min_mcost, int lambda_factor);
 
 /* ---- timing of the last jmme_search_mbs* launch (HIP events on its stream) */
 float jmme_last_kernel_ms(jmme_ctx *ctx);

@@ -120,6 +120,25 @@ def test_intpelme_signature_dropin(gpu):
             assert mv == (r["out_mv_x"][j], r["out_mv_y"][j]) and cost == r["out_cost"][j]
 
 
+def test_ffs_intpelme_signature_dropin(gpu):
+    """jmme_fast_full_search_block = fast_full_search_motion_estimation's contract
+    (with setup_fast_full_search's centre / surface range), on JM's own records."""
+    for name in ("ffs_foreman_qcif_r16", "ffs_foreman_qcif_r16_rdo0"):
+        c = g.Case(name)
+        r = c.r
+        with _engine(c, gpu) as me:
+            f, lst, rf, idx = next(iter(c.groups()))
+            me.upload_cur(c.cur[f])
+            me.upload_ref(lst, rf, c.ref[(f, lst, rf)])
+            rng = np.random.default_rng(1)
+            for j in rng.choice(idx, 40, replace=False):
+                mv, cost = me.fast_full_search_block(
+                    lst, rf, r["pos_x"][j], r["pos_y"][j], r["blocktype"][j], (r["pred_x"][j], r["pred_y"][j]),
+                    (r["ffs_center_x"][j], r["ffs_center_y"][j]), r["ffs_max_range"][j],
+                    c.ffs_block_range(np.array([j]))[0], r["rdopt"][j], r["lambda"][j])
+                assert mv == (r["out_mv_x"][j], r["out_mv_y"][j]) and cost == r["out_cost"][j], (name, j)
+
+
 def _random_units(rng, w, h, n, R, lam_max=400, mode=-1):
     from jmme import MB_REQ, BLK_CHECK00
     req = np.zeros(n, dtype=MB_REQ)

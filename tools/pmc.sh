@@ -1,9 +1,10 @@
 #!/bin/bash
-# PMC counter passes over a short bench run (one rocprofv3 pass per group).
+# PMC counter passes over a short bench run (one rocprofv3 pass per group;
+# --pmc never combined with sys/runtime traces).  Stops at the first failure.
 # Usage (GPU box, repo root): [JMME_LIB=...] tools/pmc.sh OUTDIR [groups...]
 set -e
 OUT=${1:-gpurun_out/pmc}; shift || true
-GROUPS_=${@:-sq1 sq2 sq3 tcc1 tcc2}
+GROUPS_=${@:-tcc1 tcc2 sq1 sq2}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 declare -A G
@@ -14,6 +15,6 @@ G[tcc1]="FETCH_SIZE"
 G[tcc2]="WRITE_SIZE"
 for g in $GROUPS_; do
   timeout -k 10 240 rocprofv3 --kernel-trace --pmc ${G[$g]} --output-format csv -d "$OUT/$g" -o p -- \
-    python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > "$OUT/$g.log" 2>&1 || echo "group $g failed"
+    python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > "$OUT/$g.log" 2>&1
 done
 echo pmc done
