@@ -15,6 +15,7 @@
 #include "jmme.h"
 #include "jmme_common.h"
 #include "jmme_internal.h"
+#include "jmme_tq_internal.h"
 
 using namespace jmme;
 
@@ -493,6 +494,120 @@ extern "C" jmme_distblk jmme_full_search_block(jmme_ctx *ctx, int list, int ref_
   mv_inout->mv_x = out[s].mv_x;
   mv_inout->mv_y = out[s].mv_y;
   return out[s].cost;
+}
+
+// ------------------------------------------------- transforms / quant / SATD --
+namespace {
+
+// host-array convenience: stage through device buffers owned by this call
+struct DevBuf {
+  void *p = nullptr;
+  ~DevBuf() { (void)hipFree(p); }
+  hipError_t alloc(size_t bytes) { return hipMalloc(&p, bytes ? bytes : 4); }
+};
+
+}  // namespace
+
+extern "C" int jmme_transform_async(jmme_ctx *ctx, int op, const int32_t *d_in, int32_t *d_out, int n, void *stream) {
+  if (!ctx) return fail("null ctx");
+  if (n < 0) return fail("negative block count");
+  if (!transform_elems(op)) return fail("unknown transform op %d", op);
+  if (n == 0) return 0;
+  if (!d_in || !d_out) return fail("null block array");
+  HIPCHK(launch_transform(op, d_in, d_out, n, reinterpret_cast<hipStream_t>(stream)));
+  return 0;
+}
+
+extern "C" int jmme_transform(jmme_ctx *ctx, int op, const int32_t *in, int32_t *out, int n) {
+  if (!ctx) return fail("null ctx");
+  const int e = transform_elems(op);
+  if (!e) return fail("unknown transform op %d", op);
+  if (n <= 0) return n < 0 ? fail("negative block count") : 0;
+  if (!in || !out) return fail("null block array");
+  const size_t bytes = (size_t)n * e * 4;
+  DevBuf a, b;
+  HIPCHK(a.alloc(bytes));
+  HIPCHK(b.alloc(bytes));
+  HIPCHK(hipMemcpy(a.p, in, bytes, hipMemcpyHostToDevice));
+  HIPCHK(launch_transform(op, (const int32_t *)a.p, (int32_t *)b.p, n, nullptr));
+  HIPCHK(hipMemcpy(out, b.p, bytes, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+extern "C" int jmme_satd_async(jmme_ctx *ctx, int size, const int16_t *d_diff, int32_t *d_out, int n, void *stream) {
+  if (!ctx) return fail("null ctx");
+  if (size != 4 && size != 8) return fail("SATD block size %d (4 or 8)", size);
+  if (n < 0) return fail("negative block count");
+  if (n == 0) return 0;
+  if (!d_diff || !d_out) return fail("null array");
+  HIPCHK(launch_satd(size, d_diff, d_out, n, reinterpret_cast<hipStream_t>(stream)));
+  return 0;
+}
+
+extern "C" int jmme_satd(jmme_ctx *ctx, int size, const int16_t *diff, int32_t *out, int n) {
+  if (!ctx) return fail("null ctx");
+  if (size != 4 && size != 8) return fail("SATD block size %d (4 or 8)", size);
+  if (n <= 0) return n < 0 ? fail("negative block count") : 0;
+  if (!diff || !out) return fail("null array");
+  const size_t in_b = (size_t)n * size * size * 2, out_b = (size_t)n * 4;
+  DevBuf a, b;
+  HIPCHK(a.alloc(in_b));
+  HIPCHK(b.alloc(out_b));
+  HIPCHK(hipMemcpy(a.p, diff, in_b, hipMemcpyHostToDevice));
+  HIPCHK(launch_satd(size, (const int16_t *)a.p, (int32_t *)b.p, n, nullptr));
+  HIPCHK(hipMemcpy(out, b.p, out_b, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+extern "C" int jmme_quant4x4_async(jmme_ctx *ctx, const jmme_quant4x4_params *d_params, const int32_t *d_param_idx,
+                                   int32_t *d_coef, int32_t *d_levels, int32_t *d_runs, int32_t *d_coeff_cost,
+                                   int32_t *d_nonzero, int n, void *stream) {
+  if (!ctx) return fail("null ctx");
+  if (n < 0) return fail("negative block count");
+  if (n == 0) return 0;
+  if (!d_params || !d_coef || !d_levels || !d_runs || !d_coeff_cost || !d_nonzero) return fail("null array");
+  HIPCHK(launch_quant4x4(d_params, d_param_idx, d_coef, d_levels, d_runs, d_coeff_cost, d_nonzero, n,
+                         reinterpret_cast<hipStream_t>(stream)));
+  return 0;
+}
+
+extern "C" int jmme_quant4x4(jmme_ctx *ctx, const jmme_quant4x4_params *params, int n_params, const int32_t *param_idx,
+                             int32_t *coef, int32_t *levels, int32_t *runs, int32_t *coeff_cost, int32_t *nonzero,
+                             int n) {
+  if (!ctx) return fail("null ctx");
+  if (n <= 0) return n < 0 ? fail("negative block count") : 0;
+  if (!params || n_params <= 0 || !coef || !levels || !runs || !coeff_cost || !nonzero) return fail("null array");
+  for (int p = 0; p < n_params; ++p) {
+    const jmme_quant4x4_params &q = params[p];
+    if (q.qp_per < 0 || q.qp_per > 16) return fail("quant set %d: qp_per %d out of range", p, q.qp_per);
+    for (int k = 0; k < 16; ++k)
+      if (q.scan[k][0] > 3 || q.scan[k][1] > 3) return fail("quant set %d: scan entry %d outside 4x4", p, k);
+  }
+  if (param_idx)
+    for (int b = 0; b < n; ++b)
+      if (param_idx[b] < 0 || param_idx[b] >= n_params) return fail("block %d: parameter set %d of %d", b, param_idx[b], n_params);
+  DevBuf dp, di, dc, dl, dr, dk, dn;
+  HIPCHK(dp.alloc(sizeof(jmme_quant4x4_params) * n_params));
+  HIPCHK(dc.alloc((size_t)n * 64));
+  HIPCHK(dl.alloc((size_t)n * 68));
+  HIPCHK(dr.alloc((size_t)n * 64));
+  HIPCHK(dk.alloc((size_t)n * 4));
+  HIPCHK(dn.alloc((size_t)n * 4));
+  HIPCHK(hipMemcpy(dp.p, params, sizeof(jmme_quant4x4_params) * n_params, hipMemcpyHostToDevice));
+  if (param_idx) {
+    HIPCHK(di.alloc((size_t)n * 4));
+    HIPCHK(hipMemcpy(di.p, param_idx, (size_t)n * 4, hipMemcpyHostToDevice));
+  }
+  HIPCHK(hipMemcpy(dc.p, coef, (size_t)n * 64, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dk.p, coeff_cost, (size_t)n * 4, hipMemcpyHostToDevice));
+  HIPCHK(launch_quant4x4((const jmme_quant4x4_params *)dp.p, (const int32_t *)di.p, (int32_t *)dc.p, (int32_t *)dl.p,
+                         (int32_t *)dr.p, (int32_t *)dk.p, (int32_t *)dn.p, n, nullptr));
+  HIPCHK(hipMemcpy(coef, dc.p, (size_t)n * 64, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(levels, dl.p, (size_t)n * 68, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(runs, dr.p, (size_t)n * 64, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(coeff_cost, dk.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(nonzero, dn.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+  return 0;
 }
 
 extern "C" jmme_distblk jmme_fast_full_search_block(jmme_ctx *ctx, int list, int ref_idx, int pos_x, int pos_y,

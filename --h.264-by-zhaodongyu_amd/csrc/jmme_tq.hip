@@ -1,0 +1,358 @@
+// jmme_tq.hip -- gfx950 kernels for JM 18.5's block transforms, 4x4
+// quantisation and Hadamard SATD, batched over n
+// independent blocks.
+//
+//   forward4x4 / inverse4x4 / hadamard4x4 / ihadamard4x4 /
+//   hadamard4x2 / ihadamard4x2 / hadamard2x2 / ihadamard2x2 /
+//   forward8x8 / inverse8x8           JM/lcommon/src/transform.c:20-528
+//   HadamardSAD4x4 / HadamardSAD8x8   JM/lencod/src/me_distortion.c:175-341
+//   quant_4x4_normal                  JM/lencod/src/quant4x4_normal.c:39-110
+//
+// These are streaming kernels (tens of integer ops per 32-256 B block): the
+// bound is HBM.  A wave owns 64 consecutive blocks (one per lane): it streams
+// their bytes with lane-contiguous 16-B loads/stores (fully coalesced) and
+// transposes through a padded LDS slab so each lane gets its own block.
+// Butterflies are the same integer operations in the same order as JM (the
+// >> steps make the order significant), so results are bit-exact.
+#include <hip/hip_runtime.h>
+#include "jmme.h"
+#include "jmme_tq_internal.h"
+
+namespace jmme {
+
+namespace {
+
+constexpr int kTB = 64;   // one wave per workgroup: the LDS slab is per wave
+
+// ---- 1-D butterflies: x[k*s] -> y[k*t] ------------------------------------
+__device__ __forceinline__ void fwd4(const int *x, int s, int *y, int t) {       // transform.c:32-44
+  const int a = x[0] + x[3 * s], b = x[s] + x[2 * s], c = x[s] - x[2 * s], d = x[0] - x[3 * s];
+  y[0] = a + b; y[t] = 2 * d + c; y[2 * t] = a - b; y[3 * t] = d - 2 * c;
+}
+__device__ __forceinline__ void inv4(const int *x, int s, int *y, int t) {       // transform.c:82-94
+  const int e = x[0] + x[2 * s], f = x[0] - x[2 * s];
+  const int g = (x[s] >> 1) - x[3 * s], h = x[s] + (x[3 * s] >> 1);
+  y[0] = e + h; y[t] = f + g; y[2 * t] = f - g; y[3 * t] = e - h;
+}
+__device__ __forceinline__ void had4(const int *x, int s, int *y, int t) {       // transform.c:133-145
+  const int a = x[0] + x[3 * s], b = x[s] + x[2 * s], c = x[s] - x[2 * s], d = x[0] - x[3 * s];
+  y[0] = a + b; y[t] = d + c; y[2 * t] = a - b; y[3 * t] = d - c;
+}
+__device__ __forceinline__ void ihad4(const int *x, int s, int *y, int t) {      // transform.c:183-195
+  const int e = x[0] + x[2 * s], f = x[0] - x[2 * s], g = x[s] - x[3 * s], h = x[s] + x[3 * s];
+  y[0] = e + h; y[t] = f + g; y[2 * t] = f - g; y[3 * t] = e - h;
+}
+__device__ __forceinline__ void fwd8(const int *x, int s, int *y, int t) {       // transform.c:365-402
+  const int s07 = x[0] + x[7 * s], s16 = x[s] + x[6 * s], s25 = x[2 * s] + x[5 * s], s34 = x[3 * s] + x[4 * s];
+  const int d07 = x[0] - x[7 * s], d16 = x[s] - x[6 * s], d25 = x[2 * s] - x[5 * s], d34 = x[3 * s] - x[4 * s];
+  const int e0 = s07 + s34, e1 = s16 + s25, e2 = s07 - s34, e3 = s16 - s25;
+  const int o4 = d16 + d25 + ((d07 >> 1) + d07), o5 = d07 - d34 - ((d25 >> 1) + d25);
+  const int o6 = d07 + d34 - ((d16 >> 1) + d16), o7 = d16 - d25 + ((d34 >> 1) + d34);
+  y[0] = e0 + e1; y[t] = o4 + (o7 >> 2); y[2 * t] = e2 + (e3 >> 1); y[3 * t] = o5 + (o6 >> 2);
+  y[4 * t] = e0 - e1; y[5 * t] = o6 - (o5 >> 2); y[6 * t] = (e2 >> 1) - e3; y[7 * t] = (o4 >> 2) - o7;
+}
+__device__ __forceinline__ void inv8(const int *x, int s, int *y, int t) {       // transform.c:474-506
+  const int p0 = x[0], p1 = x[s], p2 = x[2 * s], p3 = x[3 * s], p4 = x[4 * s], p5 = x[5 * s], p6 = x[6 * s],
+            p7 = x[7 * s];
+  const int a0 = p0 + p4, a1 = p0 - p4, a2 = p6 - (p2 >> 1), a3 = p2 + (p6 >> 1);
+  const int b0 = a0 + a3, b2 = a1 - a2, b4 = a1 + a2, b6 = a0 - a3;
+  const int c0 = -p3 + p5 - p7 - (p7 >> 1), c1 = p1 + p7 - p3 - (p3 >> 1);
+  const int c2 = -p1 + p7 + p5 + (p5 >> 1), c3 = p3 + p5 + p1 + (p1 >> 1);
+  const int b1 = c0 + (c3 >> 2), b3 = c1 + (c2 >> 2), b5 = c2 - (c1 >> 2), b7 = c3 - (c0 >> 2);
+  y[0] = b0 + b7; y[t] = b2 - b5; y[2 * t] = b4 + b3; y[3 * t] = b6 + b1;
+  y[4 * t] = b6 - b1; y[5 * t] = b4 - b3; y[6 * t] = b2 + b5; y[7 * t] = b0 - b7;
+}
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+
+// LDS slab stride (dwords) for D-dword blocks: +4 (16-B rows) / +1 keeps the
+// per-lane block reads and writes conflict-free
+template <int D>
+__host__ __device__ constexpr int slab_stride() { return D + ((D % 4 == 0) ? 4 : 1); }
+
+// Wave-cooperative load of nb (<= 64) consecutive D-dword blocks at src: the
+// wave reads them as lane-contiguous chunks, parks them in the slab, and lane
+// l picks up block l.
+template <int D>
+__device__ __forceinline__ void wave_load(const int32_t *src, int nb, int32_t *slab, int lane, int *v) {
+  constexpr int S = slab_stride<D>();
+  if (D % 4 == 0) {
+    constexpr int C = D / 4;   // 16-B chunks per block
+#pragma unroll
+    for (int k = 0; k < C; ++k) {
+      const int ch = k * 64 + lane, blk = ch / C, part = ch - blk * C;
+      if (blk < nb) {
+        const v4i q = __builtin_nontemporal_load(reinterpret_cast<const v4i *>(src) + ch);
+        *reinterpret_cast<v4i *>(slab + blk * S + 4 * part) = q;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      const int dw = k * 64 + lane, blk = dw / D;
+      if (blk < nb) slab[blk * S + dw - blk * D] = __builtin_nontemporal_load(src + dw);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < D; ++k) v[k] = slab[lane * S + k];
+  __syncthreads();   // the slab is free again
+}
+
+// the reverse: lane l's block v goes to dst + l*D as lane-contiguous chunks
+template <int D>
+__device__ __forceinline__ void wave_store(int32_t *dst, int nb, int32_t *slab, int lane, const int *v) {
+  constexpr int S = slab_stride<D>();
+#pragma unroll
+  for (int k = 0; k < D; ++k) slab[lane * S + k] = v[k];
+  __syncthreads();
+  if (D % 4 == 0) {
+    constexpr int C = D / 4;
+#pragma unroll
+    for (int k = 0; k < C; ++k) {
+      const int ch = k * 64 + lane, blk = ch / C, part = ch - blk * C;
+      if (blk < nb)
+        __builtin_nontemporal_store(*reinterpret_cast<const v4i *>(slab + blk * S + 4 * part),
+                                    reinterpret_cast<v4i *>(dst) + ch);
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      const int dw = k * 64 + lane, blk = dw / D;
+      if (blk < nb) __builtin_nontemporal_store(slab[blk * S + dw - blk * D], dst + dw);
+    }
+  }
+  __syncthreads();
+}
+
+// one block through op OP (a jmme_transform_op)
+template <int OP>
+__device__ __forceinline__ void transform_one(const int *in, int *out) {
+  int tmp[64];
+  if (OP == JMME_TF_FORWARD4x4 || OP == JMME_TF_INVERSE4x4 || OP == JMME_TF_IHADAMARD4x4) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (OP == JMME_TF_FORWARD4x4) fwd4(in + 4 * r, 1, tmp + 4 * r, 1);
+      if (OP == JMME_TF_INVERSE4x4) inv4(in + 4 * r, 1, tmp + 4 * r, 1);
+      if (OP == JMME_TF_IHADAMARD4x4) ihad4(in + 4 * r, 1, tmp + 4 * r, 1);
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      if (OP == JMME_TF_FORWARD4x4) fwd4(tmp + c, 4, out + c, 4);
+      if (OP == JMME_TF_INVERSE4x4) inv4(tmp + c, 4, out + c, 4);
+      if (OP == JMME_TF_IHADAMARD4x4) ihad4(tmp + c, 4, out + c, 4);
+    }
+  } else if (OP == JMME_TF_HADAMARD4x4) {          // vertical pass halves, transform.c:160-166
+#pragma unroll
+    for (int r = 0; r < 4; ++r) had4(in + 4 * r, 1, tmp + 4 * r, 1);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      int y[4];
+      had4(tmp + c, 4, y, 1);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) out[4 * k + c] = y[k] >> 1;
+    }
+  } else if (OP == JMME_TF_HADAMARD4x2 || OP == JMME_TF_IHADAMARD4x2) {   // transform.c:220-300
+#pragma unroll
+    for (int c = 0; c < 4; ++c) { tmp[c] = in[c] + in[4 + c]; tmp[4 + c] = in[c] - in[4 + c]; }
+    if (OP == JMME_TF_HADAMARD4x2) {
+      had4(tmp, 1, out, 1);
+      had4(tmp + 4, 1, out + 4, 1);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) ihad4(tmp + 4 * i, 1, out + i, 2);   // 4 rows x 2 columns out
+    }
+  } else if (OP == JMME_TF_HADAMARD2x2 || OP == JMME_TF_IHADAMARD2x2) {   // transform.c:302-331
+    const int p0 = in[0] + in[1], p1 = in[0] - in[1], p2 = in[2] + in[3], p3 = in[2] - in[3];
+    out[0] = p0 + p2; out[1] = p1 + p3; out[2] = p0 - p2; out[3] = p1 - p3;
+  } else {                                          // 8x8
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      if (OP == JMME_TF_FORWARD8x8) fwd8(in + 8 * r, 1, tmp + 8 * r, 1);
+      else inv8(in + 8 * r, 1, tmp + 8 * r, 1);
+    }
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      if (OP == JMME_TF_FORWARD8x8) fwd8(tmp + c, 8, out + c, 8);
+      else inv8(tmp + c, 8, out + c, 8);
+    }
+  }
+}
+
+__host__ __device__ constexpr int tf_elems(int op) {
+  return (op == JMME_TF_FORWARD8x8 || op == JMME_TF_INVERSE8x8) ? 64
+         : (op == JMME_TF_HADAMARD4x2 || op == JMME_TF_IHADAMARD4x2) ? 8
+         : (op == JMME_TF_HADAMARD2x2 || op == JMME_TF_IHADAMARD2x2) ? 4 : 16;
+}
+
+template <int OP>
+__global__ __launch_bounds__(kTB) void transform_kernel(const int32_t *__restrict__ in, int32_t *__restrict__ out,
+                                                        int n) {
+  constexpr int E = tf_elems(OP);
+  __shared__ __attribute__((aligned(16))) int32_t slab[64 * slab_stride<E>()];
+  const int lane = threadIdx.x;
+  for (int base = blockIdx.x * 64; base < n; base += gridDim.x * 64) {
+    const int nb = min(64, n - base);
+    int v[E], w[E];
+    wave_load<E>(in + (size_t)base * E, nb, slab, lane, v);
+    transform_one<OP>(v, w);
+    wave_store<E>(out + (size_t)base * E, nb, slab, lane, w);
+  }
+}
+
+// ---- SATD ------------------------------------------------------------------
+// Sum of |Walsh-Hadamard(d)|: every output of JM's HadamardSAD4x4/8x8 is a +-1
+// combination of the inputs with a distinct sign pattern, so the sum of
+// magnitudes does not depend on JM's output order.
+template <int N>
+__device__ __forceinline__ int wht_abs_sum(int *v) {
+#pragma unroll
+  for (int r = 0; r < N; ++r)
+#pragma unroll
+    for (int len = 1; len < N; len <<= 1)
+#pragma unroll
+      for (int j = 0; j < N; ++j)
+        if (!(j & len)) {
+          const int a = v[r * N + j], b = v[r * N + j + len];
+          v[r * N + j] = a + b;
+          v[r * N + j + len] = a - b;
+        }
+#pragma unroll
+  for (int c = 0; c < N; ++c)
+#pragma unroll
+    for (int len = 1; len < N; len <<= 1)
+#pragma unroll
+      for (int j = 0; j < N; ++j)
+        if (!(j & len)) {
+          const int a = v[j * N + c], b = v[(j + len) * N + c];
+          v[j * N + c] = a + b;
+          v[(j + len) * N + c] = a - b;
+        }
+  int s = 0;
+#pragma unroll
+  for (int k = 0; k < N * N; ++k) s += abs(v[k]);
+  return s;
+}
+
+template <int N>
+__global__ __launch_bounds__(kTB) void satd_kernel(const int16_t *__restrict__ diff, int32_t *__restrict__ out,
+                                                   int n) {
+  constexpr int D = N * N / 2;   // int16 pairs
+  __shared__ __attribute__((aligned(16))) int32_t slab[64 * slab_stride<D>()];
+  const int lane = threadIdx.x;
+  for (int base = blockIdx.x * 64; base < n; base += gridDim.x * 64) {
+    const int nb = min(64, n - base);
+    int w[D], v[N * N];
+    wave_load<D>(reinterpret_cast<const int32_t *>(diff) + (size_t)base * D, nb, slab, lane, w);
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      v[2 * k] = (int)(int16_t)(w[k] & 0xffff);
+      v[2 * k + 1] = w[k] >> 16;
+    }
+    const int s = wht_abs_sum<N>(v);
+    if (lane < nb) out[base + lane] = N == 4 ? (s + 1) >> 1 : (s + 2) >> 2;   // me_distortion.c:256, :339
+  }
+}
+
+// ---- quant_4x4_normal --------------------------------------------------------
+__global__ __launch_bounds__(kTB) void quant4x4_kernel(const jmme_quant4x4_params *__restrict__ params,
+                                                       const int32_t *__restrict__ param_idx,
+                                                       int32_t *__restrict__ coef, int32_t *__restrict__ levels,
+                                                       int32_t *__restrict__ runs,
+                                                       int32_t *__restrict__ coeff_cost,
+                                                       int32_t *__restrict__ nonzero, int n) {
+  // per-lane scratch for the scan-order walk (coefficient, level and run
+  // arrays indexed by the runtime scan position; stride 17 dwords keeps the
+  // 64 lanes on distinct banks).  The staging slab aliases it: the workgroup
+  // is one wave, and the slab is only live inside wave_load / wave_store.
+  __shared__ __attribute__((aligned(16))) int32_t lds[3 * 64 * 17];
+  static_assert(64 * slab_stride<17>() <= 3 * 64 * 17, "slab fits the scratch");
+  int32_t *slab = lds, *sc = lds, *sl = lds + 64 * 17, *sr = lds + 2 * 64 * 17;
+  const int lane = threadIdx.x;
+  int32_t *my_c = sc + lane * 17, *my_l = sl + lane * 17, *my_r = sr + lane * 17;
+  for (int base = blockIdx.x * 64; base < n; base += gridDim.x * 64) {
+    const int nb = min(64, n - base);
+    const int b = base + lane;
+    const bool live = lane < nb;
+    const jmme_quant4x4_params &q = params[(param_idx && live) ? param_idx[b] : 0];
+    int c[16];
+    wave_load<16>(coef + (size_t)base * 16, nb, slab, lane, c);
+#pragma unroll
+    for (int e = 0; e < 16; ++e) { my_c[e] = c[e]; my_l[e] = 0; my_r[e] = 0; }
+    my_l[16] = 0;
+    const int q_bits = 15 + q.qp_per;                 // Q_BITS, defines.h:311
+    int run = 0, nout = 0, nz = 0, cost = live ? coeff_cost[b] : 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int pq = q.scan[k][1] * 4 + q.scan[k][0];   // (horizontal, vertical)
+      const int x = my_c[pq];
+      if (x == 0) { ++run; continue; }
+      int level = (abs(x) * q.scale[pq] + q.offset[pq]) >> q_bits;
+      if (level == 0) {
+        my_c[pq] = 0;
+        ++run;
+        continue;
+      }
+      if (q.is_cavlc && level > 2063) level = 2063;    // CAVLC_LEVEL_LIMIT, defines.h:99
+      cost += level > 1 ? 999999 : (int)q.c_cost[run];   // MAX_VALUE, defines.h:123
+      if (x < 0) level = -level;
+      my_c[pq] = ((level * q.inv_scale[pq] << q.qp_per) + 8) >> 4;   // rshift_rnd_sf(.,4)
+      my_l[nout] = level;
+      my_r[nout] = run;
+      ++nout;
+      run = 0;
+      nz = 1;
+    }
+    int lv[17], rn[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) { c[e] = my_c[e]; lv[e] = my_l[e]; rn[e] = my_r[e]; }
+    lv[16] = my_l[16];
+    wave_store<16>(coef + (size_t)base * 16, nb, slab, lane, c);
+    wave_store<17>(levels + (size_t)base * 17, nb, slab, lane, lv);
+    wave_store<16>(runs + (size_t)base * 16, nb, slab, lane, rn);
+    if (live) {
+      coeff_cost[b] = cost;
+      nonzero[b] = nz;
+    }
+  }
+}
+
+int grid_for(int n) {
+  const int g = (n + 63) / 64;
+  return g < 1 ? 1 : (g > 8192 ? 8192 : g);
+}
+
+}  // namespace
+
+hipError_t launch_transform(int op, const int32_t *in, int32_t *out, int n, hipStream_t s) {
+  const int g = grid_for(n);
+  switch (op) {
+#define JMME_TF(OP) case OP: hipLaunchKernelGGL(transform_kernel<OP>, dim3(g), dim3(kTB), 0, s, in, out, n); break;
+    JMME_TF(JMME_TF_FORWARD4x4) JMME_TF(JMME_TF_INVERSE4x4) JMME_TF(JMME_TF_HADAMARD4x4)
+    JMME_TF(JMME_TF_IHADAMARD4x4) JMME_TF(JMME_TF_HADAMARD4x2) JMME_TF(JMME_TF_IHADAMARD4x2)
+    JMME_TF(JMME_TF_HADAMARD2x2) JMME_TF(JMME_TF_IHADAMARD2x2) JMME_TF(JMME_TF_FORWARD8x8)
+    JMME_TF(JMME_TF_INVERSE8x8)
+#undef JMME_TF
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+int transform_elems(int op) { return (op < 0 || op > JMME_TF_INVERSE8x8) ? 0 : tf_elems(op); }
+
+hipError_t launch_satd(int size, const int16_t *diff, int32_t *out, int n, hipStream_t s) {
+  const int g = grid_for(n);
+  if (size == 4) hipLaunchKernelGGL(satd_kernel<4>, dim3(g), dim3(kTB), 0, s, diff, out, n);
+  else if (size == 8) hipLaunchKernelGGL(satd_kernel<8>, dim3(g), dim3(kTB), 0, s, diff, out, n);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+hipError_t launch_quant4x4(const jmme_quant4x4_params *params, const int32_t *param_idx, int32_t *coef, int32_t *levels,
+                           int32_t *runs, int32_t *coeff_cost, int32_t *nonzero, int n, hipStream_t s) {
+  hipLaunchKernelGGL(quant4x4_kernel, dim3(grid_for(n)), dim3(kTB), 0, s, params, param_idx, coef, levels, runs,
+                     coeff_cost, nonzero, n);
+  return hipGetLastError();
+}
+
+}  // namespace jmme

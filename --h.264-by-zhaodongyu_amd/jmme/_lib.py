@@ -28,7 +28,14 @@ MB_REQ = np.dtype([("mb_x", "<i2"), ("mb_y", "<i2"), ("list", "<i2"), ("ref_idx"
                    ("ffs_pos00_valid", "<i2"), ("reserved", "<i2", (4,)),
                    ("blk", BLOCK_REQ, (NSLOT,))])
 BLOCK_RES = np.dtype([("mv_x", "<i2"), ("mv_y", "<i2"), ("reserved", "<i4"), ("cost", "<i8")])
+QUANT4x4_PARAMS = np.dtype([("scale", "<i4", (16,)), ("offset", "<i4", (16,)), ("inv_scale", "<i4", (16,)),
+                            ("qp_per", "<i4"), ("is_cavlc", "<i4"), ("scan", "u1", (16, 2)), ("c_cost", "u1", (16,))])
+TRANSFORM_OPS = {"forward4x4": (0, 16, 16), "inverse4x4": (1, 16, 16), "hadamard4x4": (2, 16, 16),
+                 "ihadamard4x4": (3, 16, 16), "hadamard4x2": (4, 8, 8), "ihadamard4x2": (5, 8, 8),
+                 "hadamard2x2": (6, 4, 4), "ihadamard2x2": (7, 4, 4), "forward8x8": (8, 64, 64),
+                 "inverse8x8": (9, 64, 64)}   # name -> (jmme_transform_op, in elems, out elems)
 assert BLOCK_REQ.itemsize == 16 and MB_REQ.itemsize == 688 and BLOCK_RES.itemsize == 16
+assert QUANT4x4_PARAMS.itemsize == 248
 
 CONFIG_FIELDS = ["SourceWidth", "SourceHeight", "SearchMode", "SearchRange", "NumberReferenceFrames",
                  "DisableSubpelME", "RDOptimization", "MEDistortionFPel", "MDDistortion", "EPZSSubPelGrid",
@@ -79,6 +86,12 @@ def lib() -> ctypes.CDLL:
         "jmme_full_search_block": (ctypes.c_int64, [P, I, I, I, I, I, P, P, ctypes.c_int64, I, I, I]),
         "jmme_fast_full_search_block": (ctypes.c_int64, [P, I, I, I, I, I, P, P, I, I, I, P, ctypes.c_int64, I]),
         "jmme_last_kernel_ms": (ctypes.c_float, [P]),
+        "jmme_transform": (I, [P, I, P, P, I]),
+        "jmme_transform_async": (I, [P, I, P, P, I, P]),
+        "jmme_satd": (I, [P, I, P, P, I]),
+        "jmme_satd_async": (I, [P, I, P, P, I, P]),
+        "jmme_quant4x4": (I, [P, P, I, P, P, P, P, P, P, I]),
+        "jmme_quant4x4_async": (I, [P, P, P, P, P, P, P, P, I, P]),
         "jmme_spiral_index": (I, [I, I]),
         "jmme_spiral_offset": (V, [I, P, P]),
         "jmme_mvbits": (I, [I]),

@@ -126,6 +126,48 @@ class MotionEstimator:
                                             int(lambda_factor), int(search_range), int(check_for_00))
         return (mv.mv_x, mv.mv_y), int(cost)
 
+    # ---- transforms / quant / SATD -----------------------
+    def transform(self, op: str, blocks: np.ndarray) -> np.ndarray:
+        """JM transform `op` (forward4x4, inverse8x8, ...) of n row-major blocks."""
+        code, ein, eout = _lib.TRANSFORM_OPS[op]
+        blocks = np.ascontiguousarray(blocks, np.int32).reshape(-1, ein)
+        out = np.empty((blocks.shape[0], eout), np.int32)
+        check(lib().jmme_transform(self._ctx, code, ptr(blocks), ptr(out), blocks.shape[0]))
+        return out
+
+    def transform_async(self, op: str, d_in: int, d_out: int, n: int, stream: int = 0) -> None:
+        check(lib().jmme_transform_async(self._ctx, _lib.TRANSFORM_OPS[op][0], d_in, d_out, int(n), stream))
+
+    def satd(self, size: int, diff: np.ndarray) -> np.ndarray:
+        """HadamardSAD4x4 / HadamardSAD8x8 of n int16 residual blocks."""
+        diff = np.ascontiguousarray(diff, np.int16).reshape(-1, size * size)
+        out = np.empty(diff.shape[0], np.int32)
+        check(lib().jmme_satd(self._ctx, int(size), ptr(diff), ptr(out), diff.shape[0]))
+        return out
+
+    def satd_async(self, size: int, d_diff: int, d_out: int, n: int, stream: int = 0) -> None:
+        check(lib().jmme_satd_async(self._ctx, int(size), d_diff, d_out, int(n), stream))
+
+    def quant4x4(self, params: np.ndarray, coef: np.ndarray, coeff_cost: np.ndarray | None = None,
+                 param_idx: np.ndarray | None = None):
+        """quant_4x4_normal over n blocks -> (coef_out, levels[n,17], runs[n,16], coeff_cost, nonzero)."""
+        params = np.ascontiguousarray(params, _lib.QUANT4x4_PARAMS).reshape(-1)
+        coef = np.array(coef, np.int32).reshape(-1, 16)
+        n = coef.shape[0]
+        cost = np.zeros(n, np.int32) if coeff_cost is None else np.array(coeff_cost, np.int32).reshape(n)
+        levels = np.empty((n, 17), np.int32)
+        runs = np.empty((n, 16), np.int32)
+        nz = np.empty(n, np.int32)
+        idx = None if param_idx is None else np.ascontiguousarray(param_idx, np.int32).reshape(n)
+        check(lib().jmme_quant4x4(self._ctx, ptr(params), params.shape[0], None if idx is None else ptr(idx),
+                                  ptr(coef), ptr(levels), ptr(runs), ptr(cost), ptr(nz), n))
+        return coef, levels, runs, cost, nz
+
+    def quant4x4_async(self, d_params: int, d_param_idx: int, d_coef: int, d_levels: int, d_runs: int,
+                       d_coeff_cost: int, d_nonzero: int, n: int, stream: int = 0) -> None:
+        check(lib().jmme_quant4x4_async(self._ctx, d_params, d_param_idx or None, d_coef, d_levels, d_runs,
+                                        d_coeff_cost, d_nonzero, int(n), stream))
+
     def fast_full_search_block(self, list_idx, ref_idx, pos_x, pos_y, blocktype, pred, search_center,
                                surface_range, block_range, rdopt, lambda_factor, min_mcost=_lib.DISTBLK_MAX):
         """fast_full_search_motion_estimation's contract for one partition (JM me_fullfast.c:618-689)."""

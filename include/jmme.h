@@ -180,6 +180,56 @@ jmme_distblk jmme_fast_full_search_block(jmme_ctx *ctx, int list, int ref_idx,
                                          int surface_range, int block_range, int rdopt,
                                          jmme_mv *mv_out, jmme_distblk min_mcost, int lambda_factor);
 
+/* ---- Block transforms, 4x4 quantisation, Hadamard SATD (batched) ---------
+ * SURVEY.md §8 rows a12/a13.  n independent blocks, each a flat row-major
+ * array (b[r*N + c] == JM's block[pos_y + r][pos_x + c]), back to back.
+ * *_async take device pointers and run on the caller's HIP stream; the plain
+ * forms take host arrays and synchronise.  All bit-exact with JM 18.5. */
+typedef enum jmme_transform_op {
+  JMME_TF_FORWARD4x4 = 0,   /* forward4x4,   JM/lcommon/src/transform.c:20-68   (16 -> 16) */
+  JMME_TF_INVERSE4x4,       /* inverse4x4,   transform.c:70-119                  (16 -> 16) */
+  JMME_TF_HADAMARD4x4,      /* hadamard4x4,  transform.c:121-169 (luma DC)       (16 -> 16) */
+  JMME_TF_IHADAMARD4x4,     /* ihadamard4x4, transform.c:171-218                 (16 -> 16) */
+  JMME_TF_HADAMARD4x2,      /* hadamard4x2,  transform.c:220-258 (2x4 chroma DC) ( 8 ->  8) */
+  JMME_TF_IHADAMARD4x2,     /* ihadamard4x2, transform.c:260-300 (2x4 -> 4x2)    ( 8 ->  8) */
+  JMME_TF_HADAMARD2x2,      /* hadamard2x2,  transform.c:302-315 ({b00,b04,b40,b44}) (4 -> 4) */
+  JMME_TF_IHADAMARD2x2,     /* ihadamard2x2, transform.c:317-331                 ( 4 ->  4) */
+  JMME_TF_FORWARD8x8,       /* forward8x8,   transform.c:353-448                 (64 -> 64) */
+  JMME_TF_INVERSE8x8        /* inverse8x8,   transform.c:450-528                 (64 -> 64) */
+} jmme_transform_op;
+
+int jmme_transform(jmme_ctx *ctx, int op, const int32_t *in, int32_t *out, int n);
+int jmme_transform_async(jmme_ctx *ctx, int op, const int32_t *d_in, int32_t *d_out, int n, void *stream);
+
+/* HadamardSAD4x4 / HadamardSAD8x8 (JM/lencod/src/me_distortion.c:175-341) of
+ * n residual blocks (int16, 16 or 64 per block) -> int32 per block, unscaled
+ * (distortion4x4SATD, me_distortion.c:70-74, is this << 5). size = 4 or 8. */
+int jmme_satd(jmme_ctx *ctx, int size, const int16_t *diff, int32_t *out, int n);
+int jmme_satd_async(jmme_ctx *ctx, int size, const int16_t *d_diff, int32_t *d_out, int n, void *stream);
+
+/* quant_4x4_normal (JM/lencod/src/quant4x4_normal.c:39-110) inputs for one
+ * parameter set: scale/offset/inv_scale = q_params_4x4[j][i].{ScaleComp,
+ * OffsetComp,InvScaleComp} at [j*4+i] (quant_params.h:17-21), qp_per =
+ * p_Quant->qp_per_matrix[qp], is_cavlc = (symbol_mode == CAVLC), scan =
+ * pos_scan as (horizontal, vertical), c_cost = COEFF_COST4x4[disthres]. */
+typedef struct jmme_quant4x4_params {
+  int32_t scale[16], offset[16], inv_scale[16];
+  int32_t qp_per;
+  int32_t is_cavlc;
+  uint8_t scan[16][2];
+  uint8_t c_cost[16];
+} jmme_quant4x4_params;   /* 248 bytes */
+
+/* Per block b (param set params[param_idx[b]], or params[0] if param_idx is
+ * NULL): coef[b][16] in = tblock, out = the dequantised block JM leaves in
+ * tblock; levels[b][17] = ACLevel (0-terminated), runs[b][16] = ACRun;
+ * coeff_cost[b] in/out (JM's *coeff_cost += ...); nonzero[b] = return value. */
+int jmme_quant4x4(jmme_ctx *ctx, const jmme_quant4x4_params *params, int n_params, const int32_t *param_idx,
+                  int32_t *coef, int32_t *levels, int32_t *runs, int32_t *coeff_cost, int32_t *nonzero, int n);
+int jmme_quant4x4_async(jmme_ctx *ctx, const jmme_quant4x4_params *d_params, const int32_t *d_param_idx,
+                        int32_t *d_coef, int32_t *d_levels, int32_t *d_runs, int32_t *d_coeff_cost,
+                        int32_t *d_nonzero, int n, void *stream);
+
 /* ---- timing of the last jmme_search_mbs* launch (HIP events on its stream) */
 float jmme_last_kernel_ms(jmme_ctx *ctx);
 

@@ -26,7 +26,8 @@ def manifest() -> dict:
 
 
 def cases() -> list[str]:
-    return sorted(manifest())
+    """The motion-search cases (captured JM encodes); other fixtures, e.g. tq_jm, are not searches."""
+    return sorted(k for k, v in manifest().items() if "cfg_overrides" in v)
 
 
 class Case:

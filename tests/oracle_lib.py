@@ -87,3 +87,92 @@ def ffs_batch(cur, ref, surf_range, max_mvd, rdopt, mbs, blk):
     load().ora_ffs_batch(_p(cur), _p(ref), w, h, surf_range, max_mvd, rdopt,
                          mbs.shape[0], _p(mbs), n, _p(blk), _p(mv), _p(cost))
     return mv, cost
+
+
+# ---- transforms / quant / SATD (oracle/tq_oracle.c) --------------------------
+TQ_SO = os.path.join(ORACLE_DIR, "build", "libtq_oracle.so")
+_tq = None
+
+TQ_OPS = {  # op -> (in elements, out elements)
+    "forward4x4": (16, 16), "inverse4x4": (16, 16), "hadamard4x4": (16, 16), "ihadamard4x4": (16, 16),
+    "hadamard4x2": (8, 8), "ihadamard4x2": (8, 8), "hadamard2x2": (4, 4), "ihadamard2x2": (4, 4),
+    "forward8x8": (64, 64), "inverse8x8": (64, 64),
+}
+
+
+class QuantParams(ctypes.Structure):
+    _fields_ = [("scale", ctypes.c_int32 * 16), ("offset", ctypes.c_int32 * 16), ("inv_scale", ctypes.c_int32 * 16),
+                ("qp_per", ctypes.c_int32), ("is_cavlc", ctypes.c_int32), ("scan", (ctypes.c_uint8 * 2) * 16),
+                ("c_cost", ctypes.c_uint8 * 16)]
+
+
+def load_tq() -> ctypes.CDLL:
+    global _tq
+    if _tq is not None:
+        return _tq
+    src = os.path.join(ORACLE_DIR, "tq_oracle.c")
+    if not os.path.exists(TQ_SO) or os.path.getmtime(TQ_SO) < os.path.getmtime(src):
+        subprocess.run(["make", "-s", "-C", ORACLE_DIR, "port"], check=True)
+    lib = ctypes.CDLL(TQ_SO)
+    for op in TQ_OPS:
+        getattr(lib, "tqo_" + op).argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    lib.tqo_hadamard_sad4x4.argtypes = [ctypes.c_void_p]
+    lib.tqo_hadamard_sad8x8.argtypes = [ctypes.c_void_p]
+    lib.tqo_quant_4x4_normal.argtypes = [ctypes.c_void_p, ctypes.POINTER(QuantParams), ctypes.c_void_p,
+                                         ctypes.c_void_p, ctypes.c_void_p]
+    _tq = lib
+    return lib
+
+
+def tq_transform(op, blocks):
+    """blocks int32 [n, in] -> [n, out] through the oracle's tqo_<op>."""
+    lib = load_tq()
+    fn = getattr(lib, "tqo_" + op)
+    blocks = np.ascontiguousarray(blocks, np.int32)
+    out = np.zeros((blocks.shape[0], TQ_OPS[op][1]), np.int32)
+    for i in range(blocks.shape[0]):
+        fn(blocks[i].ctypes.data, out[i].ctypes.data)
+    return out
+
+
+def tq_satd(diff, size):
+    lib = load_tq()
+    fn = lib.tqo_hadamard_sad4x4 if size == 4 else lib.tqo_hadamard_sad8x8
+    diff = np.ascontiguousarray(diff, np.int16)
+    return np.array([fn(diff[i].ctypes.data) for i in range(diff.shape[0])], np.int32)
+
+
+FRAME_SCAN = [(0, 0), (1, 0), (0, 1), (0, 2), (1, 1), (2, 0), (3, 0), (2, 1),
+              (1, 2), (0, 3), (1, 3), (2, 2), (3, 1), (3, 2), (2, 3), (3, 3)]
+FIELD_SCAN = [(0, 0), (0, 1), (1, 0), (0, 2), (0, 3), (1, 1), (1, 2), (1, 3),
+              (2, 0), (2, 1), (2, 2), (2, 3), (3, 0), (3, 1), (3, 2), (3, 3)]
+C_COST = [[3, 2, 2, 1, 1, 1] + [0] * 10, [9] * 16]
+
+
+def quant_params(scale, offset, inv, qp, cavlc, scan_sel, cost_sel) -> QuantParams:
+    q = QuantParams()
+    for k in range(16):
+        q.scale[k], q.offset[k], q.inv_scale[k] = int(scale[k]), int(offset[k]), int(inv[k])
+        sc = (FIELD_SCAN if scan_sel else FRAME_SCAN)[k]
+        q.scan[k][0], q.scan[k][1] = sc
+        q.c_cost[k] = C_COST[cost_sel][k]
+    q.qp_per = int(qp) // 6
+    q.is_cavlc = int(cavlc)
+    return q
+
+
+def tq_quant_records(rec_in):
+    """Rows laid out as the harness's quant4x4 records -> rows like its outputs."""
+    lib = load_tq()
+    rec_in = np.asarray(rec_in, np.int32)
+    out = np.zeros((rec_in.shape[0], 51), np.int32)
+    for i, r in enumerate(rec_in):
+        coef = r[0:16].copy()
+        q = quant_params(r[16:32], r[32:48], r[48:64], r[64], r[65], r[66], r[67])
+        levels = np.zeros(17, np.int32)
+        runs = np.zeros(16, np.int32)
+        cost = np.array([r[68]], np.int32)
+        nz = lib.tqo_quant_4x4_normal(coef.ctypes.data, ctypes.byref(q), levels.ctypes.data, runs.ctypes.data,
+                                      cost.ctypes.data)
+        out[i] = np.concatenate([coef, levels, runs, cost, [nz]])
+    return out

@@ -1,0 +1,77 @@
+#!/usr/bin/env python3
+"""Throughput of the transform / quant / SATD kernels
+against the HBM roofline: each is a one-pass stream over n blocks, so the
+algorithmic bytes are input + output per block.  Prints one JSON line per op.
+Usage (GPU): python3 tools/bench_tq.py [--blocks N] [--iters K]"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "--h.264-by-zhaodongyu_amd"))
+from jmme import MotionEstimator, QUANT4x4_PARAMS, TRANSFORM_OPS  # noqa: E402
+
+HBM = 8000.0
+
+
+def timed(fn, iters):
+    s = torch.cuda.current_stream()
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(iters):
+        fn()
+    e1.record(s)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--blocks", type=int, default=1 << 22)
+    ap.add_argument("--iters", type=int, default=20)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    st = torch.cuda.current_stream().cuda_stream
+    me = MotionEstimator()
+    n = a.blocks
+    for op, (_, ein, eout) in TRANSFORM_OPS.items():
+        x = torch.randint(-255, 256, (n, ein), dtype=torch.int32, device=dev)
+        y = torch.empty((n, eout), dtype=torch.int32, device=dev)
+        ms = timed(lambda: me.transform_async(op, x.data_ptr(), y.data_ptr(), n, st), a.iters)
+        gbs = n * (ein + eout) * 4 / (ms * 1e-3) / 1e9
+        print(json.dumps({"op": op, "blocks": n, "ms": round(ms, 4), "GB_per_s": round(gbs, 1),
+                          "hbm_frac": round(gbs / HBM, 4), "bytes_per_block": (ein + eout) * 4}))
+    for size in (4, 8):
+        d = torch.randint(-255, 256, (n, size * size), dtype=torch.int16, device=dev)
+        o = torch.empty(n, dtype=torch.int32, device=dev)
+        ms = timed(lambda: me.satd_async(size, d.data_ptr(), o.data_ptr(), n, st), a.iters)
+        b = size * size * 2 + 4
+        gbs = n * b / (ms * 1e-3) / 1e9
+        print(json.dumps({"op": f"satd{size}x{size}", "blocks": n, "ms": round(ms, 4), "GB_per_s": round(gbs, 1),
+                          "hbm_frac": round(gbs / HBM, 4), "bytes_per_block": b}))
+    p = np.zeros(1, QUANT4x4_PARAMS)
+    p["scale"], p["offset"], p["inv_scale"], p["qp_per"], p["is_cavlc"] = 8192, 1 << 16, 256, 4, 1
+    p["scan"] = [(k % 4, k // 4) for k in range(16)]
+    dp = torch.from_numpy(p.view(np.uint8).copy()).to(dev)
+    coef = torch.randint(-2000, 2001, (n, 16), dtype=torch.int32, device=dev)
+    lev = torch.empty((n, 17), dtype=torch.int32, device=dev)
+    run = torch.empty((n, 16), dtype=torch.int32, device=dev)
+    cost = torch.zeros(n, dtype=torch.int32, device=dev)
+    nz = torch.empty(n, dtype=torch.int32, device=dev)
+    ms = timed(lambda: me.quant4x4_async(dp.data_ptr(), 0, coef.data_ptr(), lev.data_ptr(), run.data_ptr(),
+                                         cost.data_ptr(), nz.data_ptr(), n, st), a.iters)
+    b = 64 + 64 + 68 + 64 + 4 + 4 + 4
+    gbs = n * b / (ms * 1e-3) / 1e9
+    print(json.dumps({"op": "quant4x4", "blocks": n, "ms": round(ms, 4), "GB_per_s": round(gbs, 1),
+                      "hbm_frac": round(gbs / HBM, 4), "bytes_per_block": b}))
+    me.close()
+
+
+if __name__ == "__main__":
+    main()
