@@ -16,6 +16,7 @@
 #include "jmme_common.h"
 #include "jmme_internal.h"
 #include "jmme_tq_internal.h"
+#include "jmme_fractal_internal.h"
 
 using namespace jmme;
 
@@ -607,6 +608,110 @@ extern "C" int jmme_quant4x4(jmme_ctx *ctx, const jmme_quant4x4_params *params, 
   HIPCHK(hipMemcpy(runs, dr.p, (size_t)n * 64, hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(coeff_cost, dk.p, (size_t)n * 4, hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(nonzero, dn.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+// ------------------------------------------------------------------ fractal --
+namespace {
+
+bool fractal_block_ok(int bsx, int bsy) {
+  return (bsx == 16 && (bsy == 16 || bsy == 8)) || (bsx == 8 && (bsy == 16 || bsy == 8 || bsy == 4)) ||
+         (bsx == 4 && (bsy == 8 || bsy == 4));
+}
+
+int fractal_geom_ok(int pitch, int w, int h) {
+  if (w < 16 || h < 16 || pitch < w || (pitch & 3)) return fail("fractal plane %dx%d pitch %d: need >= 16x16, pitch %% 4 == 0", w, h, pitch);
+  return 0;
+}
+
+}  // namespace
+
+extern "C" int jmme_fractal_words_async(jmme_ctx *ctx, const uint8_t *d_ref, int pitch, int width, int height,
+                                        uint32_t *d_words, void *stream) {
+  if (!ctx) return fail("null ctx");
+  if (fractal_geom_ok(pitch, width, height)) return -1;
+  if (!d_ref || !d_words) return fail("null plane");
+  HIPCHK(launch_fractal_words(d_ref, pitch, width, height, d_words, width, reinterpret_cast<hipStream_t>(stream)));
+  return 0;
+}
+
+extern "C" int jmme_fractal_search_async(jmme_ctx *ctx, const uint8_t *d_org, int pitch, const uint32_t *d_words,
+                                         int width, int height, int search_range, const jmme_fractal_req *d_req,
+                                         int n, jmme_fractal_res *d_out, void *stream) {
+  if (!ctx) return fail("null ctx");
+  if (fractal_geom_ok(pitch, width, height)) return -1;
+  if (search_range < 0) return fail("negative search range");
+  if (n < 0) return fail("negative request count");
+  if (n == 0) return 0;
+  if (!d_org || !d_words || !d_req || !d_out) return fail("null array");
+  FractalParams p{};
+  p.org = d_org;
+  p.pitch = pitch;
+  p.words = d_words;
+  p.wpitch = width;
+  p.width = width;
+  p.height = height;
+  p.range = search_range;
+  p.req = d_req;
+  p.out = d_out;
+  p.n = n;
+  HIPCHK(launch_fractal_search(p, reinterpret_cast<hipStream_t>(stream)));
+  return 0;
+}
+
+extern "C" int jmme_fractal_search(jmme_ctx *ctx, const uint8_t *org, const uint8_t *ref, int pitch, int width,
+                                   int height, int search_range, const jmme_fractal_req *req, int n,
+                                   jmme_fractal_res *out) {
+  if (!ctx) return fail("null ctx");
+  if (fractal_geom_ok(pitch, width, height)) return -1;
+  if (search_range < 0) return fail("negative search range");
+  if (n <= 0) return n < 0 ? fail("negative request count") : 0;
+  if (!org || !ref || !req || !out) return fail("null array");
+  for (int i = 0; i < n; ++i) {
+    const jmme_fractal_req &q = req[i];
+    if (!fractal_block_ok(q.bsx, q.bsy)) return fail("request %d: block %dx%d not a thesis block size", i, q.bsx, q.bsy);
+    if (q.block_x < 0 || q.block_y < 0 || q.block_x % q.bsx || q.block_y % q.bsy || q.block_x + q.bsx > width ||
+        q.block_y + q.bsy > height)
+      return fail("request %d: range block (%d,%d) %dx%d not aligned inside %dx%d", i, q.block_x, q.block_y, q.bsx,
+                  q.bsy, width, height);
+  }
+  const size_t plane = (size_t)pitch * height;
+  DevBuf o, r, w, dq, dout;
+  HIPCHK(o.alloc(plane));
+  HIPCHK(r.alloc(plane));
+  HIPCHK(w.alloc((size_t)width * height * 4));
+  HIPCHK(dq.alloc((size_t)n * sizeof(jmme_fractal_req)));
+  HIPCHK(dout.alloc((size_t)n * sizeof(jmme_fractal_res)));
+  HIPCHK(hipMemcpy(o.p, org, plane, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(r.p, ref, plane, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dq.p, req, (size_t)n * sizeof(jmme_fractal_req), hipMemcpyHostToDevice));
+  if (jmme_fractal_words_async(ctx, (const uint8_t *)r.p, pitch, width, height, (uint32_t *)w.p, nullptr)) return -1;
+  if (jmme_fractal_search_async(ctx, (const uint8_t *)o.p, pitch, (const uint32_t *)w.p, width, height,
+                                search_range, (const jmme_fractal_req *)dq.p, n, (jmme_fractal_res *)dout.p,
+                                nullptr))
+    return -1;
+  HIPCHK(hipMemcpy(out, dout.p, (size_t)n * sizeof(jmme_fractal_res), hipMemcpyDeviceToHost));
+  return 0;
+}
+
+extern "C" int jmme_fractal_box_sums(jmme_ctx *ctx, const uint8_t *plane, int pitch, int width, int height, int bsx,
+                                     int bsy, double *sum, double *sum2) {
+  if (!ctx) return fail("null ctx");
+  if (fractal_geom_ok(pitch, width, height)) return -1;
+  if (bsx < 1 || bsy < 1 || bsx > 16 || bsy > 16 || bsx > width || bsy > height) return fail("box %dx%d", bsx, bsy);
+  if (!plane || !sum || !sum2) return fail("null array");
+  const int w = width - bsx + 1, h = height - bsy + 1;
+  DevBuf dp, hs, hs2, ds, ds2;
+  HIPCHK(dp.alloc((size_t)pitch * height));
+  HIPCHK(hs.alloc((size_t)w * height * 4));
+  HIPCHK(hs2.alloc((size_t)w * height * 4));
+  HIPCHK(ds.alloc((size_t)w * h * 8));
+  HIPCHK(ds2.alloc((size_t)w * h * 8));
+  HIPCHK(hipMemcpy(dp.p, plane, (size_t)pitch * height, hipMemcpyHostToDevice));
+  HIPCHK(launch_box_sums((const uint8_t *)dp.p, pitch, width, height, bsx, bsy, (uint32_t *)hs.p, (uint32_t *)hs2.p,
+                         (double *)ds.p, (double *)ds2.p, nullptr));
+  HIPCHK(hipMemcpy(sum, ds.p, (size_t)w * h * 8, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(sum2, ds2.p, (size_t)w * h * 8, hipMemcpyDeviceToHost));
   return 0;
 }
 

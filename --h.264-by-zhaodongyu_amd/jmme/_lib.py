@@ -28,6 +28,8 @@ MB_REQ = np.dtype([("mb_x", "<i2"), ("mb_y", "<i2"), ("list", "<i2"), ("ref_idx"
                    ("ffs_pos00_valid", "<i2"), ("reserved", "<i2", (4,)),
                    ("blk", BLOCK_REQ, (NSLOT,))])
 BLOCK_RES = np.dtype([("mv_x", "<i2"), ("mv_y", "<i2"), ("reserved", "<i4"), ("cost", "<i8")])
+FRACTAL_REQ = np.dtype([("block_x", "<i2"), ("block_y", "<i2"), ("bsx", "<i2"), ("bsy", "<i2")])
+FRACTAL_RES = np.dtype([("rms", "<f8"), ("scale", "<f8"), ("offset", "<f8"), ("x", "<i4"), ("y", "<i4")])
 QUANT4x4_PARAMS = np.dtype([("scale", "<i4", (16,)), ("offset", "<i4", (16,)), ("inv_scale", "<i4", (16,)),
                             ("qp_per", "<i4"), ("is_cavlc", "<i4"), ("scan", "u1", (16, 2)), ("c_cost", "u1", (16,))])
 TRANSFORM_OPS = {"forward4x4": (0, 16, 16), "inverse4x4": (1, 16, 16), "hadamard4x4": (2, 16, 16),
@@ -35,7 +37,7 @@ TRANSFORM_OPS = {"forward4x4": (0, 16, 16), "inverse4x4": (1, 16, 16), "hadamard
                  "hadamard2x2": (6, 4, 4), "ihadamard2x2": (7, 4, 4), "forward8x8": (8, 64, 64),
                  "inverse8x8": (9, 64, 64)}   # name -> (jmme_transform_op, in elems, out elems)
 assert BLOCK_REQ.itemsize == 16 and MB_REQ.itemsize == 688 and BLOCK_RES.itemsize == 16
-assert QUANT4x4_PARAMS.itemsize == 248
+assert QUANT4x4_PARAMS.itemsize == 248 and FRACTAL_REQ.itemsize == 8 and FRACTAL_RES.itemsize == 32
 
 CONFIG_FIELDS = ["SourceWidth", "SourceHeight", "SearchMode", "SearchRange", "NumberReferenceFrames",
                  "DisableSubpelME", "RDOptimization", "MEDistortionFPel", "MDDistortion", "EPZSSubPelGrid",
@@ -91,6 +93,10 @@ def lib() -> ctypes.CDLL:
         "jmme_satd": (I, [P, I, P, P, I]),
         "jmme_satd_async": (I, [P, I, P, P, I, P]),
         "jmme_quant4x4": (I, [P, P, I, P, P, P, P, P, P, I]),
+        "jmme_fractal_search": (I, [P, P, P, I, I, I, I, P, I, P]),
+        "jmme_fractal_words_async": (I, [P, P, I, I, I, P, P]),
+        "jmme_fractal_search_async": (I, [P, P, I, P, I, I, I, P, I, P, P]),
+        "jmme_fractal_box_sums": (I, [P, P, I, I, I, I, I, P, P]),
         "jmme_quant4x4_async": (I, [P, P, P, P, P, P, P, P, I, P]),
         "jmme_spiral_index": (I, [I, I]),
         "jmme_spiral_offset": (V, [I, P, P]),

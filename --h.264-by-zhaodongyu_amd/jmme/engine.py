@@ -168,6 +168,36 @@ class MotionEstimator:
         check(lib().jmme_quant4x4_async(self._ctx, d_params, d_param_idx or None, d_coef, d_levels, d_runs,
                                         d_coeff_cost, d_nonzero, int(n), stream))
 
+    # ---- thesis fractal domain-range search ------------------
+    def fractal_search(self, org: np.ndarray, ref: np.ndarray, search_range: int, req: np.ndarray) -> np.ndarray:
+        """full_search (ZL/src/block_enc.c:1933) for each request -> FRACTAL_RES[n]."""
+        org = np.ascontiguousarray(org, np.uint8)
+        ref = np.ascontiguousarray(ref, np.uint8)
+        h, w = org.shape
+        req = np.ascontiguousarray(req, _lib.FRACTAL_REQ)
+        out = np.zeros(len(req), _lib.FRACTAL_RES)
+        check(lib().jmme_fractal_search(self._ctx, ptr(org), ptr(ref), w, w, h, int(search_range), ptr(req),
+                                        len(req), ptr(out)))
+        return out
+
+    def fractal_words_async(self, d_ref: int, pitch: int, width: int, height: int, d_words: int,
+                            stream: int = 0) -> None:
+        check(lib().jmme_fractal_words_async(self._ctx, d_ref, pitch, width, height, d_words, stream))
+
+    def fractal_search_async(self, d_org: int, pitch: int, d_words: int, width: int, height: int, search_range: int,
+                             d_req: int, n: int, d_out: int, stream: int = 0) -> None:
+        check(lib().jmme_fractal_search_async(self._ctx, d_org, pitch, d_words, width, height, int(search_range),
+                                              d_req, int(n), d_out, stream))
+
+    def fractal_box_sums(self, plane: np.ndarray, bsx: int, bsy: int):
+        """compute_domain_Sum for one block size -> (sum, sum2) float64 [(H-bsy+1), (W-bsx+1)]."""
+        plane = np.ascontiguousarray(plane, np.uint8)
+        h, w = plane.shape
+        s = np.zeros((h - bsy + 1, w - bsx + 1), np.float64)
+        s2 = np.zeros_like(s)
+        check(lib().jmme_fractal_box_sums(self._ctx, ptr(plane), w, w, h, int(bsx), int(bsy), ptr(s), ptr(s2)))
+        return s, s2
+
     def fast_full_search_block(self, list_idx, ref_idx, pos_x, pos_y, blocktype, pred, search_center,
                                surface_range, block_range, rdopt, lambda_factor, min_mcost=_lib.DISTBLK_MAX):
         """fast_full_search_motion_estimation's contract for one partition (JM me_fullfast.c:618-689)."""

@@ -230,6 +230,43 @@ int jmme_quant4x4_async(jmme_ctx *ctx, const jmme_quant4x4_params *d_params, con
                         int32_t *d_coef, int32_t *d_levels, int32_t *d_runs, int32_t *d_coeff_cost,
                         int32_t *d_nonzero, int n, void *stream);
 
+/* ---- Fractal domain-range block matching (thesis codec) -------------------
+ * SURVEY.md §8 rows a14-a16; ZL = /root/reference/2.论文程序/ZhangLing_Yu_
+ * version1/H264Fractal.  full_search (ZL/src/block_enc.c:1933-1977) with
+ * compute_rms / compute_rdSum / QUAN_A (ZL/src/compute.c:6-215,
+ * ZL/inc/defines_enc.h:591-601) and bound_chk (block_enc.c:2894-2919), one
+ * request per range block.  Planes are 8-bit (the thesis's byte**), rows
+ * `pitch` bytes apart (pitch % 4 == 0, W and H the picture size bound_chk
+ * uses, i.e. the component's own size).  Block sizes: 16x16, 16x8, 8x16,
+ * 8x8, 8x4, 4x8, 4x4 with the range block aligned to its size.
+ * rms/scale/offset are bit-identical doubles to the thesis's. */
+typedef struct jmme_fractal_req {
+  int16_t block_x, block_y;   /* range block origin (pels), multiple of bsx / bsy */
+  int16_t bsx, bsy;
+} jmme_fractal_req;           /* 8 bytes */
+
+typedef struct jmme_fractal_res {
+  double rms;                 /* full_search's return value (1e30: nothing in range) */
+  double scale, offset;       /* TRANS_NODE scale (alpha), offset (beta) */
+  int32_t x, y;               /* TRANS_NODE x, y: domain - range offset (0,0 when (0,0) wins) */
+} jmme_fractal_res;           /* 32 bytes */
+
+int jmme_fractal_search(jmme_ctx *ctx, const uint8_t *org, const uint8_t *ref, int pitch, int width, int height,
+                        int search_range, const jmme_fractal_req *req, int n, jmme_fractal_res *out);
+/* device-pointer form: d_words is the reference's words image built by
+ * jmme_fractal_words_async (one per reference frame, width*height uint32). */
+int jmme_fractal_words_async(jmme_ctx *ctx, const uint8_t *d_ref, int pitch, int width, int height,
+                             uint32_t *d_words, void *stream);
+int jmme_fractal_search_async(jmme_ctx *ctx, const uint8_t *d_org, int pitch, const uint32_t *d_words, int width,
+                              int height, int search_range, const jmme_fractal_req *d_req, int n,
+                              jmme_fractal_res *d_out, void *stream);
+
+/* compute_domain_Sum / compute_range_Sum (ZL/src/compute.c:277-~1091) for one
+ * block size: sum and sum of squares of every bsx x bsy box of the plane,
+ * (height-bsy+1) x (width-bsx+1) doubles each (exact integers). */
+int jmme_fractal_box_sums(jmme_ctx *ctx, const uint8_t *plane, int pitch, int width, int height, int bsx, int bsy,
+                          double *sum, double *sum2);
+
 /* ---- timing of the last jmme_search_mbs* launch (HIP events on its stream) */
 float jmme_last_kernel_ms(jmme_ctx *ctx);
 

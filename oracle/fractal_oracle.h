@@ -1,0 +1,52 @@
+/*
+ * fractal_oracle.h -- TEST INFRASTRUCTURE: plain-C restatement of the thesis
+ * codec's fractal domain-range block matching:
+ *   compute_domain_Sum / compute_range_Sum   ZL/src/compute.c:277-~1091
+ *   compute_rms, compute_rdSum, QUAN_A       ZL/src/compute.c:6-215,
+ *                                            ZL/inc/defines_enc.h:19-22,591-601
+ *   full_search, bound_chk                   ZL/src/block_enc.c:1933-1977, 2894-2919
+ * (ZL = /root/reference/2.论文程序/ZhangLing_Yu_version1/H264Fractal).
+ *
+ * PARITY UNPINNED: the thesis sources need a windows.h stand-in to compile,
+ * which makes them unbuildable here under this project's rules, and the
+ * reference ships no reproducible fixture for this path (ZLD/trans_show_*.txt
+ * lack their input).  This restatement is therefore checked by known-answer
+ * tests (planted affine maps) and is the checker for csrc/jmme_fractal.hip.
+ *
+ * Planes are 8-bit, row-major with a pitch.  Only tests/, smoke() and the
+ * bench CPU legs may load this library.
+ */
+#ifndef FRACTAL_ORACLE_H
+#define FRACTAL_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* compute_domain_Sum: sum and sum of squares of every bsx x bsy box, at every
+ * position (i, j), i < H-bsy+1, j < W-bsx+1 (out row stride W-bsx+1). */
+void fro_box_sums(const uint8_t *plane, int pitch, int W, int H, int bsx, int bsy, double *sum, double *sum2);
+
+/* compute_rms for range block (bx, by) against domain block (m, n), both
+ * bsx x bsy.  Writes alpha (scale) and beta (offset); returns rms (1e30 when
+ * the quantised parameters fall outside [MIN_ALPHA, MAX_ALPHA] x
+ * [MIN_BETA, MAX_BETA]). */
+double fro_compute_rms(const uint8_t *org, const uint8_t *ref, int pitch, int bx, int by, int m, int n, int bsx,
+                       int bsy, double *alpha, double *beta);
+
+/* full_search: (0,0) first, then rings l = 1..R in the thesis spiral, domain
+ * blocks restricted by bound_chk to the picture W x H; strict '<'.  out_x/out_y
+ * stay 0 when (0,0) wins (the caller initialises the TRANS_NODE). */
+double fro_full_search(const uint8_t *org, const uint8_t *ref, int pitch, int W, int H, int R, int bx, int by,
+                       int bsx, int bsy, int *out_x, int *out_y, double *scale, double *offset);
+
+/* batch form: req int32 [n][4] = (bx, by, bsx, bsy); out double [n][3] =
+ * (rms, scale, offset), xy int32 [n][2] */
+void fro_full_search_batch(const uint8_t *org, const uint8_t *ref, int pitch, int W, int H, int R, int n,
+                           const int32_t *req, double *out, int32_t *xy);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -176,3 +176,51 @@ def tq_quant_records(rec_in):
                                       cost.ctypes.data)
         out[i] = np.concatenate([coef, levels, runs, cost, [nz]])
     return out
+
+
+# ---- thesis fractal domain-range search (oracle/fractal_oracle.c, parity unpinned) --
+FR_SO = os.path.join(ORACLE_DIR, "build", "libfractal_oracle.so")
+_fr = None
+
+
+def load_fractal() -> ctypes.CDLL:
+    global _fr
+    if _fr is not None:
+        return _fr
+    src = os.path.join(ORACLE_DIR, "fractal_oracle.c")
+    if not os.path.exists(FR_SO) or os.path.getmtime(FR_SO) < os.path.getmtime(src):
+        subprocess.run(["make", "-s", "-C", ORACLE_DIR, "port"], check=True)
+    lib = ctypes.CDLL(FR_SO)
+    P, I, D = ctypes.c_void_p, ctypes.c_int, ctypes.c_double
+    lib.fro_box_sums.argtypes = [P, I, I, I, I, I, P, P]
+    lib.fro_compute_rms.argtypes = [P, P, I, I, I, I, I, I, I, P, P]
+    lib.fro_compute_rms.restype = D
+    lib.fro_full_search.argtypes = [P, P, I, I, I, I, I, I, I, I, P, P, P, P]
+    lib.fro_full_search.restype = D
+    lib.fro_full_search_batch.argtypes = [P, P, I, I, I, I, I, P, P, P]
+    _fr = lib
+    return lib
+
+
+def fractal_search_batch(org, ref, R, req):
+    """org/ref uint8 HxW; req int32 [n,4] (bx,by,bsx,bsy) -> (out f64 [n,3] rms/scale/offset, xy int32 [n,2])"""
+    lib = load_fractal()
+    org = np.ascontiguousarray(org, np.uint8)
+    ref = np.ascontiguousarray(ref, np.uint8)
+    req = np.ascontiguousarray(req, np.int32)
+    h, w = org.shape
+    out = np.zeros((len(req), 3), np.float64)
+    xy = np.zeros((len(req), 2), np.int32)
+    lib.fro_full_search_batch(org.ctypes.data, ref.ctypes.data, w, w, h, int(R), len(req), req.ctypes.data,
+                              out.ctypes.data, xy.ctypes.data)
+    return out, xy
+
+
+def fractal_box_sums(plane, bsx, bsy):
+    lib = load_fractal()
+    plane = np.ascontiguousarray(plane, np.uint8)
+    h, w = plane.shape
+    s = np.zeros((h - bsy + 1, w - bsx + 1), np.float64)
+    s2 = np.zeros_like(s)
+    lib.fro_box_sums(plane.ctypes.data, w, w, h, bsx, bsy, s.ctypes.data, s2.ctypes.data)
+    return s, s2
