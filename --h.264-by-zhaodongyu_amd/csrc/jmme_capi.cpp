@@ -56,6 +56,8 @@ struct jmme_ctx {
   jmme_block_res *d_out = nullptr;
   size_t cap_units = 0;
   unsigned long long *d_stamps = nullptr;    // diagnostic builds only
+  void *d_tree = nullptr;                    // fractal quadtree scratch (lists + per-level results)
+  size_t cap_tree = 0;
   size_t cap_stamps = 0;
   unsigned *d_counts = nullptr;              // [0] 32-bit items, [1] 64-bit items, [2] status
   Item *d_items = nullptr;                   // work items (one per unit x partition group)
@@ -227,6 +229,7 @@ extern "C" void jmme_destroy(jmme_ctx *ctx) {
   (void)hipFree(ctx->d_counts);
   (void)hipFree(ctx->d_items);
   (void)hipFree(ctx->d_stamps);
+  (void)hipFree(ctx->d_tree);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
   delete ctx;
@@ -712,6 +715,97 @@ extern "C" int jmme_fractal_box_sums(jmme_ctx *ctx, const uint8_t *plane, int pi
                          (double *)ds.p, (double *)ds2.p, nullptr));
   HIPCHK(hipMemcpy(sum, ds.p, (size_t)w * h * 8, hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(sum2, ds2.p, (size_t)w * h * 8, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+// fractal quadtree (encode_one_macroblock): scratch carved from
+// one ctx buffer -- counts, the three id lists, the four levels' results
+extern "C" int jmme_fractal_encode_mbs_async(jmme_ctx *ctx, const uint8_t *d_org, const uint8_t *d_ref0, int pitch,
+                                             const uint32_t *const *d_words, int n_refs, int width, int height,
+                                             int search_range, double tol_16, double tol_8, jmme_fractal_mb *d_out,
+                                             void *stream) {
+  if (!ctx) return fail("null ctx");
+  if (fractal_geom_ok(pitch, width, height)) return -1;
+  if (width % 16 || height % 16) return fail("fractal macroblock plane %dx%d: need multiples of 16", width, height);
+  if (n_refs < 1 || n_refs > JMME_FRACTAL_MAX_VIEWS) return fail("n_refs %d not in 1..%d", n_refs, JMME_FRACTAL_MAX_VIEWS);
+  if (search_range < 0) return fail("negative search range");
+  if (!d_org || !d_ref0 || !d_words || !d_out) return fail("null array");
+  for (int k = 0; k < n_refs; ++k)
+    if (!d_words[k]) return fail("null words image for view %d", k);
+  const int mbs_x = width / 16, n_mb = mbs_x * (height / 16);
+  const size_t res = sizeof(jmme_fractal_res);
+  const size_t off_list1 = 256, off_list2 = off_list1 + (size_t)n_mb * 4, off_list3 = off_list2 + (size_t)n_mb * 16;
+  const size_t off_res0 = (off_list3 + (size_t)n_mb * 16 + 255) & ~(size_t)255;
+  const size_t off_res1 = off_res0 + (size_t)n_mb * n_refs * res;
+  const size_t off_res2 = off_res1 + (size_t)n_mb * 4 * n_refs * res;
+  const size_t off_res3 = off_res2 + (size_t)n_mb * 16 * n_refs * res;
+  const size_t bytes = off_res3 + (size_t)n_mb * 16 * n_refs * res;
+  if (bytes > ctx->cap_tree) {
+    (void)hipFree(ctx->d_tree);
+    ctx->d_tree = nullptr;
+    ctx->cap_tree = 0;
+    HIPCHK(hipMalloc(&ctx->d_tree, bytes));
+    ctx->cap_tree = bytes;
+  }
+  char *base = static_cast<char *>(ctx->d_tree);
+  FractalTreeParams p{};
+  p.org = d_org;
+  p.ref0 = d_ref0;
+  p.pitch = pitch;
+  for (int k = 0; k < n_refs; ++k) p.words[k] = d_words[k];
+  p.n_refs = n_refs;
+  p.wpitch = width;
+  p.width = width;
+  p.height = height;
+  p.range = search_range;
+  p.mbs_x = mbs_x;
+  p.n_mb = n_mb;
+  // `tol*tol*no` as the thesis writes it (block_enc.c:797, 1328, 1584)
+  p.thr16 = tol_16 * tol_16 * 256;
+  p.thr8 = tol_8 * tol_8 * 64;
+  p.thr_pair = tol_8 * tol_8 * 32;
+  p.out = d_out;
+  p.count = reinterpret_cast<int *>(base);
+  p.list[1] = reinterpret_cast<int *>(base + off_list1);
+  p.list[2] = reinterpret_cast<int *>(base + off_list2);
+  p.list[3] = reinterpret_cast<int *>(base + off_list3);
+  p.res[0] = reinterpret_cast<jmme_fractal_res *>(base + off_res0);
+  p.res[1] = reinterpret_cast<jmme_fractal_res *>(base + off_res1);
+  p.res[2] = reinterpret_cast<jmme_fractal_res *>(base + off_res2);
+  p.res[3] = reinterpret_cast<jmme_fractal_res *>(base + off_res3);
+  HIPCHK(launch_fractal_tree(p, reinterpret_cast<hipStream_t>(stream)));
+  return 0;
+}
+
+extern "C" int jmme_fractal_encode_mbs(jmme_ctx *ctx, const uint8_t *org, const uint8_t *const *refs, int n_refs,
+                                       int pitch, int width, int height, int search_range, double tol_16,
+                                       double tol_8, jmme_fractal_mb *out) {
+  if (!ctx) return fail("null ctx");
+  if (fractal_geom_ok(pitch, width, height)) return -1;
+  if (width % 16 || height % 16) return fail("fractal macroblock plane %dx%d: need multiples of 16", width, height);
+  if (n_refs < 1 || n_refs > JMME_FRACTAL_MAX_VIEWS) return fail("n_refs %d not in 1..%d", n_refs, JMME_FRACTAL_MAX_VIEWS);
+  if (!org || !refs || !out) return fail("null array");
+  for (int k = 0; k < n_refs; ++k)
+    if (!refs[k]) return fail("null reference view %d", k);
+  const size_t plane = (size_t)pitch * height;
+  const int n_mb = (width / 16) * (height / 16);
+  DevBuf o, r[JMME_FRACTAL_MAX_VIEWS], w[JMME_FRACTAL_MAX_VIEWS], dout;
+  const uint32_t *words[JMME_FRACTAL_MAX_VIEWS] = {};
+  HIPCHK(o.alloc(plane));
+  HIPCHK(hipMemcpy(o.p, org, plane, hipMemcpyHostToDevice));
+  for (int k = 0; k < n_refs; ++k) {
+    HIPCHK(r[k].alloc(plane));
+    HIPCHK(w[k].alloc((size_t)width * height * 4));
+    HIPCHK(hipMemcpy(r[k].p, refs[k], plane, hipMemcpyHostToDevice));
+    if (jmme_fractal_words_async(ctx, (const uint8_t *)r[k].p, pitch, width, height, (uint32_t *)w[k].p, nullptr))
+      return -1;
+    words[k] = (const uint32_t *)w[k].p;
+  }
+  HIPCHK(dout.alloc((size_t)n_mb * sizeof(jmme_fractal_mb)));
+  if (jmme_fractal_encode_mbs_async(ctx, (const uint8_t *)o.p, (const uint8_t *)r[0].p, pitch, words, n_refs, width,
+                                    height, search_range, tol_16, tol_8, (jmme_fractal_mb *)dout.p, nullptr))
+    return -1;
+  HIPCHK(hipMemcpy(out, dout.p, (size_t)n_mb * sizeof(jmme_fractal_mb), hipMemcpyDeviceToHost));
   return 0;
 }
 

@@ -23,6 +23,9 @@
 // reference) that stays cache-resident; the range block sits in LDS and is
 // read by broadcast.
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
+
 #include "jmme.h"
 #include "jmme_fractal_internal.h"
 
@@ -227,6 +230,225 @@ __global__ __launch_bounds__(kWG) void box_vsum_kernel(const uint32_t *__restric
   sum2[(size_t)y * w + x] = (double)s2;
 }
 
+// ------------------------------------------------------------------ a17 --
+// encode_one_macroblock's quadtree (block_enc.c:508-1932) as four search
+// levels, each followed by a gate kernel that reduces over the views, decides
+// the split and appends the next level's node ids on the device (no host
+// round trip between levels).
+
+// the gate's squared correlation (block_enc.c:760-796).  The thesis sums
+// column by column (ii = x*16 + y); sR, sD are exact in any order (every
+// (R-r)^2 is a multiple of 2^-16 below 2^16, so all partial sums fit 53
+// bits), the 256 correlation terms are formed in parallel and then added in
+// ii order by one lane, so mr is bit-identical.
+__global__ __launch_bounds__(kWG) void tree_init_kernel(FractalTreeParams p) {
+#pragma clang fp contract(off)
+  __shared__ double s_t[kWaves][256];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int mb = blockIdx.x * kWaves + wave;
+  if (blockIdx.x == 0 && threadIdx.x < 4) p.count[threadIdx.x] = 0;
+  const bool valid = mb < p.n_mb;
+  if (valid) {
+    uint64_t *rec = reinterpret_cast<uint64_t *>(p.out + mb);
+    for (int i = lane; i < (int)(sizeof(jmme_fractal_mb) / 8); i += 64) rec[i] = 0;
+    const int bx = (mb % p.mbs_x) * 16, by = (mb / p.mbs_x) * 16;
+    const int x = lane >> 2, y0 = (lane & 3) * 4;     // ii = x*16 + y0 + e
+    int rv[4], dv[4], sr = 0, sd = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const size_t o = (size_t)(by + y0 + e) * p.pitch + bx + x;
+      rv[e] = p.org[o];
+      dv[e] = p.ref0[o];
+      sr += rv[e];
+      sd += dv[e];
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      sr += __shfl_xor(sr, off, 64);
+      sd += __shfl_xor(sd, off, 64);
+    }
+    const double r = (double)sr / 256, d = (double)sd / 256;
+    double sR = 0, sD = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      sR += (rv[e] - r) * (rv[e] - r);
+      sD += (dv[e] - d) * (dv[e] - d);
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      sR += __shfl_xor(sR, off, 64);
+      sD += __shfl_xor(sD, off, 64);
+    }
+    const double qR = sqrt(sR), qD = sqrt(sD);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) s_t[wave][lane * 4 + e] = ((rv[e] - r) / qR) * ((dv[e] - d) / qD);
+  }
+  __syncthreads();
+  if (valid && lane == 0) {
+    double mr = 0;
+    for (int ii = 0; ii < 256; ++ii) mr += s_t[wave][ii];
+    p.out[mb].chun = mr * mr;
+  }
+}
+
+__device__ __forceinline__ const uint32_t *view_words(const FractalTreeParams &p, int k) {
+  return k == 0 ? p.words[0] : k == 1 ? p.words[1] : k == 2 ? p.words[2] : p.words[3];
+}
+
+template <int LEVEL>
+__global__ __launch_bounds__(kWG) void tree_search_kernel(FractalTreeParams p) {
+  __shared__ uint32_t s_rng[kWaves][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  constexpr int S = LEVEL == 0 ? 1 : 4;
+  const int K = p.n_refs;
+  const int nodes = LEVEL == 0 ? p.n_mb : p.count[LEVEL];
+  const int total = nodes * S * K;
+  for (int t = blockIdx.x * kWaves + wave; t < total; t += gridDim.x * kWaves) {
+    const int k = t % K, s = (t / K) % S, i = t / (K * S);
+    const int id = LEVEL == 0 ? i : p.list[LEVEL][i];
+    FractalParams fp;
+    fp.org = p.org;
+    fp.pitch = p.pitch;
+    fp.words = view_words(p, k);
+    fp.wpitch = p.wpitch;
+    fp.width = p.width;
+    fp.height = p.height;
+    fp.range = p.range;
+    jmme_fractal_res *o = p.res[LEVEL] + t;
+    const int mb = LEVEL <= 1 ? id : id >> 2;
+    int bx = (mb % p.mbs_x) * 16, by = (mb / p.mbs_x) * 16;
+    jmme_fractal_req rq;
+    if (LEVEL == 0) {
+      rq = {(int16_t)bx, (int16_t)by, 16, 16};
+      search_one<16, 16>(fp, rq, s_rng[wave], lane, o);
+    } else if (LEVEL == 1) {
+      rq = {(int16_t)(bx + (s & 1) * 8), (int16_t)(by + (s >> 1) * 8), 8, 8};
+      search_one<8, 8>(fp, rq, s_rng[wave], lane, o);
+    } else {
+      bx += (id & 1) * 8;
+      by += ((id >> 1) & 1) * 8;
+      if (LEVEL == 3) {
+        rq = {(int16_t)(bx + (s & 1) * 4), (int16_t)(by + (s >> 1) * 4), 4, 4};
+        search_one<4, 4>(fp, rq, s_rng[wave], lane, o);
+      } else if (s < 2) {          // 8x4 pair, encode_block_rect mode 1 depth 2
+        rq = {(int16_t)bx, (int16_t)(by + 4 * s), 8, 4};
+        search_one<8, 4>(fp, rq, s_rng[wave], lane, o);
+      } else {                     // 4x8 pair, mode 2
+        rq = {(int16_t)(bx + 4 * (s - 2)), (int16_t)by, 4, 8};
+        search_one<4, 8>(fp, rq, s_rng[wave], lane, o);
+      }
+    }
+  }
+}
+
+// first strict minimum over the views (the thesis's `if (rms_rl < rms)`
+// chain); quirk4: encode_block_4 sets partition = reference = 1 when view 1
+// wins (block_enc.c:1773)
+__device__ __forceinline__ jmme_fractal_node pick_view(const jmme_fractal_res *r, int K, bool quirk4) {
+  jmme_fractal_res b = r[0];
+  int ref = 0, part = 0;
+  for (int k = 1; k < K; ++k) {
+    const jmme_fractal_res c = r[k];
+    if (c.rms < b.rms) {
+      b = c;
+      ref = k;
+      if (quirk4 && k == 1) part = 1;
+    }
+  }
+  jmme_fractal_node n;
+  n.rms = b.rms;
+  n.scale = b.scale;
+  n.offset = b.offset;
+  n.x = b.x;
+  n.y = b.y;
+  n.reference = ref;
+  n.partition = part;
+  return n;
+}
+
+// wave-aggregated append; every lane of the wave calls it
+__device__ __forceinline__ int append(int *count, bool pred) {
+  const unsigned long long m = __ballot(pred);
+  if (!m) return -1;
+  const int lane = threadIdx.x & 63;
+  const int leader = __ffsll((long long)m) - 1;
+  int base = 0;
+  if (lane == leader) base = atomicAdd(count, __popcll(m));
+  base = __shfl(base, leader, 64);
+  return base + __popcll(m & ((1ull << lane) - 1));
+}
+
+// level 0 -> 1: encode_one_macroblock's gate (block_enc.c:797)
+__global__ __launch_bounds__(kWG) void tree_gate0_kernel(FractalTreeParams p) {
+  const int mb = blockIdx.x * kWG + threadIdx.x;
+  bool split = false;
+  if (mb < p.n_mb) {
+    jmme_fractal_node n = pick_view(p.res[0] + (size_t)mb * p.n_refs, p.n_refs, false);
+    const double chun = p.out[mb].chun;
+    split = chun <= 1 && chun >= 0.9 && n.rms > p.thr16;
+    if (split) n.partition = 3;
+    p.out[mb].mb = n;
+  }
+  const int idx = append(p.count + 1, split);
+  if (split) p.list[1][idx] = mb;
+}
+
+// level 1 -> 2: encode_block_8's test (block_enc.c:1584)
+__global__ __launch_bounds__(kWG) void tree_gate1_kernel(FractalTreeParams p) {
+  const int t = blockIdx.x * kWG + threadIdx.x;
+  bool fail = false;
+  int b8 = 0;
+  if (t < p.count[1] * 4) {
+    const int mb = p.list[1][t >> 2], q = t & 3;
+    const jmme_fractal_node n = pick_view(p.res[1] + (size_t)t * p.n_refs, p.n_refs, false);
+    p.out[mb].b8[q] = n;
+    fail = n.rms > p.thr8;
+    b8 = mb * 4 + q;
+  }
+  const int idx = append(p.count + 2, fail);
+  if (fail) p.list[2][idx] = b8;
+}
+
+// level 2 -> 3: the 8x4 pair, else the 4x8 pair (block_enc.c:1586-1632; a
+// pair stops at its first unmatched half, which leaves the same outcome)
+__global__ __launch_bounds__(kWG) void tree_gate2_kernel(FractalTreeParams p) {
+  const int t = blockIdx.x * kWG + threadIdx.x;
+  bool quad = false;
+  int b8 = 0;
+  if (t < p.count[2]) {
+    b8 = p.list[2][t];
+    jmme_fractal_mb *m = p.out + (b8 >> 2);
+    const int q = b8 & 3;
+    jmme_fractal_node h[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) h[s] = pick_view(p.res[2] + ((size_t)t * 4 + s) * p.n_refs, p.n_refs, false);
+    const bool m1 = !(h[0].rms > p.thr_pair) && !(h[1].rms > p.thr_pair);
+    const bool m2 = !(h[2].rms > p.thr_pair) && !(h[3].rms > p.thr_pair);
+    if (m1) {
+      m->sub[q][0] = h[0];
+      m->sub[q][1] = h[1];
+      m->b8[q].partition = 1;
+    } else if (m2) {
+      m->sub[q][0] = h[2];
+      m->sub[q][1] = h[3];
+      m->b8[q].partition = 2;
+    } else {
+      m->b8[q].partition = 3;
+      quad = true;
+    }
+  }
+  const int idx = append(p.count + 3, quad);
+  if (quad) p.list[3][idx] = b8;
+}
+
+// level 3: the four 4x4 (encode_block_4)
+__global__ __launch_bounds__(kWG) void tree_gate3_kernel(FractalTreeParams p) {
+  const int t = blockIdx.x * kWG + threadIdx.x;
+  if (t >= p.count[3] * 4) return;
+  const int b8 = p.list[3][t >> 2], s = t & 3;
+  p.out[b8 >> 2].sub[b8 & 3][s] = pick_view(p.res[3] + (size_t)t * p.n_refs, p.n_refs, true);
+}
+
 }  // namespace
 
 hipError_t launch_fractal_words(const uint8_t *ref, int pitch, int W, int H, uint32_t *words, int wpitch,
@@ -249,6 +471,22 @@ hipError_t launch_box_sums(const uint8_t *p, int pitch, int W, int H, int bsx, i
   hipLaunchKernelGGL(box_hsum_kernel, dim3((w + kWG - 1) / kWG, H), dim3(kWG), 0, s, p, pitch, W, H, bsx, hs, hs2);
   hipLaunchKernelGGL(box_vsum_kernel, dim3((w + kWG - 1) / kWG, H - bsy + 1), dim3(kWG), 0, s, hs, hs2, w, H, bsy,
                      sum, sum2);
+  return hipGetLastError();
+}
+
+hipError_t launch_fractal_tree(const FractalTreeParams &p, hipStream_t s) {
+  const int n = p.n_mb, K = p.n_refs;
+  auto waves = [](long long w) { return (int)std::min<long long>(std::max<long long>((w + kWaves - 1) / kWaves, 1), 4096); };
+  auto threads = [](long long t) { return (int)std::max<long long>((t + kWG - 1) / kWG, 1); };
+  hipLaunchKernelGGL(tree_init_kernel, dim3((n + kWaves - 1) / kWaves), dim3(kWG), 0, s, p);
+  hipLaunchKernelGGL(tree_search_kernel<0>, dim3(waves((long long)n * K)), dim3(kWG), 0, s, p);
+  hipLaunchKernelGGL(tree_gate0_kernel, dim3(threads(n)), dim3(kWG), 0, s, p);
+  hipLaunchKernelGGL(tree_search_kernel<1>, dim3(waves((long long)n * 4 * K)), dim3(kWG), 0, s, p);
+  hipLaunchKernelGGL(tree_gate1_kernel, dim3(threads(4LL * n)), dim3(kWG), 0, s, p);
+  hipLaunchKernelGGL(tree_search_kernel<2>, dim3(waves((long long)n * 16 * K)), dim3(kWG), 0, s, p);
+  hipLaunchKernelGGL(tree_gate2_kernel, dim3(threads(4LL * n)), dim3(kWG), 0, s, p);
+  hipLaunchKernelGGL(tree_search_kernel<3>, dim3(waves((long long)n * 16 * K)), dim3(kWG), 0, s, p);
+  hipLaunchKernelGGL(tree_gate3_kernel, dim3(threads(16LL * n)), dim3(kWG), 0, s, p);
   return hipGetLastError();
 }
 

@@ -19,6 +19,27 @@ struct FractalParams {
   int n;
 };
 
+// quadtree encoder (encode_one_macroblock): level 0 = 16x16 of
+// every macroblock, 1 = the four 8x8 of split macroblocks, 2 = the 8x4 / 4x8
+// pairs of unmatched 8x8, 3 = the four 4x4 of 8x8 whose pairs failed.  Level
+// L >= 1 works on the ids in list[L] (count[L] of them), appended on the device
+// by the gate of level L-1; res[L] holds one search result per (node, block,
+// view) in that order.
+struct FractalTreeParams {
+  const uint8_t *org, *ref0;   // range plane, view 0 (the gate's co-located block)
+  int pitch;
+  const uint32_t *words[JMME_FRACTAL_MAX_VIEWS];
+  int n_refs, wpitch;
+  int width, height, range, mbs_x, n_mb;
+  double thr16, thr8, thr_pair;   // tol_16^2*256, tol_8^2*64, tol_8^2*32 (thesis operand order)
+  jmme_fractal_mb *out;
+  jmme_fractal_res *res[4];
+  int *list[4];                   // list[1..3]
+  int *count;                     // count[1..3] (count[0] unused)
+};
+
+hipError_t launch_fractal_tree(const FractalTreeParams &p, hipStream_t s);
+
 hipError_t launch_fractal_words(const uint8_t *ref, int pitch, int W, int H, uint32_t *words, int wpitch,
                                 hipStream_t s);
 hipError_t launch_fractal_search(const FractalParams &p, hipStream_t s);

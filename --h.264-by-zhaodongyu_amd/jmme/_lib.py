@@ -30,6 +30,11 @@ MB_REQ = np.dtype([("mb_x", "<i2"), ("mb_y", "<i2"), ("list", "<i2"), ("ref_idx"
 BLOCK_RES = np.dtype([("mv_x", "<i2"), ("mv_y", "<i2"), ("reserved", "<i4"), ("cost", "<i8")])
 FRACTAL_REQ = np.dtype([("block_x", "<i2"), ("block_y", "<i2"), ("bsx", "<i2"), ("bsy", "<i2")])
 FRACTAL_RES = np.dtype([("rms", "<f8"), ("scale", "<f8"), ("offset", "<f8"), ("x", "<i4"), ("y", "<i4")])
+FRACTAL_NODE = np.dtype([("rms", "<f8"), ("scale", "<f8"), ("offset", "<f8"), ("x", "<i4"), ("y", "<i4"),
+                         ("reference", "<i4"), ("partition", "<i4")])
+FRACTAL_MB = np.dtype([("mb", FRACTAL_NODE), ("b8", FRACTAL_NODE, (4,)), ("sub", FRACTAL_NODE, (4, 4)),
+                       ("chun", "<f8")])
+FRACTAL_MAX_VIEWS = 4
 QUANT4x4_PARAMS = np.dtype([("scale", "<i4", (16,)), ("offset", "<i4", (16,)), ("inv_scale", "<i4", (16,)),
                             ("qp_per", "<i4"), ("is_cavlc", "<i4"), ("scan", "u1", (16, 2)), ("c_cost", "u1", (16,))])
 TRANSFORM_OPS = {"forward4x4": (0, 16, 16), "inverse4x4": (1, 16, 16), "hadamard4x4": (2, 16, 16),
@@ -38,6 +43,7 @@ TRANSFORM_OPS = {"forward4x4": (0, 16, 16), "inverse4x4": (1, 16, 16), "hadamard
                  "inverse8x8": (9, 64, 64)}   # name -> (jmme_transform_op, in elems, out elems)
 assert BLOCK_REQ.itemsize == 16 and MB_REQ.itemsize == 688 and BLOCK_RES.itemsize == 16
 assert QUANT4x4_PARAMS.itemsize == 248 and FRACTAL_REQ.itemsize == 8 and FRACTAL_RES.itemsize == 32
+assert FRACTAL_NODE.itemsize == 40 and FRACTAL_MB.itemsize == 848
 
 CONFIG_FIELDS = ["SourceWidth", "SourceHeight", "SearchMode", "SearchRange", "NumberReferenceFrames",
                  "DisableSubpelME", "RDOptimization", "MEDistortionFPel", "MDDistortion", "EPZSSubPelGrid",
@@ -70,7 +76,7 @@ def lib() -> ctypes.CDLL:
     if not os.path.exists(LIB_PATH):
         raise JmmeError(f"{LIB_PATH} not built: run __graft_entry__.build() (make -C <pkg>)")
     L = ctypes.CDLL(LIB_PATH)
-    P, I, V = ctypes.c_void_p, ctypes.c_int, None
+    P, I, D, V = ctypes.c_void_p, ctypes.c_int, ctypes.c_double, None
     sig = {
         "jmme_config_default": (I, [P]),
         "jmme_config_parse": (I, [P, ctypes.c_char_p, I, P]),
@@ -97,6 +103,8 @@ def lib() -> ctypes.CDLL:
         "jmme_fractal_words_async": (I, [P, P, I, I, I, P, P]),
         "jmme_fractal_search_async": (I, [P, P, I, P, I, I, I, P, I, P, P]),
         "jmme_fractal_box_sums": (I, [P, P, I, I, I, I, I, P, P]),
+        "jmme_fractal_encode_mbs": (I, [P, P, P, I, I, I, I, I, D, D, P]),
+        "jmme_fractal_encode_mbs_async": (I, [P, P, P, I, P, I, I, I, I, D, D, P, P]),
         "jmme_quant4x4_async": (I, [P, P, P, P, P, P, P, P, I, P]),
         "jmme_spiral_index": (I, [I, I]),
         "jmme_spiral_offset": (V, [I, P, P]),

@@ -198,6 +198,28 @@ class MotionEstimator:
         check(lib().jmme_fractal_box_sums(self._ctx, ptr(plane), w, w, h, int(bsx), int(bsy), ptr(s), ptr(s2)))
         return s, s2
 
+    def fractal_encode_mbs(self, org: np.ndarray, refs, search_range: int, tol_16: float = 8.0,
+                           tol_8: float = 5.0) -> np.ndarray:
+        """encode_one_macroblock (ZL/src/block_enc.c:508) for every macroblock of org against the
+        reference views refs (view 0 first) -> FRACTAL_MB[(W/16)*(H/16)], raster order."""
+        org = np.ascontiguousarray(org, np.uint8)
+        refs = [np.ascontiguousarray(r, np.uint8) for r in refs]
+        h, w = org.shape
+        if any(r.shape != org.shape for r in refs):
+            raise ValueError("reference views must match the range plane's shape")
+        ptrs = (ctypes.c_void_p * len(refs))(*[ptr(r) for r in refs])
+        out = np.zeros((w // 16) * (h // 16), _lib.FRACTAL_MB)
+        check(lib().jmme_fractal_encode_mbs(self._ctx, ptr(org), ptrs, len(refs), w, w, h, int(search_range),
+                                            float(tol_16), float(tol_8), ptr(out)))
+        return out
+
+    def fractal_encode_mbs_async(self, d_org: int, d_ref0: int, pitch: int, d_words, width: int, height: int,
+                                 search_range: int, tol_16: float, tol_8: float, d_out: int, stream: int = 0) -> None:
+        """device form: d_words = list of per-view words images (fractal_words_async)."""
+        ptrs = (ctypes.c_void_p * len(d_words))(*d_words)
+        check(lib().jmme_fractal_encode_mbs_async(self._ctx, d_org, d_ref0, pitch, ptrs, len(d_words), width, height,
+                                                  int(search_range), float(tol_16), float(tol_8), d_out, stream))
+
     def fast_full_search_block(self, list_idx, ref_idx, pos_x, pos_y, blocktype, pred, search_center,
                                surface_range, block_range, rdopt, lambda_factor, min_mcost=_lib.DISTBLK_MAX):
         """fast_full_search_motion_estimation's contract for one partition (JM me_fullfast.c:618-689)."""

@@ -267,6 +267,57 @@ int jmme_fractal_search_async(jmme_ctx *ctx, const uint8_t *d_org, int pitch, co
 int jmme_fractal_box_sums(jmme_ctx *ctx, const uint8_t *plane, int pitch, int width, int height, int bsx, int bsy,
                           double *sum, double *sum2);
 
+/* ---- Fractal macroblock encoder: the quadtree gate ------
+ * encode_one_macroblock (ZL/src/block_enc.c:508-1050) with encode_block_rect
+ * / _8 / _4 (block_enc.c:1072-1932) for every 16x16 macroblock of a plane, in
+ * the configuration the thesis encodes its centre view with: search_mode 0
+ * (full_search), one region (num_regions 1), currentVideo 'C'.  Each tree
+ * level searches reference view 0 (the view's own reference frame) and then
+ * views 1..n_refs-1 (the thesis's H, M, N) and keeps the first strict minimum;
+ * `reference` is that view's index.
+ *   16x16 splits when 0.9 <= chun <= 1 and rms > tol_16^2 * 256, chun being
+ *   the squared correlation of the range block with the co-located block of
+ *   view 0; then every 8x8 is searched (the thesis's 16x8 / 8x16 attempt at
+ *   this level never ends the mode loop, block_enc.c:798-855, so it is
+ *   overwritten and not run);
+ *   8x8 with rms > tol_8^2 * 64 tries the 8x4 pair (partition 1), then the
+ *   4x8 pair (partition 2), a pair matching when neither half has rms >
+ *   tol_8^2 * 32; otherwise four 4x4 (partition 3);
+ *   a 4x4 node gets partition 1 when view 1 beat view 0 (block_enc.c:1773).
+ * Output nodes are bit-identical to the thesis's TRANS_NODE values (x, y,
+ * scale, offset, reference, partition) plus the rms the node's search
+ * returned; nodes the tree does not reach are zero (a fresh tree). */
+#define JMME_FRACTAL_MAX_VIEWS 4
+
+typedef struct jmme_fractal_node {
+  double rms, scale, offset;
+  int32_t x, y;
+  int32_t reference;          /* winning view, 0 .. n_refs-1 */
+  int32_t partition;          /* 0 leaf; 1 16x8/8x4 pair; 2 8x16/4x8 pair; 3 quadrants */
+} jmme_fractal_node;          /* 40 bytes */
+
+typedef struct jmme_fractal_mb {
+  jmme_fractal_node mb;       /* trans[0][CurMb] */
+  jmme_fractal_node b8[4];    /* its next[0..3] (raster order) when mb.partition == 3 */
+  jmme_fractal_node sub[4][4];/* b8[q].next[0..1] (pairs) or [0..3] (4x4, raster) */
+  double chun;                /* the 16x16 gate's squared correlation (NaN for a flat block) */
+} jmme_fractal_mb;            /* 848 bytes */
+
+/* host planes: org and refs[0..n_refs-1], all width x height with rows pitch
+ * bytes apart; width, height multiples of 16; out[(width/16)*(height/16)]
+ * in raster macroblock order */
+int jmme_fractal_encode_mbs(jmme_ctx *ctx, const uint8_t *org, const uint8_t *const *refs, int n_refs, int pitch,
+                            int width, int height, int search_range, double tol_16, double tol_8,
+                            jmme_fractal_mb *out);
+/* device form: d_ref0 = view 0's plane (the gate's co-located block),
+ * d_words[k] = view k's words image (jmme_fractal_words_async); all work is
+ * queued on `stream` with no host synchronisation (the tree levels size
+ * themselves on the device) */
+int jmme_fractal_encode_mbs_async(jmme_ctx *ctx, const uint8_t *d_org, const uint8_t *d_ref0, int pitch,
+                                  const uint32_t *const *d_words, int n_refs, int width, int height,
+                                  int search_range, double tol_16, double tol_8, jmme_fractal_mb *d_out,
+                                  void *stream);
+
 /* ---- timing of the last jmme_search_mbs* launch (HIP events on its stream) */
 float jmme_last_kernel_ms(jmme_ctx *ctx);
 

@@ -7,6 +7,9 @@
  */
 #include "fractal_oracle.h"
 
+#include <math.h>
+#include <string.h>
+
 #define MIN_ALPHA (-2.35)   /* ZL/inc/defines_enc.h:19-22 */
 #define MAX_ALPHA 4.0
 #define MIN_BETA (-60)
@@ -131,5 +134,163 @@ void fro_full_search_batch(const uint8_t *org, const uint8_t *ref, int pitch, in
     out[3 * t + 2] = o;
     xy[2 * t] = x;
     xy[2 * t + 1] = y;
+  }
+}
+
+/* ------------------------------------------------------------------ a17 --
+ * encode_one_macroblock and the block encoders it calls, restated for
+ * search_mode 0, num_regions 1 and the C view (currentVideo == 'C'), whose
+ * every level runs full_search on its own reference and then on the H, M, N
+ * views, keeping the first strict minimum (block_enc.c:563-700, 1131-1250,
+ * 1396-1510, 1730-1845). */
+
+typedef struct tree_ctx {
+  const uint8_t *org;
+  const uint8_t *const *refs;
+  int n_refs, pitch, W, H, R;
+  double tol_16, tol_8;
+} tree_ctx;
+
+/* full_search over every reference in view order; quirk4: encode_block_4
+ * writes `trans->partition = trans->reference = 1` when the H view wins
+ * (block_enc.c:1773), a partition that later views do not reset */
+static double search_views(const tree_ctx *c, int bx, int by, int bsx, int bsy, fro_node *t, int quirk4)
+{
+  int k, x, y;
+  double s, o, rl, rms;
+  rms = fro_full_search(c->org, c->refs[0], c->pitch, c->W, c->H, c->R, bx, by, bsx, bsy, &x, &y, &s, &o);
+  t->x = x;
+  t->y = y;
+  t->scale = s;
+  t->offset = o;
+  t->reference = 0;
+  for (k = 1; k < c->n_refs; k++) {
+    rl = fro_full_search(c->org, c->refs[k], c->pitch, c->W, c->H, c->R, bx, by, bsx, bsy, &x, &y, &s, &o);
+    if (rl < rms) {
+      rms = rl;
+      t->x = x;
+      t->y = y;
+      t->scale = s;
+      t->offset = o;
+      t->reference = k;
+      if (quirk4 && k == 1) t->partition = 1;
+    }
+  }
+  t->rms = rms;
+  return rms;
+}
+
+/* encode_block_rect, block_enc.c:1072-1336: half `half` of mode 1 (16x8 /
+ * 8x4) or mode 2 (8x16 / 4x8) at depth 1 or 2; matched when rms is not above
+ * tol_8^2 * no (no = the block's pel count, the global compute_rms sets) */
+static int encode_rect(const tree_ctx *c, int bx, int by, int half, fro_node *t, int mode, int depth)
+{
+  int bsx, bsy;
+  if (mode == 1) {
+    bsx = 16 / depth;
+    bsy = 8 / depth;
+    by += bsy * half;
+  } else {
+    bsx = 8 / depth;
+    bsy = 16 / depth;
+    bx += bsx * half;
+  }
+  return !(search_views(c, bx, by, bsx, bsy, t, 0) > c->tol_8 * c->tol_8 * (bsx * bsy));
+}
+
+/* encode_block_4, block_enc.c:1676-1932 */
+static void encode_b4(const tree_ctx *c, int bx, int by, fro_node *t)
+{
+  t->x = t->y = 0;
+  search_views(c, bx, by, 4, 4, t, 1);
+}
+
+/* encode_block_8, block_enc.c:1337-1675: 8x8; if unmatched (rms >
+ * tol_8^2 * 64) the 8x4 pair, then the 4x8 pair (a pair stops at its first
+ * unmatched half), else four 4x4 */
+static void encode_b8(const tree_ctx *c, int bx, int by, fro_node *t, fro_node *next)
+{
+  int mode, i, j, ok;
+  t->partition = 0;
+  t->reference = 0;
+  t->x = 0;
+  t->y = 0;
+  if (search_views(c, bx, by, 8, 8, t, 0) > c->tol_8 * c->tol_8 * 64) {
+    for (mode = 1; mode < 3; mode++) {
+      ok = 0;
+      t->partition = mode;
+      for (i = 0; i < 2; i++) {
+        next[i].x = 0;
+        next[i].y = 0;
+        if (!encode_rect(c, bx, by, i, &next[i], mode, 2)) break;
+        ok++;
+      }
+      if (ok == 2) break;
+    }
+    if (mode == 3) {
+      t->partition = 3;
+      for (i = 0; i < 2; i++)
+        for (j = 0; j < 2; j++) encode_b4(c, bx + j * 4, by + i * 4, &next[i * 2 + j]);
+    }
+  }
+}
+
+/* the 16x16 gate's chun: squared correlation of the range block with the
+ * co-located block of the own reference, summed column by column
+ * (block_enc.c:760-796) */
+static double mb_chun(const tree_ctx *c, int bx, int by)
+{
+  double R[256], D[256], sumR = 0, sumD = 0, r, d, sR = 0, sD = 0, mr = 0;
+  int i, j, ii = 0;
+  for (j = bx; j < bx + 16; j++)
+    for (i = by; i < by + 16; i++) {
+      R[ii] = c->org[i * c->pitch + j];
+      D[ii] = c->refs[0][i * c->pitch + j];
+      sumR += R[ii];
+      sumD += D[ii];
+      ii++;
+    }
+  r = sumR / 256;
+  d = sumD / 256;
+  for (ii = 0; ii < 256; ii++) {
+    sR += (R[ii] - r) * (R[ii] - r);
+    sD += (D[ii] - d) * (D[ii] - d);
+  }
+  for (ii = 0; ii < 256; ii++) mr += ((R[ii] - r) / (sqrt(sR))) * ((D[ii] - d) / (sqrt(sD)));
+  return mr * mr;
+}
+
+/* encode_one_macroblock, block_enc.c:508-1050 (region 0 branch, k == 0).
+ * Split when 0.9 <= chun <= 1 and rms > tol_16^2 * 256.  Its 16x8 / 8x16
+ * loop (block_enc.c:798-855) never leaves early (a matched pair does not set
+ * mode = 4), so the 8x8 split always follows and overwrites the pair's
+ * next[0..1] and stored vectors: the pair searches are dead stores and are
+ * not restated. */
+void fro_encode_mbs(const uint8_t *org, const uint8_t *const *refs, int n_refs, int pitch, int W, int H, int R,
+                    double tol_16, double tol_8, fro_mb *out)
+{
+  tree_ctx c;
+  int mbs_x = W / 16, n_mb = mbs_x * (H / 16), mb, i, j;
+  c.org = org;
+  c.refs = refs;
+  c.n_refs = n_refs;
+  c.pitch = pitch;
+  c.W = W;
+  c.H = H;
+  c.R = R;
+  c.tol_16 = tol_16;
+  c.tol_8 = tol_8;
+  for (mb = 0; mb < n_mb; mb++) {
+    fro_mb *m = &out[mb];
+    const int bx = (mb % mbs_x) * 16, by = (mb / mbs_x) * 16;
+    double rms;
+    memset(m, 0, sizeof(*m));
+    rms = search_views(&c, bx, by, 16, 16, &m->mb, 0);
+    m->chun = mb_chun(&c, bx, by);
+    if (m->chun <= 1 && m->chun >= 0.9 && rms > tol_16 * tol_16 * 256) {
+      m->mb.partition = 3;
+      for (i = 0; i < 2; i++)
+        for (j = 0; j < 2; j++) encode_b8(&c, bx + j * 8, by + i * 8, &m->b8[i * 2 + j], m->sub[i * 2 + j]);
+    }
   }
 }

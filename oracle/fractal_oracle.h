@@ -5,6 +5,8 @@
  *   compute_rms, compute_rdSum, QUAN_A       ZL/src/compute.c:6-215,
  *                                            ZL/inc/defines_enc.h:19-22,591-601
  *   full_search, bound_chk                   ZL/src/block_enc.c:1933-1977, 2894-2919
+ *   encode_one_macroblock quadtree gating    ZL/src/block_enc.c:508-1050 (row a17),
+ *     encode_block_rect / _8 / _4            ZL/src/block_enc.c:1072-1932
  * (ZL = /root/reference/2.论文程序/ZhangLing_Yu_version1/H264Fractal).
  *
  * PARITY UNPINNED: the thesis sources need a windows.h stand-in to compile,
@@ -45,6 +47,31 @@ double fro_full_search(const uint8_t *org, const uint8_t *ref, int pitch, int W,
  * (rms, scale, offset), xy int32 [n][2] */
 void fro_full_search_batch(const uint8_t *org, const uint8_t *ref, int pitch, int W, int H, int R, int n,
                            const int32_t *req, double *out, int32_t *xy);
+
+/* One TRANS_NODE of the fractal tree (ZL/inc/defines_enc.h TRANS_NODE fields
+ * x, y, scale, offset, reference, partition) plus the rms its search returned.
+ * Same layout as jmme_fractal_node in include/jmme.h. */
+typedef struct fro_node {
+  double rms, scale, offset;
+  int32_t x, y, reference, partition;
+} fro_node;                                  /* 40 bytes */
+
+/* one macroblock's tree: mb = trans[0][CurMb]; b8[q] = its next[q] (when
+ * mb.partition == 3); sub[q][c] = b8[q].next[c] (2 rect halves for partition
+ * 1/2, 4 4x4 blocks for partition 3); unused nodes are zero.  chun is the
+ * squared correlation the 16x16 gate reads.  Same layout as jmme_fractal_mb. */
+typedef struct fro_mb {
+  fro_node mb, b8[4], sub[4][4];
+  double chun;
+} fro_mb;                                    /* 848 bytes */
+
+/* encode_one_macroblock for every 16x16 macroblock of a W x H plane (raster
+ * order, W and H multiples of 16), search_mode 0 (full search), one region
+ * (num_regions == 1), the C view with n_refs reference planes searched in
+ * order (refs[0] = its own reference frame, then the H, M, N views:
+ * block_enc.c:563-700), tolerances tol_16 / tol_8 as in the config file. */
+void fro_encode_mbs(const uint8_t *org, const uint8_t *const *refs, int n_refs, int pitch, int W, int H, int R,
+                    double tol_16, double tol_8, fro_mb *out);
 
 #ifdef __cplusplus
 }

@@ -224,3 +224,25 @@ def fractal_box_sums(plane, bsx, bsy):
     s2 = np.zeros_like(s)
     lib.fro_box_sums(plane.ctypes.data, w, w, h, bsx, bsy, s.ctypes.data, s2.ctypes.data)
     return s, s2
+
+
+FRO_NODE = np.dtype([("rms", "<f8"), ("scale", "<f8"), ("offset", "<f8"), ("x", "<i4"), ("y", "<i4"),
+                     ("reference", "<i4"), ("partition", "<i4")])
+FRO_MB = np.dtype([("mb", FRO_NODE), ("b8", FRO_NODE, (4,)), ("sub", FRO_NODE, (4, 4)), ("chun", "<f8")])
+assert FRO_NODE.itemsize == 40 and FRO_MB.itemsize == 848
+
+
+def fractal_encode_mbs(org, refs, R, tol_16, tol_8):
+    """encode_one_macroblock for every macroblock of org (H x W, multiples of
+    16) against the reference views refs (list of H x W uint8) -> FRO_MB [n_mb]"""
+    lib = load_fractal()
+    org = np.ascontiguousarray(org, np.uint8)
+    refs = [np.ascontiguousarray(r, np.uint8) for r in refs]
+    h, w = org.shape
+    ptrs = (ctypes.c_void_p * len(refs))(*[r.ctypes.data for r in refs])
+    out = np.zeros((w // 16) * (h // 16), FRO_MB)
+    lib.fro_encode_mbs.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                   ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_void_p]
+    lib.fro_encode_mbs(org.ctypes.data, ptrs, len(refs), w, w, h, int(R), float(tol_16), float(tol_8),
+                       out.ctypes.data)
+    return out

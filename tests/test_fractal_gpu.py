@@ -99,3 +99,69 @@ def test_rejects_bad_requests(me):
     for bad in [(0, 0, 4, 16), (2, 0, 4, 4), (28, 0, 8, 8)]:
         with pytest.raises(JmmeError):
             me.fractal_search(org, ref, 4, np.array([bad], FRACTAL_REQ))
+
+
+# ---- a17: the macroblock quadtree (jmme_fractal_encode_mbs) vs fro_encode_mbs --
+def _tree_check(got, exp):
+    """bit-identical records; the chun of a flat block is NaN on both sides
+    (its payload differs between x86 and the GPU, so NaNs compare as NaNs)"""
+    assert got.dtype.itemsize == exp.dtype.itemsize == 848
+    g, e = got.copy(), exp.copy()
+    gn, en = np.isnan(g["chun"]), np.isnan(e["chun"])
+    assert np.array_equal(gn, en), np.nonzero(gn != en)
+    g["chun"][gn] = 0
+    e["chun"][en] = 0
+    gb = g.view(np.uint8).reshape(len(g), -1)
+    eb = e.view(np.uint8).reshape(len(e), -1)
+    bad = np.nonzero((gb != eb).any(1))[0]
+    assert len(bad) == 0, (len(bad), [(int(i), np.nonzero(gb[i] != eb[i])[0][:8].tolist(), got[i]["mb"].tolist(),
+                                       exp[i]["mb"].tolist(), got[i]["chun"], exp[i]["chun"]) for i in bad[:3]])
+
+
+@pytest.mark.parametrize("seed,K,R,tols", [(0, 1, 7, (8.0, 5.0)), (1, 2, 4, (4.0, 5.0)), (2, 4, 3, (2.0, 4.0)),
+                                           (7, 3, 7, (4.0, 3.0)), (2, 1, 0, (3.0, 5.0))])
+def test_tree_vs_oracle(me, seed, K, R, tols):
+    from fractal_scenes import gate_scene
+    org, refs = gate_scene(176, 144, seed, K, scale=6)
+    got = me.fractal_encode_mbs(org, refs, R, *tols)
+    exp = ol.fractal_encode_mbs(org, refs, R, *tols)
+    assert (exp["mb"]["partition"] == 3).any()
+    _tree_check(got, exp)
+
+
+def test_tree_cif_chroma_and_luma(me):
+    """the thesis's frame loop: CIF luma (396 MBs) and a chroma plane (99 MBs)"""
+    from fractal_scenes import gate_scene
+    for w, h, seed in [(352, 288, 11), (176, 144, 12)]:
+        org, refs = gate_scene(w, h, seed, 4, scale=6)
+        _tree_check(me.fractal_encode_mbs(org, refs, 7, 4.0, 5.0), ol.fractal_encode_mbs(org, refs, 7, 4.0, 5.0))
+
+
+def test_tree_async_device_form(me, gpu):
+    import torch
+    from jmme import FRACTAL_MB
+    from fractal_scenes import gate_scene
+    org, refs = gate_scene(128, 96, 2, 2, scale=6)
+    h, w = org.shape
+    d_org = torch.from_numpy(org).to(gpu)
+    d_refs = [torch.from_numpy(r).to(gpu) for r in refs]
+    d_words = [torch.empty(h * w, dtype=torch.int32, device=gpu) for _ in refs]
+    d_out = torch.zeros(len(org.ravel()) // 256 * FRACTAL_MB.itemsize, dtype=torch.uint8, device=gpu)
+    stream = torch.cuda.current_stream().cuda_stream
+    for r, wd in zip(d_refs, d_words):
+        me.fractal_words_async(r.data_ptr(), w, w, h, wd.data_ptr(), stream)
+    me.fractal_encode_mbs_async(d_org.data_ptr(), d_refs[0].data_ptr(), w, [wd.data_ptr() for wd in d_words], w, h,
+                                5, 4.0, 5.0, d_out.data_ptr(), stream)
+    torch.cuda.synchronize()
+    got = d_out.cpu().numpy().view(FRACTAL_MB)
+    _tree_check(got, ol.fractal_encode_mbs(org, refs, 5, 4.0, 5.0))
+
+
+def test_tree_rejects_bad_geometry(me):
+    from jmme import JmmeError
+    org = np.zeros((40, 48), np.uint8)
+    with pytest.raises(JmmeError):
+        me.fractal_encode_mbs(org, [org], 4)           # 40 not a multiple of 16
+    org = np.zeros((32, 32), np.uint8)
+    with pytest.raises(JmmeError):
+        me.fractal_encode_mbs(org, [org] * 5, 4)       # more views than the thesis has

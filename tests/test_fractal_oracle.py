@@ -97,3 +97,136 @@ def test_box_sums_are_exact_integer_sums():
     ref = np.lib.stride_tricks.sliding_window_view(p.astype(np.int64), (4, 4))
     np.testing.assert_array_equal(s, ref.sum((2, 3)))
     np.testing.assert_array_equal(s2, (ref ** 2).sum((2, 3)))
+
+
+# ---- a17: encode_one_macroblock quadtree gate (fro_encode_mbs) ----------------
+import math  # noqa: E402
+
+from fractal_scenes import gate_scene  # noqa: E402
+
+
+def _chun_py(org, ref, bx, by):
+    """block_enc.c:760-796 in plain Python floats (IEEE double, same order)"""
+    R = [float(org[i, j]) for j in range(bx, bx + 16) for i in range(by, by + 16)]
+    D = [float(ref[i, j]) for j in range(bx, bx + 16) for i in range(by, by + 16)]
+    r, d = sum(R) / 256, sum(D) / 256
+    sR = sD = 0.0
+    for a, b in zip(R, D):
+        sR += (a - r) * (a - r)
+        sD += (b - d) * (b - d)
+    mr = 0.0
+    for a, b in zip(R, D):
+        try:
+            mr += ((a - r) / math.sqrt(sR)) * ((b - d) / math.sqrt(sD))
+        except ZeroDivisionError:
+            mr = math.nan
+    return mr * mr
+
+
+def _search(org, refs, R, bx, by, bsx, bsy, quirk4=False):
+    """all views, first strict minimum -> (rms, scale, offset, x, y, reference, partition)"""
+    best = None
+    part = 0
+    for k, ref in enumerate(refs):
+        out, xy = ol.fractal_search_batch(org, ref, R, np.array([[bx, by, bsx, bsy]], np.int32))
+        cand = (out[0, 0], out[0, 1], out[0, 2], int(xy[0, 0]), int(xy[0, 1]), k)
+        if best is None or cand[0] < best[0]:
+            best = cand
+            if quirk4 and k == 1:
+                part = 1
+    return best + (part,)
+
+
+def _tree_py(org, refs, R, tol16, tol8):
+    """a second, independent statement of the gate in Python over fro_full_search"""
+    h, w = org.shape
+    recs = []
+    for by in range(0, h, 16):
+        for bx in range(0, w, 16):
+            rec = {"mb": _search(org, refs, R, bx, by, 16, 16), "b8": {}, "sub": {}}
+            chun = _chun_py(org, refs[0], bx, by)
+            rec["chun"] = chun
+            if 0.9 <= chun <= 1 and rec["mb"][0] > tol16 * tol16 * 256:
+                rec["mb"] = rec["mb"][:6] + (3,)
+                for q in range(4):
+                    x8, y8 = bx + (q & 1) * 8, by + (q >> 1) * 8
+                    n8 = _search(org, refs, R, x8, y8, 8, 8)
+                    part, kids = 0, []
+                    if n8[0] > tol8 * tol8 * 64:
+                        pairs = [[(x8, y8, 8, 4), (x8, y8 + 4, 8, 4)], [(x8, y8, 4, 8), (x8 + 4, y8, 4, 8)]]
+                        for mode, pair in ((1, pairs[0]), (2, pairs[1])):
+                            halves = [_search(org, refs, R, *b) for b in pair]
+                            if all(not (hv[0] > tol8 * tol8 * 32) for hv in halves):
+                                part, kids = mode, halves
+                                break
+                        else:
+                            part = 3
+                            kids = [_search(org, refs, R, x8 + (s & 1) * 4, y8 + (s >> 1) * 4, 4, 4, True)
+                                    for s in range(4)]
+                    rec["b8"][q] = n8[:6] + (part,)
+                    rec["sub"][q] = kids
+            recs.append(rec)
+    return recs
+
+
+def _node_eq(node, tup):
+    got = (node["rms"], node["scale"], node["offset"], node["x"], node["y"], node["reference"], node["partition"])
+    return all(a == b for a, b in zip(got, tup))
+
+
+@pytest.mark.parametrize("seed,K,tols", [(1, 1, (8.0, 5.0)), (2, 2, (4.0, 5.0)), (5, 4, (2.0, 4.0))])
+def test_tree_oracle_matches_python_statement(seed, K, tols):
+    org, refs = gate_scene(64, 48, seed, K, scale=6)
+    R = 3
+    out = ol.fractal_encode_mbs(org, refs, R, *tols)
+    exp = _tree_py(org, refs, R, *tols)
+    zero = np.zeros((), ol.FRO_NODE)
+    for m, e in zip(out, exp):
+        assert _node_eq(m["mb"], e["mb"])
+        assert (np.isnan(m["chun"]) and np.isnan(e["chun"])) or m["chun"] == e["chun"]
+        for q in range(4):
+            if q in e["b8"]:
+                assert _node_eq(m["b8"][q], e["b8"][q])
+                kids = e["sub"][q]
+                for c in range(4):
+                    if c < len(kids):
+                        assert _node_eq(m["sub"][q][c], kids[c])
+                    else:
+                        assert m["sub"][q][c].tobytes() == zero.tobytes()
+            else:
+                assert m["b8"][q].tobytes() == zero.tobytes()
+
+
+def test_tree_oracle_reaches_every_partition():
+    """the scenes used by the GPU parity tests exercise every branch of the gate"""
+    seen_mb, seen_b8, nan, q4 = set(), set(), 0, 0
+    for seed in range(3):
+        org, refs = gate_scene(128, 96, seed, 2, scale=6)
+        out = ol.fractal_encode_mbs(org, refs, 4, 4.0, 5.0)
+        seen_mb |= set(out["mb"]["partition"].tolist())
+        split = out["mb"]["partition"] == 3
+        seen_b8 |= set(out["b8"]["partition"][split].ravel().tolist())
+        nan += int(np.isnan(out["chun"]).sum())
+        q4 += int((out["sub"]["partition"] == 1).sum())
+    assert seen_mb == {0, 3} and seen_b8 == {0, 1, 2, 3} and nan > 0 and q4 > 0
+
+
+def test_tree_planted_steps_pick_the_pairs():
+    """an 8x8 carrying a horizontal offset step fails as a whole but its 8x4
+    halves match (partition 1); a vertical step picks the 4x8 pair (2)"""
+    h = w = 32
+    yy, xx = np.mgrid[0:h, 0:w]
+    ref = (128 + 100 * np.sin(xx / 3.0) * np.cos(yy / 4.0)).astype(np.float64)
+    org = ref.copy()
+    step = np.zeros((h, w))
+    step[0:4, 0:8] += 15
+    step[4:8, 0:8] -= 15          # MB 0, 8x8 #0: horizontal step
+    step[0:8, 8:12] += 15
+    step[0:8, 12:16] -= 15        # MB 0, 8x8 #1: vertical step
+    org = np.clip(np.rint(org + step), 0, 255).astype(np.uint8)
+    ref = np.clip(np.rint(ref), 0, 255).astype(np.uint8)
+    out = ol.fractal_encode_mbs(org, [ref], 0, 1.0, 5.0)
+    m = out[0]
+    assert 0.9 <= m["chun"] <= 1 and m["mb"]["partition"] == 3
+    assert m["b8"]["partition"][0] == 1 and m["b8"]["partition"][1] == 2
+    assert out[1]["mb"]["partition"] == 0 or out[1]["chun"] < 0.9 or out[1]["mb"]["rms"] > 256
