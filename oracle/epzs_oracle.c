@@ -1,0 +1,273 @@
+/*
+ * epzs_oracle.c -- TEST INFRASTRUCTURE: restatement of JM 18.5's EPZS
+ * integer-pel search; see epzs_oracle.h.  Written from the behaviour of
+ * JM/lencod/src/me_epzs.c; no JM code is copied.  Only tests/ and the bench
+ * CPU legs load this library.
+ */
+#include "epzs_oracle.h"
+
+#include <stdlib.h>
+#include <string.h>
+
+#define DMAX ((int64_t)0x7fffffffffffffffLL)   /* DISTBLK_MAX, JM/lencod/inc/defines.h:133 */
+
+/* refinement patterns (me_epzs_common.c:46-80 data, 176-230 wiring):
+ * (dx, dy, start_nmbr, next_points) in qpel */
+typedef struct pat {
+  int n;
+  short pt[12][4];
+  int stop, next_last, next;
+} pat;
+
+enum { P_SDIAMOND, P_SQUARE, P_EDIAMOND, P_LDIAMOND, P_SBDIAMOND, P_PMVFAST };
+
+static const pat PATS[6] = {
+  {4, {{0, 4, 3, 3}, {4, 0, 0, 3}, {0, -4, 1, 3}, {-4, 0, 2, 3}}, 1, 1, P_SDIAMOND},
+  {8, {{0, 4, 7, 3}, {4, 4, 7, 5}, {4, 0, 1, 3}, {4, -4, 1, 5}, {0, -4, 3, 3}, {-4, -4, 3, 5}, {-4, 0, 5, 3},
+       {-4, 4, 5, 5}}, 1, 1, P_SQUARE},
+  {12, {{-4, 4, 10, 5}, {0, 8, 10, 8}, {0, 4, 10, 7}, {4, 4, 1, 5}, {8, 0, 1, 8}, {4, 0, 1, 7}, {4, -4, 4, 5},
+        {0, -8, 4, 8}, {0, -4, 4, 7}, {-4, -4, 7, 5}, {-8, 0, 7, 8}, {-4, 0, 7, 7}}, 1, 1, P_EDIAMOND},
+  {8, {{0, 8, 6, 5}, {4, 4, 0, 3}, {8, 0, 0, 5}, {4, -4, 2, 3}, {0, -8, 2, 5}, {-4, -4, 4, 3}, {-8, 0, 4, 5},
+       {-4, 4, 6, 3}}, 1, 1, P_LDIAMOND},
+  {12, {{0, 8, 6, 12}, {4, 4, 0, 12}, {8, 0, 0, 12}, {4, -4, 2, 12}, {0, -8, 2, 12}, {-4, -4, 4, 12},
+        {-8, 0, 4, 12}, {-4, 4, 6, 12}, {0, 2, 6, 12}, {2, 0, 0, 12}, {0, -2, 2, 12}, {-2, 0, 4, 12}}, 0, 1,
+   P_SDIAMOND},
+  {8, {{0, 8, 6, 5}, {4, 4, 0, 3}, {8, 0, 0, 5}, {4, -4, 2, 3}, {0, -8, 2, 5}, {-4, -4, 4, 3}, {-8, 0, 4, 5},
+       {-4, 4, 6, 3}}, 0, 1, P_SDIAMOND},
+};
+
+/* EPZSPattern / EPZSDualRefinement -> pattern (me_epzs_common.c:530-565) */
+static int primary_pattern(int v)
+{
+  switch (v) {
+    case 5: return P_PMVFAST;
+    case 4: return P_SBDIAMOND;
+    case 3: return P_LDIAMOND;
+    case 2: return P_EDIAMOND;
+    case 1: return P_SQUARE;
+    default: return P_SDIAMOND;
+  }
+}
+
+static int dual_pattern(int v)
+{
+  switch (v) {
+    case 6: return P_PMVFAST;
+    case 5: return P_SBDIAMOND;
+    case 4: return P_LDIAMOND;
+    case 3: return P_EDIAMOND;
+    case 2: return P_SQUARE;
+    default: return P_SDIAMOND;
+  }
+}
+
+static int mvbits(int v)   /* JM/lencod/src/mv_search.c:366-374 */
+{
+  unsigned a = (unsigned)(v < 0 ? -v : v), w = 2u * a + 1u;
+  int b = 0;
+  while (w >> (b + 1)) b++;
+  return 2 * b + 1;
+}
+
+typedef struct ctx {
+  const eo_req *q;
+  const uint8_t *cur, *ref;
+  int pitch, W, H;
+  /* EPZSMap restated as the set of visited integer offsets from the centre */
+  int side_x, side_y;
+  unsigned char *map;
+} ctx;
+
+static int clampi(int v, int lo, int hi) { return v < lo ? lo : v > hi ? hi : v; }
+
+/* mv_cost + computeSAD<<5 for an integer qpel vector (UMVLine4X clamps each
+ * sample into the picture) */
+static int64_t cost_of(const ctx *c, int mx, int my)
+{
+  const eo_req *q = c->q;
+  int64_t mvc = (int64_t)q->lambda * (mvbits(mx - q->pred_x) + mvbits(my - q->pred_y));
+  int x, y, sad = 0;
+  const int ox = q->pos_x + (mx >> 2), oy = q->pos_y + (my >> 2);
+  for (y = 0; y < q->bsy; y++) {
+    const uint8_t *rrow = c->ref + (size_t)clampi(oy + y, 0, c->H - 1) * c->pitch;
+    const uint8_t *crow = c->cur + (size_t)(q->pos_y + y) * c->pitch + q->pos_x;
+    for (x = 0; x < q->bsx; x++) {
+      int d = crow[x] - rrow[clampi(ox + x, 0, c->W - 1)];
+      sad += d < 0 ? -d : d;
+    }
+  }
+  return mvc + ((int64_t)sad << 5);
+}
+
+static int in_range(const ctx *c, int mx, int my)
+{
+  int dx = mx - c->q->center_x, dy = my - c->q->center_y;
+  return (dx < 0 ? -dx : dx) <= c->q->max_x && (dy < 0 ? -dy : dy) <= c->q->max_y;
+}
+
+/* test-and-set of the map cell of an in-range integer vector */
+static int visit(ctx *c, int mx, int my)
+{
+  int cx = (mx - c->q->center_x + c->q->max_x) >> 2, cy = (my - c->q->center_y + c->q->max_y) >> 2;
+  unsigned char *m = &c->map[cy * c->side_x + cx];
+  if (*m) return 0;
+  *m = 1;
+  return 1;
+}
+
+static int16_t int_mv(int16_t v) { return (int16_t)(v & 0xFFFC); }   /* set_integer_mv, me_epzs.c:39-43 */
+
+void eo_epzs(const eo_req *q, const int16_t *preds, const int16_t *stale, const uint8_t *cur, const uint8_t *ref,
+             int pitch, int W, int H, eo_res *out)
+{
+  ctx c;
+  const int frame = q->flags & 1, pslice = (q->flags >> 1) & 1, bt = q->blocktype, refi = q->ref_idx;
+  const int64_t lambda_dist = (int64_t)q->lambda * (q->variant ? 3 : 2);
+  const int mv_range = q->variant ? 12 : 10;
+  int64_t stop = q->medthres + lambda_dist, prev = q->prev_sad, min;
+  int tmpx = q->center_x, tmpy = q->center_y, i;
+  memset(out, 0, sizeof(*out));
+  c.q = q;
+  c.cur = cur;
+  c.ref = ref;
+  c.pitch = pitch;
+  c.W = W;
+  c.H = H;
+  c.side_x = (2 * q->max_x >> 2) + 1;
+  c.side_y = (2 * q->max_y >> 2) + 1;
+  c.map = calloc((size_t)c.side_x * c.side_y, 1);
+  for (i = 0; i < q->n_stale; i++) {       /* cells left holding this BlkCount */
+    int dx = stale[2 * i], dy = stale[2 * i + 1];
+    if ((dx & 3) == 0 && (dy & 3) == 0 && in_range(&c, q->center_x + dx, q->center_y + dy))
+      visit(&c, q->center_x + dx, q->center_y + dy);
+  }
+  visit(&c, q->center_x, q->center_y);
+  min = cost_of(&c, q->center_x, q->center_y);
+
+  if (refi > 0 && frame && prev < (stop < min ? stop : min)) {
+    out->path = 1;
+    goto done_noupdate;
+  }
+  if (min > stop) {
+    int64_t second = DMAX;
+    int check_median = 0, tmp2x = 0, tmp2y = 0, P;
+    stop = q->stop_crit;
+    if (min < (stop >> 1)) {
+      out->path = 2;
+      goto done_noupdate;
+    }
+    for (i = 0; i < q->n_pred; i++) {
+      const int mx = int_mv(preds[2 * i]), my = int_mv(preds[2 * i + 1]);
+      if (in_range(&c, mx, my) && visit(&c, mx, my)) {
+        const int64_t mc = cost_of(&c, mx, my);
+        if (mc < min) {
+          tmp2x = tmpx;
+          tmp2y = tmpy;
+          tmpx = mx;
+          tmpy = my;
+          second = min;
+          min = mc;
+          check_median = 1;
+        } else if (mc < second) {
+          tmp2x = mx;
+          tmp2y = my;
+          second = mc;
+          check_median = 1;
+        }
+      }
+      if (q->variant && min < ((3 * stop) >> 2)) {     /* me_epzs.c:583-596 */
+        out->path = 3;
+        goto done_mv_noupdate;
+      }
+    }
+    if (min > stop) {
+      int cenx, ceny, point = 0, pstop = 0, next_last = 0, total, dir = 0;
+      P = primary_pattern(q->pattern);
+      if (q->pattern != 0) {
+        if (min < stop + ((3 * q->medthres) >> 1)) {
+          const int dx = abs(tmpx - q->center_x), dy = abs(tmpy - q->center_y);
+          P = ((tmpx == 0 && tmpy == 0) || (dx < mv_range && dy < mv_range)) ? P_SDIAMOND : P_SQUARE;
+        } else if (q->variant || bt > 4 || (refi > 0 && bt != 1)) {
+          P = P_SQUARE;
+        }
+      }
+      cenx = tmpx;
+      ceny = tmpy;
+      for (;;) {
+        total = PATS[P].n;
+        do {
+          int left = total;
+          do {
+            const int mx = cenx + PATS[P].pt[point][0], my = ceny + PATS[P].pt[point][1];
+            if (in_range(&c, mx, my) && visit(&c, mx, my)) {
+              const int64_t mc = cost_of(&c, mx, my);
+              if (mc < min) {
+                tmpx = mx;
+                tmpy = my;
+                min = mc;
+                dir = point;
+              }
+            }
+            if (++point >= PATS[P].n) point -= PATS[P].n;
+          } while (--left > 0);
+          if (next_last || (tmpx == cenx && tmpy == ceny)) {
+            pstop = PATS[P].stop;
+            P = PATS[P].next;
+            total = PATS[P].n;
+            next_last = PATS[P].next_last;
+            dir = 0;
+            point = 0;
+          } else {
+            total = PATS[P].pt[dir][3];
+            point = PATS[P].pt[dir][2];
+            cenx = tmpx;
+            ceny = tmpy;
+          }
+        } while (pstop != 1);
+
+        if (refi > 0 && frame && (4 * prev < min || (3 * prev < min && prev <= stop))) {
+          out->path = 4;
+          goto done_mv_noupdate;
+        }
+        if (!(check_median && (pslice || (!q->variant && bt < 5)) && min > stop && q->dual > 0)) break;
+        point = 0;
+        pstop = 0;
+        dir = 0;
+        next_last = 0;
+        if ((tmpx == 0 && tmpy == 0) || (tmpx == q->center_x && tmpy == q->center_y)) {
+          const int dx = abs(tmpx - q->center_x), dy = abs(tmpy - q->center_y);
+          P = (dx < mv_range && dy < mv_range) ? P_SDIAMOND : P_SQUARE;
+        } else {
+          P = dual_pattern(q->dual);
+        }
+        cenx = tmp2x;
+        ceny = tmp2y;
+        check_median = 0;
+      }
+    }
+  }
+  out->path = out->path ? out->path : 5;
+  if (refi == 0 || prev > min) prev = min;
+done_mv_noupdate:
+  out->mv_x = (int16_t)tmpx;
+  out->mv_y = (int16_t)tmpy;
+  out->cost = min;
+  out->prev_sad = prev;
+  free(c.map);
+  return;
+done_noupdate:
+  out->mv_x = q->center_x;
+  out->mv_y = q->center_y;
+  out->cost = min;
+  out->prev_sad = prev;
+  free(c.map);
+}
+
+void eo_epzs_batch(const eo_req *q, int n, const int16_t *preds, const int16_t *stale, const uint8_t *cur,
+                   const uint8_t *const *refs, int pitch, int W, int H, eo_res *out)
+{
+  int i;
+  for (i = 0; i < n; i++)
+    eo_epzs(&q[i], preds + 2 * (size_t)q[i].pred_off, stale + 2 * (size_t)q[i].stale_off, cur, refs[q[i].plane],
+            pitch, W, H, &out[i]);
+}

@@ -1,0 +1,59 @@
+/*
+ * epzs_oracle.h -- TEST INFRASTRUCTURE: plain-C restatement of JM 18.5's EPZS
+ * integer-pel search, the checker for
+ * csrc/jmme_epzs.hip.  JM = /root/reference/4.对比程序/jm18.5/JM:
+ *   EPZS_motion_estimation        JM/lencod/src/me_epzs.c:54-407   (variant 0)
+ *   EPZS_subMB_motion_estimation  JM/lencod/src/me_epzs.c:417-780  (variant 1)
+ *   search patterns               JM/lencod/src/me_epzs_common.c:46-80, 176-230, 530-565
+ *   computeSAD / UMVLine4X        JM/lencod/src/me_distortion.c:349-426, inc/refbuf.h:22-26
+ *   mv_cost, weighted_cost        JM/lencod/inc/mv_search.h:87-112
+ * The predictor list, the stop criterion and the prevSad slot are the state
+ * JM builds on the host before the candidate search (me_epzs_common.c), and
+ * are inputs here, as are the EPZSMap cells that already hold the search's
+ * BlkCount (the uint16 map is never cleared; me_epzs.c:92-94).
+ * Pinned against JM itself: tests/golden/epzs_*.npz hold every EPZS call of
+ * real lencod runs (oracle/capture/jm_epzs_capture.c).
+ *
+ * Request / result layouts equal jmme_epzs_req / jmme_epzs_res (include/jmme.h).
+ */
+#ifndef EPZS_ORACLE_H
+#define EPZS_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct eo_req {
+  int16_t pos_x, pos_y, bsx, bsy;
+  int16_t blocktype, ref_idx;
+  int16_t pred_x, pred_y, center_x, center_y;
+  int16_t max_x, max_y;
+  int32_t lambda;
+  uint8_t variant, flags, pattern, dual;
+  int32_t n_pred, pred_off;
+  int32_t n_stale, stale_off;
+  int32_t plane;
+  int32_t pad;
+  int64_t prev_sad, medthres, stop_crit;
+} eo_req;                       /* 80 bytes */
+
+typedef struct eo_res {
+  int16_t mv_x, mv_y;
+  int32_t path;
+  int64_t cost, prev_sad;
+} eo_res;                       /* 24 bytes */
+
+/* one search; cur / ref 8-bit W x H planes with `pitch`; preds / stale are
+ * (x, y) int16 pairs (stale: qpel offsets from the centre) */
+void eo_epzs(const eo_req *q, const int16_t *preds, const int16_t *stale, const uint8_t *cur, const uint8_t *ref,
+             int pitch, int W, int H, eo_res *out);
+
+/* batch: request i searches ref plane refs[q.plane] */
+void eo_epzs_batch(const eo_req *q, int n, const int16_t *preds, const int16_t *stale, const uint8_t *cur,
+                   const uint8_t *const *refs, int pitch, int W, int H, eo_res *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,143 @@
+#!/usr/bin/env python3
+"""Generate the EPZS golden fixtures from the REAL JM 18.5 encoder.
+
+Run in the build container only (needs /root/reference):
+    python tests/golden/make_golden_epzs.py [case ...]
+
+Same recipe as make_golden.py, with oracle/_ref/lencod_epzs_capture (the
+unmodified JM objects linked with oracle/capture/jm_epzs_capture.c): every
+EPZS integer search JM runs is stored with the predictor list, stop
+criterion, prevSad slot and pre-marked EPZSMap cells it read, and JM's
+(mv, cost, prevSad) result.  The fixtures are data, not reference source.
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+sys.path.insert(0, os.path.join(REPO, "--h.264-by-zhaodongyu_amd"))
+
+from jm_capture import read_epzs_capture  # noqa: E402
+from jmme import synth  # noqa: E402
+from make_golden import BASE_CFG, FOREMAN, coded_synth, md5  # noqa: E402
+
+EPZS_INT = {"SearchMode": 3, "EPZSSubPelGrid": 0}
+
+CASES = {
+    # JM's baseline EPZS settings (EPZSPattern 2, EPZSDualRefinement 3, all predictor kinds), sub-pel ME on
+    "epzs_foreman_qcif": dict(src="foreman", w=176, h=144, frames=3, p={**EPZS_INT}),
+    # the other refinement patterns: small diamond + square dual; square + large diamond dual;
+    # large diamond + PMVFAST dual; PMVFAST + small diamond dual (aggressive window predictors)
+    "epzs_foreman_qcif_p0d2": dict(src="foreman", w=176, h=144, frames=3,
+                                   p={**EPZS_INT, "EPZSPattern": 0, "EPZSDualRefinement": 2}),
+    "epzs_foreman_qcif_p1d4": dict(src="foreman", w=176, h=144, frames=3,
+                                   p={**EPZS_INT, "EPZSPattern": 1, "EPZSDualRefinement": 4,
+                                      "RDOptimization": 0, "MDDistortion": 0, "DisableSubpelME": 1}),
+    "epzs_foreman_qcif_p3d6": dict(src="foreman", w=176, h=144, frames=3,
+                                   p={**EPZS_INT, "EPZSPattern": 3, "EPZSDualRefinement": 6}),
+    "epzs_foreman_qcif_p5d1": dict(src="foreman", w=176, h=144, frames=3,
+                                   p={**EPZS_INT, "EPZSPattern": 5, "EPZSDualRefinement": 1,
+                                      "EPZSFixedPredictors": 3}),
+    # synthetic CIF, range 32, 3 references
+    "epzs_syn_cif_r32_3ref": dict(src="synth", w=352, h=288, frames=4, seed=7, gmv=(5, 3),
+                                  p={**EPZS_INT, "SearchRange": 32, "NumberReferenceFrames": 3,
+                                     "RDOptimization": 0, "MDDistortion": 0, "DisableSubpelME": 1}),
+    # SURVEY config 4 at 1080p: one P-frame, +-32, RDO on; 330k searches, so the
+    # uint16 BlkCount wraps and pre-marked map cells occur
+    "epzs_syn_1080p_r32": dict(src="synth", w=1920, h=1080, frames=2, seed=2024, gmv=(5, 3),
+                               p={**EPZS_INT, "SearchRange": 32, "NumberReferenceFrames": 1,
+                                  "RDOptimization": 1, "MDDistortion": 2}, keep="compact"),
+}
+
+KEEP_FIELDS = ["variant", "frame_no", "mb_addr", "blocktype", "pos_x", "pos_y", "bsx", "bsy", "list", "ref",
+               "pred_x", "pred_y", "center_x", "center_y", "sr_max_x", "sr_max_y", "lambda", "slice_type",
+               "structure", "epzs_pattern", "epzs_dual", "prev_sad_in", "medthres", "stop_crit", "n_pred",
+               "n_stale", "stale_overflow", "out_mv_x", "out_mv_y", "out_cost", "prev_sad_out"]
+
+
+def run_case(name: str, spec: dict, work: str) -> dict:
+    w, h, frames = spec["w"], spec["h"], spec["frames"]
+    if spec["src"] == "foreman":
+        yuv = FOREMAN
+    else:
+        yuv = os.path.join(work, f"{name}.yuv")
+        synth.write_yuv420(yuv, synth.luma_sequence(w, h, frames, seed=spec["seed"], gmv=spec["gmv"]))
+    cap = os.path.join(work, f"{name}.cap")
+    out264 = os.path.join(work, f"{name}.264")
+    rec = os.path.join(work, f"{name}_rec.yuv")
+    args = [os.path.join(REPO, "oracle", "_ref", "lencod_epzs_capture"), "-d", BASE_CFG,
+            "-p", f"InputFile={yuv}", "-p", f"SourceWidth={w}", "-p", f"SourceHeight={h}",
+            "-p", f"OutputWidth={w}", "-p", f"OutputHeight={h}",
+            "-p", f"FramesToBeEncoded={frames}", "-p", f"OutputFile={out264}", "-p", f"ReconFile={rec}"]
+    for k, v in spec["p"].items():
+        args += ["-p", f"{k}={v}"]
+    res = subprocess.run(args, cwd=work, env=dict(os.environ, JMME_CAPTURE=cap), capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(res.stdout[-2000:] + res.stderr[-2000:])
+    me_time = [ln for ln in res.stdout.splitlines() if "Total ME time" in ln]
+    planes, recs, preds, stale = read_epzs_capture(cap)
+    return dict(planes=planes, recs=recs, preds=preds, stale=stale, md5_264=md5(out264), md5_rec=md5(rec),
+                md5_input=md5(yuv), me_time=me_time[0].strip() if me_time else "",
+                cmd=" ".join(a if os.sep not in a else os.path.basename(a) for a in args[1:]))
+
+
+def save_case(name: str, spec: dict, r: dict) -> dict:
+    planes, recs = r["planes"], r["recs"]
+    cur_keys = sorted(k for k in planes if k[1] == 0)
+    ref_keys = sorted(k for k in planes if k[1] == 1)
+    assert max(int(planes[k].max()) for k in cur_keys + ref_keys) <= 255
+    cur = np.stack([planes[k] for k in cur_keys]).astype(np.uint8)
+    ref = np.stack([planes[k] for k in ref_keys]).astype(np.uint8)
+    arrays = {"cur_frame_no": np.array([k[0] for k in cur_keys], np.int32),
+              "ref_key": np.array([[k[0], k[2], k[3]] for k in ref_keys], np.int32),
+              "cur_md5": np.array([hashlib.md5(c.tobytes()).hexdigest() for c in cur])}
+    if spec.get("keep") == "compact":
+        orig = coded_synth(spec)
+        assert all(np.array_equal(cur[i], orig[f]) for i, f in enumerate(arrays["cur_frame_no"]))
+        res = ref.astype(np.int16) - orig[arrays["ref_key"][:, 0] - 1 - arrays["ref_key"][:, 2]]
+        assert res.min() >= -128 and res.max() <= 127
+        arrays["ref_residual"] = res.astype(np.int8)
+    else:
+        arrays["cur"] = cur
+        arrays["ref"] = ref
+    for f in KEEP_FIELDS:
+        arrays["r_" + f] = recs[f]
+    arrays["preds"] = (np.concatenate(r["preds"]) if sum(len(p) for p in r["preds"]) else
+                       np.zeros((0, 2), np.int16)).astype(np.int16)
+    arrays["stale"] = (np.concatenate(r["stale"]) if sum(len(s) for s in r["stale"]) else
+                       np.zeros((0, 2), np.int16)).astype(np.int16)
+    path = os.path.join(HERE, f"{name}.npz")
+    np.savez_compressed(path, **arrays)
+    return dict(case=name, kind="epzs", w=spec["w"], h=spec["h"], frames=spec["frames"],
+                epzs_overrides=spec["p"], src=spec["src"], seed=spec.get("seed"), gmv=spec.get("gmv"),
+                adversarial=False, n_searches=int(len(recs)), n_stale=int(recs["n_stale"].sum()),
+                stale_overflow=int(recs["stale_overflow"].sum()),
+                md5_bitstream=r["md5_264"], md5_recon=r["md5_rec"], md5_input=r["md5_input"],
+                jm_me_time=r["me_time"], jm_cmd=r["cmd"], bytes=os.path.getsize(path))
+
+
+def main(argv):
+    names = argv or list(CASES)
+    subprocess.run(["make", "-s", "-C", os.path.join(REPO, "oracle"), "-j8", "ref"], check=True)
+    mpath = os.path.join(HERE, "manifest.json")
+    manifest = json.load(open(mpath)) if os.path.exists(mpath) else {}
+    with tempfile.TemporaryDirectory() as work:
+        for n in names:
+            r = run_case(n, CASES[n], work)
+            manifest[n] = save_case(n, CASES[n], r)
+            print(n, manifest[n]["n_searches"], "searches,", manifest[n]["n_stale"], "stale cells,",
+                  manifest[n]["bytes"], "bytes", r["me_time"])
+    json.dump(manifest, open(mpath, "w"), indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])

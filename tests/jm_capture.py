@@ -57,3 +57,56 @@ def read_capture(path: str):
         else:
             raise ValueError(f"bad tag {tag:#x} at {off - 4}")
     return planes, np.array(recs, dtype=SEARCH_DTYPE)
+
+
+# ---- EPZS log (oracle/capture/jm_epzs_capture.c, struct cap_epzs) -------------
+EPZS_DTYPE = np.dtype([
+    ("variant", "<i4"), ("frame_no", "<i4"), ("mb_addr", "<i4"),
+    ("mb_x", "<i2"), ("mb_y", "<i2"),
+    ("blocktype", "<i2"), ("block_x", "<i2"), ("block_y", "<i2"),
+    ("pos_x", "<i2"), ("pos_y", "<i2"), ("bsx", "<i2"), ("bsy", "<i2"),
+    ("list", "<i2"), ("ref", "<i2"), ("list_offset", "<i2"),
+    ("pred_x", "<i2"), ("pred_y", "<i2"), ("center_x", "<i2"), ("center_y", "<i2"),
+    ("sr_min_x", "<i4"), ("sr_max_x", "<i4"), ("sr_min_y", "<i4"), ("sr_max_y", "<i4"),
+    ("lambda", "<i4"), ("slice_type", "<i4"), ("structure", "<i4"),
+    ("epzs_pattern", "<i4"), ("epzs_dual", "<i4"), ("blk_count", "<i4"),
+    ("prev_sad_in", "<i8"), ("medthres", "<i8"), ("stop_crit", "<i8"),
+    ("n_pred", "<i4"), ("n_stale", "<i4"), ("stale_overflow", "<i4"),
+    ("img_w", "<i4"), ("img_h", "<i4"),
+    ("min_mcost_in", "<i8"),
+    ("out_mv_x", "<i2"), ("out_mv_y", "<i2"), ("out_cost", "<i8"), ("prev_sad_out", "<i8"),
+])
+TAG_EPZS = 0x305A5045
+
+
+def read_epzs_capture(path: str):
+    """Return (planes, records, preds, stale): records EPZS_DTYPE in call order;
+    preds / stale int16 [total, 2] pools with per-record offsets in
+    records' order (pred_off / stale_off arrays returned inside a dict)."""
+    buf = open(path, "rb").read()
+    mv = memoryview(buf)
+    off, n = 0, len(buf)
+    planes, recs, preds, stale = {}, [], [], []
+    rsz = EPZS_DTYPE.itemsize
+    while off < n:
+        tag = int.from_bytes(mv[off:off + 4], "little")
+        off += 4
+        if tag == TAG_PLANE:
+            hdr = np.frombuffer(mv[off:off + 24], dtype="<i4")
+            off += 24
+            frame_no, kind, lst, ref, w, h = (int(v) for v in hdr)
+            planes[(frame_no, kind, lst, ref)] = np.frombuffer(mv[off:off + 2 * w * h], dtype="<u2").reshape(h, w).copy()
+            off += 2 * w * h
+        elif tag == TAG_EPZS:
+            r = np.frombuffer(mv[off:off + rsz], dtype=EPZS_DTYPE)[0]
+            off += rsz
+            k = max(int(r["n_pred"]), 0)
+            preds.append(np.frombuffer(mv[off:off + 4 * k], dtype="<i2").reshape(k, 2).copy())
+            off += 4 * k
+            s = int(r["n_stale"])
+            stale.append(np.frombuffer(mv[off:off + 4 * s], dtype="<i2").reshape(s, 2).copy())
+            off += 4 * s
+            recs.append(r)
+        else:
+            raise ValueError(f"bad tag {tag:#x} at {off - 4}")
+    return planes, np.array(recs, dtype=EPZS_DTYPE), preds, stale

@@ -246,3 +246,51 @@ def fractal_encode_mbs(org, refs, R, tol_16, tol_8):
     lib.fro_encode_mbs(org.ctypes.data, ptrs, len(refs), w, w, h, int(R), float(tol_16), float(tol_8),
                        out.ctypes.data)
     return out
+
+
+# ---- JM EPZS integer search (oracle/epzs_oracle.c, pinned against JM captures) --
+EPZS_REQ = np.dtype([("pos_x", "<i2"), ("pos_y", "<i2"), ("bsx", "<i2"), ("bsy", "<i2"),
+                     ("blocktype", "<i2"), ("ref_idx", "<i2"), ("pred_x", "<i2"), ("pred_y", "<i2"),
+                     ("center_x", "<i2"), ("center_y", "<i2"), ("max_x", "<i2"), ("max_y", "<i2"),
+                     ("lambda", "<i4"), ("variant", "u1"), ("flags", "u1"), ("pattern", "u1"), ("dual", "u1"),
+                     ("n_pred", "<i4"), ("pred_off", "<i4"), ("n_stale", "<i4"), ("stale_off", "<i4"),
+                     ("plane", "<i4"), ("pad", "<i4"),
+                     ("prev_sad", "<i8"), ("medthres", "<i8"), ("stop_crit", "<i8")])
+EPZS_RES = np.dtype([("mv_x", "<i2"), ("mv_y", "<i2"), ("path", "<i4"), ("cost", "<i8"), ("prev_sad", "<i8")])
+assert EPZS_REQ.itemsize == 80 and EPZS_RES.itemsize == 24
+EP_SO = os.path.join(ORACLE_DIR, "build", "libepzs_oracle.so")
+_ep = None
+
+
+def load_epzs() -> ctypes.CDLL:
+    global _ep
+    if _ep is not None:
+        return _ep
+    src = os.path.join(ORACLE_DIR, "epzs_oracle.c")
+    if not os.path.exists(EP_SO) or os.path.getmtime(EP_SO) < os.path.getmtime(src):
+        subprocess.run(["make", "-s", "-C", ORACLE_DIR, "port"], check=True)
+    lib = ctypes.CDLL(EP_SO)
+    P, I = ctypes.c_void_p, ctypes.c_int
+    lib.eo_epzs_batch.argtypes = [P, I, P, P, P, P, I, I, I, P]
+    _ep = lib
+    return lib
+
+
+def epzs_batch(req, preds, stale, cur, refs):
+    """req EPZS_REQ[n]; preds/stale int16 [k, 2] pools; cur / refs[plane] uint8 HxW -> EPZS_RES[n]"""
+    lib = load_epzs()
+    req = np.ascontiguousarray(req, EPZS_REQ)
+    preds = np.ascontiguousarray(preds, np.int16).reshape(-1, 2)
+    stale = np.ascontiguousarray(stale, np.int16).reshape(-1, 2)
+    if len(preds) == 0:
+        preds = np.zeros((1, 2), np.int16)
+    if len(stale) == 0:
+        stale = np.zeros((1, 2), np.int16)
+    cur = np.ascontiguousarray(cur, np.uint8)
+    refs = [np.ascontiguousarray(r, np.uint8) for r in refs]
+    h, w = cur.shape
+    ptrs = (ctypes.c_void_p * len(refs))(*[r.ctypes.data for r in refs])
+    out = np.zeros(len(req), EPZS_RES)
+    lib.eo_epzs_batch(req.ctypes.data, len(req), preds.ctypes.data, stale.ctypes.data, cur.ctypes.data, ptrs, w, w, h,
+                      out.ctypes.data)
+    return out

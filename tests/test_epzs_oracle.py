@@ -1,0 +1,39 @@
+"""CPU: the EPZS restatement (oracle/epzs_oracle.c) reproduces every EPZS
+integer search of the captured JM 18.5 runs (tests/golden/epzs_*.npz):
+JM's (mv, cost) and the prevSad slot it leaves, for both search variants
+(EPZS_motion_estimation / EPZS_subMB_motion_estimation, me_epzs.c:54, 417),
+all refinement / dual patterns except the half-pel SBP diamond, 1-3 reference
+frames, and a 1080p frame whose uint16 BlkCount wraps (pre-marked map cells)."""
+import numpy as np
+import pytest
+
+import oracle_lib as ol
+from epzs_cases import EpzsCase, cases
+
+
+@pytest.mark.parametrize("name", cases())
+def test_oracle_matches_jm(name):
+    c = EpzsCase(name)
+    n = 0
+    for f, cur, refs, req, exp in c.frames():
+        out = ol.epzs_batch(req, c.preds, c.stale, cur, refs)
+        for k in ("mv_x", "mv_y", "cost", "prev_sad"):
+            bad = np.nonzero(out[k] != exp[k])[0]
+            assert len(bad) == 0, (name, f, k, len(bad), req[bad[:2]], out[bad[:2]], exp[bad[:2]])
+        n += len(req)
+    assert n == c.meta["n_searches"]
+
+
+def test_fixtures_cover_the_search_paths():
+    """early exits (ref>0 prevSad, stop/2, subMB predictor stop, post-pattern
+    ref>0), full refinement, both variants, every supported pattern pair"""
+    paths = np.zeros(6, np.int64)
+    pats = set()
+    for name in cases():
+        c = EpzsCase(name)
+        for f, cur, refs, req, exp in c.frames():
+            out = ol.epzs_batch(req, c.preds, c.stale, cur, refs)
+            paths += np.bincount(out["path"], minlength=6)
+            pats |= set(zip(req["pattern"].tolist(), req["dual"].tolist()))
+    assert (paths[1:] > 0).all(), paths
+    assert {(2, 3), (0, 2), (1, 4), (3, 6), (5, 1)} <= pats
