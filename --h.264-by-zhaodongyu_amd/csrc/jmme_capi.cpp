@@ -16,6 +16,7 @@
 #include "jmme_common.h"
 #include "jmme_internal.h"
 #include "jmme_tq_internal.h"
+#include "jmme_epzs_internal.h"
 #include "jmme_fractal_internal.h"
 
 using namespace jmme;
@@ -715,6 +716,78 @@ extern "C" int jmme_fractal_box_sums(jmme_ctx *ctx, const uint8_t *plane, int pi
                          (double *)ds.p, (double *)ds2.p, nullptr));
   HIPCHK(hipMemcpy(sum, ds.p, (size_t)w * h * 8, hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(sum2, ds2.p, (size_t)w * h * 8, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+// -------------------------------------------------------------------- EPZS --
+static_assert(sizeof(jmme_epzs_req) == 80 && sizeof(jmme_epzs_res) == 24, "EPZS ABI layout");
+
+extern "C" int jmme_epzs_search_async(jmme_ctx *ctx, const jmme_epzs_req *d_req, int n, const int16_t *d_preds,
+                                      const int16_t *d_stale, jmme_epzs_res *d_out, void *stream) {
+  if (!ctx) return fail("null ctx");
+  if (n < 0) return fail("negative request count");
+  if (n == 0) return 0;
+  if (!ctx->d_cur) return fail("no current frame uploaded");
+  if (!d_req || !d_out || !d_preds || !d_stale) return fail("null array");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (sync_ref_table(ctx, s)) return -1;
+  EpzsParams p{};
+  p.cur = ctx->d_cur;
+  p.refs = ctx->d_ref_table;
+  p.pitch = ctx->pitch;
+  p.width = ctx->width;
+  p.height = ctx->height;
+  p.req = d_req;
+  p.preds = d_preds;
+  p.stale = d_stale;
+  p.out = d_out;
+  p.n = n;
+  HIPCHK(launch_epzs(p, s));
+  return 0;
+}
+
+extern "C" int jmme_epzs_search(jmme_ctx *ctx, const jmme_epzs_req *req, int n, const int16_t *preds, int n_preds,
+                                const int16_t *stale, int n_stale, jmme_epzs_res *out) {
+  if (!ctx) return fail("null ctx");
+  if (n <= 0) return n < 0 ? fail("negative request count") : 0;
+  if (!req || !out || (n_preds && !preds) || (n_stale && !stale)) return fail("null array");
+  if (!ctx->d_cur) return fail("no current frame uploaded");
+  for (int i = 0; i < n; ++i) {
+    const jmme_epzs_req &q = req[i];
+    const bool size_ok = (q.bsx == 16 || q.bsx == 8 || q.bsx == 4) && (q.bsy == 16 || q.bsy == 8 || q.bsy == 4) &&
+                         !(q.bsx == 16 && q.bsy == 4) && !(q.bsx == 4 && q.bsy == 16);
+    if (!size_ok) return fail("request %d: block %dx%d", i, q.bsx, q.bsy);
+    if (q.pos_x < 0 || q.pos_y < 0 || (q.pos_x & 3) || (q.pos_y & 3) || q.pos_x + q.bsx > ctx->width ||
+        q.pos_y + q.bsy > ctx->height)
+      return fail("request %d: block (%d,%d) %dx%d outside the %dx%d picture", i, q.pos_x, q.pos_y, q.bsx, q.bsy,
+                  ctx->width, ctx->height);
+    if ((q.center_x & 3) || (q.center_y & 3)) return fail("request %d: centre (%d,%d) is not integer-pel", i,
+                                                          q.center_x, q.center_y);
+    if (q.max_x < 0 || q.max_y < 0 || q.max_x > kEpzsMaxQpel || q.max_y > kEpzsMaxQpel)
+      return fail("request %d: search range (%d,%d) qpel outside 0..%d", i, q.max_x, q.max_y, kEpzsMaxQpel);
+    if (q.variant > 1 || q.pattern > 5 || q.dual > 6) return fail("request %d: variant/pattern/dual", i);
+    if (q.pattern == 4 || q.dual == 5)
+      return fail("request %d: the SBP large diamond refines on half-pel points (EPZSSubPelGrid planes)", i);
+    if (q.blocktype < 1 || q.blocktype > 7) return fail("request %d: blocktype %d", i, q.blocktype);
+    if (q.n_pred < 0 || q.pred_off < 0 || (int64_t)q.pred_off + q.n_pred > n_preds)
+      return fail("request %d: predictors [%d, +%d) outside the pool of %d", i, q.pred_off, q.n_pred, n_preds);
+    if (q.n_stale < 0 || q.stale_off < 0 || (int64_t)q.stale_off + q.n_stale > n_stale)
+      return fail("request %d: map cells [%d, +%d) outside the pool of %d", i, q.stale_off, q.n_stale, n_stale);
+    if (q.ref_slot < 0 || q.ref_slot >= kMaxLists * kMaxRefs || !ctx->d_refs[q.ref_slot])
+      return fail("request %d: reference slot %d not uploaded", i, q.ref_slot);
+  }
+  DevBuf dq, dp, ds, dout;
+  HIPCHK(dq.alloc((size_t)n * sizeof(jmme_epzs_req)));
+  HIPCHK(dp.alloc((size_t)(n_preds ? n_preds : 1) * 4));
+  HIPCHK(ds.alloc((size_t)(n_stale ? n_stale : 1) * 4));
+  HIPCHK(dout.alloc((size_t)n * sizeof(jmme_epzs_res)));
+  HIPCHK(hipMemcpy(dq.p, req, (size_t)n * sizeof(jmme_epzs_req), hipMemcpyHostToDevice));
+  if (n_preds) HIPCHK(hipMemcpy(dp.p, preds, (size_t)n_preds * 4, hipMemcpyHostToDevice));
+  if (n_stale) HIPCHK(hipMemcpy(ds.p, stale, (size_t)n_stale * 4, hipMemcpyHostToDevice));
+  if (jmme_epzs_search_async(ctx, (const jmme_epzs_req *)dq.p, n, (const int16_t *)dp.p, (const int16_t *)ds.p,
+                             (jmme_epzs_res *)dout.p, nullptr))
+    return -1;
+  HIPCHK(hipMemcpy(out, dout.p, (size_t)n * sizeof(jmme_epzs_res), hipMemcpyDeviceToHost));
   return 0;
 }
 

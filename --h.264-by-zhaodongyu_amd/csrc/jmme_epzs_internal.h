@@ -1,0 +1,24 @@
+// jmme_epzs_internal.h -- launcher of the EPZS kernel (csrc/jmme_epzs.hip);
+// not part of the C ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "jmme.h"
+
+namespace jmme {
+
+constexpr int kEpzsMaxQpel = 4 * JMME_MAX_RANGE;   // largest searchRange.max_x / max_y (qpel)
+
+struct EpzsParams {
+  const uint8_t *cur;                  // current frame, 8-bit
+  const uint8_t *const *refs;          // device table of reference planes (list * 32 + ref_idx)
+  int pitch, width, height;
+  const jmme_epzs_req *req;
+  const int16_t *preds, *stale;        // (x, y) pools
+  jmme_epzs_res *out;
+  int n;
+};
+
+hipError_t launch_epzs(const EpzsParams &p, hipStream_t s);
+
+}  // namespace jmme

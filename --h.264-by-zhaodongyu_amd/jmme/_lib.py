@@ -35,6 +35,15 @@ FRACTAL_NODE = np.dtype([("rms", "<f8"), ("scale", "<f8"), ("offset", "<f8"), ("
 FRACTAL_MB = np.dtype([("mb", FRACTAL_NODE), ("b8", FRACTAL_NODE, (4,)), ("sub", FRACTAL_NODE, (4, 4)),
                        ("chun", "<f8")])
 FRACTAL_MAX_VIEWS = 4
+EPZS_REQ = np.dtype([("pos_x", "<i2"), ("pos_y", "<i2"), ("bsx", "<i2"), ("bsy", "<i2"),
+                     ("blocktype", "<i2"), ("ref_idx", "<i2"), ("pred_x", "<i2"), ("pred_y", "<i2"),
+                     ("center_x", "<i2"), ("center_y", "<i2"), ("max_x", "<i2"), ("max_y", "<i2"),
+                     ("lambda", "<i4"), ("variant", "u1"), ("flags", "u1"), ("pattern", "u1"), ("dual", "u1"),
+                     ("n_pred", "<i4"), ("pred_off", "<i4"), ("n_stale", "<i4"), ("stale_off", "<i4"),
+                     ("ref_slot", "<i4"), ("reserved", "<i4"),
+                     ("prev_sad", "<i8"), ("medthres", "<i8"), ("stop_crit", "<i8")])
+EPZS_RES = np.dtype([("mv_x", "<i2"), ("mv_y", "<i2"), ("path", "<i4"), ("cost", "<i8"), ("prev_sad", "<i8")])
+EPZS_FRAME, EPZS_PSLICE = 1, 2
 QUANT4x4_PARAMS = np.dtype([("scale", "<i4", (16,)), ("offset", "<i4", (16,)), ("inv_scale", "<i4", (16,)),
                             ("qp_per", "<i4"), ("is_cavlc", "<i4"), ("scan", "u1", (16, 2)), ("c_cost", "u1", (16,))])
 TRANSFORM_OPS = {"forward4x4": (0, 16, 16), "inverse4x4": (1, 16, 16), "hadamard4x4": (2, 16, 16),
@@ -44,6 +53,7 @@ TRANSFORM_OPS = {"forward4x4": (0, 16, 16), "inverse4x4": (1, 16, 16), "hadamard
 assert BLOCK_REQ.itemsize == 16 and MB_REQ.itemsize == 688 and BLOCK_RES.itemsize == 16
 assert QUANT4x4_PARAMS.itemsize == 248 and FRACTAL_REQ.itemsize == 8 and FRACTAL_RES.itemsize == 32
 assert FRACTAL_NODE.itemsize == 40 and FRACTAL_MB.itemsize == 848
+assert EPZS_REQ.itemsize == 80 and EPZS_RES.itemsize == 24
 
 CONFIG_FIELDS = ["SourceWidth", "SourceHeight", "SearchMode", "SearchRange", "NumberReferenceFrames",
                  "DisableSubpelME", "RDOptimization", "MEDistortionFPel", "MDDistortion", "EPZSSubPelGrid",
@@ -104,6 +114,8 @@ def lib() -> ctypes.CDLL:
         "jmme_fractal_search_async": (I, [P, P, I, P, I, I, I, P, I, P, P]),
         "jmme_fractal_box_sums": (I, [P, P, I, I, I, I, I, P, P]),
         "jmme_fractal_encode_mbs": (I, [P, P, P, I, I, I, I, I, D, D, P]),
+        "jmme_epzs_search": (I, [P, P, I, P, I, P, I, P]),
+        "jmme_epzs_search_async": (I, [P, P, I, P, P, P, P]),
         "jmme_fractal_encode_mbs_async": (I, [P, P, P, I, P, I, I, I, I, D, D, P, P]),
         "jmme_quant4x4_async": (I, [P, P, P, P, P, P, P, P, I, P]),
         "jmme_spiral_index": (I, [I, I]),

@@ -198,6 +198,20 @@ class MotionEstimator:
         check(lib().jmme_fractal_box_sums(self._ctx, ptr(plane), w, w, h, int(bsx), int(bsy), ptr(s), ptr(s2)))
         return s, s2
 
+    def epzs_search(self, req: np.ndarray, preds: np.ndarray, stale: np.ndarray | None = None) -> np.ndarray:
+        """EPZS_motion_estimation / EPZS_subMB_motion_estimation (JM me_epzs.c:54, 417) for each
+        request against the uploaded current frame and reference slots -> EPZS_RES[n]."""
+        req = np.ascontiguousarray(req, _lib.EPZS_REQ)
+        preds = np.ascontiguousarray(preds, np.int16).reshape(-1, 2)
+        stale = np.zeros((0, 2), np.int16) if stale is None else np.ascontiguousarray(stale, np.int16).reshape(-1, 2)
+        out = np.zeros(len(req), _lib.EPZS_RES)
+        check(lib().jmme_epzs_search(self._ctx, ptr(req), len(req), ptr(preds), len(preds), ptr(stale), len(stale),
+                                     ptr(out)))
+        return out
+
+    def epzs_search_async(self, d_req: int, n: int, d_preds: int, d_stale: int, d_out: int, stream: int = 0) -> None:
+        check(lib().jmme_epzs_search_async(self._ctx, d_req, int(n), d_preds, d_stale, d_out, stream))
+
     def fractal_encode_mbs(self, org: np.ndarray, refs, search_range: int, tol_16: float = 8.0,
                            tol_8: float = 5.0) -> np.ndarray:
         """encode_one_macroblock (ZL/src/block_enc.c:508) for every macroblock of org against the

@@ -230,6 +230,57 @@ int jmme_quant4x4_async(jmme_ctx *ctx, const jmme_quant4x4_params *d_params, con
                         int32_t *d_coef, int32_t *d_levels, int32_t *d_runs, int32_t *d_coeff_cost,
                         int32_t *d_nonzero, int n, void *stream);
 
+/* ---- EPZS integer-pel search --------------------------
+ * EPZS_motion_estimation (variant 0) and EPZS_subMB_motion_estimation
+ * (variant 1), JM/lencod/src/me_epzs.c:54-407 / 417-780, with
+ * EPZSSubPelGrid = 0: median check and its early exits, the predictor list
+ * (deduplicated through the EPZSMap), the refinement pattern walk
+ * (EPZSPattern 0-3, 5; the half-pel SBP diamond 4 is not supported) and the
+ * dual refinement around the second best (EPZSDualRefinement 0-4, 6).
+ * What JM builds on the host before the candidate search is input: the
+ * predictor list (EPZS_spatial / _spatial_memory / _temporal /
+ * EPZSWindowPredictors / EPZSBlockTypePredictors(MB), me_epzs_common.c), the
+ * stop criterion (EPZSDetermineStopCriterion :1764), the prevSad slot
+ * (p_EPZS->distortion[list][blocktype-1][pos_x2]) and the EPZSMap cells that
+ * already hold the search's BlkCount (the uint16 map is never cleared).
+ * The result is JM's (mv, cost) and the prevSad value JM leaves. */
+typedef struct jmme_epzs_req {
+  int16_t pos_x, pos_y;        /* block origin, luma pels */
+  int16_t bsx, bsy;            /* 16 / 8 / 4 */
+  int16_t blocktype, ref_idx;  /* 1..7; reference index (the ref > 0 thresholds) */
+  int16_t pred_x, pred_y;      /* MV predictor, qpel */
+  int16_t center_x, center_y;  /* mv_block->mv[list] on entry, qpel, integer (multiple of 4) */
+  int16_t max_x, max_y;        /* mv_block->searchRange.max_x / max_y, qpel */
+  int32_t lambda;              /* lambda_factor[F_PEL] */
+  uint8_t variant;             /* 0 EPZS_motion_estimation, 1 EPZS_subMB_motion_estimation */
+  uint8_t flags;               /* JMME_EPZS_FRAME | JMME_EPZS_PSLICE */
+  uint8_t pattern, dual;       /* EPZSPattern, EPZSDualRefinement */
+  int32_t n_pred, pred_off;    /* predictor list: (x, y) qpel pairs at preds[pred_off ..] */
+  int32_t n_stale, stale_off;  /* pre-marked EPZSMap cells: (dx, dy) qpel from the centre */
+  int32_t ref_slot;            /* list * 32 + ref_idx of jmme_upload_ref */
+  int32_t reserved;
+  int64_t prev_sad;            /* *prevSad on entry */
+  int64_t medthres;            /* p_EPZS->medthres[blocktype] */
+  int64_t stop_crit;           /* EPZSDetermineStopCriterion's value (read only when JM calls it) */
+} jmme_epzs_req;               /* 80 bytes */
+
+#define JMME_EPZS_FRAME 1      /* currSlice->structure == FRAME */
+#define JMME_EPZS_PSLICE 2     /* currSlice->slice_type == P_SLICE */
+
+typedef struct jmme_epzs_res {
+  int16_t mv_x, mv_y;          /* mv_block->mv[list] on return, qpel */
+  int32_t path;                /* 1..5: which return of the JM function was taken */
+  int64_t cost;                /* return value (min_mcost) */
+  int64_t prev_sad;            /* *prevSad on return */
+} jmme_epzs_res;               /* 24 bytes */
+
+/* against the uploaded current frame and reference slots; host arrays */
+int jmme_epzs_search(jmme_ctx *ctx, const jmme_epzs_req *req, int n, const int16_t *preds, int n_preds,
+                     const int16_t *stale, int n_stale, jmme_epzs_res *out);
+/* device arrays on `stream` (requests validated by the caller) */
+int jmme_epzs_search_async(jmme_ctx *ctx, const jmme_epzs_req *d_req, int n, const int16_t *d_preds,
+                           const int16_t *d_stale, jmme_epzs_res *d_out, void *stream);
+
 /* ---- Fractal domain-range block matching (thesis codec) -------------------
  * SURVEY.md §8 rows a14-a16; ZL = /root/reference/2.论文程序/ZhangLing_Yu_
  * version1/H264Fractal.  full_search (ZL/src/block_enc.c:1933-1977) with

@@ -9,7 +9,7 @@
 #include <stdlib.h>
 #include <string.h>
 
-#define DMAX ((int64_t)0x7fffffffffffffffLL)   /* DISTBLK_MAX, JM/lencod/inc/defines.h:133 */
+#define DMAX (((int64_t)0x7fffffff) << 5)   /* DISTBLK_MAX, JM/lencod/inc/defines.h:135 */
 
 /* refinement patterns (me_epzs_common.c:46-80 data, 176-230 wiring):
  * (dx, dy, start_nmbr, next_points) in qpel */
