@@ -73,6 +73,7 @@ __device__ __forceinline__ void wave_sync() { asm volatile("s_waitcnt lgkmcnt(0)
 struct WaveLds {
   uint32_t map[kMapWords];
   uint32_t cur[64];
+  int pk[64][3];          // compacted candidates (x, y, source index)
 };
 
 struct Search {
@@ -85,64 +86,96 @@ struct Search {
   uint32_t *map;
 };
 
-// SAD of the block at (ox, oy) of the reference against the current block
-// (LDS); arguments by value so the out-of-line call keeps them in registers
-template <int BSX, int BSY>
-__device__ __forceinline__ unsigned sad_t(const uint8_t *ref, int pitch, int W, int H, const uint32_t *cur, int ox,
-                                          int oy) {
-  constexpr int NQ = BSX / 4;
+// SAD of row r of the block at (ox, oy) against the current block's row r
+// (LDS).  UMVLine4X semantics: the row index and, off the picture's sides,
+// every sample are clamped into the picture.
+template <int NQ>
+__device__ __forceinline__ unsigned row_sad(const Search &s, int ox, int oy, int r) {
+  const uint8_t *row = s.ref + (size_t)min(max(oy + r, 0), s.H - 1) * s.pitch;
+  const uint32_t *cur = s.cur + r * NQ;
   unsigned sad = 0;
-  if (ox >= 0 && oy >= 0 && ox + BSX <= W && oy + BSY <= H) {
+  if (ox >= 0 && ox + 4 * NQ <= s.W) {
     const int xa = ox & ~3, sh = ox & 3;
-    const uint8_t *base = ref + (size_t)oy * pitch + xa;
-    const int last = sh ? 4 * NQ : 4 * NQ - 4;   // the extra dword stays inside the row
+    const uint8_t *base = row + xa;
+    uint32_t w[NQ + 1];
 #pragma unroll
-    for (int r = 0; r < BSY; ++r) {
-      const uint8_t *row = base + (size_t)r * pitch;
-      uint32_t w[NQ + 1];
+    for (int q = 0; q < NQ; ++q) w[q] = *reinterpret_cast<const uint32_t *>(base + 4 * q);
+    w[NQ] = *reinterpret_cast<const uint32_t *>(base + (sh ? 4 * NQ : 4 * NQ - 4));   // stays inside the row
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) w[q] = *reinterpret_cast<const uint32_t *>(row + 4 * q);
-      w[NQ] = *reinterpret_cast<const uint32_t *>(row + last);
-#pragma unroll
-      for (int q = 0; q < NQ; ++q)
-        sad = __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(w[q + 1], w[q], sh), cur[r * NQ + q], sad);
-    }
+    for (int q = 0; q < NQ; ++q) sad = __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(w[q + 1], w[q], sh), cur[q], sad);
   } else {
-    // UMVLine4X: every sample clamped into the picture
 #pragma unroll
-    for (int r = 0; r < BSY; ++r) {
-      const uint8_t *row = ref + (size_t)min(max(oy + r, 0), H - 1) * pitch;
+    for (int q = 0; q < NQ; ++q) {
+      uint32_t d = 0;
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        uint32_t d = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) d |= (uint32_t)row[min(max(ox + 4 * q + k, 0), W - 1)] << (8 * k);
-        sad = __builtin_amdgcn_sad_u8(d, cur[r * NQ + q], sad);
-      }
+      for (int k = 0; k < 4; ++k) d |= (uint32_t)row[min(max(ox + 4 * q + k, 0), s.W - 1)] << (8 * k);
+      sad = __builtin_amdgcn_sad_u8(d, cur[q], sad);
     }
   }
   return sad;
 }
 
-__device__ __noinline__ unsigned block_sad(const uint8_t *ref, int pitch, int W, int H, const uint32_t *cur, int bs,
-                                           int ox, int oy) {
-  switch (bs) {
-    case (16 << 8) | 16: return sad_t<16, 16>(ref, pitch, W, H, cur, ox, oy);
-    case (16 << 8) | 8: return sad_t<16, 8>(ref, pitch, W, H, cur, ox, oy);
-    case (8 << 8) | 16: return sad_t<8, 16>(ref, pitch, W, H, cur, ox, oy);
-    case (8 << 8) | 8: return sad_t<8, 8>(ref, pitch, W, H, cur, ox, oy);
-    case (8 << 8) | 4: return sad_t<8, 4>(ref, pitch, W, H, cur, ox, oy);
-    case (4 << 8) | 8: return sad_t<4, 8>(ref, pitch, W, H, cur, ox, oy);
-    default: return sad_t<4, 4>(ref, pitch, W, H, cur, ox, oy);
+// Costs (mv_cost + SAD << 5) of the candidates held by lanes 0..K-1 (qpel
+// (mx, my)), returned in the same lanes.  One lane per (candidate, row):
+// 64/bsy candidates per pass, row sums reduced inside aligned lane groups.
+template <int NQ, int LOGR>
+__device__ __forceinline__ int64_t eval_t(const Search &s, int lane, int K, int mx, int my) {
+  constexpr int R = 1 << LOGR, C = 64 >> LOGR;
+  const int grp = lane >> LOGR, r = lane & (R - 1);
+  unsigned mine = 0;
+  for (int base = 0; base < K; base += C) {
+    const int c = base + grp;
+    const int cmx = __shfl(mx, c & 63, 64), cmy = __shfl(my, c & 63, 64);
+    unsigned sad = c < K ? row_sad<NQ>(s, s.pos_x + (cmx >> 2), s.pos_y + (cmy >> 2), r) : 0u;
+#pragma unroll
+    for (int m = 1; m < R; m <<= 1) sad += __shfl_xor(sad, m, 64);
+    const int j = lane - base;
+    const unsigned v = __shfl(sad, (j & (C - 1)) << LOGR, 64);
+    if (j >= 0 && j < C) mine = v;
+  }
+  const int64_t mvc = (int64_t)s.lambda * (mvbits(mx - s.pred_x) + mvbits(my - s.pred_y));
+  return mvc + ((int64_t)mine << 5);
+}
+
+__device__ __noinline__ int64_t eval_costs_v(const uint8_t *ref, int pitch, int W, int H, const uint32_t *cur,
+                                              int pos_x, int pos_y, int bsx, int bsy, int pred_x, int pred_y,
+                                              int lambda, int lane, int K, int mx, int my) {
+  Search s;
+  s.ref = ref;
+  s.pitch = pitch;
+  s.W = W;
+  s.H = H;
+  s.cur = cur;
+  s.pos_x = pos_x;
+  s.pos_y = pos_y;
+  s.bsx = bsx;
+  s.bsy = bsy;
+  s.pred_x = pred_x;
+  s.pred_y = pred_y;
+  s.lambda = lambda;
+  switch ((bsx << 8) | bsy) {
+    case (16 << 8) | 16: return eval_t<4, 4>(s, lane, K, mx, my);
+    case (16 << 8) | 8: return eval_t<4, 3>(s, lane, K, mx, my);
+    case (8 << 8) | 16: return eval_t<2, 4>(s, lane, K, mx, my);
+    case (8 << 8) | 8: return eval_t<2, 3>(s, lane, K, mx, my);
+    case (8 << 8) | 4: return eval_t<2, 2>(s, lane, K, mx, my);
+    case (4 << 8) | 8: return eval_t<1, 3>(s, lane, K, mx, my);
+    default: return eval_t<1, 2>(s, lane, K, mx, my);
   }
 }
 
-// mv_cost + (computeSAD << 5) of an integer qpel vector
-__device__ __forceinline__ int64_t cand_cost(const Search &s, int mx, int my) {
-  const int64_t mvc = (int64_t)s.lambda * (mvbits(mx - s.pred_x) + mvbits(my - s.pred_y));
-  const unsigned sad =
-      block_sad(s.ref, s.pitch, s.W, s.H, s.cur, (s.bsx << 8) | s.bsy, s.pos_x + (mx >> 2), s.pos_y + (my >> 2));
-  return mvc + ((int64_t)sad << 5);
+// scalar arguments keep the out-of-line call's context in registers
+__device__ __forceinline__ int64_t eval_costs(const Search &s, int lane, int K, int mx, int my) {
+  return eval_costs_v(s.ref, s.pitch, s.W, s.H, s.cur, s.pos_x, s.pos_y, s.bsx, s.bsy, s.pred_x, s.pred_y, s.lambda,
+                      lane, K, mx, my);
+}
+
+// order-preserving compaction of the lanes with `pred` set: returns the
+// packed position of this lane (valid where pred) and the count
+__device__ __forceinline__ int pack_index(bool pred, int &count) {
+  const unsigned long long m = __ballot(pred);
+  count = __popcll(m);
+  return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
 }
 
 __device__ __forceinline__ bool in_range(const Search &s, int mx, int my) {
@@ -198,7 +231,7 @@ __device__ void search_one(const EpzsParams &p, const jmme_epzs_req &q, WaveLds 
   const int64_t lambda_dist = (int64_t)q.lambda * (variant ? 3 : 2);
   const int mv_range = variant ? 12 : 10;
   int64_t stop = q.medthres + lambda_dist, prev = q.prev_sad;
-  int64_t best = cand_cost(s, s.cx, s.cy);   // every lane, same addresses
+  int64_t best = __shfl(eval_costs(s, lane, 1, s.cx, s.cy), 0, 64);
   int tmpx = s.cx, tmpy = s.cy, path = 5;
   bool update = true;
 
@@ -227,40 +260,53 @@ __device__ void search_one(const EpzsParams &p, const jmme_epzs_req &q, WaveLds 
       const bool inr = valid && in_range(s, mx, my);
       const int cell = inr ? cell_of(s, mx, my) : -1 - lane;
       bool dup = inr && test_cell(s, cell);
-      for (int j = 0; j < 63; ++j) {   // an earlier predictor of this chunk on the same cell
+      const int cnt = min(64, q.n_pred - base);
+      for (int j = 0; j < cnt - 1; ++j) {   // an earlier predictor of this chunk on the same cell
         const int cj = __shfl(cell, j, 64);
         dup |= j < lane && cj == cell;
       }
       const bool eval = inr && !dup;
-      const int64_t cost = eval ? cand_cost(s, mx, my) : 0;
       if (eval) set_cell(s, cell);
+      int ke;
+      const int k = pack_index(eval, ke);
+      if (eval) {
+        w.pk[k][0] = mx;
+        w.pk[k][1] = my;
+      }
       wave_sync();
-      const unsigned long long emask = __ballot(eval);
-      const int cnt = min(64, q.n_pred - base);
-      for (int j = 0; j < cnt; ++j) {
-        if ((emask >> j) & 1ull) {
-          const int64_t c = __shfl(cost, j, 64);
-          const int jx = __shfl(mx, j, 64), jy = __shfl(my, j, 64);
-          if (c < best) {
-            tmp2x = tmpx;
-            tmp2y = tmpy;
-            tmpx = jx;
-            tmpy = jy;
-            second = best;
-            best = c;
-            check_median = true;
-          } else if (c < second) {
-            tmp2x = jx;
-            tmp2y = jy;
-            second = c;
-            check_median = true;
-          }
+      const int px = lane < ke ? w.pk[lane][0] : 0, py = lane < ke ? w.pk[lane][1] : 0;
+      wave_sync();
+      const int64_t cost = eval_costs(s, lane, ke, px, py);
+      const int64_t thr3 = (3 * stop) >> 2;
+      // me_epzs.c:583-596 checks after every predictor; between updates the
+      // minimum is unchanged, so checking after index 0 and after each
+      // evaluated one is the same
+      if (variant && base == 0 && !(__ballot(eval) & 1ull) && best < thr3) {
+        path = 3;
+        update = false;
+        done = true;
+      }
+      for (int j = 0; !done && j < ke; ++j) {
+        const int64_t c = __shfl(cost, j, 64);
+        const int jx = __shfl(px, j, 64), jy = __shfl(py, j, 64);
+        if (c < best) {
+          tmp2x = tmpx;
+          tmp2y = tmpy;
+          tmpx = jx;
+          tmpy = jy;
+          second = best;
+          best = c;
+          check_median = true;
+        } else if (c < second) {
+          tmp2x = jx;
+          tmp2y = jy;
+          second = c;
+          check_median = true;
         }
-        if (variant && best < ((3 * stop) >> 2)) {   // me_epzs.c:583-596
+        if (variant && best < thr3) {
           path = 3;
           update = false;
           done = true;
-          break;
         }
       }
     }
@@ -286,19 +332,26 @@ __device__ void search_one(const EpzsParams &p, const jmme_epzs_req &q, WaveLds 
           const bool inr = active && in_range(s, mx, my);
           const int cell = inr ? cell_of(s, mx, my) : 0;
           const bool eval = inr && !test_cell(s, cell);
-          const int64_t cost = eval ? cand_cost(s, mx, my) : 0;
           if (eval) set_cell(s, cell);
+          int ke;
+          const int k = pack_index(eval, ke);
+          if (eval) {
+            w.pk[k][0] = mx;
+            w.pk[k][1] = my;
+            w.pk[k][2] = idx;
+          }
           wave_sync();
-          const unsigned long long emask = __ballot(eval);
-          for (int j = 0; j < total; ++j) {
-            if ((emask >> j) & 1ull) {
-              const int64_t c = __shfl(cost, j, 64);
-              if (c < best) {
-                best = c;
-                tmpx = __shfl(mx, j, 64);
-                tmpy = __shfl(my, j, 64);
-                dir = __shfl(idx, j, 64);
-              }
+          const int px = lane < ke ? w.pk[lane][0] : 0, py = lane < ke ? w.pk[lane][1] : 0;
+          const int pi = lane < ke ? w.pk[lane][2] : 0;
+          wave_sync();
+          const int64_t cost = eval_costs(s, lane, ke, px, py);
+          for (int j = 0; j < ke; ++j) {
+            const int64_t c = __shfl(cost, j, 64);
+            if (c < best) {
+              best = c;
+              tmpx = __shfl(px, j, 64);
+              tmpy = __shfl(py, j, 64);
+              dir = __shfl(pi, j, 64);
             }
           }
           if (next_last || (tmpx == cenx && tmpy == ceny)) {
