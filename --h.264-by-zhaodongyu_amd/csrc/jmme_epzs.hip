@@ -187,6 +187,13 @@ __device__ __forceinline__ int cell_of(const Search &s, int mx, int my) {
 __device__ __forceinline__ bool test_cell(const Search &s, int c) { return (s.map[c >> 5] >> (c & 31)) & 1u; }
 __device__ __forceinline__ void set_cell(const Search &s, int c) { atomicOr(&s.map[c >> 5], 1u << (c & 31)); }
 
+// value of lane j (j wave-uniform) as a scalar
+__device__ __forceinline__ int rl(int v, int j) { return __builtin_amdgcn_readlane(v, j); }
+__device__ __forceinline__ int64_t rl64(int64_t v, int j) {
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, j), hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), j);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
 __device__ __forceinline__ int16_t int_mv(int v) { return (int16_t)(v & 0xFFFC); }   // set_integer_mv
 
 __device__ void search_one(const EpzsParams &p, const jmme_epzs_req &q, WaveLds &w, int lane, jmme_epzs_res *out) {
@@ -231,7 +238,7 @@ __device__ void search_one(const EpzsParams &p, const jmme_epzs_req &q, WaveLds 
   const int64_t lambda_dist = (int64_t)q.lambda * (variant ? 3 : 2);
   const int mv_range = variant ? 12 : 10;
   int64_t stop = q.medthres + lambda_dist, prev = q.prev_sad;
-  int64_t best = __shfl(eval_costs(s, lane, 1, s.cx, s.cy), 0, 64);
+  int64_t best = rl64(eval_costs(s, lane, 1, s.cx, s.cy), 0);
   int tmpx = s.cx, tmpy = s.cy, path = 5;
   bool update = true;
 
@@ -287,8 +294,8 @@ __device__ void search_one(const EpzsParams &p, const jmme_epzs_req &q, WaveLds 
         done = true;
       }
       for (int j = 0; !done && j < ke; ++j) {
-        const int64_t c = __shfl(cost, j, 64);
-        const int jx = __shfl(px, j, 64), jy = __shfl(py, j, 64);
+        const int64_t c = rl64(cost, j);
+        const int jx = rl(px, j), jy = rl(py, j);
         if (c < best) {
           tmp2x = tmpx;
           tmp2y = tmpy;
@@ -346,12 +353,12 @@ __device__ void search_one(const EpzsParams &p, const jmme_epzs_req &q, WaveLds 
           wave_sync();
           const int64_t cost = eval_costs(s, lane, ke, px, py);
           for (int j = 0; j < ke; ++j) {
-            const int64_t c = __shfl(cost, j, 64);
+            const int64_t c = rl64(cost, j);
             if (c < best) {
               best = c;
-              tmpx = __shfl(px, j, 64);
-              tmpy = __shfl(py, j, 64);
-              dir = __shfl(pi, j, 64);
+              tmpx = rl(px, j);
+              tmpy = rl(py, j);
+              dir = rl(pi, j);
             }
           }
           if (next_last || (tmpx == cenx && tmpy == ceny)) {
@@ -406,7 +413,13 @@ __device__ void search_one(const EpzsParams &p, const jmme_epzs_req &q, WaveLds 
   wave_sync();
 }
 
-__global__ __launch_bounds__(kWG) void epzs_kernel(EpzsParams p) {
+#ifndef JMME_EPZS_WAVES_PER_EU
+#define JMME_EPZS_WAVES_PER_EU 4
+#endif
+// the search is latency-bound (a few dependent cache-resident fetch rounds
+// per search): waves in flight matter more than a few spilled registers
+__global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(JMME_EPZS_WAVES_PER_EU))) void epzs_kernel(
+    EpzsParams p) {
   __shared__ WaveLds s_w[kWaves];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   for (int t = blockIdx.x * kWaves + wave; t < p.n; t += gridDim.x * kWaves) {
