@@ -1,0 +1,157 @@
+#!/usr/bin/env python3
+"""Generate the sub-pel golden fixtures from the REAL JM 18.5 encoder
+(getSubImagesLuma + the sub-pel refinements).
+
+Run in the build container only (needs /root/reference):
+    python tests/golden/make_golden_subpel.py [case ...]
+
+Same recipe as make_golden.py, with oracle/_ref/lencod_subpel_capture (the
+unmodified JM objects linked with oracle/capture/jm_subpel_capture.c): every
+sub-pel refinement JM runs (sub_pel_motion_estimation or
+EPZS_sub_pel_motion_estimation) is stored with its inputs and JM's (mv, cost)
+result, and the first `subimg` interpolations are stored as JM built them (the
+16 padded quarter-pel sub-images, 8-bit content) with their source picture.
+The fixtures are data (inputs and JM's outputs), not reference source.
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+sys.path.insert(0, os.path.join(REPO, "--h.264-by-zhaodongyu_amd"))
+
+from jm_capture import read_subpel_capture  # noqa: E402
+from jmme import synth  # noqa: E402
+from make_golden import BASE_CFG, FOREMAN, coded_synth, md5  # noqa: E402
+
+SUB = {"DisableSubpelME": 0, "EPZSSubPelGrid": 0}
+HIGH = {"ProfileIDC": 100, "Transform8x8Mode": 1}
+
+CASES = {
+    # BASELINE configs[0] with JM's default sub-pel ME: SATD half/quarter (start_hp 0, start_qp 1)
+    "subpel_foreman_fs16": dict(src="foreman", w=176, h=144, frames=3, subimg=2,
+                                p={"SearchMode": -1, "SearchRange": 16, **SUB}),
+    # RDO off, SAD everywhere: start_hp = start_qp = 1 (refinement continues from the integer cost)
+    "subpel_foreman_fs16_sad_rdo0": dict(src="foreman", w=176, h=144, frames=3,
+                                         p={"SearchMode": -1, "SearchRange": 16, "RDOptimization": 0,
+                                            "MDDistortion": 0, "MEDistortionHPel": 0, "MEDistortionQPel": 0,
+                                            **SUB}),
+    # SSE half-pel, SATD quarter-pel: start_qp 0 (the quarter-pel pass restarts from DISTBLK_MAX)
+    "subpel_foreman_ffs16_sse": dict(src="foreman", w=176, h=144, frames=3,
+                                     p={"SearchMode": 0, "SearchRange": 16, "MEDistortionHPel": 1,
+                                        "MEDistortionQPel": 2, **SUB}),
+    # High profile with the 8x8 transform: test8x8 -> HadamardSAD8x8 for 16x16/16x8/8x16/8x8
+    "subpel_foreman_fs16_t8x8": dict(src="foreman", w=176, h=144, frames=3,
+                                     p={"SearchMode": -1, "SearchRange": 16, **HIGH, **SUB}),
+    # EPZS with EPZS_sub_pel_motion_estimation (EPZSSubPelME 1, JM baseline cfg)
+    "subpel_epzs_foreman": dict(src="foreman", w=176, h=144, frames=3,
+                                p={"SearchMode": 3, **SUB}),
+    # EPZS, SAD half-pel / SATD quarter-pel, 8x8 transform
+    "subpel_epzs_foreman_sad_t8x8": dict(src="foreman", w=176, h=144, frames=3,
+                                         p={"SearchMode": 3, "MEDistortionHPel": 0, **HIGH, **SUB}),
+    # synthetic high-contrast CIF (clipping in the 6-tap filters), +-32, 3 refs, picture-edge vectors
+    "subpel_syn_cif_fs32_3ref": dict(src="synth", w=352, h=288, frames=4, seed=7, gmv=(5, 3), subimg=1,
+                                     p={"SearchMode": -1, "SearchRange": 32, "NumberReferenceFrames": 3,
+                                        **SUB}),
+    "subpel_syn_cif_epzs_3ref": dict(src="synth", w=352, h=288, frames=3, seed=9, gmv=(-6, 4),
+                                     p={"SearchMode": 3, "SearchRange": 32, "NumberReferenceFrames": 3,
+                                        **SUB}),
+    # BASELINE configs[1] with sub-pel ME on: one 1080p P-frame, FS +-32, RDO off
+    "subpel_syn_1080p_fs32": dict(src="synth", w=1920, h=1080, frames=2, seed=2024, gmv=(5, 3),
+                                  p={"SearchMode": -1, "SearchRange": 32, "NumberReferenceFrames": 1,
+                                     "RDOptimization": 0, "MDDistortion": 2, **SUB}, keep="compact"),
+}
+
+KEEP_FIELDS = ["kind", "frame_no", "blocktype", "pos_x", "pos_y", "bsx", "bsy", "list", "ref",
+               "pred_x", "pred_y", "mv_in_x", "mv_in_y", "min_mcost_in", "lambda_h", "lambda_q", "rdopt",
+               "slice_type", "start_hp", "start_qp", "metric_h", "metric_q", "test8x8", "search_pos2",
+               "search_pos4", "subthres", "out_mv_x", "out_mv_y", "out_cost"]
+
+
+def run_case(name: str, spec: dict, work: str) -> dict:
+    w, h, frames = spec["w"], spec["h"], spec["frames"]
+    if spec["src"] == "foreman":
+        yuv = FOREMAN
+    else:
+        yuv = os.path.join(work, f"{name}.yuv")
+        synth.write_yuv420(yuv, synth.luma_sequence(w, h, frames, seed=spec["seed"], gmv=spec["gmv"]))
+    cap = os.path.join(work, f"{name}.cap")
+    out264 = os.path.join(work, f"{name}.264")
+    rec = os.path.join(work, f"{name}_rec.yuv")
+    args = [os.path.join(REPO, "oracle", "_ref", "lencod_subpel_capture"), "-d", BASE_CFG,
+            "-p", f"InputFile={yuv}", "-p", f"SourceWidth={w}", "-p", f"SourceHeight={h}",
+            "-p", f"OutputWidth={w}", "-p", f"OutputHeight={h}",
+            "-p", f"FramesToBeEncoded={frames}", "-p", f"OutputFile={out264}", "-p", f"ReconFile={rec}"]
+    for k, v in spec["p"].items():
+        args += ["-p", f"{k}={v}"]
+    env = dict(os.environ, JMME_CAPTURE=cap, JMME_CAPTURE_SUBIMG=str(spec.get("subimg", 0)))
+    res = subprocess.run(args, cwd=work, env=env, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(res.stdout[-2000:] + res.stderr[-2000:])
+    me_time = [ln for ln in res.stdout.splitlines() if "Total ME time" in ln]
+    planes, subimgs, recs = read_subpel_capture(cap)
+    return dict(planes=planes, subimgs=subimgs, recs=recs, md5_264=md5(out264), md5_rec=md5(rec),
+                md5_input=md5(yuv), me_time=me_time[0].strip() if me_time else "",
+                cmd=" ".join(a if os.sep not in a else os.path.basename(a) for a in args[1:]))
+
+
+def save_case(name: str, spec: dict, r: dict) -> dict:
+    planes, recs = r["planes"], r["recs"]
+    cur_keys = sorted(k for k in planes if k[1] == 0)
+    ref_keys = sorted(k for k in planes if k[1] == 1)
+    src_keys = sorted(k for k in planes if k[1] == 2)
+    assert max(int(planes[k].max()) for k in cur_keys + ref_keys + src_keys) <= 255
+    assert (recs["chroma_me"] == 0).all() and (recs["metric_h"] >= 0).all() and (recs["metric_q"] >= 0).all()
+    cur = np.stack([planes[k] for k in cur_keys]).astype(np.uint8)
+    ref = np.stack([planes[k] for k in ref_keys]).astype(np.uint8)
+    arrays = {"cur_frame_no": np.array([k[0] for k in cur_keys], np.int32),
+              "ref_key": np.array([[k[0], k[2], k[3]] for k in ref_keys], np.int32),
+              "cur_md5": np.array([hashlib.md5(c.tobytes()).hexdigest() for c in cur])}
+    if spec.get("keep") == "compact":
+        orig = coded_synth(spec)
+        assert all(np.array_equal(cur[i], orig[f]) for i, f in enumerate(arrays["cur_frame_no"]))
+        res = ref.astype(np.int16) - orig[arrays["ref_key"][:, 0] - 1 - arrays["ref_key"][:, 2]]
+        assert res.min() >= -128 and res.max() <= 127
+        arrays["ref_residual"] = res.astype(np.int8)
+    else:
+        arrays["cur"] = cur
+        arrays["ref"] = ref
+    if src_keys:
+        arrays["sub_src"] = np.stack([planes[k] for k in src_keys]).astype(np.uint8)
+        arrays["sub_img"] = np.stack([r["subimgs"][k[0]] for k in src_keys]).astype(np.uint8)
+    for f in KEEP_FIELDS:
+        arrays["r_" + f] = recs[f]
+    path = os.path.join(HERE, f"{name}.npz")
+    np.savez_compressed(path, **arrays)
+    return dict(case=name, kind="subpel", w=spec["w"], h=spec["h"], frames=spec["frames"],
+                cfg_overrides=spec["p"], src=spec["src"], seed=spec.get("seed"), gmv=spec.get("gmv"),
+                adversarial=False, n_searches=int(len(recs)), n_subimg=len(src_keys),
+                md5_bitstream=r["md5_264"], md5_recon=r["md5_rec"], md5_input=r["md5_input"],
+                jm_me_time=r["me_time"], jm_cmd=r["cmd"], bytes=os.path.getsize(path))
+
+
+def main(argv):
+    names = argv or list(CASES)
+    subprocess.run(["make", "-s", "-C", os.path.join(REPO, "oracle"), "-j8", "ref"], check=True)
+    mpath = os.path.join(HERE, "manifest.json")
+    manifest = json.load(open(mpath)) if os.path.exists(mpath) else {}
+    with tempfile.TemporaryDirectory() as work:
+        for n in names:
+            r = run_case(n, CASES[n], work)
+            manifest[n] = save_case(n, CASES[n], r)
+            print(n, manifest[n]["n_searches"], "refinements,", manifest[n]["n_subimg"], "sub-image sets,",
+                  manifest[n]["bytes"], "bytes", r["me_time"])
+    json.dump(manifest, open(mpath, "w"), indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])

@@ -27,7 +27,7 @@ def manifest() -> dict:
 
 def cases() -> list[str]:
     """The motion-search cases (captured JM encodes); other fixtures, e.g. tq_jm, are not searches."""
-    return sorted(k for k, v in manifest().items() if "cfg_overrides" in v)
+    return sorted(k for k, v in manifest().items() if "cfg_overrides" in v and "kind" not in v)
 
 
 class Case:
@@ -37,7 +37,7 @@ class Case:
         self.meta = manifest()[name]
         z = np.load(os.path.join(GOLDEN, f"{name}.npz"))
         self.r = {k[2:]: z[k] for k in z.files if k.startswith("r_")}
-        self.n = len(self.r["mode"])
+        self.n = len(next(iter(self.r.values())))
         cur_fn = z["cur_frame_no"]
         ref_key = z["ref_key"]
         if "cur" in z.files:

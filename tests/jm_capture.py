@@ -110,3 +110,54 @@ def read_epzs_capture(path: str):
         else:
             raise ValueError(f"bad tag {tag:#x} at {off - 4}")
     return planes, np.array(recs, dtype=EPZS_DTYPE), preds, stale
+
+
+# ---- sub-pel capture (oracle/capture/jm_subpel_capture.c) -------------------
+SUBPEL_DTYPE = np.dtype([
+    ("kind", "<i4"), ("frame_no", "<i4"), ("mb_addr", "<i4"),
+    ("pix_x", "<i2"), ("pix_y", "<i2"),
+    ("blocktype", "<i2"), ("block_x", "<i2"), ("block_y", "<i2"),
+    ("pos_x", "<i2"), ("pos_y", "<i2"), ("bsx", "<i2"), ("bsy", "<i2"),
+    ("list", "<i2"), ("ref", "<i2"),
+    ("pred_x", "<i2"), ("pred_y", "<i2"), ("mv_in_x", "<i2"), ("mv_in_y", "<i2"),
+    ("min_mcost_in", "<i8"),
+    ("lambda_f", "<i4"), ("lambda_h", "<i4"), ("lambda_q", "<i4"),
+    ("rdopt", "<i4"), ("slice_type", "<i4"), ("start_hp", "<i4"), ("start_qp", "<i4"),
+    ("metric_h", "<i4"), ("metric_q", "<i4"), ("test8x8", "<i4"),
+    ("search_pos2", "<i4"), ("search_pos4", "<i4"), ("chroma_me", "<i4"),
+    ("subthres", "<i8"), ("img_w", "<i4"), ("img_h", "<i4"),
+    ("out_mv_x", "<i2"), ("out_mv_y", "<i2"), ("out_cost", "<i8"),
+])
+TAG_SUBPEL = 0x304C5053
+TAG_SUBIMG = 0x30425553
+
+
+def read_subpel_capture(path: str):
+    """Return (planes, subimgs, records): planes as read_capture (kind 2 = the
+    source of an interpolation, keyed by its sequence number); subimgs {seq:
+    uint16 [16, H+40, W+64]}; records SUBPEL_DTYPE in call order."""
+    buf = open(path, "rb").read()
+    mv = memoryview(buf)
+    off, n = 0, len(buf)
+    planes, subimgs, recs = {}, {}, []
+    rsz = SUBPEL_DTYPE.itemsize
+    while off < n:
+        tag = int.from_bytes(mv[off:off + 4], "little")
+        off += 4
+        if tag == TAG_PLANE:
+            frame_no, kind, lst, ref, w, h = (int(v) for v in np.frombuffer(mv[off:off + 24], dtype="<i4"))
+            off += 24
+            planes[(frame_no, kind, lst, ref)] = np.frombuffer(mv[off:off + 2 * w * h], "<u2").reshape(h, w).copy()
+            off += 2 * w * h
+        elif tag == TAG_SUBIMG:
+            seq, w, h = (int(v) for v in np.frombuffer(mv[off:off + 12], dtype="<i4"))
+            off += 12
+            cnt = 16 * (h + 40) * (w + 64)
+            subimgs[seq] = np.frombuffer(mv[off:off + 2 * cnt], "<u2").reshape(16, h + 40, w + 64).copy()
+            off += 2 * cnt
+        elif tag == TAG_SUBPEL:
+            recs.append(np.frombuffer(mv[off:off + rsz], dtype=SUBPEL_DTYPE)[0])
+            off += rsz
+        else:
+            raise ValueError(f"bad tag {tag:#x} at {off - 4}")
+    return planes, subimgs, np.array(recs, dtype=SUBPEL_DTYPE)

@@ -294,3 +294,53 @@ def epzs_batch(req, preds, stale, cur, refs):
     lib.eo_epzs_batch(req.ctypes.data, len(req), preds.ctypes.data, stale.ctypes.data, cur.ctypes.data, ptrs, w, w, h,
                       out.ctypes.data)
     return out
+
+
+# ---- sub-pel interpolation and refinement (oracle/subpel_oracle.c) ----------
+SPO_REQ = np.dtype([("pos_x", "<i4"), ("pos_y", "<i4"), ("bsx", "<i4"), ("bsy", "<i4"), ("blocktype", "<i4"),
+                    ("ref", "<i4"), ("pred_x", "<i4"), ("pred_y", "<i4"), ("mv_x", "<i4"), ("mv_y", "<i4"),
+                    ("min_mcost", "<i8"), ("lambda_h", "<i4"), ("lambda_q", "<i4"), ("rdopt", "<i4"),
+                    ("slice_type", "<i4"), ("start_hp", "<i4"), ("start_qp", "<i4"), ("metric_h", "<i4"),
+                    ("metric_q", "<i4"), ("test8x8", "<i4"), ("search_pos2", "<i4"), ("search_pos4", "<i4"),
+                    ("pad", "<i4"), ("subthres", "<i8")], align=True)
+SP_SO = os.path.join(ORACLE_DIR, "build", "libsubpel_oracle.so")
+_sp = None
+
+
+def load_subpel() -> ctypes.CDLL:
+    global _sp
+    if _sp is not None:
+        return _sp
+    src = os.path.join(ORACLE_DIR, "subpel_oracle.c")
+    if not os.path.exists(SP_SO) or os.path.getmtime(SP_SO) < os.path.getmtime(src):
+        subprocess.run(["make", "-s", "-C", ORACLE_DIR, "port"], check=True)
+    lib = ctypes.CDLL(SP_SO)
+    P, I = ctypes.c_void_p, ctypes.c_int
+    lib.spo_sub_images.argtypes = [P, I, I, P]
+    lib.spo_sub_pel_batch.argtypes = [P, P, I, I, P, I, I, P, P]
+    _sp = lib
+    return lib
+
+
+def sub_images(plane: np.ndarray) -> np.ndarray:
+    """getSubImagesLuma of an HxW plane -> uint16 [16, H+40, W+64] (JM's padded sub-images)"""
+    lib = load_subpel()
+    src = np.ascontiguousarray(plane, np.uint16)
+    h, w = src.shape
+    out = np.zeros((16, h + 40, w + 64), np.uint16)
+    lib.spo_sub_images(src.ctypes.data, w, h, out.ctypes.data)
+    return out
+
+
+def sub_pel_batch(cur: np.ndarray, sub: np.ndarray, req: np.ndarray, epzs: bool):
+    """req SPO_REQ[n] against one reference's sub-images -> (mv int16 [n,2], cost int64 [n])"""
+    lib = load_subpel()
+    cur = np.ascontiguousarray(cur, np.uint16)
+    sub = np.ascontiguousarray(sub, np.uint16)
+    req = np.ascontiguousarray(req, SPO_REQ)
+    h, w = cur.shape
+    mv = np.zeros((len(req), 2), np.int16)
+    cost = np.zeros(len(req), np.int64)
+    lib.spo_sub_pel_batch(cur.ctypes.data, sub.ctypes.data, w, h, req.ctypes.data, len(req), int(epzs),
+                          mv.ctypes.data, cost.ctypes.data)
+    return mv, cost
