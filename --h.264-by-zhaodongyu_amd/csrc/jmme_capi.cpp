@@ -18,6 +18,7 @@
 #include "jmme_tq_internal.h"
 #include "jmme_epzs_internal.h"
 #include "jmme_fractal_internal.h"
+#include "jmme_subpel_internal.h"
 
 using namespace jmme;
 
@@ -65,6 +66,11 @@ struct jmme_ctx {
   size_t cap_items = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
+  // quarter-pel sub-images per reference slot (getSubImagesLuma), built lazily
+  uint8_t *d_subs[kMaxLists * kMaxRefs] = {};
+  bool sub_stale[kMaxLists * kMaxRefs] = {};
+  const uint8_t **d_sub_table = nullptr;     // device copy of d_subs
+  bool sub_table_dirty = true;
 };
 
 // ----------------------------------------------------------------- config --
@@ -212,6 +218,7 @@ extern "C" jmme_ctx *jmme_create(const jmme_config *cfg, int device) {
   (void)hipGetDevice(&ctx->device);
   if ((e = hipMalloc(&ctx->d_ref_table, sizeof(uint8_t *) * kMaxLists * kMaxRefs)) != hipSuccess ||
       (e = hipMalloc(&ctx->d_counts, 16)) != hipSuccess ||
+      (e = hipMalloc(&ctx->d_sub_table, sizeof(uint8_t *) * kMaxLists * kMaxRefs)) != hipSuccess ||
       (e = hipEventCreate(&ctx->ev0)) != hipSuccess || (e = hipEventCreate(&ctx->ev1)) != hipSuccess) {
     fail("jmme_create: %s", hipGetErrorString(e));
     jmme_destroy(ctx);
@@ -231,6 +238,8 @@ extern "C" void jmme_destroy(jmme_ctx *ctx) {
   (void)hipFree(ctx->d_items);
   (void)hipFree(ctx->d_stamps);
   (void)hipFree(ctx->d_tree);
+  for (auto *p : ctx->d_subs) (void)hipFree(p);
+  (void)hipFree(ctx->d_sub_table);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
   delete ctx;
@@ -283,6 +292,7 @@ extern "C" int jmme_upload_ref(jmme_ctx *ctx, int list, int ref_idx, const jmme_
   bool fresh = *slot == nullptr;
   if (upload_plane(ctx, slot, rows, w, h)) return -1;
   if (fresh) ctx->ref_table_dirty = true;
+  ctx->sub_stale[list * kMaxRefs + ref_idx] = true;
   return 0;
 }
 
@@ -957,3 +967,158 @@ extern "C" int jmme_debug_stamps(jmme_ctx *ctx, uint64_t *out, int max_units) {
   HIPCHK(hipMemcpy(out, ctx->d_stamps, n * 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
   return (int)n;
 }
+
+// ------------------------------------------------------------- sub-pel ME --
+// getSubImagesLuma (img_luma.c:611-680) + sub_pel_motion_estimation /
+// EPZS_sub_pel_motion_estimation (me_fullsearch.c:186-289, me_epzs_sub.c:30-222)
+namespace {
+
+int build_sub_images(jmme_ctx *ctx, int slot, hipStream_t s) {
+  if (!ctx->d_refs[slot]) return fail("reference slot %d not uploaded", slot);
+  const SubGeom g = sub_geom(ctx->width, ctx->height);
+  if (!ctx->d_subs[slot]) {
+    HIPCHK(hipMalloc(&ctx->d_subs[slot], 16 * g.plane_stride));
+    ctx->sub_table_dirty = true;
+  }
+  HIPCHK(launch_sub_images(ctx->d_refs[slot], ctx->pitch, ctx->width, ctx->height, ctx->d_subs[slot], g.pitch,
+                           g.plane_stride, s));
+  ctx->sub_stale[slot] = false;
+  return 0;
+}
+
+// build every stale uploaded slot, then publish the table
+int prepare_subs(jmme_ctx *ctx, hipStream_t s) {
+  for (int k = 0; k < kMaxLists * kMaxRefs; ++k)
+    if (ctx->d_refs[k] && (ctx->sub_stale[k] || !ctx->d_subs[k]))
+      if (build_sub_images(ctx, k, s)) return -1;
+  if (ctx->sub_table_dirty) {
+    HIPCHK(hipMemcpyAsync(ctx->d_sub_table, ctx->d_subs, sizeof(ctx->d_subs), hipMemcpyHostToDevice, s));
+    HIPCHK(hipStreamSynchronize(s));
+    ctx->sub_table_dirty = false;
+  }
+  return 0;
+}
+
+}  // namespace
+
+extern "C" int jmme_interpolate_ref(jmme_ctx *ctx, int list, int ref_idx, void *stream) {
+  if (!ctx) return fail("null ctx");
+  if (list < 0 || list >= kMaxLists || ref_idx < 0 || ref_idx >= kMaxRefs)
+    return fail("list/ref_idx (%d,%d) out of range", list, ref_idx);
+  return build_sub_images(ctx, list * kMaxRefs + ref_idx, reinterpret_cast<hipStream_t>(stream));
+}
+
+extern "C" int jmme_get_sub_images(jmme_ctx *ctx, int list, int ref_idx, jmme_imgpel ****sub) {
+  if (!ctx) return fail("null ctx");
+  if (!sub) return fail("null sub-image array");
+  if (list < 0 || list >= kMaxLists || ref_idx < 0 || ref_idx >= kMaxRefs)
+    return fail("list/ref_idx (%d,%d) out of range", list, ref_idx);
+  const int slot = list * kMaxRefs + ref_idx;
+  if (!ctx->d_refs[slot]) return fail("reference slot %d not uploaded", slot);
+  if ((ctx->sub_stale[slot] || !ctx->d_subs[slot]) && build_sub_images(ctx, slot, nullptr)) return -1;
+  const SubGeom g = sub_geom(ctx->width, ctx->height);
+  std::vector<uint8_t> h(16 * g.plane_stride);
+  HIPCHK(hipMemcpy(h.data(), ctx->d_subs[slot], h.size(), hipMemcpyDeviceToHost));
+  for (int k = 0; k < 16; ++k) {
+    jmme_imgpel **rows = sub[k >> 2][k & 3];
+    if (!rows) return fail("null row array for sub-image [%d][%d]", k >> 2, k & 3);
+    for (int j = 0; j < g.ph; ++j) {
+      jmme_imgpel *d = rows[j - JMME_SUBPEL_PAD_Y];
+      if (!d) return fail("null row %d of sub-image [%d][%d]", j - JMME_SUBPEL_PAD_Y, k >> 2, k & 3);
+      d -= JMME_SUBPEL_PAD_X;
+      const uint8_t *srow = &h[(size_t)k * g.plane_stride + (size_t)j * g.pitch];
+      for (int i = 0; i < g.pw; ++i) d[i] = srow[i];
+    }
+  }
+  return 0;
+}
+
+extern "C" int jmme_sub_images_async(jmme_ctx *ctx, const uint8_t *d_src, int src_pitch, int width, int height,
+                                     uint8_t *d_dst, int dst_pitch, size_t plane_stride, void *stream) {
+  if (!ctx) return fail("null ctx");
+  if (!d_src || !d_dst) return fail("null plane");
+  if (width <= 0 || height <= 0 || src_pitch < width) return fail("bad source plane %dx%d pitch %d", width, height,
+                                                                    src_pitch);
+  const int pw = width + 2 * JMME_SUBPEL_PAD_X, ph = height + 2 * JMME_SUBPEL_PAD_Y;
+  if (dst_pitch < ((pw + 3) & ~3) || (dst_pitch & 3) || (reinterpret_cast<uintptr_t>(d_dst) & 3))
+    return fail("sub-image pitch %d: need a multiple of 4 >= %d and a 4-byte aligned buffer", dst_pitch, pw);
+  if (plane_stride < (size_t)ph * dst_pitch || (plane_stride & 3)) return fail("sub-image plane stride too small");
+  HIPCHK(launch_sub_images(d_src, src_pitch, width, height, d_dst, dst_pitch, plane_stride,
+                           reinterpret_cast<hipStream_t>(stream)));
+  return 0;
+}
+
+extern "C" int jmme_subpel_validate(jmme_ctx *ctx, const jmme_subpel_req *req, int n) {
+  if (!ctx) return fail("null ctx");
+  if (n < 0) return fail("negative request count");
+  if (n && !req) return fail("null request array");
+  if (!ctx->d_cur) return fail("no current frame uploaded");
+  for (int i = 0; i < n; ++i) {
+    const jmme_subpel_req &q = req[i];
+    if (q.blocktype == 0) continue;
+    if (q.blocktype < 1 || q.blocktype > 7) return fail("request %d: blocktype %d", i, q.blocktype);
+    const int bsx = (q.blocktype <= 2) ? 16 : (q.blocktype <= 5) ? 8 : 4;
+    const int bsy = (q.blocktype == 1 || q.blocktype == 3) ? 16 : (q.blocktype == 2 || q.blocktype == 4 ||
+                                                                   q.blocktype == 6) ? 8 : 4;
+    if (q.pos_x < 0 || q.pos_y < 0 || (q.pos_x & 3) || (q.pos_y & 3) || q.pos_x + bsx > ctx->width ||
+        q.pos_y + bsy > ctx->height)
+      return fail("request %d: block (%d,%d) %dx%d outside the %dx%d picture", i, q.pos_x, q.pos_y, bsx, bsy,
+                  ctx->width, ctx->height);
+    if (q.ref_slot < 0 || q.ref_slot >= kMaxLists * kMaxRefs || !ctx->d_refs[q.ref_slot])
+      return fail("request %d: reference slot %d not uploaded", i, q.ref_slot);
+    if (q.variant > 1) return fail("request %d: variant %d", i, q.variant);
+    if (q.metric_h > 2 || q.metric_q > 2) return fail("request %d: metric %d/%d", i, q.metric_h, q.metric_q);
+    if (q.start_hp > 1 || q.start_qp > 1) return fail("request %d: start_hp/qp", i);
+    if (q.search_pos2 > 9 || q.search_pos4 > 9)
+      return fail("request %d: search_pos2/4 %d/%d beyond JM's 9-point rings", i, q.search_pos2, q.search_pos4);
+    if ((q.flags & JMME_SP_TEST8x8) && (bsx < 8 || bsy < 8))
+      return fail("request %d: test8x8 on a %dx%d block", i, bsx, bsy);
+    if (q.min_mcost < 0 || q.min_mcost > JMME_DISTBLK_MAX) return fail("request %d: min_mcost out of range", i);
+    if (q.lambda_h < 0 || q.lambda_q < 0) return fail("request %d: negative lambda", i);
+    // the refined vector stays within +-(3/4 pel) of mv; mvbits is closed-form for any difference
+    if (std::abs(q.mv_x) > 8192 || std::abs(q.mv_y) > 8192) return fail("request %d: mv out of range", i);
+  }
+  return 0;
+}
+
+extern "C" int jmme_subpel_refine_async(jmme_ctx *ctx, const jmme_subpel_req *d_req, int n,
+                                        const jmme_block_res *d_int, jmme_block_res *d_out, void *stream) {
+  if (!ctx) return fail("null ctx");
+  if (n < 0) return fail("negative request count");
+  if (n == 0) return 0;
+  if (!d_req || !d_out) return fail("null array");
+  if (!ctx->d_cur) return fail("no current frame uploaded");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (prepare_subs(ctx, s)) return -1;
+  const SubGeom g = sub_geom(ctx->width, ctx->height);
+  SubpelParams p;
+  p.cur = ctx->d_cur;
+  p.cur_pitch = ctx->pitch;
+  p.width = ctx->width;
+  p.height = ctx->height;
+  p.subs = ctx->d_sub_table;
+  p.sub_pitch = g.pitch;
+  p.plane_stride = g.plane_stride;
+  p.req = d_req;
+  p.int_res = d_int;
+  p.out = d_out;
+  p.n = n;
+  HIPCHK(launch_subpel(p, s));
+  return 0;
+}
+
+extern "C" int jmme_subpel_refine(jmme_ctx *ctx, const jmme_subpel_req *req, int n, jmme_block_res *out) {
+  if (jmme_subpel_validate(ctx, req, n)) return -1;
+  if (n == 0) return 0;
+  if (!out) return fail("null output array");
+  DevBuf dq, dout;
+  HIPCHK(dq.alloc((size_t)n * sizeof(jmme_subpel_req)));
+  HIPCHK(dout.alloc((size_t)n * sizeof(jmme_block_res)));
+  HIPCHK(hipMemcpy(dq.p, req, (size_t)n * sizeof(jmme_subpel_req), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dout.p, out, (size_t)n * sizeof(jmme_block_res), hipMemcpyHostToDevice));
+  if (jmme_subpel_refine_async(ctx, (const jmme_subpel_req *)dq.p, n, nullptr, (jmme_block_res *)dout.p, nullptr))
+    return -1;
+  HIPCHK(hipMemcpy(out, dout.p, (size_t)n * sizeof(jmme_block_res), hipMemcpyDeviceToHost));
+  return 0;
+}
+static_assert(sizeof(jmme_subpel_req) == 48, "sub-pel ABI layout");

@@ -1,0 +1,487 @@
+// jmme_subpel.hip -- gfx950 kernels for JM 18.5's quarter-pel reference
+// interpolation and sub-pel motion refinement,
+// JM = /root/reference/4.对比程序/jm18.5/JM:
+//
+//   getSubImagesLuma               JM/lencod/src/img_luma.c:611-680 (six-tap :151-431,
+//                                  bilinear :448-600, taps img_luma.h:21)
+//   sub_pel_motion_estimation      JM/lencod/src/me_fullsearch.c:186-289
+//   EPZS_sub_pel_motion_estimation JM/lencod/src/me_epzs_sub.c:30-222 (tables me_epzs.h:23-42)
+//   computeSAD / computeSSE / computeSATD, HadamardSAD4x4 / 8x8
+//                                  JM/lencod/src/me_distortion.c:175-426, 745-825, 1189-1240
+//   UMVLine4X                      JM/lencod/inc/refbuf.h:22-26
+//
+// Interpolation.  Every JM sub-image, including its padding, equals the
+// filter evaluated on the edge-replicated picture (JM clamps each tap into
+// the padded plane, whose border is itself a replica), so a 16 x 64 output
+// tile needs only a 22 x 73 integer tile with clamped reads.  One thread
+// makes 4 columns of one row for all 16 sub-images: 24 horizontal and 5
+// vertical six-tap sums, the (+512)>>10 centre sample, then the 12 bilinear
+// averages, written as one dword per sub-image.  The kernel is a one-pass
+// stream: 1 B read, 16 B written per padded sample (HBM roofline).
+//
+// Refinement.  One wave per refinement.  Each phase of JM's loop (the half-pel
+// ring, the quarter-pel ring; EPZS: first ring, the next_start_pos..
+// next_end_pos follow-up, for both levels) costs all its candidates at once,
+// one lane per (candidate, 4x4 or 8x8 block), group sums reduced with xor
+// shuffles; the fold then walks the candidates in JM's order with JM's
+// comparisons.  JM's distortion functions stop early and return their bound
+// T once the partial sum exceeds T >> 5; sums only grow, so that happens
+// exactly when the full sum does, and the fold computes the same value:
+// d = (sum > T >> 5) ? T : sum << 5.
+#include <hip/hip_runtime.h>
+
+#include "jmme.h"
+#include "jmme_common.h"
+#include "jmme_subpel_internal.h"
+
+namespace jmme {
+
+namespace {
+
+constexpr int64_t kDistMax = ((int64_t)0x7fffffff) << 5;   // DISTBLK_MAX, JM/lencod/inc/defines.h:135
+constexpr int kPadY = JMME_SUBPEL_PAD_Y, kPadX = JMME_SUBPEL_PAD_X;
+
+__device__ __forceinline__ int clip255(int v) { return min(max(v, 0), 255); }
+__device__ __forceinline__ int avg2(int a, int b) { return (a + b + 1) >> 1; }   // rshift_rnd_sf(a + b, 1)
+__device__ __forceinline__ int six(int c, int d, int b, int e, int a, int f) {   // ONE_FOURTH_TAP {20, -5, 1}
+  return 20 * (c + d) - 5 * (b + e) + (a + f);
+}
+__device__ __forceinline__ uint32_t pack4(int a, int b, int c, int d) {
+  return (uint32_t)a | ((uint32_t)b << 8) | ((uint32_t)c << 16) | ((uint32_t)d << 24);
+}
+
+// ------------------------------------------------------------ sub-images --
+constexpr int kTileW = 64, kTileH = 16, kSW = 80, kSH = kTileH + 6;
+
+__global__ __launch_bounds__(256) void sub_images_kernel(const uint8_t *__restrict__ src, int src_pitch, int W, int H,
+                                                         uint8_t *__restrict__ dst, int dst_pitch, size_t plane_stride,
+                                                         int pw, int ph) {
+  __shared__ uint8_t S[kSH][kSW];
+  const int X0 = blockIdx.x * kTileW, Y0 = blockIdx.y * kTileH;   // padded output coordinates
+  // S[r][c] = picture sample (Y0 - kPadY - 2 + r, X0 - kPadX - 2 + c), clamped
+  for (int k = threadIdx.x; k < kSH * kSW; k += 256) {
+    const int r = k / kSW, c = k - r * kSW;
+    const int y = min(max(Y0 - kPadY - 2 + r, 0), H - 1), x = min(max(X0 - kPadX - 2 + c, 0), W - 1);
+    S[r][c] = src[(size_t)y * src_pitch + x];
+  }
+  __syncthreads();
+  const int ty = threadIdx.x >> 4, tx = threadIdx.x & 15;
+  const int row = Y0 + ty, col = X0 + 4 * tx;
+  if (row >= ph || col >= pw) return;
+  int I[6][9];   // I[dr + 2][dc + 2] = sample at (row + dr, col + dc)
+#pragma unroll
+  for (int r = 0; r < 6; ++r)
+#pragma unroll
+    for (int c = 0; c < 9; ++c) I[r][c] = S[ty + r][4 * tx + c];
+  // horizontal six-tap (getHorSubImageSixTap) at rows -2..3, columns 0..3: the
+  // unrounded sums are p_Vid->imgY_sub_tmp
+  int h[6][4];
+#pragma unroll
+  for (int r = 0; r < 6; ++r)
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      h[r][k] = six(I[r][k + 2], I[r][k + 3], I[r][k + 1], I[r][k + 4], I[r][k], I[r][k + 5]);
+  int s00[2][5], s02[2][4], s20[5], s22[4];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    s00[0][k] = I[2][k + 2];
+    s00[1][k] = I[3][k + 2];
+    // getVerSubImageSixTap
+    s20[k] = clip255((six(I[2][k + 2], I[3][k + 2], I[1][k + 2], I[4][k + 2], I[0][k + 2], I[5][k + 2]) + 16) >> 5);
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    s02[0][k] = clip255((h[2][k] + 16) >> 5);
+    s02[1][k] = clip255((h[3][k] + 16) >> 5);
+    // getVerSubImageSixTapTmp
+    s22[k] = clip255((six(h[2][k], h[3][k], h[1][k], h[4][k], h[0][k], h[5][k]) + 512) >> 10);
+  }
+  uint32_t o[16];
+  o[0] = pack4(s00[0][0], s00[0][1], s00[0][2], s00[0][3]);
+  o[2] = pack4(s02[0][0], s02[0][1], s02[0][2], s02[0][3]);
+  o[8] = pack4(s20[0], s20[1], s20[2], s20[3]);
+  o[10] = pack4(s22[0], s22[1], s22[2], s22[3]);
+  int q[12][4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    q[0][k] = avg2(s00[0][k], s02[0][k]);       // [0][1] getSubImageBiLinear
+    q[1][k] = avg2(s00[0][k], s20[k]);          // [1][0]
+    q[2][k] = avg2(s02[0][k], s20[k]);          // [1][1]
+    q[3][k] = avg2(s02[0][k], s22[k]);          // [1][2]
+    q[4][k] = avg2(s20[k], s22[k]);             // [2][1]
+    q[5][k] = avg2(s02[0][k], s00[0][k + 1]);   // [0][3] getHorSubImageBiLinear
+    q[6][k] = avg2(s02[0][k], s20[k + 1]);      // [1][3]
+    q[7][k] = avg2(s22[k], s20[k + 1]);         // [2][3]
+    q[8][k] = avg2(s20[k], s00[1][k]);          // [3][0] getVerSubImageBiLinear
+    q[9][k] = avg2(s20[k], s02[1][k]);          // [3][1]
+    q[10][k] = avg2(s22[k], s02[1][k]);         // [3][2]
+    q[11][k] = avg2(s02[1][k], s20[k + 1]);     // [3][3] getDiagSubImageBiLinear
+  }
+  const int qi[12] = {1, 4, 5, 6, 9, 3, 7, 11, 12, 13, 14, 15};
+#pragma unroll
+  for (int j = 0; j < 12; ++j) o[qi[j]] = pack4(q[j][0], q[j][1], q[j][2], q[j][3]);
+  uint8_t *d = dst + (size_t)row * dst_pitch + col;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) *reinterpret_cast<uint32_t *>(d + (size_t)k * plane_stride) = o[k];
+}
+
+// ------------------------------------------------------------- refinement --
+// spiral_search[0..8] (mv_search.c:406-442) and EPZS search_point_qp[0..9]
+// (me_epzs.h:42; search_point_hp = 2x), as (x, y)
+__constant__ int8_t kSpiral9[9][2] = {{0, 0}, {0, -1}, {0, 1}, {-1, -1}, {1, -1}, {-1, 0}, {1, 0}, {-1, 1}, {1, 1}};
+__constant__ int8_t kEpzsPt[10][2] = {{0, 0}, {-1, 0}, {0, 1}, {1, 0}, {0, -1}, {-1, 1}, {1, 1}, {1, -1}, {-1, -1}, {-1, 1}};
+// next_start_pos / next_end_pos (me_epzs.h:23-39), row-major
+__constant__ int8_t kNextStart[25] = {0, 8, 5, 6, 7, 8, 0, 5, 8, 8, 5, 5, 0, 6, 5, 6, 6, 6, 0, 7, 7, 8, 7, 7, 0};
+__constant__ int8_t kNextEnd[25] = {0, 10, 7, 8, 9, 10, 0, 6, 10, 9, 7, 6, 0, 7, 7, 8, 8, 7, 0, 8, 9, 9, 9, 8, 0};
+
+__device__ __forceinline__ void wave_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+__device__ __forceinline__ int64_t mv_cost(int lambda, int cx, int cy, int px, int py) {   // mv_search.h:100-104
+  return (int64_t)lambda * (int64_t)(mvbits(cx - px) + mvbits(cy - py));
+}
+
+struct Ref {
+  const uint8_t *cur;      // block origin in the current picture
+  int cur_pitch;
+  const uint8_t *sub;      // sub-image 0 of the reference
+  int sp;
+  size_t ps;
+  int ymax, xmax;          // UMVLine4X clamps: size_y_pad, size_x_pad (mbuffer.c:549-550)
+  int bsx, bsy, lg_nbx;
+};
+
+// 4 reference bytes of sub-image plane `pl`, padded row `y`, column `x` (any alignment)
+__device__ __forceinline__ uint32_t ref4(const Ref &R, int pl, int y, int x) {
+  const uint8_t *a = R.sub + (size_t)pl * R.ps + (size_t)(y + kPadY) * R.sp + (x + kPadX);
+  const uintptr_t u = reinterpret_cast<uintptr_t>(a);
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(u & ~(uintptr_t)3);
+  return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(u & 3));
+}
+
+__device__ __forceinline__ int had4_sum(const int *d) {   // HadamardSAD4x4 before its (s+1)>>1
+  int m[16], e[16];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {   // vertical pairs (rows 0/3, 1/2)
+    m[i] = d[i] + d[12 + i];
+    m[4 + i] = d[4 + i] + d[8 + i];
+    m[8 + i] = d[4 + i] - d[8 + i];
+    m[12 + i] = d[i] - d[12 + i];
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    e[i] = m[i] + m[4 + i];
+    e[4 + i] = m[8 + i] + m[12 + i];
+    e[8 + i] = m[i] - m[4 + i];
+    e[12 + i] = m[12 + i] - m[8 + i];
+  }
+  int s = 0;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int a0 = e[4 * r] + e[4 * r + 3], a1 = e[4 * r + 1] + e[4 * r + 2];
+    const int a2 = e[4 * r + 1] - e[4 * r + 2], a3 = e[4 * r] - e[4 * r + 3];
+    s += abs(a0 + a1) + abs(a0 - a1) + abs(a2 + a3) + abs(a3 - a2);
+  }
+  return s;
+}
+
+// 8x8 Walsh-Hadamard sum of magnitudes: every output of JM's HadamardSAD8x8
+// is a distinct-sign +-1 combination of the 64 inputs, so the order of the
+// butterflies does not change the sum
+__device__ __forceinline__ int had8_sum(int (&d)[64]) {
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+#pragma unroll
+    for (int h = 1; h < 8; h <<= 1)
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        if (!(i & h)) {
+          const int a = d[8 * r + i], b = d[8 * r + i + h];
+          d[8 * r + i] = a + b;
+          d[8 * r + i + h] = a - b;
+        }
+  }
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+#pragma unroll
+    for (int h = 1; h < 8; h <<= 1)
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        if (!(i & h)) {
+          const int a = d[8 * i + c], b = d[8 * (i + h) + c];
+          d[8 * i + c] = a + b;
+          d[8 * (i + h) + c] = a - b;
+        }
+  }
+  int s = 0;
+#pragma unroll
+  for (int k = 0; k < 64; ++k) s += abs(d[k]);
+  return s;
+}
+
+// Distortion sums (unscaled, as JM's int mcost) of the candidates at
+// positions p0 .. p1-1 of table `tab` (0 spiral_search, 1 EPZS points) scaled by
+// `sc` (2 half-pel, 1 quarter-pel) around the padded qpel position (mx, my),
+// into sums[0 .. p1-p0).
+__device__ void eval_phase(const Ref &R, int metric, bool t8, int tab, int sc, int p0, int p1, int mx, int my,
+                           int *sums, int lane) {
+  const int nc = p1 - p0;
+  if (nc <= 0) return;
+  const bool big = metric == 2 && t8;
+  const int bs = big ? 8 : 4;
+  const int lg_nbx = big ? R.lg_nbx - 1 : R.lg_nbx;
+  const int lg_nb = lg_nbx + (big ? (R.bsy == 16 ? 1 : 0) : (R.bsy == 16 ? 2 : R.bsy == 8 ? 1 : 0));
+  const int nb = 1 << lg_nb;
+  for (int base = 0; base < nc << lg_nb; base += 64) {
+    const int j = base + lane;
+    const int c = j >> lg_nb, b = j & (nb - 1);
+    int s = 0;
+    if (c < nc) {
+      const int pos = p0 + c;
+      const int ox = tab ? kEpzsPt[pos][0] : kSpiral9[pos][0];
+      const int oy = tab ? kEpzsPt[pos][1] : kSpiral9[pos][1];
+      const int cx = mx + sc * ox, cy = my + sc * oy;
+      const int bxo = (b & ((1 << lg_nbx) - 1)) * bs, byo = (b >> lg_nbx) * bs;
+      const int pl = ((cy & 3) << 2) | (cx & 3);
+      int yy, xx;
+      if (metric == 2) {   // computeSATD: UMVLine4X per transform block
+        yy = min(max((cy + (byo << 2)) >> 2, -kPadY), R.ymax);
+        xx = min(max((cx + (bxo << 2)) >> 2, -kPadX), R.xmax);
+      } else {             // computeSAD / computeSSE: UMVLine4X of the block origin
+        yy = min(max(cy >> 2, -kPadY), R.ymax) + byo;
+        xx = min(max(cx >> 2, -kPadX), R.xmax) + bxo;
+      }
+      const uint8_t *org = R.cur + (size_t)byo * R.cur_pitch + bxo;
+      if (metric == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          s = __builtin_amdgcn_sad_u8(ref4(R, pl, yy + r, xx), *reinterpret_cast<const uint32_t *>(org + r * R.cur_pitch),
+                                      s);
+      } else if (metric == 1) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const uint32_t a = *reinterpret_cast<const uint32_t *>(org + r * R.cur_pitch), w = ref4(R, pl, yy + r, xx);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int d = (int)((a >> (8 * k)) & 255) - (int)((w >> (8 * k)) & 255);
+            s += d * d;
+          }
+        }
+      } else if (!big) {
+        int d[16];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const uint32_t a = *reinterpret_cast<const uint32_t *>(org + r * R.cur_pitch), w = ref4(R, pl, yy + r, xx);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) d[4 * r + k] = (int)((a >> (8 * k)) & 255) - (int)((w >> (8 * k)) & 255);
+        }
+        s = (had4_sum(d) + 1) >> 1;
+      } else {
+        int d[64];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const uint32_t a = *reinterpret_cast<const uint32_t *>(org + r * R.cur_pitch + 4 * h);
+            const uint32_t w = ref4(R, pl, yy + r, xx + 4 * h);
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+              d[8 * r + 4 * h + k] = (int)((a >> (8 * k)) & 255) - (int)((w >> (8 * k)) & 255);
+          }
+        }
+        s = (had8_sum(d) + 2) >> 2;
+      }
+    }
+    for (int off = nb >> 1; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+    if (c < nc && b == 0) sums[c] = s;
+  }
+  wave_sync();
+}
+
+// computePred*'s return value for bound T (> 0): JM stops once the partial sum
+// exceeds T >> 5 and then returns T (dist_scale_f, mv_search.h:19-20)
+__device__ __forceinline__ int64_t dist(int sum, int64_t T) { return (int64_t)sum > (T >> 5) ? T : (int64_t)sum << 5; }
+
+__device__ __forceinline__ void blk_size(int bt, int &bsx, int &bsy) {   // block_size[], macroblock.h:58-68
+  bsx = (bt == 1 || bt == 2) ? 16 : (bt == 3 || bt == 4 || bt == 5) ? 8 : 4;
+  bsy = (bt == 1 || bt == 3) ? 16 : (bt == 2 || bt == 4 || bt == 6) ? 8 : 4;
+}
+
+constexpr int kWaves = 4;
+
+__global__ __launch_bounds__(256) void subpel_kernel(SubpelParams p) {
+  __shared__ int lds[kWaves][16];
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int i = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + wv);
+  if (i >= p.n) return;
+  const jmme_subpel_req q = p.req[i];
+  const int bt = q.blocktype;
+  if (bt < 1 || bt > 7) return;
+  int mvx = q.mv_x, mvy = q.mv_y;
+  int64_t min_mcost = q.min_mcost;
+  if (p.int_res) {
+    const jmme_block_res ir = p.int_res[i];
+    mvx = ir.mv_x;
+    mvy = ir.mv_y;
+    min_mcost = q.start_hp ? (int64_t)ir.cost : kDistMax;
+  }
+  Ref R;
+  int bsx, bsy;
+  blk_size(bt, bsx, bsy);
+  R.bsx = bsx;
+  R.bsy = bsy;
+  R.lg_nbx = bsx == 16 ? 2 : bsx == 8 ? 1 : 0;
+  R.cur = p.cur + (size_t)q.pos_y * p.cur_pitch + q.pos_x;
+  R.cur_pitch = p.cur_pitch;
+  R.sub = p.subs[q.ref_slot];
+  R.sp = p.sub_pitch;
+  R.ps = p.plane_stride;
+  R.ymax = p.height + 2 * kPadY - 1 - 16 - kPadY;
+  R.xmax = p.width + 2 * kPadX - 1 - 16 - kPadX;
+  const bool t8 = q.flags & JMME_SP_TEST8x8;
+  const int pxp = q.pos_x << 2, pyp = q.pos_y << 2;   // pos_x_padded (mv_search.c:685-686)
+  const int px = q.pred_x, py = q.pred_y;
+  int *sums = lds[wv];
+  int best_pos;
+
+  if (q.variant == 0) {
+    // ---- sub_pel_motion_estimation, me_fullsearch.c:186-289
+    const bool chk0 = (q.flags & JMME_SP_CHECK0) && (q.ref_slot & 31) == 0 && bt == 1 && mvx == 0 && mvy == 0;
+    const int max_pos2 = !q.start_hp ? max(1, (int)q.search_pos2) : (int)q.search_pos2;
+    int lambda = q.lambda_h;
+    eval_phase(R, q.metric_h, t8, 0, 2, q.start_hp, max_pos2, mvx + pxp, mvy + pyp, sums, lane);
+    best_pos = 0;
+    for (int pos = q.start_hp; pos < max_pos2; ++pos) {
+      const int cx = mvx + 2 * kSpiral9[pos][0], cy = mvy + 2 * kSpiral9[pos][1];
+      int64_t mcost = mv_cost(lambda, cx, cy, px, py);
+      if (mcost >= min_mcost) continue;
+      mcost += dist(sums[pos - q.start_hp], min_mcost - mcost);
+      if (pos == 0 && chk0) mcost -= (int64_t)lambda * 16;   // weighted_cost(lambda_factor, 16)
+      if (mcost < min_mcost) { min_mcost = mcost; best_pos = pos; }
+    }
+    if (best_pos) { mvx += 2 * kSpiral9[best_pos][0]; mvy += 2 * kSpiral9[best_pos][1]; }
+    if (!q.start_qp) min_mcost = kDistMax;
+    lambda = q.lambda_q;
+    wave_sync();
+    eval_phase(R, q.metric_q, t8, 0, 1, q.start_qp, q.search_pos4, mvx + pxp, mvy + pyp, sums, lane);
+    best_pos = 0;
+    for (int pos = q.start_qp; pos < q.search_pos4; ++pos) {
+      const int cx = mvx + kSpiral9[pos][0], cy = mvy + kSpiral9[pos][1];
+      int64_t mcost = mv_cost(lambda, cx, cy, px, py);
+      if (mcost >= min_mcost) continue;
+      mcost += dist(sums[pos - q.start_qp], min_mcost - mcost);
+      if (mcost < min_mcost) { min_mcost = mcost; best_pos = pos; }
+    }
+    if (best_pos) { mvx += kSpiral9[best_pos][0]; mvy += kSpiral9[best_pos][1]; }
+  } else {
+    // ---- EPZS_sub_pel_motion_estimation, me_epzs_sub.c:30-222
+    int64_t second_mcost = kDistMax;
+    int second_pos = 0;
+    const int max_pos2 = (!q.start_hp || !q.start_qp) ? max(1, (int)q.search_pos2) : (int)q.search_pos2;
+    int lambda = q.lambda_h;
+    const int64_t sub_threshold = q.subthres + (int64_t)lambda * 2;
+    int padx = mvx + pxp, pady = mvy + pyp;
+    const int ppx = px + pxp, ppy = py + pyp;
+    const int e1 = min(5, max_pos2);
+    eval_phase(R, q.metric_h, t8, 1, 2, q.start_hp, e1, padx, pady, sums, lane);
+    best_pos = 0;
+    for (int pos = q.start_hp; pos < e1; ++pos) {
+      const int cx = padx + 2 * kEpzsPt[pos][0], cy = pady + 2 * kEpzsPt[pos][1];
+      int64_t mcost = mv_cost(lambda, cx, cy, ppx, ppy);
+      if (mcost < second_mcost) {
+        mcost += dist(sums[pos - q.start_hp], second_mcost - mcost);
+        if (mcost < min_mcost) {
+          second_mcost = min_mcost; second_pos = best_pos; min_mcost = mcost; best_pos = pos;
+        } else if (mcost < second_mcost) {
+          second_mcost = mcost; second_pos = pos;
+        }
+      }
+    }
+    const bool early = best_pos == 0 && px == mvx && py == mvy && min_mcost < sub_threshold;   // :90-93
+    if (!early) {
+      if (q.search_pos2 >= 9 && (best_pos != 0 || (abs(px - mvx) + abs(py - mvy)))) {   // :96-121
+        const int s0 = kNextStart[best_pos * 5 + second_pos], s1 = kNextEnd[best_pos * 5 + second_pos];
+        wave_sync();
+        eval_phase(R, q.metric_h, t8, 1, 2, s0, s1, padx, pady, sums, lane);
+        for (int pos = s0; pos < s1; ++pos) {
+          const int cx = padx + 2 * kEpzsPt[pos][0], cy = pady + 2 * kEpzsPt[pos][1];
+          int64_t mcost = mv_cost(lambda, cx, cy, ppx, ppy);
+          if (mcost < min_mcost) {
+            mcost += dist(sums[pos - s0], min_mcost - mcost);
+            if (mcost < min_mcost) { min_mcost = mcost; best_pos = pos; }
+          }
+        }
+      }
+      if (best_pos) {
+        mvx += 2 * kEpzsPt[best_pos][0];
+        mvy += 2 * kEpzsPt[best_pos][1];
+        padx = mvx + pxp;
+        pady = mvy + pyp;
+      }
+      // quarter-pel, :135-172
+      const int e2 = (min_mcost < sub_threshold) ? 1 : 5;
+      second_mcost = kDistMax;
+      if (!q.start_qp) { best_pos = -1; min_mcost = kDistMax; } else best_pos = 0;
+      lambda = q.lambda_q;
+      wave_sync();
+      eval_phase(R, q.metric_q, t8, 1, 1, q.start_qp, e2, padx, pady, sums, lane);
+      for (int pos = q.start_qp; pos < e2; ++pos) {
+        const int cx = padx + kEpzsPt[pos][0], cy = pady + kEpzsPt[pos][1];
+        int64_t mcost = mv_cost(lambda, cx, cy, ppx, ppy);
+        if (mcost < second_mcost) {
+          mcost += dist(sums[pos - q.start_qp], second_mcost - mcost);
+          if (mcost < min_mcost) {
+            second_mcost = min_mcost; second_pos = best_pos; min_mcost = mcost; best_pos = pos;
+          } else if (mcost < second_mcost) {
+            second_mcost = mcost; second_pos = pos;
+          }
+        }
+      }
+      if (min_mcost > sub_threshold && (best_pos != 0 || (abs(px - mvx) + abs(py - mvy)))) {   // :175-204
+        // JM reads next_start_pos[best][second] with second possibly -1 (start_qp 0):
+        // row-major [best-1][4], or, for best 0, the zero padding before the
+        // tables in JM's build (see oracle/subpel_oracle.c) -> an empty loop
+        const int k = best_pos * 5 + second_pos;
+        const int s0 = k >= 0 ? kNextStart[k] : 0, s1 = k >= 0 ? kNextEnd[k] : 0;
+        wave_sync();
+        eval_phase(R, q.metric_q, t8, 1, 1, s0, s1, padx, pady, sums, lane);
+        for (int pos = s0; pos < s1; ++pos) {
+          const int cx = padx + kEpzsPt[pos][0], cy = pady + kEpzsPt[pos][1];
+          int64_t mcost = mv_cost(lambda, cx, cy, ppx, ppy);
+          if (mcost < min_mcost) {
+            mcost += dist(sums[pos - s0], min_mcost - mcost);
+            if (mcost < min_mcost) { min_mcost = mcost; best_pos = pos; }
+          }
+        }
+      }
+      if (best_pos > 0) { mvx += kEpzsPt[best_pos][0]; mvy += kEpzsPt[best_pos][1]; }
+    }
+  }
+  if (lane == 0) {
+    jmme_block_res r;
+    r.mv_x = (int16_t)mvx;
+    r.mv_y = (int16_t)mvy;
+    r.reserved = 0;
+    r.cost = min_mcost;
+    p.out[i] = r;
+  }
+}
+
+}  // namespace
+
+hipError_t launch_sub_images(const uint8_t *src, int src_pitch, int w, int h, uint8_t *dst, int dst_pitch,
+                             size_t plane_stride, hipStream_t s) {
+  const int pw = w + 2 * kPadX, ph = h + 2 * kPadY;
+  dim3 grid((pw + kTileW - 1) / kTileW, (ph + kTileH - 1) / kTileH);
+  hipLaunchKernelGGL(sub_images_kernel, grid, dim3(256), 0, s, src, src_pitch, w, h, dst, dst_pitch, plane_stride,
+                     pw, ph);
+  return hipGetLastError();
+}
+
+hipError_t launch_subpel(const SubpelParams &p, hipStream_t s) {
+  if (p.n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(subpel_kernel, dim3((p.n + kWaves - 1) / kWaves), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+}  // namespace jmme

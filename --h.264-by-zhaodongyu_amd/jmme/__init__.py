@@ -7,5 +7,5 @@ buffers, the IntPelME search contract) over the C ABI of libjmme.so
 from ._lib import (BLK_CHECK00, BLOCK_REQ, BLOCK_RES, DISTBLK_MAX, EPZS_REQ, EPZS_RES,  # noqa: F401
                    FAST_FULL_SEARCH,
                    FRACTAL_MB, FRACTAL_NODE, FRACTAL_REQ, FRACTAL_RES, FULL_SEARCH, MB_REQ, NSLOT, QUANT4x4_PARAMS,
-                   TRANSFORM_OPS, JmmeError)
+                   SP_CHECK0, SP_TEST8x8, SUBPEL_REQ, TRANSFORM_OPS, JmmeError)
 from .engine import MotionEstimator, config_from_cfg, slot_of, spiral  # noqa: F401

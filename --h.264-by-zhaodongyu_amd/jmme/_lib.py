@@ -44,6 +44,13 @@ EPZS_REQ = np.dtype([("pos_x", "<i2"), ("pos_y", "<i2"), ("bsx", "<i2"), ("bsy",
                      ("prev_sad", "<i8"), ("medthres", "<i8"), ("stop_crit", "<i8")])
 EPZS_RES = np.dtype([("mv_x", "<i2"), ("mv_y", "<i2"), ("path", "<i4"), ("cost", "<i8"), ("prev_sad", "<i8")])
 EPZS_FRAME, EPZS_PSLICE = 1, 2
+SUBPEL_REQ = np.dtype([("pos_x", "<i2"), ("pos_y", "<i2"), ("blocktype", "<i2"), ("ref_slot", "<i2"),
+                       ("pred_x", "<i2"), ("pred_y", "<i2"), ("mv_x", "<i2"), ("mv_y", "<i2"),
+                       ("lambda_h", "<i4"), ("lambda_q", "<i4"), ("min_mcost", "<i8"), ("subthres", "<i8"),
+                       ("variant", "u1"), ("flags", "u1"), ("metric_h", "u1"), ("metric_q", "u1"),
+                       ("start_hp", "u1"), ("start_qp", "u1"), ("search_pos2", "u1"), ("search_pos4", "u1")])
+SP_TEST8x8, SP_CHECK0 = 1, 2
+SUBPEL_PAD_Y, SUBPEL_PAD_X = 20, 32
 QUANT4x4_PARAMS = np.dtype([("scale", "<i4", (16,)), ("offset", "<i4", (16,)), ("inv_scale", "<i4", (16,)),
                             ("qp_per", "<i4"), ("is_cavlc", "<i4"), ("scan", "u1", (16, 2)), ("c_cost", "u1", (16,))])
 TRANSFORM_OPS = {"forward4x4": (0, 16, 16), "inverse4x4": (1, 16, 16), "hadamard4x4": (2, 16, 16),
@@ -53,7 +60,7 @@ TRANSFORM_OPS = {"forward4x4": (0, 16, 16), "inverse4x4": (1, 16, 16), "hadamard
 assert BLOCK_REQ.itemsize == 16 and MB_REQ.itemsize == 688 and BLOCK_RES.itemsize == 16
 assert QUANT4x4_PARAMS.itemsize == 248 and FRACTAL_REQ.itemsize == 8 and FRACTAL_RES.itemsize == 32
 assert FRACTAL_NODE.itemsize == 40 and FRACTAL_MB.itemsize == 848
-assert EPZS_REQ.itemsize == 80 and EPZS_RES.itemsize == 24
+assert EPZS_REQ.itemsize == 80 and EPZS_RES.itemsize == 24 and SUBPEL_REQ.itemsize == 48
 
 CONFIG_FIELDS = ["SourceWidth", "SourceHeight", "SearchMode", "SearchRange", "NumberReferenceFrames",
                  "DisableSubpelME", "RDOptimization", "MEDistortionFPel", "MDDistortion", "EPZSSubPelGrid",
@@ -118,6 +125,12 @@ def lib() -> ctypes.CDLL:
         "jmme_epzs_search_async": (I, [P, P, I, P, P, P, P]),
         "jmme_fractal_encode_mbs_async": (I, [P, P, P, I, P, I, I, I, I, D, D, P, P]),
         "jmme_quant4x4_async": (I, [P, P, P, P, P, P, P, P, I, P]),
+        "jmme_interpolate_ref": (I, [P, I, I, P]),
+        "jmme_get_sub_images": (I, [P, I, I, P]),
+        "jmme_sub_images_async": (I, [P, P, I, I, I, P, I, ctypes.c_size_t, P]),
+        "jmme_subpel_validate": (I, [P, P, I]),
+        "jmme_subpel_refine": (I, [P, P, I, P]),
+        "jmme_subpel_refine_async": (I, [P, P, I, P, P, P]),
         "jmme_spiral_index": (I, [I, I]),
         "jmme_spiral_offset": (V, [I, P, P]),
         "jmme_mvbits": (I, [I]),

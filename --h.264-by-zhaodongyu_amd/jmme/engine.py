@@ -86,10 +86,12 @@ class MotionEstimator:
     # ---- frame buffers -------------------------------------------------
     def upload_cur(self, plane: np.ndarray) -> None:
         keep, rows = _rows(plane)
+        self._shape = keep.shape
         check(lib().jmme_upload_cur(self._ctx, ctypes.cast(rows, ctypes.c_void_p), keep.shape[1], keep.shape[0]))
 
     def upload_ref(self, list_idx: int, ref_idx: int, plane: np.ndarray) -> None:
         keep, rows = _rows(plane)
+        self._shape = keep.shape
         check(lib().jmme_upload_ref(self._ctx, int(list_idx), int(ref_idx), ctypes.cast(rows, ctypes.c_void_p),
                                     keep.shape[1], keep.shape[0]))
 
@@ -211,6 +213,50 @@ class MotionEstimator:
 
     def epzs_search_async(self, d_req: int, n: int, d_preds: int, d_stale: int, d_out: int, stream: int = 0) -> None:
         check(lib().jmme_epzs_search_async(self._ctx, d_req, int(n), d_preds, d_stale, d_out, stream))
+
+    # ---- quarter-pel planes and sub-pel refinement ----
+    def sub_images(self, list_idx: int, ref_idx: int) -> np.ndarray:
+        """getSubImagesLuma (JM img_luma.c:611) of an uploaded reference, in JM's padded layout:
+        uint16 [16, H+40, W+64], plane dy*4+dx, padded row 0 = picture row -20."""
+        h, w = self._shape
+        out = np.zeros((16, h + 2 * _lib.SUBPEL_PAD_Y, w + 2 * _lib.SUBPEL_PAD_X), np.uint16)
+        RowP = ctypes.POINTER(ctypes.c_uint16)
+        keep = []
+        quad = (ctypes.POINTER(ctypes.POINTER(RowP)) * 4)()
+        for dy in range(4):
+            pair = (ctypes.POINTER(RowP) * 4)()
+            for dx in range(4):
+                plane = out[dy * 4 + dx]
+                rows = (RowP * plane.shape[0])(*[ctypes.cast(plane[j].ctypes.data + 2 * _lib.SUBPEL_PAD_X, RowP)
+                                                 for j in range(plane.shape[0])])
+                # JM's row pointer array is offset so [0] is picture row 0
+                base = ctypes.addressof(rows) + _lib.SUBPEL_PAD_Y * ctypes.sizeof(RowP)
+                pair[dx] = ctypes.cast(base, ctypes.POINTER(RowP))
+                keep.append(rows)
+            quad[dy] = ctypes.cast(pair, ctypes.POINTER(ctypes.POINTER(RowP)))
+            keep.append(pair)
+        check(lib().jmme_get_sub_images(self._ctx, int(list_idx), int(ref_idx), quad))
+        return out
+
+    def subpel_refine(self, req: np.ndarray) -> np.ndarray:
+        """sub_pel_motion_estimation / EPZS_sub_pel_motion_estimation (JM me_fullsearch.c:186,
+        me_epzs_sub.c:30) for each request -> BLOCK_RES[n] (mv, cost)."""
+        req = np.ascontiguousarray(req, _lib.SUBPEL_REQ)
+        out = np.zeros(len(req), _lib.BLOCK_RES)
+        check(lib().jmme_subpel_refine(self._ctx, ptr(req), len(req), ptr(out)))
+        return out
+
+    def subpel_refine_async(self, d_req: int, n: int, d_int: int, d_out: int, stream: int = 0) -> None:
+        check(lib().jmme_subpel_refine_async(self._ctx, d_req, int(n), d_int, d_out, stream))
+
+    def subpel_validate(self, req: np.ndarray) -> None:
+        req = np.ascontiguousarray(req, _lib.SUBPEL_REQ)
+        check(lib().jmme_subpel_validate(self._ctx, ptr(req), len(req)))
+
+    def sub_images_async(self, d_src: int, src_pitch: int, width: int, height: int, d_dst: int, dst_pitch: int,
+                         plane_stride: int, stream: int = 0) -> None:
+        check(lib().jmme_sub_images_async(self._ctx, d_src, src_pitch, width, height, d_dst, dst_pitch,
+                                          plane_stride, stream))
 
     def fractal_encode_mbs(self, org: np.ndarray, refs, search_range: int, tol_16: float = 8.0,
                            tol_8: float = 5.0) -> np.ndarray:

@@ -281,6 +281,75 @@ int jmme_epzs_search(jmme_ctx *ctx, const jmme_epzs_req *req, int n, const int16
 int jmme_epzs_search_async(jmme_ctx *ctx, const jmme_epzs_req *d_req, int n, const int16_t *d_preds,
                            const int16_t *d_stale, jmme_epzs_res *d_out, void *stream);
 
+/* ---- Quarter-pel reference planes and sub-pel refinement -----------------
+ * SURVEY.md §8(f) rank 1.
+ *
+ * Sub-images: getSubImagesLuma (JM/lencod/src/img_luma.c:611-680,
+ * OnTheFlyFractMCP = 0) -- the 16 quarter-pel sub-images of a reference,
+ * sub[dy][dx], built with JM's six-tap / bilinear filters over the
+ * edge-replicated picture, padded by IMG_PAD_SIZE_Y = 20 rows and
+ * IMG_PAD_SIZE_X = 32 columns (JM/lencod/inc/defines.h) exactly as
+ * get_mem4Dpel_pad lays them out (memalloc.c:881-904).  Built on the device
+ * for each uploaded reference slot when first needed (jmme_upload_ref marks a
+ * slot's sub-images stale). */
+#define JMME_SUBPEL_PAD_Y 20
+#define JMME_SUBPEL_PAD_X 32
+
+/* (re)build the sub-images of an uploaded reference slot on `stream` */
+int jmme_interpolate_ref(jmme_ctx *ctx, int list, int ref_idx, void *stream);
+/* getSubImagesLuma drop-in: copy them out in JM's layout.  sub[dy][dx][j][i]
+ * for j in [-20, H+20), i in [-32, W+32) (JM's s->imgY_sub after
+ * UnifiedOneForthPix, image.c:2148-2164); row pointers as get_mem4Dpel_pad
+ * makes them (sub[dy][dx][j] points at column 0 of padded row j). */
+int jmme_get_sub_images(jmme_ctx *ctx, int list, int ref_idx, jmme_imgpel ****sub);
+/* device form over caller planes: d_src = 8-bit W x H plane (src_pitch bytes
+ * a row); d_dst = 16 planes, plane k = dy*4+dx at d_dst + k*plane_stride,
+ * (H+40) rows of dst_pitch >= W+64 bytes, padded row 0 = picture row -20 */
+int jmme_sub_images_async(jmme_ctx *ctx, const uint8_t *d_src, int src_pitch, int width, int height,
+                          uint8_t *d_dst, int dst_pitch, size_t plane_stride, void *stream);
+
+/* One sub-pel refinement: what BlockMotionSearch (mv_search.c:966-976) hands
+ * currMB->SubPelME for one partition.
+ *   variant 0: sub_pel_motion_estimation       (JM/lencod/src/me_fullsearch.c:186-289;
+ *              SearchMode FS / FFS, and EPZS with EPZSSubPelME 0)
+ *   variant 1: EPZS_sub_pel_motion_estimation  (JM/lencod/src/me_epzs_sub.c:30-222;
+ *              EPZS with EPZSSubPelME 1)
+ * Metrics (MEDistortionHPel / QPel): 0 SAD (computeSAD), 1 SSE (computeSSE),
+ * 2 SATD (computeSATD: 4x4 Hadamard, or 8x8 when test8x8 is set), evaluated on
+ * the sub-images with UMVLine4X clamping (refbuf.h:22-26). */
+typedef struct jmme_subpel_req {
+  int16_t pos_x, pos_y;       /* block origin (luma pels) */
+  int16_t blocktype;          /* 1..7 (0: skip this entry, its output is left untouched) */
+  int16_t ref_slot;           /* list * 32 + ref_idx of jmme_upload_ref */
+  int16_t pred_x, pred_y;     /* MV predictor (qpel) */
+  int16_t mv_x, mv_y;         /* mv_block->mv[list] on entry: the integer-pel result (qpel) */
+  int32_t lambda_h, lambda_q; /* lambda_factor[H_PEL], lambda_factor[Q_PEL] */
+  int64_t min_mcost;          /* what SubPelME receives (DISTBLK_MAX when start_hp == 0) */
+  int64_t subthres;           /* variant 1: p_EPZS->subthres[blocktype] (me_epzs_common.c:448-466) */
+  uint8_t variant;
+  uint8_t flags;              /* JMME_SP_* */
+  uint8_t metric_h, metric_q; /* 0 SAD, 1 SSE, 2 SATD */
+  uint8_t start_hp, start_qp; /* p_Vid->start_me_refinement_hp / _qp (mv_search.c:445-446) */
+  uint8_t search_pos2, search_pos4;   /* mv_block->search_pos2 / 4 (JM: 9, mv_search.c:720-721) */
+} jmme_subpel_req;            /* 48 bytes */
+
+#define JMME_SP_TEST8x8 1     /* mv_block->test8x8 (mv_search.c:1630,1770) */
+#define JMME_SP_CHECK0  2     /* variant 0: !rdopt && slice_type != B_SLICE (check_position0's slice terms,
+                                 me_fullsearch.c:205; ref 0, blocktype 1 and mv (0,0) are read from the request) */
+
+/* host arrays, synchronous; out[i] = (mv, cost) SubPelME returns */
+int jmme_subpel_refine(jmme_ctx *ctx, const jmme_subpel_req *req, int n, jmme_block_res *out);
+/* device arrays on `stream`.  d_int (may be NULL): integer-pel results aligned
+ * with the requests (e.g. the jmme_search_mbs_async output with requests in
+ * unit x slot order); when given, entry i takes mv = d_int[i].mv and
+ * min_mcost = start_hp ? d_int[i].cost : DISTBLK_MAX instead of the request's,
+ * as BlockMotionSearch does (mv_search.c:960-976).  The requests must have
+ * been validated (jmme_subpel_validate) and their sub-images built. */
+int jmme_subpel_refine_async(jmme_ctx *ctx, const jmme_subpel_req *d_req, int n, const jmme_block_res *d_int,
+                             jmme_block_res *d_out, void *stream);
+/* host-side check of requests against the context (0 = OK) */
+int jmme_subpel_validate(jmme_ctx *ctx, const jmme_subpel_req *req, int n);
+
 /* ---- Fractal domain-range block matching (thesis codec) -------------------
  * SURVEY.md §8 rows a14-a16; ZL = /root/reference/2.论文程序/ZhangLing_Yu_
  * version1/H264Fractal.  full_search (ZL/src/block_enc.c:1933-1977) with
