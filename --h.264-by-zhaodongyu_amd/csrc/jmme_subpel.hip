@@ -12,18 +12,20 @@
 //
 // Interpolation.  Every JM sub-image, including its padding, equals the
 // filter evaluated on the edge-replicated picture (JM clamps each tap into
-// the padded plane, whose border is itself a replica), so a 16 x 64 output
-// tile needs only a 22 x 73 integer tile with clamped reads.  One thread
+// the padded plane, whose border is itself a replica), so a 4 x 256 output
+// tile needs only a 10 x 265 integer tile with clamped reads.  One thread
 // makes 4 columns of one row for all 16 sub-images: 24 horizontal and 5
 // vertical six-tap sums, the (+512)>>10 centre sample, then the 12 bilinear
 // averages, written as one dword per sub-image.  The kernel is a one-pass
 // stream: 1 B read, 16 B written per padded sample (HBM roofline).
 //
-// Refinement.  One wave per refinement.  Each phase of JM's loop (the half-pel
-// ring, the quarter-pel ring; EPZS: first ring, the next_start_pos..
-// next_end_pos follow-up, for both levels) costs all its candidates at once,
-// one lane per (candidate, 4x4 or 8x8 block), group sums reduced with xor
-// shuffles; the fold then walks the candidates in JM's order with JM's
+// Refinement.  One wave per 16 refinements; lane k < 16 owns refinement k and
+// runs JM's control flow for it.  Each phase of JM's loop (the half-pel ring,
+// the quarter-pel ring; EPZS: first ring, the next_start_pos..next_end_pos
+// follow-up, for both levels) is costed for all 16 at once: the (candidate,
+// 4x4 or 8x8 block) jobs of the 16 are dealt over the 64 lanes, pass after
+// pass, and block sums are added into a per-(refinement, candidate) LDS
+// slot; the owners then walk their candidates in JM's order with JM's
 // comparisons.  JM's distortion functions stop early and return their bound
 // T once the partial sum exceeds T >> 5; sums only grow, so that happens
 // exactly when the full sum does, and the fold computes the same value:
@@ -51,7 +53,7 @@ __device__ __forceinline__ uint32_t pack4(int a, int b, int c, int d) {
 }
 
 // ------------------------------------------------------------ sub-images --
-constexpr int kTileW = 64, kTileH = 16, kSW = 80, kSH = kTileH + 6;
+constexpr int kTileW = 256, kTileH = 4, kSW = kTileW + 16, kSH = kTileH + 6;
 
 __global__ __launch_bounds__(256) void sub_images_kernel(const uint8_t *__restrict__ src, int src_pitch, int W, int H,
                                                          uint8_t *__restrict__ dst, int dst_pitch, size_t plane_stride,
@@ -65,7 +67,7 @@ __global__ __launch_bounds__(256) void sub_images_kernel(const uint8_t *__restri
     S[r][c] = src[(size_t)y * src_pitch + x];
   }
   __syncthreads();
-  const int ty = threadIdx.x >> 4, tx = threadIdx.x & 15;
+  const int ty = threadIdx.x >> 6, tx = threadIdx.x & 63;   // a wave writes 256 contiguous bytes per sub-image
   const int row = Y0 + ty, col = X0 + 4 * tx;
   if (row >= ph || col >= pw) return;
   int I[6][9];   // I[dr + 2][dc + 2] = sample at (row + dr, col + dc)
@@ -140,19 +142,9 @@ __device__ __forceinline__ int64_t mv_cost(int lambda, int cx, int cy, int px, i
   return (int64_t)lambda * (int64_t)(mvbits(cx - px) + mvbits(cy - py));
 }
 
-struct Ref {
-  const uint8_t *cur;      // block origin in the current picture
-  int cur_pitch;
-  const uint8_t *sub;      // sub-image 0 of the reference
-  int sp;
-  size_t ps;
-  int ymax, xmax;          // UMVLine4X clamps: size_y_pad, size_x_pad (mbuffer.c:549-550)
-  int bsx, bsy, lg_nbx;
-};
-
-// 4 reference bytes of sub-image plane `pl`, padded row `y`, column `x` (any alignment)
-__device__ __forceinline__ uint32_t ref4(const Ref &R, int pl, int y, int x) {
-  const uint8_t *a = R.sub + (size_t)pl * R.ps + (size_t)(y + kPadY) * R.sp + (x + kPadX);
+// 4 reference bytes of one sub-image at padded row `y`, column `x` (any alignment)
+__device__ __forceinline__ uint32_t ref4(const uint8_t *plane, int sp, int y, int x) {
+  const uint8_t *a = plane + (size_t)(y + kPadY) * sp + (x + kPadX);
   const uintptr_t u = reinterpret_cast<uintptr_t>(a);
   const uint32_t *w = reinterpret_cast<const uint32_t *>(u & ~(uintptr_t)3);
   return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(u & 3));
@@ -218,85 +210,6 @@ __device__ __forceinline__ int had8_sum(int (&d)[64]) {
   return s;
 }
 
-// Distortion sums (unscaled, as JM's int mcost) of the candidates at
-// positions p0 .. p1-1 of table `tab` (0 spiral_search, 1 EPZS points) scaled by
-// `sc` (2 half-pel, 1 quarter-pel) around the padded qpel position (mx, my),
-// into sums[0 .. p1-p0).
-__device__ void eval_phase(const Ref &R, int metric, bool t8, int tab, int sc, int p0, int p1, int mx, int my,
-                           int *sums, int lane) {
-  const int nc = p1 - p0;
-  if (nc <= 0) return;
-  const bool big = metric == 2 && t8;
-  const int bs = big ? 8 : 4;
-  const int lg_nbx = big ? R.lg_nbx - 1 : R.lg_nbx;
-  const int lg_nb = lg_nbx + (big ? (R.bsy == 16 ? 1 : 0) : (R.bsy == 16 ? 2 : R.bsy == 8 ? 1 : 0));
-  const int nb = 1 << lg_nb;
-  for (int base = 0; base < nc << lg_nb; base += 64) {
-    const int j = base + lane;
-    const int c = j >> lg_nb, b = j & (nb - 1);
-    int s = 0;
-    if (c < nc) {
-      const int pos = p0 + c;
-      const int ox = tab ? kEpzsPt[pos][0] : kSpiral9[pos][0];
-      const int oy = tab ? kEpzsPt[pos][1] : kSpiral9[pos][1];
-      const int cx = mx + sc * ox, cy = my + sc * oy;
-      const int bxo = (b & ((1 << lg_nbx) - 1)) * bs, byo = (b >> lg_nbx) * bs;
-      const int pl = ((cy & 3) << 2) | (cx & 3);
-      int yy, xx;
-      if (metric == 2) {   // computeSATD: UMVLine4X per transform block
-        yy = min(max((cy + (byo << 2)) >> 2, -kPadY), R.ymax);
-        xx = min(max((cx + (bxo << 2)) >> 2, -kPadX), R.xmax);
-      } else {             // computeSAD / computeSSE: UMVLine4X of the block origin
-        yy = min(max(cy >> 2, -kPadY), R.ymax) + byo;
-        xx = min(max(cx >> 2, -kPadX), R.xmax) + bxo;
-      }
-      const uint8_t *org = R.cur + (size_t)byo * R.cur_pitch + bxo;
-      if (metric == 0) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          s = __builtin_amdgcn_sad_u8(ref4(R, pl, yy + r, xx), *reinterpret_cast<const uint32_t *>(org + r * R.cur_pitch),
-                                      s);
-      } else if (metric == 1) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const uint32_t a = *reinterpret_cast<const uint32_t *>(org + r * R.cur_pitch), w = ref4(R, pl, yy + r, xx);
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const int d = (int)((a >> (8 * k)) & 255) - (int)((w >> (8 * k)) & 255);
-            s += d * d;
-          }
-        }
-      } else if (!big) {
-        int d[16];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const uint32_t a = *reinterpret_cast<const uint32_t *>(org + r * R.cur_pitch), w = ref4(R, pl, yy + r, xx);
-#pragma unroll
-          for (int k = 0; k < 4; ++k) d[4 * r + k] = (int)((a >> (8 * k)) & 255) - (int)((w >> (8 * k)) & 255);
-        }
-        s = (had4_sum(d) + 1) >> 1;
-      } else {
-        int d[64];
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const uint32_t a = *reinterpret_cast<const uint32_t *>(org + r * R.cur_pitch + 4 * h);
-            const uint32_t w = ref4(R, pl, yy + r, xx + 4 * h);
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-              d[8 * r + 4 * h + k] = (int)((a >> (8 * k)) & 255) - (int)((w >> (8 * k)) & 255);
-          }
-        }
-        s = (had8_sum(d) + 2) >> 2;
-      }
-    }
-    for (int off = nb >> 1; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
-    if (c < nc && b == 0) sums[c] = s;
-  }
-  wave_sync();
-}
-
 // computePred*'s return value for bound T (> 0): JM stops once the partial sum
 // exceeds T >> 5 and then returns T (dist_scale_f, mv_search.h:19-20)
 __device__ __forceinline__ int64_t dist(int sum, int64_t T) { return (int64_t)sum > (T >> 5) ? T : (int64_t)sum << 5; }
@@ -306,130 +219,202 @@ __device__ __forceinline__ void blk_size(int bt, int &bsx, int &bsy) {   // bloc
   bsy = (bt == 1 || bt == 3) ? 16 : (bt == 2 || bt == 4 || bt == 6) ? 8 : 4;
 }
 
+constexpr int kK = 16;        // refinements per wave (lanes 0..15 own one each)
 constexpr int kWaves = 4;
+constexpr int kMaxCand = 10;  // candidates of one phase (search_point tables: 10 entries)
+
+// One phase's job description of request k, as the cooperating lanes read it.
+// code: p0 [0,4) | lg_nb [4,7) | lg_nbx [8,10) | metric [12,14) | big 14 | sc [15,17) | tab 17
+struct WaveLds {
+  int sums[kK][kMaxCand];
+  int4 job[kK];                  // (mx, my, code, pos_x | pos_y << 16)
+  const uint8_t *sub[kK];
+};
+
+// The distortion sum of one transform / 4x4 block of one candidate
+// (computeSAD / computeSSE / computeSATD restated per block; their per-row or
+// per-block early exits are reproduced by dist() in the fold).
+__device__ __forceinline__ int job_sum(const uint8_t *sub, size_t ps, int sp, const uint8_t *org, int cp, int ymax,
+                                       int xmax, int metric, bool big, int cx, int cy, int bxo, int byo) {
+  const int pl = ((cy & 3) << 2) | (cx & 3);
+  const uint8_t *plane = sub + (size_t)pl * ps;
+  int yy, xx;
+  if (metric == 2) {   // computeSATD: UMVLine4X per transform block
+    yy = min(max((cy + (byo << 2)) >> 2, -kPadY), ymax);
+    xx = min(max((cx + (bxo << 2)) >> 2, -kPadX), xmax);
+  } else {             // computeSAD / computeSSE: UMVLine4X of the block origin
+    yy = min(max(cy >> 2, -kPadY), ymax) + byo;
+    xx = min(max(cx >> 2, -kPadX), xmax) + bxo;
+  }
+  org += (size_t)byo * cp + bxo;
+  int s = 0;
+  if (metric == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      s = __builtin_amdgcn_sad_u8(ref4(plane, sp, yy + r, xx), *reinterpret_cast<const uint32_t *>(org + r * cp), s);
+  } else if (metric == 1) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const uint32_t a = *reinterpret_cast<const uint32_t *>(org + r * cp), w = ref4(plane, sp, yy + r, xx);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int d = (int)((a >> (8 * k)) & 255) - (int)((w >> (8 * k)) & 255);
+        s += d * d;
+      }
+    }
+  } else if (!big) {
+    int d[16];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const uint32_t a = *reinterpret_cast<const uint32_t *>(org + r * cp), w = ref4(plane, sp, yy + r, xx);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) d[4 * r + k] = (int)((a >> (8 * k)) & 255) - (int)((w >> (8 * k)) & 255);
+    }
+    s = (had4_sum(d) + 1) >> 1;
+  } else {
+    int d[64];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint32_t a = *reinterpret_cast<const uint32_t *>(org + r * cp + 4 * h);
+        const uint32_t w = ref4(plane, sp, yy + r, xx + 4 * h);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) d[8 * r + 4 * h + k] = (int)((a >> (8 * k)) & 255) - (int)((w >> (8 * k)) & 255);
+      }
+    }
+    s = (had8_sum(d) + 2) >> 2;
+  }
+  return s;
+}
+
+// Per-request geometry the owner lane keeps.
+struct Own {
+  int bsy, lg_nbx, pos_x, pos_y;
+  const uint8_t *sub;
+};
+
+// One phase for the whole wave: owner lane k asks for the candidates at table
+// positions [p0, p1) of table `tab` scaled by `sc` around padded (mx, my) with
+// its metric; all 64 lanes share the (candidate, block) jobs of the 16
+// requests, pass after pass, and add the block sums into sums[k][c].
+__device__ void run_phase(const SubpelParams &p, WaveLds &L, int lane, const Own &o, int p0, int p1, int metric,
+                          bool t8, int sc, int tab, int mx, int my) {
+  const bool big = metric == 2 && t8;
+  const int lg_nbx = big ? o.lg_nbx - 1 : o.lg_nbx;
+  const int lg_nb = lg_nbx + (big ? (o.bsy == 16 ? 1 : 0) : (o.bsy == 16 ? 2 : o.bsy == 8 ? 1 : 0));
+  const int nc = (lane < kK && p1 > p0) ? p1 - p0 : 0;
+  const int jobs = nc << lg_nb;
+  if (lane < kK) {
+    L.job[lane] = make_int4(mx, my, p0 | (lg_nb << 4) | (lg_nbx << 8) | (metric << 12) | ((int)big << 14) |
+                                        (sc << 15) | (tab << 17),
+                            o.pos_x | (o.pos_y << 16));
+    L.sub[lane] = o.sub;
+#pragma unroll
+    for (int c = 0; c < kMaxCand; ++c) L.sums[lane][c] = 0;
+  }
+  // inclusive scan of the job counts over lanes 0..15
+  int incl = jobs;
+#pragma unroll
+  for (int off = 1; off < kK; off <<= 1) {
+    const int t = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += t;
+  }
+  const int total = __builtin_amdgcn_readlane(incl, kK - 1);
+  int pre[kK];   // exclusive prefix (uniform)
+#pragma unroll
+  for (int m = 0; m < kK; ++m) pre[m] = __builtin_amdgcn_readlane(incl, m) - __builtin_amdgcn_readlane(jobs, m);
+  wave_sync();
+  const int ymax = p.height + 2 * kPadY - 1 - 16 - kPadY, xmax = p.width + 2 * kPadX - 1 - 16 - kPadX;
+  for (int base = 0; base < total; base += 64) {
+    const int j = base + lane;
+    if (j < total) {
+      int k = 0;
+#pragma unroll
+      for (int m = 1; m < kK; ++m) k += j >= pre[m];
+      const int4 jb = L.job[k];
+      const int e = j - pre[k];
+      const int jl_nb = (jb.z >> 4) & 7, jl_nbx = (jb.z >> 8) & 3;
+      const int c = e >> jl_nb, b = e & ((1 << jl_nb) - 1);
+      const int jm = (jb.z >> 12) & 3;
+      const bool jbig = (jb.z >> 14) & 1;
+      const int jsc = (jb.z >> 15) & 3, pos = (jb.z & 15) + c;
+      const int ox = ((jb.z >> 17) & 1) ? kEpzsPt[pos][0] : kSpiral9[pos][0];
+      const int oy = ((jb.z >> 17) & 1) ? kEpzsPt[pos][1] : kSpiral9[pos][1];
+      const int bs = jbig ? 8 : 4;
+      const int bxo = (b & ((1 << jl_nbx) - 1)) * bs, byo = (b >> jl_nbx) * bs;
+      const uint8_t *org = p.cur + (size_t)(jb.w >> 16) * p.cur_pitch + (jb.w & 0xffff);
+      const int s = job_sum(L.sub[k], p.plane_stride, p.sub_pitch, org, p.cur_pitch, ymax, xmax, jm, jbig,
+                            jb.x + jsc * ox, jb.y + jsc * oy, bxo, byo);
+      atomicAdd(&L.sums[k][c], s);
+    }
+  }
+  wave_sync();
+}
 
 __global__ __launch_bounds__(256) void subpel_kernel(SubpelParams p) {
-  __shared__ int lds[kWaves][16];
+  __shared__ WaveLds lds[kWaves];
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int i = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + wv);
-  if (i >= p.n) return;
-  const jmme_subpel_req q = p.req[i];
-  const int bt = q.blocktype;
-  if (bt < 1 || bt > 7) return;
+  const int i0 = __builtin_amdgcn_readfirstlane((blockIdx.x * kWaves + wv) * kK);
+  if (i0 >= p.n) return;
+  WaveLds &L = lds[wv];
+  const int i = i0 + lane;
+  // owner lanes: lane k < 16 holds request i0 + k; inactive owners ask for nothing
+  jmme_subpel_req q{};
+  bool act = false;
+  if (lane < kK && i < p.n) {
+    q = p.req[i];
+    act = q.blocktype >= 1 && q.blocktype <= 7;
+  }
   int mvx = q.mv_x, mvy = q.mv_y;
   int64_t min_mcost = q.min_mcost;
-  if (p.int_res) {
+  if (act && p.int_res) {
     const jmme_block_res ir = p.int_res[i];
     mvx = ir.mv_x;
     mvy = ir.mv_y;
     min_mcost = q.start_hp ? (int64_t)ir.cost : kDistMax;
   }
-  Ref R;
-  int bsx, bsy;
-  blk_size(bt, bsx, bsy);
-  R.bsx = bsx;
-  R.bsy = bsy;
-  R.lg_nbx = bsx == 16 ? 2 : bsx == 8 ? 1 : 0;
-  R.cur = p.cur + (size_t)q.pos_y * p.cur_pitch + q.pos_x;
-  R.cur_pitch = p.cur_pitch;
-  R.sub = p.subs[q.ref_slot];
-  R.sp = p.sub_pitch;
-  R.ps = p.plane_stride;
-  R.ymax = p.height + 2 * kPadY - 1 - 16 - kPadY;
-  R.xmax = p.width + 2 * kPadX - 1 - 16 - kPadX;
+  Own o;
+  int bsx = 4;
+  o.bsy = 4;
+  if (act) blk_size(q.blocktype, bsx, o.bsy);
+  o.lg_nbx = bsx == 16 ? 2 : bsx == 8 ? 1 : 0;
+  o.pos_x = q.pos_x;
+  o.pos_y = q.pos_y;
+  o.sub = act ? p.subs[q.ref_slot] : p.subs[0];
   const bool t8 = q.flags & JMME_SP_TEST8x8;
   const int pxp = q.pos_x << 2, pyp = q.pos_y << 2;   // pos_x_padded (mv_search.c:685-686)
   const int px = q.pred_x, py = q.pred_y;
-  int *sums = lds[wv];
-  int best_pos;
+  const bool epzs = q.variant == 1;
+  const int *sums = L.sums[lane < kK ? lane : 0];
+  int best_pos = 0, second_pos = 0;
+  int64_t second_mcost = kDistMax;
+  int lambda = q.lambda_h;
+  // EPZS bookkeeping (me_epzs_sub.c:43-57)
+  const int max_pos2 = epzs ? ((!q.start_hp || !q.start_qp) ? max(1, (int)q.search_pos2) : (int)q.search_pos2)
+                            : (!q.start_hp ? max(1, (int)q.search_pos2) : (int)q.search_pos2);
+  const int64_t sub_threshold = q.subthres + (int64_t)q.lambda_h * 2;
+  bool early = false;
+  const bool chk0 = (q.flags & JMME_SP_CHECK0) && (q.ref_slot & 31) == 0 && q.blocktype == 1 && mvx == 0 && mvy == 0;
 
-  if (q.variant == 0) {
-    // ---- sub_pel_motion_estimation, me_fullsearch.c:186-289
-    const bool chk0 = (q.flags & JMME_SP_CHECK0) && (q.ref_slot & 31) == 0 && bt == 1 && mvx == 0 && mvy == 0;
-    const int max_pos2 = !q.start_hp ? max(1, (int)q.search_pos2) : (int)q.search_pos2;
-    int lambda = q.lambda_h;
-    eval_phase(R, q.metric_h, t8, 0, 2, q.start_hp, max_pos2, mvx + pxp, mvy + pyp, sums, lane);
-    best_pos = 0;
-    for (int pos = q.start_hp; pos < max_pos2; ++pos) {
-      const int cx = mvx + 2 * kSpiral9[pos][0], cy = mvy + 2 * kSpiral9[pos][1];
-      int64_t mcost = mv_cost(lambda, cx, cy, px, py);
-      if (mcost >= min_mcost) continue;
-      mcost += dist(sums[pos - q.start_hp], min_mcost - mcost);
-      if (pos == 0 && chk0) mcost -= (int64_t)lambda * 16;   // weighted_cost(lambda_factor, 16)
-      if (mcost < min_mcost) { min_mcost = mcost; best_pos = pos; }
-    }
-    if (best_pos) { mvx += 2 * kSpiral9[best_pos][0]; mvy += 2 * kSpiral9[best_pos][1]; }
-    if (!q.start_qp) min_mcost = kDistMax;
-    lambda = q.lambda_q;
-    wave_sync();
-    eval_phase(R, q.metric_q, t8, 0, 1, q.start_qp, q.search_pos4, mvx + pxp, mvy + pyp, sums, lane);
-    best_pos = 0;
-    for (int pos = q.start_qp; pos < q.search_pos4; ++pos) {
-      const int cx = mvx + kSpiral9[pos][0], cy = mvy + kSpiral9[pos][1];
-      int64_t mcost = mv_cost(lambda, cx, cy, px, py);
-      if (mcost >= min_mcost) continue;
-      mcost += dist(sums[pos - q.start_qp], min_mcost - mcost);
-      if (mcost < min_mcost) { min_mcost = mcost; best_pos = pos; }
-    }
-    if (best_pos) { mvx += kSpiral9[best_pos][0]; mvy += kSpiral9[best_pos][1]; }
-  } else {
-    // ---- EPZS_sub_pel_motion_estimation, me_epzs_sub.c:30-222
-    int64_t second_mcost = kDistMax;
-    int second_pos = 0;
-    const int max_pos2 = (!q.start_hp || !q.start_qp) ? max(1, (int)q.search_pos2) : (int)q.search_pos2;
-    int lambda = q.lambda_h;
-    const int64_t sub_threshold = q.subthres + (int64_t)lambda * 2;
-    int padx = mvx + pxp, pady = mvy + pyp;
-    const int ppx = px + pxp, ppy = py + pyp;
-    const int e1 = min(5, max_pos2);
-    eval_phase(R, q.metric_h, t8, 1, 2, q.start_hp, e1, padx, pady, sums, lane);
-    best_pos = 0;
-    for (int pos = q.start_hp; pos < e1; ++pos) {
-      const int cx = padx + 2 * kEpzsPt[pos][0], cy = pady + 2 * kEpzsPt[pos][1];
-      int64_t mcost = mv_cost(lambda, cx, cy, ppx, ppy);
-      if (mcost < second_mcost) {
-        mcost += dist(sums[pos - q.start_hp], second_mcost - mcost);
-        if (mcost < min_mcost) {
-          second_mcost = min_mcost; second_pos = best_pos; min_mcost = mcost; best_pos = pos;
+  // ---- phase A: half-pel ring (me_fullsearch.c:221-250 | me_epzs_sub.c:66-88)
+  {
+    const int p1 = epzs ? min(5, max_pos2) : max_pos2;
+    run_phase(p, L, lane, o, q.start_hp, act ? p1 : 0, q.metric_h, t8, 2, epzs, mvx + pxp, mvy + pyp);
+    if (act) {
+      for (int pos = q.start_hp; pos < p1; ++pos) {
+        const int ox = epzs ? kEpzsPt[pos][0] : kSpiral9[pos][0], oy = epzs ? kEpzsPt[pos][1] : kSpiral9[pos][1];
+        const int cx = mvx + 2 * ox, cy = mvy + 2 * oy;
+        int64_t mcost = mv_cost(lambda, cx, cy, px, py);
+        const int sm = sums[pos - q.start_hp];
+        if (!epzs) {
+          if (mcost >= min_mcost) continue;
+          mcost += dist(sm, min_mcost - mcost);
+          if (pos == 0 && chk0) mcost -= (int64_t)lambda * 16;   // weighted_cost(lambda_factor, 16)
+          if (mcost < min_mcost) { min_mcost = mcost; best_pos = pos; }
         } else if (mcost < second_mcost) {
-          second_mcost = mcost; second_pos = pos;
-        }
-      }
-    }
-    const bool early = best_pos == 0 && px == mvx && py == mvy && min_mcost < sub_threshold;   // :90-93
-    if (!early) {
-      if (q.search_pos2 >= 9 && (best_pos != 0 || (abs(px - mvx) + abs(py - mvy)))) {   // :96-121
-        const int s0 = kNextStart[best_pos * 5 + second_pos], s1 = kNextEnd[best_pos * 5 + second_pos];
-        wave_sync();
-        eval_phase(R, q.metric_h, t8, 1, 2, s0, s1, padx, pady, sums, lane);
-        for (int pos = s0; pos < s1; ++pos) {
-          const int cx = padx + 2 * kEpzsPt[pos][0], cy = pady + 2 * kEpzsPt[pos][1];
-          int64_t mcost = mv_cost(lambda, cx, cy, ppx, ppy);
-          if (mcost < min_mcost) {
-            mcost += dist(sums[pos - s0], min_mcost - mcost);
-            if (mcost < min_mcost) { min_mcost = mcost; best_pos = pos; }
-          }
-        }
-      }
-      if (best_pos) {
-        mvx += 2 * kEpzsPt[best_pos][0];
-        mvy += 2 * kEpzsPt[best_pos][1];
-        padx = mvx + pxp;
-        pady = mvy + pyp;
-      }
-      // quarter-pel, :135-172
-      const int e2 = (min_mcost < sub_threshold) ? 1 : 5;
-      second_mcost = kDistMax;
-      if (!q.start_qp) { best_pos = -1; min_mcost = kDistMax; } else best_pos = 0;
-      lambda = q.lambda_q;
-      wave_sync();
-      eval_phase(R, q.metric_q, t8, 1, 1, q.start_qp, e2, padx, pady, sums, lane);
-      for (int pos = q.start_qp; pos < e2; ++pos) {
-        const int cx = padx + kEpzsPt[pos][0], cy = pady + kEpzsPt[pos][1];
-        int64_t mcost = mv_cost(lambda, cx, cy, ppx, ppy);
-        if (mcost < second_mcost) {
-          mcost += dist(sums[pos - q.start_qp], second_mcost - mcost);
+          mcost += dist(sm, second_mcost - mcost);
           if (mcost < min_mcost) {
             second_mcost = min_mcost; second_pos = best_pos; min_mcost = mcost; best_pos = pos;
           } else if (mcost < second_mcost) {
@@ -437,27 +422,98 @@ __global__ __launch_bounds__(256) void subpel_kernel(SubpelParams p) {
           }
         }
       }
-      if (min_mcost > sub_threshold && (best_pos != 0 || (abs(px - mvx) + abs(py - mvy)))) {   // :175-204
-        // JM reads next_start_pos[best][second] with second possibly -1 (start_qp 0):
-        // row-major [best-1][4], or, for best 0, the zero padding before the
-        // tables in JM's build (see oracle/subpel_oracle.c) -> an empty loop
-        const int k = best_pos * 5 + second_pos;
-        const int s0 = k >= 0 ? kNextStart[k] : 0, s1 = k >= 0 ? kNextEnd[k] : 0;
-        wave_sync();
-        eval_phase(R, q.metric_q, t8, 1, 1, s0, s1, padx, pady, sums, lane);
-        for (int pos = s0; pos < s1; ++pos) {
-          const int cx = padx + kEpzsPt[pos][0], cy = pady + kEpzsPt[pos][1];
-          int64_t mcost = mv_cost(lambda, cx, cy, ppx, ppy);
+      if (!epzs) {
+        if (best_pos) { mvx += 2 * kSpiral9[best_pos][0]; mvy += 2 * kSpiral9[best_pos][1]; }
+      } else {
+        early = best_pos == 0 && px == mvx && py == mvy && min_mcost < sub_threshold;   // :90-93
+      }
+    }
+  }
+  // ---- phase B: EPZS half-pel follow-up (me_epzs_sub.c:96-127)
+  {
+    int s0 = 0, s1 = 0;
+    if (act && epzs && !early && q.search_pos2 >= 9 && (best_pos != 0 || (abs(px - mvx) + abs(py - mvy)))) {
+      s0 = kNextStart[best_pos * 5 + second_pos];
+      s1 = kNextEnd[best_pos * 5 + second_pos];
+    }
+    run_phase(p, L, lane, o, s0, s1, q.metric_h, t8, 2, 1, mvx + pxp, mvy + pyp);
+    if (act && epzs && !early) {
+      for (int pos = s0; pos < s1; ++pos) {
+        const int cx = mvx + 2 * kEpzsPt[pos][0], cy = mvy + 2 * kEpzsPt[pos][1];
+        int64_t mcost = mv_cost(lambda, cx, cy, px, py);
+        if (mcost < min_mcost) {
+          mcost += dist(sums[pos - s0], min_mcost - mcost);
+          if (mcost < min_mcost) { min_mcost = mcost; best_pos = pos; }
+        }
+      }
+      if (best_pos) { mvx += 2 * kEpzsPt[best_pos][0]; mvy += 2 * kEpzsPt[best_pos][1]; }
+    }
+  }
+  // ---- phase C: quarter-pel ring (me_fullsearch.c:252-282 | me_epzs_sub.c:135-172)
+  lambda = q.lambda_q;
+  {
+    int p1 = 0;
+    if (act && !early) {
+      if (!epzs) {
+        if (!q.start_qp) min_mcost = kDistMax;
+        best_pos = 0;
+        p1 = q.search_pos4;
+      } else {
+        p1 = (min_mcost < sub_threshold) ? 1 : 5;
+        second_mcost = kDistMax;
+        if (!q.start_qp) { best_pos = -1; min_mcost = kDistMax; } else best_pos = 0;
+      }
+    }
+    run_phase(p, L, lane, o, q.start_qp, p1, q.metric_q, t8, 1, epzs, mvx + pxp, mvy + pyp);
+    if (act && !early) {
+      for (int pos = q.start_qp; pos < p1; ++pos) {
+        const int ox = epzs ? kEpzsPt[pos][0] : kSpiral9[pos][0], oy = epzs ? kEpzsPt[pos][1] : kSpiral9[pos][1];
+        const int cx = mvx + ox, cy = mvy + oy;
+        int64_t mcost = mv_cost(lambda, cx, cy, px, py);
+        const int sm = sums[pos - q.start_qp];
+        if (!epzs) {
+          if (mcost >= min_mcost) continue;
+          mcost += dist(sm, min_mcost - mcost);
+          if (mcost < min_mcost) { min_mcost = mcost; best_pos = pos; }
+        } else if (mcost < second_mcost) {
+          mcost += dist(sm, second_mcost - mcost);
           if (mcost < min_mcost) {
-            mcost += dist(sums[pos - s0], min_mcost - mcost);
-            if (mcost < min_mcost) { min_mcost = mcost; best_pos = pos; }
+            second_mcost = min_mcost; second_pos = best_pos; min_mcost = mcost; best_pos = pos;
+          } else if (mcost < second_mcost) {
+            second_mcost = mcost; second_pos = pos;
           }
         }
       }
-      if (best_pos > 0) { mvx += kEpzsPt[best_pos][0]; mvy += kEpzsPt[best_pos][1]; }
+      if (!epzs && best_pos) { mvx += kSpiral9[best_pos][0]; mvy += kSpiral9[best_pos][1]; }
     }
   }
-  if (lane == 0) {
+  // ---- phase D: EPZS quarter-pel follow-up (me_epzs_sub.c:175-210)
+  {
+    int s0 = 0, s1 = 0;
+    const bool go = act && epzs && !early && min_mcost > sub_threshold &&
+                    (best_pos != 0 || (abs(px - mvx) + abs(py - mvy)));
+    if (go) {
+      // JM reads next_start_pos[best][second] with second possibly -1 (start_qp 0):
+      // row-major [best-1][4], or, for best 0, the zero padding before the
+      // tables in JM's build (see oracle/subpel_oracle.c) -> an empty loop
+      const int k = best_pos * 5 + second_pos;
+      s0 = k >= 0 ? kNextStart[k] : 0;
+      s1 = k >= 0 ? kNextEnd[k] : 0;
+    }
+    run_phase(p, L, lane, o, s0, s1, q.metric_q, t8, 1, 1, mvx + pxp, mvy + pyp);
+    if (go) {
+      for (int pos = s0; pos < s1; ++pos) {
+        const int cx = mvx + kEpzsPt[pos][0], cy = mvy + kEpzsPt[pos][1];
+        int64_t mcost = mv_cost(lambda, cx, cy, px, py);
+        if (mcost < min_mcost) {
+          mcost += dist(sums[pos - s0], min_mcost - mcost);
+          if (mcost < min_mcost) { min_mcost = mcost; best_pos = pos; }
+        }
+      }
+    }
+    if (act && epzs && !early && best_pos > 0) { mvx += kEpzsPt[best_pos][0]; mvy += kEpzsPt[best_pos][1]; }
+  }
+  if (act) {
     jmme_block_res r;
     r.mv_x = (int16_t)mvx;
     r.mv_y = (int16_t)mvy;
@@ -480,7 +536,8 @@ hipError_t launch_sub_images(const uint8_t *src, int src_pitch, int w, int h, ui
 
 hipError_t launch_subpel(const SubpelParams &p, hipStream_t s) {
   if (p.n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(subpel_kernel, dim3((p.n + kWaves - 1) / kWaves), dim3(256), 0, s, p);
+  const int per_wg = kWaves * kK;
+  hipLaunchKernelGGL(subpel_kernel, dim3((p.n + per_wg - 1) / per_wg), dim3(256), 0, s, p);
   return hipGetLastError();
 }
 
