@@ -148,6 +148,64 @@ def pmc_traffic():
     return None
 
 
+SUBPEL_CASE = "subpel_syn_1080p_fs32"
+
+
+def subpel_block(dev, local: int, iters: int = 20) -> dict | None:
+    """JM's sub-pel half of the same ME, measured on rank 0:
+    getSubImagesLuma of the 1080p reference + the 334,560 sub_pel_motion_estimation
+    calls JM ran for the frame (FS +-32, SATD), with JM's inputs, parity vs JM."""
+    import golden_io as g
+    from jmme import BLOCK_RES, SP_CHECK0, SP_TEST8x8, SUBPEL_REQ, MotionEstimator, _lib
+    if SUBPEL_CASE not in g.manifest():
+        return None
+    from subpel_cases import SubpelCase
+    c = SubpelCase(SUBPEL_CASE)
+    (f, lst, rf, idx), = list(c.groups())
+    r = c.r
+    q = np.zeros(len(idx), SUBPEL_REQ)
+    for k in ("pos_x", "pos_y", "blocktype", "pred_x", "pred_y", "lambda_h", "lambda_q", "subthres", "metric_h",
+              "metric_q", "start_hp", "start_qp", "search_pos2", "search_pos4"):
+        q[k] = r[k][idx]
+    q["ref_slot"] = r["list"][idx] * 32 + r["ref"][idx]
+    q["mv_x"], q["mv_y"], q["min_mcost"], q["variant"] = r["mv_in_x"][idx], r["mv_in_y"][idx], r["min_mcost_in"][idx], \
+        r["kind"][idx]
+    q["flags"] = (np.where(r["test8x8"][idx] != 0, SP_TEST8x8, 0) |
+                  np.where((r["rdopt"][idx] == 0) & (r["slice_type"][idx] != 1), SP_CHECK0, 0))
+    me = MotionEstimator(device=local)
+    me.upload_cur(c.cur[f])
+    me.upload_ref(lst, rf, c.ref[(f, lst, rf)])
+    me.subpel_validate(q)
+    d_q = torch.from_numpy(q.view(np.uint8).copy()).to(dev)
+    d_o = torch.zeros(len(q) * BLOCK_RES.itemsize, dtype=torch.uint8, device=dev)
+    st = torch.cuda.current_stream(dev)
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(iters):
+            fn()
+        e1.record(st)
+        torch.cuda.synchronize(dev)
+        return e0.elapsed_time(e1) / iters
+    ms_i = timed(lambda: _lib.check(_lib.lib().jmme_interpolate_ref(me._ctx, lst, rf, st.cuda_stream)))
+    ms_r = timed(lambda: me.subpel_refine_async(d_q.data_ptr(), len(q), 0, d_o.data_ptr(), st.cuda_stream))
+    got = d_o.cpu().numpy().view(BLOCK_RES)
+    emv, ecost = c.expected(idx)
+    exact = int(np.sum((got["mv_x"] == emv[:, 0]) & (got["mv_y"] == emv[:, 1]) & (got["cost"] == ecost)))
+    me.close()
+    h, w = c.cur[f].shape
+    ibytes = w * h + 16 * (w + 64) * (h + 40)
+    return {"workload": "JM 18.5 sub_pel_motion_estimation for one 1080p P-frame (FS +-32, SATD half/quarter-pel)",
+            "refinements": int(len(q)), "refine_ms": round(ms_r, 4), "interpolate_ms": round(ms_i, 4),
+            "mb_per_s": round((w // 16) * (h // 16) / ((ms_r + ms_i) * 1e-3), 1),
+            "interpolate_hbm_frac": round(ibytes / (ms_i * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "parity": {"reference": "JM 18.5 lencod (captured)", "refinements": int(len(q)), "bit_exact": exact},
+            "jm_me_time_with_subpel": c.meta.get("jm_me_time")}
+
+
 def reduce_over_ranks(wall: float, exact: int, ws: int, dev) -> tuple[float, int]:
     """Job time = the slowest rank's time; parity = the worst rank's count.
     The only collectives of the run (no data-path exchange: ranks own whole GOPs)."""
@@ -172,6 +230,7 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-subpel", action="store_true")
     args = ap.parse_args()
 
     ws, rank, local = dist_env()
@@ -263,6 +322,8 @@ def main():
             "event_ms_per_step": round(ev_ms / args.steps, 4),
             "cpu_baseline": cpu,
         }
+        if not args.no_subpel:
+            line["subpel"] = subpel_block(dev, local)
         print(json.dumps(line))
     me.close()
     if ws > 1:
