@@ -5,6 +5,9 @@
  * every EPZS integer-pel search:
  *   EPZS_motion_estimation        JM/lencod/src/me_epzs.c:54-407
  *   EPZS_subMB_motion_estimation  JM/lencod/src/me_epzs.c:417-780
+ *   EPZS_integer_motion_estimation / EPZS_integer_subMB_motion_estimation
+ *                                 JM/lencod/src/me_epzs_int.c:41-380 / 431-782
+ *                                 (EPZSSubPelGrid = 1: variants 2 / 3)
  * together with the host-side state each search reads -- the predictor list
  * JM generated for it (EPZS_spatial_predictors / _spatial_memory_ /
  * _temporal_ / EPZSWindowPredictors / EPZSBlockTypePredictors(MB),
@@ -30,6 +33,8 @@
 
 extern distblk __real_EPZS_motion_estimation(Macroblock *, MotionVector *, MEBlock *, distblk, int);
 extern distblk __real_EPZS_subMB_motion_estimation(Macroblock *, MotionVector *, MEBlock *, distblk, int);
+extern distblk __real_EPZS_integer_motion_estimation(Macroblock *, MotionVector *, MEBlock *, distblk, int);
+extern distblk __real_EPZS_integer_subMB_motion_estimation(Macroblock *, MotionVector *, MEBlock *, distblk, int);
 extern distblk __real_EPZSDetermineStopCriterion(EPZSParameters *, distblk *, MEBlock *, distblk);
 extern short __real_EPZS_spatial_predictors(EPZSParameters *, MEBlock *, int, int, short, struct pic_motion_params **);
 extern void __real_EPZS_spatial_memory_predictors(EPZSParameters *, MEBlock *, int, int *, int);
@@ -43,7 +48,8 @@ extern void __real_EPZSBlockTypePredictors(Slice *, MEBlock *, SPoint *, int *);
 
 #pragma pack(push, 1)
 struct cap_epzs {
-  int32_t variant;       /* 0 EPZS_motion_estimation, 1 EPZS_subMB_motion_estimation */
+  int32_t variant;       /* 0 EPZS_motion_estimation, 1 EPZS_subMB_motion_estimation,
+                            2 EPZS_integer_motion_estimation, 3 EPZS_integer_subMB_motion_estimation */
   int32_t frame_no;
   int32_t mb_addr;
   int16_t mb_x, mb_y;    /* currMB->mb_x / mb_y (MB units) */
@@ -114,6 +120,17 @@ static int map_side(Macroblock *currMB)
   return (2 * sr + 1) << 2;       /* me_epzs_common.c:428-431 */
 }
 
+static distblk call_real(int variant, Macroblock *currMB, MotionVector *pred_mv, MEBlock *mv_block, distblk min_mcost,
+                         int lambda_factor)
+{
+  switch (variant) {
+    case 0: return __real_EPZS_motion_estimation(currMB, pred_mv, mv_block, min_mcost, lambda_factor);
+    case 1: return __real_EPZS_subMB_motion_estimation(currMB, pred_mv, mv_block, min_mcost, lambda_factor);
+    case 2: return __real_EPZS_integer_motion_estimation(currMB, pred_mv, mv_block, min_mcost, lambda_factor);
+    default: return __real_EPZS_integer_subMB_motion_estimation(currMB, pred_mv, mv_block, min_mcost, lambda_factor);
+  }
+}
+
 static distblk run(int variant, Macroblock *currMB, MotionVector *pred_mv, MEBlock *mv_block, distblk min_mcost,
                    int lambda_factor)
 {
@@ -134,9 +151,7 @@ static distblk run(int variant, Macroblock *currMB, MotionVector *pred_mv, MEBlo
   distblk c;
   int i, j, side;
 
-  if (!fp)
-    return variant ? __real_EPZS_subMB_motion_estimation(currMB, pred_mv, mv_block, min_mcost, lambda_factor)
-                   : __real_EPZS_motion_estimation(currMB, pred_mv, mv_block, min_mcost, lambda_factor);
+  if (!fp) return call_real(variant, currMB, pred_mv, mv_block, min_mcost, lambda_factor);
   if (next == 0) next = 1;
   memset(&r, 0, sizeof(r));
   /* cells already equal to the BlkCount this search will use (left by the
@@ -160,8 +175,7 @@ static distblk run(int variant, Macroblock *currMB, MotionVector *pred_mv, MEBlo
   r.prev_sad_in = (int64_t)*prevSad;
   g_stop = -1;
   g_npred = -1;
-  c = variant ? __real_EPZS_subMB_motion_estimation(currMB, pred_mv, mv_block, min_mcost, lambda_factor)
-              : __real_EPZS_motion_estimation(currMB, pred_mv, mv_block, min_mcost, lambda_factor);
+  c = call_real(variant, currMB, pred_mv, mv_block, min_mcost, lambda_factor);
 
   if (p_Vid->frame_no != g_last_cur_frame) {
     g_last_cur_frame = p_Vid->frame_no;
@@ -239,6 +253,18 @@ distblk __wrap_EPZS_subMB_motion_estimation(Macroblock *currMB, MotionVector *pr
                                             distblk min_mcost, int lambda_factor)
 {
   return run(1, currMB, pred_mv, mv_block, min_mcost, lambda_factor);
+}
+
+distblk __wrap_EPZS_integer_motion_estimation(Macroblock *currMB, MotionVector *pred_mv, MEBlock *mv_block,
+                                              distblk min_mcost, int lambda_factor)
+{
+  return run(2, currMB, pred_mv, mv_block, min_mcost, lambda_factor);
+}
+
+distblk __wrap_EPZS_integer_subMB_motion_estimation(Macroblock *currMB, MotionVector *pred_mv, MEBlock *mv_block,
+                                                    distblk min_mcost, int lambda_factor)
+{
+  return run(3, currMB, pred_mv, mv_block, min_mcost, lambda_factor);
 }
 
 distblk __wrap_EPZSDetermineStopCriterion(EPZSParameters *p_EPZS, distblk *prevSad, MEBlock *mv_block,

@@ -271,3 +271,236 @@ void eo_epzs_batch(const eo_req *q, int n, const int16_t *preds, const int16_t *
     eo_epzs(&q[i], preds + 2 * (size_t)q[i].pred_off, stale + 2 * (size_t)q[i].stale_off, cur, refs[q[i].plane],
             pitch, W, H, &out[i]);
 }
+
+
+/* ===========================================================================
+ * EPZSSubPelGrid = 1: EPZS_integer_motion_estimation (variant 2) and
+ * EPZS_integer_subMB_motion_estimation (variant 3), JM/lencod/src/
+ * me_epzs_int.c:41-380 / 431-782.  Same skeleton as the integer-grid
+ * functions above, with: the centre and the predictors kept at quarter-pel
+ * precision (no set_integer_mv), the EPZSMap indexed per quarter-pel
+ * position, computePredFPel = computeSAD on the quarter-pel sub-images
+ * (UMVLine4X), and the control-flow differences marked inline.
+ * subs: the reference's 16 sub-images, plane dy*4+dx, (H+40) x (W+64) 8-bit,
+ * padded row 0 = picture row -20 (getSubImagesLuma layout). */
+typedef struct gctx {
+  const eo_req *q;
+  const uint8_t *cur, *subs;
+  int pitch, W, H, sp, sh;   /* cur pitch; sub-image pitch / rows */
+  int side_x;
+  unsigned char *map;
+} gctx;
+
+/* mv_cost + computeSAD<<5 at quarter-pel vector (mx, my) (me_distortion.c:349-426) */
+static int64_t gcost_of(const gctx *c, int mx, int my)
+{
+  const eo_req *q = c->q;
+  int64_t mvc = (int64_t)q->lambda * (mvbits(mx - q->pred_x) + mvbits(my - q->pred_y));
+  const int cx = mx + (q->pos_x << 2), cy = my + (q->pos_y << 2);   /* pad_MVs */
+  /* UMVLine4X (refbuf.h:22-26): size_y_pad = H+3, size_x_pad = W+15 (mbuffer.c:549-550) */
+  const int yy = clampi(cy >> 2, -20, c->H + 3), xx = clampi(cx >> 2, -32, c->W + 15);
+  const uint8_t *plane = c->subs + (size_t)((cy & 3) * 4 + (cx & 3)) * c->sp * c->sh;
+  int x, y, sad = 0;
+  for (y = 0; y < q->bsy; y++) {
+    const uint8_t *rrow = plane + (size_t)(yy + 20 + y) * c->sp + (xx + 32);
+    const uint8_t *crow = c->cur + (size_t)(q->pos_y + y) * c->pitch + q->pos_x;
+    for (x = 0; x < q->bsx; x++) {
+      int d = crow[x] - rrow[x];
+      sad += d < 0 ? -d : d;
+    }
+  }
+  return mvc + ((int64_t)sad << 5);
+}
+
+static int gin_range(const gctx *c, int mx, int my)
+{
+  int dx = mx - c->q->center_x, dy = my - c->q->center_y;
+  return (dx < 0 ? -dx : dx) <= c->q->max_x && (dy < 0 ? -dy : dy) <= c->q->max_y;
+}
+
+/* EPZSMap[max_y - mv.y + my][max_x - mv.x + mx] (me_epzs_int.c:214-219): one cell per qpel position */
+static int gvisit(gctx *c, int mx, int my)
+{
+  unsigned char *m = &c->map[(my - c->q->center_y + c->q->max_y) * c->side_x + (mx - c->q->center_x + c->q->max_x)];
+  if (*m) return 0;
+  *m = 1;
+  return 1;
+}
+
+void eo_epzs_grid(const eo_req *q, const int16_t *preds, const int16_t *stale, const uint8_t *cur, int pitch,
+                  const uint8_t *subs, int W, int H, eo_res *out)
+{
+  gctx c;
+  const int frame = q->flags & 1, pslice = (q->flags >> 1) & 1, bt = q->blocktype, refi = q->ref_idx;
+  const int sub = q->variant == 3;
+  const int64_t lambda_dist = (int64_t)q->lambda * (sub ? 3 : 2);
+  const int mv_range = sub ? 12 : 10;
+  int64_t stop = q->medthres + lambda_dist, prev = q->prev_sad, min;
+  int tmpx = q->center_x, tmpy = q->center_y, i;
+  memset(out, 0, sizeof(*out));
+  c.q = q;
+  c.cur = cur;
+  c.subs = subs;
+  c.pitch = pitch;
+  c.W = W;
+  c.H = H;
+  c.sp = W + 64;
+  c.sh = H + 40;
+  c.side_x = 2 * q->max_x + 1;
+  c.map = calloc((size_t)c.side_x * (2 * q->max_y + 1), 1);
+  for (i = 0; i < q->n_stale; i++) {       /* cells left holding this BlkCount */
+    int dx = stale[2 * i], dy = stale[2 * i + 1];
+    if (gin_range(&c, q->center_x + dx, q->center_y + dy)) gvisit(&c, q->center_x + dx, q->center_y + dy);
+  }
+  gvisit(&c, q->center_x, q->center_y);
+  min = gcost_of(&c, q->center_x, q->center_y);
+
+  /* :67-80 / :496-507: the ref > 0 early exit also fires when prevSad * 8 (6 for subMB) < min */
+  if (refi > 0 && frame && (prev < (stop < min ? stop : min) || prev * (sub ? 6 : 8) < min)) {
+    out->path = 1;
+    goto done_noupdate;
+  }
+  if (min > stop) {
+    int64_t second = DMAX;
+    int check_median = 0, tmp2x = 0, tmp2y = 0, P;
+    stop = q->stop_crit;
+    if (min < (stop >> 1)) {               /* :112-124 (variant 2 updates prevSad) / :525-536 */
+      out->path = 2;
+      if (!sub && (refi == 0 || prev > min)) prev = min;
+      goto done_noupdate;
+    }
+    for (i = 0; i < q->n_pred; i++) {
+      const int mx = preds[2 * i], my = preds[2 * i + 1];   /* no set_integer_mv */
+      if (gin_range(&c, mx, my) && gvisit(&c, mx, my)) {
+        int64_t mc = (int64_t)q->lambda * (mvbits(mx - q->pred_x) + mvbits(my - q->pred_y));
+        if (mc < second) {   /* :224-226: the SAD of a candidate whose mv cost reaches second is skipped */
+          mc = gcost_of(&c, mx, my);
+          if (mc < min) {
+            tmp2x = tmpx;
+            tmp2y = tmpy;
+            tmpx = mx;
+            tmpy = my;
+            second = min;
+            min = mc;
+            check_median = 1;
+          } else if (mc < second) {
+            tmp2x = mx;
+            tmp2y = my;
+            second = mc;
+            check_median = 1;
+          }
+        }
+      }
+      if (sub) {
+        if (refi > 0 && frame && prev * 3 < min) {   /* :590-600: returns without touching *mv */
+          out->path = 6;
+          goto done_noupdate;
+        }
+        if (min < ((3 * stop) >> 2)) {                /* :604-615 */
+          out->path = 3;
+          goto done_mv_noupdate;
+        }
+      }
+    }
+    if (!sub && refi > 0 && frame && prev * 3 < min) {   /* :249-265 */
+      out->path = 7;
+      goto done_mv_noupdate;
+    }
+    if (min > stop) {
+      int cenx, ceny, point = 0, pstop = 0, next_last = 0, total, dir = 0;
+      P = primary_pattern(q->pattern);
+      if (q->pattern != 0) {
+        if (min < stop + ((3 * q->medthres) >> 1)) {
+          const int dx = abs(tmpx - q->center_x), dy = abs(tmpy - q->center_y);
+          P = ((sub && bt == 7) || (tmpx == 0 && tmpy == 0) || (dx < mv_range && dy < mv_range)) ? P_SDIAMOND
+                                                                                                  : P_SQUARE;
+        } else if (sub || (refi > 0 && bt != 1)) {   /* variant 2 drops the bt > 4 test (:282) */
+          P = P_SQUARE;
+        }
+      }
+      cenx = tmpx;
+      ceny = tmpy;
+      for (;;) {
+        total = PATS[P].n;
+        do {
+          int left = total;
+          do {
+            const int mx = cenx + PATS[P].pt[point][0], my = ceny + PATS[P].pt[point][1];
+            if (gin_range(&c, mx, my) && gvisit(&c, mx, my)) {
+              int64_t mc = (int64_t)q->lambda * (mvbits(mx - q->pred_x) + mvbits(my - q->pred_y));
+              if (mc < min) {
+                mc = gcost_of(&c, mx, my);
+                if (mc < min) {
+                  tmpx = mx;
+                  tmpy = my;
+                  min = mc;
+                  dir = point;
+                }
+              }
+            }
+            if (++point >= PATS[P].n) point -= PATS[P].n;
+          } while (--left > 0);
+          if (next_last || (tmpx == cenx && tmpy == ceny)) {
+            pstop = PATS[P].stop;
+            P = PATS[P].next;
+            total = PATS[P].n;
+            next_last = PATS[P].next_last;
+            dir = 0;
+            point = 0;
+          } else {
+            total = PATS[P].pt[dir][3];
+            point = PATS[P].pt[dir][2];
+            cenx = tmpx;
+            ceny = tmpy;
+          }
+        } while (pstop != 1);
+
+        if (refi > 0 && frame && (4 * prev < min || (3 * prev < min && prev <= stop))) {
+          out->path = 4;
+          goto done_mv_noupdate;
+        }
+        /* second-best refinement, :337-340 / :298-301 */
+        if (!(check_median && (!sub || bt != 7) && (refi == 0 || min < 2 * prev) && (!sub || pslice) &&
+              min > ((3 * stop) >> 1) && q->dual > 0))
+          break;
+        point = 0;
+        pstop = 0;
+        dir = 0;
+        next_last = 0;
+        if ((tmpx == 0 && tmpy == 0) || (tmpx == q->center_x && tmpy == q->center_y)) {
+          const int dx = abs(tmpx - q->center_x), dy = abs(tmpy - q->center_y);
+          P = ((sub && bt == 7) || (dx < mv_range && dy < mv_range)) ? P_SDIAMOND : P_SQUARE;
+        } else {
+          P = dual_pattern(q->dual);
+        }
+        cenx = tmp2x;
+        ceny = tmp2y;
+        check_median = 0;
+      }
+    }
+  }
+  out->path = out->path ? out->path : 5;
+  if (refi == 0 || prev > min) prev = min;
+done_mv_noupdate:
+  out->mv_x = (int16_t)tmpx;
+  out->mv_y = (int16_t)tmpy;
+  out->cost = min;
+  out->prev_sad = prev;
+  free(c.map);
+  return;
+done_noupdate:
+  out->mv_x = q->center_x;
+  out->mv_y = q->center_y;
+  out->cost = min;
+  out->prev_sad = prev;
+  free(c.map);
+}
+
+void eo_epzs_grid_batch(const eo_req *q, int n, const int16_t *preds, const int16_t *stale, const uint8_t *cur,
+                        int pitch, const uint8_t *const *subs, int W, int H, eo_res *out)
+{
+  int i;
+  for (i = 0; i < n; i++)
+    eo_epzs_grid(&q[i], preds + 2 * (size_t)q[i].pred_off, stale + 2 * (size_t)q[i].stale_off, cur, pitch,
+                 subs[q[i].plane], W, H, &out[i]);
+}

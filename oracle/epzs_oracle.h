@@ -53,6 +53,17 @@ void eo_epzs(const eo_req *q, const int16_t *preds, const int16_t *stale, const 
 void eo_epzs_batch(const eo_req *q, int n, const int16_t *preds, const int16_t *stale, const uint8_t *cur,
                    const uint8_t *const *refs, int pitch, int W, int H, eo_res *out);
 
+/* EPZSSubPelGrid = 1 (variants 2 EPZS_integer_motion_estimation, 3
+ * EPZS_integer_subMB_motion_estimation, JM/lencod/src/me_epzs_int.c:41-782):
+ * subs = the reference's 16 padded sub-images (plane dy*4+dx, (H+40) x (W+64)
+ * 8-bit, getSubImagesLuma layout, subpel_oracle.h).  Extra paths: 6 = the
+ * subMB predictor-loop prevSad exit (mv untouched), 7 = the post-predictor
+ * prevSad exit of variant 2 (mv = best). */
+void eo_epzs_grid(const eo_req *q, const int16_t *preds, const int16_t *stale, const uint8_t *cur, int pitch,
+                  const uint8_t *subs, int W, int H, eo_res *out);
+void eo_epzs_grid_batch(const eo_req *q, int n, const int16_t *preds, const int16_t *stale, const uint8_t *cur,
+                        int pitch, const uint8_t *const *subs, int W, int H, eo_res *out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -31,6 +31,8 @@ from jmme import synth  # noqa: E402
 from make_golden import BASE_CFG, FOREMAN, coded_synth, md5  # noqa: E402
 
 EPZS_INT = {"SearchMode": 3, "EPZSSubPelGrid": 0}
+# JM's own baseline setting: EPZS on the quarter-pel grid (EPZS_integer_motion_estimation, me_epzs_int.c)
+EPZS_GRID = {"SearchMode": 3, "EPZSSubPelGrid": 1}
 
 CASES = {
     # JM's baseline EPZS settings (EPZSPattern 2, EPZSDualRefinement 3, all predictor kinds), sub-pel ME on
@@ -56,6 +58,18 @@ CASES = {
     "epzs_syn_1080p_r32": dict(src="synth", w=1920, h=1080, frames=2, seed=2024, gmv=(5, 3),
                                p={**EPZS_INT, "SearchRange": 32, "NumberReferenceFrames": 1,
                                   "RDOptimization": 1, "MDDistortion": 2}, keep="compact"),
+    # EPZSSubPelGrid = 1 (variants 2 / 3): JM's encoder_baseline.cfg as shipped, + the SBP diamond pattern
+    "epzs_grid_foreman_qcif": dict(src="foreman", w=176, h=144, frames=3, p={**EPZS_GRID}),
+    "epzs_grid_foreman_qcif_p4d5": dict(src="foreman", w=176, h=144, frames=3,
+                                        p={**EPZS_GRID, "EPZSPattern": 4, "EPZSDualRefinement": 5}),
+    "epzs_grid_foreman_qcif_p1d6_rdo0": dict(src="foreman", w=176, h=144, frames=3,
+                                             p={**EPZS_GRID, "EPZSPattern": 1, "EPZSDualRefinement": 6,
+                                                "RDOptimization": 0, "MDDistortion": 2}),
+    "epzs_grid_syn_cif_r32_3ref": dict(src="synth", w=352, h=288, frames=4, seed=7, gmv=(5, 3),
+                                       p={**EPZS_GRID, "SearchRange": 32, "NumberReferenceFrames": 3}),
+    "epzs_grid_syn_1080p_r32": dict(src="synth", w=1920, h=1080, frames=2, seed=2024, gmv=(5, 3),
+                                    p={**EPZS_GRID, "SearchRange": 32, "NumberReferenceFrames": 1,
+                                       "RDOptimization": 1, "MDDistortion": 2}, keep="compact"),
 }
 
 KEEP_FIELDS = ["variant", "frame_no", "mb_addr", "blocktype", "pos_x", "pos_y", "bsx", "bsy", "list", "ref",

@@ -344,3 +344,27 @@ def sub_pel_batch(cur: np.ndarray, sub: np.ndarray, req: np.ndarray, epzs: bool)
     lib.spo_sub_pel_batch(cur.ctypes.data, sub.ctypes.data, w, h, req.ctypes.data, len(req), int(epzs),
                           mv.ctypes.data, cost.ctypes.data)
     return mv, cost
+
+
+def epzs_grid_batch(req, preds, stale, cur, refs):
+    """EPZSSubPelGrid = 1 searches (variants 2 / 3) against the sub-images of refs[plane] -> EPZS_RES[n]"""
+    lib = load_epzs()
+    if not hasattr(lib, "_grid_sig"):
+        P, I = ctypes.c_void_p, ctypes.c_int
+        lib.eo_epzs_grid_batch.argtypes = [P, I, P, P, P, I, P, I, I, P]
+        lib._grid_sig = True
+    req = np.ascontiguousarray(req, EPZS_REQ)
+    preds = np.ascontiguousarray(preds, np.int16).reshape(-1, 2)
+    stale = np.ascontiguousarray(stale, np.int16).reshape(-1, 2)
+    if len(preds) == 0:
+        preds = np.zeros((1, 2), np.int16)
+    if len(stale) == 0:
+        stale = np.zeros((1, 2), np.int16)
+    cur = np.ascontiguousarray(cur, np.uint8)
+    subs = [np.ascontiguousarray(sub_images(r).astype(np.uint8)) for r in refs]
+    h, w = cur.shape
+    ptrs = (ctypes.c_void_p * len(subs))(*[s.ctypes.data for s in subs])
+    out = np.zeros(len(req), EPZS_RES)
+    lib.eo_epzs_grid_batch(req.ctypes.data, len(req), preds.ctypes.data, stale.ctypes.data, cur.ctypes.data, w, ptrs,
+                           w, h, out.ctypes.data)
+    return out

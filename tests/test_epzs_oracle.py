@@ -16,7 +16,9 @@ def test_oracle_matches_jm(name):
     c = EpzsCase(name)
     n = 0
     for f, cur, refs, req, exp in c.frames():
-        out = ol.epzs_batch(req, c.preds, c.stale, cur, refs)
+        grid = req["variant"] >= 2
+        assert grid.all() or not grid.any()
+        out = (ol.epzs_grid_batch if grid.any() else ol.epzs_batch)(req, c.preds, c.stale, cur, refs)
         for k in ("mv_x", "mv_y", "cost", "prev_sad"):
             bad = np.nonzero(out[k] != exp[k])[0]
             assert len(bad) == 0, (name, f, k, len(bad), req[bad[:2]], out[bad[:2]], exp[bad[:2]])
@@ -32,8 +34,30 @@ def test_fixtures_cover_the_search_paths():
     for name in cases():
         c = EpzsCase(name)
         for f, cur, refs, req, exp in c.frames():
+            if (req["variant"] >= 2).any():
+                continue
             out = ol.epzs_batch(req, c.preds, c.stale, cur, refs)
             paths += np.bincount(out["path"], minlength=6)
             pats |= set(zip(req["pattern"].tolist(), req["dual"].tolist()))
     assert (paths[1:] > 0).all(), paths
     assert {(2, 3), (0, 2), (1, 4), (3, 6), (5, 1)} <= pats
+
+
+def test_grid_fixtures_cover_the_search_paths():
+    """EPZSSubPelGrid = 1: both variants, the SBP diamond (half-pel points), quarter-pel
+    predictors, and the early exits of me_epzs_int.c (paths 1-3, 6, 7; 4 is not reached by these encodes)"""
+    paths = np.zeros(8, np.int64)
+    pats, variants, frac = set(), set(), 0
+    for name in cases():
+        c = EpzsCase(name)
+        for f, cur, refs, req, exp in c.frames():
+            if not (req["variant"] >= 2).any():
+                continue
+            out = ol.epzs_grid_batch(req, c.preds, c.stale, cur, refs)
+            paths += np.bincount(out["path"], minlength=8)
+            pats |= set(zip(req["pattern"].tolist(), req["dual"].tolist()))
+            variants |= set(req["variant"].tolist())
+            frac += int(((out["mv_x"] & 3) != 0).sum() + ((out["mv_y"] & 3) != 0).sum())
+    assert variants == {2, 3}
+    assert (4, 5) in pats and frac > 0
+    assert (paths[[1, 2, 3, 5, 6, 7]] > 0).all(), paths
