@@ -179,6 +179,8 @@ extern "C" int jmme_config_parse(jmme_config *c, const char *path, int argc, con
   }
   for (int i = 0; i < argc; ++i)
     if (argv[i] && parse_text(c, argv[i])) return -1;
+  // JM clears EPZSSubPelGrid unless SearchMode is EPZS (PatchInp, configfile.c:1330-1335)
+  if (c->SearchMode != JMME_EPZS) c->EPZSSubPelGrid = 0;
   return 0;
 }
 
@@ -732,6 +734,10 @@ extern "C" int jmme_fractal_box_sums(jmme_ctx *ctx, const uint8_t *plane, int pi
 // -------------------------------------------------------------------- EPZS --
 static_assert(sizeof(jmme_epzs_req) == 80 && sizeof(jmme_epzs_res) == 24, "EPZS ABI layout");
 
+namespace {
+int prepare_subs(jmme_ctx *ctx, hipStream_t s);   // sub-pel section below
+}  // namespace
+
 extern "C" int jmme_epzs_search_async(jmme_ctx *ctx, const jmme_epzs_req *d_req, int n, const int16_t *d_preds,
                                       const int16_t *d_stale, jmme_epzs_res *d_out, void *stream) {
   if (!ctx) return fail("null ctx");
@@ -752,6 +758,19 @@ extern "C" int jmme_epzs_search_async(jmme_ctx *ctx, const jmme_epzs_req *d_req,
   p.stale = d_stale;
   p.out = d_out;
   p.n = n;
+  p.grid = ctx->cfg.EPZSSubPelGrid ? 1 : 0;
+  if (p.grid) {   // EPZS_integer_(subMB_)motion_estimation: candidates on the quarter-pel sub-images
+    if (ctx->cfg.SearchRange > 64) return fail("EPZSSubPelGrid: SearchRange %d > 64", ctx->cfg.SearchRange);
+    if (prepare_subs(ctx, s)) return -1;
+    const SubGeom g = sub_geom(ctx->width, ctx->height);
+    p.subs = ctx->d_sub_table;
+    p.sub_pitch = g.pitch;
+    p.plane_stride = g.plane_stride;
+    p.max_qpel = 4 * ctx->cfg.SearchRange;
+  } else {
+    p.max_qpel = kEpzsMaxQpel;
+  }
+  p.map_words = (int)epzs_map_words(p.grid, p.max_qpel);
   HIPCHK(launch_epzs(p, s));
   return 0;
 }
@@ -771,13 +790,19 @@ extern "C" int jmme_epzs_search(jmme_ctx *ctx, const jmme_epzs_req *req, int n, 
         q.pos_y + q.bsy > ctx->height)
       return fail("request %d: block (%d,%d) %dx%d outside the %dx%d picture", i, q.pos_x, q.pos_y, q.bsx, q.bsy,
                   ctx->width, ctx->height);
-    if ((q.center_x & 3) || (q.center_y & 3)) return fail("request %d: centre (%d,%d) is not integer-pel", i,
-                                                          q.center_x, q.center_y);
+    const bool grid = ctx->cfg.EPZSSubPelGrid != 0;
+    if (grid ? q.variant < 2 : q.variant > 1)
+      return fail("request %d: variant %d does not match EPZSSubPelGrid %d (0/1: integer grid, 2/3: quarter-pel grid)",
+                  i, q.variant, ctx->cfg.EPZSSubPelGrid);
+    if (!grid && ((q.center_x & 3) || (q.center_y & 3)))
+      return fail("request %d: centre (%d,%d) is not integer-pel", i, q.center_x, q.center_y);
+    if (grid && (q.max_x > 4 * ctx->cfg.SearchRange || q.max_y > 4 * ctx->cfg.SearchRange))
+      return fail("request %d: search range (%d,%d) qpel beyond 4 x SearchRange", i, q.max_x, q.max_y);
     if (q.max_x < 0 || q.max_y < 0 || q.max_x > kEpzsMaxQpel || q.max_y > kEpzsMaxQpel)
       return fail("request %d: search range (%d,%d) qpel outside 0..%d", i, q.max_x, q.max_y, kEpzsMaxQpel);
-    if (q.variant > 1 || q.pattern > 5 || q.dual > 6) return fail("request %d: variant/pattern/dual", i);
-    if (q.pattern == 4 || q.dual == 5)
-      return fail("request %d: the SBP large diamond refines on half-pel points (EPZSSubPelGrid planes)", i);
+    if (q.variant > 3 || q.pattern > 5 || q.dual > 6) return fail("request %d: variant/pattern/dual", i);
+    if (!grid && (q.pattern == 4 || q.dual == 5))
+      return fail("request %d: the SBP large diamond refines on half-pel points (needs EPZSSubPelGrid 1)", i);
     if (q.blocktype < 1 || q.blocktype > 7) return fail("request %d: blocktype %d", i, q.blocktype);
     if (q.n_pred < 0 || q.pred_off < 0 || (int64_t)q.pred_off + q.n_pred > n_preds)
       return fail("request %d: predictors [%d, +%d) outside the pool of %d", i, q.pred_off, q.n_pred, n_preds);

@@ -29,8 +29,6 @@ namespace {
 
 constexpr int kWG = 256;
 constexpr int kWaves = kWG / 64;
-constexpr int kMaxSide = 2 * (kEpzsMaxQpel >> 2) + 1;
-constexpr int kMapWords = (kMaxSide * kMaxSide + 31) / 32;
 constexpr int64_t kDistMax = ((int64_t)0x7fffffff) << 5;   // DISTBLK_MAX, JM/lencod/inc/defines.h:135
 
 // (dx, dy, start_nmbr, next_points) in qpel; me_epzs_common.c:46-80 data and
@@ -51,7 +49,9 @@ __constant__ Pat kPats[6] = {
     {8, 1, 1, P_LDIAMOND,
      {{0, 8, 6, 5}, {4, 4, 0, 3}, {8, 0, 0, 5}, {4, -4, 2, 3}, {0, -8, 2, 5}, {-4, -4, 4, 3}, {-8, 0, 4, 5},
       {-4, 4, 6, 3}}},
-    {12, 0, 1, P_SDIAMOND, {}},   // SBP large diamond: half-pel points, rejected on the host
+    {12, 0, 1, P_SDIAMOND,        // SBP large diamond: half-pel points, EPZSSubPelGrid = 1 only
+     {{0, 8, 6, 12}, {4, 4, 0, 12}, {8, 0, 0, 12}, {4, -4, 2, 12}, {0, -8, 2, 12}, {-4, -4, 4, 12}, {-8, 0, 4, 12},
+      {-4, 4, 6, 12}, {0, 2, 6, 12}, {2, 0, 0, 12}, {0, -2, 2, 12}, {-2, 0, 4, 12}}},
     {8, 0, 1, P_SDIAMOND,
      {{0, 8, 6, 5}, {4, 4, 0, 3}, {8, 0, 0, 5}, {4, -4, 2, 3}, {0, -8, 2, 5}, {-4, -4, 4, 3}, {-8, 0, 4, 5},
       {-4, 4, 6, 3}}},
@@ -71,14 +71,16 @@ __device__ __forceinline__ int dual_pattern(int v) {
 __device__ __forceinline__ void wave_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 struct WaveLds {
-  uint32_t map[kMapWords];
   uint32_t cur[64];
   int pk[64][3];          // compacted candidates (x, y, source index)
 };
+// the visited-position bitmap (EPZSMap) lives in dynamic LDS, map_words per wave:
+// integer-pel cells on the integer grid, quarter-pel cells on the sub-pel grid
 
 struct Search {
-  const uint8_t *ref;
-  int pitch, W, H;
+  const uint8_t *ref;    // integer grid: the reference plane; sub-pel grid: its 16 sub-images
+  int pitch, W, H;       // pitch: of the plane, or of the sub-images
+  size_t ps;             // sub-pel grid: bytes per sub-image
   int pos_x, pos_y, bsx, bsy;
   int pred_x, pred_y, cx, cy, max_x, max_y, side_x;
   int lambda;
@@ -115,10 +117,32 @@ __device__ __forceinline__ unsigned row_sad(const Search &s, int ox, int oy, int
   return sad;
 }
 
+// Sub-pel grid: SAD of row r of the block at padded quarter-pel position
+// (cx, cy): UMVLine4X picks sub-image (cy & 3, cx & 3) and clamps the origin
+// to [-20, H+3] x [-32, W+15] (refbuf.h:22-26, mbuffer.c:549-550); the padded
+// sub-image holds every sample the block then reads.
+template <int NQ>
+__device__ __forceinline__ unsigned row_sad_grid(const Search &s, int cx, int cy, int r) {
+  const int pl = ((cy & 3) << 2) | (cx & 3);
+  const int yy = min(max(cy >> 2, -20), s.H + 3), xx = min(max(cx >> 2, -32), s.W + 15);
+  const uint8_t *a = s.ref + (size_t)pl * s.ps + (size_t)(yy + 20 + r) * s.pitch + (xx + 32);
+  const uintptr_t u = reinterpret_cast<uintptr_t>(a);
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(u & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)(u & 3);
+  const uint32_t *cur = s.cur + r * NQ;
+  uint32_t v[NQ + 1];
+#pragma unroll
+  for (int q = 0; q <= NQ; ++q) v[q] = w[q];
+  unsigned sad = 0;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) sad = __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(v[q + 1], v[q], sh), cur[q], sad);
+  return sad;
+}
+
 // Costs (mv_cost + SAD << 5) of the candidates held by lanes 0..K-1 (qpel
 // (mx, my)), returned in the same lanes.  One lane per (candidate, row):
 // 64/bsy candidates per pass, row sums reduced inside aligned lane groups.
-template <int NQ, int LOGR>
+template <int NQ, int LOGR, bool GRID>
 __device__ __forceinline__ int64_t eval_t(const Search &s, int lane, int K, int mx, int my) {
   constexpr int R = 1 << LOGR, C = 64 >> LOGR;
   const int grp = lane >> LOGR, r = lane & (R - 1);
@@ -126,7 +150,10 @@ __device__ __forceinline__ int64_t eval_t(const Search &s, int lane, int K, int 
   for (int base = 0; base < K; base += C) {
     const int c = base + grp;
     const int cmx = __shfl(mx, c & 63, 64), cmy = __shfl(my, c & 63, 64);
-    unsigned sad = c < K ? row_sad<NQ>(s, s.pos_x + (cmx >> 2), s.pos_y + (cmy >> 2), r) : 0u;
+    unsigned sad = 0u;
+    if (c < K)
+      sad = GRID ? row_sad_grid<NQ>(s, (s.pos_x << 2) + cmx, (s.pos_y << 2) + cmy, r)
+                 : row_sad<NQ>(s, s.pos_x + (cmx >> 2), s.pos_y + (cmy >> 2), r);
 #pragma unroll
     for (int m = 1; m < R; m <<= 1) sad += __shfl_xor(sad, m, 64);
     const int j = lane - base;
@@ -137,12 +164,14 @@ __device__ __forceinline__ int64_t eval_t(const Search &s, int lane, int K, int 
   return mvc + ((int64_t)mine << 5);
 }
 
-__device__ __noinline__ int64_t eval_costs_v(const uint8_t *ref, int pitch, int W, int H, const uint32_t *cur,
+template <bool GRID>
+__device__ __noinline__ int64_t eval_costs_v(const uint8_t *ref, int pitch, size_t ps, int W, int H, const uint32_t *cur,
                                               int pos_x, int pos_y, int bsx, int bsy, int pred_x, int pred_y,
                                               int lambda, int lane, int K, int mx, int my) {
   Search s;
   s.ref = ref;
   s.pitch = pitch;
+  s.ps = ps;
   s.W = W;
   s.H = H;
   s.cur = cur;
@@ -154,20 +183,21 @@ __device__ __noinline__ int64_t eval_costs_v(const uint8_t *ref, int pitch, int 
   s.pred_y = pred_y;
   s.lambda = lambda;
   switch ((bsx << 8) | bsy) {
-    case (16 << 8) | 16: return eval_t<4, 4>(s, lane, K, mx, my);
-    case (16 << 8) | 8: return eval_t<4, 3>(s, lane, K, mx, my);
-    case (8 << 8) | 16: return eval_t<2, 4>(s, lane, K, mx, my);
-    case (8 << 8) | 8: return eval_t<2, 3>(s, lane, K, mx, my);
-    case (8 << 8) | 4: return eval_t<2, 2>(s, lane, K, mx, my);
-    case (4 << 8) | 8: return eval_t<1, 3>(s, lane, K, mx, my);
-    default: return eval_t<1, 2>(s, lane, K, mx, my);
+    case (16 << 8) | 16: return eval_t<4, 4, GRID>(s, lane, K, mx, my);
+    case (16 << 8) | 8: return eval_t<4, 3, GRID>(s, lane, K, mx, my);
+    case (8 << 8) | 16: return eval_t<2, 4, GRID>(s, lane, K, mx, my);
+    case (8 << 8) | 8: return eval_t<2, 3, GRID>(s, lane, K, mx, my);
+    case (8 << 8) | 4: return eval_t<2, 2, GRID>(s, lane, K, mx, my);
+    case (4 << 8) | 8: return eval_t<1, 3, GRID>(s, lane, K, mx, my);
+    default: return eval_t<1, 2, GRID>(s, lane, K, mx, my);
   }
 }
 
 // scalar arguments keep the out-of-line call's context in registers
+template <bool GRID>
 __device__ __forceinline__ int64_t eval_costs(const Search &s, int lane, int K, int mx, int my) {
-  return eval_costs_v(s.ref, s.pitch, s.W, s.H, s.cur, s.pos_x, s.pos_y, s.bsx, s.bsy, s.pred_x, s.pred_y, s.lambda,
-                      lane, K, mx, my);
+  return eval_costs_v<GRID>(s.ref, s.pitch, s.ps, s.W, s.H, s.cur, s.pos_x, s.pos_y, s.bsx, s.bsy, s.pred_x, s.pred_y,
+                            s.lambda, lane, K, mx, my);
 }
 
 // order-preserving compaction of the lanes with `pred` set: returns the
@@ -181,8 +211,12 @@ __device__ __forceinline__ int pack_index(bool pred, int &count) {
 __device__ __forceinline__ bool in_range(const Search &s, int mx, int my) {
   return abs(mx - s.cx) <= s.max_x && abs(my - s.cy) <= s.max_y;
 }
+// EPZSMap[max_y - mv.y + my][max_x - mv.x + mx] (me_epzs.c:223, me_epzs_int.c:214): on the integer
+// grid only every 4th cell is used, so cells are numbered per integer offset there
+template <bool GRID>
 __device__ __forceinline__ int cell_of(const Search &s, int mx, int my) {
-  return ((my - s.cy + s.max_y) >> 2) * s.side_x + ((mx - s.cx + s.max_x) >> 2);
+  return GRID ? (my - s.cy + s.max_y) * s.side_x + (mx - s.cx + s.max_x)
+              : ((my - s.cy + s.max_y) >> 2) * s.side_x + ((mx - s.cx + s.max_x) >> 2);
 }
 __device__ __forceinline__ bool test_cell(const Search &s, int c) { return (s.map[c >> 5] >> (c & 31)) & 1u; }
 __device__ __forceinline__ void set_cell(const Search &s, int c) { atomicOr(&s.map[c >> 5], 1u << (c & 31)); }
@@ -196,10 +230,13 @@ __device__ __forceinline__ int64_t rl64(int64_t v, int j) {
 
 __device__ __forceinline__ int16_t int_mv(int v) { return (int16_t)(v & 0xFFFC); }   // set_integer_mv
 
-__device__ void search_one(const EpzsParams &p, const jmme_epzs_req &q, WaveLds &w, int lane, jmme_epzs_res *out) {
+template <bool GRID>
+__device__ void search_one(const EpzsParams &p, const jmme_epzs_req &q, WaveLds &w, uint32_t *map, int lane,
+                           jmme_epzs_res *out) {
   Search s;
-  s.ref = p.refs[q.ref_slot];
-  s.pitch = p.pitch;
+  s.ref = GRID ? p.subs[q.ref_slot] : p.refs[q.ref_slot];
+  s.pitch = GRID ? p.sub_pitch : p.pitch;
+  s.ps = p.plane_stride;
   s.W = p.width;
   s.H = p.height;
   s.pos_x = q.pos_x;
@@ -212,11 +249,11 @@ __device__ void search_one(const EpzsParams &p, const jmme_epzs_req &q, WaveLds 
   s.cy = q.center_y;
   s.max_x = q.max_x;
   s.max_y = q.max_y;
-  s.side_x = (2 * q.max_x >> 2) + 1;
+  s.side_x = GRID ? 2 * q.max_x + 1 : (2 * q.max_x >> 2) + 1;
   s.lambda = q.lambda;
   s.cur = w.cur;
-  s.map = w.map;
-  const int side_y = (2 * q.max_y >> 2) + 1;
+  s.map = map;
+  const int side_y = GRID ? 2 * q.max_y + 1 : (2 * q.max_y >> 2) + 1;
   const int nq = q.bsx >> 2;
 
   if (lane < nq * q.bsy) {
@@ -224,25 +261,28 @@ __device__ void search_one(const EpzsParams &p, const jmme_epzs_req &q, WaveLds 
     w.cur[lane] = *reinterpret_cast<const uint32_t *>(p.cur + (size_t)(q.pos_y + r) * p.pitch + q.pos_x + 4 * c);
   }
   const int words = (s.side_x * side_y + 31) >> 5;
-  for (int i = lane; i < words; i += 64) w.map[i] = 0;
+  for (int i = lane; i < words; i += 64) map[i] = 0;
   wave_sync();
   for (int i = lane; i < q.n_stale; i += 64) {   // cells already holding this BlkCount
     const int dx = p.stale[2 * (q.stale_off + i)], dy = p.stale[2 * (q.stale_off + i) + 1];
-    if (!(dx & 3) && !(dy & 3) && in_range(s, s.cx + dx, s.cy + dy)) set_cell(s, cell_of(s, s.cx + dx, s.cy + dy));
+    if ((GRID || (!(dx & 3) && !(dy & 3))) && in_range(s, s.cx + dx, s.cy + dy))
+      set_cell(s, cell_of<GRID>(s, s.cx + dx, s.cy + dy));
   }
-  if (lane == 0) set_cell(s, cell_of(s, s.cx, s.cy));
+  if (lane == 0) set_cell(s, cell_of<GRID>(s, s.cx, s.cy));
   wave_sync();
 
   const bool frame = q.flags & JMME_EPZS_FRAME, pslice = q.flags & JMME_EPZS_PSLICE;
-  const int bt = q.blocktype, refi = q.ref_idx, variant = q.variant;
+  // variant: the subMB form (EPZS_subMB_motion_estimation / EPZS_integer_subMB_motion_estimation)
+  const int bt = q.blocktype, refi = q.ref_idx, variant = GRID ? q.variant == 3 : q.variant;
   const int64_t lambda_dist = (int64_t)q.lambda * (variant ? 3 : 2);
   const int mv_range = variant ? 12 : 10;
   int64_t stop = q.medthres + lambda_dist, prev = q.prev_sad;
-  int64_t best = rl64(eval_costs(s, lane, 1, s.cx, s.cy), 0);
+  int64_t best = rl64(eval_costs<GRID>(s, lane, 1, s.cx, s.cy), 0);
   int tmpx = s.cx, tmpy = s.cy, path = 5;
   bool update = true;
 
-  if (refi > 0 && frame && prev < (stop < best ? stop : best)) {
+  // me_epzs_int.c:67-80 / 496-507 add prevSad * 8 (subMB: 6) < min to the ref > 0 early exit
+  if (refi > 0 && frame && (prev < (stop < best ? stop : best) || (GRID && prev * (variant ? 6 : 8) < best))) {
     path = 1;
     update = false;
   } else if (best > stop) {
@@ -252,7 +292,7 @@ __device__ void search_one(const EpzsParams &p, const jmme_epzs_req &q, WaveLds 
     stop = q.stop_crit;
     if (best < (stop >> 1)) {
       path = 2;
-      update = false;
+      update = GRID && !variant;   // EPZS_integer_motion_estimation keeps the value (me_epzs_int.c:118-120)
       done = true;
     }
     // predictors, 64 at a time; JM's order is restored in the fold
@@ -261,11 +301,15 @@ __device__ void search_one(const EpzsParams &p, const jmme_epzs_req &q, WaveLds 
       const bool valid = i < q.n_pred;
       int mx = 0, my = 0;
       if (valid) {
-        mx = int_mv(p.preds[2 * (q.pred_off + i)]);
-        my = int_mv(p.preds[2 * (q.pred_off + i) + 1]);
+        mx = p.preds[2 * (q.pred_off + i)];
+        my = p.preds[2 * (q.pred_off + i) + 1];
+        if (!GRID) {   // set_integer_mv (me_epzs.c:165)
+          mx = int_mv(mx);
+          my = int_mv(my);
+        }
       }
       const bool inr = valid && in_range(s, mx, my);
-      const int cell = inr ? cell_of(s, mx, my) : -1 - lane;
+      const int cell = inr ? cell_of<GRID>(s, mx, my) : -1 - lane;
       bool dup = inr && test_cell(s, cell);
       const int cnt = min(64, q.n_pred - base);
       for (int j = 0; j < cnt - 1; ++j) {   // an earlier predictor of this chunk on the same cell
@@ -283,15 +327,24 @@ __device__ void search_one(const EpzsParams &p, const jmme_epzs_req &q, WaveLds 
       wave_sync();
       const int px = lane < ke ? w.pk[lane][0] : 0, py = lane < ke ? w.pk[lane][1] : 0;
       wave_sync();
-      const int64_t cost = eval_costs(s, lane, ke, px, py);
+      const int64_t cost = eval_costs<GRID>(s, lane, ke, px, py);
       const int64_t thr3 = (3 * stop) >> 2;
+      // sub-pel grid subMB: before the 3/4 check, the ref > 0 prevSad exit that
+      // returns without touching *mv (me_epzs_int.c:590-600)
+      const bool pexit = GRID && variant && refi > 0 && frame;
       // me_epzs.c:583-596 checks after every predictor; between updates the
       // minimum is unchanged, so checking after index 0 and after each
       // evaluated one is the same
-      if (variant && base == 0 && !(__ballot(eval) & 1ull) && best < thr3) {
-        path = 3;
-        update = false;
-        done = true;
+      if (variant && base == 0 && !(__ballot(eval) & 1ull)) {
+        if (pexit && prev * 3 < best) {
+          path = 6;
+          update = false;
+          done = true;
+        } else if (best < thr3) {
+          path = 3;
+          update = false;
+          done = true;
+        }
       }
       for (int j = 0; !done && j < ke; ++j) {
         const int64_t c = rl64(cost, j);
@@ -310,20 +363,30 @@ __device__ void search_one(const EpzsParams &p, const jmme_epzs_req &q, WaveLds 
           second = c;
           check_median = true;
         }
-        if (variant && best < thr3) {
+        if (variant && pexit && prev * 3 < best) {
+          path = 6;
+          update = false;
+          done = true;
+        } else if (variant && best < thr3) {
           path = 3;
           update = false;
           done = true;
         }
       }
     }
+    if (GRID && !done && !variant && refi > 0 && frame && prev * 3 < best) {   // me_epzs_int.c:249-265
+      path = 7;
+      update = false;
+      done = true;
+    }
     if (!done && best > stop) {
       int P = primary_pattern(q.pattern);
       if (q.pattern != 0) {
         if (best < stop + ((3 * q.medthres) >> 1)) {
-          P = ((tmpx == 0 && tmpy == 0) || (abs(tmpx - s.cx) < mv_range && abs(tmpy - s.cy) < mv_range))
+          P = ((GRID && variant && bt == 7) || (tmpx == 0 && tmpy == 0) ||
+               (abs(tmpx - s.cx) < mv_range && abs(tmpy - s.cy) < mv_range))
                   ? P_SDIAMOND : P_SQUARE;
-        } else if (variant || bt > 4 || (refi > 0 && bt != 1)) {
+        } else if (variant || (!GRID && bt > 4) || (refi > 0 && bt != 1)) {   // me_epzs_int.c:282 drops bt > 4
           P = P_SQUARE;
         }
       }
@@ -337,7 +400,7 @@ __device__ void search_one(const EpzsParams &p, const jmme_epzs_req &q, WaveLds 
           const bool active = lane < total;
           const int mx = cenx + kPats[P].pt[active ? idx : 0][0], my = ceny + kPats[P].pt[active ? idx : 0][1];
           const bool inr = active && in_range(s, mx, my);
-          const int cell = inr ? cell_of(s, mx, my) : 0;
+          const int cell = inr ? cell_of<GRID>(s, mx, my) : 0;
           const bool eval = inr && !test_cell(s, cell);
           if (eval) set_cell(s, cell);
           int ke;
@@ -351,7 +414,7 @@ __device__ void search_one(const EpzsParams &p, const jmme_epzs_req &q, WaveLds 
           const int px = lane < ke ? w.pk[lane][0] : 0, py = lane < ke ? w.pk[lane][1] : 0;
           const int pi = lane < ke ? w.pk[lane][2] : 0;
           wave_sync();
-          const int64_t cost = eval_costs(s, lane, ke, px, py);
+          const int64_t cost = eval_costs<GRID>(s, lane, ke, px, py);
           for (int j = 0; j < ke; ++j) {
             const int64_t c = rl64(cost, j);
             if (c < best) {
@@ -381,13 +444,18 @@ __device__ void search_one(const EpzsParams &p, const jmme_epzs_req &q, WaveLds 
           update = false;
           break;
         }
-        if (!(check_median && (pslice || (!variant && bt < 5)) && best > stop && q.dual > 0)) break;
+        const bool dual_ok =
+            GRID ? check_median && !(variant && bt == 7) && (refi == 0 || best < 2 * prev) && (!variant || pslice) &&
+                       best > ((3 * stop) >> 1) && q.dual > 0   // me_epzs_int.c:337-340 / 298-301
+                 : check_median && (pslice || (!variant && bt < 5)) && best > stop && q.dual > 0;
+        if (!dual_ok) break;
         point = 0;
         pstop = 0;
         dir = 0;
         next_last = 0;
         if ((tmpx == 0 && tmpy == 0) || (tmpx == s.cx && tmpy == s.cy))
-          P = (abs(tmpx - s.cx) < mv_range && abs(tmpy - s.cy) < mv_range) ? P_SDIAMOND : P_SQUARE;
+          P = ((GRID && variant && bt == 7) || (abs(tmpx - s.cx) < mv_range && abs(tmpy - s.cy) < mv_range))
+                  ? P_SDIAMOND : P_SQUARE;
         else
           P = dual_pattern(q.dual);
         cenx = tmp2x;
@@ -397,7 +465,7 @@ __device__ void search_one(const EpzsParams &p, const jmme_epzs_req &q, WaveLds 
     }
   }
   if (update && (refi == 0 || prev > best)) prev = best;
-  if (path <= 2) {   // returned before touching *mv
+  if (path <= 2 || path == 6) {   // returned before touching *mv
     tmpx = s.cx;
     tmpy = s.cy;
   }
@@ -418,23 +486,48 @@ __device__ void search_one(const EpzsParams &p, const jmme_epzs_req &q, WaveLds 
 #endif
 // the search is latency-bound (a few dependent cache-resident fetch rounds
 // per search): waves in flight matter more than a few spilled registers
+template <bool GRID>
 __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(JMME_EPZS_WAVES_PER_EU))) void epzs_kernel(
     EpzsParams p) {
   __shared__ WaveLds s_w[kWaves];
+  extern __shared__ uint32_t s_map[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t *map = s_map + (size_t)wave * p.map_words;
   for (int t = blockIdx.x * kWaves + wave; t < p.n; t += gridDim.x * kWaves) {
     const jmme_epzs_req q = p.req[t];
-    search_one(p, q, s_w[wave], lane, p.out + t);
+    // requests of the other grid, or with a window the map was not sized for, are refused
+    const bool ok = (GRID ? q.variant >= 2 : q.variant <= 1) && q.max_x <= p.max_qpel && q.max_y <= p.max_qpel;
+    if (ok) {
+      search_one<GRID>(p, q, s_w[wave], map, lane, p.out + t);
+    } else if (lane == 0) {
+      jmme_epzs_res r{};
+      r.path = -1;
+      p.out[t] = r;
+    }
   }
 }
 
 }  // namespace
 
+size_t epzs_map_words(bool grid, int max_qpel) {
+  const size_t side = grid ? 2 * (size_t)max_qpel + 1 : 2 * (size_t)(max_qpel >> 2) + 1;
+  return (side * side + 31) / 32;
+}
+
 hipError_t launch_epzs(const EpzsParams &p, hipStream_t s) {
   int grid = (p.n + kWaves - 1) / kWaves;
   if (grid > 8192) grid = 8192;
   if (grid < 1) grid = 1;
-  hipLaunchKernelGGL(epzs_kernel, dim3(grid), dim3(kWG), 0, s, p);
+  const size_t lds = (size_t)kWaves * p.map_words * sizeof(uint32_t);
+  if (lds > 65536) {   // sub-pel grid beyond R = 45: one workgroup may take up to 160 KiB
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(p.grid ? epzs_kernel<true> : epzs_kernel<false>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  if (p.grid)
+    hipLaunchKernelGGL(epzs_kernel<true>, dim3(grid), dim3(kWG), lds, s, p);
+  else
+    hipLaunchKernelGGL(epzs_kernel<false>, dim3(grid), dim3(kWG), lds, s, p);
   return hipGetLastError();
 }
 

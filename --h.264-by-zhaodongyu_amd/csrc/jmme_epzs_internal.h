@@ -17,8 +17,16 @@ struct EpzsParams {
   const int16_t *preds, *stale;        // (x, y) pools
   jmme_epzs_res *out;
   int n;
+  // EPZSSubPelGrid = 1 (variants 2 / 3): candidates on the quarter-pel sub-images
+  int grid;
+  const uint8_t *const *subs;          // device table of sub-image sets (list * 32 + ref_idx)
+  int sub_pitch;
+  size_t plane_stride;
+  int max_qpel;                        // largest searchRange.max_x / max_y the map is sized for
+  int map_words;                       // epzs_map_words(grid, max_qpel)
 };
 
+size_t epzs_map_words(bool grid, int max_qpel);
 hipError_t launch_epzs(const EpzsParams &p, hipStream_t s);
 
 }  // namespace jmme

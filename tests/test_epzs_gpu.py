@@ -25,12 +25,19 @@ def _run_frame(me, cur, refs, req, preds, stale):
     return me.epzs_search(q, preds, stale)
 
 
+def _cfg_for(c):
+    """EPZSSubPelGrid fixtures need a context in grid mode, its map sized for their ranges"""
+    grid = int((c.r["variant"] >= 2).any())
+    rng = int(max(c.r["sr_max_x"].max(), c.r["sr_max_y"].max()) + 3) // 4
+    return {"EPZSSubPelGrid": grid, "SearchRange": max(rng, 1), "SearchMode": 3}
+
+
 @pytest.mark.parametrize("name", cases())
 def test_epzs_matches_jm(gpu, name):
     from jmme import MotionEstimator
     c = EpzsCase(name)
     n = 0
-    with MotionEstimator() as me:
+    with MotionEstimator(_cfg_for(c)) as me:
         for f, cur, refs, req, exp in c.frames():
             got = _run_frame(me, cur, refs, req, c.preds, c.stale)
             for k in ("mv_x", "mv_y", "cost", "prev_sad"):
@@ -97,6 +104,31 @@ def test_epzs_random_vs_restatement(gpu, seed):
         bad = np.nonzero(got[k] != exp[k])[0]
         assert len(bad) == 0, (k, len(bad), req[bad[:2]], got[bad[:2]], exp[bad[:2]])
     assert set(np.unique(exp["path"])) == {1, 2, 3, 4, 5}
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_epzs_grid_random_vs_restatement(gpu, seed):
+    """EPZSSubPelGrid = 1: quarter-pel centres / predictors / stale cells, the SBP diamond,
+    both variants, ranges up to 4 x SearchRange, picture-edge clamping on the sub-images"""
+    from jmme import MotionEstimator, synth
+    rng = np.random.default_rng(100 + seed)
+    w, h = 96, 64
+    luma = synth.luma_sequence(w, h, 3, seed=seed, gmv=(2, -1))
+    cur, refs = luma[2].astype(np.uint8), [luma[1].astype(np.uint8), luma[0].astype(np.uint8)]
+    req, preds, stale = _random_requests(rng, w, h, 2000)
+    req["variant"] += 2
+    req["center_x"] += rng.integers(-3, 4, len(req))
+    req["center_y"] += rng.integers(-3, 4, len(req))
+    req["max_x"] = np.minimum(req["max_x"], 128)
+    req["pattern"] = rng.choice([0, 1, 2, 3, 4, 5], len(req))
+    req["dual"] = rng.choice([0, 1, 2, 3, 4, 5, 6], len(req))
+    exp = ol.epzs_grid_batch(req, preds, stale, cur, refs)
+    with MotionEstimator({"EPZSSubPelGrid": 1, "SearchRange": 32, "SearchMode": 3}) as me:
+        got = _run_frame(me, cur, refs, req, preds, stale)
+    for k in ("mv_x", "mv_y", "path", "cost", "prev_sad"):
+        bad = np.nonzero(got[k] != exp[k])[0]
+        assert len(bad) == 0, (k, len(bad), req[bad[:2]], got[bad[:2]], exp[bad[:2]])
+    assert {1, 2, 3, 4, 5, 6, 7} <= set(np.unique(exp["path"]))
 
 
 def test_epzs_async_device_arrays(gpu):
