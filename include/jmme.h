@@ -232,11 +232,15 @@ int jmme_quant4x4_async(jmme_ctx *ctx, const jmme_quant4x4_params *d_params, con
 
 /* ---- EPZS integer-pel search --------------------------
  * EPZS_motion_estimation (variant 0) and EPZS_subMB_motion_estimation
- * (variant 1), JM/lencod/src/me_epzs.c:54-407 / 417-780, with
- * EPZSSubPelGrid = 0: median check and its early exits, the predictor list
- * (deduplicated through the EPZSMap), the refinement pattern walk
- * (EPZSPattern 0-3, 5; the half-pel SBP diamond 4 is not supported) and the
- * dual refinement around the second best (EPZSDualRefinement 0-4, 6).
+ * (variant 1), JM/lencod/src/me_epzs.c:54-407 / 417-780 (EPZSSubPelGrid = 0),
+ * and on the quarter-pel grid EPZS_integer_motion_estimation (variant 2) and
+ * EPZS_integer_subMB_motion_estimation (variant 3), me_epzs_int.c:41-782
+ * (EPZSSubPelGrid = 1 in the context's config; candidates costed on the
+ * sub-images of jmme_interpolate_ref, built automatically): median check and
+ * its early exits, the predictor list (deduplicated through the EPZSMap), the
+ * refinement pattern walk (EPZSPattern 0-5; the half-pel SBP diamond 4 only
+ * on the quarter-pel grid) and the dual refinement around the second best
+ * (EPZSDualRefinement 0-6, 5 only on the quarter-pel grid).
  * What JM builds on the host before the candidate search is input: the
  * predictor list (EPZS_spatial / _spatial_memory / _temporal /
  * EPZSWindowPredictors / EPZSBlockTypePredictors(MB), me_epzs_common.c), the
@@ -249,10 +253,11 @@ typedef struct jmme_epzs_req {
   int16_t bsx, bsy;            /* 16 / 8 / 4 */
   int16_t blocktype, ref_idx;  /* 1..7; reference index (the ref > 0 thresholds) */
   int16_t pred_x, pred_y;      /* MV predictor, qpel */
-  int16_t center_x, center_y;  /* mv_block->mv[list] on entry, qpel, integer (multiple of 4) */
+  int16_t center_x, center_y;  /* mv_block->mv[list] on entry, qpel (a multiple of 4 for variants 0/1) */
   int16_t max_x, max_y;        /* mv_block->searchRange.max_x / max_y, qpel */
   int32_t lambda;              /* lambda_factor[F_PEL] */
-  uint8_t variant;             /* 0 EPZS_motion_estimation, 1 EPZS_subMB_motion_estimation */
+  uint8_t variant;             /* 0 EPZS_motion_estimation, 1 EPZS_subMB_motion_estimation,
+                                  2 / 3 their EPZSSubPelGrid forms (me_epzs_int.c) */
   uint8_t flags;               /* JMME_EPZS_FRAME | JMME_EPZS_PSLICE */
   uint8_t pattern, dual;       /* EPZSPattern, EPZSDualRefinement */
   int32_t n_pred, pred_off;    /* predictor list: (x, y) qpel pairs at preds[pred_off ..] */
@@ -269,7 +274,7 @@ typedef struct jmme_epzs_req {
 
 typedef struct jmme_epzs_res {
   int16_t mv_x, mv_y;          /* mv_block->mv[list] on return, qpel */
-  int32_t path;                /* 1..5: which return of the JM function was taken */
+  int32_t path;                /* 1..7: which return of the JM function was taken (-1: refused) */
   int64_t cost;                /* return value (min_mcost) */
   int64_t prev_sad;            /* *prevSad on return */
 } jmme_epzs_res;               /* 24 bytes */
