@@ -8,6 +8,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -60,6 +61,9 @@ struct jmme_ctx {
   unsigned long long *d_stamps = nullptr;    // diagnostic builds only
   void *d_tree = nullptr;                    // fractal quadtree scratch (lists + per-level results)
   size_t cap_tree = 0;
+  void *d_pool = nullptr;                    // fractal pool images (7 sizes) + flags + survivor counter
+  size_t cap_pool = 0;
+  int pool_min_range = 80;                   // jmme_fractal_search: pruned pool search from this radius up
   size_t cap_stamps = 0;
   unsigned *d_counts = nullptr;              // [0] 32-bit items, [1] 64-bit items, [2] status
   Item *d_items = nullptr;                   // work items (one per unit x partition group)
@@ -240,6 +244,7 @@ extern "C" void jmme_destroy(jmme_ctx *ctx) {
   (void)hipFree(ctx->d_items);
   (void)hipFree(ctx->d_stamps);
   (void)hipFree(ctx->d_tree);
+  (void)hipFree(ctx->d_pool);
   for (auto *p : ctx->d_subs) (void)hipFree(p);
   (void)hipFree(ctx->d_sub_table);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
@@ -667,11 +672,53 @@ extern "C" int jmme_fractal_search_async(jmme_ctx *ctx, const uint8_t *d_org, in
   p.wpitch = width;
   p.width = width;
   p.height = height;
-  p.range = search_range;
+  // beyond max(W, H) every window is the whole picture: same candidates, same ranks
+  p.range = std::min(search_range, std::max(width, height));
   p.req = d_req;
   p.out = d_out;
   p.n = n;
-  HIPCHK(launch_fractal_search(p, reinterpret_cast<hipStream_t>(stream)));
+  if (p.range < ctx->pool_min_range) {
+    HIPCHK(launch_fractal_search(p, reinterpret_cast<hipStream_t>(stream)));
+    return 0;
+  }
+  // pruned pool search: scratch = 7 pool images + flags + counter
+  const size_t img = ((size_t)width * height * sizeof(float) * 2 + 255) & ~(size_t)255;
+  const size_t bytes = 7 * img + 256;
+  if (bytes > ctx->cap_pool) {
+    (void)hipFree(ctx->d_pool);
+    ctx->d_pool = nullptr;
+    ctx->cap_pool = 0;
+    HIPCHK(hipMalloc(&ctx->d_pool, bytes));
+    HIPCHK(hipMemset(ctx->d_pool, 0, bytes));
+    ctx->cap_pool = bytes;
+  }
+  char *base = static_cast<char *>(ctx->d_pool);
+  FractalPoolParams pp{};
+  pp.base = p;
+  // [0, 256): flags, counter (fixed offsets: the buffer outlives a smaller frame); then the images
+  pp.flags = reinterpret_cast<int *>(base);
+  pp.stats = reinterpret_cast<unsigned long long *>(base + 64);
+  for (int s = 0; s < 7; ++s) pp.pool[s] = base + 256 + (size_t)s * img;
+  pp.seed_range = 4;
+  HIPCHK(launch_fractal_pool(pp, reinterpret_cast<hipStream_t>(stream)));
+  return 0;
+}
+
+extern "C" int jmme_fractal_set_pool_min_range(jmme_ctx *ctx, int min_range) {
+  if (!ctx) return fail("null ctx");
+  if (min_range < 0) return fail("negative pool radius");
+  ctx->pool_min_range = min_range;
+  return 0;
+}
+
+extern "C" int jmme_fractal_pool_survivors(jmme_ctx *ctx, unsigned long long *survivors) {
+  if (!ctx || !survivors) return fail("null argument");
+  *survivors = 0;
+  if (!ctx->d_pool) return 0;
+  unsigned long long *d = reinterpret_cast<unsigned long long *>(static_cast<char *>(ctx->d_pool) + 64);
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(survivors, d, sizeof *survivors, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemset(d, 0, sizeof *survivors));
   return 0;
 }
 

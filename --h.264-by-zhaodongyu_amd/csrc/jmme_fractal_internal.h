@@ -38,6 +38,20 @@ struct FractalTreeParams {
   int *count;                     // count[1..3] (count[0] unused)
 };
 
+// pruned domain-pool search (jmme_fractal_pool.hip): the windowed kernel at
+// radius seed_range seeds out[], then per block size present in req[] a pool
+// image (pool[s]: float2 {Σd, n·Σd² − (Σd)²} per domain position, wpitch x
+// height) and the pruned search over the full window
+struct FractalPoolParams {
+  FractalParams base;
+  void *pool[7];                  // 16x16, 16x8, 8x16, 8x8, 8x4, 4x8, 4x4
+  int *flags;                     // [8] sizes present (zeroed by the launcher)
+  unsigned long long *stats;      // [0] += exactly evaluated survivors
+  int seed_range;
+};
+
+hipError_t launch_fractal_pool(const FractalPoolParams &p, hipStream_t s);
+
 hipError_t launch_fractal_tree(const FractalTreeParams &p, hipStream_t s);
 
 hipError_t launch_fractal_words(const uint8_t *ref, int pitch, int W, int H, uint32_t *words, int wpitch,

@@ -191,6 +191,16 @@ class MotionEstimator:
         check(lib().jmme_fractal_search_async(self._ctx, d_org, pitch, d_words, width, height, int(search_range),
                                               d_req, int(n), d_out, stream))
 
+    def fractal_set_pool_min_range(self, min_range: int) -> None:
+        """radius from which fractal_search runs the pruned pool search (0: always, huge: never)."""
+        check(lib().jmme_fractal_set_pool_min_range(self._ctx, int(min_range)))
+
+    def fractal_pool_survivors(self) -> int:
+        """exactly evaluated pool-search candidates since the last call (synchronises)."""
+        v = np.zeros(1, np.uint64)
+        check(lib().jmme_fractal_pool_survivors(self._ctx, ptr(v)))
+        return int(v[0])
+
     def fractal_box_sums(self, plane: np.ndarray, bsx: int, bsy: int):
         """compute_domain_Sum for one block size -> (sum, sum2) float64 [(H-bsy+1), (W-bsx+1)]."""
         plane = np.ascontiguousarray(plane, np.uint8)

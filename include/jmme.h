@@ -386,6 +386,20 @@ int jmme_fractal_search_async(jmme_ctx *ctx, const uint8_t *d_org, int pitch, co
                               int height, int search_range, const jmme_fractal_req *d_req, int n,
                               jmme_fractal_res *d_out, void *stream);
 
+/* Large radii (search_range >= the pool radius, default 80; the BASELINE
+ * "full domain pool" is search_range >= max(width, height)) run the pruned
+ * pool search: every candidate whose least-squares bound
+ *   K - C^2/D  (K = sum (r - offset)^2, C = sum r*d - sum r * sum d / n,
+ *               D = sum d^2 - (sum d)^2 / n)
+ * already exceeds an exactly evaluated rms is skipped, the rest are evaluated
+ * exactly -- same results as the windowed kernel, bit for bit.  A radius
+ * above max(width, height) is the same search as max(width, height).
+ * set_pool_min_range chooses the switch-over radius (0: always pool, a huge
+ * value: never); pool_survivors returns (and clears) the number of exactly
+ * evaluated candidates since the last call (synchronises the device). */
+int jmme_fractal_set_pool_min_range(jmme_ctx *ctx, int min_range);
+int jmme_fractal_pool_survivors(jmme_ctx *ctx, unsigned long long *survivors);
+
 /* compute_domain_Sum / compute_range_Sum (ZL/src/compute.c:277-~1091) for one
  * block size: sum and sum of squares of every bsx x bsy box of the plane,
  * (height-bsy+1) x (width-bsx+1) doubles each (exact integers). */

@@ -3,7 +3,12 @@
 every 4x4 range block of a synthetic 1080p frame (129,600 blocks) searched over
 the thesis spiral of radius R, on one MI355X, next to the C restatement of the
 thesis's full_search on a bounded CPU sample.  One JSON line per R.
-Usage (GPU): python3 tools/bench_fractal.py [--ranges 7,16,32] [--iters 5]"""
+R = "full" is the full domain pool (R >= max(W, H)); radii >= 16 run the pruned
+pool search (csrc/jmme_fractal_pool.hip), --windowed forces the windowed kernel
+for comparison, --check-windowed compares every block of the pool result with
+the windowed kernel at the same radius, --content unrelated searches a noise
+frame against an unrelated noise reference (the least prunable case).
+Usage (GPU): python3 tools/bench_fractal.py [--ranges 7,16,32,full] [--iters 5]"""
 import argparse
 import json
 import os
@@ -24,10 +29,20 @@ def main():
     ap.add_argument("--ranges", default="7,16,32")
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--cpu-sample", type=int, default=1500)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bound on the CPU sample's estimated time")
+    ap.add_argument("--windowed", action="store_true")
+    ap.add_argument("--pool-min", type=int, default=80, help="radius from which the pruned pool search runs")
+    ap.add_argument("--check-windowed", action="store_true")
+    ap.add_argument("--content", default="motion", choices=["motion", "unrelated"])
     a = ap.parse_args()
     W, H = 1920, 1080
-    luma = synth.luma_sequence(W, H, 2, seed=77, gmv=(3, 2))
-    org, ref = luma[1].astype(np.uint8), luma[0].astype(np.uint8)
+    if a.content == "motion":
+        luma = synth.luma_sequence(W, H, 2, seed=77, gmv=(3, 2))
+        org, ref = luma[1].astype(np.uint8), luma[0].astype(np.uint8)
+    else:
+        g = np.random.default_rng(78)
+        org = g.integers(0, 256, (H, W), dtype=np.uint8)
+        ref = g.integers(0, 256, (H, W), dtype=np.uint8)
     ys, xs = np.mgrid[0:H:4, 0:W:4]
     req = np.zeros(xs.size, FRACTAL_REQ)
     req["block_x"], req["block_y"], req["bsx"], req["bsy"] = xs.ravel(), ys.ravel(), 4, 4
@@ -41,13 +56,16 @@ def main():
     d_out = torch.empty(n * FRACTAL_RES.itemsize, dtype=torch.uint8, device=dev)
     me = MotionEstimator()
     import oracle_lib as ol
-    for R in [int(r) for r in a.ranges.split(",")]:
+    pool_min = (1 << 30) if a.windowed else a.pool_min
+    me.fractal_set_pool_min_range(pool_min)
+    for R in [max(W, H) if r == "full" else int(r) for r in a.ranges.split(",")]:
         def step():
             me.fractal_words_async(d_ref.data_ptr(), W, W, H, d_words.data_ptr(), st)
             me.fractal_search_async(d_org.data_ptr(), W, d_words.data_ptr(), W, H, R, d_req.data_ptr(), n,
                                     d_out.data_ptr(), st)
         step()
         torch.cuda.synchronize()
+        me.fractal_pool_survivors()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(a.iters):
@@ -55,19 +73,34 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / a.iters
-        got = d_out.cpu().numpy().view(FRACTAL_RES)
-        # CPU: the restatement on a bounded sample (evenly spread blocks), checked too
-        sel = np.linspace(0, n - 1, min(a.cpu_sample, n)).astype(np.int64)
+        surv = me.fractal_pool_survivors() / a.iters
+        got = d_out.cpu().numpy().view(FRACTAL_RES).copy()
+        cand = (min(2 * R + 1, W) * min(2 * R + 1, H)) if R < max(W, H) else (W - 3) * (H - 3)
+        win_check = None
+        if a.check_windowed and R >= pool_min:
+            # the windowed kernel walks all (2R+1)^2 spiral ranks: an evenly spread subset of blocks
+            selw = np.linspace(0, n - 1, min(n, 4096)).astype(np.int64)
+            me.fractal_set_pool_min_range(1 << 30)
+            win = me.fractal_search(org, ref, R, req[selw])
+            me.fractal_set_pool_min_range(pool_min)
+            same = (win.view(np.uint8).reshape(len(selw), -1) == got[selw].view(np.uint8).reshape(len(selw), -1))
+            win_check = {"blocks": len(selw), "identical": int(same.all(1).sum())}
+        # CPU: the restatement on a bounded sample (evenly spread blocks), checked too;
+        # ~28 M candidate evaluations/s on one core bounds the sample
+        nsel = max(8, min(a.cpu_sample, n, int(a.cpu_seconds * 2.8e7 / cand)))
+        sel = np.linspace(0, n - 1, nsel).astype(np.int64)
         rq = np.stack([req["block_x"][sel], req["block_y"][sel], req["bsx"][sel], req["bsy"][sel]], 1).astype(np.int32)
         t0 = time.time()
         exp, xy = ol.fractal_search_batch(org, ref, R, rq)
         cpu_s = time.time() - t0
         exact = int(np.sum((got["rms"][sel] == exp[:, 0]) & (got["scale"][sel] == exp[:, 1]) &
                            (got["offset"][sel] == exp[:, 2]) & (got["x"][sel] == xy[:, 0]) & (got["y"][sel] == xy[:, 1])))
-        cand = (2 * R + 1) ** 2
         print(json.dumps({
             "metric": "fractal range blocks/sec (4x4, 1080p, thesis full_search)", "R": R,
+            "pool": R >= max(W, H), "content": a.content,
+            "kernel": "windowed" if R < pool_min else "pruned pool",
             "range_blocks": n, "candidates_per_block": cand, "ms_per_frame": round(ms, 4),
+            "exact_evals_per_block": round(surv / n, 2) if surv else None, "windowed_check": win_check,
             "value": round(n / (ms * 1e-3), 1), "unit": "range blocks/sec",
             "candidate_evals_per_s": round(n * cand / (ms * 1e-3), 1),
             "parity_vs_restatement": {"sample": len(sel), "exact": exact},
