@@ -71,9 +71,9 @@ def dist_env():
     return ws, rank, local
 
 
-def load_workload():
+def load_workload(case: str = CASE):
     import golden_io as g
-    c = g.Case(CASE)
+    c = g.Case(case)
     (f, lst, rf, idx), = list(c.groups())
     from jmme import FULL_SEARCH
     req, unit_of, slots = c.units(idx, FULL_SEARCH)
@@ -206,6 +206,49 @@ def subpel_block(dev, local: int, iters: int = 20) -> dict | None:
             "jm_me_time_with_subpel": c.meta.get("jm_me_time")}
 
 
+UHD_CASE = "c2_syn_4k_fs32"
+
+
+def uhd_block(dev, local: int, iters: int = 10) -> dict | None:
+    """The same full search at 4K (3840x2160: 32,400 MB x ref per P-frame), measured
+    on rank 0 with JM 18.5's own requests for a seeded 4K clip, parity vs JM."""
+    import golden_io as g
+    from jmme import BLOCK_RES, FULL_SEARCH, MotionEstimator, NSLOT
+    if UHD_CASE not in g.manifest():
+        return None
+    cur, ref, req, unit_of, slots, expect, meta = load_workload(UHD_CASE)
+    n = len(req)
+    me = MotionEstimator({"SearchRange": 32, "SearchMode": -1, "RDOptimization": 0}, device=local)
+    me.upload_cur(cur)
+    me.upload_ref(0, 0, ref)
+    d_req = torch.from_numpy(req.view(np.uint8).copy()).to(dev)
+    d_out = torch.zeros(n * NSLOT * BLOCK_RES.itemsize, dtype=torch.uint8, device=dev)
+    st = torch.cuda.current_stream(dev)
+    me.search_async(FULL_SEARCH, d_req.data_ptr(), n, d_out.data_ptr(), st.cuda_stream)
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    kms = []
+    e0.record(st)
+    for _ in range(iters):
+        me.search_async(FULL_SEARCH, d_req.data_ptr(), n, d_out.data_ptr(), st.cuda_stream)
+        kms.append(me.last_kernel_ms())
+    e1.record(st)
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / iters
+    out = d_out.cpu().numpy().view(BLOCK_RES).reshape(n, NSLOT)[unit_of, slots]
+    exact = int(np.sum((out["mv_x"] == expect[0]) & (out["mv_y"] == expect[1]) & (out["cost"] == expect[2])))
+    me.close()
+    kernel_ms = float(np.mean(kms))
+    return {"workload": "4K (3840x2160) FS +-32 SAD integer-pel, 1 ref, 32,400 MB x ref per frame, "
+                        "JM 18.5's own requests", "mb_per_step": n, "ms_per_frame": round(ms, 4),
+            "kernel_ms": round(kernel_ms, 4), "mb_per_s": round(n / (ms * 1e-3), 1),
+            "valu_frac": round(ABSDIFF_PER_UNIT * n / (kernel_ms * 1e-3) / VSAD_PEAK, 4),
+            "hbm_frac": round(ALG_BYTES_PER_UNIT * n / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6),
+            "parity": {"reference": "JM 18.5 lencod (captured)", "searches": int(len(expect[0])),
+                       "bit_exact": exact},
+            "jm_me_time_at_capture": meta.get("jm_me_time")}
+
+
 def reduce_over_ranks(wall: float, exact: int, ws: int, dev) -> tuple[float, int]:
     """Job time = the slowest rank's time; parity = the worst rank's count.
     The only collectives of the run (no data-path exchange: ranks own whole GOPs)."""
@@ -231,6 +274,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-subpel", action="store_true")
+    ap.add_argument("--no-uhd", action="store_true")
     args = ap.parse_args()
 
     ws, rank, local = dist_env()
@@ -324,6 +368,8 @@ def main():
         }
         if not args.no_subpel:
             line["subpel"] = subpel_block(dev, local)
+        if not args.no_uhd:
+            line["uhd"] = uhd_block(dev, local)
         print(json.dumps(line))
     me.close()
     if ws > 1:
