@@ -964,6 +964,72 @@ extern "C" int jmme_fractal_encode_mbs(jmme_ctx *ctx, const uint8_t *org, const 
   return 0;
 }
 
+// fractal decoder (block_dec.c:20-1160): views are device planes
+extern "C" int jmme_fractal_decode_mbs_async(jmme_ctx *ctx, const jmme_fractal_mb *d_mbs,
+                                             const uint8_t *const *d_views, int n_views, int pitch, int width,
+                                             int height, int component, uint8_t *d_rec, int *d_status,
+                                             void *stream) {
+  if (!ctx) return fail("null ctx");
+  if (fractal_geom_ok(pitch, width, height)) return -1;
+  if (width % 16 || height % 16) return fail("fractal macroblock plane %dx%d: need multiples of 16", width, height);
+  if (n_views < 1 || n_views > JMME_FRACTAL_MAX_VIEWS) return fail("n_views %d not in 1..%d", n_views, JMME_FRACTAL_MAX_VIEWS);
+  if (component < 1 || component > 3) return fail("component %d not 1 (Y), 2 (U) or 3 (V)", component);
+  if (!d_mbs || !d_views || !d_rec) return fail("null array");
+  FractalDecodeParams p{};
+  p.mbs = d_mbs;
+  for (int k = 0; k < n_views; ++k) {
+    if (!d_views[k]) return fail("null view %d", k);
+    p.views[k] = d_views[k];
+  }
+  p.n_views = n_views;
+  p.pitch = pitch;
+  p.width = width;
+  p.height = height;
+  p.component = component;
+  p.mbs_x = width / 16;
+  p.n_mb = (width / 16) * (height / 16);
+  p.rec = d_rec;
+  p.status = d_status;
+  HIPCHK(launch_fractal_decode(p, reinterpret_cast<hipStream_t>(stream)));
+  return 0;
+}
+
+extern "C" int jmme_fractal_decode_mbs(jmme_ctx *ctx, const jmme_fractal_mb *mbs, const uint8_t *const *views,
+                                       int n_views, int pitch, int width, int height, int component, uint8_t *rec) {
+  if (!ctx) return fail("null ctx");
+  if (fractal_geom_ok(pitch, width, height)) return -1;
+  if (width % 16 || height % 16) return fail("fractal macroblock plane %dx%d: need multiples of 16", width, height);
+  if (n_views < 1 || n_views > JMME_FRACTAL_MAX_VIEWS) return fail("n_views %d not in 1..%d", n_views, JMME_FRACTAL_MAX_VIEWS);
+  if (!mbs || !views || !rec) return fail("null array");
+  const size_t plane = (size_t)pitch * height;
+  const int n_mb = (width / 16) * (height / 16);
+  DevBuf dm, v[JMME_FRACTAL_MAX_VIEWS], dr, ds;
+  const uint8_t *dv[JMME_FRACTAL_MAX_VIEWS] = {};
+  HIPCHK(dm.alloc((size_t)n_mb * sizeof(jmme_fractal_mb)));
+  HIPCHK(hipMemcpy(dm.p, mbs, (size_t)n_mb * sizeof(jmme_fractal_mb), hipMemcpyHostToDevice));
+  for (int k = 0; k < n_views; ++k) {
+    if (!views[k]) return fail("null view %d", k);
+    HIPCHK(v[k].alloc(plane));
+    HIPCHK(hipMemcpy(v[k].p, views[k], plane, hipMemcpyHostToDevice));
+    dv[k] = (const uint8_t *)v[k].p;
+  }
+  HIPCHK(dr.alloc(plane));
+  HIPCHK(hipMemset(dr.p, 0, plane));
+  HIPCHK(ds.alloc(sizeof(int)));
+  HIPCHK(hipMemset(ds.p, 0, sizeof(int)));
+  if (jmme_fractal_decode_mbs_async(ctx, (const jmme_fractal_mb *)dm.p, dv, n_views, pitch, width, height, component,
+                                    (uint8_t *)dr.p, (int *)ds.p, nullptr))
+    return -1;
+  int status = 0;
+  HIPCHK(hipMemcpy(&status, ds.p, sizeof(int), hipMemcpyDeviceToHost));
+  if (status) return fail("fractal decode: a leaf maps to a view >= %d or its domain block leaves the plane", n_views);
+  // rows beyond `width` in a pitched plane are not the decoder's
+  std::vector<uint8_t> tmp(plane);
+  HIPCHK(hipMemcpy(tmp.data(), dr.p, plane, hipMemcpyDeviceToHost));
+  for (int y = 0; y < height; ++y) memcpy(rec + (size_t)y * pitch, tmp.data() + (size_t)y * pitch, width);
+  return 0;
+}
+
 extern "C" jmme_distblk jmme_fast_full_search_block(jmme_ctx *ctx, int list, int ref_idx, int pos_x, int pos_y,
                                                     int blocktype, const jmme_mv *pred_mv,
                                                     const jmme_mv *search_center, int surface_range,

@@ -406,7 +406,79 @@ __global__ __launch_bounds__(kWG) void tree_gate3_kernel(FractalTreeParams p) {
   p.out[b8 >> 2].sub[b8 & 3][s] = pick_view(p.res[3] + (size_t)t * p.n_refs, p.n_refs, true);
 }
 
+// ------------------------------------------------------------ decoder --
+// decode_one_macroblock / decode_block_rect / _8 / _4 (ZL/src/block_dec.c:
+// 20-1160), num_regions == 1.  The view a leaf reads depends on the level,
+// the component and the reference index (the thesis's per-level branches,
+// quirks included -- see oracle/fractal_oracle.c fro_leaf_view).
+enum { kL16, kL8, kL84, kL48, kL4 };
+
+__device__ __forceinline__ int leaf_view(int kind, int component, int ref) {
+  switch (kind) {
+    case kL16: return (ref >= 0 && ref <= 3) ? ref : -1;            // :126-209
+    case kL8: return ref == 0 ? 0 : 1;                              // :861-904
+    case kL84:
+    case kL48: return (ref == 0 || ref == 1 || ref == 2) ? ref : 3; // :558-701
+    default:                                                        // :1078-1146
+      if (component == 3) return ref == 0 ? 0 : ref == 2 ? 2 : 3;   // V repeats `reference==0` (:1135)
+      return (ref == 0 || ref == 1 || ref == 2) ? ref : 3;
+  }
+}
+
+// one workgroup per macroblock, one thread per pel; each leaf's domain box sum
+// is accumulated in LDS (exact integers), then every pel evaluates the
+// thesis's expression in its operand order
+__global__ __launch_bounds__(kWG) void fractal_decode_kernel(FractalDecodeParams p) {
+#pragma clang fp contract(off)
+  __shared__ int s_sum[16];
+  const int m = blockIdx.x, t = threadIdx.x;
+  const int px = t & 15, py = t >> 4;
+  if (t < 16) s_sum[t] = 0;
+  __syncthreads();
+  const jmme_fractal_mb &mb = p.mbs[m];
+  const int bx = (m % p.mbs_x) * 16, by = (m / p.mbs_x) * 16;
+  const jmme_fractal_node *node;
+  int kind, lx, ly, bsx, bsy;
+  if (mb.mb.partition == 0) {
+    node = &mb.mb; kind = kL16; lx = 0; ly = 0; bsx = 16; bsy = 16;
+  } else {
+    const int q = (py >> 3) * 2 + (px >> 3);
+    const int x8 = (px >> 3) * 8, y8 = (py >> 3) * 8;
+    const int part = mb.b8[q].partition;
+    if (part == 0) {
+      node = &mb.b8[q]; kind = kL8; lx = x8; ly = y8; bsx = 8; bsy = 8;
+    } else if (part == 1) {
+      const int h = (py & 7) >> 2;
+      node = &mb.sub[q][h]; kind = kL84; lx = x8; ly = y8 + 4 * h; bsx = 8; bsy = 4;
+    } else if (part == 2) {
+      const int h = (px & 7) >> 2;
+      node = &mb.sub[q][h]; kind = kL48; lx = x8 + 4 * h; ly = y8; bsx = 4; bsy = 8;
+    } else {
+      const int c = ((py & 7) >> 2) * 2 + ((px & 7) >> 2);
+      node = &mb.sub[q][c]; kind = kL4; lx = x8 + (c & 1) * 4; ly = y8 + (c >> 1) * 4; bsx = 4; bsy = 4;
+    }
+  }
+  const int leaf = (ly >> 2) * 4 + (lx >> 2);
+  const int v = leaf_view(kind, p.component, node->reference);
+  const int dx = bx + lx + node->x, dy = by + ly + node->y;
+  const bool ok = v >= 0 && v < p.n_views && dx >= 0 && dy >= 0 && dx + bsx <= p.width && dy + bsy <= p.height;
+  int d = 0;
+  if (ok) d = p.views[v][(size_t)(dy + py - ly) * p.pitch + dx + px - lx];
+  else if (p.status) atomicOr(p.status, 1);
+  atomicAdd(&s_sum[leaf], d);
+  __syncthreads();
+  const double scale = node->scale, offset = node->offset;
+  const double average_domain = (double)s_sum[leaf] / (double)(bsx * bsy);
+  const double a = 0.5 + scale * d + offset - scale * average_domain;
+  p.rec[(size_t)(by + py) * p.pitch + bx + px] = ok ? (uint8_t)(a < 0.0 ? 0 : (a > 255.0 ? 255 : a)) : 0;
+}
+
 }  // namespace
+
+hipError_t launch_fractal_decode(const FractalDecodeParams &p, hipStream_t s) {
+  if (p.n_mb > 0) hipLaunchKernelGGL(fractal_decode_kernel, dim3(p.n_mb), dim3(kWG), 0, s, p);
+  return hipGetLastError();
+}
 
 hipError_t launch_fractal_words(const uint8_t *ref, int pitch, int W, int H, uint32_t *words, int wpitch,
                                 hipStream_t s) {

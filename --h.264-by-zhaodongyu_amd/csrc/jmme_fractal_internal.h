@@ -54,6 +54,17 @@ hipError_t launch_fractal_pool(const FractalPoolParams &p, hipStream_t s);
 
 hipError_t launch_fractal_tree(const FractalTreeParams &p, hipStream_t s);
 
+// decoder (decode_one_macroblock and the block decoders, block_dec.c:20-1160)
+struct FractalDecodeParams {
+  const jmme_fractal_mb *mbs;
+  const uint8_t *views[JMME_FRACTAL_MAX_VIEWS];
+  int n_views, pitch, width, height, component, mbs_x, n_mb;
+  uint8_t *rec;
+  int *status;                    // |= 1 when a leaf's view or domain block is out of range (nullable)
+};
+
+hipError_t launch_fractal_decode(const FractalDecodeParams &p, hipStream_t s);
+
 hipError_t launch_fractal_words(const uint8_t *ref, int pitch, int W, int H, uint32_t *words, int wpitch,
                                 hipStream_t s);
 hipError_t launch_fractal_search(const FractalParams &p, hipStream_t s);

@@ -126,6 +126,8 @@ def lib() -> ctypes.CDLL:
         "jmme_epzs_search": (I, [P, P, I, P, I, P, I, P]),
         "jmme_epzs_search_async": (I, [P, P, I, P, P, P, P]),
         "jmme_fractal_encode_mbs_async": (I, [P, P, P, I, P, I, I, I, I, D, D, P, P]),
+        "jmme_fractal_decode_mbs": (I, [P, P, P, I, I, I, I, I, P]),
+        "jmme_fractal_decode_mbs_async": (I, [P, P, P, I, I, I, I, I, P, P, P]),
         "jmme_quant4x4_async": (I, [P, P, P, P, P, P, P, P, I, P]),
         "jmme_interpolate_ref": (I, [P, I, I, P]),
         "jmme_get_sub_images": (I, [P, I, I, P]),

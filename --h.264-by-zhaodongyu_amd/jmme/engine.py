@@ -283,6 +283,25 @@ class MotionEstimator:
                                             float(tol_16), float(tol_8), ptr(out)))
         return out
 
+    def fractal_decode_mbs(self, mbs: np.ndarray, views, component: int = 1) -> np.ndarray:
+        """decode_one_macroblock (ZL/src/block_dec.c:20) for every macroblock: the
+        reconstructed H x W plane of `component` (1 Y, 2 U, 3 V) from the trees `mbs`
+        (FRACTAL_MB, as fractal_encode_mbs returns them) and the decoder's views."""
+        views = [np.ascontiguousarray(v, np.uint8) for v in views]
+        h, w = views[0].shape
+        mbs = np.ascontiguousarray(mbs, _lib.FRACTAL_MB)
+        ptrs = (ctypes.c_void_p * len(views))(*[v.ctypes.data for v in views])
+        rec = np.zeros((h, w), np.uint8)
+        check(lib().jmme_fractal_decode_mbs(self._ctx, ptr(mbs), ptrs, len(views), w, w, h, int(component),
+                                            ptr(rec)))
+        return rec
+
+    def fractal_decode_mbs_async(self, d_mbs: int, d_views, pitch: int, width: int, height: int, component: int,
+                                 d_rec: int, d_status: int = 0, stream: int = 0) -> None:
+        ptrs = (ctypes.c_void_p * len(d_views))(*d_views)
+        check(lib().jmme_fractal_decode_mbs_async(self._ctx, d_mbs, ptrs, len(d_views), pitch, width, height,
+                                                  int(component), d_rec, d_status or None, stream))
+
     def fractal_encode_mbs_async(self, d_org: int, d_ref0: int, pitch: int, d_words, width: int, height: int,
                                  search_range: int, tol_16: float, tol_8: float, d_out: int, stream: int = 0) -> None:
         """device form: d_words = list of per-view words images (fractal_words_async)."""

@@ -457,6 +457,25 @@ int jmme_fractal_encode_mbs_async(jmme_ctx *ctx, const uint8_t *d_org, const uin
                                   int search_range, double tol_16, double tol_8, jmme_fractal_mb *d_out,
                                   void *stream);
 
+/* ---- Fractal decoder (reconstruction of a P plane from its trees) -------
+ * decode_one_macroblock, decode_block_rect, decode_block_8, decode_block_4
+ * (ZL/src/block_dec.c:20-1160), num_regions == 1, for every macroblock of a
+ * width x height plane (multiples of 16) of component 1 (Y), 2 (U) or 3 (V),
+ * from the jmme_fractal_mb trees jmme_fractal_encode_mbs produces.  views[k]
+ * is the plane the thesis's decoder reads for reference k (imgY_ref, _h, _m,
+ * _n or the chroma equivalents).  Each leaf pel is
+ *   (unsigned char) bound(0.5 + scale*d + offset - scale*avg),
+ * avg = (box sum of the leaf's domain block) / n, with the thesis's per-level
+ * view choice (8x8 leaves: reference 0 -> view 0, else view 1; V 4x4 leaves:
+ * reference 1 -> view 3).  Fails (sync form) when a leaf
+ * maps to a view >= n_views or its domain block leaves the plane; the async
+ * form sets *d_status |= 1 instead (d_status may be NULL) and writes 0 there. */
+int jmme_fractal_decode_mbs(jmme_ctx *ctx, const jmme_fractal_mb *mbs, const uint8_t *const *views, int n_views,
+                            int pitch, int width, int height, int component, uint8_t *rec);
+int jmme_fractal_decode_mbs_async(jmme_ctx *ctx, const jmme_fractal_mb *d_mbs, const uint8_t *const *d_views,
+                                  int n_views, int pitch, int width, int height, int component, uint8_t *d_rec,
+                                  int *d_status, void *stream);
+
 /* ---- timing of the last jmme_search_mbs* launch (HIP events on its stream) */
 float jmme_last_kernel_ms(jmme_ctx *ctx);
 

@@ -294,3 +294,87 @@ void fro_encode_mbs(const uint8_t *org, const uint8_t *const *refs, int n_refs, 
     }
   }
 }
+
+/* ---- decoder: block_dec.c -------------------------------------------------
+ * Leaf kinds and the view each one reads, per component and reference index
+ * (num_regions == 1 branches):
+ *   16x16  decode_one_macroblock  :126-209  reference 0..3 -> that view
+ *   8x8    decode_block_8         :861-904  reference 0 -> 0, anything else -> 1
+ *   8x4    decode_block_rect      :558-628  0, 1, 2 -> same; anything else -> 3
+ *   4x8    decode_block_rect      :637-701  0, 1, 2 -> same; anything else -> 3
+ *   4x4    decode_block_4         :1078-1146 0, 1, 2 -> same, else 3; for V
+ *          the second test repeats `reference==0` (:1135), so 1 -> 3
+ * The box sum is always taken from the same view as the pixels for these
+ * kinds (the mismatched 16x8 U branch, :437-440, belongs to the 16x8 / 8x16
+ * macroblock partitions the encoder never leaves behind). */
+enum { FRO_L16, FRO_L8, FRO_L84, FRO_L48, FRO_L4 };
+
+static int fro_leaf_view(int kind, int component, int ref) {
+  switch (kind) {
+    case FRO_L16: return (ref >= 0 && ref <= 3) ? ref : -1;
+    case FRO_L8: return ref == 0 ? 0 : 1;
+    case FRO_L84:
+    case FRO_L48: return (ref == 0 || ref == 1 || ref == 2) ? ref : 3;
+    default:
+      if (component == 3) return ref == 0 ? 0 : ref == 2 ? 2 : 3;
+      return (ref == 0 || ref == 1 || ref == 2) ? ref : 3;
+  }
+}
+
+/* one leaf: block_dec.c:212-227 (16x16), :712-727 (rect), :912-928 (8x8),
+ * :1150-1163 (4x4) -- avg = sum / (double)(bsx*bsy) with the box sum of the
+ * domain block (compute_domain_Sum's exact integer as a double) */
+static int fro_decode_leaf(const fro_node *t, int kind, int bx, int by, int bsx, int bsy,
+                           const uint8_t *const *views, int n_views, int pitch, int W, int H, int component,
+                           uint8_t *rec) {
+  const int v = fro_leaf_view(kind, component, t->reference);
+  if (v < 0 || v >= n_views) return -1;
+  const int dx = bx + t->x, dy = by + t->y;
+  if (dx < 0 || dy < 0 || dx + bsx > W || dy + bsy > H) return -1;
+  const uint8_t *ref = views[v];
+  long sum = 0;
+  for (int j = 0; j < bsy; ++j)
+    for (int i = 0; i < bsx; ++i) sum += ref[(size_t)(dy + j) * pitch + dx + i];
+  const double scale = t->scale, offset = t->offset;
+  const double average_domain = (double)sum / (double)(bsx * bsy);
+  for (int j = 0; j < bsy; ++j)
+    for (int i = 0; i < bsx; ++i) {
+      const double a = 0.5 + scale * ref[(size_t)(dy + j) * pitch + dx + i] + offset - scale * average_domain;
+      rec[(size_t)(by + j) * pitch + bx + i] = (unsigned char)(a < 0.0 ? 0 : (a > 255.0 ? 255 : a));   /* bound() */
+    }
+  return 0;
+}
+
+int fro_decode_mbs(const fro_mb *mbs, const uint8_t *const *views, int n_views, int pitch, int W, int H,
+                   int component, uint8_t *rec) {
+  const int mbs_x = W / 16, n_mb = mbs_x * (H / 16);
+  for (int m = 0; m < n_mb; ++m) {
+    const fro_mb *t = &mbs[m];
+    const int bx = (m % mbs_x) * 16, by = (m / mbs_x) * 16;
+    if (t->mb.partition == 0) {                                 /* :34 16x16 */
+      if (fro_decode_leaf(&t->mb, FRO_L16, bx, by, 16, 16, views, n_views, pitch, W, H, component, rec)) return -1;
+      continue;
+    }
+    for (int q = 0; q < 4; ++q) {                               /* :238-245 four 8x8 */
+      const int x8 = bx + (q & 1) * 8, y8 = by + (q >> 1) * 8;
+      const fro_node *b = &t->b8[q];
+      int e = 0;
+      if (b->partition == 0)                                    /* decode_block_8 :771 */
+        e = fro_decode_leaf(b, FRO_L8, x8, y8, 8, 8, views, n_views, pitch, W, H, component, rec);
+      else if (b->partition == 1)                               /* :932-937 rect pair, depth 2 */
+        for (int h = 0; h < 2 && !e; ++h)
+          e = fro_decode_leaf(&t->sub[q][h], FRO_L84, x8, y8 + 4 * h, 8, 4, views, n_views, pitch, W, H,
+                              component, rec);
+      else if (b->partition == 2)
+        for (int h = 0; h < 2 && !e; ++h)
+          e = fro_decode_leaf(&t->sub[q][h], FRO_L48, x8 + 4 * h, y8, 4, 8, views, n_views, pitch, W, H,
+                              component, rec);
+      else                                                      /* :940-945 four 4x4 */
+        for (int c = 0; c < 4 && !e; ++c)
+          e = fro_decode_leaf(&t->sub[q][c], FRO_L4, x8 + (c & 1) * 4, y8 + (c >> 1) * 4, 4, 4, views, n_views,
+                              pitch, W, H, component, rec);
+      if (e) return -1;
+    }
+  }
+  return 0;
+}

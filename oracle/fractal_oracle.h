@@ -73,6 +73,20 @@ typedef struct fro_mb {
 void fro_encode_mbs(const uint8_t *org, const uint8_t *const *refs, int n_refs, int pitch, int W, int H, int R,
                     double tol_16, double tol_8, fro_mb *out);
 
+/* decode_one_macroblock / decode_block_rect / decode_block_8 / decode_block_4
+ * (ZL/src/block_dec.c:20-1160), num_regions == 1, for every macroblock of a
+ * W x H plane of component `component` (1 = Y, 2 = U, 3 = V), from the trees
+ * fro_encode_mbs produces (16x16 leaves, 8x8 leaves, 8x4 / 4x8 pairs, 4x4).
+ * views[k] is the plane the decoder reads for reference k (the thesis's
+ * imgY_ref, _h, _m, _n, or the chroma equivalents).  Each leaf pixel is
+ *   (unsigned char) bound(0.5 + scale*d + offset - scale*avg),
+ * avg = (box sum of the domain block) / n.  Returns 0, or -1 when a leaf maps
+ * to a view index >= n_views (the per-level view quirks can map reference 1
+ * to view 3) or its domain block leaves the plane; rec is W x H, pitch bytes
+ * per row. */
+int fro_decode_mbs(const fro_mb *mbs, const uint8_t *const *views, int n_views, int pitch, int W, int H,
+                   int component, uint8_t *rec);
+
 #ifdef __cplusplus
 }
 #endif

@@ -368,3 +368,18 @@ def epzs_grid_batch(req, preds, stale, cur, refs):
     lib.eo_epzs_grid_batch(req.ctypes.data, len(req), preds.ctypes.data, stale.ctypes.data, cur.ctypes.data, w, ptrs,
                            w, h, out.ctypes.data)
     return out
+
+
+def fractal_decode_mbs(mbs, views, component=1):
+    """fro_decode_mbs: the thesis decoder (block_dec.c) -> (rc, rec H x W uint8)"""
+    lib = load_fractal()
+    views = [np.ascontiguousarray(v, np.uint8) for v in views]
+    h, w = views[0].shape
+    mbs = np.ascontiguousarray(mbs, FRO_MB)
+    ptrs = (ctypes.c_void_p * len(views))(*[v.ctypes.data for v in views])
+    rec = np.zeros((h, w), np.uint8)
+    lib.fro_decode_mbs.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                   ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    lib.fro_decode_mbs.restype = ctypes.c_int
+    rc = lib.fro_decode_mbs(mbs.ctypes.data, ptrs, len(views), w, w, h, int(component), rec.ctypes.data)
+    return rc, rec
