@@ -64,6 +64,7 @@ struct jmme_ctx {
   void *d_pool = nullptr;                    // fractal pool images (7 sizes) + flags + survivor counter
   size_t cap_pool = 0;
   int pool_min_range = 80;                   // jmme_fractal_search: pruned pool search from this radius up
+  int pool_mfma = 1;                         // 4x4 full pool: matrix-core bound test (0: VALU)
   size_t cap_stamps = 0;
   unsigned *d_counts = nullptr;              // [0] 32-bit items, [1] 64-bit items, [2] status
   Item *d_items = nullptr;                   // work items (one per unit x partition group)
@@ -683,7 +684,7 @@ extern "C" int jmme_fractal_search_async(jmme_ctx *ctx, const uint8_t *d_org, in
   }
   // pruned pool search: scratch = 7 pool images + flags + counter
   const size_t img = ((size_t)width * height * sizeof(float) * 2 + 255) & ~(size_t)255;
-  const size_t bytes = 7 * img + 256;
+  const size_t bytes = 8 * img + 256;
   if (bytes > ctx->cap_pool) {
     (void)hipFree(ctx->d_pool);
     ctx->d_pool = nullptr;
@@ -699,6 +700,8 @@ extern "C" int jmme_fractal_search_async(jmme_ctx *ctx, const uint8_t *d_org, in
   pp.flags = reinterpret_cast<int *>(base);
   pp.stats = reinterpret_cast<unsigned long long *>(base + 64);
   for (int s = 0; s < 7; ++s) pp.pool[s] = base + 256 + (size_t)s * img;
+  pp.bw = base + 256 + (size_t)7 * img;
+  pp.use_mfma = ctx->pool_mfma;
   pp.seed_range = 4;
   HIPCHK(launch_fractal_pool(pp, reinterpret_cast<hipStream_t>(stream)));
   return 0;
@@ -708,6 +711,12 @@ extern "C" int jmme_fractal_set_pool_min_range(jmme_ctx *ctx, int min_range) {
   if (!ctx) return fail("null ctx");
   if (min_range < 0) return fail("negative pool radius");
   ctx->pool_min_range = min_range;
+  return 0;
+}
+
+extern "C" int jmme_fractal_set_pool_mfma(jmme_ctx *ctx, int on) {
+  if (!ctx) return fail("null ctx");
+  ctx->pool_mfma = on != 0;
   return 0;
 }
 

@@ -48,6 +48,8 @@ struct FractalPoolParams {
   int *flags;                     // [8] sizes present (zeroed by the launcher)
   unsigned long long *stats;      // [0] += exactly evaluated survivors
   int seed_range;
+  void *bw;                       // 4x4 full pool on the matrix cores: bf16 words image (uint2, wpitch x height)
+  int use_mfma;
 };
 
 hipError_t launch_fractal_pool(const FractalPoolParams &p, hipStream_t s);

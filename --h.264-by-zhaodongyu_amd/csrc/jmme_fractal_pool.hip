@@ -272,6 +272,237 @@ __global__ __launch_bounds__(kPoolWG) void pool_search_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// 4x4 full pool on the matrix cores.  For a 32 x 32 tile of (domain position,
+// range block) pairs, Σrd is one v_mfma_f32_32x32x16_bf16: pels are integers
+// 0..255, exact in bf16, their products exact in f32 and every partial sum of
+// 16 of them (< 2^24) too, so D = Σrd exactly -- the same integer the VALU path
+// forms with v_dot4.  Operands: A = 32 domain positions of one row (lane l:
+// position x0 + (l & 31), pels of block rows 2h, 2h+1, h = l >> 5, from the
+// "bf16 words" image: 4 bf16 per position), B = 32 range blocks (lane l: block
+// l & 31, the same pel order -- A and B share the lane map, so the k order is
+// irrelevant).  D: lane l holds column l & 31 (its range block) and rows
+// (v&3) + 8(v>>2) + 4h (domain positions).  Epilogue per pair: one fma for
+// num', one mul and one fma for the bound test, a min -- the domain's {Σd, n·D}
+// come from the pool image through LDS.  A workgroup owns 128 range blocks
+// (4 column groups, B fragments in VGPRs for the whole stream) and its four
+// waves split the rows; survivors are evaluated exactly, one at a time, by the
+// whole wave (uniform), and update the wave's LDS copy of the block's best.
+typedef __bf16 mf_bf16x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t mf_u32x4 __attribute__((ext_vector_type(4)));
+typedef float mf_f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kMfCols = 4;
+constexpr int kMfBlocks = 32 * kMfCols;
+
+__device__ __forceinline__ uint32_t bf16_bits(uint32_t pel) { return __float_as_uint((float)pel) >> 16; }
+
+// bw[y][x] = pels x..x+3 of row y as 4 bf16 (x <= W-4)
+__global__ __launch_bounds__(kPoolWG) void bf16_words_kernel(const uint32_t *__restrict__ words, int wpitch, int W,
+                                                             int H, const int *__restrict__ flags,
+                                                             uint2 *__restrict__ bw) {
+  if (!flags[6]) return;
+  const int x = blockIdx.x * kPoolWG + threadIdx.x, y = blockIdx.y;
+  if (x > W - 4 || y >= H) return;
+  const uint32_t w = words[(size_t)y * wpitch + x];
+  bw[(size_t)y * wpitch + x] = make_uint2(bf16_bits(w & 255) | bf16_bits((w >> 8) & 255) << 16,
+                                          bf16_bits((w >> 16) & 255) | bf16_bits(w >> 24) << 16);
+}
+
+struct MfRange { double rs1, rs2, beta, K; int bx, by, bad, active; };
+
+__global__ __launch_bounds__(kPoolWG) void pool_mfma44_kernel(
+    const uint8_t *__restrict__ org, int pitch, const uint32_t *__restrict__ words, const uint2 *__restrict__ bw,
+    int wpitch, const float2 *__restrict__ pool, int W, int H, const jmme_fractal_req *__restrict__ req, int n,
+    const int *__restrict__ flags, jmme_fractal_res *__restrict__ out, unsigned long long *__restrict__ stats) {
+#pragma clang fp contract(off)
+  constexpr int NO = 16;
+  __shared__ MfRange s_rg[kMfBlocks];
+  __shared__ PoolBest s_best[kPoolWaves][kMfBlocks];
+  __shared__ float s_thr[kPoolWaves][kMfBlocks];
+  __shared__ float4 s_pd[kPoolWaves][16];          // the tile's 32 {Σd, n·D}
+  if (!flags[6]) return;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int hh = lane >> 5, col = lane & 31;
+  const int base = blockIdx.x * kMfBlocks;
+
+  // ---- range blocks: stats (one thread per block) and seeds ----
+  bool mine = false;
+  if (threadIdx.x < kMfBlocks) {
+    const int i = base + threadIdx.x;
+    MfRange rr{};
+    rr.active = i < n && req[i].bsx == 4 && req[i].bsy == 4;
+    mine = rr.active;
+    if (rr.active) {
+      rr.bx = req[i].block_x;
+      rr.by = req[i].block_y;
+      unsigned s1 = 0, s2 = 0;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const uint32_t v = *reinterpret_cast<const uint32_t *>(org + (size_t)(rr.by + r) * pitch + rr.bx);
+        s1 = __builtin_amdgcn_sad_u8(v, 0u, s1);
+        s2 = __builtin_amdgcn_udot4(v, v, s2, false);
+      }
+      rr.rs1 = (double)s1;
+      rr.rs2 = (double)s2;
+      rr.beta = (double)quan_a((int)(rr.rs1 / NO));
+      rr.bad = rr.beta < -60 || rr.beta > 255;
+      rr.K = rr.rs2 - 2.0 * rr.beta * rr.rs1 + NO * rr.beta * rr.beta;
+    }
+    s_rg[threadIdx.x] = rr;
+  }
+  if (!__syncthreads_or(mine)) return;
+  auto threshold = [&](const MfRange &rr, double T) -> float {
+    if (!rr.active || rr.bad) return INFINITY;
+    return (float)(((rr.K - T) - kMargin) / NO) * kShrink;
+  };
+  for (int t = lane; t < kMfBlocks; t += 64) {
+    const MfRange &rr = s_rg[t];
+    PoolBest b{2e30, 0x7fffffff, 0};
+    if (rr.active) {
+      const jmme_fractal_res sd = out[base + t];
+      b.rms = sd.rms;
+      b.rank = spiral_rank(sd.x, sd.y);
+      b.a = (int)lrint(sd.scale * 100);
+    }
+    s_best[wave][t] = b;
+    s_thr[wave][t] = threshold(rr, b.rms);
+  }
+  __syncthreads();
+
+  // ---- B fragments (range blocks) and per-lane constants, whole stream ----
+  mf_bf16x8 B[kMfCols];
+  float nsr[kMfCols], thr[kMfCols];
+#pragma unroll
+  for (int cb = 0; cb < kMfCols; ++cb) {
+    const MfRange &rr = s_rg[cb * 32 + col];
+    mf_u32x4 f = {0u, 0u, 0u, 0u};
+    if (rr.active) {
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        const uint32_t v = *reinterpret_cast<const uint32_t *>(org + (size_t)(rr.by + 2 * hh + r) * pitch + rr.bx);
+        f[2 * r] = bf16_bits(v & 255) | bf16_bits((v >> 8) & 255) << 16;
+        f[2 * r + 1] = bf16_bits((v >> 16) & 255) | bf16_bits(v >> 24) << 16;
+      }
+    }
+    B[cb] = __builtin_bit_cast(mf_bf16x8, f);
+    nsr[cb] = -(float)rr.rs1 / NO;
+    thr[cb] = s_thr[wave][cb * 32 + col];
+  }
+
+  const int xb = W - 4, yb = H - 4;
+  const int rows = yb + 1;
+  const int y0 = (int)((long long)rows * wave / kPoolWaves);
+  const int y1 = (int)((long long)rows * (wave + 1) / kPoolWaves);
+  unsigned long long surv_count = 0;
+  float2 *pdl = reinterpret_cast<float2 *>(s_pd[wave]);
+
+  // exact evaluation of one survivor (wave-uniform arguments)
+  auto exact = [&](int t, int xs, int y, unsigned rd) {
+    const MfRange &rr = s_rg[t];
+    unsigned ds1 = 0, ds2 = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const uint32_t d = words[(size_t)(y + r) * wpitch + xs];
+      ds1 = __builtin_amdgcn_sad_u8(d, 0u, ds1);
+      ds2 = __builtin_amdgcn_udot4(d, d, ds2, false);
+    }
+    RangeStats rg;
+    rg.rs1 = rr.rs1;
+    rg.rs2 = rr.rs2;
+    rg.beta = rr.beta;
+    rg.bad_beta = rr.bad;
+    int a;
+    const double rms = rms_of(ds1, ds2, rd, NO, rg, a);
+    const int rank = spiral_rank(xs - rr.bx, y - rr.by);
+    const PoolBest b = s_best[wave][t];
+    if (rms < b.rms || (rms == b.rms && rank < b.rank)) {
+      if (lane == 0) {
+        s_best[wave][t] = PoolBest{rms, rank, a};
+        s_thr[wave][t] = threshold(rr, rms);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  };
+
+  for (int y = y0; y < y1; ++y) {
+    const uint2 *brow0 = bw + (size_t)(y + 2 * hh) * wpitch;
+    const uint2 *brow1 = brow0 + wpitch;
+    const float2 *prow = pool + (size_t)y * wpitch;
+    for (int x0 = 0; x0 <= xb; x0 += 32) {
+      const int xc = min(x0 + col, xb);
+      const uint2 a0 = brow0[xc], a1 = brow1[xc];
+      const mf_u32x4 af = {a0.x, a0.y, a1.x, a1.y};
+      const mf_bf16x8 A = __builtin_bit_cast(mf_bf16x8, af);
+      if (hh == 0) pdl[col] = prow[xc];
+      __builtin_amdgcn_wave_barrier();
+      float sd[16], dt[16];
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const float4 q = s_pd[wave][4 * g + 2 * hh + p];     // positions 8g + 4h + 2p, +1
+          sd[4 * g + 2 * p] = q.x;
+          dt[4 * g + 2 * p] = q.y;
+          sd[4 * g + 2 * p + 1] = q.z;
+          dt[4 * g + 2 * p + 1] = q.w;
+        }
+      const bool tail = x0 + 31 > xb;
+#pragma unroll
+      for (int cb = 0; cb < kMfCols; ++cb) {
+        const mf_f32x16 D = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, B[cb], mf_f32x16{}, 0, 0, 0);
+        float e[16];
+        float emin = 1.0f;
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          const float num = __builtin_fmaf(nsr[cb], sd[v], D[v]);
+          e[v] = __builtin_fmaf(num, -num, thr[cb] * dt[v]);
+          if (tail) e[v] = (x0 + (v & 3) + 8 * (v >> 2) + 4 * hh <= xb) ? e[v] : 1.0f;
+          emin = fminf(emin, e[v]);
+        }
+        if (__any(!(emin > 0.0f))) {
+#pragma unroll
+          for (int v = 0; v < 16; ++v) {
+            unsigned long long m = __ballot(!(e[v] > 0.0f));
+            while (m) {
+              const int ln = __ffsll((long long)m) - 1;
+              m &= m - 1;
+              ++surv_count;
+              const int t = cb * 32 + (ln & 31);
+              const int xs = x0 + (v & 3) + 8 * (v >> 2) + 4 * (ln >> 5);
+              const unsigned rd = (unsigned)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(D[v]), ln));
+              exact(t, xs, y, rd);
+            }
+          }
+          thr[cb] = s_thr[wave][cb * 32 + col];
+        }
+      }
+    }
+  }
+
+  if (lane == 0 && surv_count) atomicAdd(stats, surv_count);
+  __syncthreads();
+  if (threadIdx.x < kMfBlocks && s_rg[threadIdx.x].active) {
+    const int t = threadIdx.x;
+    PoolBest best = s_best[0][t];
+#pragma unroll
+    for (int w = 1; w < kPoolWaves; ++w) {
+      const PoolBest o = s_best[w][t];
+      if (o.rms < best.rms || (o.rms == best.rms && o.rank < best.rank)) best = o;
+    }
+    int xi, yj;
+    spiral_xy(best.rank, xi, yj);
+    jmme_fractal_res res;
+    res.rms = best.rms;
+    res.scale = (double)best.a / 100;
+    res.offset = s_rg[t].beta;
+    res.x = xi;
+    res.y = yj;
+    out[base + t] = res;
+  }
+}
+
 template <int BSX, int BSY>
 hipError_t launch_size(const FractalPoolParams &p, int sidx, hipStream_t s) {
   const int W = p.base.width, H = p.base.height;
@@ -280,7 +511,13 @@ hipError_t launch_size(const FractalPoolParams &p, int sidx, hipStream_t s) {
                      0, s, p.base.words, p.base.wpitch, W, H, p.flags, sidx, pool);
   const bool full = p.base.range >= std::max(W - BSX, H - BSY);
   const dim3 grid((p.base.n + 63) / 64);
-  if (full)
+  if (BSX == 4 && BSY == 4 && full && p.bw && p.use_mfma) {
+    hipLaunchKernelGGL(bf16_words_kernel, dim3((W - 4 + kPoolWG) / kPoolWG, H), dim3(kPoolWG), 0, s, p.base.words,
+                       p.base.wpitch, W, H, p.flags, reinterpret_cast<uint2 *>(p.bw));
+    hipLaunchKernelGGL(pool_mfma44_kernel, dim3((p.base.n + kMfBlocks - 1) / kMfBlocks), dim3(kPoolWG), 0, s,
+                       p.base.org, p.base.pitch, p.base.words, reinterpret_cast<const uint2 *>(p.bw), p.base.wpitch,
+                       pool, W, H, p.base.req, p.base.n, p.flags, p.base.out, p.stats);
+  } else if (full)
     hipLaunchKernelGGL((pool_search_kernel<BSX, BSY, true>), grid, dim3(kPoolWG), 0, s, p.base.org, p.base.pitch,
                        p.base.words, p.base.wpitch, pool, W, H, p.base.range, p.base.req, p.base.n, p.flags, sidx,
                        p.base.out, p.stats);

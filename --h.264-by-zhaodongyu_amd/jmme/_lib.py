@@ -122,6 +122,7 @@ def lib() -> ctypes.CDLL:
         "jmme_fractal_box_sums": (I, [P, P, I, I, I, I, I, P, P]),
         "jmme_fractal_set_pool_min_range": (I, [P, I]),
         "jmme_fractal_pool_survivors": (I, [P, P]),
+        "jmme_fractal_set_pool_mfma": (I, [P, I]),
         "jmme_fractal_encode_mbs": (I, [P, P, P, I, I, I, I, I, D, D, P]),
         "jmme_epzs_search": (I, [P, P, I, P, I, P, I, P]),
         "jmme_epzs_search_async": (I, [P, P, I, P, P, P, P]),

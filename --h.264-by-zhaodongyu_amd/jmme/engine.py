@@ -195,6 +195,10 @@ class MotionEstimator:
         """radius from which fractal_search runs the pruned pool search (0: always, huge: never)."""
         check(lib().jmme_fractal_set_pool_min_range(self._ctx, int(min_range)))
 
+    def fractal_set_pool_mfma(self, on: bool) -> None:
+        """4x4 full-pool bound test on the matrix cores (default) or on the VALU."""
+        check(lib().jmme_fractal_set_pool_mfma(self._ctx, int(bool(on))))
+
     def fractal_pool_survivors(self) -> int:
         """exactly evaluated pool-search candidates since the last call (synchronises)."""
         v = np.zeros(1, np.uint64)

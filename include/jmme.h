@@ -399,6 +399,10 @@ int jmme_fractal_search_async(jmme_ctx *ctx, const uint8_t *d_org, int pitch, co
  * evaluated candidates since the last call (synchronises the device). */
 int jmme_fractal_set_pool_min_range(jmme_ctx *ctx, int min_range);
 int jmme_fractal_pool_survivors(jmme_ctx *ctx, unsigned long long *survivors);
+/* 4x4 blocks over the full pool run the bound test on the matrix cores
+ * (exact bf16 products, f32 sums of 16); on = 0 selects the VALU kernel
+ * (for comparison; same results). */
+int jmme_fractal_set_pool_mfma(jmme_ctx *ctx, int on);
 
 /* compute_domain_Sum / compute_range_Sum (ZL/src/compute.c:277-~1091) for one
  * block size: sum and sum of squares of every bsx x bsy box of the plane,

@@ -58,6 +58,10 @@ CASES = {
     "epzs_syn_1080p_r32": dict(src="synth", w=1920, h=1080, frames=2, seed=2024, gmv=(5, 3),
                                p={**EPZS_INT, "SearchRange": 32, "NumberReferenceFrames": 1,
                                   "RDOptimization": 1, "MDDistortion": 2}, keep="compact"),
+    # BASELINE configs[3] at one GPU: 4K EPZS with RDO mode decision and SATD (level 5.1 for the picture size)
+    "epzs_syn_4k_r32": dict(src="synth", w=3840, h=2160, frames=2, seed=4096, gmv=(5, 3),
+                            p={**EPZS_INT, "LevelIDC": 51, "SearchRange": 32, "NumberReferenceFrames": 1,
+                               "RDOptimization": 1, "MDDistortion": 2}, keep="compact"),
     # EPZSSubPelGrid = 1 (variants 2 / 3): JM's encoder_baseline.cfg as shipped, + the SBP diamond pattern
     "epzs_grid_foreman_qcif": dict(src="foreman", w=176, h=144, frames=3, p={**EPZS_GRID}),
     "epzs_grid_foreman_qcif_p4d5": dict(src="foreman", w=176, h=144, frames=3,

@@ -151,8 +151,31 @@ def test_pool_matches_windowed_kernel(me):
 def test_pool_survivor_counter(me):
     h, w = 64, 64
     org, ref = _frames(h, w, 1)
+    me.fractal_set_pool_min_range(0)          # a 64x64 picture clamps the radius to 64 < the default 80
     me.fractal_pool_survivors()
     me.fractal_search(org, ref, 1000, _all_blocks(w, h, 4, 4))
+    me.fractal_set_pool_min_range(80)
     n = me.fractal_pool_survivors()
     assert 0 < n < 256 * 61 * 61
     assert me.fractal_pool_survivors() == 0
+
+
+def test_pool_mfma_matches_valu_kernel(me):
+    """4x4 full pool: the matrix-core bound test and the VALU one give the same
+    bits (both exact; they differ only in which candidates they evaluate)"""
+    h, w = 144, 176
+    for seed, content in [(31, "motion"), (32, "noise")]:
+        if content == "motion":
+            org, ref = _frames(h, w, seed, gmv=(-2, 3))
+        else:
+            rng = np.random.default_rng(seed)
+            org = rng.integers(0, 256, (h, w), dtype=np.uint8)
+            ref = rng.integers(0, 256, (h, w), dtype=np.uint8)
+        req = _all_blocks(w, h, 4, 4)
+        me.fractal_set_pool_min_range(0)
+        me.fractal_set_pool_mfma(False)
+        valu = me.fractal_search(org, ref, 4096, req)
+        me.fractal_set_pool_mfma(True)
+        mfma = me.fractal_search(org, ref, 4096, req)
+        me.fractal_set_pool_min_range(80)
+        assert valu.tobytes() == mfma.tobytes()
