@@ -291,6 +291,7 @@ __global__ __launch_bounds__(kPoolWG) void pool_search_kernel(
 typedef __bf16 mf_bf16x8 __attribute__((ext_vector_type(8)));
 typedef uint32_t mf_u32x4 __attribute__((ext_vector_type(4)));
 typedef float mf_f32x16 __attribute__((ext_vector_type(16)));
+typedef float mf_f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int kMfCols = 4;
 constexpr int kMfBlocks = 32 * kMfCols;
@@ -320,7 +321,7 @@ __global__ __launch_bounds__(kPoolWG) void pool_mfma44_kernel(
   __shared__ MfRange s_rg[kMfBlocks];
   __shared__ PoolBest s_best[kPoolWaves][kMfBlocks];
   __shared__ float s_thr[kPoolWaves][kMfBlocks];
-  __shared__ float4 s_pd[kPoolWaves][16];          // the tile's 32 {Σd, n·D}
+  __shared__ float4 s_sd[kPoolWaves][8], s_dt[kPoolWaves][8];   // the tile's 32 Σd and n·D
   if (!flags[6]) return;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -396,7 +397,7 @@ __global__ __launch_bounds__(kPoolWG) void pool_mfma44_kernel(
   const int y0 = (int)((long long)rows * wave / kPoolWaves);
   const int y1 = (int)((long long)rows * (wave + 1) / kPoolWaves);
   unsigned long long surv_count = 0;
-  float2 *pdl = reinterpret_cast<float2 *>(s_pd[wave]);
+  float *sdl = reinterpret_cast<float *>(s_sd[wave]), *dtl = reinterpret_cast<float *>(s_dt[wave]);
 
   // exact evaluation of one survivor (wave-uniform arguments)
   auto exact = [&](int t, int xs, int y, unsigned rd) {
@@ -435,36 +436,59 @@ __global__ __launch_bounds__(kPoolWG) void pool_mfma44_kernel(
       const uint2 a0 = brow0[xc], a1 = brow1[xc];
       const mf_u32x4 af = {a0.x, a0.y, a1.x, a1.y};
       const mf_bf16x8 A = __builtin_bit_cast(mf_bf16x8, af);
-      if (hh == 0) pdl[col] = prow[xc];
+      if (hh == 0) {
+        const float2 pd = prow[xc];
+        sdl[col] = pd.x;
+        dtl[col] = pd.y;
+      }
       __builtin_amdgcn_wave_barrier();
       float sd[16], dt[16];
 #pragma unroll
-      for (int g = 0; g < 4; ++g)
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-          const float4 q = s_pd[wave][4 * g + 2 * hh + p];     // positions 8g + 4h + 2p, +1
-          sd[4 * g + 2 * p] = q.x;
-          dt[4 * g + 2 * p] = q.y;
-          sd[4 * g + 2 * p + 1] = q.z;
-          dt[4 * g + 2 * p + 1] = q.w;
-        }
+      for (int g = 0; g < 4; ++g) {                             // positions 8g + 4h .. +3
+        const float4 q = s_sd[wave][2 * g + hh], r = s_dt[wave][2 * g + hh];
+        sd[4 * g] = q.x; sd[4 * g + 1] = q.y; sd[4 * g + 2] = q.z; sd[4 * g + 3] = q.w;
+        dt[4 * g] = r.x; dt[4 * g + 1] = r.y; dt[4 * g + 2] = r.z; dt[4 * g + 3] = r.w;
+      }
       const bool tail = x0 + 31 > xb;
+      // e <= 0  <=>  the pair survives; the slow path recomputes D and e bit-identically
+      auto test = [&](const mf_f32x16 &D, float ns, float th, int v) {
+        const float num = __builtin_fmaf(ns, sd[v], D[v]);
+        const float e = __builtin_fmaf(num, -num, th * dt[v]);
+        return (tail && x0 + (v & 3) + 8 * (v >> 2) + 4 * hh > xb) ? 1.0f : e;
+      };
+      // the same arithmetic two values at a time (v_pk_fma_f32 / v_pk_mul_f32), tail-free tiles
+      auto emin_fast = [&](const mf_f32x16 &D, float ns, float th) {
+        const mf_f32x2 ns2 = {ns, ns}, th2 = {th, th};
+        float m = 1.0f;
+#pragma unroll
+        for (int v = 0; v < 16; v += 2) {
+          const mf_f32x2 d2 = {D[v], D[v + 1]}, s2 = {sd[v], sd[v + 1]}, t2 = {dt[v], dt[v + 1]};
+          const mf_f32x2 num = __builtin_elementwise_fma(ns2, s2, d2);
+          const mf_f32x2 e = __builtin_elementwise_fma(num, -num, th2 * t2);
+          m = fminf(m, fminf(e.x, e.y));
+        }
+        return m;
+      };
+      unsigned hit = 0;
 #pragma unroll
       for (int cb = 0; cb < kMfCols; ++cb) {
         const mf_f32x16 D = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, B[cb], mf_f32x16{}, 0, 0, 0);
-        float e[16];
-        float emin = 1.0f;
+        float emin;
+        if (!tail) {
+          emin = emin_fast(D, nsr[cb], thr[cb]);
+        } else {
+          emin = 1.0f;
 #pragma unroll
-        for (int v = 0; v < 16; ++v) {
-          const float num = __builtin_fmaf(nsr[cb], sd[v], D[v]);
-          e[v] = __builtin_fmaf(num, -num, thr[cb] * dt[v]);
-          if (tail) e[v] = (x0 + (v & 3) + 8 * (v >> 2) + 4 * hh <= xb) ? e[v] : 1.0f;
-          emin = fminf(emin, e[v]);
+          for (int v = 0; v < 16; ++v) emin = fminf(emin, test(D, nsr[cb], thr[cb], v));
         }
-        if (__any(!(emin > 0.0f))) {
-#pragma unroll
+        if (__any(!(emin > 0.0f))) hit |= 1u << cb;
+      }
+      if (hit) {                                           // rare: survivors, one at a time
+        for (int cb = 0; cb < kMfCols; ++cb) {
+          if (!((hit >> cb) & 1)) continue;
+          const mf_f32x16 D = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, B[cb], mf_f32x16{}, 0, 0, 0);
           for (int v = 0; v < 16; ++v) {
-            unsigned long long m = __ballot(!(e[v] > 0.0f));
+            unsigned long long m = __ballot(!(test(D, nsr[cb], thr[cb], v) > 0.0f));
             while (m) {
               const int ln = __ffsll((long long)m) - 1;
               m &= m - 1;
