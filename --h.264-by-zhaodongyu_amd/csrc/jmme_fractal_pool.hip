@@ -312,7 +312,7 @@ __global__ __launch_bounds__(kPoolWG) void bf16_words_kernel(const uint32_t *__r
 
 struct MfRange { double rs1, rs2, beta, K; int bx, by, bad, active; };
 
-__global__ __launch_bounds__(kPoolWG) void pool_mfma44_kernel(
+__global__ __launch_bounds__(kPoolWG, 4) void pool_mfma44_kernel(
     const uint8_t *__restrict__ org, int pitch, const uint32_t *__restrict__ words, const uint2 *__restrict__ bw,
     int wpitch, const float2 *__restrict__ pool, int W, int H, const jmme_fractal_req *__restrict__ req, int n,
     const int *__restrict__ flags, jmme_fractal_res *__restrict__ out, unsigned long long *__restrict__ stats) {
@@ -321,7 +321,7 @@ __global__ __launch_bounds__(kPoolWG) void pool_mfma44_kernel(
   __shared__ MfRange s_rg[kMfBlocks];
   __shared__ PoolBest s_best[kPoolWaves][kMfBlocks];
   __shared__ float s_thr[kPoolWaves][kMfBlocks];
-  __shared__ float4 s_sd[kPoolWaves][8], s_dt[kPoolWaves][8];   // the tile's 32 Σd and n·D
+  __shared__ float4 s_sd[2][kPoolWaves][8], s_dt[2][kPoolWaves][8];   // a tile's 32 Σd and n·D, double-buffered
   if (!flags[6]) return;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -372,6 +372,9 @@ __global__ __launch_bounds__(kPoolWG) void pool_mfma44_kernel(
   }
   __syncthreads();
 
+  // the bound test compares |num'| with sqrt(thr) * sqrt(n·D): thr <= 0 prunes nothing (st = -1),
+  // thr = inf prunes everything; sqrt's <= 1 ulp errors are far inside the 2^-18 shrink
+  auto st_of = [](float t) { return t > 0.0f ? __builtin_sqrtf(t) : -1.0f; };
   // ---- B fragments (range blocks) and per-lane constants, whole stream ----
   mf_bf16x8 B[kMfCols];
   float nsr[kMfCols], thr[kMfCols];
@@ -389,7 +392,7 @@ __global__ __launch_bounds__(kPoolWG) void pool_mfma44_kernel(
     }
     B[cb] = __builtin_bit_cast(mf_bf16x8, f);
     nsr[cb] = -(float)rr.rs1 / NO;
-    thr[cb] = s_thr[wave][cb * 32 + col];
+    thr[cb] = st_of(s_thr[wave][cb * 32 + col]);
   }
 
   const int xb = W - 4, yb = H - 4;
@@ -397,18 +400,15 @@ __global__ __launch_bounds__(kPoolWG) void pool_mfma44_kernel(
   const int y0 = (int)((long long)rows * wave / kPoolWaves);
   const int y1 = (int)((long long)rows * (wave + 1) / kPoolWaves);
   unsigned long long surv_count = 0;
-  float *sdl = reinterpret_cast<float *>(s_sd[wave]), *dtl = reinterpret_cast<float *>(s_dt[wave]);
+  auto sdl_of = [&](int b) { return reinterpret_cast<float *>(s_sd[b][wave]); };
+  auto dtl_of = [&](int b) { return reinterpret_cast<float *>(s_dt[b][wave]); };
+  float *sdl = sdl_of(0), *dtl = dtl_of(0);
 
-  // exact evaluation of one survivor (wave-uniform arguments)
-  auto exact = [&](int t, int xs, int y, unsigned rd) {
+  // exact evaluation of one survivor (wave-uniform arguments; ds1, ds2 are the
+  // domain block's integer sums, taken from the A fragment -- no memory access
+  // here, so the tile loop's vmcnt accounting stays exact)
+  auto exact = [&](int t, int xs, int y, unsigned rd, unsigned ds1, unsigned ds2) {
     const MfRange &rr = s_rg[t];
-    unsigned ds1 = 0, ds2 = 0;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const uint32_t d = words[(size_t)(y + r) * wpitch + xs];
-      ds1 = __builtin_amdgcn_sad_u8(d, 0u, ds1);
-      ds2 = __builtin_amdgcn_udot4(d, d, ds2, false);
-    }
     RangeStats rg;
     rg.rs1 = rr.rs1;
     rg.rs2 = rr.rs2;
@@ -427,83 +427,109 @@ __global__ __launch_bounds__(kPoolWG) void pool_mfma44_kernel(
     __builtin_amdgcn_wave_barrier();
   };
 
-  for (int y = y0; y < y1; ++y) {
-    const uint2 *brow0 = bw + (size_t)(y + 2 * hh) * wpitch;
-    const uint2 *brow1 = brow0 + wpitch;
-    const float2 *prow = pool + (size_t)y * wpitch;
-    for (int x0 = 0; x0 <= xb; x0 += 32) {
-      const int xc = min(x0 + col, xb);
-      const uint2 a0 = brow0[xc], a1 = brow1[xc];
-      const mf_u32x4 af = {a0.x, a0.y, a1.x, a1.y};
-      const mf_bf16x8 A = __builtin_bit_cast(mf_bf16x8, af);
-      if (hh == 0) {
-        const float2 pd = prow[xc];
-        sdl[col] = pd.x;
-        dtl[col] = pd.y;
+
+  // tiles (y, x0) in row-major order; the next tile's global loads are issued
+  // before the current tile's arithmetic, its {Σd, n·D} land in the other LDS
+  // buffer at the end of the step
+  const int ntx = xb / 32 + 1;                     // tiles per row
+  const int ntiles = (y1 - y0) * ntx;
+  struct TileIn { uint2 a0, a1; float2 pd; };
+  auto load = [&](int t, TileIn &in) {
+    if (t >= ntiles) return;
+    const int ty = y0 + t / ntx, tx = (t % ntx) * 32;
+    const int xc = min(tx + col, xb);
+    const uint2 *r0 = bw + (size_t)(ty + 2 * hh) * wpitch;
+    in.a0 = r0[xc];
+    in.a1 = r0[wpitch + xc];
+    in.pd = pool[(size_t)ty * wpitch + xc];        // both lane halves (one address per column)
+  };
+  int buf = 0;
+  // one tile: its {Σd, sqrt(n·D)} are in LDS buffer `buf`; at the end the next
+  // tile's (already loaded) values go to the other buffer
+  auto step = [&](int t, const TileIn &cur, const TileIn &nxt) {
+    const int y = y0 + t / ntx, x0 = (t % ntx) * 32;
+    const mf_u32x4 af = {cur.a0.x, cur.a0.y, cur.a1.x, cur.a1.y};
+    const mf_bf16x8 A = __builtin_bit_cast(mf_bf16x8, af);
+    __builtin_amdgcn_wave_barrier();
+    float sd[16], dt[16];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {                             // positions 8g + 4h .. +3
+      const float4 q = s_sd[buf][wave][2 * g + hh], r = s_dt[buf][wave][2 * g + hh];
+      sd[4 * g] = q.x; sd[4 * g + 1] = q.y; sd[4 * g + 2] = q.z; sd[4 * g + 3] = q.w;
+      dt[4 * g] = r.x; dt[4 * g + 1] = r.y; dt[4 * g + 2] = r.z; dt[4 * g + 3] = r.w;
+    }
+    const bool tail = x0 + 31 > xb;
+    // e < 0  <=>  |num'| < sqrt(thr) * sqrt(n·D): pruned; e >= 0: the pair survives
+    // (st = sqrt(thr) per lane, sdt = sqrt(n·D) per position; the slow path recomputes e bit-identically)
+    auto test = [&](const mf_f32x16 &D, float ns, float st, int v) {
+      const float num = __builtin_fmaf(ns, sd[v], D[v]);
+      const float e = __builtin_fmaf(-st, dt[v], __builtin_fabsf(num));
+      return (tail && x0 + (v & 3) + 8 * (v >> 2) + 4 * hh > xb) ? -1.0f : e;
+    };
+    unsigned hit = 0;
+#pragma unroll
+    for (int cb = 0; cb < kMfCols; ++cb) {
+      const mf_f32x16 D = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, B[cb], mf_f32x16{}, 0, 0, 0);
+      float emax = -1.0f;
+      if (!tail) {                    // the same arithmetic without the column mask
+#pragma unroll
+        for (int v = 0; v < 16; ++v)
+          emax = fmaxf(emax, __builtin_fmaf(-thr[cb], dt[v], __builtin_fabsf(__builtin_fmaf(nsr[cb], sd[v], D[v]))));
+      } else {
+#pragma unroll
+        for (int v = 0; v < 16; ++v) emax = fmaxf(emax, test(D, nsr[cb], thr[cb], v));
       }
-      __builtin_amdgcn_wave_barrier();
-      float sd[16], dt[16];
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {                             // positions 8g + 4h .. +3
-        const float4 q = s_sd[wave][2 * g + hh], r = s_dt[wave][2 * g + hh];
-        sd[4 * g] = q.x; sd[4 * g + 1] = q.y; sd[4 * g + 2] = q.z; sd[4 * g + 3] = q.w;
-        dt[4 * g] = r.x; dt[4 * g + 1] = r.y; dt[4 * g + 2] = r.z; dt[4 * g + 3] = r.w;
-      }
-      const bool tail = x0 + 31 > xb;
-      // e <= 0  <=>  the pair survives; the slow path recomputes D and e bit-identically
-      auto test = [&](const mf_f32x16 &D, float ns, float th, int v) {
-        const float num = __builtin_fmaf(ns, sd[v], D[v]);
-        const float e = __builtin_fmaf(num, -num, th * dt[v]);
-        return (tail && x0 + (v & 3) + 8 * (v >> 2) + 4 * hh > xb) ? 1.0f : e;
-      };
-      // the same arithmetic two values at a time (v_pk_fma_f32 / v_pk_mul_f32), tail-free tiles
-      auto emin_fast = [&](const mf_f32x16 &D, float ns, float th) {
-        const mf_f32x2 ns2 = {ns, ns}, th2 = {th, th};
-        float m = 1.0f;
-#pragma unroll
-        for (int v = 0; v < 16; v += 2) {
-          const mf_f32x2 d2 = {D[v], D[v + 1]}, s2 = {sd[v], sd[v + 1]}, t2 = {dt[v], dt[v + 1]};
-          const mf_f32x2 num = __builtin_elementwise_fma(ns2, s2, d2);
-          const mf_f32x2 e = __builtin_elementwise_fma(num, -num, th2 * t2);
-          m = fminf(m, fminf(e.x, e.y));
-        }
-        return m;
-      };
-      unsigned hit = 0;
-#pragma unroll
+      if (__any(!(emax < 0.0f))) hit |= 1u << cb;
+    }
+    if (hit) {                                           // rare: survivors, one at a time
       for (int cb = 0; cb < kMfCols; ++cb) {
+        if (!((hit >> cb) & 1)) continue;
         const mf_f32x16 D = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, B[cb], mf_f32x16{}, 0, 0, 0);
-        float emin;
-        if (!tail) {
-          emin = emin_fast(D, nsr[cb], thr[cb]);
-        } else {
-          emin = 1.0f;
+        for (int v = 0; v < 16; ++v) {
+          unsigned long long m = __ballot(!(test(D, nsr[cb], thr[cb], v) < 0.0f));
+          while (m) {
+            const int ln = __ffsll((long long)m) - 1;
+            m &= m - 1;
+            ++surv_count;
+            const int tb = cb * 32 + (ln & 31);
+            const int xs = x0 + (v & 3) + 8 * (v >> 2) + 4 * (ln >> 5);
+            const unsigned rd = (unsigned)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(D[v]), ln));
+            const int pos = (v & 3) + 8 * (v >> 2) + 4 * (ln >> 5);   // lanes pos (rows 0-1), pos + 32 (rows 2-3)
+            unsigned ds1 = 0, ds2 = 0;
 #pragma unroll
-          for (int v = 0; v < 16; ++v) emin = fminf(emin, test(D, nsr[cb], thr[cb], v));
-        }
-        if (__any(!(emin > 0.0f))) hit |= 1u << cb;
-      }
-      if (hit) {                                           // rare: survivors, one at a time
-        for (int cb = 0; cb < kMfCols; ++cb) {
-          if (!((hit >> cb) & 1)) continue;
-          const mf_f32x16 D = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, B[cb], mf_f32x16{}, 0, 0, 0);
-          for (int v = 0; v < 16; ++v) {
-            unsigned long long m = __ballot(!(test(D, nsr[cb], thr[cb], v) > 0.0f));
-            while (m) {
-              const int ln = __ffsll((long long)m) - 1;
-              m &= m - 1;
-              ++surv_count;
-              const int t = cb * 32 + (ln & 31);
-              const int xs = x0 + (v & 3) + 8 * (v >> 2) + 4 * (ln >> 5);
-              const unsigned rd = (unsigned)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(D[v]), ln));
-              exact(t, xs, y, rd);
-            }
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+              for (int hl = 0; hl < 2; ++hl) {
+                const unsigned w = (unsigned)__builtin_amdgcn_readlane((int)af[k], pos + 32 * hl);
+                const unsigned p0 = (unsigned)__uint_as_float(w << 16), p1 = (unsigned)__uint_as_float(w & 0xffff0000u);
+                ds1 += p0 + p1;
+                ds2 += p0 * p0 + p1 * p1;
+              }
+            exact(tb, xs, y, rd, ds1, ds2);
           }
-          thr[cb] = s_thr[wave][cb * 32 + col];
         }
+        thr[cb] = st_of(s_thr[wave][cb * 32 + col]);
       }
     }
+    buf ^= 1;
+    sdl_of(buf)[col] = nxt.pd.x;                         // both halves store the same value: no branch,
+    dtl_of(buf)[col] = __builtin_sqrtf(nxt.pd.y);        // so the waitcnt pass sees one straight path
+  };
+  // two register sets X, Y alternate (unrolled by two, so no register copies
+  // wait on loads in flight): the tile after next loads while one computes
+  TileIn X{make_uint2(0, 0), make_uint2(0, 0), make_float2(0.f, 1.f)}, Y = X;
+  load(0, X);
+  load(1, Y);
+  sdl[col] = X.pd.x;
+  dtl[col] = __builtin_sqrtf(X.pd.y);
+  int t = 0;
+  for (; t + 1 < ntiles; t += 2) {       // both steps on every trip: exact vmcnt at the loop head
+    step(t, X, Y);
+    load(t + 2, X);
+    step(t + 1, Y, X);
+    load(t + 3, Y);
   }
+  if (t < ntiles) step(t, X, Y);
 
   if (lane == 0 && surv_count) atomicAdd(stats, surv_count);
   __syncthreads();
