@@ -321,7 +321,7 @@ __global__ __launch_bounds__(kPoolWG, 4) void pool_mfma44_kernel(
   __shared__ MfRange s_rg[kMfBlocks];
   __shared__ PoolBest s_best[kPoolWaves][kMfBlocks];
   __shared__ float s_thr[kPoolWaves][kMfBlocks];
-  __shared__ float4 s_sd[2][kPoolWaves][8], s_dt[2][kPoolWaves][8];   // a tile's 32 Σd and n·D, double-buffered
+  __shared__ float4 s_dt[2][kPoolWaves][8];        // a tile's 32 sqrt(n·D), double-buffered
   if (!flags[6]) return;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -375,23 +375,34 @@ __global__ __launch_bounds__(kPoolWG, 4) void pool_mfma44_kernel(
   // the bound test compares |num'| with sqrt(thr) * sqrt(n·D): thr <= 0 prunes nothing (st = -1),
   // thr = inf prunes everything; sqrt's <= 1 ulp errors are far inside the 2^-18 shrink
   auto st_of = [](float t) { return t > 0.0f ? __builtin_sqrtf(t) : -1.0f; };
-  // ---- B fragments (range blocks) and per-lane constants, whole stream ----
-  mf_bf16x8 B[kMfCols];
-  float nsr[kMfCols], thr[kMfCols];
+  // ---- B fragments (range blocks, centred) and per-lane constants, whole stream ----
+  // r~ = r - Σr/16 is a multiple of 1/16 below 256: hi = its top 8 significant
+  // bits (a bf16), lo = r~ - hi (exact in bf16 too), so two MFMAs give
+  // num' = Σ d·r~ = Σrd - Σr·Σd/16 exactly: every product and partial sum is a
+  // multiple of 1/16 below 2^20
+  mf_bf16x8 Bh[kMfCols], Bl[kMfCols];
+  float thr[kMfCols];
 #pragma unroll
   for (int cb = 0; cb < kMfCols; ++cb) {
     const MfRange &rr = s_rg[cb * 32 + col];
-    mf_u32x4 f = {0u, 0u, 0u, 0u};
+    mf_u32x4 fh = {0u, 0u, 0u, 0u}, fl = fh;
     if (rr.active) {
+      const float mean = (float)rr.rs1 / NO;
 #pragma unroll
       for (int r = 0; r < 2; ++r) {
         const uint32_t v = *reinterpret_cast<const uint32_t *>(org + (size_t)(rr.by + 2 * hh + r) * pitch + rr.bx);
-        f[2 * r] = bf16_bits(v & 255) | bf16_bits((v >> 8) & 255) << 16;
-        f[2 * r + 1] = bf16_bits((v >> 16) & 255) | bf16_bits(v >> 24) << 16;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const float rt = (float)((v >> (8 * c)) & 255) - mean;
+          const uint32_t hb = __float_as_uint(rt) >> 16;
+          const uint32_t lb = __float_as_uint(rt - __uint_as_float(hb << 16)) >> 16;
+          fh[2 * r + (c >> 1)] |= hb << (16 * (c & 1));
+          fl[2 * r + (c >> 1)] |= lb << (16 * (c & 1));
+        }
       }
     }
-    B[cb] = __builtin_bit_cast(mf_bf16x8, f);
-    nsr[cb] = -(float)rr.rs1 / NO;
+    Bh[cb] = __builtin_bit_cast(mf_bf16x8, fh);
+    Bl[cb] = __builtin_bit_cast(mf_bf16x8, fl);
     thr[cb] = st_of(s_thr[wave][cb * 32 + col]);
   }
 
@@ -400,9 +411,8 @@ __global__ __launch_bounds__(kPoolWG, 4) void pool_mfma44_kernel(
   const int y0 = (int)((long long)rows * wave / kPoolWaves);
   const int y1 = (int)((long long)rows * (wave + 1) / kPoolWaves);
   unsigned long long surv_count = 0;
-  auto sdl_of = [&](int b) { return reinterpret_cast<float *>(s_sd[b][wave]); };
   auto dtl_of = [&](int b) { return reinterpret_cast<float *>(s_dt[b][wave]); };
-  float *sdl = sdl_of(0), *dtl = dtl_of(0);
+  float *dtl = dtl_of(0);
 
   // exact evaluation of one survivor (wave-uniform arguments; ds1, ds2 are the
   // domain block's integer sums, taken from the A fragment -- no memory access
@@ -451,49 +461,50 @@ __global__ __launch_bounds__(kPoolWG, 4) void pool_mfma44_kernel(
     const mf_u32x4 af = {cur.a0.x, cur.a0.y, cur.a1.x, cur.a1.y};
     const mf_bf16x8 A = __builtin_bit_cast(mf_bf16x8, af);
     __builtin_amdgcn_wave_barrier();
-    float sd[16], dt[16];
+    float dt[16];
 #pragma unroll
     for (int g = 0; g < 4; ++g) {                             // positions 8g + 4h .. +3
-      const float4 q = s_sd[buf][wave][2 * g + hh], r = s_dt[buf][wave][2 * g + hh];
-      sd[4 * g] = q.x; sd[4 * g + 1] = q.y; sd[4 * g + 2] = q.z; sd[4 * g + 3] = q.w;
+      const float4 r = s_dt[buf][wave][2 * g + hh];
       dt[4 * g] = r.x; dt[4 * g + 1] = r.y; dt[4 * g + 2] = r.z; dt[4 * g + 3] = r.w;
     }
     const bool tail = x0 + 31 > xb;
     // e < 0  <=>  |num'| < sqrt(thr) * sqrt(n·D): pruned; e >= 0: the pair survives
     // (st = sqrt(thr) per lane, sdt = sqrt(n·D) per position; the slow path recomputes e bit-identically)
-    auto test = [&](const mf_f32x16 &D, float ns, float st, int v) {
-      const float num = __builtin_fmaf(ns, sd[v], D[v]);
-      const float e = __builtin_fmaf(-st, dt[v], __builtin_fabsf(num));
+    auto test = [&](const mf_f32x16 &D, float st, int v) {
+      const float e = __builtin_fmaf(-st, dt[v], __builtin_fabsf(D[v]));
       return (tail && x0 + (v & 3) + 8 * (v >> 2) + 4 * hh > xb) ? -1.0f : e;
+    };
+    auto num_of = [&](int cb) {
+      const mf_f32x16 Dh = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, Bh[cb], mf_f32x16{}, 0, 0, 0);
+      return __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, Bl[cb], Dh, 0, 0, 0);
     };
     unsigned hit = 0;
 #pragma unroll
     for (int cb = 0; cb < kMfCols; ++cb) {
-      const mf_f32x16 D = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, B[cb], mf_f32x16{}, 0, 0, 0);
+      const mf_f32x16 D = num_of(cb);
       float emax = -1.0f;
       if (!tail) {                    // the same arithmetic without the column mask
 #pragma unroll
-        for (int v = 0; v < 16; ++v)
-          emax = fmaxf(emax, __builtin_fmaf(-thr[cb], dt[v], __builtin_fabsf(__builtin_fmaf(nsr[cb], sd[v], D[v]))));
+        for (int v = 0; v < 16; ++v) emax = fmaxf(emax, __builtin_fmaf(-thr[cb], dt[v], __builtin_fabsf(D[v])));
       } else {
 #pragma unroll
-        for (int v = 0; v < 16; ++v) emax = fmaxf(emax, test(D, nsr[cb], thr[cb], v));
+        for (int v = 0; v < 16; ++v) emax = fmaxf(emax, test(D, thr[cb], v));
       }
       if (__any(!(emax < 0.0f))) hit |= 1u << cb;
     }
     if (hit) {                                           // rare: survivors, one at a time
       for (int cb = 0; cb < kMfCols; ++cb) {
         if (!((hit >> cb) & 1)) continue;
-        const mf_f32x16 D = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, B[cb], mf_f32x16{}, 0, 0, 0);
+        const mf_f32x16 D = num_of(cb);
         for (int v = 0; v < 16; ++v) {
-          unsigned long long m = __ballot(!(test(D, nsr[cb], thr[cb], v) < 0.0f));
+          unsigned long long m = __ballot(!(test(D, thr[cb], v) < 0.0f));
           while (m) {
             const int ln = __ffsll((long long)m) - 1;
             m &= m - 1;
             ++surv_count;
             const int tb = cb * 32 + (ln & 31);
             const int xs = x0 + (v & 3) + 8 * (v >> 2) + 4 * (ln >> 5);
-            const unsigned rd = (unsigned)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(D[v]), ln));
+            const float num = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(D[v]), ln));
             const int pos = (v & 3) + 8 * (v >> 2) + 4 * (ln >> 5);   // lanes pos (rows 0-1), pos + 32 (rows 2-3)
             unsigned ds1 = 0, ds2 = 0;
 #pragma unroll
@@ -505,6 +516,8 @@ __global__ __launch_bounds__(kPoolWG, 4) void pool_mfma44_kernel(
                 ds1 += p0 + p1;
                 ds2 += p0 * p0 + p1 * p1;
               }
+            // Σrd = num' + Σr·Σd/16, an integer (both terms are multiples of 1/16, exact in double)
+            const unsigned rd = (unsigned)((double)num + s_rg[tb].rs1 * (double)ds1 / NO);
             exact(tb, xs, y, rd, ds1, ds2);
           }
         }
@@ -512,15 +525,14 @@ __global__ __launch_bounds__(kPoolWG, 4) void pool_mfma44_kernel(
       }
     }
     buf ^= 1;
-    sdl_of(buf)[col] = nxt.pd.x;                         // both halves store the same value: no branch,
-    dtl_of(buf)[col] = __builtin_sqrtf(nxt.pd.y);        // so the waitcnt pass sees one straight path
+    dtl_of(buf)[col] = __builtin_sqrtf(nxt.pd.y);        // both halves store the same value: no branch,
+                                                         // so the waitcnt pass sees one straight path
   };
   // two register sets X, Y alternate (unrolled by two, so no register copies
   // wait on loads in flight): the tile after next loads while one computes
   TileIn X{make_uint2(0, 0), make_uint2(0, 0), make_float2(0.f, 1.f)}, Y = X;
   load(0, X);
   load(1, Y);
-  sdl[col] = X.pd.x;
   dtl[col] = __builtin_sqrtf(X.pd.y);
   int t = 0;
   for (; t + 1 < ntiles; t += 2) {       // both steps on every trip: exact vmcnt at the loop head
