@@ -444,9 +444,16 @@ __global__ __launch_bounds__(kPoolWG, 4) void pool_mfma44_kernel(
   const int ntx = xb / 32 + 1;                     // tiles per row
   const int ntiles = (y1 - y0) * ntx;
   struct TileIn { uint2 a0, a1; float2 pd; };
-  auto load = [&](int t, TileIn &in) {
-    if (t >= ntiles) return;
-    const int ty = y0 + t / ntx, tx = (t % ntx) * 32;
+  // tile coordinates advance incrementally (no divisions in the loop)
+  auto adv = [&](int &ty, int &tx) {
+    tx += 32;
+    if (tx > xb) {
+      tx = 0;
+      ++ty;
+    }
+  };
+  auto load = [&](int ty, int tx, TileIn &in) {
+    if (ty >= y1) return;
     const int xc = min(tx + col, xb);
     const uint2 *r0 = bw + (size_t)(ty + 2 * hh) * wpitch;
     in.a0 = r0[xc];
@@ -456,8 +463,7 @@ __global__ __launch_bounds__(kPoolWG, 4) void pool_mfma44_kernel(
   int buf = 0;
   // one tile: its {Σd, sqrt(n·D)} are in LDS buffer `buf`; at the end the next
   // tile's (already loaded) values go to the other buffer
-  auto step = [&](int t, const TileIn &cur, const TileIn &nxt) {
-    const int y = y0 + t / ntx, x0 = (t % ntx) * 32;
+  auto step = [&](int y, int x0, const TileIn &cur, const TileIn &nxt) {
     const mf_u32x4 af = {cur.a0.x, cur.a0.y, cur.a1.x, cur.a1.y};
     const mf_bf16x8 A = __builtin_bit_cast(mf_bf16x8, af);
     __builtin_amdgcn_wave_barrier();
@@ -479,9 +485,7 @@ __global__ __launch_bounds__(kPoolWG, 4) void pool_mfma44_kernel(
       return __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, Bl[cb], Dh, 0, 0, 0);
     };
     unsigned hit = 0;
-#pragma unroll
-    for (int cb = 0; cb < kMfCols; ++cb) {
-      const mf_f32x16 D = num_of(cb);
+    auto emax_of = [&](const mf_f32x16 &D, int cb) {
       float emax = -1.0f;
       if (!tail) {                    // the same arithmetic without the column mask
 #pragma unroll
@@ -490,7 +494,18 @@ __global__ __launch_bounds__(kPoolWG, 4) void pool_mfma44_kernel(
 #pragma unroll
         for (int v = 0; v < 16; ++v) emax = fmaxf(emax, test(D, thr[cb], v));
       }
-      if (__any(!(emax < 0.0f))) hit |= 1u << cb;
+      return emax;
+    };
+    // column groups in pairs: both hi MFMAs, then both lo MFMAs (each lo finds its hi
+    // done), then the two epilogues -- two accumulators live, no MFMA waits on its own chain
+#pragma unroll
+    for (int cb = 0; cb < kMfCols; cb += 2) {
+      mf_f32x16 D0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, Bh[cb], mf_f32x16{}, 0, 0, 0);
+      mf_f32x16 D1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, Bh[cb + 1], mf_f32x16{}, 0, 0, 0);
+      D0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, Bl[cb], D0, 0, 0, 0);
+      D1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, Bl[cb + 1], D1, 0, 0, 0);
+      if (__any(!(emax_of(D0, cb) < 0.0f))) hit |= 1u << cb;
+      if (__any(!(emax_of(D1, cb + 1) < 0.0f))) hit |= 2u << cb;
     }
     if (hit) {                                           // rare: survivors, one at a time
       for (int cb = 0; cb < kMfCols; ++cb) {
@@ -531,17 +546,25 @@ __global__ __launch_bounds__(kPoolWG, 4) void pool_mfma44_kernel(
   // two register sets X, Y alternate (unrolled by two, so no register copies
   // wait on loads in flight): the tile after next loads while one computes
   TileIn X{make_uint2(0, 0), make_uint2(0, 0), make_float2(0.f, 1.f)}, Y = X;
-  load(0, X);
-  load(1, Y);
+  int cy = y0, cx = 0;                 // the tile being computed
+  int ly = y0, lx = 0;                 // the next tile to load
+  load(ly, lx, X);
+  adv(ly, lx);
+  load(ly, lx, Y);
+  adv(ly, lx);
   dtl[col] = __builtin_sqrtf(X.pd.y);
   int t = 0;
   for (; t + 1 < ntiles; t += 2) {       // both steps on every trip: exact vmcnt at the loop head
-    step(t, X, Y);
-    load(t + 2, X);
-    step(t + 1, Y, X);
-    load(t + 3, Y);
+    step(cy, cx, X, Y);
+    adv(cy, cx);
+    load(ly, lx, X);
+    adv(ly, lx);
+    step(cy, cx, Y, X);
+    adv(cy, cx);
+    load(ly, lx, Y);
+    adv(ly, lx);
   }
-  if (t < ntiles) step(t, X, Y);
+  if (t < ntiles) step(cy, cx, X, Y);
 
   if (lane == 0 && surv_count) atomicAdd(stats, surv_count);
   __syncthreads();
