@@ -410,7 +410,7 @@ def main():
         ms_per_step = wall * 1e3 / args.steps
         ach = ALG_BYTES_PER_UNIT * n / (kernel_ms * 1e-3) / 1e9
         cpu = None
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and ws == 1:       # the CPU baseline is an N=1 figure
             cpu = cpu_baseline_jm(meta) or cpu_baseline_oracle(cur, ref, req)
         line = {
             "metric": "macroblocks/sec full-search ME @1080p; bit-exact MV/SAD vs JM18.5",
@@ -442,9 +442,9 @@ def main():
             "event_ms_per_step": round(ev_ms / args.steps, 4),
             "cpu_baseline": cpu,
         }
-        if not args.no_subpel:
+        if not args.no_subpel and ws == 1:
             line["subpel"] = subpel_block(dev, local)
-        if not args.no_uhd:
+        if not args.no_uhd and ws == 1:
             line["uhd"] = uhd_block(dev, local)
         print(json.dumps(line))
     me.close()
