@@ -1,0 +1,304 @@
+/*
+ * jm_gpu_me.c -- the JM side of the drop-in, built into a
+ * JM 18.5 lencod whose integer-pel motion search runs on the MI355X through
+ * libjmme (include/jmme.h).  JM's sources are not modified: this file is linked
+ * with JM's own objects (compiled from /root/reference by oracle/Makefile) and
+ * the GNU ld `--wrap` of three symbols, so the encoder's own call sites reach
+ * the GPU:
+ *
+ *   full_search_motion_estimation       JM/lencod/src/me_fullsearch.c:39-103
+ *       currMB->IntPelME for SearchMode = -1 (assigned mv_search.c:161,
+ *       called mv_search.c:960; signature JM/lencod/inc/global.h:459)
+ *   fast_full_search_motion_estimation  JM/lencod/src/me_fullfast.c:618-689
+ *       currMB->IntPelME for SearchMode = 0 (mv_search.c:168)
+ *   setup_fast_full_search              JM/lencod/src/me_fullfast.c:269-608
+ *       p_Vid->p_SetupFastFullPelSearch (global.h:469, mv_search.c:172): here it
+ *       only derives the search centre (me_fullfast.c:312-327) -- the SAD
+ *       surface JM would build on the CPU is the GPU's job
+ *
+ * Frame buffers: p_Vid->pCurImg (image.c:2868) and the reference pictures'
+ * imgY (StorablePicture, mbuffer.c:2116-2122) are uploaded once per coded
+ * picture (jmme_upload_cur / jmme_upload_ref).  Errors follow JM's error()
+ * convention (message, exit code 500).
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "global.h"
+#include "mbuffer.h"
+#include "me_fullfast.h"
+#include "mv_search.h"
+#include "jmme.h"
+
+extern void get_neighbors(Macroblock *currMB, PixelPos *block, int mb_x, int mb_y, int blockshape_x);
+
+static jmme_ctx *g_me = NULL;
+static int g_frame = -1000000;          /* p_Vid->frame_no of the uploaded planes */
+static int g_ref_up[2][32];              /* (list, ref) uploaded for g_frame */
+static long long g_calls = 0;
+
+static void fail_jm(const char *what)
+{
+  char buf[600];
+  snprintf(buf, sizeof buf, "jm_gpu_me: %s: %s", what, jmme_last_error());
+  error(buf, 500);
+}
+
+/* the encoder's ME configuration, from JM's own parsed parameters
+ * (JM/lencod/inc/configfile.h Map[] entries named in include/jmme.h) */
+static void init_once(VideoParameters *p_Vid, InputParameters *p_Inp)
+{
+  jmme_config c;
+  if (g_me) return;
+  jmme_config_default(&c);
+  c.SourceWidth = p_Vid->width;
+  c.SourceHeight = p_Vid->height;
+  c.SearchMode = p_Inp->SearchMode[0];
+  c.SearchRange = p_Inp->search_range[0];
+  c.NumberReferenceFrames = p_Inp->num_ref_frames;
+  c.DisableSubpelME = p_Inp->DisableSubpelME[0];
+  c.RDOptimization = p_Inp->rdopt;
+  c.MEDistortionFPel = p_Inp->MEErrorMetric[F_PEL];
+  c.MDDistortion = p_Inp->ModeDecisionMetric;
+  c.EPZSSubPelGrid = p_Inp->EPZSSubPelGrid;
+  c.RestrictSearchRange = p_Inp->full_search;
+  c.UseMVLimits = p_Inp->UseMVLimits;
+  c.SetMVXLimit = p_Inp->SetMVXLimit;
+  c.SetMVYLimit = p_Inp->SetMVYLimit;
+  c.ChromaMEEnable = p_Inp->ChromaMEEnable;
+  c.SourceBitDepthLuma = p_Inp->source.bit_depth[0];
+  g_me = jmme_create(&c, -1);
+  if (!g_me) fail_jm("jmme_create");
+}
+
+/* planes of the picture being coded and of the reference (list, ref) */
+static void ensure_planes(Macroblock *currMB, int list, int ref)
+{
+  VideoParameters *p_Vid = currMB->p_Vid;
+  Slice *currSlice = currMB->p_Slice;
+  StorablePicture *pic;
+  init_once(p_Vid, currMB->p_Inp);
+  if (p_Vid->frame_no != g_frame) {
+    g_frame = p_Vid->frame_no;
+    memset(g_ref_up, 0, sizeof g_ref_up);
+    if (jmme_upload_cur(g_me, (const jmme_imgpel *const *)p_Vid->pCurImg, p_Vid->width, p_Vid->height))
+      fail_jm("jmme_upload_cur");
+  }
+  if (list < 0 || list > 1 || ref < 0 || ref >= 32) error("jm_gpu_me: reference index out of range", 500);
+  if (!g_ref_up[list][ref]) {
+    pic = currSlice->listX[list + currMB->list_offset][ref];
+    if (jmme_upload_ref(g_me, list, ref, (const jmme_imgpel *const *)pic->imgY, pic->size_x, pic->size_y))
+      fail_jm("jmme_upload_ref");
+    g_ref_up[list][ref] = 1;
+  }
+}
+
+/* ---- speculative batching of full-search calls ----------------------------
+ * JM issues IntPelME one partition at a time, each with the predictor its
+ * neighbours' final vectors give, so the inputs of later searches are not known
+ * in advance.  They are usually the same as the current one's (smooth motion:
+ * every partition of a macroblock, and the next macroblocks, get the same
+ * predictor and centre), so on a miss the adapter searches, in ONE batched
+ * call (jmme_search_mbs), all 41 partitions of the next `g_batch` macroblocks
+ * with the current call's inputs as the guess, and caches (inputs -> result).
+ * A later call is answered from the cache only when its inputs are identical
+ * to the guessed ones -- a search is a pure function of (block, centre,
+ * predictor, lambda, range, check_for_00) on the uploaded planes -- so the
+ * encoder's output is unchanged; a miss re-batches from the missing
+ * macroblock.  The batch length adapts: it doubles when the cache ran out
+ * and halves when a guess failed.  JMME_SPECULATE=0 sends every call on its
+ * own (jmme_full_search_block). */
+typedef struct spec_ent {
+  int16_t cx, cy, px, py, sr, chk;
+  int32_t lambda;
+  int16_t mvx, mvy;
+  int64_t cost;
+  int8_t valid;
+} spec_ent;
+
+static spec_ent *g_spec[2][32];
+static int g_spec_frame[2][32];
+static int g_spec_end[2][32];      /* first macroblock past the last batch */
+static int g_batch = 64, g_speculate = -1, g_mbs_x = 0, g_n_mb = 0;
+static long long g_hits = 0, g_batches = 0;
+static jmme_mb_req *g_req = NULL;
+static jmme_block_res *g_res = NULL;
+static int g_req_cap = 0;
+
+static spec_ent *spec_table(VideoParameters *p_Vid, int list, int ref)
+{
+  int i;
+  if (!g_n_mb) {
+    g_mbs_x = p_Vid->width / 16;
+    g_n_mb = g_mbs_x * (p_Vid->height / 16);
+  }
+  if (!g_spec[list][ref]) {
+    g_spec[list][ref] = (spec_ent *)calloc((size_t)g_n_mb * JMME_NSLOT, sizeof(spec_ent));
+    if (!g_spec[list][ref]) error("jm_gpu_me: out of memory", 500);
+    g_spec_frame[list][ref] = -1000000;
+  }
+  if (g_spec_frame[list][ref] != p_Vid->frame_no) {       /* new picture: forget every guess */
+    for (i = 0; i < g_n_mb * JMME_NSLOT; i++) g_spec[list][ref][i].valid = 0;
+    g_spec_frame[list][ref] = p_Vid->frame_no;
+    g_spec_end[list][ref] = 0;
+  }
+  return g_spec[list][ref];
+}
+
+static void spec_batch(int list, int ref, int mb0, const spec_ent *guess, int chk00_slot0)
+{
+  spec_ent *tab = g_spec[list][ref];
+  int n = imin(g_batch, g_n_mb - mb0), i, s;
+  if (n > g_req_cap) {
+    free(g_req);
+    free(g_res);
+    g_req = (jmme_mb_req *)malloc((size_t)n * sizeof(jmme_mb_req));
+    g_res = (jmme_block_res *)malloc((size_t)n * JMME_NSLOT * sizeof(jmme_block_res));
+    if (!g_req || !g_res) error("jm_gpu_me: out of memory", 500);
+    g_req_cap = n;
+  }
+  memset(g_req, 0, (size_t)n * sizeof(jmme_mb_req));
+  for (i = 0; i < n; i++) {
+    jmme_mb_req *r = &g_req[i];
+    int mb = mb0 + i;
+    r->mb_x = (int16_t)((mb % g_mbs_x) * 16);
+    r->mb_y = (int16_t)((mb / g_mbs_x) * 16);
+    r->list = (int16_t)list;
+    r->ref_idx = (int16_t)ref;
+    r->slot_mask = (1ull << JMME_NSLOT) - 1;
+    for (s = 0; s < JMME_NSLOT; s++) {
+      jmme_block_req *b = &r->blk[s];
+      b->pred_x = guess->px;
+      b->pred_y = guess->py;
+      b->center_x = guess->cx;
+      b->center_y = guess->cy;
+      b->search_range = guess->sr;
+      b->flags = (int16_t)((s == 0 && chk00_slot0) ? JMME_BLK_CHECK00 : 0);
+      b->lambda = guess->lambda;
+    }
+  }
+  if (jmme_search_mbs(g_me, JMME_FULL_SEARCH, g_req, n, g_res)) fail_jm("jmme_search_mbs");
+  for (i = 0; i < n; i++)
+    for (s = 0; s < JMME_NSLOT; s++) {
+      spec_ent *e = &tab[(size_t)(mb0 + i) * JMME_NSLOT + s];
+      *e = *guess;
+      e->chk = (int16_t)(s == 0 && chk00_slot0);
+      e->mvx = g_res[i * JMME_NSLOT + s].mv_x;
+      e->mvy = g_res[i * JMME_NSLOT + s].mv_y;
+      e->cost = g_res[i * JMME_NSLOT + s].cost;
+      e->valid = 1;
+    }
+  g_spec_end[list][ref] = mb0 + n;
+  ++g_batches;
+}
+
+/* full_search_motion_estimation's contract (me_fullsearch.c:39-103) */
+distblk __wrap_full_search_motion_estimation(Macroblock *currMB, MotionVector *pred_mv, MEBlock *mv_block,
+                                             distblk min_mcost, int lambda_factor)
+{
+  VideoParameters *p_Vid = currMB->p_Vid;
+  Slice *currSlice = currMB->p_Slice;
+  int list = mv_block->list, ref = mv_block->ref_idx;
+  /* search_range and check_for_00 as me_fullsearch.c:49,61 derive them */
+  int search_range = imin(mv_block->searchRange.max_x, mv_block->searchRange.max_y) >> 2;
+  int chk_rule = !currMB->p_Inp->rdopt && currSlice->slice_type != B_SLICE && ref == 0;
+  int check_for_00 = mv_block->blocktype == 1 && chk_rule;
+  jmme_mv pred = {pred_mv->mv_x, pred_mv->mv_y};
+  jmme_mv mv = {mv_block->mv[list].mv_x, mv_block->mv[list].mv_y};   /* centre in */
+  distblk cost;
+  ensure_planes(currMB, list, ref);
+  ++g_calls;
+  if (g_speculate < 0) {
+    const char *e = getenv("JMME_SPECULATE");
+    g_speculate = !(e && e[0] == '0');
+  }
+  if (g_speculate) {
+    int mb_x = mv_block->pos_x >> 4, mb_y = mv_block->pos_y >> 4;
+    int mb = mb_y * (p_Vid->width / 16) + mb_x;
+    int s = jmme_slot(mv_block->blocktype, (mv_block->pos_x & 15) >> 2, (mv_block->pos_y & 15) >> 2);
+    spec_ent *tab = spec_table(p_Vid, list, ref), *e, want;
+    memset(&want, 0, sizeof want);
+    want.cx = mv.mv_x; want.cy = mv.mv_y; want.px = pred.mv_x; want.py = pred.mv_y;
+    want.sr = (int16_t)search_range; want.chk = (int16_t)check_for_00; want.lambda = lambda_factor;
+    if (s < 0 || mb < 0 || mb >= g_n_mb) error("jm_gpu_me: block outside the picture", 500);
+    e = &tab[(size_t)mb * JMME_NSLOT + s];
+    if (!(e->valid && e->cx == want.cx && e->cy == want.cy && e->px == want.px && e->py == want.py &&
+          e->sr == want.sr && e->chk == want.chk && e->lambda == want.lambda)) {
+      if (mb < g_spec_end[list][ref]) g_batch = imax(1, g_batch / 2);       /* a guess failed */
+      else g_batch = imin(2048, g_batch * 2);                              /* ran past the batch */
+      spec_batch(list, ref, mb, &want, chk_rule);
+    } else {
+      ++g_hits;
+    }
+    cost = e->cost;
+    if (cost >= min_mcost) return min_mcost;
+    mv_block->mv[list].mv_x = e->mvx;
+    mv_block->mv[list].mv_y = e->mvy;
+    return cost;
+  }
+  cost = jmme_full_search_block(g_me, list, ref, mv_block->pos_x, mv_block->pos_y, mv_block->blocktype, &pred, &mv,
+                                min_mcost, lambda_factor, search_range, check_for_00);
+  mv_block->mv[list].mv_x = mv.mv_x;                                     /* best out */
+  mv_block->mv[list].mv_y = mv.mv_y;
+  return cost;
+}
+
+/* setup_fast_full_search without the CPU SAD surface: the search centre of
+ * me_fullfast.c:312-327 (predictor of the 16x16 block, rounded, clipped so
+ * that (0,0) stays inside when RDO is off, then to the level's MV range) */
+void __wrap_setup_fast_full_search(Macroblock *currMB, MEBlock *mv_block, int list)
+{
+  VideoParameters *p_Vid = currMB->p_Vid;
+  InputParameters *p_Inp = currMB->p_Inp;
+  MEFullFast *ff = p_Vid->p_ffast_me;
+  short ref = mv_block->ref_idx;
+  int search_range = ff->max_search_range[list][ref] << 2;
+  PixelPos block[4];
+  MotionVector pmv, *c = &ff->search_center[list][ref];
+  get_neighbors(currMB, block, 0, 0, 16);
+  currMB->GetMVPredictor(currMB, block, &pmv, ref, p_Vid->enc_picture->mv_info, list, 0, 0, 16, 16);
+  c->mv_x = (short)(((pmv.mv_x + 2) >> 2) * 4);              /* JM_INT_DIVIDE (defines.h:44) */
+  c->mv_y = (short)(((pmv.mv_y + 2) >> 2) * 4);
+  if (!p_Inp->rdopt) {
+    c->mv_x = (short)iClip3(-search_range, search_range, c->mv_x);
+    c->mv_y = (short)iClip3(-search_range, search_range, c->mv_y);
+  }
+  c->mv_x = (short)iClip3(p_Vid->MaxHmvR[4] + search_range, p_Vid->MaxHmvR[5] - search_range, c->mv_x);
+  c->mv_y = (short)iClip3(p_Vid->MaxVmvR[4] + search_range, p_Vid->MaxVmvR[5] - search_range, c->mv_y);
+  ff->search_setup_done[list][ref] = 1;
+}
+
+/* fast_full_search_motion_estimation's contract (me_fullfast.c:618-689) */
+distblk __wrap_fast_full_search_motion_estimation(Macroblock *currMB, MotionVector *pred_mv, MEBlock *mv_block,
+                                                  distblk min_mcost, int lambda_factor)
+{
+  VideoParameters *p_Vid = currMB->p_Vid;
+  MEFullFast *ff = p_Vid->p_ffast_me;
+  int list = mv_block->list, ref = mv_block->ref_idx;
+  jmme_mv pred = {pred_mv->mv_x, pred_mv->mv_y}, centre, mv;
+  distblk cost;
+  if (!ff->search_setup_done[list][ref]) currMB->p_SetupFastFullPelSearch(currMB, mv_block, list);
+  centre.mv_x = ff->search_center[list][ref].mv_x;
+  centre.mv_y = ff->search_center[list][ref].mv_y;
+  ensure_planes(currMB, list, ref);
+  cost = jmme_fast_full_search_block(g_me, list, ref, mv_block->pos_x, mv_block->pos_y, mv_block->blocktype, &pred,
+                                     &centre, ff->max_search_range[list][ref],
+                                     imax(mv_block->searchRange.max_x, mv_block->searchRange.max_y) >> 2,
+                                     currMB->p_Inp->rdopt, &mv, min_mcost, lambda_factor);
+  mv_block->mv[list].mv_x = mv.mv_x;
+  mv_block->mv[list].mv_y = mv.mv_y;
+  ++g_calls;
+  return cost;
+}
+
+/* reported at exit, so a run shows the searches really went to the GPU */
+static void report(void) __attribute__((destructor));
+static void report(void)
+{
+  if (g_me) {
+    fprintf(stderr, "jm_gpu_me: %lld integer-pel searches on the GPU (libjmme): %lld from %lld speculative "
+                    "batches, the rest one call each\n", g_calls, g_hits + g_batches, g_batches);
+    jmme_destroy(g_me);
+  }
+}

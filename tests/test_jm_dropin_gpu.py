@@ -1,0 +1,75 @@
+"""GPU: the drop-in itself.  JM 18.5 lencod with its integer-pel motion search
+redirected to libjmme (integration/_build/lencod_jmme: JM's own objects +
+integration/jm_gpu_me.c, JM sources untouched) encodes the same input as the
+stock lencod (oracle/_ref/lencod, CPU) with the same configuration: the
+bitstreams and reconstructions must be byte-identical, for full search and fast
+full search, with RDO on and off and several reference frames.  The stock
+encoder is the oracle here; both binaries are built in this container
+(`make -C integration`)."""
+import hashlib
+import os
+import subprocess
+import tempfile
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+STOCK = os.path.join(REPO, "oracle", "_ref", "lencod")
+GPU = os.path.join(REPO, "integration", "_build", "lencod_jmme")
+
+CFG = """# minimal JM 18.5 configuration (unlisted keys: JM defaults)
+ProfileIDC            = 66
+LevelIDC              = 40
+IntraPeriod           = 0
+QPISlice              = 28
+QPPSlice              = 28
+DisableSubpelME       = 1
+EPZSSubPelGrid        = 0
+MDDistortion          = 0
+LeakyBucketParamFile  = "leakybucketparam.cfg"
+"""
+
+
+def _md5(p):
+    return hashlib.md5(open(p, "rb").read()).hexdigest()
+
+
+def _encode(binary, d, tag, yuv, w, h, frames, params, env=None):
+    cfg = os.path.join(d, "enc.cfg")
+    open(cfg, "w").write(CFG)
+    out, rec = os.path.join(d, f"{tag}.264"), os.path.join(d, f"{tag}_rec.yuv")
+    args = [binary, "-d", cfg, "-p", f"InputFile={yuv}", "-p", f"SourceWidth={w}", "-p", f"SourceHeight={h}",
+            "-p", f"OutputWidth={w}", "-p", f"OutputHeight={h}", "-p", f"FramesToBeEncoded={frames}",
+            "-p", f"OutputFile={out}", "-p", f"ReconFile={rec}"]
+    for k, v in params.items():
+        args += ["-p", f"{k}={v}"]
+    r = subprocess.run(args, cwd=d, capture_output=True, text=True, timeout=600,
+                       env=dict(os.environ, **(env or {})))
+    assert r.returncode == 0, (tag, r.stdout[-1500:], r.stderr[-1500:])
+    return _md5(out), _md5(rec), r
+
+
+@pytest.mark.parametrize("speculate", ["1", "0"])
+@pytest.mark.parametrize("w,h,frames,params", [
+    (176, 144, 3, {"SearchMode": -1, "SearchRange": 16, "RDOptimization": 0, "NumberReferenceFrames": 1}),
+    (176, 144, 3, {"SearchMode": -1, "SearchRange": 16, "RDOptimization": 1, "NumberReferenceFrames": 1}),
+    (176, 144, 4, {"SearchMode": 0, "SearchRange": 16, "RDOptimization": 0, "NumberReferenceFrames": 2}),
+    (176, 144, 3, {"SearchMode": 0, "SearchRange": 32, "RDOptimization": 1, "NumberReferenceFrames": 1}),
+    (352, 288, 4, {"SearchMode": -1, "SearchRange": 32, "RDOptimization": 0, "NumberReferenceFrames": 3,
+                   "RestrictSearchRange": 0}),
+])
+def test_lencod_with_gpu_me_is_byte_identical(gpu, w, h, frames, params, speculate):
+    """speculate=1: full-search calls answered from speculative batches (jm_gpu_me.c);
+    speculate=0: every IntPelME call goes to the GPU on its own"""
+    if not (os.path.exists(STOCK) and os.path.exists(GPU)):
+        pytest.fail("lencod builds missing: run `make -C oracle ref && make -C integration` in the build container")
+    from jmme import synth
+    with tempfile.TemporaryDirectory() as d:
+        yuv = os.path.join(d, "in.yuv")
+        synth.write_yuv420(yuv, synth.luma_sequence(w, h, frames, seed=w + frames, gmv=(3, -2)))
+        ref264, refrec, _ = _encode(STOCK, d, "cpu", yuv, w, h, frames, params)
+        gpu264, gpurec, r = _encode(GPU, d, "gpu", yuv, w, h, frames, params, {"JMME_SPECULATE": speculate})
+        assert "searches on the GPU" in r.stderr and " 0 integer-pel" not in r.stderr, r.stderr[-500:]
+        assert (gpu264, gpurec) == (ref264, refrec)
