@@ -107,10 +107,13 @@ static void ensure_planes(Macroblock *currMB, int list, int ref)
  * predictor, lambda, range, check_for_00) on the uploaded planes -- so the
  * encoder's output is unchanged; a miss re-batches from the missing
  * macroblock.  The batch length adapts: it doubles when the cache ran out
- * and halves when a guess failed.  JMME_SPECULATE=0 sends every call on its
- * own (jmme_full_search_block). */
+ * and halves when a guess failed.  Fast full search is batched the same way
+ * (its key adds the macroblock's surface centre and range).  JMME_SPECULATE=0
+ * sends every call on its own (jmme_full_search_block /
+ * jmme_fast_full_search_block). */
 typedef struct spec_ent {
-  int16_t cx, cy, px, py, sr, chk;
+  int16_t cx, cy, px, py, sr, chk;       /* FS: centre, predictor, range, check_for_00 */
+  int16_t fcx, fcy, frange, mode;        /* FFS: search_center, surface range; mode 0 FS, 1 FFS */
   int32_t lambda;
   int16_t mvx, mvy;
   int64_t cost;
@@ -146,7 +149,15 @@ static spec_ent *spec_table(VideoParameters *p_Vid, int list, int ref)
   return g_spec[list][ref];
 }
 
-static void spec_batch(int list, int ref, int mb0, const spec_ent *guess, int chk00_slot0)
+static int spec_same(const spec_ent *e, const spec_ent *w)
+{
+  return e->valid && e->mode == w->mode && e->cx == w->cx && e->cy == w->cy && e->px == w->px && e->py == w->py &&
+         e->sr == w->sr && e->chk == w->chk && e->fcx == w->fcx && e->fcy == w->fcy && e->frange == w->frange &&
+         e->lambda == w->lambda;
+}
+
+/* one batched search of all 41 partitions of macroblocks mb0.. with the guessed inputs */
+static void spec_batch(int list, int ref, int mb0, const spec_ent *guess, int chk00_slot0, int rdopt)
 {
   spec_ent *tab = g_spec[list][ref];
   int n = imin(g_batch, g_n_mb - mb0), i, s;
@@ -167,6 +178,12 @@ static void spec_batch(int list, int ref, int mb0, const spec_ent *guess, int ch
     r->list = (int16_t)list;
     r->ref_idx = (int16_t)ref;
     r->slot_mask = (1ull << JMME_NSLOT) - 1;
+    if (guess->mode) {                   /* FFS: the MB's surface (setup_fast_full_search) */
+      r->ffs_center_x = guess->fcx;
+      r->ffs_center_y = guess->fcy;
+      r->ffs_range = guess->frange;
+      r->ffs_pos00_valid = (int16_t)(rdopt == 0);
+    }
     for (s = 0; s < JMME_NSLOT; s++) {
       jmme_block_req *b = &r->blk[s];
       b->pred_x = guess->px;
@@ -174,16 +191,17 @@ static void spec_batch(int list, int ref, int mb0, const spec_ent *guess, int ch
       b->center_x = guess->cx;
       b->center_y = guess->cy;
       b->search_range = guess->sr;
-      b->flags = (int16_t)((s == 0 && chk00_slot0) ? JMME_BLK_CHECK00 : 0);
+      b->flags = (int16_t)((!guess->mode && s == 0 && chk00_slot0) ? JMME_BLK_CHECK00 : 0);
       b->lambda = guess->lambda;
     }
   }
-  if (jmme_search_mbs(g_me, JMME_FULL_SEARCH, g_req, n, g_res)) fail_jm("jmme_search_mbs");
+  if (jmme_search_mbs(g_me, guess->mode ? JMME_FAST_FULL_SEARCH : JMME_FULL_SEARCH, g_req, n, g_res))
+    fail_jm("jmme_search_mbs");
   for (i = 0; i < n; i++)
     for (s = 0; s < JMME_NSLOT; s++) {
       spec_ent *e = &tab[(size_t)(mb0 + i) * JMME_NSLOT + s];
       *e = *guess;
-      e->chk = (int16_t)(s == 0 && chk00_slot0);
+      e->chk = (int16_t)(!guess->mode && s == 0 && chk00_slot0);
       e->mvx = g_res[i * JMME_NSLOT + s].mv_x;
       e->mvy = g_res[i * JMME_NSLOT + s].mv_y;
       e->cost = g_res[i * JMME_NSLOT + s].cost;
@@ -191,6 +209,35 @@ static void spec_batch(int list, int ref, int mb0, const spec_ent *guess, int ch
     }
   g_spec_end[list][ref] = mb0 + n;
   ++g_batches;
+}
+
+static int speculating(void)
+{
+  if (g_speculate < 0) {
+    const char *e = getenv("JMME_SPECULATE");
+    g_speculate = !(e && e[0] == '0');
+  }
+  return g_speculate;
+}
+
+/* the cached answer for this call, batching on a miss */
+static const spec_ent *spec_lookup(Macroblock *currMB, MEBlock *mv_block, int list, int ref, const spec_ent *want,
+                                   int chk_rule)
+{
+  VideoParameters *p_Vid = currMB->p_Vid;
+  int mb = (mv_block->pos_y >> 4) * (p_Vid->width / 16) + (mv_block->pos_x >> 4);
+  int s = jmme_slot(mv_block->blocktype, (mv_block->pos_x & 15) >> 2, (mv_block->pos_y & 15) >> 2);
+  spec_ent *tab = spec_table(p_Vid, list, ref), *e;
+  if (s < 0 || mb < 0 || mb >= g_n_mb) error("jm_gpu_me: block outside the picture", 500);
+  e = &tab[(size_t)mb * JMME_NSLOT + s];
+  if (!spec_same(e, want)) {
+    if (mb < g_spec_end[list][ref]) g_batch = imax(1, g_batch / 2);       /* a guess failed */
+    else g_batch = imin(2048, g_batch * 2);                              /* ran past the batch */
+    spec_batch(list, ref, mb, want, chk_rule, currMB->p_Inp->rdopt);
+  } else {
+    ++g_hits;
+  }
+  return e;
 }
 
 /* full_search_motion_estimation's contract (me_fullsearch.c:39-103) */
@@ -209,28 +256,13 @@ distblk __wrap_full_search_motion_estimation(Macroblock *currMB, MotionVector *p
   distblk cost;
   ensure_planes(currMB, list, ref);
   ++g_calls;
-  if (g_speculate < 0) {
-    const char *e = getenv("JMME_SPECULATE");
-    g_speculate = !(e && e[0] == '0');
-  }
-  if (g_speculate) {
-    int mb_x = mv_block->pos_x >> 4, mb_y = mv_block->pos_y >> 4;
-    int mb = mb_y * (p_Vid->width / 16) + mb_x;
-    int s = jmme_slot(mv_block->blocktype, (mv_block->pos_x & 15) >> 2, (mv_block->pos_y & 15) >> 2);
-    spec_ent *tab = spec_table(p_Vid, list, ref), *e, want;
+  if (speculating()) {
+    spec_ent want;
+    const spec_ent *e;
     memset(&want, 0, sizeof want);
     want.cx = mv.mv_x; want.cy = mv.mv_y; want.px = pred.mv_x; want.py = pred.mv_y;
     want.sr = (int16_t)search_range; want.chk = (int16_t)check_for_00; want.lambda = lambda_factor;
-    if (s < 0 || mb < 0 || mb >= g_n_mb) error("jm_gpu_me: block outside the picture", 500);
-    e = &tab[(size_t)mb * JMME_NSLOT + s];
-    if (!(e->valid && e->cx == want.cx && e->cy == want.cy && e->px == want.px && e->py == want.py &&
-          e->sr == want.sr && e->chk == want.chk && e->lambda == want.lambda)) {
-      if (mb < g_spec_end[list][ref]) g_batch = imax(1, g_batch / 2);       /* a guess failed */
-      else g_batch = imin(2048, g_batch * 2);                              /* ran past the batch */
-      spec_batch(list, ref, mb, &want, chk_rule);
-    } else {
-      ++g_hits;
-    }
+    e = spec_lookup(currMB, mv_block, list, ref, &want, chk_rule);
     cost = e->cost;
     if (cost >= min_mcost) return min_mcost;
     mv_block->mv[list].mv_x = e->mvx;
@@ -282,13 +314,34 @@ distblk __wrap_fast_full_search_motion_estimation(Macroblock *currMB, MotionVect
   centre.mv_x = ff->search_center[list][ref].mv_x;
   centre.mv_y = ff->search_center[list][ref].mv_y;
   ensure_planes(currMB, list, ref);
+  ++g_calls;
+  if (speculating()) {
+    spec_ent want;
+    const spec_ent *e;
+    memset(&want, 0, sizeof want);
+    want.mode = 1;
+    want.px = pred.mv_x; want.py = pred.mv_y;
+    want.sr = (int16_t)(imax(mv_block->searchRange.max_x, mv_block->searchRange.max_y) >> 2);
+    want.fcx = centre.mv_x; want.fcy = centre.mv_y;
+    want.frange = (int16_t)ff->max_search_range[list][ref];
+    want.lambda = lambda_factor;
+    e = spec_lookup(currMB, mv_block, list, ref, &want, 0);
+    cost = e->cost;
+    if (cost >= min_mcost) {                /* nothing beat the bound: JM keeps the centre */
+      mv_block->mv[list].mv_x = centre.mv_x;
+      mv_block->mv[list].mv_y = centre.mv_y;
+      return min_mcost;
+    }
+    mv_block->mv[list].mv_x = e->mvx;
+    mv_block->mv[list].mv_y = e->mvy;
+    return cost;
+  }
   cost = jmme_fast_full_search_block(g_me, list, ref, mv_block->pos_x, mv_block->pos_y, mv_block->blocktype, &pred,
                                      &centre, ff->max_search_range[list][ref],
                                      imax(mv_block->searchRange.max_x, mv_block->searchRange.max_y) >> 2,
                                      currMB->p_Inp->rdopt, &mv, min_mcost, lambda_factor);
   mv_block->mv[list].mv_x = mv.mv_x;
   mv_block->mv[list].mv_y = mv.mv_y;
-  ++g_calls;
   return cost;
 }
 
