@@ -15,6 +15,9 @@
  *       p_Vid->p_SetupFastFullPelSearch (global.h:469, mv_search.c:172): here it
  *       only derives the search centre (me_fullfast.c:312-327) -- the SAD
  *       surface JM would build on the CPU is the GPU's job
+ *   sub_pel_motion_estimation           JM/lencod/src/me_fullsearch.c:186-289
+ *       currMB->SubPelME for FS / FFS (called mv_search.c:966-976): half- and
+ *       quarter-pel refinement on the GPU's quarter-pel planes
  *
  * Frame buffers: p_Vid->pCurImg (image.c:2868) and the reference pictures'
  * imgY (StorablePicture, mbuffer.c:2116-2122) are uploaded once per coded
@@ -27,9 +30,12 @@
 
 #include "global.h"
 #include "mbuffer.h"
+#include "me_distortion.h"
 #include "me_fullfast.h"
 #include "mv_search.h"
 #include "jmme.h"
+
+extern distblk __real_sub_pel_motion_estimation(Macroblock *, MotionVector *, MEBlock *, distblk, int *);
 
 extern void get_neighbors(Macroblock *currMB, PixelPos *block, int mb_x, int mb_y, int blockshape_x);
 
@@ -345,6 +351,175 @@ distblk __wrap_fast_full_search_motion_estimation(Macroblock *currMB, MotionVect
   return cost;
 }
 
+/* ---- sub-pel refinement (SubPelME) ------------------------------------------
+ * Speculated like the integer search: a sub-pel batch covers the macroblocks
+ * whose integer results are cached, each slot guessed with that slot's cached
+ * integer vector / cost and predictor and this call's lambdas, metrics and
+ * switches; a call uses a cached answer only when every input matches. */
+typedef struct sp_ent {
+  int16_t px, py, mx, my;
+  int64_t min_mcost;
+  int32_t lam_h, lam_q;
+  uint8_t metric_h, metric_q, start_hp, start_qp, pos2, pos4, flags, valid;
+  int16_t omx, omy;
+  int64_t cost;
+} sp_ent;
+
+static sp_ent *g_sp[2][32];
+static int g_sp_frame[2][32];
+static long long g_sp_calls = 0, g_sp_hits = 0, g_sp_batches = 0, g_sp_cpu = 0;
+static jmme_subpel_req *g_sreq = NULL;
+static jmme_block_res *g_sres = NULL;
+static int g_sreq_cap = 0;
+static int8_t g_slot_bt[JMME_NSLOT], g_slot_bx[JMME_NSLOT], g_slot_by[JMME_NSLOT];
+
+static int metric_id(distblk (*f)(StorablePicture *, MEBlock *, distblk, MotionVector *))
+{
+  if (f == computeSAD) return 0;
+  if (f == computeSSE) return 1;
+  if (f == computeSATD) return 2;
+  return -1;                                  /* weighted / on-the-fly: stays on the CPU */
+}
+
+static int sp_same(const sp_ent *e, const sp_ent *w)
+{
+  return e->valid && e->px == w->px && e->py == w->py && e->mx == w->mx && e->my == w->my &&
+         e->min_mcost == w->min_mcost && e->lam_h == w->lam_h && e->lam_q == w->lam_q &&
+         e->metric_h == w->metric_h && e->metric_q == w->metric_q && e->start_hp == w->start_hp &&
+         e->start_qp == w->start_qp && e->pos2 == w->pos2 && e->pos4 == w->pos4 && e->flags == w->flags;
+}
+
+static void slot_geometry(void)
+{
+  static const int bw[8] = {0, 16, 16, 8, 8, 8, 4, 4}, bh[8] = {0, 16, 8, 16, 8, 4, 8, 4};
+  int bt, x, y, sl;
+  for (bt = 1; bt <= 7; bt++)
+    for (y = 0; y < 16; y += bh[bt])
+      for (x = 0; x < 16; x += bw[bt]) {
+        sl = jmme_slot(bt, x >> 2, y >> 2);
+        if (sl >= 0) { g_slot_bt[sl] = (int8_t)bt; g_slot_bx[sl] = (int8_t)x; g_slot_by[sl] = (int8_t)y; }
+      }
+}
+
+static void sp_batch(int list, int ref, int mb0, int s0, const sp_ent *w, int t8)
+{
+  const spec_ent *itab = g_spec[list][ref];
+  sp_ent *tab = g_sp[list][ref];
+  int mb1 = imax(g_spec_end[list][ref], mb0 + 1), n = 0, i, s, mb;
+  int count = (mb1 - mb0) * JMME_NSLOT;
+  if (!g_slot_bt[0]) slot_geometry();
+  if (count > g_sreq_cap) {
+    free(g_sreq);
+    free(g_sres);
+    g_sreq = (jmme_subpel_req *)malloc((size_t)count * sizeof(jmme_subpel_req));
+    g_sres = (jmme_block_res *)malloc((size_t)count * sizeof(jmme_block_res));
+    if (!g_sreq || !g_sres) error("jm_gpu_me: out of memory", 500);
+    g_sreq_cap = count;
+  }
+  memset(g_sreq, 0, (size_t)count * sizeof(jmme_subpel_req));
+  for (mb = mb0; mb < mb1; mb++)
+    for (s = 0; s < JMME_NSLOT; s++, n++) {
+      const spec_ent *ie = itab ? &itab[(size_t)mb * JMME_NSLOT + s] : NULL;
+      jmme_subpel_req *q = &g_sreq[n];
+      int bt = g_slot_bt[s];
+      /* the calling block gets its real inputs, the others their cached integer result */
+      int here = (mb == mb0 && s == s0);
+      if (!here && (!ie || !ie->valid)) continue;      /* blocktype 0: skipped */
+      q->pos_x = (int16_t)((mb % g_mbs_x) * 16 + g_slot_bx[s]);
+      q->pos_y = (int16_t)((mb / g_mbs_x) * 16 + g_slot_by[s]);
+      q->blocktype = (int16_t)bt;
+      q->ref_slot = (int16_t)(list * 32 + ref);
+      q->pred_x = here ? w->px : ie->px;
+      q->pred_y = here ? w->py : ie->py;
+      q->mv_x = here ? w->mx : ie->mvx;
+      q->mv_y = here ? w->my : ie->mvy;
+      q->lambda_h = w->lam_h;
+      q->lambda_q = w->lam_q;
+      q->min_mcost = here ? w->min_mcost : w->start_hp ? ie->cost : JMME_DISTBLK_MAX;
+      q->variant = 0;
+      /* test8x8 as mv_search.c:1630,1770 set it: Transform8x8Mode on block types 1..4 */
+      q->flags = here ? w->flags : (uint8_t)((w->flags & JMME_SP_CHECK0) | (t8 && bt <= 4 ? JMME_SP_TEST8x8 : 0));
+      q->metric_h = w->metric_h;
+      q->metric_q = w->metric_q;
+      q->start_hp = w->start_hp;
+      q->start_qp = w->start_qp;
+      q->search_pos2 = w->pos2;
+      q->search_pos4 = w->pos4;
+    }
+  if (jmme_subpel_refine(g_me, g_sreq, n, g_sres)) fail_jm("jmme_subpel_refine");
+  for (i = 0; i < n; i++) {
+    const jmme_subpel_req *q = &g_sreq[i];
+    sp_ent *e;
+    if (!q->blocktype) continue;
+    e = &tab[(size_t)(mb0 + i / JMME_NSLOT) * JMME_NSLOT + i % JMME_NSLOT];
+    e->px = q->pred_x; e->py = q->pred_y; e->mx = q->mv_x; e->my = q->mv_y;
+    e->min_mcost = q->min_mcost; e->lam_h = q->lambda_h; e->lam_q = q->lambda_q;
+    e->metric_h = q->metric_h; e->metric_q = q->metric_q; e->start_hp = q->start_hp; e->start_qp = q->start_qp;
+    e->pos2 = q->search_pos2; e->pos4 = q->search_pos4; e->flags = q->flags;
+    e->omx = g_sres[i].mv_x; e->omy = g_sres[i].mv_y; e->cost = g_sres[i].cost;
+    e->valid = 1;
+  }
+  ++g_sp_batches;
+}
+
+/* sub_pel_motion_estimation's contract (me_fullsearch.c:186-289) */
+distblk __wrap_sub_pel_motion_estimation(Macroblock *currMB, MotionVector *pred_mv, MEBlock *mv_block,
+                                         distblk min_mcost, int *lambda_factor)
+{
+  VideoParameters *p_Vid = currMB->p_Vid;
+  Slice *currSlice = currMB->p_Slice;
+  int list = mv_block->list, ref = mv_block->ref_idx;
+  int mh = metric_id(mv_block->computePredHPel), mq = metric_id(mv_block->computePredQPel);
+  int mb, s, i;
+  sp_ent want, *e, *tab;
+  ++g_sp_calls;
+  int mode = currMB->p_Inp->SearchMode[p_Vid->view_id];
+  /* GPU sub-pel follows a GPU integer search (FS / FFS); UMHEX's direct calls and
+   * weighted / chroma metrics stay on the CPU */
+  if (!speculating() || (mode != FULL_SEARCH && mode != FAST_FULL_SEARCH) || mh < 0 || mq < 0 ||
+      mv_block->ChromaMEEnable || mv_block->search_pos2 > 9 || mv_block->search_pos4 > 9 ||
+      (mv_block->test8x8 && mv_block->blocktype > 4)) {
+    ++g_sp_cpu;
+    return __real_sub_pel_motion_estimation(currMB, pred_mv, mv_block, min_mcost, lambda_factor);
+  }
+  ensure_planes(currMB, list, ref);
+  memset(&want, 0, sizeof want);
+  want.px = pred_mv->mv_x; want.py = pred_mv->mv_y;
+  want.mx = mv_block->mv[list].mv_x; want.my = mv_block->mv[list].mv_y;
+  want.min_mcost = (int64_t)min_mcost;
+  want.lam_h = lambda_factor[H_PEL]; want.lam_q = lambda_factor[Q_PEL];
+  want.metric_h = (uint8_t)mh; want.metric_q = (uint8_t)mq;
+  want.start_hp = (uint8_t)(p_Vid->start_me_refinement_hp != 0);
+  want.start_qp = (uint8_t)(p_Vid->start_me_refinement_qp != 0);
+  want.pos2 = (uint8_t)mv_block->search_pos2; want.pos4 = (uint8_t)mv_block->search_pos4;
+  want.flags = (uint8_t)((mv_block->test8x8 ? JMME_SP_TEST8x8 : 0) |
+                         ((!currMB->p_Inp->rdopt && currSlice->slice_type != B_SLICE) ? JMME_SP_CHECK0 : 0));
+  spec_table(p_Vid, list, ref);                       /* sizes and per-picture reset of the integer table */
+  if (!g_sp[list][ref]) {
+    g_sp[list][ref] = (sp_ent *)calloc((size_t)g_n_mb * JMME_NSLOT, sizeof(sp_ent));
+    if (!g_sp[list][ref]) error("jm_gpu_me: out of memory", 500);
+    g_sp_frame[list][ref] = -1000000;
+  }
+  tab = g_sp[list][ref];
+  if (g_sp_frame[list][ref] != p_Vid->frame_no) {
+    for (i = 0; i < g_n_mb * JMME_NSLOT; i++) tab[i].valid = 0;
+    g_sp_frame[list][ref] = p_Vid->frame_no;
+  }
+  mb = (mv_block->pos_y >> 4) * g_mbs_x + (mv_block->pos_x >> 4);
+  s = jmme_slot(mv_block->blocktype, (mv_block->pos_x & 15) >> 2, (mv_block->pos_y & 15) >> 2);
+  if (s < 0 || mb < 0 || mb >= g_n_mb) error("jm_gpu_me: block outside the picture", 500);
+  e = &tab[(size_t)mb * JMME_NSLOT + s];
+  if (!sp_same(e, &want)) {
+    sp_batch(list, ref, mb, s, &want, currMB->p_Inp->Transform8x8Mode != 0);
+    if (!sp_same(e, &want)) error("jm_gpu_me: sub-pel batch lost its own request", 500);
+  } else {
+    ++g_sp_hits;
+  }
+  mv_block->mv[list].mv_x = e->omx;
+  mv_block->mv[list].mv_y = e->omy;
+  return (distblk)e->cost;
+}
+
 /* reported at exit, so a run shows the searches really went to the GPU */
 static void report(void) __attribute__((destructor));
 static void report(void)
@@ -352,6 +527,8 @@ static void report(void)
   if (g_me) {
     fprintf(stderr, "jm_gpu_me: %lld integer-pel searches on the GPU (libjmme): %lld from %lld speculative "
                     "batches, the rest one call each\n", g_calls, g_hits + g_batches, g_batches);
+    fprintf(stderr, "jm_gpu_me: %lld sub-pel refinements: %lld cached, %lld batches, %lld on the CPU\n",
+            g_sp_calls, g_sp_hits, g_sp_batches, g_sp_cpu);
     jmme_destroy(g_me);
   }
 }

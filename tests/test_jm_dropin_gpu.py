@@ -3,11 +3,13 @@ redirected to libjmme (integration/_build/lencod_jmme: JM's own objects +
 integration/jm_gpu_me.c, JM sources untouched) encodes the same input as the
 stock lencod (oracle/_ref/lencod, CPU) with the same configuration: the
 bitstreams and reconstructions must be byte-identical, for full search and fast
-full search, with RDO on and off and several reference frames.  The stock
+full search, with RDO on and off, several reference frames, and sub-pel
+refinement (SubPelME) off and on (SAD/SSE/SATD, 8x8-transform SATD).  The stock
 encoder is the oracle here; both binaries are built in this container
 (`make -C integration`)."""
 import hashlib
 import os
+import re
 import subprocess
 import tempfile
 
@@ -59,6 +61,16 @@ def _encode(binary, d, tag, yuv, w, h, frames, params, env=None):
     (176, 144, 3, {"SearchMode": 0, "SearchRange": 32, "RDOptimization": 1, "NumberReferenceFrames": 1}),
     (352, 288, 4, {"SearchMode": -1, "SearchRange": 32, "RDOptimization": 0, "NumberReferenceFrames": 3,
                    "RestrictSearchRange": 0}),
+    # sub-pel refinement on (JM's default): SubPelME on the GPU too (JM wants the
+    # quarter-pel metric to be the mode-decision one)
+    (176, 144, 3, {"SearchMode": -1, "SearchRange": 16, "RDOptimization": 0, "NumberReferenceFrames": 1,
+                   "DisableSubpelME": 0, "MEDistortionQPel": 0}),
+    (176, 144, 4, {"SearchMode": 0, "SearchRange": 16, "RDOptimization": 1, "NumberReferenceFrames": 2,
+                   "DisableSubpelME": 0, "MEDistortionHPel": 2, "MEDistortionQPel": 1, "MDDistortion": 1}),
+    (352, 288, 3, {"SearchMode": -1, "SearchRange": 32, "RDOptimization": 0, "NumberReferenceFrames": 2,
+                   "DisableSubpelME": 0, "ProfileIDC": 100, "Transform8x8Mode": 1, "MDDistortion": 2}),
+    (352, 288, 3, {"SearchMode": 0, "SearchRange": 32, "RDOptimization": 1, "NumberReferenceFrames": 1,
+                   "DisableSubpelME": 0, "ProfileIDC": 100, "Transform8x8Mode": 2, "MDDistortion": 2}),
 ])
 def test_lencod_with_gpu_me_is_byte_identical(gpu, w, h, frames, params, speculate):
     """speculate=1: full-search calls answered from speculative batches (jm_gpu_me.c);
@@ -73,3 +85,6 @@ def test_lencod_with_gpu_me_is_byte_identical(gpu, w, h, frames, params, specula
         gpu264, gpurec, r = _encode(GPU, d, "gpu", yuv, w, h, frames, params, {"JMME_SPECULATE": speculate})
         assert "searches on the GPU" in r.stderr and " 0 integer-pel" not in r.stderr, r.stderr[-500:]
         assert (gpu264, gpurec) == (ref264, refrec)
+        if params.get("DisableSubpelME") == 0 and speculate == "1":
+            m = re.search(r"(\d+) sub-pel refinements: (\d+) cached, (\d+) batches, (\d+) on the CPU", r.stderr)
+            assert m and int(m.group(1)) > 0 and int(m.group(4)) == 0, r.stderr[-500:]

@@ -5,7 +5,7 @@ JM objects, integer-pel ME through libjmme on the GPU, one IntPelME call per
 partition exactly as JM issues them) encode the same synthetic clip with the
 same configuration; reports both wall times, JM's own "Total ME time", and
 whether the bitstreams / reconstructions are byte-identical.
-Usage (GPU box): python3 tools/bench_dropin.py [--size 1920x1080] [--frames 2] [--mode -1]"""
+Usage (GPU box): python3 tools/bench_dropin.py [--size 1920x1080] [--frames 2] [--mode -1] [--subpel]"""
 import argparse
 import hashlib
 import json
@@ -39,7 +39,9 @@ def run(binary, d, tag, yuv, w, h, frames, params, env=None):
     me = re.search(r"Total ME time for sequence\s*:\s*([0-9.]+) sec", r.stdout)
     calls = re.search(r"jm_gpu_me: (\d+) integer-pel searches on the GPU \(libjmme\): (\d+) from (\d+) speculative",
                       r.stderr)
+    sp = re.search(r"(\d+) sub-pel refinements: (\d+) cached, (\d+) batches, (\d+) on the CPU", r.stderr)
     return dict(wall_s=round(wall, 3), me_s=float(me.group(1)) if me else None,
+                subpel=dict(zip(("calls", "cached", "batches", "cpu"), map(int, sp.groups()))) if sp else None,
                 gpu_searches=int(calls.group(1)) if calls else None,
                 from_speculative_batches=int(calls.group(2)) if calls else None,
                 batches=int(calls.group(3)) if calls else None,
@@ -52,11 +54,15 @@ def main():
     ap.add_argument("--frames", type=int, default=2)
     ap.add_argument("--mode", type=int, default=-1)
     ap.add_argument("--range", type=int, default=32)
+    ap.add_argument("--subpel", action="store_true",
+                    help="sub-pel refinement on (JM default), SATD quarter-pel = mode-decision metric")
     ap.add_argument("--per-call", action="store_true", help="also time JMME_SPECULATE=0 (one GPU call per search)")
     a = ap.parse_args()
     from jmme import synth
     w, h = (int(v) for v in a.size.split("x"))
     params = {"SearchMode": a.mode, "SearchRange": a.range, "RDOptimization": 0, "NumberReferenceFrames": 1}
+    if a.subpel:
+        params.update(DisableSubpelME=0, MEDistortionQPel=2, MDDistortion=2)
     with tempfile.TemporaryDirectory() as d:
         yuv = os.path.join(d, "in.yuv")
         synth.write_yuv420(yuv, synth.luma_sequence(w, h, a.frames, seed=2024, gmv=(5, 3)))
