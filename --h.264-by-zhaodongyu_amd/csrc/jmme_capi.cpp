@@ -76,6 +76,12 @@ struct jmme_ctx {
   bool sub_stale[kMaxLists * kMaxRefs] = {};
   const uint8_t **d_sub_table = nullptr;     // device copy of d_subs
   bool sub_table_dirty = true;
+  // synchronous calls: pinned host staging + a device scratch for sub-pel requests,
+  // kept across calls (one DMA each way and one stream sync per call)
+  uint8_t *h_pin = nullptr;
+  size_t cap_pin = 0;
+  uint8_t *d_sp = nullptr;
+  size_t cap_sp = 0;
 };
 
 // ----------------------------------------------------------------- config --
@@ -248,6 +254,8 @@ extern "C" void jmme_destroy(jmme_ctx *ctx) {
   (void)hipFree(ctx->d_pool);
   for (auto *p : ctx->d_subs) (void)hipFree(p);
   (void)hipFree(ctx->d_sub_table);
+  (void)hipFree(ctx->d_sp);
+  if (ctx->h_pin) (void)hipHostFree(ctx->h_pin);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
   delete ctx;
@@ -385,6 +393,37 @@ int launch(jmme_ctx *ctx, int mode, const uint8_t *d_cur, const uint8_t *const *
   return 0;
 }
 
+int ensure_pin(jmme_ctx *ctx, size_t bytes) {
+  if (bytes <= ctx->cap_pin) return 0;
+  if (ctx->h_pin) (void)hipHostFree(ctx->h_pin);
+  ctx->h_pin = nullptr;
+  ctx->cap_pin = 0;
+  size_t cap = bytes < (1u << 20) ? (1u << 20) : bytes + bytes / 2;
+  HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_pin), cap, hipHostMallocDefault));
+  ctx->cap_pin = cap;
+  return 0;
+}
+
+int ensure_sp(jmme_ctx *ctx, size_t bytes) {
+  if (bytes <= ctx->cap_sp) return 0;
+  (void)hipFree(ctx->d_sp);
+  ctx->d_sp = nullptr;
+  ctx->cap_sp = 0;
+  size_t cap = bytes < (1u << 20) ? (1u << 20) : bytes + bytes / 2;
+  HIPCHK(hipMalloc(&ctx->d_sp, cap));
+  ctx->cap_sp = cap;
+  return 0;
+}
+
+constexpr size_t align64(size_t v) { return (v + 63) & ~size_t(63); }
+
+int status_words(const unsigned *st, const jmme_ctx *ctx) {
+  if (st[2] & 4u) return fail("internal: the refine pass lost a winner");
+  if (st[2] & 1u) return fail("a request's search range exceeds the configured SearchRange %d", ctx->cfg.SearchRange);
+  if (st[2] & 2u) return fail("a full-search centre is not on the integer grid (EPZSSubPelGrid sub-pel centres are not supported)");
+  return 0;
+}
+
 int check_status(jmme_ctx *ctx) {
   unsigned st[3] = {0, 0, 0};
   HIPCHK(hipMemcpy(st, ctx->d_counts, sizeof st, hipMemcpyDeviceToHost));
@@ -437,15 +476,22 @@ extern "C" int jmme_search_mbs(jmme_ctx *ctx, int mode, const jmme_mb_req *req, 
   if (ensure_units(ctx, (size_t)n)) return -1;
   hipStream_t s = nullptr;
   if (sync_ref_table(ctx, s)) return -1;
-  HIPCHK(hipMemcpyAsync(ctx->d_req, req, (size_t)n * sizeof(jmme_mb_req), hipMemcpyHostToDevice, s));
+  // pinned staging: [requests | results | status words]
+  const size_t rq = align64((size_t)n * sizeof(jmme_mb_req)), rs = align64((size_t)n * JMME_NSLOT * sizeof(jmme_block_res));
+  if (ensure_pin(ctx, rq + rs + 64)) return -1;
+  std::memcpy(ctx->h_pin, req, (size_t)n * sizeof(jmme_mb_req));
+  HIPCHK(hipMemcpyAsync(ctx->d_req, ctx->h_pin, (size_t)n * sizeof(jmme_mb_req), hipMemcpyHostToDevice, s));
   if (launch(ctx, mode, ctx->d_cur, ctx->d_ref_table, ctx->pitch, ctx->width, ctx->height, ctx->d_req, n,
              ctx->d_out, s))
     return -1;
   // results for searched slots only: copy the whole block, then merge
-  std::vector<jmme_block_res> tmp((size_t)n * JMME_NSLOT);
-  HIPCHK(hipMemcpyAsync(tmp.data(), ctx->d_out, tmp.size() * sizeof(jmme_block_res), hipMemcpyDeviceToHost, s));
+  const jmme_block_res *tmp = reinterpret_cast<const jmme_block_res *>(ctx->h_pin + rq);
+  const unsigned *st = reinterpret_cast<const unsigned *>(ctx->h_pin + rq + rs);
+  HIPCHK(hipMemcpyAsync(ctx->h_pin + rq, ctx->d_out, (size_t)n * JMME_NSLOT * sizeof(jmme_block_res),
+                        hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(ctx->h_pin + rq + rs, ctx->d_counts, 3 * sizeof(unsigned), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
-  if (check_status(ctx)) return -1;
+  if (status_words(st, ctx)) return -1;
   for (int i = 0; i < n; ++i)
     for (int sl = 0; sl < JMME_NSLOT; ++sl)
       if ((req[i].slot_mask >> sl) & 1) out[(size_t)i * JMME_NSLOT + sl] = tmp[(size_t)i * JMME_NSLOT + sl];
@@ -1258,14 +1304,19 @@ extern "C" int jmme_subpel_refine(jmme_ctx *ctx, const jmme_subpel_req *req, int
   if (jmme_subpel_validate(ctx, req, n)) return -1;
   if (n == 0) return 0;
   if (!out) return fail("null output array");
-  DevBuf dq, dout;
-  HIPCHK(dq.alloc((size_t)n * sizeof(jmme_subpel_req)));
-  HIPCHK(dout.alloc((size_t)n * sizeof(jmme_block_res)));
-  HIPCHK(hipMemcpy(dq.p, req, (size_t)n * sizeof(jmme_subpel_req), hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(dout.p, out, (size_t)n * sizeof(jmme_block_res), hipMemcpyHostToDevice));
-  if (jmme_subpel_refine_async(ctx, (const jmme_subpel_req *)dq.p, n, nullptr, (jmme_block_res *)dout.p, nullptr))
+  // one H2D of [requests | entry outputs] (blocktype-0 entries keep theirs), one D2H, one sync
+  const size_t rq = align64((size_t)n * sizeof(jmme_subpel_req)), ro = (size_t)n * sizeof(jmme_block_res);
+  if (ensure_pin(ctx, rq + ro) || ensure_sp(ctx, rq + ro)) return -1;
+  std::memcpy(ctx->h_pin, req, (size_t)n * sizeof(jmme_subpel_req));
+  std::memcpy(ctx->h_pin + rq, out, ro);
+  hipStream_t s = nullptr;
+  HIPCHK(hipMemcpyAsync(ctx->d_sp, ctx->h_pin, rq + ro, hipMemcpyHostToDevice, s));
+  if (jmme_subpel_refine_async(ctx, reinterpret_cast<const jmme_subpel_req *>(ctx->d_sp), n, nullptr,
+                               reinterpret_cast<jmme_block_res *>(ctx->d_sp + rq), s))
     return -1;
-  HIPCHK(hipMemcpy(out, dout.p, (size_t)n * sizeof(jmme_block_res), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpyAsync(ctx->h_pin + rq, ctx->d_sp + rq, ro, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  std::memcpy(out, ctx->h_pin + rq, ro);
   return 0;
 }
 static_assert(sizeof(jmme_subpel_req) == 48, "sub-pel ABI layout");

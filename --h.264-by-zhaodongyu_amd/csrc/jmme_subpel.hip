@@ -356,14 +356,14 @@ __global__ __launch_bounds__(256) void subpel_kernel(SubpelParams p) {
   __shared__ WaveLds lds[kWaves];
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int i0 = __builtin_amdgcn_readfirstlane((blockIdx.x * kWaves + wv) * kK);
+  const int i0 = __builtin_amdgcn_readfirstlane((blockIdx.x * kWaves + wv) * p.per_wave);
   if (i0 >= p.n) return;
   WaveLds &L = lds[wv];
   const int i = i0 + lane;
   // owner lanes: lane k < 16 holds request i0 + k; inactive owners ask for nothing
   jmme_subpel_req q{};
   bool act = false;
-  if (lane < kK && i < p.n) {
+  if (lane < p.per_wave && i < p.n) {
     q = p.req[i];
     act = q.blocktype >= 1 && q.blocktype <= 7;
   }
@@ -536,8 +536,14 @@ hipError_t launch_sub_images(const uint8_t *src, int src_pitch, int w, int h, ui
 
 hipError_t launch_subpel(const SubpelParams &p, hipStream_t s) {
   if (p.n <= 0) return hipSuccess;
-  const int per_wg = kWaves * kK;
-  hipLaunchKernelGGL(subpel_kernel, dim3((p.n + per_wg - 1) / per_wg), dim3(256), 0, s, p);
+  // small batches (the drop-in's speculative ones) spread over more waves: the
+  // wave's passes over its (candidate, block) jobs are the latency, so with
+  // fewer owners per wave the chip finishes them sooner; full frames keep 16
+  SubpelParams q = p;
+  const int waves_wanted = 256 * 4 * 2;   // two waves per SIMD over 256 CUs
+  q.per_wave = std::min(kK, std::max(1, (p.n + waves_wanted - 1) / waves_wanted));
+  const int per_wg = kWaves * q.per_wave;
+  hipLaunchKernelGGL(subpel_kernel, dim3((p.n + per_wg - 1) / per_wg), dim3(256), 0, s, q);
   return hipGetLastError();
 }
 

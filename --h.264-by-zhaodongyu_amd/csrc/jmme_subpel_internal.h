@@ -35,6 +35,7 @@ struct SubpelParams {
   const jmme_block_res *int_res;       // optional integer-pel results aligned with req
   jmme_block_res *out;
   int n;
+  int per_wave;                        // refinements per wave (1..16), set by launch_subpel
 };
 
 hipError_t launch_subpel(const SubpelParams &p, hipStream_t s);

@@ -103,11 +103,12 @@ static void ensure_planes(Macroblock *currMB, int list, int ref)
 /* ---- speculative batching of full-search calls ----------------------------
  * JM issues IntPelME one partition at a time, each with the predictor its
  * neighbours' final vectors give, so the inputs of later searches are not known
- * in advance.  They are usually the same as the current one's (smooth motion:
+ * in advance.  They are usually close to ones already seen (smooth motion:
  * every partition of a macroblock, and the next macroblocks, get the same
- * predictor and centre), so on a miss the adapter searches, in ONE batched
- * call (jmme_search_mbs), all 41 partitions of the next `g_batch` macroblocks
- * with the current call's inputs as the guess, and caches (inputs -> result).
+ * predictor and centre, or the ones the same partition of a neighbour got), so
+ * on a miss the adapter searches, in ONE batched call (jmme_search_mbs), all 41
+ * partitions of the next `g_batch` macroblocks under up to KHYP distinct
+ * guesses (spec_hyp) and caches (inputs -> result) per guess.
  * A later call is answered from the cache only when its inputs are identical
  * to the guessed ones -- a search is a pure function of (block, centre,
  * predictor, lambda, range, check_for_00) on the uploaded planes -- so the
@@ -126,13 +127,17 @@ typedef struct spec_ent {
   int8_t valid;
 } spec_ent;
 
-static spec_ent *g_spec[2][32];
+#define KHYP 4                     /* guesses per (macroblock, partition) */
+static spec_ent *g_spec[2][32];    /* KHYP cached (inputs -> result) per (macroblock, slot) */
+static spec_ent *g_seen[2][32];    /* the inputs each (macroblock, slot) was really searched with */
 static int g_spec_frame[2][32];
 static int g_spec_end[2][32];      /* first macroblock past the last batch */
 static int g_batch = 64, g_speculate = -1, g_mbs_x = 0, g_n_mb = 0;
 static long long g_hits = 0, g_batches = 0;
 static jmme_mb_req *g_req = NULL;
 static jmme_block_res *g_res = NULL;
+static spec_ent *g_hyp = NULL;     /* the inputs behind each request's 41 slots */
+static int *g_req_mb = NULL;
 static int g_req_cap = 0;
 
 static spec_ent *spec_table(VideoParameters *p_Vid, int list, int ref)
@@ -143,76 +148,136 @@ static spec_ent *spec_table(VideoParameters *p_Vid, int list, int ref)
     g_n_mb = g_mbs_x * (p_Vid->height / 16);
   }
   if (!g_spec[list][ref]) {
-    g_spec[list][ref] = (spec_ent *)calloc((size_t)g_n_mb * JMME_NSLOT, sizeof(spec_ent));
-    if (!g_spec[list][ref]) error("jm_gpu_me: out of memory", 500);
+    g_spec[list][ref] = (spec_ent *)calloc((size_t)g_n_mb * JMME_NSLOT * KHYP, sizeof(spec_ent));
+    g_seen[list][ref] = (spec_ent *)calloc((size_t)g_n_mb * JMME_NSLOT, sizeof(spec_ent));
+    if (!g_spec[list][ref] || !g_seen[list][ref]) error("jm_gpu_me: out of memory", 500);
     g_spec_frame[list][ref] = -1000000;
   }
   if (g_spec_frame[list][ref] != p_Vid->frame_no) {       /* new picture: forget every guess */
-    for (i = 0; i < g_n_mb * JMME_NSLOT; i++) g_spec[list][ref][i].valid = 0;
+    for (i = 0; i < g_n_mb * JMME_NSLOT * KHYP; i++) g_spec[list][ref][i].valid = 0;
+    for (i = 0; i < g_n_mb * JMME_NSLOT; i++) g_seen[list][ref][i].valid = 0;
     g_spec_frame[list][ref] = p_Vid->frame_no;
     g_spec_end[list][ref] = 0;
   }
   return g_spec[list][ref];
 }
 
-static int spec_same(const spec_ent *e, const spec_ent *w)
+static int spec_key_eq(const spec_ent *e, const spec_ent *w)
 {
-  return e->valid && e->mode == w->mode && e->cx == w->cx && e->cy == w->cy && e->px == w->px && e->py == w->py &&
+  return e->mode == w->mode && e->cx == w->cx && e->cy == w->cy && e->px == w->px && e->py == w->py &&
          e->sr == w->sr && e->chk == w->chk && e->fcx == w->fcx && e->fcy == w->fcy && e->frange == w->frange &&
          e->lambda == w->lambda;
 }
 
-/* one batched search of all 41 partitions of macroblocks mb0.. with the guessed inputs */
-static void spec_batch(int list, int ref, int mb0, const spec_ent *guess, int chk00_slot0, int rdopt)
+static int spec_same(const spec_ent *e, const spec_ent *w) { return e->valid && spec_key_eq(e, w); }
+
+/* Guess h for the 41 partitions of macroblock mb, the search having missed at
+ * macroblock mb0 (mb >= mb0) with inputs `want`:
+ *   0  every partition gets `want` (uniform motion);
+ *   1  each partition gets what the same partition of mb0's left neighbour was searched with;
+ *   2  ... of mb's upper neighbour (when that row is done);
+ *   3  ... of mb0 itself, so far (the next macroblocks move like this one).
+ * Partitions without a known source take `want`.  Returns 0 when the guess has
+ * no source at all.  Only inputs are guessed: a cached result is used only for
+ * a call whose inputs equal them. */
+static int spec_hyp(int list, int ref, int h, int mb0, int mb, const spec_ent *want, int chk00_slot0, spec_ent *out)
+{
+  const spec_ent *seen = g_seen[list][ref], *src = NULL;
+  int s, any = (h == 0), fmb = -1;
+  if (h == 1 && mb0 > 0) fmb = mb0 - 1;
+  if (h == 2 && mb - g_mbs_x >= 0 && mb - g_mbs_x < mb0) fmb = mb - g_mbs_x;
+  if (h == 3 && mb > mb0) fmb = mb0;
+  for (s = 0; s < JMME_NSLOT; s++) {
+    src = fmb >= 0 ? &seen[(size_t)fmb * JMME_NSLOT + s] : NULL;
+    if (src && src->valid && src->mode == want->mode) {
+      out[s] = *src;
+      any = 1;
+    } else {
+      out[s] = *want;
+    }
+    out[s].chk = (int16_t)(!want->mode && s == 0 && chk00_slot0);
+    out[s].valid = 0;
+  }
+  if (want->mode)                         /* FFS: one surface centre per macroblock */
+    for (s = 1; s < JMME_NSLOT; s++) {
+      out[s].fcx = out[0].fcx;
+      out[s].fcy = out[0].fcy;
+      out[s].frange = out[0].frange;
+    }
+  return any;
+}
+
+/* one batched search: all 41 partitions of macroblocks mb0.., under every distinct guess */
+static void spec_batch(int list, int ref, int mb0, const spec_ent *want, int chk00_slot0, int rdopt)
 {
   spec_ent *tab = g_spec[list][ref];
-  int n = imin(g_batch, g_n_mb - mb0), i, s;
-  if (n > g_req_cap) {
+  int n = imin(g_batch, g_n_mb - mb0), nreq = 0, i, s, h, k, mb;
+  if (n * KHYP > g_req_cap) {
     free(g_req);
     free(g_res);
-    g_req = (jmme_mb_req *)malloc((size_t)n * sizeof(jmme_mb_req));
-    g_res = (jmme_block_res *)malloc((size_t)n * JMME_NSLOT * sizeof(jmme_block_res));
-    if (!g_req || !g_res) error("jm_gpu_me: out of memory", 500);
-    g_req_cap = n;
+    free(g_hyp);
+    free(g_req_mb);
+    g_req_cap = n * KHYP;
+    g_req = (jmme_mb_req *)malloc((size_t)g_req_cap * sizeof(jmme_mb_req));
+    g_res = (jmme_block_res *)malloc((size_t)g_req_cap * JMME_NSLOT * sizeof(jmme_block_res));
+    g_hyp = (spec_ent *)malloc((size_t)g_req_cap * JMME_NSLOT * sizeof(spec_ent));
+    g_req_mb = (int *)malloc((size_t)g_req_cap * sizeof(int));
+    if (!g_req || !g_res || !g_hyp || !g_req_mb) error("jm_gpu_me: out of memory", 500);
   }
-  memset(g_req, 0, (size_t)n * sizeof(jmme_mb_req));
-  for (i = 0; i < n; i++) {
-    jmme_mb_req *r = &g_req[i];
-    int mb = mb0 + i;
-    r->mb_x = (int16_t)((mb % g_mbs_x) * 16);
-    r->mb_y = (int16_t)((mb / g_mbs_x) * 16);
-    r->list = (int16_t)list;
-    r->ref_idx = (int16_t)ref;
-    r->slot_mask = (1ull << JMME_NSLOT) - 1;
-    if (guess->mode) {                   /* FFS: the MB's surface (setup_fast_full_search) */
-      r->ffs_center_x = guess->fcx;
-      r->ffs_center_y = guess->fcy;
-      r->ffs_range = guess->frange;
-      r->ffs_pos00_valid = (int16_t)(rdopt == 0);
-    }
-    for (s = 0; s < JMME_NSLOT; s++) {
-      jmme_block_req *b = &r->blk[s];
-      b->pred_x = guess->px;
-      b->pred_y = guess->py;
-      b->center_x = guess->cx;
-      b->center_y = guess->cy;
-      b->search_range = guess->sr;
-      b->flags = (int16_t)((!guess->mode && s == 0 && chk00_slot0) ? JMME_BLK_CHECK00 : 0);
-      b->lambda = guess->lambda;
+  for (mb = mb0; mb < mb0 + n; mb++) {
+    int first = nreq;
+    for (h = 0; h < KHYP; h++) {
+      spec_ent *hy = &g_hyp[(size_t)nreq * JMME_NSLOT];
+      jmme_mb_req *r = &g_req[nreq];
+      int dup = 0;
+      if (!spec_hyp(list, ref, h, mb0, mb, want, chk00_slot0, hy)) continue;
+      for (k = first; k < nreq && !dup; k++) {
+        const spec_ent *o = &g_hyp[(size_t)k * JMME_NSLOT];
+        for (dup = 1, s = 0; s < JMME_NSLOT && dup; s++) dup = spec_key_eq(&o[s], &hy[s]);
+      }
+      if (dup) continue;
+      memset(r, 0, sizeof *r);
+      r->mb_x = (int16_t)((mb % g_mbs_x) * 16);
+      r->mb_y = (int16_t)((mb / g_mbs_x) * 16);
+      r->list = (int16_t)list;
+      r->ref_idx = (int16_t)ref;
+      r->slot_mask = (1ull << JMME_NSLOT) - 1;
+      if (want->mode) {                  /* FFS: the MB's surface (setup_fast_full_search) */
+        r->ffs_center_x = hy[0].fcx;
+        r->ffs_center_y = hy[0].fcy;
+        r->ffs_range = hy[0].frange;
+        r->ffs_pos00_valid = (int16_t)(rdopt == 0);
+      }
+      for (s = 0; s < JMME_NSLOT; s++) {
+        jmme_block_req *b = &r->blk[s];
+        b->pred_x = hy[s].px;
+        b->pred_y = hy[s].py;
+        b->center_x = hy[s].cx;
+        b->center_y = hy[s].cy;
+        b->search_range = hy[s].sr;
+        b->flags = (int16_t)(hy[s].chk ? JMME_BLK_CHECK00 : 0);
+        b->lambda = hy[s].lambda;
+      }
+      g_req_mb[nreq++] = mb;
     }
   }
-  if (jmme_search_mbs(g_me, guess->mode ? JMME_FAST_FULL_SEARCH : JMME_FULL_SEARCH, g_req, n, g_res))
+  if (jmme_search_mbs(g_me, want->mode ? JMME_FAST_FULL_SEARCH : JMME_FULL_SEARCH, g_req, nreq, g_res))
     fail_jm("jmme_search_mbs");
-  for (i = 0; i < n; i++)
+  for (i = 0; i < nreq; i++) {
+    mb = g_req_mb[i];
+    k = (i == 0 || g_req_mb[i - 1] != mb) ? 0 : k + 1;       /* guesses of one MB are consecutive */
     for (s = 0; s < JMME_NSLOT; s++) {
-      spec_ent *e = &tab[(size_t)(mb0 + i) * JMME_NSLOT + s];
-      *e = *guess;
-      e->chk = (int16_t)(!guess->mode && s == 0 && chk00_slot0);
+      spec_ent *e = &tab[((size_t)mb * JMME_NSLOT + s) * KHYP + k];
+      *e = g_hyp[(size_t)i * JMME_NSLOT + s];
       e->mvx = g_res[i * JMME_NSLOT + s].mv_x;
       e->mvy = g_res[i * JMME_NSLOT + s].mv_y;
       e->cost = g_res[i * JMME_NSLOT + s].cost;
       e->valid = 1;
     }
+    if (i + 1 == nreq || g_req_mb[i + 1] != mb)               /* drop older guesses of this MB */
+      for (s = 0; s < JMME_NSLOT; s++)
+        for (h = k + 1; h < KHYP; h++) tab[((size_t)mb * JMME_NSLOT + s) * KHYP + h].valid = 0;
+  }
   g_spec_end[list][ref] = mb0 + n;
   ++g_batches;
 }
@@ -232,18 +297,22 @@ static const spec_ent *spec_lookup(Macroblock *currMB, MEBlock *mv_block, int li
 {
   VideoParameters *p_Vid = currMB->p_Vid;
   int mb = (mv_block->pos_y >> 4) * (p_Vid->width / 16) + (mv_block->pos_x >> 4);
-  int s = jmme_slot(mv_block->blocktype, (mv_block->pos_x & 15) >> 2, (mv_block->pos_y & 15) >> 2);
+  int s = jmme_slot(mv_block->blocktype, (mv_block->pos_x & 15) >> 2, (mv_block->pos_y & 15) >> 2), k;
   spec_ent *tab = spec_table(p_Vid, list, ref), *e;
   if (s < 0 || mb < 0 || mb >= g_n_mb) error("jm_gpu_me: block outside the picture", 500);
-  e = &tab[(size_t)mb * JMME_NSLOT + s];
-  if (!spec_same(e, want)) {
-    if (mb < g_spec_end[list][ref]) g_batch = imax(1, g_batch / 2);       /* a guess failed */
-    else g_batch = imin(2048, g_batch * 2);                              /* ran past the batch */
-    spec_batch(list, ref, mb, want, chk_rule, currMB->p_Inp->rdopt);
-  } else {
-    ++g_hits;
-  }
-  return e;
+  g_seen[list][ref][(size_t)mb * JMME_NSLOT + s] = *want;
+  g_seen[list][ref][(size_t)mb * JMME_NSLOT + s].valid = 1;
+  e = &tab[((size_t)mb * JMME_NSLOT + s) * KHYP];
+  for (k = 0; k < KHYP; k++)
+    if (spec_same(&e[k], want)) {
+      ++g_hits;
+      return &e[k];
+    }
+  if (mb < g_spec_end[list][ref]) g_batch = imax(1, g_batch / 2);         /* every guess failed */
+  else g_batch = imin(2048, g_batch * 2);                                /* ran past the batch */
+  spec_batch(list, ref, mb, want, chk_rule, currMB->p_Inp->rdopt);
+  if (!spec_same(&e[0], want)) error("jm_gpu_me: batch lost its own request", 500);
+  return &e[0];
 }
 
 /* full_search_motion_estimation's contract (me_fullsearch.c:39-103) */
@@ -353,9 +422,10 @@ distblk __wrap_fast_full_search_motion_estimation(Macroblock *currMB, MotionVect
 
 /* ---- sub-pel refinement (SubPelME) ------------------------------------------
  * Speculated like the integer search: a sub-pel batch covers the macroblocks
- * whose integer results are cached, each slot guessed with that slot's cached
- * integer vector / cost and predictor and this call's lambdas, metrics and
- * switches; a call uses a cached answer only when every input matches. */
+ * whose integer results are cached, each slot guessed with each of that slot's
+ * cached integer answers (vector, cost, predictor) and this call's lambdas,
+ * metrics and switches; a call uses a cached answer only when every input
+ * matches. */
 typedef struct sp_ent {
   int16_t px, py, mx, my;
   int64_t min_mcost;
@@ -401,57 +471,75 @@ static void slot_geometry(void)
       }
 }
 
+#define SPK (KHYP + 1)                  /* sub-pel answers kept per (macroblock, slot) */
+static int *g_sp_dst = NULL;
+
+static void sp_fill(jmme_subpel_req *q, int mb, int s, int list, int ref, const sp_ent *w)
+{
+  memset(q, 0, sizeof *q);
+  q->pos_x = (int16_t)((mb % g_mbs_x) * 16 + g_slot_bx[s]);
+  q->pos_y = (int16_t)((mb / g_mbs_x) * 16 + g_slot_by[s]);
+  q->blocktype = (int16_t)g_slot_bt[s];
+  q->ref_slot = (int16_t)(list * 32 + ref);
+  q->pred_x = w->px;
+  q->pred_y = w->py;
+  q->mv_x = w->mx;
+  q->mv_y = w->my;
+  q->lambda_h = w->lam_h;
+  q->lambda_q = w->lam_q;
+  q->min_mcost = w->min_mcost;
+  q->variant = 0;
+  q->flags = w->flags;
+  q->metric_h = w->metric_h;
+  q->metric_q = w->metric_q;
+  q->start_hp = w->start_hp;
+  q->start_qp = w->start_qp;
+  q->search_pos2 = w->pos2;
+  q->search_pos4 = w->pos4;
+}
+
+/* one batched refinement: the calling block with its real inputs (answer kept
+ * in way KHYP) and, for the macroblocks the integer cache covers, every cached
+ * integer answer of every slot (way k for integer way k) */
 static void sp_batch(int list, int ref, int mb0, int s0, const sp_ent *w, int t8)
 {
   const spec_ent *itab = g_spec[list][ref];
   sp_ent *tab = g_sp[list][ref];
-  int mb1 = imax(g_spec_end[list][ref], mb0 + 1), n = 0, i, s, mb;
-  int count = (mb1 - mb0) * JMME_NSLOT;
+  int mb1 = imax(g_spec_end[list][ref], mb0 + 1), n = 0, i, s, k, mb;
+  int count = (mb1 - mb0) * JMME_NSLOT * KHYP + 1;
   if (!g_slot_bt[0]) slot_geometry();
   if (count > g_sreq_cap) {
     free(g_sreq);
     free(g_sres);
+    free(g_sp_dst);
     g_sreq = (jmme_subpel_req *)malloc((size_t)count * sizeof(jmme_subpel_req));
     g_sres = (jmme_block_res *)malloc((size_t)count * sizeof(jmme_block_res));
-    if (!g_sreq || !g_sres) error("jm_gpu_me: out of memory", 500);
+    g_sp_dst = (int *)malloc((size_t)count * sizeof(int));
+    if (!g_sreq || !g_sres || !g_sp_dst) error("jm_gpu_me: out of memory", 500);
     g_sreq_cap = count;
   }
-  memset(g_sreq, 0, (size_t)count * sizeof(jmme_subpel_req));
+  sp_fill(&g_sreq[n], mb0, s0, list, ref, w);
+  g_sp_dst[n++] = (mb0 * JMME_NSLOT + s0) * SPK + KHYP;
   for (mb = mb0; mb < mb1; mb++)
-    for (s = 0; s < JMME_NSLOT; s++, n++) {
-      const spec_ent *ie = itab ? &itab[(size_t)mb * JMME_NSLOT + s] : NULL;
-      jmme_subpel_req *q = &g_sreq[n];
-      int bt = g_slot_bt[s];
-      /* the calling block gets its real inputs, the others their cached integer result */
-      int here = (mb == mb0 && s == s0);
-      if (!here && (!ie || !ie->valid)) continue;      /* blocktype 0: skipped */
-      q->pos_x = (int16_t)((mb % g_mbs_x) * 16 + g_slot_bx[s]);
-      q->pos_y = (int16_t)((mb / g_mbs_x) * 16 + g_slot_by[s]);
-      q->blocktype = (int16_t)bt;
-      q->ref_slot = (int16_t)(list * 32 + ref);
-      q->pred_x = here ? w->px : ie->px;
-      q->pred_y = here ? w->py : ie->py;
-      q->mv_x = here ? w->mx : ie->mvx;
-      q->mv_y = here ? w->my : ie->mvy;
-      q->lambda_h = w->lam_h;
-      q->lambda_q = w->lam_q;
-      q->min_mcost = here ? w->min_mcost : w->start_hp ? ie->cost : JMME_DISTBLK_MAX;
-      q->variant = 0;
-      /* test8x8 as mv_search.c:1630,1770 set it: Transform8x8Mode on block types 1..4 */
-      q->flags = here ? w->flags : (uint8_t)((w->flags & JMME_SP_CHECK0) | (t8 && bt <= 4 ? JMME_SP_TEST8x8 : 0));
-      q->metric_h = w->metric_h;
-      q->metric_q = w->metric_q;
-      q->start_hp = w->start_hp;
-      q->start_qp = w->start_qp;
-      q->search_pos2 = w->pos2;
-      q->search_pos4 = w->pos4;
-    }
+    for (s = 0; s < JMME_NSLOT; s++)
+      for (k = 0; k < KHYP; k++) {
+        const spec_ent *ie = &itab[((size_t)mb * JMME_NSLOT + s) * KHYP + k];
+        sp_ent g = *w;
+        if (!ie->valid) continue;
+        g.px = ie->px;
+        g.py = ie->py;
+        g.mx = ie->mvx;
+        g.my = ie->mvy;
+        g.min_mcost = w->start_hp ? ie->cost : JMME_DISTBLK_MAX;
+        /* test8x8 as mv_search.c:1630,1770 set it: Transform8x8Mode on block types 1..4 */
+        g.flags = (uint8_t)((w->flags & JMME_SP_CHECK0) | (t8 && g_slot_bt[s] <= 4 ? JMME_SP_TEST8x8 : 0));
+        sp_fill(&g_sreq[n], mb, s, list, ref, &g);
+        g_sp_dst[n++] = (mb * JMME_NSLOT + s) * SPK + k;
+      }
   if (jmme_subpel_refine(g_me, g_sreq, n, g_sres)) fail_jm("jmme_subpel_refine");
   for (i = 0; i < n; i++) {
     const jmme_subpel_req *q = &g_sreq[i];
-    sp_ent *e;
-    if (!q->blocktype) continue;
-    e = &tab[(size_t)(mb0 + i / JMME_NSLOT) * JMME_NSLOT + i % JMME_NSLOT];
+    sp_ent *e = &tab[g_sp_dst[i]];
     e->px = q->pred_x; e->py = q->pred_y; e->mx = q->mv_x; e->my = q->mv_y;
     e->min_mcost = q->min_mcost; e->lam_h = q->lambda_h; e->lam_q = q->lambda_q;
     e->metric_h = q->metric_h; e->metric_q = q->metric_q; e->start_hp = q->start_hp; e->start_qp = q->start_qp;
@@ -496,24 +584,27 @@ distblk __wrap_sub_pel_motion_estimation(Macroblock *currMB, MotionVector *pred_
                          ((!currMB->p_Inp->rdopt && currSlice->slice_type != B_SLICE) ? JMME_SP_CHECK0 : 0));
   spec_table(p_Vid, list, ref);                       /* sizes and per-picture reset of the integer table */
   if (!g_sp[list][ref]) {
-    g_sp[list][ref] = (sp_ent *)calloc((size_t)g_n_mb * JMME_NSLOT, sizeof(sp_ent));
+    g_sp[list][ref] = (sp_ent *)calloc((size_t)g_n_mb * JMME_NSLOT * SPK, sizeof(sp_ent));
     if (!g_sp[list][ref]) error("jm_gpu_me: out of memory", 500);
     g_sp_frame[list][ref] = -1000000;
   }
   tab = g_sp[list][ref];
   if (g_sp_frame[list][ref] != p_Vid->frame_no) {
-    for (i = 0; i < g_n_mb * JMME_NSLOT; i++) tab[i].valid = 0;
+    for (i = 0; i < g_n_mb * JMME_NSLOT * SPK; i++) tab[i].valid = 0;
     g_sp_frame[list][ref] = p_Vid->frame_no;
   }
   mb = (mv_block->pos_y >> 4) * g_mbs_x + (mv_block->pos_x >> 4);
   s = jmme_slot(mv_block->blocktype, (mv_block->pos_x & 15) >> 2, (mv_block->pos_y & 15) >> 2);
   if (s < 0 || mb < 0 || mb >= g_n_mb) error("jm_gpu_me: block outside the picture", 500);
-  e = &tab[(size_t)mb * JMME_NSLOT + s];
-  if (!sp_same(e, &want)) {
-    sp_batch(list, ref, mb, s, &want, currMB->p_Inp->Transform8x8Mode != 0);
-    if (!sp_same(e, &want)) error("jm_gpu_me: sub-pel batch lost its own request", 500);
-  } else {
+  e = &tab[((size_t)mb * JMME_NSLOT + s) * SPK];
+  for (i = 0; i < SPK && !sp_same(&e[i], &want); i++) {}
+  if (i < SPK) {
     ++g_sp_hits;
+    e += i;
+  } else {
+    sp_batch(list, ref, mb, s, &want, currMB->p_Inp->Transform8x8Mode != 0);
+    e += KHYP;
+    if (!sp_same(e, &want)) error("jm_gpu_me: sub-pel batch lost its own request", 500);
   }
   mv_block->mv[list].mv_x = e->omx;
   mv_block->mv[list].mv_y = e->omy;

@@ -1,0 +1,25 @@
+#!/bin/bash
+# rocprofv3 kernel + runtime trace of the drop-in encoder itself (1080p, 2 frames,
+# sub-pel on): where a speculative batch's time goes.  GPU box.
+set -e
+cd "$(dirname "$0")/.."
+out=gpurun_out/prof_dropin
+mkdir -p $out
+export TMPDIR=/tmp
+d=$(mktemp -d)
+python3 - "$d" <<'PY'
+import os, sys
+sys.path.insert(0, "--h.264-by-zhaodongyu_amd"); sys.path.insert(0, "tests")
+from jmme import synth
+from test_jm_dropin_gpu import CFG
+d = sys.argv[1]
+synth.write_yuv420(os.path.join(d, "in.yuv"), synth.luma_sequence(1920, 1080, 2, seed=2024, gmv=(5, 3)))
+open(os.path.join(d, "enc.cfg"), "w").write(CFG)
+PY
+args="-d $d/enc.cfg -p InputFile=$d/in.yuv -p SourceWidth=1920 -p SourceHeight=1080 -p OutputWidth=1920
+ -p OutputHeight=1080 -p FramesToBeEncoded=2 -p OutputFile=$d/o.264 -p ReconFile=$d/r.yuv -p SearchMode=${MODE:--1}
+ -p SearchRange=32 -p RDOptimization=0 -p NumberReferenceFrames=1 -p DisableSubpelME=0 -p MEDistortionQPel=2
+ -p MDDistortion=2"
+timeout -k 10 300 rocprofv3 --kernel-trace --runtime-trace --stats -d $out -o run -- \
+  "$PWD/integration/_build/lencod_jmme" $args > $out/lencod.log 2>&1
+find $out -name "*stats.csv" | head
