@@ -4,7 +4,8 @@ integration/jm_gpu_me.c, JM sources untouched) encodes the same input as the
 stock lencod (oracle/_ref/lencod, CPU) with the same configuration: the
 bitstreams and reconstructions must be byte-identical, for full search and fast
 full search, with RDO on and off, several reference frames, and sub-pel
-refinement (SubPelME) off and on (SAD/SSE/SATD, 8x8-transform SATD).  The stock
+refinement (SubPelME) off and on (SAD/SSE/SATD, 8x8-transform SATD), P and B
+pictures.  The stock
 encoder is the oracle here; both binaries are built in this container
 (`make -C integration`)."""
 import hashlib
@@ -71,6 +72,11 @@ def _encode(binary, d, tag, yuv, w, h, frames, params, env=None):
                    "DisableSubpelME": 0, "ProfileIDC": 100, "Transform8x8Mode": 1, "MDDistortion": 2}),
     (352, 288, 3, {"SearchMode": 0, "SearchRange": 32, "RDOptimization": 1, "NumberReferenceFrames": 1,
                    "DisableSubpelME": 0, "ProfileIDC": 100, "Transform8x8Mode": 2, "MDDistortion": 2}),
+    # B pictures (Main profile): list-1 searches and the B-slice sub-pel rules (no check_position0)
+    (176, 144, 5, {"SearchMode": -1, "SearchRange": 16, "RDOptimization": 0, "NumberReferenceFrames": 2,
+                   "NumberBFrames": 1, "ProfileIDC": 77, "DisableSubpelME": 0, "MEDistortionQPel": 0}),
+    (176, 144, 5, {"SearchMode": 0, "SearchRange": 16, "RDOptimization": 1, "NumberReferenceFrames": 2,
+                   "NumberBFrames": 1, "ProfileIDC": 77, "DisableSubpelME": 0, "MEDistortionQPel": 0}),
 ])
 def test_lencod_with_gpu_me_is_byte_identical(gpu, w, h, frames, params, speculate):
     """speculate=1: full-search calls answered from speculative batches (jm_gpu_me.c);
@@ -88,3 +94,22 @@ def test_lencod_with_gpu_me_is_byte_identical(gpu, w, h, frames, params, specula
         if params.get("DisableSubpelME") == 0 and speculate == "1":
             m = re.search(r"(\d+) sub-pel refinements: (\d+) cached, (\d+) batches, (\d+) on the CPU", r.stderr)
             assert m and int(m.group(1)) > 0 and int(m.group(4)) == 0, r.stderr[-500:]
+
+
+def test_lencod_720p_ffs_subpel_speculative(gpu):
+    """a 720p P picture (3600 macroblocks): batches grow to their cap and the four-guess
+    cache is exercised at scale; fast full search + SATD sub-pel, JM's defaults"""
+    if not (os.path.exists(STOCK) and os.path.exists(GPU)):
+        pytest.fail("lencod builds missing: run `make -C oracle ref && make -C integration` in the build container")
+    from jmme import synth
+    w, h, frames = 1280, 720, 2
+    params = {"SearchMode": 0, "SearchRange": 32, "RDOptimization": 0, "NumberReferenceFrames": 1,
+              "DisableSubpelME": 0, "MEDistortionQPel": 2, "MDDistortion": 2}
+    with tempfile.TemporaryDirectory() as d:
+        yuv = os.path.join(d, "in.yuv")
+        synth.write_yuv420(yuv, synth.luma_sequence(w, h, frames, seed=w + frames, gmv=(3, -2)))
+        ref264, refrec, _ = _encode(STOCK, d, "cpu", yuv, w, h, frames, params)
+        gpu264, gpurec, r = _encode(GPU, d, "gpu", yuv, w, h, frames, params)
+        assert (gpu264, gpurec) == (ref264, refrec)
+        m = re.search(r"(\d+) sub-pel refinements: (\d+) cached, (\d+) batches, (\d+) on the CPU", r.stderr)
+        assert m and int(m.group(1)) == 3600 * 41 and int(m.group(4)) == 0, r.stderr[-500:]
