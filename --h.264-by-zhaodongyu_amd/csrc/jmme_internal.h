@@ -32,6 +32,8 @@ static_assert(sizeof(Item) == 48, "Item layout");
 constexpr int kItemChk00 = 1;     // slot 0 takes check_for_00 (me_fullsearch.c:61)
 constexpr int kItemPreseed = 2;   // FFS pos00 pre-seed (me_fullfast.c:640-648)
 
+constexpr uint32_t kMaxLambda32 = 28450;   // 32*65280 + lambda*74 < 2^22: 22-bit cost field exact
+
 struct KParams {
   const uint8_t *cur;                 // 8-bit current picture
   const uint8_t *const *refs;         // device table [kMaxLists*kMaxRefs] of 8-bit reference planes
@@ -44,6 +46,7 @@ struct KParams {
   int max_mvd;                        // p_Vid->max_mvd (FFS gate)
   int lds_range;                      // largest search range in the launch (LDS sizing)
   int key32;                          // plan: route items to the 32-bit list (else all to the 64-bit list)
+  int no64;                           // host-checked: no unit needs the 64-bit list (skip its drain launch)
   Item *items;                        // [item_cap]: 32-bit list grows up from 0, 64-bit list down from the top
   unsigned item_cap;
   unsigned *counts;                   // [0] 32-bit items, [1] 64-bit items, [2] status

@@ -53,7 +53,6 @@ namespace {
 constexpr int kNS = JMME_NSLOT;
 constexpr int kWaves = kWG / 64;
 constexpr unsigned long long kAll = (1ull << kNS) - 1;
-constexpr uint32_t kMaxLambda32 = 28450;   // 32*65280 + lambda*74 < 2^22: 22-bit cost field exact
 constexpr int kCostShift = 10;             // key32 = cost << 10 | rank >> 3
 constexpr int kRankDrop = 3;
 constexpr int kCand = 1 << kRankDrop;      // refine candidates per partition
@@ -919,7 +918,7 @@ hipError_t launch_search(const KParams &p, hipStream_t s, hipEvent_t ev0, hipEve
     if (ev1) (void)hipEventRecord(ev1, s);
     // units whose lambda could saturate the 32-bit cost field (none in
     // practice) were planned into the 64-bit list: a small grid drains it
-    hipLaunchKernelGGL(k64, dim3(64), dim3(kWG), lds, s, p);
+    if (!p.no64) hipLaunchKernelGGL(k64, dim3(64), dim3(kWG), lds, s, p);
   } else {
     hipLaunchKernelGGL(k64, dim3(resident_grid(occ, v + 1, k64, p.lds_range, lds)), dim3(kWG), lds, s, p);
     if ((e = hipGetLastError()) != hipSuccess) return e;
