@@ -319,7 +319,6 @@ static const spec_ent *spec_lookup(Macroblock *currMB, MEBlock *mv_block, int li
 distblk __wrap_full_search_motion_estimation(Macroblock *currMB, MotionVector *pred_mv, MEBlock *mv_block,
                                              distblk min_mcost, int lambda_factor)
 {
-  VideoParameters *p_Vid = currMB->p_Vid;
   Slice *currSlice = currMB->p_Slice;
   int list = mv_block->list, ref = mv_block->ref_idx;
   /* search_range and check_for_00 as me_fullsearch.c:49,61 derive them */
