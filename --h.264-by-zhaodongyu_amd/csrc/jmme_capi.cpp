@@ -43,6 +43,18 @@ int fail(const char *fmt, ...) {
     if (e_ != hipSuccess) return fail("%s: %s", #x, hipGetErrorString(e_));      \
   } while (0)
 
+
+// Every entry point that takes a context runs on the context's device and
+// restores the caller's current device on return, so contexts on several GPUs
+// (or a caller such as torch that switches devices) never mix pointers.
+struct DevGuard {
+  int prev = -1;
+  explicit DevGuard(const jmme_ctx *c);
+  ~DevGuard() { if (prev >= 0) (void)hipSetDevice(prev); }
+  DevGuard(const DevGuard &) = delete;
+  DevGuard &operator=(const DevGuard &) = delete;
+};
+
 }  // namespace
 
 struct jmme_ctx {
@@ -83,6 +95,11 @@ struct jmme_ctx {
   uint8_t *d_sp = nullptr;
   size_t cap_sp = 0;
 };
+
+DevGuard::DevGuard(const jmme_ctx *c) {
+  int cur = 0;
+  if (c && hipGetDevice(&cur) == hipSuccess && cur != c->device && hipSetDevice(c->device) == hipSuccess) prev = cur;
+}
 
 // ----------------------------------------------------------------- config --
 extern "C" int jmme_config_default(jmme_config *c) {
@@ -216,6 +233,13 @@ extern "C" jmme_ctx *jmme_create(const jmme_config *cfg, int device) {
   if (!cfg) { fail("null config"); return nullptr; }
   if (cfg->ChromaMEEnable) { fail("ChromaMEEnable != 0 is not supported"); return nullptr; }
   if (cfg->SourceBitDepthLuma != 8) { fail("only 8-bit luma is supported"); return nullptr; }
+  // the integer-pel kernels compute JM's computeSAD (me_distortion.c:349); SSE /
+  // SATD full-pel metrics (MEDistortionFPel 1/2, lencod.c:782-796) would give
+  // different vectors, so they are refused rather than silently searched with SAD
+  if (cfg->MEDistortionFPel != 0) {
+    fail("MEDistortionFPel %d: only SAD (0) integer-pel search is supported", cfg->MEDistortionFPel);
+    return nullptr;
+  }
   if (cfg->SearchRange < 0 || cfg->SearchRange > JMME_MAX_RANGE) {
     fail("SearchRange %d outside [0,%d]", cfg->SearchRange, JMME_MAX_RANGE);
     return nullptr;
@@ -224,11 +248,18 @@ extern "C" jmme_ctx *jmme_create(const jmme_config *cfg, int device) {
   ctx->cfg = *cfg;
   ctx->max_mvd = jmme_max_mvd(cfg);
   hipError_t e;
-  if (device >= 0) {
+  int caller_dev = -1;
+  (void)hipGetDevice(&caller_dev);
+  if (device >= 0 && device != caller_dev) {
     e = hipSetDevice(device);
     if (e != hipSuccess) { fail("hipSetDevice(%d): %s", device, hipGetErrorString(e)); delete ctx; return nullptr; }
   }
   (void)hipGetDevice(&ctx->device);
+  // allocations below go to ctx->device; the caller's current device is restored on return
+  struct Restore {
+    int d, was;
+    ~Restore() { if (d >= 0 && d != was) (void)hipSetDevice(d); }
+  } restore_{caller_dev, ctx->device};
   if ((e = hipMalloc(&ctx->d_ref_table, sizeof(uint8_t *) * kMaxLists * kMaxRefs)) != hipSuccess ||
       (e = hipMalloc(&ctx->d_counts, 16)) != hipSuccess ||
       (e = hipMalloc(&ctx->d_sub_table, sizeof(uint8_t *) * kMaxLists * kMaxRefs)) != hipSuccess ||
@@ -241,6 +272,7 @@ extern "C" jmme_ctx *jmme_create(const jmme_config *cfg, int device) {
 }
 
 extern "C" void jmme_destroy(jmme_ctx *ctx) {
+  DevGuard dg_(ctx);
   if (!ctx) return;
   (void)hipFree(ctx->d_cur);
   for (auto *p : ctx->d_refs) (void)hipFree(p);
@@ -296,11 +328,13 @@ int upload_plane(jmme_ctx *ctx, uint8_t **dst, const jmme_imgpel *const *rows, i
 }  // namespace
 
 extern "C" int jmme_upload_cur(jmme_ctx *ctx, const jmme_imgpel *const *rows, int w, int h) {
+  DevGuard dg_(ctx);
   if (!ctx) return fail("null ctx");
   return upload_plane(ctx, &ctx->d_cur, rows, w, h);
 }
 
 extern "C" int jmme_upload_ref(jmme_ctx *ctx, int list, int ref_idx, const jmme_imgpel *const *rows, int w, int h) {
+  DevGuard dg_(ctx);
   if (!ctx) return fail("null ctx");
   if (list < 0 || list >= kMaxLists || ref_idx < 0 || ref_idx >= kMaxRefs)
     return fail("list/ref_idx (%d,%d) out of range", list, ref_idx);
@@ -469,6 +503,7 @@ int validate(const jmme_ctx *ctx, int mode, const jmme_mb_req *req, int n) {
 }  // namespace
 
 extern "C" int jmme_search_mbs(jmme_ctx *ctx, int mode, const jmme_mb_req *req, int n, jmme_block_res *out) {
+  DevGuard dg_(ctx);
   if (!ctx) return fail("null ctx");
   if (!ctx->d_cur) return fail("current picture not uploaded");
   if (n == 0) return 0;
@@ -507,6 +542,7 @@ extern "C" int jmme_search_mbs(jmme_ctx *ctx, int mode, const jmme_mb_req *req, 
 
 extern "C" int jmme_search_mbs_async(jmme_ctx *ctx, int mode, const jmme_mb_req *d_req, int n,
                                      jmme_block_res *d_out, void *stream) {
+  DevGuard dg_(ctx);
   if (!ctx) return fail("null ctx");
   if (!ctx->d_cur) return fail("current picture not uploaded");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -517,6 +553,7 @@ extern "C" int jmme_search_mbs_async(jmme_ctx *ctx, int mode, const jmme_mb_req 
 extern "C" int jmme_search_mbs_planes_async(jmme_ctx *ctx, int mode, const uint8_t *d_cur, const uint8_t *d_ref,
                                             int pitch, int w, int h, const jmme_mb_req *d_req, int n,
                                             jmme_block_res *d_out, void *stream) {
+  DevGuard dg_(ctx);
   if (!ctx) return fail("null ctx");
   if (!d_cur || !d_ref) return fail("null plane");
   if (pitch < w || (pitch & 3) || (w & 15) || (h & 15)) return fail("bad plane geometry %dx%d pitch %d", w, h, pitch);
@@ -529,6 +566,7 @@ extern "C" int jmme_search_mbs_planes_async(jmme_ctx *ctx, int mode, const uint8
 }
 
 extern "C" float jmme_last_kernel_ms(jmme_ctx *ctx) {
+  DevGuard dg_(ctx);
   if (!ctx || !ctx->timed) return -1.0f;
   float ms = -1.0f;
   if (hipEventSynchronize(ctx->ev1) != hipSuccess) return -1.0f;
@@ -540,6 +578,7 @@ extern "C" jmme_distblk jmme_full_search_block(jmme_ctx *ctx, int list, int ref_
                                                int blocktype, const jmme_mv *pred_mv, jmme_mv *mv_inout,
                                                jmme_distblk min_mcost, int lambda_factor, int search_range,
                                                int check_for_00) {
+  DevGuard dg_(ctx);
   // IntPelME-signature drop-in: one partition as a one-slot unit.  JM's
   // error() semantics on failure (print, exit 500).
   int mb_x = pos_x & ~15, mb_y = pos_y & ~15;
@@ -585,6 +624,7 @@ struct DevBuf {
 }  // namespace
 
 extern "C" int jmme_transform_async(jmme_ctx *ctx, int op, const int32_t *d_in, int32_t *d_out, int n, void *stream) {
+  DevGuard dg_(ctx);
   if (!ctx) return fail("null ctx");
   if (n < 0) return fail("negative block count");
   if (!transform_elems(op)) return fail("unknown transform op %d", op);
@@ -595,6 +635,7 @@ extern "C" int jmme_transform_async(jmme_ctx *ctx, int op, const int32_t *d_in, 
 }
 
 extern "C" int jmme_transform(jmme_ctx *ctx, int op, const int32_t *in, int32_t *out, int n) {
+  DevGuard dg_(ctx);
   if (!ctx) return fail("null ctx");
   const int e = transform_elems(op);
   if (!e) return fail("unknown transform op %d", op);
@@ -611,6 +652,7 @@ extern "C" int jmme_transform(jmme_ctx *ctx, int op, const int32_t *in, int32_t 
 }
 
 extern "C" int jmme_satd_async(jmme_ctx *ctx, int size, const int16_t *d_diff, int32_t *d_out, int n, void *stream) {
+  DevGuard dg_(ctx);
   if (!ctx) return fail("null ctx");
   if (size != 4 && size != 8) return fail("SATD block size %d (4 or 8)", size);
   if (n < 0) return fail("negative block count");
@@ -621,6 +663,7 @@ extern "C" int jmme_satd_async(jmme_ctx *ctx, int size, const int16_t *d_diff, i
 }
 
 extern "C" int jmme_satd(jmme_ctx *ctx, int size, const int16_t *diff, int32_t *out, int n) {
+  DevGuard dg_(ctx);
   if (!ctx) return fail("null ctx");
   if (size != 4 && size != 8) return fail("SATD block size %d (4 or 8)", size);
   if (n <= 0) return n < 0 ? fail("negative block count") : 0;
@@ -638,6 +681,7 @@ extern "C" int jmme_satd(jmme_ctx *ctx, int size, const int16_t *diff, int32_t *
 extern "C" int jmme_quant4x4_async(jmme_ctx *ctx, const jmme_quant4x4_params *d_params, const int32_t *d_param_idx,
                                    int32_t *d_coef, int32_t *d_levels, int32_t *d_runs, int32_t *d_coeff_cost,
                                    int32_t *d_nonzero, int n, void *stream) {
+  DevGuard dg_(ctx);
   if (!ctx) return fail("null ctx");
   if (n < 0) return fail("negative block count");
   if (n == 0) return 0;
@@ -650,6 +694,7 @@ extern "C" int jmme_quant4x4_async(jmme_ctx *ctx, const jmme_quant4x4_params *d_
 extern "C" int jmme_quant4x4(jmme_ctx *ctx, const jmme_quant4x4_params *params, int n_params, const int32_t *param_idx,
                              int32_t *coef, int32_t *levels, int32_t *runs, int32_t *coeff_cost, int32_t *nonzero,
                              int n) {
+  DevGuard dg_(ctx);
   if (!ctx) return fail("null ctx");
   if (n <= 0) return n < 0 ? fail("negative block count") : 0;
   if (!params || n_params <= 0 || !coef || !levels || !runs || !coeff_cost || !nonzero) return fail("null array");
@@ -703,6 +748,7 @@ int fractal_geom_ok(int pitch, int w, int h) {
 
 extern "C" int jmme_fractal_words_async(jmme_ctx *ctx, const uint8_t *d_ref, int pitch, int width, int height,
                                         uint32_t *d_words, void *stream) {
+  DevGuard dg_(ctx);
   if (!ctx) return fail("null ctx");
   if (fractal_geom_ok(pitch, width, height)) return -1;
   if (!d_ref || !d_words) return fail("null plane");
@@ -713,6 +759,7 @@ extern "C" int jmme_fractal_words_async(jmme_ctx *ctx, const uint8_t *d_ref, int
 extern "C" int jmme_fractal_search_async(jmme_ctx *ctx, const uint8_t *d_org, int pitch, const uint32_t *d_words,
                                          int width, int height, int search_range, const jmme_fractal_req *d_req,
                                          int n, jmme_fractal_res *d_out, void *stream) {
+  DevGuard dg_(ctx);
   if (!ctx) return fail("null ctx");
   if (fractal_geom_ok(pitch, width, height)) return -1;
   if (search_range < 0) return fail("negative search range");
@@ -761,6 +808,7 @@ extern "C" int jmme_fractal_search_async(jmme_ctx *ctx, const uint8_t *d_org, in
 }
 
 extern "C" int jmme_fractal_set_pool_min_range(jmme_ctx *ctx, int min_range) {
+  DevGuard dg_(ctx);
   if (!ctx) return fail("null ctx");
   if (min_range < 0) return fail("negative pool radius");
   ctx->pool_min_range = min_range;
@@ -768,12 +816,14 @@ extern "C" int jmme_fractal_set_pool_min_range(jmme_ctx *ctx, int min_range) {
 }
 
 extern "C" int jmme_fractal_set_pool_mfma(jmme_ctx *ctx, int on) {
+  DevGuard dg_(ctx);
   if (!ctx) return fail("null ctx");
   ctx->pool_mfma = on != 0;
   return 0;
 }
 
 extern "C" int jmme_fractal_pool_survivors(jmme_ctx *ctx, unsigned long long *survivors) {
+  DevGuard dg_(ctx);
   if (!ctx || !survivors) return fail("null argument");
   *survivors = 0;
   if (!ctx->d_pool) return 0;
@@ -787,6 +837,7 @@ extern "C" int jmme_fractal_pool_survivors(jmme_ctx *ctx, unsigned long long *su
 extern "C" int jmme_fractal_search(jmme_ctx *ctx, const uint8_t *org, const uint8_t *ref, int pitch, int width,
                                    int height, int search_range, const jmme_fractal_req *req, int n,
                                    jmme_fractal_res *out) {
+  DevGuard dg_(ctx);
   if (!ctx) return fail("null ctx");
   if (fractal_geom_ok(pitch, width, height)) return -1;
   if (search_range < 0) return fail("negative search range");
@@ -821,6 +872,7 @@ extern "C" int jmme_fractal_search(jmme_ctx *ctx, const uint8_t *org, const uint
 
 extern "C" int jmme_fractal_box_sums(jmme_ctx *ctx, const uint8_t *plane, int pitch, int width, int height, int bsx,
                                      int bsy, double *sum, double *sum2) {
+  DevGuard dg_(ctx);
   if (!ctx) return fail("null ctx");
   if (fractal_geom_ok(pitch, width, height)) return -1;
   if (bsx < 1 || bsy < 1 || bsx > 16 || bsy > 16 || bsx > width || bsy > height) return fail("box %dx%d", bsx, bsy);
@@ -849,6 +901,7 @@ int prepare_subs(jmme_ctx *ctx, hipStream_t s);   // sub-pel section below
 
 extern "C" int jmme_epzs_search_async(jmme_ctx *ctx, const jmme_epzs_req *d_req, int n, const int16_t *d_preds,
                                       const int16_t *d_stale, jmme_epzs_res *d_out, void *stream) {
+  DevGuard dg_(ctx);
   if (!ctx) return fail("null ctx");
   if (n < 0) return fail("negative request count");
   if (n == 0) return 0;
@@ -886,6 +939,7 @@ extern "C" int jmme_epzs_search_async(jmme_ctx *ctx, const jmme_epzs_req *d_req,
 
 extern "C" int jmme_epzs_search(jmme_ctx *ctx, const jmme_epzs_req *req, int n, const int16_t *preds, int n_preds,
                                 const int16_t *stale, int n_stale, jmme_epzs_res *out) {
+  DevGuard dg_(ctx);
   if (!ctx) return fail("null ctx");
   if (n <= 0) return n < 0 ? fail("negative request count") : 0;
   if (!req || !out || (n_preds && !preds) || (n_stale && !stale)) return fail("null array");
@@ -941,6 +995,7 @@ extern "C" int jmme_fractal_encode_mbs_async(jmme_ctx *ctx, const uint8_t *d_org
                                              const uint32_t *const *d_words, int n_refs, int width, int height,
                                              int search_range, double tol_16, double tol_8, jmme_fractal_mb *d_out,
                                              void *stream) {
+  DevGuard dg_(ctx);
   if (!ctx) return fail("null ctx");
   if (fractal_geom_ok(pitch, width, height)) return -1;
   if (width % 16 || height % 16) return fail("fractal macroblock plane %dx%d: need multiples of 16", width, height);
@@ -997,6 +1052,7 @@ extern "C" int jmme_fractal_encode_mbs_async(jmme_ctx *ctx, const uint8_t *d_org
 extern "C" int jmme_fractal_encode_mbs(jmme_ctx *ctx, const uint8_t *org, const uint8_t *const *refs, int n_refs,
                                        int pitch, int width, int height, int search_range, double tol_16,
                                        double tol_8, jmme_fractal_mb *out) {
+  DevGuard dg_(ctx);
   if (!ctx) return fail("null ctx");
   if (fractal_geom_ok(pitch, width, height)) return -1;
   if (width % 16 || height % 16) return fail("fractal macroblock plane %dx%d: need multiples of 16", width, height);
@@ -1031,6 +1087,7 @@ extern "C" int jmme_fractal_decode_mbs_async(jmme_ctx *ctx, const jmme_fractal_m
                                              const uint8_t *const *d_views, int n_views, int pitch, int width,
                                              int height, int component, uint8_t *d_rec, int *d_status,
                                              void *stream) {
+  DevGuard dg_(ctx);
   if (!ctx) return fail("null ctx");
   if (fractal_geom_ok(pitch, width, height)) return -1;
   if (width % 16 || height % 16) return fail("fractal macroblock plane %dx%d: need multiples of 16", width, height);
@@ -1058,6 +1115,7 @@ extern "C" int jmme_fractal_decode_mbs_async(jmme_ctx *ctx, const jmme_fractal_m
 
 extern "C" int jmme_fractal_decode_mbs(jmme_ctx *ctx, const jmme_fractal_mb *mbs, const uint8_t *const *views,
                                        int n_views, int pitch, int width, int height, int component, uint8_t *rec) {
+  DevGuard dg_(ctx);
   if (!ctx) return fail("null ctx");
   if (fractal_geom_ok(pitch, width, height)) return -1;
   if (width % 16 || height % 16) return fail("fractal macroblock plane %dx%d: need multiples of 16", width, height);
@@ -1097,6 +1155,7 @@ extern "C" jmme_distblk jmme_fast_full_search_block(jmme_ctx *ctx, int list, int
                                                     const jmme_mv *search_center, int surface_range,
                                                     int block_range, int rdopt, jmme_mv *mv_out,
                                                     jmme_distblk min_mcost, int lambda_factor) {
+  DevGuard dg_(ctx);
   // fast_full_search_motion_estimation's contract for one partition, as a
   // one-slot FFS unit (the surface of setup_fast_full_search is the unit's
   // window).  JM's error() semantics on failure (print, exit 500).
@@ -1137,6 +1196,7 @@ extern "C" jmme_distblk jmme_fast_full_search_block(jmme_ctx *ctx, int list, int
 }
 
 extern "C" int jmme_debug_window(jmme_ctx *ctx, int mode, const jmme_mb_req *req, uint32_t *out, int max_words) {
+  DevGuard dg_(ctx);
   // Test hook: run unit `req` (one unit) and return the first reference
   // window it staged in LDS (rows x pitch words, word[y][x] = pels x..x+3).
   if (!ctx) return fail("null ctx");
@@ -1158,6 +1218,7 @@ extern "C" int jmme_debug_window(jmme_ctx *ctx, int mode, const jmme_mb_req *req
 }
 
 extern "C" int jmme_debug_stamps(jmme_ctx *ctx, uint64_t *out, int max_units) {
+  DevGuard dg_(ctx);
   // Diagnostic builds (-DJMME_STAMPS): per-unit s_memtime phase sums of the
   // last launch: [wait, expand, sweep, reduce, refine, output, nslots, items].
   if (!ctx) return fail("null ctx");
@@ -1202,6 +1263,7 @@ int prepare_subs(jmme_ctx *ctx, hipStream_t s) {
 }  // namespace
 
 extern "C" int jmme_interpolate_ref(jmme_ctx *ctx, int list, int ref_idx, void *stream) {
+  DevGuard dg_(ctx);
   if (!ctx) return fail("null ctx");
   if (list < 0 || list >= kMaxLists || ref_idx < 0 || ref_idx >= kMaxRefs)
     return fail("list/ref_idx (%d,%d) out of range", list, ref_idx);
@@ -1209,6 +1271,7 @@ extern "C" int jmme_interpolate_ref(jmme_ctx *ctx, int list, int ref_idx, void *
 }
 
 extern "C" int jmme_get_sub_images(jmme_ctx *ctx, int list, int ref_idx, jmme_imgpel ****sub) {
+  DevGuard dg_(ctx);
   if (!ctx) return fail("null ctx");
   if (!sub) return fail("null sub-image array");
   if (list < 0 || list >= kMaxLists || ref_idx < 0 || ref_idx >= kMaxRefs)
@@ -1235,6 +1298,7 @@ extern "C" int jmme_get_sub_images(jmme_ctx *ctx, int list, int ref_idx, jmme_im
 
 extern "C" int jmme_sub_images_async(jmme_ctx *ctx, const uint8_t *d_src, int src_pitch, int width, int height,
                                      uint8_t *d_dst, int dst_pitch, size_t plane_stride, void *stream) {
+  DevGuard dg_(ctx);
   if (!ctx) return fail("null ctx");
   if (!d_src || !d_dst) return fail("null plane");
   if (width <= 0 || height <= 0 || src_pitch < width) return fail("bad source plane %dx%d pitch %d", width, height,
@@ -1249,6 +1313,7 @@ extern "C" int jmme_sub_images_async(jmme_ctx *ctx, const uint8_t *d_src, int sr
 }
 
 extern "C" int jmme_subpel_validate(jmme_ctx *ctx, const jmme_subpel_req *req, int n) {
+  DevGuard dg_(ctx);
   if (!ctx) return fail("null ctx");
   if (n < 0) return fail("negative request count");
   if (n && !req) return fail("null request array");
@@ -1283,6 +1348,7 @@ extern "C" int jmme_subpel_validate(jmme_ctx *ctx, const jmme_subpel_req *req, i
 
 extern "C" int jmme_subpel_refine_async(jmme_ctx *ctx, const jmme_subpel_req *d_req, int n,
                                         const jmme_block_res *d_int, jmme_block_res *d_out, void *stream) {
+  DevGuard dg_(ctx);
   if (!ctx) return fail("null ctx");
   if (n < 0) return fail("negative request count");
   if (n == 0) return 0;
@@ -1308,6 +1374,7 @@ extern "C" int jmme_subpel_refine_async(jmme_ctx *ctx, const jmme_subpel_req *d_
 }
 
 extern "C" int jmme_subpel_refine(jmme_ctx *ctx, const jmme_subpel_req *req, int n, jmme_block_res *out) {
+  DevGuard dg_(ctx);
   if (jmme_subpel_validate(ctx, req, n)) return -1;
   if (n == 0) return 0;
   if (!out) return fail("null output array");

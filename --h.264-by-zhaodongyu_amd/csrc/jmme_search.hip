@@ -872,10 +872,8 @@ struct Occupancy {
 };
 
 template <typename K>
-int resident_grid(Occupancy &o, int variant, K kernel, int lds_range, size_t lds) {
+int resident_grid(Occupancy &o, int dev, int variant, K kernel, int lds_range, size_t lds) {
   if (!o.cus) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
     if (hipDeviceGetAttribute(&o.cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || o.cus <= 0)
       o.cus = 256;
   }
@@ -900,7 +898,13 @@ size_t items_lds_bytes(int R) {
 }
 
 hipError_t launch_search(const KParams &p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
-  static thread_local Occupancy occ;
+  // occupancy per device: the caller (jmme_capi) has made the context's device current
+  constexpr int kMaxDev = 64;
+  static thread_local Occupancy occ_tab[kMaxDev];
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  Occupancy spare;
+  Occupancy &occ = (dev >= 0 && dev < kMaxDev) ? occ_tab[dev] : spare;
   const size_t lds = items_lds_bytes(p.lds_range);
   const bool ffs = p.mode == JMME_FAST_FULL_SEARCH;
   const int plan_grid = (p.n + kPlanWaves - 1) / kPlanWaves;
@@ -913,14 +917,14 @@ hipError_t launch_search(const KParams &p, hipStream_t s, hipEvent_t ev0, hipEve
   const int v = ffs ? 2 : 0;
   if (ev0) (void)hipEventRecord(ev0, s);
   if (p.key32) {
-    hipLaunchKernelGGL(k32, dim3(resident_grid(occ, v, k32, p.lds_range, lds)), dim3(kWG), lds, s, p);
+    hipLaunchKernelGGL(k32, dim3(resident_grid(occ, dev, v, k32, p.lds_range, lds)), dim3(kWG), lds, s, p);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (ev1) (void)hipEventRecord(ev1, s);
     // units whose lambda could saturate the 32-bit cost field (none in
     // practice) were planned into the 64-bit list: a small grid drains it
     if (!p.no64) hipLaunchKernelGGL(k64, dim3(64), dim3(kWG), lds, s, p);
   } else {
-    hipLaunchKernelGGL(k64, dim3(resident_grid(occ, v + 1, k64, p.lds_range, lds)), dim3(kWG), lds, s, p);
+    hipLaunchKernelGGL(k64, dim3(resident_grid(occ, dev, v + 1, k64, p.lds_range, lds)), dim3(kWG), lds, s, p);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (ev1) (void)hipEventRecord(ev1, s);
   }

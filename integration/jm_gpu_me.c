@@ -36,13 +36,31 @@
 #include "jmme.h"
 
 extern distblk __real_sub_pel_motion_estimation(Macroblock *, MotionVector *, MEBlock *, distblk, int *);
+extern distblk __real_full_search_motion_estimation(Macroblock *, MotionVector *, MEBlock *, distblk, int);
+extern distblk __real_fast_full_search_motion_estimation(Macroblock *, MotionVector *, MEBlock *, distblk, int);
+extern void __real_setup_fast_full_search(Macroblock *, MEBlock *, int);
 
 extern void get_neighbors(Macroblock *currMB, PixelPos *block, int mb_x, int mb_y, int blockshape_x);
 
 static jmme_ctx *g_me = NULL;
-static int g_frame = -1000000;          /* p_Vid->frame_no of the uploaded planes */
-static int g_ref_up[2][32];              /* (list, ref) uploaded for g_frame */
-static long long g_calls = 0;
+static long long g_calls = 0, g_cpu_calls = 0;
+
+/* What the uploaded planes and every cached answer belong to.  frame_no alone
+ * does not identify a coded picture: MVC view 1 shares view 0's frame_no with
+ * another pCurImg, and RDPictureDecision codes one frame again (rd_pass 1, 2)
+ * with other reference lists or weights.  So the current plane is keyed on
+ * (frame_no, pCurImg, view_id, structure, rd_pass) and each (list, ref) slot on
+ * the StorablePicture* bound to it (currSlice->listX[list + list_offset][ref]).
+ * Any change bumps a generation; the caches of a slot are valid only for the
+ * generation its picture was uploaded in. */
+typedef struct pic_key {
+  int frame_no, view_id, structure, rd_pass;
+  imgpel **cur;
+} pic_key;
+static pic_key g_pic = {-1000000, -1, -1, -1, NULL};
+static StorablePicture *g_ref_pic[2][32];  /* picture uploaded into each slot (NULL: none) */
+static unsigned g_slot_gen[2][32];         /* generation of that upload */
+static unsigned g_gen = 0;
 
 static void fail_jm(const char *what)
 {
@@ -58,14 +76,23 @@ static void init_once(VideoParameters *p_Vid, InputParameters *p_Inp)
   jmme_config c;
   if (g_me) return;
   jmme_config_default(&c);
+  /* the adapter numbers macroblocks of a frame picture; field pictures and MBAFF
+   * pairs (other plane heights, list_offset 2..5) are not handled */
+  if (p_Inp->PicInterlace || p_Inp->MbInterlace)
+    error("jm_gpu_me: PicInterlace / MbInterlace are not supported by the GPU drop-in", 500);
   c.SourceWidth = p_Vid->width;
   c.SourceHeight = p_Vid->height;
   c.SearchMode = p_Inp->SearchMode[0];
-  c.SearchRange = p_Inp->search_range[0];
+  /* MVC: each view has its own SearchRange (configfile.h:62,539); the context
+   * must admit the larger one */
+  c.SearchRange = p_Inp->num_of_views > 1 ? imax(p_Inp->search_range[0], p_Inp->search_range[1])
+                                           : p_Inp->search_range[0];
   c.NumberReferenceFrames = p_Inp->num_ref_frames;
   c.DisableSubpelME = p_Inp->DisableSubpelME[0];
   c.RDOptimization = p_Inp->rdopt;
-  c.MEDistortionFPel = p_Inp->MEErrorMetric[F_PEL];
+  /* only SAD integer-pel searches reach the GPU (fs_on_cpu / ffs_on_cpu send
+   * SSE, SATD and weighted ones to JM's own code), so the context is a SAD one */
+  c.MEDistortionFPel = 0;
   c.MDDistortion = p_Inp->ModeDecisionMetric;
   c.EPZSSubPelGrid = p_Inp->EPZSSubPelGrid;
   c.RestrictSearchRange = p_Inp->full_search;
@@ -84,20 +111,53 @@ static void ensure_planes(Macroblock *currMB, int list, int ref)
   VideoParameters *p_Vid = currMB->p_Vid;
   Slice *currSlice = currMB->p_Slice;
   StorablePicture *pic;
+  pic_key k;
   init_once(p_Vid, currMB->p_Inp);
-  if (p_Vid->frame_no != g_frame) {
-    g_frame = p_Vid->frame_no;
-    memset(g_ref_up, 0, sizeof g_ref_up);
+  k.frame_no = p_Vid->frame_no;
+  k.view_id = p_Vid->view_id;
+  k.structure = p_Vid->structure;
+  k.rd_pass = p_Vid->rd_pass;
+  k.cur = p_Vid->pCurImg;
+  if (k.frame_no != g_pic.frame_no || k.view_id != g_pic.view_id || k.structure != g_pic.structure ||
+      k.rd_pass != g_pic.rd_pass || k.cur != g_pic.cur) {   /* another coded picture: every slot is stale */
+    g_pic = k;
+    memset(g_ref_pic, 0, sizeof g_ref_pic);
+    ++g_gen;
     if (jmme_upload_cur(g_me, (const jmme_imgpel *const *)p_Vid->pCurImg, p_Vid->width, p_Vid->height))
       fail_jm("jmme_upload_cur");
   }
   if (list < 0 || list > 1 || ref < 0 || ref >= 32) error("jm_gpu_me: reference index out of range", 500);
-  if (!g_ref_up[list][ref]) {
-    pic = currSlice->listX[list + currMB->list_offset][ref];
+  pic = currSlice->listX[list + currMB->list_offset][ref];
+  if (g_ref_pic[list][ref] != pic) {           /* first use, or the slot now names another picture */
     if (jmme_upload_ref(g_me, list, ref, (const jmme_imgpel *const *)pic->imgY, pic->size_x, pic->size_y))
       fail_jm("jmme_upload_ref");
-    g_ref_up[list][ref] = 1;
+    g_ref_pic[list][ref] = pic;
+    g_slot_gen[list][ref] = ++g_gen;
   }
+}
+
+/* JM's integer-pel metric for this block is not the plain SAD the GPU computes:
+ * SSE / SATD (MEDistortionFPel 1/2, lencod.c:782-796), the weighted variants
+ * (mv_search.c:741-755) or the on-the-fly ones (mv_search.c:456-473).  Full
+ * search calls mv_block->computePredFPel, so that pointer decides. */
+static int fs_on_cpu(const MEBlock *mv_block)
+{
+  return mv_block->computePredFPel != computeSAD || mv_block->ChromaMEEnable;
+}
+
+/* setup_fast_full_search builds its surface with its own rule
+ * (me_fullfast.c:274,294-295): squared differences for MEDistortionFPel 1 and
+ * weighted samples when weighted prediction and UseWeightedReferenceME are on */
+static int ffs_on_cpu(Macroblock *currMB, const MEBlock *mv_block)
+{
+  VideoParameters *p_Vid = currMB->p_Vid;
+  InputParameters *p_Inp = currMB->p_Inp;
+  Slice *currSlice = currMB->p_Slice;
+  int apply_weights = ((p_Vid->active_pps->weighted_pred_flag &&
+                        (currSlice->slice_type == P_SLICE || currSlice->slice_type == SP_SLICE)) ||
+                       (p_Vid->active_pps->weighted_bipred_idc && currSlice->slice_type == B_SLICE)) &&
+                      p_Inp->UseWeightedReferenceME;
+  return p_Inp->MEErrorMetric[F_PEL] != 0 || apply_weights || mv_block->ChromaMEEnable;
 }
 
 /* ---- speculative batching of full-search calls ----------------------------
@@ -130,7 +190,7 @@ typedef struct spec_ent {
 #define KHYP 4                     /* guesses per (macroblock, partition) */
 static spec_ent *g_spec[2][32];    /* KHYP cached (inputs -> result) per (macroblock, slot) */
 static spec_ent *g_seen[2][32];    /* the inputs each (macroblock, slot) was really searched with */
-static int g_spec_frame[2][32];
+static unsigned g_spec_gen[2][32]; /* g_slot_gen the cached guesses belong to */
 static int g_spec_end[2][32];      /* first macroblock past the last batch */
 static int g_batch = 64, g_speculate = -1, g_mbs_x = 0, g_n_mb = 0;
 static long long g_hits = 0, g_batches = 0;
@@ -151,12 +211,12 @@ static spec_ent *spec_table(VideoParameters *p_Vid, int list, int ref)
     g_spec[list][ref] = (spec_ent *)calloc((size_t)g_n_mb * JMME_NSLOT * KHYP, sizeof(spec_ent));
     g_seen[list][ref] = (spec_ent *)calloc((size_t)g_n_mb * JMME_NSLOT, sizeof(spec_ent));
     if (!g_spec[list][ref] || !g_seen[list][ref]) error("jm_gpu_me: out of memory", 500);
-    g_spec_frame[list][ref] = -1000000;
+    g_spec_gen[list][ref] = 0;
   }
-  if (g_spec_frame[list][ref] != p_Vid->frame_no) {       /* new picture: forget every guess */
+  if (g_spec_gen[list][ref] != g_slot_gen[list][ref]) {   /* other planes: forget every guess */
     for (i = 0; i < g_n_mb * JMME_NSLOT * KHYP; i++) g_spec[list][ref][i].valid = 0;
     for (i = 0; i < g_n_mb * JMME_NSLOT; i++) g_seen[list][ref][i].valid = 0;
-    g_spec_frame[list][ref] = p_Vid->frame_no;
+    g_spec_gen[list][ref] = g_slot_gen[list][ref];
     g_spec_end[list][ref] = 0;
   }
   return g_spec[list][ref];
@@ -328,6 +388,10 @@ distblk __wrap_full_search_motion_estimation(Macroblock *currMB, MotionVector *p
   jmme_mv pred = {pred_mv->mv_x, pred_mv->mv_y};
   jmme_mv mv = {mv_block->mv[list].mv_x, mv_block->mv[list].mv_y};   /* centre in */
   distblk cost;
+  if (fs_on_cpu(mv_block)) {
+    ++g_cpu_calls;
+    return __real_full_search_motion_estimation(currMB, pred_mv, mv_block, min_mcost, lambda_factor);
+  }
   ensure_planes(currMB, list, ref);
   ++g_calls;
   if (speculating()) {
@@ -362,6 +426,10 @@ void __wrap_setup_fast_full_search(Macroblock *currMB, MEBlock *mv_block, int li
   int search_range = ff->max_search_range[list][ref] << 2;
   PixelPos block[4];
   MotionVector pmv, *c = &ff->search_center[list][ref];
+  if (ffs_on_cpu(currMB, mv_block)) {          /* JM's own surface for JM's own search */
+    __real_setup_fast_full_search(currMB, mv_block, list);
+    return;
+  }
   get_neighbors(currMB, block, 0, 0, 16);
   currMB->GetMVPredictor(currMB, block, &pmv, ref, p_Vid->enc_picture->mv_info, list, 0, 0, 16, 16);
   c->mv_x = (short)(((pmv.mv_x + 2) >> 2) * 4);              /* JM_INT_DIVIDE (defines.h:44) */
@@ -384,6 +452,10 @@ distblk __wrap_fast_full_search_motion_estimation(Macroblock *currMB, MotionVect
   int list = mv_block->list, ref = mv_block->ref_idx;
   jmme_mv pred = {pred_mv->mv_x, pred_mv->mv_y}, centre, mv;
   distblk cost;
+  if (ffs_on_cpu(currMB, mv_block)) {
+    ++g_cpu_calls;
+    return __real_fast_full_search_motion_estimation(currMB, pred_mv, mv_block, min_mcost, lambda_factor);
+  }
   if (!ff->search_setup_done[list][ref]) currMB->p_SetupFastFullPelSearch(currMB, mv_block, list);
   centre.mv_x = ff->search_center[list][ref].mv_x;
   centre.mv_y = ff->search_center[list][ref].mv_y;
@@ -435,7 +507,7 @@ typedef struct sp_ent {
 } sp_ent;
 
 static sp_ent *g_sp[2][32];
-static int g_sp_frame[2][32];
+static unsigned g_sp_gen[2][32];   /* g_slot_gen the cached refinements belong to */
 static long long g_sp_calls = 0, g_sp_hits = 0, g_sp_batches = 0, g_sp_cpu = 0;
 static jmme_subpel_req *g_sreq = NULL;
 static jmme_block_res *g_sres = NULL;
@@ -585,12 +657,12 @@ distblk __wrap_sub_pel_motion_estimation(Macroblock *currMB, MotionVector *pred_
   if (!g_sp[list][ref]) {
     g_sp[list][ref] = (sp_ent *)calloc((size_t)g_n_mb * JMME_NSLOT * SPK, sizeof(sp_ent));
     if (!g_sp[list][ref]) error("jm_gpu_me: out of memory", 500);
-    g_sp_frame[list][ref] = -1000000;
+    g_sp_gen[list][ref] = 0;
   }
   tab = g_sp[list][ref];
-  if (g_sp_frame[list][ref] != p_Vid->frame_no) {
+  if (g_sp_gen[list][ref] != g_slot_gen[list][ref]) {
     for (i = 0; i < g_n_mb * JMME_NSLOT * SPK; i++) tab[i].valid = 0;
-    g_sp_frame[list][ref] = p_Vid->frame_no;
+    g_sp_gen[list][ref] = g_slot_gen[list][ref];
   }
   mb = (mv_block->pos_y >> 4) * g_mbs_x + (mv_block->pos_x >> 4);
   s = jmme_slot(mv_block->blocktype, (mv_block->pos_x & 15) >> 2, (mv_block->pos_y & 15) >> 2);
@@ -614,11 +686,12 @@ distblk __wrap_sub_pel_motion_estimation(Macroblock *currMB, MotionVector *pred_
 static void report(void) __attribute__((destructor));
 static void report(void)
 {
-  if (g_me) {
+  if (g_me || g_cpu_calls) {
     fprintf(stderr, "jm_gpu_me: %lld integer-pel searches on the GPU (libjmme): %lld from %lld speculative "
-                    "batches, the rest one call each\n", g_calls, g_hits + g_batches, g_batches);
+                    "batches, the rest one call each; %lld on the CPU (non-SAD or weighted metric)\n",
+            g_calls, g_hits + g_batches, g_batches, g_cpu_calls);
     fprintf(stderr, "jm_gpu_me: %lld sub-pel refinements: %lld cached, %lld batches, %lld on the CPU\n",
             g_sp_calls, g_sp_hits, g_sp_batches, g_sp_cpu);
-    jmme_destroy(g_me);
+    if (g_me) jmme_destroy(g_me);
   }
 }

@@ -96,6 +96,52 @@ def test_lencod_with_gpu_me_is_byte_identical(gpu, w, h, frames, params, specula
             assert m and int(m.group(1)) > 0 and int(m.group(4)) == 0, r.stderr[-500:]
 
 
+@pytest.mark.parametrize("w,h,frames,params,cpu_integer", [
+    # SATD / SSE integer-pel metrics: JM's own search (fs_on_cpu / ffs_on_cpu), sub-pel still on the GPU
+    (176, 144, 3, {"SearchMode": -1, "SearchRange": 16, "RDOptimization": 0, "NumberReferenceFrames": 1,
+                   "MEDistortionFPel": 2, "DisableSubpelME": 0, "MEDistortionQPel": 2, "MDDistortion": 2}, "all"),
+    (176, 144, 3, {"SearchMode": 0, "SearchRange": 16, "RDOptimization": 1, "NumberReferenceFrames": 1,
+                   "MEDistortionFPel": 1}, "all"),
+    # weighted prediction with weighted reference ME: weighted pictures on the CPU, the others on the GPU
+    (176, 144, 4, {"SearchMode": -1, "SearchRange": 16, "RDOptimization": 0, "NumberReferenceFrames": 2,
+                   "ProfileIDC": 77, "WeightedPrediction": 1, "UseWeightedReferenceME": 1,
+                   "DisableSubpelME": 0, "MEDistortionQPel": 0}, "some"),
+    (176, 144, 4, {"SearchMode": 0, "SearchRange": 16, "RDOptimization": 1, "NumberReferenceFrames": 2,
+                   "ProfileIDC": 77, "WeightedPrediction": 1, "UseWeightedReferenceME": 1}, "some"),
+    # RDPictureDecision codes each frame again (rd_pass 1, 2) with other lists / QPs: the planes
+    # and cached answers are keyed on the coded picture, not on frame_no
+    (176, 144, 4, {"SearchMode": -1, "SearchRange": 16, "RDOptimization": 0, "NumberReferenceFrames": 2,
+                   "RDPictureDecision": 1, "DisableSubpelME": 0, "MEDistortionQPel": 0}, "none"),
+    (176, 144, 5, {"SearchMode": 0, "SearchRange": 16, "RDOptimization": 1, "NumberReferenceFrames": 2,
+                   "NumberBFrames": 1, "ProfileIDC": 77, "RDPictureDecision": 1, "DisableSubpelME": 0,
+                   "MEDistortionQPel": 0}, "none"),
+])
+def test_lencod_metric_and_picture_rules(gpu, w, h, frames, params, cpu_integer):
+    """configurations the GPU search cannot serve go to JM's own integer-pel code (and
+    are counted); re-coded pictures re-key the uploads.  Bitstreams stay byte-identical."""
+    if not (os.path.exists(STOCK) and os.path.exists(GPU)):
+        pytest.fail("lencod builds missing: run `make -C oracle ref && make -C integration` in the build container")
+    from jmme import synth
+    with tempfile.TemporaryDirectory() as d:
+        yuv = os.path.join(d, "in.yuv")
+        seq = synth.luma_sequence(w, h, frames, seed=w + 7 * frames, gmv=(2, 1))
+        # a brightness ramp so that weighted prediction is chosen for some pictures
+        seq = np.stack([np.clip(f.astype(np.int32) + 6 * i, 0, 255).astype(np.uint8) for i, f in enumerate(seq)])
+        synth.write_yuv420(yuv, seq)
+        ref264, refrec, _ = _encode(STOCK, d, "cpu", yuv, w, h, frames, params)
+        gpu264, gpurec, r = _encode(GPU, d, "gpu", yuv, w, h, frames, params)
+        assert (gpu264, gpurec) == (ref264, refrec)
+        m = re.search(r"(\d+) integer-pel searches on the GPU .*; (\d+) on the CPU", r.stderr)
+        assert m, r.stderr[-500:]
+        on_gpu, on_cpu = int(m.group(1)), int(m.group(2))
+        if cpu_integer == "all":
+            assert on_gpu == 0 and on_cpu > 0, r.stderr[-500:]
+        elif cpu_integer == "none":
+            assert on_gpu > 0 and on_cpu == 0, r.stderr[-500:]
+        else:
+            assert on_gpu > 0 and on_cpu > 0, r.stderr[-500:]
+
+
 def test_lencod_720p_ffs_subpel_speculative(gpu):
     """a 720p P picture (3600 macroblocks): batches grow to their cap and the four-guess
     cache is exercised at scale; fast full search + SATD sub-pel, JM's defaults"""
