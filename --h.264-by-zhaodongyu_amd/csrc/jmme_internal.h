@@ -32,7 +32,10 @@ static_assert(sizeof(Item) == 48, "Item layout");
 constexpr int kItemChk00 = 1;     // slot 0 takes check_for_00 (me_fullsearch.c:61)
 constexpr int kItemPreseed = 2;   // FFS pos00 pre-seed (me_fullfast.c:640-648)
 
-constexpr uint32_t kMaxLambda32 = 28450;   // 32*65280 + lambda*74 < 2^22: 22-bit cost field exact
+// 32-bit keys are cost << 11 | rank >> 2 (21-bit cost field).  Every partition
+// but 16x16 stays exact while 32*32640 + lambda*74 < 2^21; the 16x16 key
+// saturates instead (and an all-saturated 16x16 is searched again exactly).
+constexpr uint32_t kMaxLambda32 = 14225;
 
 struct KParams {
   const uint8_t *cur;                 // 8-bit current picture

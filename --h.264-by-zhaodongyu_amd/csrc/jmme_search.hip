@@ -29,17 +29,23 @@
 //     global_load_lds (no VGPRs held), so the sweep hides the fetch latency;
 //   * window in LDS as "word[y][x] = pels x..x+3": every SAD row read is an
 //     aligned ds_read_b32;
-//   * a thread takes a vertical PAIR of search positions: the 17 reference
-//     rows they need are read once, the 2 x 16 4x4 SADs formed with v_sad_u8
-//     (the current MB row is a broadcast ds_read_b128), summed to the 41
-//     partition SADs, and a running minimum per partition kept in registers;
-//   * key (fast path): 32 bits = cost << 10 | rank >> 3.  cost < 2^22 holds for
-//     every partition while lambda <= kMaxLambda32, so one v_lshl_add_u32 and
-//     one v_min_u32 update a partition.  The 3 dropped rank bits are recovered
-//     exactly afterwards: the winner's rank lies in [8c, 8c+8), and those <= 8
-//     positions are re-evaluated per partition (refine pass);
-//   * key (exact fallback): 64 bits = cost << 32 | rank, for ranges > 44 or
-//     huge lambdas.
+//   * the current MB lives in SGPRs (64 dwords, read once per item): every
+//     v_sad uses it as its scalar operand, so the LDS only serves the window;
+//   * a thread takes a vertical TRIPLE of search positions: the 18 reference
+//     rows they need are read once and feed 3 x 16 4x4 SAD chains;
+//   * key (fast path): 32 bits = cost << 11 | rank >> 2, built without a
+//     shift per partition: a 4x4 chain starts from K(pos) = mvcost << 11 |
+//     rank >> 2 and v_sad_hi_u8 adds SAD << 16 (= (32 * SAD) << 11), so the
+//     chain ends on the 4x4 key; a larger partition's key is a + b - K (one
+//     v_add3_u32); the 16x16 key, whose SAD may reach 65280, is a saturating
+//     add.  One v_min_u32 per partition and position folds it.  The 2 dropped
+//     rank bits are recovered exactly afterwards: the winner's rank lies in
+//     [4c, 4c+4), and those <= 4 positions are re-evaluated per partition;
+//   * JM's special (0,0) candidate (check_for_00's discount, FFS's pre-seed
+//     with rank 0) is evaluated once per item after the sweep, not per position;
+//   * key (exact fallback): 64 bits = cost << 32 | rank, for ranges > 44,
+//     huge lambdas, FFS windows the GetMaxMVD gate cuts, and a 16x16 whose
+//     every key saturated.
 #include <hip/hip_runtime.h>
 #include <type_traits>
 #include "jmme.h"
@@ -53,8 +59,8 @@ namespace {
 constexpr int kNS = JMME_NSLOT;
 constexpr int kWaves = kWG / 64;
 constexpr unsigned long long kAll = (1ull << kNS) - 1;
-constexpr int kCostShift = 10;             // key32 = cost << 10 | rank >> 3
-constexpr int kRankDrop = 3;
+constexpr int kCostShift = 11;             // key32 = cost << 11 | rank >> 2
+constexpr int kRankDrop = 2;
 constexpr int kCand = 1 << kRankDrop;      // refine candidates per partition
 constexpr int kPlanWaves = 16;             // plan kernel: units per workgroup
 constexpr int kRed1 = (kNS + 3) / 4 * 2;      // reduce: registers after the permlane32 level (22)
@@ -93,19 +99,42 @@ struct Lds {
   uint32_t *cur;            // 64 words: MB row r, column group c at [r*4+c] (static LDS)
   unsigned long long *red;  // kWaves x 41 reduction scratch
   uint32_t *match;          // 41 x kCand refine flags
+  uint4 *tx, *ty;           // per-item position tables (2R+1 each), see build_tabs
+  uint32_t *spec;           // 16 4x4 SADs at the special (0,0) candidate
+  unsigned long long *fb;   // exact 16x16 result of the saturation fallback
 };
+
+// one layout for the kernel (carve) and the host (items_lds_bytes)
+struct LdsPlan { size_t words, raw, red, match, tx, ty, spec, fb, total; };
+__host__ __device__ inline LdsPlan lds_plan(int R) {
+  LdsPlan q;
+  const int rows = 2 * R + 16, wp = (2 * R + 13) | 1, d = 2 * R + 1;
+  size_t off = 0;
+  auto take = [&](size_t bytes) { const size_t at = off; off = (off + bytes + 15) & ~(size_t)15; return at; };
+  q.words = take((size_t)rows * wp * 4);
+  q.raw = take(((size_t)rows * raw_row_dwords(R) + kRawExtra) * 4);
+  q.red = take((size_t)kWaves * kNS * 8);
+  q.match = take((size_t)kNS * kCand * 4);
+  q.tx = take((size_t)d * 16);
+  q.ty = take((size_t)d * 16);
+  q.spec = take(16 * 4);
+  q.fb = take(kWaves * 8);
+  q.total = off;
+  return q;
+}
 
 __device__ __forceinline__ Lds carve(unsigned char *smem, int R) {
   Lds L;
-  const int rows = 2 * R + 16;
+  const LdsPlan q = lds_plan(R);
   L.wp = (2 * R + 13) | 1;
-  size_t off = 0;
-  L.words = reinterpret_cast<uint32_t *>(smem + off); off += (size_t)rows * L.wp * 4;
-  off = (off + 15) & ~(size_t)15;
-  L.raw = reinterpret_cast<uint32_t *>(smem + off);   off += ((size_t)rows * raw_row_dwords(R) + kRawExtra) * 4;
-  off = (off + 15) & ~(size_t)15;
-  L.red = reinterpret_cast<unsigned long long *>(smem + off); off += kWaves * kNS * 8;
-  L.match = reinterpret_cast<uint32_t *>(smem + off);    off += kNS * kCand * 4;
+  L.words = reinterpret_cast<uint32_t *>(smem + q.words);
+  L.raw = reinterpret_cast<uint32_t *>(smem + q.raw);
+  L.red = reinterpret_cast<unsigned long long *>(smem + q.red);
+  L.match = reinterpret_cast<uint32_t *>(smem + q.match);
+  L.tx = reinterpret_cast<uint4 *>(smem + q.tx);
+  L.ty = reinterpret_cast<uint4 *>(smem + q.ty);
+  L.spec = reinterpret_cast<uint32_t *>(smem + q.spec);
+  L.fb = reinterpret_cast<unsigned long long *>(smem + q.fb);
   return L;
 }
 
@@ -262,8 +291,10 @@ __device__ __forceinline__ void update_slots(const uint32_t (&ps)[kNS], const Gr
 #pragma unroll
     for (int s = 0; s < kNS; ++s) {
       if (!ALL && !((g.gmask >> s) & 1)) continue;
-      // cost<<10 | rank>>3  ==  (SAD << 15) + ((mvc << 10) | rank >> 3)
-      const uint32_t k = (ps[s] << (5 + kCostShift)) + (s == 0 ? k32_0 : k32);
+      // cost<<11 | rank>>2  ==  (SAD << 16) + ((mvc << 11) | rank >> 2); the
+      // 16x16 SAD may reach 65280, so its key saturates instead of wrapping
+      const uint32_t k = s == 0 ? __builtin_elementwise_add_sat(ps[0] << (5 + kCostShift), k32_0)
+                                : (ps[s] << (5 + kCostShift)) + k32;
       const uint32_t kk = FFS ? (c.ok ? k : ~0u) : k;
       best[s] = min((uint32_t)best[s], kk);
     }
@@ -470,6 +501,214 @@ __device__ __forceinline__ void expand(const KParams &p, const Item &it, const L
   }
 }
 
+// ------------------------------------------------------- v5 fast sweep --
+// Is item `it` served by the v5 sweep?  32-bit keys, a sub-window of at least
+// 3x3, and (FFS) no position of it cut by the GetMaxMVD gate (me_fullfast.c:663):
+// the window's farthest vector from the predictor passes, so all do.
+template <bool KEY32, bool FFS>
+__device__ __forceinline__ bool item_fast(const KParams &p, const Item &it) {
+  if (!KEY32 || it.rs < 1) return false;
+  if (!FFS) return true;
+  const int ex = max(abs(it.cqx - 4 * it.rs - it.px), abs(it.cqx + 4 * it.rs - it.px));
+  const int ey = max(abs(it.cqy - 4 * it.rs - it.py), abs(it.cqy + 4 * it.rs - it.py));
+  return max(ex, ey) < p.max_mvd - 1;
+}
+
+// Position tables of one item (LDS, built before its sweep).  For a window
+// offset o in [-rs, rs] (entry o + rs):
+//   tx[] = { lambda * mvbits(cqx + 4o - px) << 11, G', |o|, 2o }
+//   ty[] = { lambda * mvbits(cqy + 4o - py) << 11, F', |o|, 2o }
+// The spiral rank (spiral_index, jmme_common.h) splits by the side of the ring:
+//   |oy| >  |ox| (top/bottom row of ring |oy|):   rank = F(oy) + 2 ox,
+//       F(o) = 4a^2 - 2a - 1 + (o > 0), a = |o|
+//   |oy| <= |ox| (left/right column of ring |ox|): rank = G(ox) + 2 oy,
+//       G(o) = 4a^2 + 2a - 1 + (o > 0), G(0) = 0
+// and F' = F + FFS, G' = G + FFS (FFS ranks are the spiral index + 1; rank 0
+// is the pre-seeded (0,0), me_fullfast.c:650-657).
+template <bool FFS>
+__device__ __forceinline__ void build_tabs(const Item &it, const Lds &L) {
+  const int tid = opaque_tid();
+  const int rs = it.rs, D = 2 * rs + 1;
+  for (int i = tid; i < 2 * D; i += kWG) {
+    const bool y = i >= D;
+    const int j = y ? i - D : i, o = j - rs, a = abs(o);
+    const int cq = y ? it.cqy : it.cqx, pp = y ? it.py : it.px;
+    const uint32_t m = ((uint32_t)it.lam * (uint32_t)mvbits(cq + 4 * o - pp)) << kCostShift;
+    int f = y ? 4 * a * a - 2 * a - 1 + (o > 0) : (a == 0 ? 0 : 4 * a * a + 2 * a - 1 + (o > 0));
+    f += FFS ? 1 : 0;
+    (y ? L.ty : L.tx)[j] = make_uint4(m, (uint32_t)f, (uint32_t)a, (uint32_t)(2 * o));
+  }
+}
+
+// The 41 partition keys of one position from its 16 4x4 keys (SAD << 16 + K
+// each): a sum of two keys minus K is the key of the union (exact modulo 2^32
+// because every true key is < 2^32 under kMaxLambda32); the 16x16 key
+// saturates.  The sums are JM's (update_full_search_large_blocks,
+// me_fullfast.c:196-260).
+__device__ __forceinline__ uint32_t add3(uint32_t a, uint32_t b, uint32_t c) {
+  // one v_add3_u32 (the compiler would split a + b - K into an add and a sub)
+  uint32_t d;
+  asm("v_add3_u32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+
+__device__ __forceinline__ void partition_keys(const uint32_t (&a)[16], uint32_t K, uint32_t (&ps)[kNS]) {
+  const uint32_t nk = 0u - K;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) ps[25 + k] = a[k];                                                    // 4x4
+#pragma unroll
+  for (int by = 0; by < 4; ++by)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) ps[9 + by * 2 + h] = add3(a[by * 4 + 2 * h], a[by * 4 + 2 * h + 1], nk);      // 8x4
+#pragma unroll
+  for (int v = 0; v < 2; ++v)
+#pragma unroll
+    for (int bx = 0; bx < 4; ++bx) ps[17 + v * 4 + bx] = add3(a[(2 * v) * 4 + bx], a[(2 * v + 1) * 4 + bx], nk);  // 4x8
+#pragma unroll
+  for (int v = 0; v < 2; ++v)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) ps[5 + v * 2 + h] = add3(ps[9 + (2 * v) * 2 + h], ps[9 + (2 * v + 1) * 2 + h], nk);  // 8x8
+  ps[3] = add3(ps[5], ps[7], nk);
+  ps[4] = add3(ps[6], ps[8], nk);   // 8x16
+  ps[1] = add3(ps[5], ps[6], nk);
+  ps[2] = add3(ps[7], ps[8], nk);   // 16x8
+  ps[0] = __builtin_elementwise_add_sat(ps[1] + nk, ps[2]);   // 16x16: S_top << 16, + S_bot << 16 + K
+}
+
+// The v5 sweep of the sub-window [-rs, rs]^2 (rs >= 1) of the staged window.
+// A task is a vertical triple of positions (x, y..y+2); the 18 window rows
+// they need are read once; row r meets MB row r - j of position j.  The
+// current MB comes from SGPRs (cs), so the only LDS traffic is the window.
+__device__ __forceinline__ void sweep_v5(const Lds &L, const uint32_t (&cs)[64], int R, int rs,
+                                         uint32_t (&best)[kNS]) {
+  const int tid = opaque_tid();
+  const int D = 2 * rs + 1;
+  const int DT = (D + 2) / 3;            // triples per column (the last one shifted up)
+  const int ntask = D * DT;
+  const int off = R - rs;
+  const int qstep = kWG / D, rstep = kWG - qstep * D;
+  int tx = tid % D, tq = tid / D;        // task column, triple row
+  const uint32_t rowb = 4u * (uint32_t)L.wp;
+  for (int t = tid; t < ntask; t += kWG) {
+    const int y0 = min(3 * tq, D - 3);
+    uint32_t K[3];
+    {
+      const u32x4 cx = ds_read_b128(lds_addr(L.tx) + 16u * (uint32_t)tx);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const u32x4 cy = ds_read_b128(lds_addr(L.ty) + 16u * (uint32_t)(y0 + j));
+        const uint32_t rk = cy.z > cx.z ? cy.y + cx.w : cx.y + cy.w;
+        K[j] = cx.x + cy.x + (rk >> kRankDrop);
+      }
+    }
+    uint32_t a[3][16];
+    const uint32_t wrow = lds_addr(L.words) + 4u * (uint32_t)((off + y0) * L.wp + off + tx);
+    u32x2 n01 = ds_read2_0_4(wrow), n23 = ds_read2_8_12(wrow);
+#pragma unroll
+    for (int r = 0; r < 18; ++r) {
+      const u32x2 w01 = n01, w23 = n23;
+      if (r < 17) {
+        const uint32_t ad = wrow + (uint32_t)(r + 1) * rowb;
+        n01 = ds_read2_0_4(ad);
+        n23 = ds_read2_8_12(ad);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const int mr = r - j;
+        if (mr < 0 || mr > 15) continue;
+        const int b = (mr >> 2) * 4;
+        const bool first = (mr & 3) == 0;
+        a[j][b + 0] = __builtin_amdgcn_sad_hi_u8(w01.x, cs[mr * 4 + 0], first ? K[j] : a[j][b + 0]);
+        a[j][b + 1] = __builtin_amdgcn_sad_hi_u8(w01.y, cs[mr * 4 + 1], first ? K[j] : a[j][b + 1]);
+        a[j][b + 2] = __builtin_amdgcn_sad_hi_u8(w23.x, cs[mr * 4 + 2], first ? K[j] : a[j][b + 2]);
+        a[j][b + 3] = __builtin_amdgcn_sad_hi_u8(w23.y, cs[mr * 4 + 3], first ? K[j] : a[j][b + 3]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      uint32_t ps[kNS];
+      partition_keys(a[j], K[j], ps);
+#pragma unroll
+      for (int s = 0; s < kNS; ++s) best[s] = min(best[s], ps[s]);
+    }
+    tx += rstep;
+    tq += qstep;
+    if (tx >= D) { tx -= D; ++tq; }
+  }
+}
+
+// JM's special (0,0) candidate, once per item after the v5 sweep: FS
+// check_for_00 (slot 0 at (0,0) costs mvcost - 16*lambda, me_fullsearch.c:61,
+// 78-82) and the FFS pre-seed (every partition, rank 0, me_fullfast.c:650-657).
+// Its exact key joins the reduced minima in L.red before the refine (the
+// sweep's own key for that position is never below it).
+template <bool FFS>
+__device__ __forceinline__ void special_00(const GroupCtx &g, const Lds &L) {
+  const int ox = -(g.cqx >> 2), oy = -(g.cqy >> 2);   // the (0,0) vector as a window offset
+  const MvCost mc = mv_cost<FFS>(0, 0, g.px, g.py, g.lam, g.max_mvd);
+  const bool inside = abs(ox) <= g.R && abs(oy) <= g.R;
+  const bool on = FFS ? (g.preseed && inside && mc.ok) : (g.chk00 && (g.gmask & 1) && inside);
+  if (!on) return;
+  const int tid = opaque_tid();
+  if (tid < 16) {
+    const int bx = tid & 3, by = tid >> 2;
+    const uint32_t *w = L.words + (oy + g.R + 4 * by) * L.wp + ox + g.R + 4 * bx;
+    uint32_t sad = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sad = __builtin_amdgcn_sad_u8(w[r * L.wp], L.cur[(4 * by + r) * 4 + bx], sad);
+    L.spec[tid] = sad;
+  }
+  __syncthreads();
+  if (tid < kNS && ((g.gmask >> tid) & 1) && (FFS || tid == 0)) {
+    const SlotGeom gm = slot_geom(tid);
+    uint32_t sad = 0;
+    for (int j = 0; j < gm.h; ++j)
+      for (int i = 0; i < gm.w; ++i) sad += L.spec[(gm.by + j) * 4 + gm.bx + i];
+    const uint32_t mvc = FFS ? mc.mvc : check00_adjust(mc.mvc, g.lam, true);
+    const uint32_t rank = FFS ? 0u : (uint32_t)spiral_index_bl(ox, oy);
+    const uint32_t cost = (sad << 5) + mvc;
+    const uint32_t key = cost < (1u << (32 - kCostShift)) ? (cost << kCostShift) | (rank >> kRankDrop) : ~0u;
+    L.red[tid] = min((uint32_t)L.red[tid], key);
+  }
+  __syncthreads();
+}
+
+// Exact 16x16 search with 64-bit keys, for an item whose every 32-bit 16x16
+// key saturated (only possible when lambda * mvbits > 8160 and the 16x16 SADs
+// are near 65280).  Result: min over the waves' L.fb entries.
+template <bool FFS>
+__device__ __noinline__ void exact_16x16(const GroupCtx &g, const Lds &L) {
+  const int tid = opaque_tid(), lane = tid & 63, wave = tid >> 6;
+  const int R = g.R, D = 2 * R + 1;
+  unsigned long long best = ~0ull;
+  for (int i = tid; i < D * D; i += kWG) {
+    const int oyw = i / D, oxw = i - oyw * D, ox = oxw - R, oy = oyw - R;
+    const int candx = g.cqx + 4 * ox, candy = g.cqy + 4 * oy;
+    const bool is00 = candx == 0 && candy == 0;
+    const MvCost mc = mv_cost<FFS>(candx, candy, g.px, g.py, g.lam, g.max_mvd);
+    if (!pos_eligible<FFS>(g, mc.ok, max(abs(ox), abs(oy)), is00)) continue;
+    uint32_t sad = 0;
+    for (int r = 0; r < 16; ++r)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) sad = __builtin_amdgcn_sad_u8(L.words[(oyw + r) * L.wp + oxw + 4 * c], L.cur[r * 4 + c], sad);
+    const int sidx = spiral_index_bl(ox, oy);
+    const uint32_t rank = FFS ? ((g.preseed && is00) ? 0u : (uint32_t)sidx + 1u) : (uint32_t)sidx;
+    const uint32_t mvc = (!FFS && g.chk00) ? check00_adjust(mc.mvc, g.lam, is00) : mc.mvc;
+    const unsigned long long k = ((unsigned long long)((sad << 5) + mvc) << 32) | rank;
+    best = k < best ? k : best;
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const unsigned lo = __shfl_xor((unsigned)best, o, 64), hi = __shfl_xor((unsigned)(best >> 32), o, 64);
+    const unsigned long long x = ((unsigned long long)hi << 32) | lo;
+    best = x < best ? x : best;
+  }
+  if (lane == 0) L.fb[wave] = best;
+  __syncthreads();
+}
+
 template <bool KEY32, bool FFS>
 struct ItemStamps {
   unsigned long long wait = 0, expand = 0, sweep = 0, reduce = 0, refine = 0, out = 0;
@@ -477,7 +716,8 @@ struct ItemStamps {
 
 // sweep + reduce + refine + output of one item whose window is in L.words
 template <bool KEY32, bool FFS>
-__device__ __forceinline__ void search_item(const KParams &p, const Item &it, const Lds &L
+__device__ __forceinline__ void search_item(const KParams &p, const Item &it, const Lds &L, bool fast,
+                                            const uint32_t (&cs)[64]
 #ifdef JMME_STAMPS
                                             , unsigned long long &t_last, ItemStamps<KEY32, FFS> &st
 #endif
@@ -627,7 +867,11 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
   // every partition's minimum is tracked even when the group is a subset: the
   // slots outside gmask are simply never read back (one code path, no
   // per-partition masks in the loop)
-  sweep(std::integral_constant<bool, true>{});
+  if (KEY32 && fast) {
+    if constexpr (KEY32) sweep_v5(L, cs, R, g.rs, best);
+  } else {
+    sweep(std::integral_constant<bool, true>{});
+  }
   STAMP(st.sweep);
 
   // ---- workgroup reduction of this group's per-thread minima
@@ -685,6 +929,7 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
     L.red[tid] = k;   // wave 0's row now holds the group result
   }
   __syncthreads();
+  if (KEY32 && fast) special_00<FFS>(g, L);
   STAMP(st.reduce);
 
   // ---- refine (32-bit keys): recover the 3 rank bits the key dropped.
@@ -746,6 +991,9 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
     }
     __syncthreads();
   }
+  // every 32-bit 16x16 key saturated: search the 16x16 again with exact keys
+  const bool fb16 = KEY32 && (gmask & 1) && (uint32_t)L.red[0] == ~0u;
+  if (fb16) exact_16x16<FFS>(g, L);
   STAMP(st.refine);
 
   // ---- results of this group
@@ -756,7 +1004,16 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
     res.reserved = 0;
     uint32_t rank = 0, cost = 0;
     bool found = false;
-    if (KEY32) {
+    if (KEY32 && tid == 0 && fb16) {
+      unsigned long long kb = L.fb[0];
+#pragma unroll
+      for (int w = 1; w < kWaves; ++w) kb = L.fb[w] < kb ? L.fb[w] : kb;
+      if (kb != ~0ull) {
+        found = true;
+        rank = (uint32_t)(kb & 0x7fffffffu);
+        cost = (uint32_t)(kb >> 32);
+      }
+    } else if (KEY32) {
       const uint32_t key = (uint32_t)k;
       if (key != ~0u) {
         for (int j = 0; j < kCand && !found; ++j)
@@ -836,7 +1093,9 @@ __global__ __launch_bounds__(kWG, KEY32 ? JMME_WAVES_PER_EU : 2) void me_items_k
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     STAMP(st.wait);
+    const bool fast = it.gmask && item_fast<KEY32, FFS>(p, it);
     if (it.gmask) expand(p, it, L);
+    if (fast) build_tabs<FFS>(it, L);
     __syncthreads();
     if (p.debug_words && it.u == 0 && (it.gmask & dbg_slot)) {
       const Win w = win_of(p, it);
@@ -846,10 +1105,18 @@ __global__ __launch_bounds__(kWG, KEY32 ? JMME_WAVES_PER_EU : 2) void me_items_k
     // the raw buffer is free: start fetching the next item behind this sweep
     if (more) prefetch(p, nx, L);
     if (it.gmask) {
+      // the current MB into SGPRs: every v_sad of the v5 sweep takes it as
+      // its scalar operand
+      uint32_t cs[64];
+      {
+        const uint32_t v = L.cur[threadIdx.x & 63];
+#pragma unroll
+        for (int i = 0; i < 64; ++i) cs[i] = __builtin_amdgcn_readlane(v, i);
+      }
 #ifdef JMME_STAMPS
-      search_item<KEY32, FFS>(p, it, L, t_last, st);
+      search_item<KEY32, FFS>(p, it, L, fast, cs, t_last, st);
 #else
-      search_item<KEY32, FFS>(p, it, L);
+      search_item<KEY32, FFS>(p, it, L, fast, cs);
 #endif
     }
 #ifdef JMME_STAMPS
@@ -886,16 +1153,7 @@ int resident_grid(Occupancy &o, int dev, int variant, K kernel, int lds_range, s
 
 }  // namespace
 
-size_t items_lds_bytes(int R) {
-  const int rows = 2 * R + 16;
-  const int wp = (2 * R + 13) | 1;
-  size_t off = (size_t)rows * wp * 4;
-  off = (off + 15) & ~(size_t)15;
-  off += ((size_t)rows * raw_row_dwords(R) + kRawExtra) * 4;
-  off = (off + 15) & ~(size_t)15;
-  off += kWaves * kNS * 8 + kNS * kCand * 4;
-  return off;
-}
+size_t items_lds_bytes(int R) { return lds_plan(R).total; }
 
 hipError_t launch_search(const KParams &p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
   // occupancy per device: the caller (jmme_capi) has made the context's device current

@@ -221,6 +221,35 @@ def test_saturated_32bit_keys_take_the_64bit_path(gpu):
         assert (out[u, s]["mv_x"], out[u, s]["mv_y"], out[u, s]["cost"]) == (mv[i, 0], mv[i, 1], cost[i])
 
 
+@pytest.mark.parametrize("scene", ["flat", "inverted"])
+def test_saturated_16x16_keys_are_searched_exactly(scene, gpu):
+    """Lambdas just inside the 32-bit key range on pictures whose 16x16 SADs
+    reach (flat: equal) 65280: every 16x16 key of the sweep saturates, so the
+    16x16 result comes from the exact 64-bit re-search; the other partitions
+    stay on the 32-bit keys.  HIP == oracle on every partition."""
+    from jmme import FULL_SEARCH, MotionEstimator, synth
+    w, h, R = 176, 144, 8
+    rng = np.random.default_rng(17)
+    if scene == "flat":
+        cur = np.full((h, w), 255, np.uint8)
+        ref = np.zeros((h, w), np.uint8)
+    else:
+        ref = synth.luma_sequence(w, h, 1, seed=6)[0]
+        ref = np.where(ref > 127, 255, 0).astype(np.uint8)
+        cur = (255 - ref).astype(np.uint8)
+    req = _random_units(rng, w, h, 8, R)
+    req["blk"]["lambda"] = rng.integers(13000, 14226, size=req["blk"]["lambda"].shape)
+    with MotionEstimator({"SearchRange": R, "SearchMode": -1}) as me:
+        me.upload_cur(cur)
+        me.upload_ref(0, 0, ref)
+        out = me.search(FULL_SEARCH, req)
+    keys, mv, cost = _oracle_units(cur, ref, req)
+    got = np.array([(out[u, s]["mv_x"], out[u, s]["mv_y"], out[u, s]["cost"]) for u, s in keys])
+    exp = np.column_stack([mv[:, 0], mv[:, 1], cost])
+    bad = np.nonzero(np.any(got != exp, axis=1))[0]
+    assert len(bad) == 0, [(keys[i], got[i].tolist(), exp[i].tolist()) for i in bad[:5]]
+
+
 def test_requests_outside_contract_are_rejected(gpu):
     from jmme import FULL_SEARCH, JmmeError, MotionEstimator, MB_REQ, synth
     luma = synth.luma_sequence(176, 144, 2, seed=1)
