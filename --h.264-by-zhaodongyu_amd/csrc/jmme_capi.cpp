@@ -1198,12 +1198,12 @@ extern "C" jmme_distblk jmme_fast_full_search_block(jmme_ctx *ctx, int list, int
 extern "C" int jmme_debug_window(jmme_ctx *ctx, int mode, const jmme_mb_req *req, uint32_t *out, int max_words) {
   DevGuard dg_(ctx);
   // Test hook: run unit `req` (one unit) and return the first reference
-  // window it staged in LDS (rows x pitch words, word[y][x] = pels x..x+3).
+  // window it staged in LDS (rows x (2R+13) words, word[y][x] = pels x..x+3).
   if (!ctx) return fail("null ctx");
   if (validate(ctx, mode, req, 1)) return -1;
   if (ensure_units(ctx, 1)) return -1;
   const int R = ctx->cfg.SearchRange;
-  const int words = (2 * R + 16) * ((2 * R + 13) | 1);
+  const int words = (2 * R + 16) * (2 * R + 13);
   if (max_words < words) return fail("debug buffer needs %d words", words);
   uint32_t *d = nullptr;
   HIPCHK(hipMalloc(&d, (size_t)words * 4));

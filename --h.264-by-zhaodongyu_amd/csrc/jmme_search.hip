@@ -104,11 +104,15 @@ struct Lds {
   unsigned long long *fb;   // exact 16x16 result of the saturation fallback
 };
 
+// words per window row in LDS: the 2R+13 words a row needs, rounded up to the
+// expand's groups of 4 (it writes whole groups), odd for bank spread
+__host__ __device__ inline int words_pitch(int R) { return 4 * ((2 * R + 13 + 3) / 4) + 1; }
+
 // one layout for the kernel (carve) and the host (items_lds_bytes)
 struct LdsPlan { size_t words, raw, red, match, tx, ty, spec, fb, total; };
 __host__ __device__ inline LdsPlan lds_plan(int R) {
   LdsPlan q;
-  const int rows = 2 * R + 16, wp = (2 * R + 13) | 1, d = 2 * R + 1;
+  const int rows = 2 * R + 16, wp = words_pitch(R), d = 2 * R + 1;
   size_t off = 0;
   auto take = [&](size_t bytes) { const size_t at = off; off = (off + bytes + 15) & ~(size_t)15; return at; };
   q.words = take((size_t)rows * wp * 4);
@@ -126,7 +130,7 @@ __host__ __device__ inline LdsPlan lds_plan(int R) {
 __device__ __forceinline__ Lds carve(unsigned char *smem, int R) {
   Lds L;
   const LdsPlan q = lds_plan(R);
-  L.wp = (2 * R + 13) | 1;
+  L.wp = words_pitch(R);
   L.words = reinterpret_cast<uint32_t *>(smem + q.words);
   L.raw = reinterpret_cast<uint32_t *>(smem + q.raw);
   L.red = reinterpret_cast<unsigned long long *>(smem + q.red);
@@ -438,13 +442,18 @@ __device__ __forceinline__ void prefetch(const KParams &p, const Item &it, const
   const uint8_t *ref = p.refs[it.ref];
   const int total = w.wrows * w.nd;
   const int w4 = p.width >> 2, xq = w.xa >> 2;
-  for (int base = wave * 64; base < total; base += kWG) {
-    const int i = base + lane;
-    if (i < total) {
-      const int r = i / w.nd, d = i - r * w.nd;
-      const int gy = clampi(w.y0 + r, 0, p.height - 1);
-      const int pd = clampi(xq + d, 0, w4 - 1);
-      __builtin_amdgcn_global_load_lds(ref + (size_t)gy * p.pitch + 4 * pd, L.raw + base, 4, 0, 0);
+  // k = 64 / nd whole rows per wave instruction: lane l writes dword l of the
+  // instruction's LDS span, i.e. dword l % nd of row l / nd (rows dense, nd
+  // dwords each), so the per-lane column and row offset are fixed per item
+  const int k = 64 / w.nd;
+  const int dr = lane / w.nd, d = lane - dr * w.nd;
+  const bool act = dr < k;
+  const uint8_t *col = ref + 4 * clampi(xq + d, 0, w4 - 1);
+  for (int r = wave * k; r < w.wrows; r += kWaves * k) {
+    const int rr = r + dr;
+    if (act && rr < w.wrows) {
+      const int gy = clampi(w.y0 + rr, 0, p.height - 1);
+      __builtin_amdgcn_global_load_lds(col + (size_t)gy * p.pitch, L.raw + r * w.nd, 4, 0, 0);
     }
   }
   // behind the window: the current MB (wave 0)
@@ -456,47 +465,79 @@ __device__ __forceinline__ void prefetch(const KParams &p, const Item &it, const
 }
 
 // raw dwords -> words (word[y][x] = pels x..x+3 of the window)
+// inner window, byte shift SH of its first pel inside the first fetched dword:
+// words 4g..4g+3 of a row from its fetched dwords g..g+2 (rows r0, r0+rstep, ..;
+// the next row's dwords are read before this row's words are written)
+template <int SH>
+__device__ __forceinline__ void expand_inner(const uint32_t *src, uint32_t *dst, int nd, int wp, int wrows, int r0,
+                                             int rstep) {
+  int r = r0;
+  if (r >= wrows) return;
+  uint32_t d0 = src[r * nd], d1 = src[r * nd + 1], d2 = src[r * nd + 2];
+  for (;;) {
+    const int rn = r + rstep;
+    uint32_t e0 = 0, e1 = 0, e2 = 0;
+    if (rn < wrows) { e0 = src[rn * nd]; e1 = src[rn * nd + 1]; e2 = src[rn * nd + 2]; }
+    uint32_t *o = dst + r * wp;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int b = k + SH;   // byte offset of word 4g+k from dword g (0..6), compile-time
+      o[k] = b < 4 ? __builtin_amdgcn_alignbyte(d1, d0, b & 3) : __builtin_amdgcn_alignbyte(d2, d1, b & 3);
+    }
+    if (rn >= wrows) break;
+    r = rn; d0 = e0; d1 = e1; d2 = e2;
+  }
+}
+
 __device__ __forceinline__ void expand(const KParams &p, const Item &it, const Lds &L) {
   const int tid = opaque_tid();
   const Win w = win_of(p, it);
-  const int n = w.wrows * w.wpr;
   const uint32_t *tail = L.raw + w.wrows * w.nd;
   if (tid < 64) L.cur[tid] = tail[tid];
+  // a thread makes 4 consecutive words 4g..4g+3 of rows r0, r0+rstep, ...
+  // (L.wp >= 4*ng: the words past wpr of the last group are scratch)
+  const int ng = (w.wpr + 3) >> 2;          // word groups per row
+  const int rstep = kWG / ng;               // rows per pass
+  const int r0 = tid / ng, g = tid - r0 * ng;
+  if (r0 >= rstep) return;
+  uint32_t *dst = L.words + 4 * g;
   if (w.inner) {
-    // a thread makes 4 consecutive words of a row from 3 fetched dwords
-    const int ng = (w.wpr + 3) >> 2;          // word groups per row
-    const int rstep = kWG / ng;               // rows per pass
-    const int r0 = tid / ng, g = tid - r0 * ng;
-    if (r0 < rstep) {
-      for (int r = r0; r < w.wrows; r += rstep) {
-        const uint32_t *rw = L.raw + r * w.nd + g;
-        const uint32_t d0 = rw[0], d1 = rw[1], d2 = rw[2];
-        uint32_t *dst = L.words + r * L.wp + 4 * g;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int o = k + w.sh;   // byte offset of word 4g+k from dword g (0..6)
-          if (4 * g + k < w.wpr)
-            dst[k] = o < 4 ? __builtin_amdgcn_alignbyte(d1, d0, o) : __builtin_amdgcn_alignbyte(d2, d1, o - 4);
-        }
-      }
+    const uint32_t *src = L.raw + g;
+    switch (w.sh) {   // wave-uniform
+      case 0: expand_inner<0>(src, dst, w.nd, L.wp, w.wrows, r0, rstep); break;
+      case 1: expand_inner<1>(src, dst, w.nd, L.wp, w.wrows, r0, rstep); break;
+      case 2: expand_inner<2>(src, dst, w.nd, L.wp, w.wrows, r0, rstep); break;
+      default: expand_inner<3>(src, dst, w.nd, L.wp, w.wrows, r0, rstep); break;
     }
   } else {
     // window crosses (or lies beyond) the left/right picture edge: pel x of
-    // the window is picture column gx = clamp(x, 0, W-1); fetched dword d holds
-    // picture dword clamp(xa/4 + d, 0, W/4-1), so gx sits in dword
-    // clamp(gx/4 - xa/4, 0, nd-1), byte gx & 3
-    const uint8_t *raw8 = reinterpret_cast<const uint8_t *>(L.raw);
+    // the window is picture column gx = clamp(x, 0, W-1) (UMVLine4X); fetched
+    // dword d holds picture dword clamp(xa/4 + d, 0, W/4-1), so gx sits in
+    // dword clamp(gx/4 - xa/4, 0, nd-1), byte gx & 3.  The 4 pels of a word lie
+    // in two neighbouring fetched dwords: one v_perm_b32 per word and row, with
+    // the (dword, selector) pair fixed per column.
     const int xq = w.xa >> 2;
-    for (int i = tid; i < n; i += kWG) {
-      const int r = i / w.wpr, c = i - r * w.wpr;
-      const uint8_t *rb = raw8 + r * 4 * w.nd;
-      uint32_t v = 0;
+    int dq[4];
+    uint32_t sel[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int c = 4 * g + k;
+      const int q0 = clampi((clampi(w.x0 + c, 0, p.width - 1) >> 2) - xq, 0, w.nd - 1);
+      dq[k] = min(q0, w.nd - 2);
+      uint32_t s = 0;
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
         const int gx = clampi(w.x0 + c + b, 0, p.width - 1);
-        v |= (uint32_t)rb[4 * clampi((gx >> 2) - xq, 0, w.nd - 1) + (gx & 3)] << (8 * b);
+        const int q = clampi((gx >> 2) - xq, 0, w.nd - 1);
+        s |= (uint32_t)(4 * (q - dq[k]) + (gx & 3)) << (8 * b);
       }
-      L.words[r * L.wp + c] = v;
+      sel[k] = s;
+    }
+    for (int r = r0; r < w.wrows; r += rstep) {
+      const uint32_t *rw = L.raw + r * w.nd;
+      uint32_t *o = dst + r * L.wp;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[k] = __builtin_amdgcn_perm(rw[dq[k] + 1], rw[dq[k]], sel[k]);
     }
   }
 }
@@ -1099,7 +1140,10 @@ __global__ __launch_bounds__(kWG, KEY32 ? JMME_WAVES_PER_EU : 2) void me_items_k
     __syncthreads();
     if (p.debug_words && it.u == 0 && (it.gmask & dbg_slot)) {
       const Win w = win_of(p, it);
-      for (int i = opaque_tid(); i < w.wrows * L.wp; i += kWG) p.debug_words[i] = L.words[i];
+      for (int i = opaque_tid(); i < w.wrows * w.wpr; i += kWG) {
+        const int r = i / w.wpr;
+        p.debug_words[i] = L.words[r * L.wp + i - r * w.wpr];
+      }
     }
     STAMP(st.expand);
     // the raw buffer is free: start fetching the next item behind this sweep

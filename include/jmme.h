@@ -489,7 +489,7 @@ void jmme_spiral_offset(int index, int *ox, int *oy); /* inverse */
 int jmme_mvbits(int v);                                /* mvbits[v], mv_search.c:366-374 */
 
 /* Test hook (GPU): run one unit and copy out the first reference window it
- * staged in LDS, (2R+16) rows x ((2R+13)|1) words, word[y][x] = pels x..x+3
+ * staged in LDS, (2R+16) rows x (2R+13) words, word[y][x] = pels x..x+3
  * of the clamped reference; R = the context's SearchRange. */
 int jmme_debug_window(jmme_ctx *ctx, int mode, const jmme_mb_req *req, uint32_t *out, int max_words);
 

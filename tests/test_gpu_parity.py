@@ -290,7 +290,7 @@ def test_staged_window_is_the_clamped_reference(mb, cen, gpu):
     with MotionEstimator({"SearchRange": R, "SearchMode": -1}) as me:
         me.upload_cur(luma[1])
         me.upload_ref(0, 0, luma[0])
-        wp = (2 * R + 13) | 1
+        wp = 2 * R + 13
         out = np.zeros((2 * R + 16) * wp, np.uint32)
         _lib.check(_lib.lib().jmme_debug_window(me._ctx, FULL_SEARCH, _lib.ptr(req), _lib.ptr(out), out.size))
     out = out.reshape(2 * R + 16, wp)
