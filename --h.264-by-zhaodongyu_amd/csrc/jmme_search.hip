@@ -328,7 +328,9 @@ __device__ __forceinline__ uint32_t partition_sad_at(const Lds &L, const uint32_
 
 template <int CTRL>
 __device__ __forceinline__ uint32_t dpp_min(uint32_t v) {
-  return min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, 0xf, 0xf, false));
+  // full row/bank masks and in-row patterns: every lane reads a valid source,
+  // so the mov folds into v_min_u32_dpp (GCNDPPCombine)
+  return min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, true));
 }
 
 // ------------------------------------------------------------ plan kernel --
@@ -680,20 +682,23 @@ __device__ __forceinline__ void sweep_v5(const Lds &L, const uint32_t (&cs)[64],
   }
 }
 
-// JM's special (0,0) candidate, once per item after the v5 sweep: FS
+// JM's special (0,0) candidate, once per item instead of per position: FS
 // check_for_00 (slot 0 at (0,0) costs mvcost - 16*lambda, me_fullsearch.c:61,
 // 78-82) and the FFS pre-seed (every partition, rank 0, me_fullfast.c:650-657).
-// Its exact key joins the reduced minima in L.red before the refine (the
-// sweep's own key for that position is never below it).
+// Its 4x4 SADs are taken before the sweep (special_sads, wave 0) and its exact
+// key joins the reduced minima in the reduce's combine step (special_key), so
+// it adds no barrier; the sweep's own key for that position is never below it.
 template <bool FFS>
-__device__ __forceinline__ void special_00(const GroupCtx &g, const Lds &L) {
+__device__ __forceinline__ bool special_on(const GroupCtx &g) {
   const int ox = -(g.cqx >> 2), oy = -(g.cqy >> 2);   // the (0,0) vector as a window offset
-  const MvCost mc = mv_cost<FFS>(0, 0, g.px, g.py, g.lam, g.max_mvd);
   const bool inside = abs(ox) <= g.R && abs(oy) <= g.R;
-  const bool on = FFS ? (g.preseed && inside && mc.ok) : (g.chk00 && (g.gmask & 1) && inside);
-  if (!on) return;
-  const int tid = opaque_tid();
+  if (FFS) return g.preseed && inside && mv_cost<FFS>(0, 0, g.px, g.py, g.lam, g.max_mvd).ok;
+  return g.chk00 && (g.gmask & 1) && inside;
+}
+
+__device__ __forceinline__ void special_sads(const GroupCtx &g, const Lds &L, int tid) {
   if (tid < 16) {
+    const int ox = -(g.cqx >> 2), oy = -(g.cqy >> 2);
     const int bx = tid & 3, by = tid >> 2;
     const uint32_t *w = L.words + (oy + g.R + 4 * by) * L.wp + ox + g.R + 4 * bx;
     uint32_t sad = 0;
@@ -701,19 +706,22 @@ __device__ __forceinline__ void special_00(const GroupCtx &g, const Lds &L) {
     for (int r = 0; r < 4; ++r) sad = __builtin_amdgcn_sad_u8(w[r * L.wp], L.cur[(4 * by + r) * 4 + bx], sad);
     L.spec[tid] = sad;
   }
-  __syncthreads();
-  if (tid < kNS && ((g.gmask >> tid) & 1) && (FFS || tid == 0)) {
-    const SlotGeom gm = slot_geom(tid);
-    uint32_t sad = 0;
-    for (int j = 0; j < gm.h; ++j)
-      for (int i = 0; i < gm.w; ++i) sad += L.spec[(gm.by + j) * 4 + gm.bx + i];
-    const uint32_t mvc = FFS ? mc.mvc : check00_adjust(mc.mvc, g.lam, true);
-    const uint32_t rank = FFS ? 0u : (uint32_t)spiral_index_bl(ox, oy);
-    const uint32_t cost = (sad << 5) + mvc;
-    const uint32_t key = cost < (1u << (32 - kCostShift)) ? (cost << kCostShift) | (rank >> kRankDrop) : ~0u;
-    L.red[tid] = min((uint32_t)L.red[tid], key);
-  }
-  __syncthreads();
+}
+
+// the special candidate's 32-bit key for slot s (~0u when it is not one)
+template <bool FFS>
+__device__ __forceinline__ uint32_t special_key(const GroupCtx &g, const Lds &L, int s) {
+  if (!((g.gmask >> s) & 1) || !(FFS || s == 0)) return ~0u;
+  const int ox = -(g.cqx >> 2), oy = -(g.cqy >> 2);
+  const SlotGeom gm = slot_geom(s);
+  uint32_t sad = 0;
+  for (int j = 0; j < gm.h; ++j)
+    for (int i = 0; i < gm.w; ++i) sad += L.spec[(gm.by + j) * 4 + gm.bx + i];
+  const MvCost mc = mv_cost<FFS>(0, 0, g.px, g.py, g.lam, g.max_mvd);
+  const uint32_t mvc = FFS ? mc.mvc : check00_adjust(mc.mvc, g.lam, true);
+  const uint32_t rank = FFS ? 0u : (uint32_t)spiral_index_bl(ox, oy);
+  const uint32_t cost = (sad << 5) + mvc;
+  return cost < (1u << (32 - kCostShift)) ? (cost << kCostShift) | (rank >> kRankDrop) : ~0u;
 }
 
 // Exact 16x16 search with 64-bit keys, for an item whose every 32-bit 16x16
@@ -908,7 +916,9 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
   // every partition's minimum is tracked even when the group is a subset: the
   // slots outside gmask are simply never read back (one code path, no
   // per-partition masks in the loop)
+  const bool spec = KEY32 && fast && special_on<FFS>(g);
   if (KEY32 && fast) {
+    if (spec) special_sads(g, L, tid);   // read back after the reduce's first barrier
     if constexpr (KEY32) sweep_v5(L, cs, R, g.rs, best);
   } else {
     sweep(std::integral_constant<bool, true>{});
@@ -967,14 +977,14 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
     unsigned long long k = L.red[tid];
 #pragma unroll
     for (int w = 1; w < kWaves; ++w) { const unsigned long long o = L.red[w * kNS + tid]; k = o < k ? o : k; }
+    if (spec) k = min(k, (unsigned long long)special_key<FFS>(g, L, tid));
     L.red[tid] = k;   // wave 0's row now holds the group result
   }
   __syncthreads();
-  if (KEY32 && fast) special_00<FFS>(g, L);
   STAMP(st.reduce);
 
-  // ---- refine (32-bit keys): recover the 3 rank bits the key dropped.
-  // The winner has cost == key>>10 and rank in [8c, 8c+8), c = key & 1023;
+  // ---- refine (32-bit keys): recover the 2 rank bits the key dropped.
+  // The winner has cost == key>>11 and rank in [4c, 4c+4), c = key & 2047;
   // re-evaluate those positions exactly and take the smallest matching rank.
   tid = opaque_tid();
   if (KEY32) {
