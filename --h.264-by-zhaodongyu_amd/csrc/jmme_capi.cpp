@@ -388,7 +388,7 @@ int sync_ref_table(jmme_ctx *ctx, hipStream_t s) {
 
 int launch(jmme_ctx *ctx, int mode, const uint8_t *d_cur, const uint8_t *const *d_ref_table, int pitch,
            int w, int h, const jmme_mb_req *d_req, int n, jmme_block_res *d_out, hipStream_t s,
-           uint32_t *debug_words = nullptr, bool no64 = false) {
+           uint32_t *debug_words = nullptr) {
   if (mode != JMME_FULL_SEARCH && mode != JMME_FAST_FULL_SEARCH)
     return fail("search mode %d not supported by the batched engine (FS=-1, FFS=0)", mode);
   if (n < 0) return fail("negative unit count");
@@ -407,7 +407,6 @@ int launch(jmme_ctx *ctx, int mode, const uint8_t *d_cur, const uint8_t *const *
   p.max_mvd = ctx->max_mvd;
   p.lds_range = ctx->cfg.SearchRange;
   p.key32 = p.lds_range <= kKey32MaxRange;
-  p.no64 = no64 && p.key32;
   p.items = ctx->d_items;
   p.item_cap = (unsigned)ctx->cap_items;
   p.counts = ctx->d_counts;
@@ -517,14 +516,8 @@ extern "C" int jmme_search_mbs(jmme_ctx *ctx, int mode, const jmme_mb_req *req, 
   if (ensure_pin(ctx, rq + rs + 64)) return -1;
   std::memcpy(ctx->h_pin, req, (size_t)n * sizeof(jmme_mb_req));
   HIPCHK(hipMemcpyAsync(ctx->d_req, ctx->h_pin, (size_t)n * sizeof(jmme_mb_req), hipMemcpyHostToDevice, s));
-  // host-visible requests: when no searched slot's lambda needs the 64-bit cost key,
-  // the (then empty) 64-bit drain launch is skipped
-  bool no64 = true;
-  for (int i = 0; i < n && no64; ++i)
-    for (int sl = 0; sl < JMME_NSLOT; ++sl)
-      if (((req[i].slot_mask >> sl) & 1) && (uint32_t)req[i].blk[sl].lambda > kMaxLambda32) { no64 = false; break; }
   if (launch(ctx, mode, ctx->d_cur, ctx->d_ref_table, ctx->pitch, ctx->width, ctx->height, ctx->d_req, n,
-             ctx->d_out, s, nullptr, no64))
+             ctx->d_out, s))
     return -1;
   // results for searched slots only: copy the whole block, then merge
   const jmme_block_res *tmp = reinterpret_cast<const jmme_block_res *>(ctx->h_pin + rq);

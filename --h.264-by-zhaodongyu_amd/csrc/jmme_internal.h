@@ -31,6 +31,7 @@ struct Item {
 static_assert(sizeof(Item) == 48, "Item layout");
 constexpr int kItemChk00 = 1;     // slot 0 takes check_for_00 (me_fullsearch.c:61)
 constexpr int kItemPreseed = 2;   // FFS pos00 pre-seed (me_fullfast.c:640-648)
+constexpr int kItemSlow64 = 4;    // lambda beyond the 32-bit keys: exact per-partition search
 
 // 32-bit keys are cost << 11 | rank >> 2 (21-bit cost field).  Every partition
 // but 16x16 stays exact while 32*32640 + lambda*74 < 2^21; the 16x16 key
@@ -49,10 +50,9 @@ struct KParams {
   int max_mvd;                        // p_Vid->max_mvd (FFS gate)
   int lds_range;                      // largest search range in the launch (LDS sizing)
   int key32;                          // plan: route items to the 32-bit list (else all to the 64-bit list)
-  int no64;                           // host-checked: no unit needs the 64-bit list (skip its drain launch)
   Item *items;                        // [item_cap]: 32-bit list grows up from 0, 64-bit list down from the top
   unsigned item_cap;
-  unsigned *counts;                   // [0] 32-bit items, [1] 64-bit items, [2] status
+  unsigned *counts;                   // [0] 32-bit items, [1] 64-bit items (launch range > 44), [2] status
   uint32_t *debug_words;              // debug: unit 0's first staged window (rows x wp words)
   unsigned long long *stamps;         // diagnostic builds (JMME_STAMPS): per-unit phase clocks
 };

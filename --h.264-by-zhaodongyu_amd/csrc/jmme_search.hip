@@ -342,7 +342,8 @@ __global__ __launch_bounds__(64 * kPlanWaves) void me_plan_kernel(KParams p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int u = blockIdx.x * kPlanWaves + wave;
   int ng = 0;
-  bool to64 = !p.key32;
+  const bool to64 = !p.key32;   // the launch's range is beyond the 32-bit keys
+  bool slow = false;            // a lambda beyond the 32-bit keys: kItemSlow64 items
   unsigned long long my_gm = 0;
   int my_lead = 0;
   if (u < p.n) {
@@ -350,7 +351,7 @@ __global__ __launch_bounds__(64 * kPlanWaves) void me_plan_kernel(KParams p) {
     const unsigned long long mask = ufl64(rq->slot_mask) & kAll;
     const int4 me = lane < kNS ? reinterpret_cast<const int4 *>(&rq->blk[0])[lane] : make_int4(0, 0, 0, 0);
     const bool valid = lane < kNS && ((mask >> lane) & 1);
-    if (__builtin_amdgcn_ballot_w64(valid && (uint32_t)rq_lambda(me) > kMaxLambda32)) to64 = true;
+    slow = p.key32 && __builtin_amdgcn_ballot_w64(valid && (uint32_t)rq_lambda(me) > kMaxLambda32);
     unsigned long long rem = mask;
     while (rem) {
       const int lead = __builtin_ctzll(rem);
@@ -399,7 +400,7 @@ __global__ __launch_bounds__(64 * kPlanWaves) void me_plan_kernel(KParams p) {
     it.cqy = (int16_t)cqy;
     it.R = (int16_t)R;
     it.flags = (int16_t)(((!FFS && my_lead == 0 && (rq_flags(lq) & JMME_BLK_CHECK00)) ? kItemChk00 : 0) |
-                         ((FFS && rq->ffs_pos00_valid) ? kItemPreseed : 0));
+                         ((FFS && rq->ffs_pos00_valid) ? kItemPreseed : 0) | (slow ? kItemSlow64 : 0));
     it.px = (int16_t)rq_pred_x(lq);
     it.py = (int16_t)rq_pred_y(lq);
     it.lam = rq_lambda(lq);
@@ -724,13 +725,18 @@ __device__ __forceinline__ uint32_t special_key(const GroupCtx &g, const Lds &L,
   return cost < (1u << (32 - kCostShift)) ? (cost << kCostShift) | (rank >> kRankDrop) : ~0u;
 }
 
-// Exact 16x16 search with 64-bit keys, for an item whose every 32-bit 16x16
-// key saturated (only possible when lambda * mvbits > 8160 and the 16x16 SADs
-// are near 65280).  Result: min over the waves' L.fb entries.
+// Exact search of one partition with 64-bit keys (cost << 32 | rank), every
+// position of the window in the legacy per-position form.  Two users: a 16x16
+// whose every 32-bit key saturated (only when lambda * mvbits > 8160 and its
+// SADs are near 65280), and every partition of a unit whose lambda exceeds the
+// 32-bit keys' range (kItemSlow64; no JM configuration comes near it).  The
+// result is the min over this call's half of L.fb (slots alternate halves, so
+// one barrier per call suffices).
 template <bool FFS>
-__device__ __noinline__ void exact_16x16(const GroupCtx &g, const Lds &L) {
+__device__ __forceinline__ unsigned long long exact_slot(const GroupCtx &g, const Lds &L, int s) {
   const int tid = opaque_tid(), lane = tid & 63, wave = tid >> 6;
   const int R = g.R, D = 2 * R + 1;
+  const SlotGeom gm = slot_geom(s);
   unsigned long long best = ~0ull;
   for (int i = tid; i < D * D; i += kWG) {
     const int oyw = i / D, oxw = i - oyw * D, ox = oxw - R, oy = oyw - R;
@@ -739,12 +745,13 @@ __device__ __noinline__ void exact_16x16(const GroupCtx &g, const Lds &L) {
     const MvCost mc = mv_cost<FFS>(candx, candy, g.px, g.py, g.lam, g.max_mvd);
     if (!pos_eligible<FFS>(g, mc.ok, max(abs(ox), abs(oy)), is00)) continue;
     uint32_t sad = 0;
-    for (int r = 0; r < 16; ++r)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) sad = __builtin_amdgcn_sad_u8(L.words[(oyw + r) * L.wp + oxw + 4 * c], L.cur[r * 4 + c], sad);
+    for (int r = 0; r < 4 * gm.h; ++r)
+      for (int c = 0; c < gm.w; ++c)
+        sad = __builtin_amdgcn_sad_u8(L.words[(oyw + 4 * gm.by + r) * L.wp + oxw + 4 * (gm.bx + c)],
+                                      L.cur[(4 * gm.by + r) * 4 + gm.bx + c], sad);
     const int sidx = spiral_index_bl(ox, oy);
     const uint32_t rank = FFS ? ((g.preseed && is00) ? 0u : (uint32_t)sidx + 1u) : (uint32_t)sidx;
-    const uint32_t mvc = (!FFS && g.chk00) ? check00_adjust(mc.mvc, g.lam, is00) : mc.mvc;
+    const uint32_t mvc = (!FFS && g.chk00 && s == 0) ? check00_adjust(mc.mvc, g.lam, is00) : mc.mvc;
     const unsigned long long k = ((unsigned long long)((sad << 5) + mvc) << 32) | rank;
     best = k < best ? k : best;
   }
@@ -754,8 +761,32 @@ __device__ __noinline__ void exact_16x16(const GroupCtx &g, const Lds &L) {
     const unsigned long long x = ((unsigned long long)hi << 32) | lo;
     best = x < best ? x : best;
   }
-  if (lane == 0) L.fb[wave] = best;
+  unsigned long long *fb = L.fb + (s & 1) * kWaves;
+  if (lane == 0) fb[wave] = best;
   __syncthreads();
+  unsigned long long k = fb[0];
+#pragma unroll
+  for (int w = 1; w < kWaves; ++w) k = fb[w] < k ? fb[w] : k;
+  return k;
+}
+
+// one partition's result from its exact (cost, rank) -- JM leaves best_pos = 0
+// and returns the incoming min_mcost when nothing was eligible
+template <bool FFS>
+__device__ __forceinline__ jmme_block_res block_result(const GroupCtx &g, bool found, uint32_t rank, uint32_t cost) {
+  jmme_block_res res;
+  res.reserved = 0;
+  if (!found) {
+    res.mv_x = (int16_t)g.cqx; res.mv_y = (int16_t)g.cqy; res.cost = JMME_DISTBLK_MAX;
+    return res;
+  }
+  int ox, oy;
+  if (FFS && rank == 0) { ox = -(g.cqx >> 2); oy = -(g.cqy >> 2); }   // the pre-seeded (0,0)
+  else spiral_offset_fast(FFS ? (int)rank - 1 : (int)rank, &ox, &oy);
+  res.mv_x = (int16_t)(g.cqx + 4 * ox);
+  res.mv_y = (int16_t)(g.cqy + 4 * oy);
+  res.cost = (int64_t)cost;
+  return res;
 }
 
 template <bool KEY32, bool FFS>
@@ -1044,27 +1075,16 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
   }
   // every 32-bit 16x16 key saturated: search the 16x16 again with exact keys
   const bool fb16 = KEY32 && (gmask & 1) && (uint32_t)L.red[0] == ~0u;
-  if (fb16) exact_16x16<FFS>(g, L);
+  const unsigned long long k16 = fb16 ? exact_slot<FFS>(g, L, 0) : ~0ull;
   STAMP(st.refine);
 
   // ---- results of this group
   tid = opaque_tid();
   if (tid < kNS && ((gmask >> tid) & 1)) {
-    const unsigned long long k = L.red[tid];
-    jmme_block_res res;
-    res.reserved = 0;
+    const unsigned long long k = (KEY32 && tid == 0 && fb16) ? k16 : L.red[tid];
     uint32_t rank = 0, cost = 0;
     bool found = false;
-    if (KEY32 && tid == 0 && fb16) {
-      unsigned long long kb = L.fb[0];
-#pragma unroll
-      for (int w = 1; w < kWaves; ++w) kb = L.fb[w] < kb ? L.fb[w] : kb;
-      if (kb != ~0ull) {
-        found = true;
-        rank = (uint32_t)(kb & 0x7fffffffu);
-        cost = (uint32_t)(kb >> 32);
-      }
-    } else if (KEY32) {
+    if (KEY32 && !(tid == 0 && fb16)) {
       const uint32_t key = (uint32_t)k;
       if (key != ~0u) {
         for (int j = 0; j < kCand && !found; ++j)
@@ -1080,20 +1100,29 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
       rank = (uint32_t)(k & 0x7fffffffu);
       cost = (uint32_t)(k >> 32);
     }
-    if (!found) {
-      // nothing eligible: JM leaves best_pos = 0 and returns the incoming min_mcost
-      res.mv_x = (int16_t)g.cqx; res.mv_y = (int16_t)g.cqy; res.cost = JMME_DISTBLK_MAX;
-    } else {
-      int ox, oy;
-      if (FFS && rank == 0) { ox = -(g.cqx >> 2); oy = -(g.cqy >> 2); }   // the pre-seeded (0,0)
-      else spiral_offset_fast(FFS ? (int)rank - 1 : (int)rank, &ox, &oy);
-      res.mv_x = (int16_t)(g.cqx + 4 * ox);
-      res.mv_y = (int16_t)(g.cqy + 4 * oy);
-      res.cost = (int64_t)cost;
-    }
-    p.out[(size_t)u * kNS + tid] = res;
+    p.out[(size_t)u * kNS + tid] = block_result<FFS>(g, found, rank, cost);
   }
   STAMP(st.out);
+}
+
+// A unit whose lambda exceeds the 32-bit keys' range (kItemSlow64): every
+// partition of the item by the exact 64-bit search, one after the other.
+template <bool FFS>
+__device__ __forceinline__ void search_item_slow64(const KParams &p, const Item &it, const Lds &L) {
+  GroupCtx g;
+  g.cqx = it.cqx; g.cqy = it.cqy; g.R = it.R; g.px = it.px; g.py = it.py; g.lam = it.lam;
+  g.max_mvd = p.max_mvd;
+  g.preseed = FFS && (it.flags & kItemPreseed);
+  g.gmask = it.gmask;
+  g.rs = it.rs;
+  g.chk00 = !FFS && (it.flags & kItemChk00);
+  for (int s = 0; s < kNS; ++s) {
+    if (!((g.gmask >> s) & 1)) continue;
+    const unsigned long long k = exact_slot<FFS>(g, L, s);
+    if (opaque_tid() == 0)
+      p.out[(size_t)it.u * kNS + s] =
+          block_result<FFS>(g, k != ~0ull, (uint32_t)(k & 0x7fffffffu), (uint32_t)(k >> 32));
+  }
 }
 
 // item descriptors are wave-uniform: keep every field in SGPRs
@@ -1167,11 +1196,15 @@ __global__ __launch_bounds__(kWG, KEY32 ? JMME_WAVES_PER_EU : 2) void me_items_k
 #pragma unroll
         for (int i = 0; i < 64; ++i) cs[i] = __builtin_amdgcn_readlane(v, i);
       }
+      if (KEY32 && (it.flags & kItemSlow64)) {
+        search_item_slow64<FFS>(p, it, L);
+      } else {
 #ifdef JMME_STAMPS
-      search_item<KEY32, FFS>(p, it, L, fast, cs, t_last, st);
+        search_item<KEY32, FFS>(p, it, L, fast, cs, t_last, st);
 #else
-      search_item<KEY32, FFS>(p, it, L, fast, cs);
+        search_item<KEY32, FFS>(p, it, L, fast, cs);
 #endif
+      }
     }
 #ifdef JMME_STAMPS
     if (p.stamps && threadIdx.x == 0) {
@@ -1229,12 +1262,11 @@ hipError_t launch_search(const KParams &p, hipStream_t s, hipEvent_t ev0, hipEve
   const int v = ffs ? 2 : 0;
   if (ev0) (void)hipEventRecord(ev0, s);
   if (p.key32) {
+    // (units whose lambda is beyond the 32-bit keys are served in this kernel
+    // too, by the exact per-partition search: no second launch)
     hipLaunchKernelGGL(k32, dim3(resident_grid(occ, dev, v, k32, p.lds_range, lds)), dim3(kWG), lds, s, p);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (ev1) (void)hipEventRecord(ev1, s);
-    // units whose lambda could saturate the 32-bit cost field (none in
-    // practice) were planned into the 64-bit list: a small grid drains it
-    if (!p.no64) hipLaunchKernelGGL(k64, dim3(64), dim3(kWG), lds, s, p);
   } else {
     hipLaunchKernelGGL(k64, dim3(resident_grid(occ, dev, v + 1, k64, p.lds_range, lds)), dim3(kWG), lds, s, p);
     if ((e = hipGetLastError()) != hipSuccess) return e;
