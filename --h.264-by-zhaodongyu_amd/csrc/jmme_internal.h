@@ -50,9 +50,9 @@ struct KParams {
   int max_mvd;                        // p_Vid->max_mvd (FFS gate)
   int lds_range;                      // largest search range in the launch (LDS sizing)
   int key32;                          // plan: route items to the 32-bit list (else all to the 64-bit list)
-  Item *items;                        // [item_cap]: 32-bit list grows up from 0, 64-bit list down from the top
+  Item *items;                        // [item_cap]: unit u's first group at u, further groups from n on
   unsigned item_cap;
-  unsigned *counts;                   // [0] 32-bit items, [1] 64-bit items (launch range > 44), [2] status
+  unsigned *counts;                   // [0] further groups, [1] unused, [2] status
   uint32_t *debug_words;              // debug: unit 0's first staged window (rows x wp words)
   unsigned long long *stamps;         // diagnostic builds (JMME_STAMPS): per-unit phase clocks
 };

@@ -338,11 +338,10 @@ __device__ __forceinline__ uint32_t dpp_min(uint32_t v) {
 // readlane + ballot; items appended with one atomic per workgroup per list.
 template <bool FFS>
 __global__ __launch_bounds__(64 * kPlanWaves) void me_plan_kernel(KParams p) {
-  __shared__ unsigned s_n[kPlanWaves], s_64[kPlanWaves], s_off[kPlanWaves];
+  __shared__ unsigned s_n[kPlanWaves], s_off[kPlanWaves];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int u = blockIdx.x * kPlanWaves + wave;
   int ng = 0;
-  const bool to64 = !p.key32;   // the launch's range is beyond the 32-bit keys
   bool slow = false;            // a lambda beyond the 32-bit keys: kItemSlow64 items
   unsigned long long my_gm = 0;
   int my_lead = 0;
@@ -369,20 +368,23 @@ __global__ __launch_bounds__(64 * kPlanWaves) void me_plan_kernel(KParams p) {
       rem &= ~gm;
     }
   }
-  if (lane == 0) { s_n[wave] = ng; s_64[wave] = to64; }
+  // list layout: a unit's first group is item u (raster order: neighbouring
+  // macroblocks' windows overlap, and the item kernel deals contiguous runs to
+  // an XCD); its further groups (1.5 % of the 1080p units) follow the n first
+  // ones, one atomic per workgroup
+  if (lane == 0) s_n[wave] = ng > 1 ? ng - 1 : 0;
   __syncthreads();
   if (tid == 0) {
-    unsigned na = 0, nb = 0;
+    unsigned na = 0;
     for (int w = 0; w < kPlanWaves; ++w) {
-      unsigned &c = s_64[w] ? nb : na;
-      s_off[w] = c;
-      c += s_n[w];
+      s_off[w] = na;
+      na += s_n[w];
     }
     const unsigned ba = na ? atomicAdd(&p.counts[0], na) : 0u;
-    const unsigned bb = nb ? atomicAdd(&p.counts[1], nb) : 0u;
-    for (int w = 0; w < kPlanWaves; ++w) s_off[w] += s_64[w] ? bb : ba;
+    for (int w = 0; w < kPlanWaves; ++w) s_off[w] += ba;
   }
   __syncthreads();
+  if (u < p.n && ng == 0 && lane == 0) p.items[u].gmask = 0;   // nothing searched
   if (u < p.n && lane < ng) {
     const jmme_mb_req *rq = p.req + u;
     const int4 lq = reinterpret_cast<const int4 *>(&rq->blk[0])[my_lead];
@@ -412,8 +414,7 @@ __global__ __launch_bounds__(64 * kPlanWaves) void me_plan_kernel(KParams p) {
       atomicOr(&p.counts[2], (R < 0 || R > p.lds_range) ? 1u : 2u);
       it.gmask = 0;
     }
-    const unsigned idx = s_off[wave] + lane;
-    p.items[to64 ? p.item_cap - 1 - idx : idx] = it;
+    p.items[lane == 0 ? (unsigned)u : (unsigned)p.n + s_off[wave] + lane - 1] = it;
   }
 }
 
@@ -1142,8 +1143,8 @@ template <bool KEY32, bool FFS>
 __global__ __launch_bounds__(kWG, KEY32 ? JMME_WAVES_PER_EU : 2) void me_items_kernel(KParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ __attribute__((aligned(16))) uint32_t s_cur[64];
-  const unsigned cnt = p.counts[KEY32 ? 0 : 1];
-  const Item *items = KEY32 ? p.items : p.items + (p.item_cap - cnt);
+  const unsigned cnt = (unsigned)p.n + p.counts[0];   // first groups, then the further groups
+  const Item *items = p.items;
   const int x = blockIdx.x & 7, lb = blockIdx.x >> 3, nbx = (gridDim.x - x + 7) >> 3;
   const unsigned start = (unsigned)(((unsigned long long)cnt * x) >> 3);
   const unsigned end = (unsigned)(((unsigned long long)cnt * (x + 1)) >> 3);
