@@ -78,7 +78,7 @@ struct jmme_ctx {
   int pool_min_range = 80;                   // jmme_fractal_search: pruned pool search from this radius up
   int pool_mfma = 1;                         // 4x4 full pool: matrix-core bound test (0: VALU)
   size_t cap_stamps = 0;
-  unsigned *d_counts = nullptr;              // [0] 32-bit items, [1] 64-bit items, [2] status
+  unsigned *d_counts = nullptr;              // kCountWords: [0] further groups, [2] status, [8..15] XCD tickets
   Item *d_items = nullptr;                   // work items (one per unit x partition group)
   size_t cap_items = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -261,7 +261,7 @@ extern "C" jmme_ctx *jmme_create(const jmme_config *cfg, int device) {
     ~Restore() { if (d >= 0 && d != was) (void)hipSetDevice(d); }
   } restore_{caller_dev, ctx->device};
   if ((e = hipMalloc(&ctx->d_ref_table, sizeof(uint8_t *) * kMaxLists * kMaxRefs)) != hipSuccess ||
-      (e = hipMalloc(&ctx->d_counts, 16)) != hipSuccess ||
+      (e = hipMalloc(&ctx->d_counts, kCountWords * sizeof(unsigned))) != hipSuccess ||
       (e = hipMalloc(&ctx->d_sub_table, sizeof(uint8_t *) * kMaxLists * kMaxRefs)) != hipSuccess ||
       (e = hipEventCreate(&ctx->ev0)) != hipSuccess || (e = hipEventCreate(&ctx->ev1)) != hipSuccess) {
     fail("jmme_create: %s", hipGetErrorString(e));
@@ -412,15 +412,17 @@ int launch(jmme_ctx *ctx, int mode, const uint8_t *d_cur, const uint8_t *const *
   p.counts = ctx->d_counts;
   p.debug_words = debug_words;
 #ifdef JMME_STAMPS
-  if ((size_t)n > ctx->cap_stamps) {
+  // n units x 8 words, then 4 words per workgroup (up to kStampWGs)
+  const size_t words = (size_t)n * 8 + (size_t)kStampWGs * 4;
+  if (words > ctx->cap_stamps) {
     (void)hipFree(ctx->d_stamps);
-    HIPCHK(hipMalloc(&ctx->d_stamps, (size_t)n * 8 * sizeof(unsigned long long)));
-    ctx->cap_stamps = (size_t)n;
+    HIPCHK(hipMalloc(&ctx->d_stamps, words * sizeof(unsigned long long)));
+    ctx->cap_stamps = words;
   }
   p.stamps = ctx->d_stamps;
-  HIPCHK(hipMemsetAsync(ctx->d_stamps, 0, (size_t)n * 8 * sizeof(unsigned long long), s));
+  HIPCHK(hipMemsetAsync(ctx->d_stamps, 0, words * sizeof(unsigned long long), s));
 #endif
-  HIPCHK(hipMemsetAsync(ctx->d_counts, 0, 16, s));
+  HIPCHK(hipMemsetAsync(ctx->d_counts, 0, kCountWords * sizeof(unsigned), s));
   // jmme_last_kernel_ms: the main item kernel alone (ev0 .. ev1)
   HIPCHK(launch_search(p, s, ctx->ev0, ctx->ev1));
   ctx->timed = true;
@@ -1216,7 +1218,9 @@ extern "C" int jmme_debug_stamps(jmme_ctx *ctx, uint64_t *out, int max_units) {
   // last launch: [wait, expand, sweep, reduce, refine, output, nslots, items].
   if (!ctx) return fail("null ctx");
   if (!ctx->d_stamps) return fail("library built without JMME_STAMPS");
-  size_t n = (size_t)max_units < ctx->cap_stamps ? (size_t)max_units : ctx->cap_stamps;
+  // Rows of 8 words; the first n rows are the units, the rest per-workgroup
+  // records (4 words each: start, end, HW_ID, XCC_ID << 32 | items).
+  size_t n = (size_t)max_units < ctx->cap_stamps / 8 ? (size_t)max_units : ctx->cap_stamps / 8;
   HIPCHK(hipDeviceSynchronize());
   HIPCHK(hipMemcpy(out, ctx->d_stamps, n * 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
   return (int)n;

@@ -10,6 +10,8 @@ constexpr int kMaxLists = 2;
 constexpr int kMaxRefs = 32;
 constexpr int kKey32MaxRange = 44;   // (2R+1)^2 < 2^13 spiral ranks fit the 32-bit key
 constexpr int kWG = 256;             // 4 waves of 64
+constexpr int kStampWGs = 4096;      // diagnostic builds: per-workgroup records
+constexpr int kCountWords = 16;      // KParams::counts, zeroed before every search launch
 
 // One work item of the search kernels: the partitions of one MB x ref unit
 // that share a search window AND a predictor/lambda (one SAD sweep serves all
@@ -52,7 +54,8 @@ struct KParams {
   int key32;                          // plan: route items to the 32-bit list (else all to the 64-bit list)
   Item *items;                        // [item_cap]: unit u's first group at u, further groups from n on
   unsigned item_cap;
-  unsigned *counts;                   // [0] further groups, [1] unused, [2] status
+  unsigned *counts;                   // kCountWords: [0] further groups, [1] unused, [2] status,
+                                      // [8 + x] XCD x's item tickets (item kernel)
   uint32_t *debug_words;              // debug: unit 0's first staged window (rows x wp words)
   unsigned long long *stamps;         // diagnostic builds (JMME_STAMPS): per-unit phase clocks
 };

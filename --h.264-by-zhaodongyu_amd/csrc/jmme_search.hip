@@ -66,20 +66,6 @@ constexpr int kPlanWaves = 16;             // plan kernel: units per workgroup
 constexpr int kRed1 = (kNS + 3) / 4 * 2;      // reduce: registers after the permlane32 level (22)
 constexpr int kRed2 = kRed1 / 2;              //         ... after the permlane16 level (11)
 
-// refine work list: every 4x4 block of every partition, (slot << 4) | (by*4 + bx)
-constexpr int kBlkItems = 112;
-struct BlkTab { uint16_t v[kBlkItems]; };
-constexpr BlkTab make_blk_tab() {
-  BlkTab t{};
-  int n = 0;
-  for (int s = 0; s < kNS; ++s) {
-    const SlotGeom gm = slot_geom(s);
-    for (int j = 0; j < gm.h; ++j)
-      for (int i = 0; i < gm.w; ++i) t.v[n++] = (uint16_t)((s << 4) | ((gm.by + j) * 4 + gm.bx + i));
-  }
-  return t;
-}
-__constant__ BlkTab kBlkTab = make_blk_tab();
 #ifndef JMME_WAVES_PER_EU
 #define JMME_WAVES_PER_EU 4
 #endif
@@ -98,7 +84,6 @@ struct Lds {
                             // then its current MB (64 dwords)
   uint32_t *cur;            // 64 words: MB row r, column group c at [r*4+c] (static LDS)
   unsigned long long *red;  // kWaves x 41 reduction scratch
-  uint32_t *match;          // 41 x kCand refine flags
   uint4 *tx, *ty;           // per-item position tables (2R+1 each), see build_tabs
   uint32_t *spec;           // 16 4x4 SADs at the special (0,0) candidate
   unsigned long long *fb;   // exact 16x16 result of the saturation fallback
@@ -109,7 +94,7 @@ struct Lds {
 __host__ __device__ inline int words_pitch(int R) { return 4 * ((2 * R + 13 + 3) / 4) + 1; }
 
 // one layout for the kernel (carve) and the host (items_lds_bytes)
-struct LdsPlan { size_t words, raw, red, match, tx, ty, spec, fb, total; };
+struct LdsPlan { size_t words, raw, red, tx, ty, spec, fb, total; };
 __host__ __device__ inline LdsPlan lds_plan(int R) {
   LdsPlan q;
   const int rows = 2 * R + 16, wp = words_pitch(R), d = 2 * R + 1;
@@ -118,7 +103,6 @@ __host__ __device__ inline LdsPlan lds_plan(int R) {
   q.words = take((size_t)rows * wp * 4);
   q.raw = take(((size_t)rows * raw_row_dwords(R) + kRawExtra) * 4);
   q.red = take((size_t)kWaves * kNS * 8);
-  q.match = take((size_t)kNS * kCand * 4);
   q.tx = take((size_t)d * 16);
   q.ty = take((size_t)d * 16);
   q.spec = take(16 * 4);
@@ -134,7 +118,6 @@ __device__ __forceinline__ Lds carve(unsigned char *smem, int R) {
   L.words = reinterpret_cast<uint32_t *>(smem + q.words);
   L.raw = reinterpret_cast<uint32_t *>(smem + q.raw);
   L.red = reinterpret_cast<unsigned long long *>(smem + q.red);
-  L.match = reinterpret_cast<uint32_t *>(smem + q.match);
   L.tx = reinterpret_cast<uint4 *>(smem + q.tx);
   L.ty = reinterpret_cast<uint4 *>(smem + q.ty);
   L.spec = reinterpret_cast<uint32_t *>(smem + q.spec);
@@ -790,6 +773,108 @@ __device__ __forceinline__ jmme_block_res block_result(const GroupCtx &g, bool f
   return res;
 }
 
+// Refine + output for 32-bit keys, after the reduce's one barrier and without
+// another: the winner of slot s has cost key >> 11 and a rank in [4c, 4c+4),
+// c = key & 2047; those <= 4 candidates are re-evaluated exactly and the
+// smallest matching rank wins.  Each lane owns (slot s, candidate j, part q of
+// nq), at most two 4x4 blocks of one candidate, so every lane does <= 8 SADs:
+//   wave 0: 4x4 slots (25-40), one block;    wave 1: 8x4 / 4x8 (9-24), two blocks;
+//   wave 2: 8x8 (5-8) in 2 parts, 16x16 (0) in 8 parts;  wave 3: 16x8 / 8x16 (1-4) in 4 parts.
+// The parts of a candidate are consecutive lanes (summed by DPP), its four
+// candidates consecutive groups (the winner found by one ballot).  Every lane
+// forms its slot's key from the per-wave minima itself, so nothing else needs
+// the LDS combine.  skip0: slot 0 is served by the exact fallback instead.
+template <bool FFS>
+__device__ __forceinline__ void refine_output32(const KParams &p, const GroupCtx &g, const Lds &L, bool spec,
+                                                bool skip0, int u) {
+  const int tid = opaque_tid(), lane = tid & 63, wave = ufl(tid >> 6);
+  int s, j, q, nq;
+  if (wave == 0) { s = 25 + (lane >> 2); j = lane & 3; q = 0; nq = 1; }
+  else if (wave == 1) { s = 9 + (lane >> 2); j = lane & 3; q = 0; nq = 1; }
+  else if (wave == 2) {
+    if (lane < 32) { s = 5 + (lane >> 3); j = (lane >> 1) & 3; q = lane & 1; nq = 2; }
+    else { s = 0; j = (lane >> 3) & 3; q = lane & 7; nq = 8; }
+  } else { s = 1 + (lane >> 4); j = (lane >> 2) & 3; q = lane & 3; nq = 4; }
+  const bool mine = ((g.gmask >> s) & 1) && !(skip0 && s == 0);
+  uint32_t key = ~0u;
+  if (mine) {
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) key = min(key, (uint32_t)L.red[w * kNS + s]);
+    if (spec) key = min(key, special_key<FFS>(g, L, s));
+  }
+  // candidate j: its window offset, or none
+  const int R = g.R, D = 2 * R + 1;
+  const int rk = (int)(((key & ((1u << kCostShift) - 1)) << kRankDrop) + j);
+  int ox = 0, oy = 0;
+  bool exists = mine && key != ~0u;
+  if (exists) {
+    if (FFS && rk == 0) {            // the pre-seeded (0,0) vector
+      ox = -(g.cqx >> 2); oy = -(g.cqy >> 2);
+      exists = g.preseed && abs(ox) <= R && abs(oy) <= R;
+    } else {
+      const int sidx = FFS ? rk - 1 : rk;
+      exists = sidx < D * D;
+      if (exists) spiral_offset_fast(sidx, &ox, &oy);
+    }
+  }
+  // this lane's blocks of the candidate
+  uint32_t sad = 0;
+  if (exists) {
+    const SlotGeom gm = slot_geom(s);
+    const int per = (gm.w * gm.h) / nq;   // 1 or 2, uniform per wave
+    for (int k = q * per; k < (q + 1) * per; ++k) {
+      const int bx = gm.bx + k % gm.w, by = gm.by + k / gm.w;
+      const uint32_t *w = L.words + (oy + R + 4 * by) * L.wp + ox + R + 4 * bx;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sad = __builtin_amdgcn_sad_u8(w[r * L.wp], L.cur[(4 * by + r) * 4 + bx], sad);
+    }
+  }
+  // sum the parts (groups of nq aligned lanes; every lane active here)
+  {
+    const uint32_t x1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)sad, 0xB1, 0xf, 0xf, true);    // lane ^ 1
+    sad += nq >= 2 ? x1 : 0u;
+    const uint32_t x2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)sad, 0x4E, 0xf, 0xf, true);    // lane ^ 2
+    sad += nq >= 4 ? x2 : 0u;
+    const uint32_t x4 = (uint32_t)__builtin_amdgcn_mov_dpp((int)sad, 0x141, 0xf, 0xf, true);   // the other quad of 8
+    sad += nq >= 8 ? x4 : 0u;
+  }
+  // exact cost, rank and eligibility at the group leader
+  bool m = false;
+  if (exists && q == 0) {
+    const int candx = g.cqx + 4 * ox, candy = g.cqy + 4 * oy;
+    const bool is00 = (candx == 0) && (candy == 0);
+    const int sidx = spiral_index_bl(ox, oy);
+    const uint32_t rank = FFS ? ((g.preseed && is00) ? 0u : (uint32_t)sidx + 1u) : (uint32_t)sidx;
+    const MvCost mc = mv_cost<FFS>(candx, candy, g.px, g.py, g.lam, g.max_mvd);
+    const bool ok = pos_eligible<FFS>(g, mc.ok, max(abs(ox), abs(oy)), is00);
+    const uint32_t mv = (s == 0 && g.chk00) ? check00_adjust(mc.mvc, g.lam, is00) : mc.mvc;
+    m = rank == (uint32_t)rk && (sad << 5) + mv == (key >> kCostShift) && ok;
+  }
+  const unsigned long long M = __builtin_amdgcn_ballot_w64(m);
+  const int base = lane - q - j * nq;   // leader lane of (s, candidate 0)
+  unsigned long long lower = 0, all = 0;
+#pragma unroll
+  for (int jj = 0; jj < kCand; ++jj) {
+    const unsigned long long b = 1ull << (base + jj * nq);
+    all |= b;
+    lower |= jj < j ? b : 0ull;
+  }
+  if (!mine || q != 0) return;
+  jmme_block_res res;
+  res.reserved = 0;
+  if (m && !(M & lower)) {
+    res.mv_x = (int16_t)(g.cqx + 4 * ox);
+    res.mv_y = (int16_t)(g.cqy + 4 * oy);
+    res.cost = (int64_t)(key >> kCostShift);
+  } else if (j == 0 && key == ~0u) {   // nothing eligible: JM leaves the centre and DISTBLK_MAX
+    res.mv_x = (int16_t)g.cqx; res.mv_y = (int16_t)g.cqy; res.cost = JMME_DISTBLK_MAX;
+  } else {
+    if (j == 0 && !(M & all)) atomicOr(&p.counts[2], 4u);   // cannot happen: refine lost the winner
+    return;
+  }
+  p.out[(size_t)u * kNS + s] = res;
+}
+
 template <bool KEY32, bool FFS>
 struct ItemStamps {
   unsigned long long wait = 0, expand = 0, sweep = 0, reduce = 0, refine = 0, out = 0;
@@ -798,7 +883,7 @@ struct ItemStamps {
 // sweep + reduce + refine + output of one item whose window is in L.words
 template <bool KEY32, bool FFS>
 __device__ __forceinline__ void search_item(const KParams &p, const Item &it, const Lds &L, bool fast,
-                                            const uint32_t (&cs)[64]
+                                            const uint32_t (&cs)[64], unsigned *tick, unsigned *s_tick
 #ifdef JMME_STAMPS
                                             , unsigned long long &t_last, ItemStamps<KEY32, FFS> &st
 #endif
@@ -961,6 +1046,10 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
   tid = opaque_tid();
   lane = tid & 63;
   wave = tid >> 6;
+  // the workgroup's next ticket (see me_items_kernel): issued here, written to
+  // LDS once the reduce and refine have hidden the atomic's round trip
+  unsigned tk = 0;
+  if (tick && tid == 0) tk = atomicAdd(tick, 1u);
   if (KEY32) {
     // reduce-scatter through the wave: permlane32_swap pairs slots (lanes
     // 0-31 keep one, 32-63 the other), permlane16_swap pairs again (one slot
@@ -1002,9 +1091,30 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
       if (lane == 0) L.red[wave * kNS + s] = k;
     }
   }
-  if (KEY32)
-    for (int i = tid; i < kNS * kCand; i += kWG) L.match[i] = 0;   // refine SAD accumulators
   __syncthreads();
+  if constexpr (KEY32) {
+    // every 32-bit 16x16 key saturated (uniform: every thread forms slot 0's key)
+    bool fb16 = false;
+    if (gmask & 1) {
+      uint32_t k0 = ~0u;
+#pragma unroll
+      for (int w = 0; w < kWaves; ++w) k0 = min(k0, (uint32_t)L.red[w * kNS]);
+      if (spec) k0 = min(k0, special_key<FFS>(g, L, 0));
+      fb16 = k0 == ~0u;
+    }
+    STAMP(st.reduce);
+    refine_output32<FFS>(p, g, L, spec, fb16, u);
+    if (tick && opaque_tid() == 0) *s_tick = tk;
+    STAMP(st.refine);
+    if (fb16) {   // search the 16x16 again with exact keys
+      const unsigned long long k16 = exact_slot<FFS>(g, L, 0);
+      if (opaque_tid() == 0)
+        p.out[(size_t)u * kNS] =
+            block_result<FFS>(g, k16 != ~0ull, (uint32_t)(k16 & 0x7fffffffu), (uint32_t)(k16 >> 32));
+    }
+    STAMP(st.out);
+    return;
+  }
   if (tid < kNS) {
     unsigned long long k = L.red[tid];
 #pragma unroll
@@ -1015,93 +1125,15 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
   __syncthreads();
   STAMP(st.reduce);
 
-  // ---- refine (32-bit keys): recover the 2 rank bits the key dropped.
-  // The winner has cost == key>>11 and rank in [4c, 4c+4), c = key & 2047;
-  // re-evaluate those positions exactly and take the smallest matching rank.
-  tid = opaque_tid();
-  if (KEY32) {
-    const int D = 2 * R + 1;
-    // candidate j of slot s: its window offset, or false if it does not exist
-    auto candidate = [&](int s, int j, int &ox, int &oy, int &rk) -> bool {
-      const uint32_t key = (uint32_t)L.red[s];
-      if (!((gmask >> s) & 1) || key == ~0u) return false;
-      rk = (int)(((key & ((1u << kCostShift) - 1)) << kRankDrop) + j);
-      if (FFS && rk == 0) {          // the pre-seeded (0,0) vector
-        ox = -(g.cqx >> 2); oy = -(g.cqy >> 2);
-        return g.preseed && abs(ox) <= R && abs(oy) <= R;
-      }
-      const int sidx = FFS ? rk - 1 : rk;
-      if (sidx >= D * D) return false;
-      spiral_offset_fast(sidx, &ox, &oy);
-      return true;
-    };
-    // (a) the partition SADs at the candidates, one 4x4 block per work item
-    //     (896 items: a 16x16 candidate is 16 of them), summed in LDS
-    for (int e = tid; e < kBlkItems * kCand; e += kWG) {
-      const int j = e & (kCand - 1);
-      const int sb = kBlkTab.v[e >> kRankDrop];
-      const int s = sb >> 4, bx = sb & 3, by = (sb >> 2) & 3;
-      int ox, oy, rk;
-      if (candidate(s, j, ox, oy, rk)) {
-        const uint32_t *w = L.words + (oy + R + 4 * by) * L.wp + ox + R + 4 * bx;
-        uint32_t sad = 0;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) sad = __builtin_amdgcn_sad_u8(w[r * L.wp], curw[(4 * by + r) * 4 + bx], sad);
-        atomicAdd(&L.match[s * kCand + j], sad);
-      }
-    }
-    __syncthreads();
-    // (b) exact cost and eligibility of each candidate
-    for (int item = tid; item < kNS * kCand; item += kWG) {
-      const int s = item / kCand, j = item - s * kCand;
-      uint32_t m = 0;
-      int ox, oy, rk;
-      if (candidate(s, j, ox, oy, rk)) {
-        const uint32_t mincost = (uint32_t)L.red[s] >> kCostShift;
-        const int candx = g.cqx + 4 * ox, candy = g.cqy + 4 * oy;
-        PosCtx c;
-        c.is00 = (candx == 0) && (candy == 0);
-        c.lring = max(abs(ox), abs(oy));
-        const int sidx = spiral_index_bl(ox, oy);
-        c.rank = FFS ? ((g.preseed && c.is00) ? 0u : (uint32_t)sidx + 1u) : (uint32_t)sidx;
-        const MvCost mc = mv_cost<FFS>(candx, candy, g.px, g.py, g.lam, g.max_mvd);
-        c.ok = pos_eligible<FFS>(g, mc.ok, c.lring, c.is00);
-        const uint32_t mv = (s == 0 && g.chk00) ? check00_adjust(mc.mvc, g.lam, c.is00) : mc.mvc;
-        const uint32_t cost = (L.match[item] << 5) + mv;
-        m = (c.rank == (uint32_t)rk) && cost == mincost && c.ok;
-      }
-      L.match[item] = m;
-    }
-    __syncthreads();
-  }
-  // every 32-bit 16x16 key saturated: search the 16x16 again with exact keys
-  const bool fb16 = KEY32 && (gmask & 1) && (uint32_t)L.red[0] == ~0u;
-  const unsigned long long k16 = fb16 ? exact_slot<FFS>(g, L, 0) : ~0ull;
   STAMP(st.refine);
 
-  // ---- results of this group
+  // ---- results of this group (64-bit keys: cost << 32 | rank)
   tid = opaque_tid();
+  if (tick && tid == 0) *s_tick = tk;
   if (tid < kNS && ((gmask >> tid) & 1)) {
-    const unsigned long long k = (KEY32 && tid == 0 && fb16) ? k16 : L.red[tid];
-    uint32_t rank = 0, cost = 0;
-    bool found = false;
-    if (KEY32 && !(tid == 0 && fb16)) {
-      const uint32_t key = (uint32_t)k;
-      if (key != ~0u) {
-        for (int j = 0; j < kCand && !found; ++j)
-          if (L.match[tid * kCand + j]) {
-            found = true;
-            rank = ((key & ((1u << kCostShift) - 1)) << kRankDrop) + j;
-          }
-        cost = key >> kCostShift;
-        if (!found) atomicOr(&p.counts[2], 4u);   // cannot happen: refine lost the winner
-      }
-    } else if (k != ~0ull) {
-      found = true;
-      rank = (uint32_t)(k & 0x7fffffffu);
-      cost = (uint32_t)(k >> 32);
-    }
-    p.out[(size_t)u * kNS + tid] = block_result<FFS>(g, found, rank, cost);
+    const unsigned long long k = L.red[tid];
+    p.out[(size_t)u * kNS + tid] =
+        block_result<FFS>(g, k != ~0ull, (uint32_t)(k & 0x7fffffffu), (uint32_t)(k >> 32));
   }
   STAMP(st.out);
 }
@@ -1137,19 +1169,33 @@ __device__ __forceinline__ Item load_item(const Item *items, unsigned j) {
 }
 
 // Persistent item kernel.  The KEY32 instance drains the 32-bit list, the
-// other the 64-bit list.  Items are dealt to XCD x (= blockIdx % 8) as the
-// contiguous run [x*cnt/8, (x+1)*cnt/8), strided over that XCD's workgroups.
+// other the 64-bit list.  XCD x (= blockIdx % 8) serves the contiguous run
+// [x*cnt/8, (x+1)*cnt/8) of the items (neighbouring macroblocks' windows
+// overlap in its L2).  Inside the run the first two items of each workgroup
+// are static (start + lb, start + lb + nbx); the rest are dealt by tickets,
+// one atomic per item on the XCD's counter: the workgroups resident on one CU
+// do not progress at the same rate (the oldest wave wins the SIMD's issue
+// arbitration: on MI355X a CU's four workgroups finished equal static shares
+// at 131, 171, 220 and 257 us), so a static deal leaves CUs with one or two
+// workgroups for the last third of the launch.  A workgroup takes its ticket
+// for the item after next while it serves an item, so the index is in LDS by
+// the next item's first barrier.  Every ticket below the run's end is served by
+// the workgroup that drew it: tickets are only drawn while a next item exists.
 template <bool KEY32, bool FFS>
 __global__ __launch_bounds__(kWG, KEY32 ? JMME_WAVES_PER_EU : 2) void me_items_kernel(KParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ __attribute__((aligned(16))) uint32_t s_cur[64];
+  __shared__ unsigned s_tick;
   const unsigned cnt = (unsigned)p.n + p.counts[0];   // first groups, then the further groups
   const Item *items = p.items;
   const int x = blockIdx.x & 7, lb = blockIdx.x >> 3, nbx = (gridDim.x - x + 7) >> 3;
   const unsigned start = (unsigned)(((unsigned long long)cnt * x) >> 3);
   const unsigned end = (unsigned)(((unsigned long long)cnt * (x + 1)) >> 3);
-  unsigned j = start + lb;
+  const unsigned j = start + lb;
   if (j >= end) return;
+  unsigned jn = j + nbx;                                  // the second item (static)
+  const unsigned dyn0 = start + 2u * (unsigned)nbx;       // ticket t serves item dyn0 + t
+  unsigned *const tick = p.counts + 8 + x;
 
   Lds L = carve(smem, p.lds_range);
   L.cur = s_cur;
@@ -1161,18 +1207,25 @@ __global__ __launch_bounds__(kWG, KEY32 ? JMME_WAVES_PER_EU : 2) void me_items_k
 
   Item it = load_item(items, j);
   prefetch(p, it, L);
-  for (;;) {
+#ifdef JMME_STAMPS
+  // per-workgroup record behind the per-unit ones: start / end (s_memrealtime,
+  // 100 MHz), HW_ID, XCC_ID, items served
+  const unsigned long long wg_t0 = __builtin_amdgcn_s_memrealtime();
+  unsigned wg_items = 0;
+#endif
+  for (bool first = true;; first = false) {
 #ifdef JMME_STAMPS
     ItemStamps<KEY32, FFS> st;
 #endif
-    const unsigned jn = j + nbx;
+    // this item's fetch has landed (every wave waits for its own loads, the
+    // barrier for everyone's); the previous item is completely done with LDS,
+    // and the ticket it drew is visible
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (!first) jn = dyn0 + (unsigned)ufl((int)s_tick);
     const bool more = jn < end;
     Item nx;
     if (more) nx = load_item(items, jn);
-    // this item's fetch has landed (every wave waits for its own loads, the
-    // barrier for everyone's); the previous item is completely done with LDS
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
     STAMP(st.wait);
     const bool fast = it.gmask && item_fast<KEY32, FFS>(p, it);
     if (it.gmask) expand(p, it, L);
@@ -1188,6 +1241,7 @@ __global__ __launch_bounds__(kWG, KEY32 ? JMME_WAVES_PER_EU : 2) void me_items_k
     STAMP(st.expand);
     // the raw buffer is free: start fetching the next item behind this sweep
     if (more) prefetch(p, nx, L);
+    bool ticketed = false;
     if (it.gmask) {
       // the current MB into SGPRs: every v_sad of the v5 sweep takes it as
       // its scalar operand
@@ -1200,13 +1254,15 @@ __global__ __launch_bounds__(kWG, KEY32 ? JMME_WAVES_PER_EU : 2) void me_items_k
       if (KEY32 && (it.flags & kItemSlow64)) {
         search_item_slow64<FFS>(p, it, L);
       } else {
+        ticketed = true;
 #ifdef JMME_STAMPS
-        search_item<KEY32, FFS>(p, it, L, fast, cs, t_last, st);
+        search_item<KEY32, FFS>(p, it, L, fast, cs, more ? tick : nullptr, &s_tick, t_last, st);
 #else
-        search_item<KEY32, FFS>(p, it, L, fast, cs);
+        search_item<KEY32, FFS>(p, it, L, fast, cs, more ? tick : nullptr, &s_tick);
 #endif
       }
     }
+    if (more && !ticketed && threadIdx.x == 0) s_tick = atomicAdd(tick, 1u);
 #ifdef JMME_STAMPS
     if (p.stamps && threadIdx.x == 0) {
       unsigned long long *o = p.stamps + (size_t)it.u * 8;
@@ -1214,11 +1270,20 @@ __global__ __launch_bounds__(kWG, KEY32 ? JMME_WAVES_PER_EU : 2) void me_items_k
       atomicAdd(o + 3, st.reduce); atomicAdd(o + 4, st.refine); atomicAdd(o + 5, st.out);
       atomicAdd(o + 6, (unsigned long long)__builtin_popcountll(it.gmask)); atomicAdd(o + 7, 1ull);
     }
+    ++wg_items;
 #endif
     if (!more) break;
     it = nx;
-    j = jn;
   }
+#ifdef JMME_STAMPS
+  if (p.stamps && threadIdx.x == 0) {
+    unsigned hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    unsigned long long *o = p.stamps + (size_t)p.n * 8 + (size_t)blockIdx.x * 4;
+    o[0] = wg_t0; o[1] = __builtin_amdgcn_s_memrealtime(); o[2] = hw; o[3] = ((unsigned long long)xcc << 32) | wg_items;
+  }
+#endif
 }
 
 struct Occupancy {
