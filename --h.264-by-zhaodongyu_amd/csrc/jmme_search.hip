@@ -418,6 +418,18 @@ __device__ __forceinline__ Win win_of(const KParams &p, const Item &it) {
   return w;
 }
 
+// One LDS-DMA dword per lane: lane l's dword lands at LDS byte address
+// lds + 4*l (lds wave-uniform, in M0).  Issued from inline asm on purpose:
+// with the builtin (__builtin_amdgcn_global_load_lds) the compiler tracks the
+// pending DMA and, for every LDS read that follows while it is in flight, waits
+// with lgkmcnt(0) -- which undoes the sweep's one-row-ahead pipelining (each
+// wait then covers the reads just issued for the next row).  Completion of these
+// loads is awaited explicitly (s_waitcnt vmcnt(0) + barrier at the top of the
+// next item) before anything reads the destination.
+__device__ __forceinline__ void lds_dma_dword(const void *gptr, uint32_t lds) {
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(gptr), "s"(lds) : "memory", "m0");
+}
+
 // Issue the HBM -> LDS fetch of item `it` (window rows clamped into the
 // picture, dword columns clamped into it -- UMVLine4X) and its current MB.  global_load_lds: per-lane global address, LDS destination
 // contiguous per wave instruction; completion is awaited (vmcnt) only at the
@@ -440,14 +452,13 @@ __device__ __forceinline__ void prefetch(const KParams &p, const Item &it, const
     const int rr = r + dr;
     if (act && rr < w.wrows) {
       const int gy = clampi(w.y0 + rr, 0, p.height - 1);
-      __builtin_amdgcn_global_load_lds(col + (size_t)gy * p.pitch, L.raw + r * w.nd, 4, 0, 0);
+      lds_dma_dword(col + (size_t)gy * p.pitch, (uint32_t)ufl((int)lds_addr(L.raw + r * w.nd)));
     }
   }
   // behind the window: the current MB (wave 0)
   if (wave == 0) {
     const int r = lane >> 2, c = lane & 3;
-    __builtin_amdgcn_global_load_lds(p.cur + (size_t)(it.mb_y + r) * p.pitch + it.mb_x + 4 * c, L.raw + total, 4, 0,
-                                     0);
+    lds_dma_dword(p.cur + (size_t)(it.mb_y + r) * p.pitch + it.mb_x + 4 * c, (uint32_t)ufl((int)lds_addr(L.raw + total)));
   }
 }
 
@@ -615,7 +626,9 @@ __device__ __forceinline__ void sweep_v5(const Lds &L, const uint32_t (&cs)[64],
   const int ntask = D * DT;
   const int off = R - rs;
   const int qstep = kWG / D, rstep = kWG - qstep * D;
-  int tx = tid % D, tq = tid / D;        // task column, triple row
+  // tid / D by a multiply: exact for tid * D < 2^16 (tid < 256, D <= 89)
+  const unsigned dm = (65536u + (unsigned)D - 1u) / (unsigned)D;
+  int tq = (int)(((unsigned)tid * dm) >> 16), tx = tid - tq * D;   // task column, triple row
   const uint32_t rowb = 4u * (uint32_t)L.wp;
   for (int t = tid; t < ntask; t += kWG) {
     const int y0 = min(3 * tq, D - 3);
@@ -631,14 +644,22 @@ __device__ __forceinline__ void sweep_v5(const Lds &L, const uint32_t (&cs)[64],
     }
     uint32_t a[3][16];
     const uint32_t wrow = lds_addr(L.words) + 4u * (uint32_t)((off + y0) * L.wp + off + tx);
+#ifdef JMME_ABL_NOLDS    // timing ablation only: no window reads
+    u32x2 n01 = u32x2{wrow, wrow ^ 1u}, n23 = u32x2{wrow ^ 2u, wrow ^ 3u};
+#else
     u32x2 n01 = ds_read2_0_4(wrow), n23 = ds_read2_8_12(wrow);
+#endif
 #pragma unroll
     for (int r = 0; r < 18; ++r) {
       const u32x2 w01 = n01, w23 = n23;
       if (r < 17) {
         const uint32_t ad = wrow + (uint32_t)(r + 1) * rowb;
+#ifdef JMME_ABL_NOLDS
+        n01 = u32x2{ad, ad ^ 5u}; n23 = u32x2{ad ^ 6u, ad ^ 7u};
+#else
         n01 = ds_read2_0_4(ad);
         n23 = ds_read2_8_12(ad);
+#endif
       }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -654,6 +675,12 @@ __device__ __forceinline__ void sweep_v5(const Lds &L, const uint32_t (&cs)[64],
       }
       __builtin_amdgcn_sched_barrier(0);
     }
+#ifdef JMME_ABL_NOFOLD   // timing ablation only: keep the 4x4 keys live, no partition keys / minima
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+      for (int k = 0; k < 16; ++k) asm volatile("" :: "v"(a[j][k]));
+#else
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
       uint32_t ps[kNS];
@@ -661,6 +688,7 @@ __device__ __forceinline__ void sweep_v5(const Lds &L, const uint32_t (&cs)[64],
 #pragma unroll
       for (int s = 0; s < kNS; ++s) best[s] = min(best[s], ps[s]);
     }
+#endif
     tx += rstep;
     tq += qstep;
     if (tx >= D) { tx -= D; ++tq; }
@@ -1103,7 +1131,9 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
       fb16 = k0 == ~0u;
     }
     STAMP(st.reduce);
+#ifndef JMME_ABL_NOREFINE   // timing ablation only: no refine / output
     refine_output32<FFS>(p, g, L, spec, fb16, u);
+#endif
     if (tick && opaque_tid() == 0) *s_tick = tk;
     STAMP(st.refine);
     if (fb16) {   // search the 16x16 again with exact keys
@@ -1158,13 +1188,20 @@ __device__ __forceinline__ void search_item_slow64(const KParams &p, const Item 
   }
 }
 
-// item descriptors are wave-uniform: keep every field in SGPRs
+// Wave-uniform loads through the scalar data cache (s_load): the constant
+// address space tells the compiler the bytes do not change during the kernel.
+// For data another launch (or the host) wrote before this one started.
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(4))) const v4i const_v4i;
+__device__ __forceinline__ v4i sload16(const void *p) { return *reinterpret_cast<const_v4i *>((uintptr_t)p); }
+
+// item descriptors are wave-uniform: keep every field in SGPRs (the plan
+// kernel wrote them in the previous launch)
 __device__ __forceinline__ Item load_item(const Item *items, unsigned j) {
-  const int *src = reinterpret_cast<const int *>(items + j);
   Item it;
-  int *dst = reinterpret_cast<int *>(&it);
+  v4i *dst = reinterpret_cast<v4i *>(&it);
 #pragma unroll
-  for (int k = 0; k < (int)(sizeof(Item) / 4); ++k) dst[k] = ufl(src[k]);
+  for (int k = 0; k < (int)(sizeof(Item) / 16); ++k) dst[k] = sload16(reinterpret_cast<const v4i *>(items + j) + k);
   return it;
 }
 
@@ -1228,7 +1265,9 @@ __global__ __launch_bounds__(kWG, KEY32 ? JMME_WAVES_PER_EU : 2) void me_items_k
     if (more) nx = load_item(items, jn);
     STAMP(st.wait);
     const bool fast = it.gmask && item_fast<KEY32, FFS>(p, it);
+#ifndef JMME_ABL_NOEXPAND   // timing ablation only: the window stays as the previous item left it
     if (it.gmask) expand(p, it, L);
+#endif
     if (fast) build_tabs<FFS>(it, L);
     __syncthreads();
     if (p.debug_words && it.u == 0 && (it.gmask & dbg_slot)) {
@@ -1247,9 +1286,14 @@ __global__ __launch_bounds__(kWG, KEY32 ? JMME_WAVES_PER_EU : 2) void me_items_k
       // its scalar operand
       uint32_t cs[64];
       {
-        const uint32_t v = L.cur[threadIdx.x & 63];
+        // straight from the current picture (s_load_dwordx4 per MB row)
+        const uint8_t *mb = p.cur + (size_t)it.mb_y * p.pitch + it.mb_x;
 #pragma unroll
-        for (int i = 0; i < 64; ++i) cs[i] = __builtin_amdgcn_readlane(v, i);
+        for (int r = 0; r < 16; ++r) {
+          const v4i q = sload16(mb + (size_t)r * p.pitch);
+          cs[4 * r + 0] = (uint32_t)q.x; cs[4 * r + 1] = (uint32_t)q.y;
+          cs[4 * r + 2] = (uint32_t)q.z; cs[4 * r + 3] = (uint32_t)q.w;
+        }
       }
       if (KEY32 && (it.flags & kItemSlow64)) {
         search_item_slow64<FFS>(p, it, L);

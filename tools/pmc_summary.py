@@ -13,7 +13,7 @@ ap.add_argument("--traffic-json")
 a_ = ap.parse_args()
 root, kern, out_json = a_.root, a_.kernel, a_.traffic_json
 means = {}
-for f in sorted(glob.glob(os.path.join(root, "*", "**", "*counter_collection.csv"), recursive=True)):
+for f in sorted(set(glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True))):
     agg = collections.defaultdict(list)
     for r in csv.DictReader(open(f)):
         if kern in r["Kernel_Name"]:
