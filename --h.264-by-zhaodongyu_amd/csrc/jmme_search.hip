@@ -85,13 +85,13 @@ struct Lds {
   uint32_t *cur;            // 64 words: MB row r, column group c at [r*4+c] (static LDS)
   unsigned long long *red;  // kWaves x 41 reduction scratch
   uint4 *tx, *ty;           // per-item position tables (2R+1 each), see build_tabs
-  uint32_t *spec;           // 16 4x4 SADs at the special (0,0) candidate
+  uint32_t *spec;           // 16 4x4 SADs at the special (0,0) candidate, then its 41 keys
   unsigned long long *fb;   // exact 16x16 result of the saturation fallback
 };
 
 // words per window row in LDS: the 2R+13 words a row needs, rounded up to the
-// expand's groups of 4 (it writes whole groups), odd for bank spread
-__host__ __device__ inline int words_pitch(int R) { return 4 * ((2 * R + 13 + 3) / 4) + 1; }
+// expand's groups of 4 (it writes whole groups, 16-B aligned: one ds_write_b128)
+__host__ __device__ inline int words_pitch(int R) { return 4 * ((2 * R + 13 + 3) / 4); }
 
 // one layout for the kernel (carve) and the host (items_lds_bytes)
 struct LdsPlan { size_t words, raw, red, tx, ty, spec, fb, total; };
@@ -105,7 +105,7 @@ __host__ __device__ inline LdsPlan lds_plan(int R) {
   q.red = take((size_t)kWaves * kNS * 8);
   q.tx = take((size_t)d * 16);
   q.ty = take((size_t)d * 16);
-  q.spec = take(16 * 4);
+  q.spec = take((16 + kNS) * 4);
   q.fb = take(kWaves * 8);
   q.total = off;
   return q;
@@ -476,12 +476,13 @@ __device__ __forceinline__ void expand_inner(const uint32_t *src, uint32_t *dst,
     const int rn = r + rstep;
     uint32_t e0 = 0, e1 = 0, e2 = 0;
     if (rn < wrows) { e0 = src[rn * nd]; e1 = src[rn * nd + 1]; e2 = src[rn * nd + 2]; }
-    uint32_t *o = dst + r * wp;
+    u32x4 v;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int b = k + SH;   // byte offset of word 4g+k from dword g (0..6), compile-time
-      o[k] = b < 4 ? __builtin_amdgcn_alignbyte(d1, d0, b & 3) : __builtin_amdgcn_alignbyte(d2, d1, b & 3);
+      v[k] = b < 4 ? __builtin_amdgcn_alignbyte(d1, d0, b & 3) : __builtin_amdgcn_alignbyte(d2, d1, b & 3);
     }
+    *reinterpret_cast<u32x4 *>(dst + r * wp) = v;   // ds_write_b128 (conflict-free: consecutive lanes, consecutive 16 B)
     if (rn >= wrows) break;
     r = rn; d0 = e0; d1 = e1; d2 = e2;
   }
@@ -496,7 +497,8 @@ __device__ __forceinline__ void expand(const KParams &p, const Item &it, const L
   // (L.wp >= 4*ng: the words past wpr of the last group are scratch)
   const int ng = (w.wpr + 3) >> 2;          // word groups per row
   const int rstep = kWG / ng;               // rows per pass
-  const int r0 = tid / ng, g = tid - r0 * ng;
+  const int r0 = (int)(((unsigned)tid * ((65536u + (unsigned)ng - 1u) / (unsigned)ng)) >> 16);   // tid / ng (tid * ng < 2^16)
+  const int g = tid - r0 * ng;
   if (r0 >= rstep) return;
   uint32_t *dst = L.words + 4 * g;
   if (w.inner) {
@@ -533,9 +535,10 @@ __device__ __forceinline__ void expand(const KParams &p, const Item &it, const L
     }
     for (int r = r0; r < w.wrows; r += rstep) {
       const uint32_t *rw = L.raw + r * w.nd;
-      uint32_t *o = dst + r * L.wp;
+      u32x4 v;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) o[k] = __builtin_amdgcn_perm(rw[dq[k] + 1], rw[dq[k]], sel[k]);
+      for (int k = 0; k < 4; ++k) v[k] = __builtin_amdgcn_perm(rw[dq[k] + 1], rw[dq[k]], sel[k]);
+      *reinterpret_cast<u32x4 *>(dst + r * L.wp) = v;
     }
   }
 }
@@ -698,8 +701,8 @@ __device__ __forceinline__ void sweep_v5(const Lds &L, const uint32_t (&cs)[64],
 // JM's special (0,0) candidate, once per item instead of per position: FS
 // check_for_00 (slot 0 at (0,0) costs mvcost - 16*lambda, me_fullsearch.c:61,
 // 78-82) and the FFS pre-seed (every partition, rank 0, me_fullfast.c:650-657).
-// Its 4x4 SADs are taken before the sweep (special_sads, wave 0) and its exact
-// key joins the reduced minima in the reduce's combine step (special_key), so
+// Its keys are formed before the sweep (special_keys, wave 0) and join the
+// reduced minima where the reduce's per-wave minima are combined, so
 // it adds no barrier; the sweep's own key for that position is never below it.
 template <bool FFS>
 __device__ __forceinline__ bool special_on(const GroupCtx &g) {
@@ -707,18 +710,6 @@ __device__ __forceinline__ bool special_on(const GroupCtx &g) {
   const bool inside = abs(ox) <= g.R && abs(oy) <= g.R;
   if (FFS) return g.preseed && inside && mv_cost<FFS>(0, 0, g.px, g.py, g.lam, g.max_mvd).ok;
   return g.chk00 && (g.gmask & 1) && inside;
-}
-
-__device__ __forceinline__ void special_sads(const GroupCtx &g, const Lds &L, int tid) {
-  if (tid < 16) {
-    const int ox = -(g.cqx >> 2), oy = -(g.cqy >> 2);
-    const int bx = tid & 3, by = tid >> 2;
-    const uint32_t *w = L.words + (oy + g.R + 4 * by) * L.wp + ox + g.R + 4 * bx;
-    uint32_t sad = 0;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) sad = __builtin_amdgcn_sad_u8(w[r * L.wp], L.cur[(4 * by + r) * 4 + bx], sad);
-    L.spec[tid] = sad;
-  }
 }
 
 // the special candidate's 32-bit key for slot s (~0u when it is not one)
@@ -735,6 +726,23 @@ __device__ __forceinline__ uint32_t special_key(const GroupCtx &g, const Lds &L,
   const uint32_t rank = FFS ? 0u : (uint32_t)spiral_index_bl(ox, oy);
   const uint32_t cost = (sad << 5) + mvc;
   return cost < (1u << (32 - kCostShift)) ? (cost << kCostShift) | (rank >> kRankDrop) : ~0u;
+}
+
+// Wave 0, before the sweep: the special candidate's 16 4x4 SADs, then its key
+// for every slot into L.spec[16 + s] (one wave: its LDS writes land before its
+// own later reads, no barrier); read back after the reduce's barrier.
+template <bool FFS>
+__device__ __forceinline__ void special_keys(const GroupCtx &g, const Lds &L, int tid) {
+  if (tid < 16) {
+    const int ox = -(g.cqx >> 2), oy = -(g.cqy >> 2);
+    const int bx = tid & 3, by = tid >> 2;
+    const uint32_t *w = L.words + (oy + g.R + 4 * by) * L.wp + ox + g.R + 4 * bx;
+    uint32_t sad = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sad = __builtin_amdgcn_sad_u8(w[r * L.wp], L.cur[(4 * by + r) * 4 + bx], sad);
+    L.spec[tid] = sad;
+  }
+  if (tid < kNS) L.spec[16 + tid] = special_key<FFS>(g, L, tid);
 }
 
 // Exact search of one partition with 64-bit keys (cost << 32 | rank), every
@@ -828,7 +836,7 @@ __device__ __forceinline__ void refine_output32(const KParams &p, const GroupCtx
   if (mine) {
 #pragma unroll
     for (int w = 0; w < kWaves; ++w) key = min(key, (uint32_t)L.red[w * kNS + s]);
-    if (spec) key = min(key, special_key<FFS>(g, L, s));
+    if (spec) key = min(key, L.spec[16 + s]);
   }
   // candidate j: its window offset, or none
   const int R = g.R, D = 2 * R + 1;
@@ -871,12 +879,13 @@ __device__ __forceinline__ void refine_output32(const KParams &p, const GroupCtx
   if (exists && q == 0) {
     const int candx = g.cqx + 4 * ox, candy = g.cqy + 4 * oy;
     const bool is00 = (candx == 0) && (candy == 0);
-    const int sidx = spiral_index_bl(ox, oy);
-    const uint32_t rank = FFS ? ((g.preseed && is00) ? 0u : (uint32_t)sidx + 1u) : (uint32_t)sidx;
+    // the decoded position's rank is rk, except that under an FFS pre-seed the
+    // (0,0) vector ranks 0 (me_fullfast.c:650-657) whatever its spiral index
+    const bool rank_ok = !FFS || !(g.preseed && is00) || rk == 0;
     const MvCost mc = mv_cost<FFS>(candx, candy, g.px, g.py, g.lam, g.max_mvd);
     const bool ok = pos_eligible<FFS>(g, mc.ok, max(abs(ox), abs(oy)), is00);
     const uint32_t mv = (s == 0 && g.chk00) ? check00_adjust(mc.mvc, g.lam, is00) : mc.mvc;
-    m = rank == (uint32_t)rk && (sad << 5) + mv == (key >> kCostShift) && ok;
+    m = rank_ok && (sad << 5) + mv == (key >> kCostShift) && ok;
   }
   const unsigned long long M = __builtin_amdgcn_ballot_w64(m);
   const int base = lane - q - j * nq;   // leader lane of (s, candidate 0)
@@ -1063,7 +1072,7 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
   // per-partition masks in the loop)
   const bool spec = KEY32 && fast && special_on<FFS>(g);
   if (KEY32 && fast) {
-    if (spec) special_sads(g, L, tid);   // read back after the reduce's first barrier
+    if (spec && wave == 0) special_keys<FFS>(g, L, tid);   // read back after the reduce's barrier
     if constexpr (KEY32) sweep_v5(L, cs, R, g.rs, best);
   } else {
     sweep(std::integral_constant<bool, true>{});
@@ -1078,7 +1087,11 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
   // LDS once the reduce and refine have hidden the atomic's round trip
   unsigned tk = 0;
   if (tick && tid == 0) tk = atomicAdd(tick, 1u);
+#ifdef JMME_ABL_NOREDUCE   // timing ablation only: no cross-lane reduction
+  if (KEY32 && false) {
+#else
   if (KEY32) {
+#endif
     // reduce-scatter through the wave: permlane32_swap pairs slots (lanes
     // 0-31 keep one, 32-63 the other), permlane16_swap pairs again (one slot
     // per row of 16), four DPP steps finish each row -- 11 registers carry
@@ -1127,7 +1140,7 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
       uint32_t k0 = ~0u;
 #pragma unroll
       for (int w = 0; w < kWaves; ++w) k0 = min(k0, (uint32_t)L.red[w * kNS]);
-      if (spec) k0 = min(k0, special_key<FFS>(g, L, 0));
+      if (spec) k0 = min(k0, L.spec[16]);
       fb16 = k0 == ~0u;
     }
     STAMP(st.reduce);
@@ -1149,7 +1162,7 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
     unsigned long long k = L.red[tid];
 #pragma unroll
     for (int w = 1; w < kWaves; ++w) { const unsigned long long o = L.red[w * kNS + tid]; k = o < k ? o : k; }
-    if (spec) k = min(k, (unsigned long long)special_key<FFS>(g, L, tid));
+    if (spec) k = min(k, (unsigned long long)L.spec[16 + tid]);
     L.red[tid] = k;   // wave 0's row now holds the group result
   }
   __syncthreads();
