@@ -90,8 +90,11 @@ struct Lds {
 };
 
 // words per window row in LDS: the 2R+13 words a row needs, rounded up to the
-// expand's groups of 4 (it writes whole groups, 16-B aligned: one ds_write_b128)
-__host__ __device__ inline int words_pitch(int R) { return 4 * ((2 * R + 13 + 3) / 4); }
+// expand's groups of 4 (it writes whole groups, 16-B aligned: one ds_write_b128);
+// every launch up to R = 32 uses the R = 32 pitch, a compile-time constant of
+// the sweep (its row offsets then fold into the ds_read2 offset fields)
+constexpr int kWP32 = 80;
+__host__ __device__ inline int words_pitch(int R) { return R <= 32 ? kWP32 : 4 * ((2 * R + 13 + 3) / 4); }
 
 // one layout for the kernel (carve) and the host (items_lds_bytes)
 struct LdsPlan { size_t words, raw, red, tx, ty, spec, fb, total; };
@@ -621,6 +624,7 @@ __device__ __forceinline__ void partition_keys(const uint32_t (&a)[16], uint32_t
 // A task is a vertical triple of positions (x, y..y+2); the 18 window rows
 // they need are read once; row r meets MB row r - j of position j.  The
 // current MB comes from SGPRs (cs), so the only LDS traffic is the window.
+template <int WP>   // words pitch when known at compile time (kWP32), else 0 (L.wp)
 __device__ __forceinline__ void sweep_v5(const Lds &L, const uint32_t (&cs)[64], int R, int rs,
                                          uint32_t (&best)[kNS]) {
   const int tid = opaque_tid();
@@ -632,7 +636,7 @@ __device__ __forceinline__ void sweep_v5(const Lds &L, const uint32_t (&cs)[64],
   // tid / D by a multiply: exact for tid * D < 2^16 (tid < 256, D <= 89)
   const unsigned dm = (65536u + (unsigned)D - 1u) / (unsigned)D;
   int tq = (int)(((unsigned)tid * dm) >> 16), tx = tid - tq * D;   // task column, triple row
-  const uint32_t rowb = 4u * (uint32_t)L.wp;
+  const int wp = WP ? WP : L.wp;
   for (int t = tid; t < ntask; t += kWG) {
     const int y0 = min(3 * tq, D - 3);
     uint32_t K[3];
@@ -646,23 +650,21 @@ __device__ __forceinline__ void sweep_v5(const Lds &L, const uint32_t (&cs)[64],
       }
     }
     uint32_t a[3][16];
-    const uint32_t wrow = lds_addr(L.words) + 4u * (uint32_t)((off + y0) * L.wp + off + tx);
-#ifdef JMME_ABL_NOLDS    // timing ablation only: no window reads
-    u32x2 n01 = u32x2{wrow, wrow ^ 1u}, n23 = u32x2{wrow ^ 2u, wrow ^ 3u};
-#else
-    u32x2 n01 = ds_read2_0_4(wrow), n23 = ds_read2_8_12(wrow);
-#endif
+    // one base per task; every read carries its row / column as the 16-bit
+    // offset of a single ds_read_b32 (volatile: not merged into ds_read2, whose
+    // 8-bit offsets cannot reach past row 3, so each row would cost an add).
+    // The base's sign bit is provably clear, which the compiler requires before
+    // it folds DS offsets.
+    const uint32_t wbase = (lds_addr(L.words) + 4u * (uint32_t)((off + y0) * wp + off + tx)) & 0x7fffffffu;
+    const lds_u32 *wrow = reinterpret_cast<const lds_u32 *>((uintptr_t)wbase);
+    u32x2 n01 = u32x2{wrow[0], wrow[4]}, n23 = u32x2{wrow[8], wrow[12]};
 #pragma unroll
     for (int r = 0; r < 18; ++r) {
       const u32x2 w01 = n01, w23 = n23;
       if (r < 17) {
-        const uint32_t ad = wrow + (uint32_t)(r + 1) * rowb;
-#ifdef JMME_ABL_NOLDS
-        n01 = u32x2{ad, ad ^ 5u}; n23 = u32x2{ad ^ 6u, ad ^ 7u};
-#else
-        n01 = ds_read2_0_4(ad);
-        n23 = ds_read2_8_12(ad);
-#endif
+        const lds_u32 *ad = wrow + (r + 1) * wp;
+        n01 = u32x2{ad[0], ad[4]};
+        n23 = u32x2{ad[8], ad[12]};
       }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -1073,7 +1075,10 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
   const bool spec = KEY32 && fast && special_on<FFS>(g);
   if (KEY32 && fast) {
     if (spec && wave == 0) special_keys<FFS>(g, L, tid);   // read back after the reduce's barrier
-    if constexpr (KEY32) sweep_v5(L, cs, R, g.rs, best);
+    if constexpr (KEY32) {
+      if (L.wp == kWP32) sweep_v5<kWP32>(L, cs, R, g.rs, best);
+      else sweep_v5<0>(L, cs, R, g.rs, best);
+    }
   } else {
     sweep(std::integral_constant<bool, true>{});
   }
