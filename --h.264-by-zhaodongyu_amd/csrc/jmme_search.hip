@@ -66,6 +66,9 @@ constexpr int kPlanWaves = 16;             // plan kernel: units per workgroup
 constexpr int kRed1 = (kNS + 3) / 4 * 2;      // reduce: registers after the permlane32 level (22)
 constexpr int kRed2 = kRed1 / 2;              //         ... after the permlane16 level (11)
 
+#ifndef JMME_SWEEP_P
+#define JMME_SWEEP_P 3   // positions per sweep task (vertical run)
+#endif
 #ifndef JMME_WAVES_PER_EU
 #define JMME_WAVES_PER_EU 4
 #endif
@@ -621,54 +624,52 @@ __device__ __forceinline__ void partition_keys(const uint32_t (&a)[16], uint32_t
 }
 
 // The v5 sweep of the sub-window [-rs, rs]^2 (rs >= 1) of the staged window.
-// A task is a vertical triple of positions (x, y..y+2); the 18 window rows
+// A task is a vertical run of P positions (x, y..y+P-1); the 15+P window rows
 // they need are read once; row r meets MB row r - j of position j.  The
 // current MB comes from SGPRs (cs), so the only LDS traffic is the window.
-template <int WP>   // words pitch when known at compile time (kWP32), else 0 (L.wp)
+template <int WP, int P>   // WP: words pitch when known at compile time (kWP32), else 0 (L.wp)
 __device__ __forceinline__ void sweep_v5(const Lds &L, const uint32_t (&cs)[64], int R, int rs,
                                          uint32_t (&best)[kNS]) {
   const int tid = opaque_tid();
   const int D = 2 * rs + 1;
-  const int DT = (D + 2) / 3;            // triples per column (the last one shifted up)
+  const int DT = (D + P - 1) / P;        // tasks per column (the last one shifted up)
   const int ntask = D * DT;
   const int off = R - rs;
   const int qstep = kWG / D, rstep = kWG - qstep * D;
   // tid / D by a multiply: exact for tid * D < 2^16 (tid < 256, D <= 89)
   const unsigned dm = (65536u + (unsigned)D - 1u) / (unsigned)D;
-  int tq = (int)(((unsigned)tid * dm) >> 16), tx = tid - tq * D;   // task column, triple row
+  int tq = (int)(((unsigned)tid * dm) >> 16), tx = tid - tq * D;   // task column, task row
   const int wp = WP ? WP : L.wp;
   for (int t = tid; t < ntask; t += kWG) {
-    const int y0 = min(3 * tq, D - 3);
-    uint32_t K[3];
+    const int y0 = min(P * tq, D - P);
+    uint32_t K[P];
     {
       const u32x4 cx = ds_read_b128(lds_addr(L.tx) + 16u * (uint32_t)tx);
 #pragma unroll
-      for (int j = 0; j < 3; ++j) {
+      for (int j = 0; j < P; ++j) {
         const u32x4 cy = ds_read_b128(lds_addr(L.ty) + 16u * (uint32_t)(y0 + j));
         const uint32_t rk = cy.z > cx.z ? cy.y + cx.w : cx.y + cy.w;
         K[j] = cx.x + cy.x + (rk >> kRankDrop);
       }
     }
-    uint32_t a[3][16];
-    // one base per task; every read carries its row / column as the 16-bit
-    // offset of a single ds_read_b32 (volatile: not merged into ds_read2, whose
-    // 8-bit offsets cannot reach past row 3, so each row would cost an add).
-    // The base's sign bit is provably clear, which the compiler requires before
-    // it folds DS offsets.
+    uint32_t a[P][16];
+    // the row base with its sign bit provably clear: the compiler only folds DS
+    // offsets onto a base known to be non-negative, and with the compile-time
+    // pitch the row offsets then ride in the ds_read2 offset fields
     const uint32_t wbase = (lds_addr(L.words) + 4u * (uint32_t)((off + y0) * wp + off + tx)) & 0x7fffffffu;
     const lds_u32 *wrow = reinterpret_cast<const lds_u32 *>((uintptr_t)wbase);
     u32x2 n01 = u32x2{wrow[0], wrow[4]}, n23 = u32x2{wrow[8], wrow[12]};
 #pragma unroll
-    for (int r = 0; r < 18; ++r) {
+    for (int r = 0; r < 15 + P; ++r) {
       const u32x2 w01 = n01, w23 = n23;
-      if (r < 17) {
+      if (r < 14 + P) {
         const lds_u32 *ad = wrow + (r + 1) * wp;
         n01 = u32x2{ad[0], ad[4]};
         n23 = u32x2{ad[8], ad[12]};
       }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int j = 0; j < 3; ++j) {
+      for (int j = 0; j < P; ++j) {
         const int mr = r - j;
         if (mr < 0 || mr > 15) continue;
         const int b = (mr >> 2) * 4;
@@ -682,16 +683,24 @@ __device__ __forceinline__ void sweep_v5(const Lds &L, const uint32_t (&cs)[64],
     }
 #ifdef JMME_ABL_NOFOLD   // timing ablation only: keep the 4x4 keys live, no partition keys / minima
 #pragma unroll
-    for (int j = 0; j < 3; ++j)
+    for (int j = 0; j < P; ++j)
 #pragma unroll
       for (int k = 0; k < 16; ++k) asm volatile("" :: "v"(a[j][k]));
 #else
+    // positions in pairs: both keys of a partition fold with one v_min3_u32
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      uint32_t ps[kNS];
-      partition_keys(a[j], K[j], ps);
+    for (int j = 0; j + 1 < P; j += 2) {
+      uint32_t p0[kNS], p1[kNS];
+      partition_keys(a[j], K[j], p0);
+      partition_keys(a[j + 1], K[j + 1], p1);
 #pragma unroll
-      for (int s = 0; s < kNS; ++s) best[s] = min(best[s], ps[s]);
+      for (int s = 0; s < kNS; ++s) best[s] = min(best[s], min(p0[s], p1[s]));
+    }
+    if (P & 1) {
+      uint32_t p0[kNS];
+      partition_keys(a[P - 1], K[P - 1], p0);
+#pragma unroll
+      for (int s = 0; s < kNS; ++s) best[s] = min(best[s], p0[s]);
     }
 #endif
     tx += rstep;
@@ -1076,8 +1085,8 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
   if (KEY32 && fast) {
     if (spec && wave == 0) special_keys<FFS>(g, L, tid);   // read back after the reduce's barrier
     if constexpr (KEY32) {
-      if (L.wp == kWP32) sweep_v5<kWP32>(L, cs, R, g.rs, best);
-      else sweep_v5<0>(L, cs, R, g.rs, best);
+      if (L.wp == kWP32) sweep_v5<kWP32, JMME_SWEEP_P>(L, cs, R, g.rs, best);
+      else sweep_v5<0, JMME_SWEEP_P>(L, cs, R, g.rs, best);
     }
   } else {
     sweep(std::integral_constant<bool, true>{});
