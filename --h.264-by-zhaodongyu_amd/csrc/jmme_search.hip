@@ -719,6 +719,10 @@ template <bool FFS>
 __device__ __forceinline__ bool special_on(const GroupCtx &g) {
   const int ox = -(g.cqx >> 2), oy = -(g.cqy >> 2);   // the (0,0) vector as a window offset
   const bool inside = abs(ox) <= g.R && abs(oy) <= g.R;
+  // FFS: JM pre-seeds with block_sad[pos_00], which setup_fast_full_search only
+  // writes when (0,0) is in the window -- and with RDO off (the only case that
+  // pre-seeds) it clips the centre so that (0,0) is (me_fullfast.c:319-324).
+  // A caller-made window without (0,0) is outside JM's contract: no pre-seed.
   if (FFS) return g.preseed && inside && mv_cost<FFS>(0, 0, g.px, g.py, g.lam, g.max_mvd).ok;
   return g.chk00 && (g.gmask & 1) && inside;
 }

@@ -203,6 +203,77 @@ def test_random_requests_vs_oracle(size, R, gpu):
     assert len(bad) == 0, [(keys[i], got[i].tolist(), exp[i].tolist()) for i in bad[:5]]
 
 
+def _ffs_random(rng, w, h, n, R, rdopt, far_frac):
+    """n FFS units (all 41 partitions): surface centre, per-partition ranges at
+    or below the surface's, predictors near the window or -- for far_frac of
+    the partitions -- beyond JM's GetMaxMVD gate (me_fullfast.c:637,663); with
+    RDO off the centre stays within +-R so that (0,0) is in the window, as
+    setup_fast_full_search clips it (me_fullfast.c:319-324)."""
+    from jmme import MB_REQ, slot_of
+    geo = {}
+    for bt, (bw, bh) in {1: (16, 16), 2: (16, 8), 3: (8, 16), 4: (8, 8), 5: (8, 4), 6: (4, 8), 7: (4, 4)}.items():
+        for by in range(0, 16, bh):
+            for bx in range(0, 16, bw):
+                geo[slot_of(bt, bx // 4, by // 4)] = (bt, bx // 4, by // 4)
+    req = np.zeros(n, dtype=MB_REQ)
+    req["mb_x"] = rng.integers(0, w // 16, n) * 16
+    req["mb_y"] = rng.integers(0, h // 16, n) * 16
+    req["slot_mask"] = (1 << 41) - 1
+    span = R if rdopt == 0 else 3 * R
+    req["ffs_center_x"] = rng.integers(-span, span + 1, n) * 4
+    req["ffs_center_y"] = rng.integers(-span, span + 1, n) * 4
+    req["ffs_range"] = R
+    req["ffs_pos00_valid"] = 1 if rdopt == 0 else 0
+    mbs, blk = [], []
+    for u in range(n):
+        cx, cy = int(req["ffs_center_x"][u]), int(req["ffs_center_y"][u])
+        mbs.append([int(req["mb_x"][u]), int(req["mb_y"][u]), cx, cy])
+        # pos_00: the (0,0) vector's index in the surface's spiral (me_fullfast.c:353-365)
+        ox, oy = -cx // 4, -cy // 4
+        pos00 = int(np.nonzero((SPIRAL[R][:, 0] == ox) & (SPIRAL[R][:, 1] == oy))[0][0]) if max(abs(ox), abs(oy)) <= R else 0
+        for sl in range(41):
+            b = req["blk"][u, sl]
+            far = rng.random() < far_frac
+            d = rng.integers(-700, 701, size=2) if far else rng.integers(-9 * R, 9 * R + 1, size=2)
+            b["pred_x"], b["pred_y"] = cx + d[0], cy + d[1]
+            b["search_range"] = R if rng.random() < 0.6 else rng.integers(0, R + 1)
+            b["lambda"] = rng.integers(0, 400)
+            req["blk"][u, sl] = b
+            bt, bx, by = geo[sl]
+            blk.append([u, bt, bx, by, int(b["pred_x"]), int(b["pred_y"]), int(b["search_range"]), int(b["lambda"]),
+                        pos00])
+    return req, np.array(mbs, np.int32), np.array(blk, np.int32)
+
+
+SPIRAL = {R: ol.spiral(R) for R in (8, 16, 32)}
+
+
+@pytest.mark.parametrize("R,rdopt,far", [(16, 0, 0.0), (16, 1, 0.0), (32, 0, 0.3), (8, 1, 0.5)])
+def test_ffs_random_requests_vs_oracle(R, rdopt, far, gpu):
+    """Fast full search on inputs no JM run produced: surface centres across
+    the window, partitions with their own smaller ranges, the (0,0) pre-seed
+    on and off, predictors the GetMaxMVD gate cuts (the kernel's exact path):
+    HIP == oracle (ora_ffs_batch, pinned to JM's FFS captures) on every partition."""
+    from jmme import FAST_FULL_SEARCH, MotionEstimator
+    from jmme import synth
+    w, h = 352, 288
+    rng = np.random.default_rng(100 * R + 10 * rdopt + int(10 * far))
+    luma = synth.luma_sequence(w, h, 2, seed=R + rdopt, gmv=(3, -2))
+    cur, ref = luma[1], luma[0]
+    req, mbs, blk = _ffs_random(rng, w, h, 16, R, rdopt, far)
+    with MotionEstimator({"SearchRange": R, "SearchMode": 0, "RDOptimization": rdopt}) as me:
+        me.upload_cur(cur)
+        me.upload_ref(0, 0, ref)
+        out = me.search(FAST_FULL_SEARCH, req)
+        max_mvd = me.max_mvd
+    mv, cost = ol.ffs_batch(cur, ref, R, max_mvd, rdopt, mbs, blk)
+    got = np.array([(out[u, s]["mv_x"], out[u, s]["mv_y"], out[u, s]["cost"]) for u in range(len(req))
+                    for s in range(41)])
+    exp = np.column_stack([mv[:, 0], mv[:, 1], cost])
+    bad = np.nonzero(np.any(got != exp, axis=1))[0]
+    assert len(bad) == 0, [(divmod(int(i), 41), got[i].tolist(), exp[i].tolist()) for i in bad[:5]]
+
+
 def test_saturated_32bit_keys_take_the_64bit_path(gpu):
     """Huge lambdas push every candidate of the small partitions past the
     32-bit key's cost field; the deferred 64-bit pass must keep results exact."""
