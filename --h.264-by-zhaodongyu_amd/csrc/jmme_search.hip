@@ -89,6 +89,8 @@ struct Lds {
   unsigned long long *red;  // kWaves x 41 reduction scratch
   uint4 *tx, *ty;           // per-item position tables (2R+1 each), see build_tabs
   uint32_t *spec;           // 16 4x4 SADs at the special (0,0) candidate, then its 41 keys
+  uint32_t *ctr;            // the window centre's 41 keys, then its 16 4x4 SADs (exact elimination)
+  uint32_t *tmax;           // per wave: 8 words, the centre's per-size key bounds (elimination test)
   unsigned long long *fb;   // exact 16x16 result of the saturation fallback
 };
 
@@ -100,7 +102,7 @@ constexpr int kWP32 = 80;
 __host__ __device__ inline int words_pitch(int R) { return R <= 32 ? kWP32 : 4 * ((2 * R + 13 + 3) / 4); }
 
 // one layout for the kernel (carve) and the host (items_lds_bytes)
-struct LdsPlan { size_t words, raw, red, tx, ty, spec, fb, total; };
+struct LdsPlan { size_t words, raw, red, tx, ty, spec, ctr, tmax, fb, total; };
 __host__ __device__ inline LdsPlan lds_plan(int R) {
   LdsPlan q;
   const int rows = 2 * R + 16, wp = words_pitch(R), d = 2 * R + 1;
@@ -112,6 +114,8 @@ __host__ __device__ inline LdsPlan lds_plan(int R) {
   q.tx = take((size_t)d * 16);
   q.ty = take((size_t)d * 16);
   q.spec = take((16 + kNS) * 4);
+  q.ctr = take((kNS + 16) * 4);
+  q.tmax = take(kWaves * 8 * 4);
   q.fb = take(kWaves * 8);
   q.total = off;
   return q;
@@ -127,6 +131,8 @@ __device__ __forceinline__ Lds carve(unsigned char *smem, int R) {
   L.tx = reinterpret_cast<uint4 *>(smem + q.tx);
   L.ty = reinterpret_cast<uint4 *>(smem + q.ty);
   L.spec = reinterpret_cast<uint32_t *>(smem + q.spec);
+  L.ctr = reinterpret_cast<uint32_t *>(smem + q.ctr);
+  L.tmax = reinterpret_cast<uint32_t *>(smem + q.tmax);
   L.fb = reinterpret_cast<unsigned long long *>(smem + q.fb);
   return L;
 }
@@ -141,6 +147,9 @@ __device__ __forceinline__ Lds carve(unsigned char *smem, int R) {
 #endif
 
 __device__ __forceinline__ int ufl(int v) { return __builtin_amdgcn_readfirstlane(v); }
+#ifdef JMME_ELIM_COUNT
+__device__ unsigned long long g_elim_tasks[2];   // diagnostic: wave-tasks tested, skipped
+#endif
 __device__ __forceinline__ unsigned long long ufl64(unsigned long long v) {
   unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
   unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
@@ -623,6 +632,66 @@ __device__ __forceinline__ void partition_keys(const uint32_t (&a)[16], uint32_t
   ps[0] = __builtin_elementwise_add_sat(ps[1] + nk, ps[2]);   // 16x16: S_top << 16, + S_bot << 16 + K
 }
 
+// Exact elimination (fast path).  The keys of the window centre (offset (0,0)
+// of the sweep: FS the search centre, FFS the surface centre -- an eligible
+// candidate of every partition in the fast path) are real candidates' keys;
+// wave 0 writes them to L.ctr and they join the minima where the per-wave
+// minima are combined.  A task of positions whose every partition key is
+// provably >= the centre's holds no winner -- an equal key shares the centre's
+// (cost, rank >> 2) group, whose ranks the refine re-evaluates exactly -- so its
+// partition keys need not be formed: with e = (smallest 4x4 SAD) << 16 at a
+// position, a partition of n 4x4 blocks has key >= K(pos) + n*e.  Each wave
+// keeps, per size n in {1, 2, 4, 8, 16}, the largest centre key of that size
+// plus n-1 (for a rounded-up division) in its 8-word L.tmax slot.
+// On the bench clip 92 % of the 64-lane tasks skip the keys and minima.
+template <bool FFS>
+__device__ __forceinline__ void centre_bounds(const GroupCtx &g, const Lds &L, int lane, int wave) {
+  const int b = lane & 15, i = lane >> 4;   // 4x4 block, row in it
+  const int bx = b & 3, by = b >> 2;
+  uint32_t sad = __builtin_amdgcn_sad_u8(L.words[(g.R + 4 * by + i) * L.wp + g.R + 4 * bx],
+                                         L.cur[(4 * by + i) * 4 + bx], 0u);
+  sad += __shfl_xor(sad, 16, 64);
+  sad += __shfl_xor(sad, 32, 64);           // every lane: the SAD of its block
+  uint32_t S[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) S[k] = __builtin_amdgcn_readlane(sad, k);
+  // K at the centre: mvcost << 11 | rank >> 2, rank 0 (FFS 1: still 0 after >> 2)
+  const uint64_t Kc =
+      (uint64_t)(((uint32_t)g.lam * (uint32_t)(mvbits(g.cqx - g.px) + mvbits(g.cqy - g.py))) << kCostShift);
+  uint32_t m1 = 0, m2 = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) m1 = max(m1, S[k]);
+#pragma unroll
+  for (int y = 0; y < 4; ++y) m2 = max(m2, max(S[4 * y] + S[4 * y + 1], S[4 * y + 2] + S[4 * y + 3]));   // 8x4
+#pragma unroll
+  for (int x = 0; x < 4; ++x) m2 = max(m2, max(S[x] + S[4 + x], S[8 + x] + S[12 + x]));                 // 4x8
+  const uint32_t q00 = S[0] + S[1] + S[4] + S[5], q10 = S[2] + S[3] + S[6] + S[7];
+  const uint32_t q01 = S[8] + S[9] + S[12] + S[13], q11 = S[10] + S[11] + S[14] + S[15];
+  const uint32_t m4 = max(max(q00, q10), max(q01, q11));
+  const uint32_t m8 = max(max(q00 + q10, q01 + q11), max(q00 + q01, q10 + q11));
+  const uint32_t m16 = q00 + q10 + q01 + q11;
+  auto bound = [&](uint32_t m, uint32_t n) -> uint32_t {
+    const uint64_t v = Kc + ((uint64_t)m << 16) + (n - 1);
+    return v > 0xffffffffull ? 0xffffffffu : (uint32_t)v;
+  };
+  if (lane < 5) {
+    const uint32_t v = lane == 0 ? bound(m1, 1) : lane == 1 ? bound(m2, 2) : lane == 2 ? bound(m4, 4)
+                                                : lane == 3 ? bound(m8, 8) : bound(m16, 16);
+    L.tmax[wave * 8 + lane] = v;
+  }
+  if (wave == 0) {   // the centre's keys for the combine (same form as the sweep's, 16x16 saturating)
+    if (lane < 16) L.ctr[kNS + lane] = sad;
+    if (lane < kNS) {
+      const SlotGeom gm = slot_geom(lane);
+      uint32_t sum = 0;
+      for (int j = 0; j < gm.h; ++j)
+        for (int k = 0; k < gm.w; ++k) sum += L.ctr[kNS + (gm.by + j) * 4 + gm.bx + k];
+      const uint64_t v = Kc + ((uint64_t)sum << 16);
+      L.ctr[lane] = v > 0xffffffffull ? 0xffffffffu : (uint32_t)v;
+    }
+  }
+}
+
 // The v5 sweep of the sub-window [-rs, rs]^2 (rs >= 1) of the staged window.
 // A task is a vertical run of P positions (x, y..y+P-1); the 15+P window rows
 // they need are read once; row r meets MB row r - j of position j.  The
@@ -640,6 +709,7 @@ __device__ __forceinline__ void sweep_v5(const Lds &L, const uint32_t (&cs)[64],
   const unsigned dm = (65536u + (unsigned)D - 1u) / (unsigned)D;
   int tq = (int)(((unsigned)tid * dm) >> 16), tx = tid - tq * D;   // task column, task row
   const int wp = WP ? WP : L.wp;
+  const uint32_t tb = lds_addr(L.tmax) + 32u * (uint32_t)ufl(tid >> 6);   // this wave's elimination bounds
   for (int t = tid; t < ntask; t += kWG) {
     const int y0 = min(P * tq, D - P);
     uint32_t K[P];
@@ -681,12 +751,43 @@ __device__ __forceinline__ void sweep_v5(const Lds &L, const uint32_t (&cs)[64],
       }
       __builtin_amdgcn_sched_barrier(0);
     }
+    // exact elimination (centre_bounds): skip the keys and minima when no lane's
+    // task can beat the centre in any partition
+    bool fold = true;
+    {
+      uint32_t kmin = K[0], e = ~0u;
+#pragma unroll
+      for (int j = 1; j < P; ++j) kmin = min(kmin, K[j]);
+#pragma unroll
+      for (int j = 0; j < P; ++j) {
+        uint32_t m = a[j][0];
+#pragma unroll
+        for (int k = 1; k < 16; ++k) m = min(m, a[j][k]);
+        e = min(e, m - K[j]);
+      }
+      const u32x4 t = ds_read_b128(tb);
+      const uint32_t t16 = reinterpret_cast<const lds_u32 *>((uintptr_t)tb)[4];
+      uint32_t need = __builtin_elementwise_sub_sat(t.x, kmin);
+      need = max(need, __builtin_elementwise_sub_sat(t.y, kmin) >> 1);
+      need = max(need, __builtin_elementwise_sub_sat(t.z, kmin) >> 2);
+      need = max(need, __builtin_elementwise_sub_sat(t.w, kmin) >> 3);
+      need = max(need, __builtin_elementwise_sub_sat(t16, kmin) >> 4);
+#ifndef JMME_NO_ELIM
+      fold = __builtin_amdgcn_ballot_w64(e < need) != 0;
+#else
+      fold = __builtin_amdgcn_ballot_w64(e < need) != 0 || true;
+#endif
+#ifdef JMME_ELIM_COUNT   // diagnostic (contended atomics: distorts timing)
+      if ((tid & 63) == 0) { atomicAdd(&g_elim_tasks[0], 1ull); if (!fold) atomicAdd(&g_elim_tasks[1], 1ull); }
+#endif
+    }
 #ifdef JMME_ABL_NOFOLD   // timing ablation only: keep the 4x4 keys live, no partition keys / minima
 #pragma unroll
     for (int j = 0; j < P; ++j)
 #pragma unroll
       for (int k = 0; k < 16; ++k) asm volatile("" :: "v"(a[j][k]));
 #else
+    if (fold) {
     // positions in pairs: both keys of a partition fold with one v_min3_u32
 #pragma unroll
     for (int j = 0; j + 1 < P; j += 2) {
@@ -701,6 +802,7 @@ __device__ __forceinline__ void sweep_v5(const Lds &L, const uint32_t (&cs)[64],
       partition_keys(a[P - 1], K[P - 1], p0);
 #pragma unroll
       for (int s = 0; s < kNS; ++s) best[s] = min(best[s], p0[s]);
+    }
     }
 #endif
     tx += rstep;
@@ -837,7 +939,7 @@ __device__ __forceinline__ jmme_block_res block_result(const GroupCtx &g, bool f
 // the LDS combine.  skip0: slot 0 is served by the exact fallback instead.
 template <bool FFS>
 __device__ __forceinline__ void refine_output32(const KParams &p, const GroupCtx &g, const Lds &L, bool spec,
-                                                bool skip0, int u) {
+                                                bool fast, bool skip0, int u) {
   const int tid = opaque_tid(), lane = tid & 63, wave = ufl(tid >> 6);
   int s, j, q, nq;
   if (wave == 0) { s = 25 + (lane >> 2); j = lane & 3; q = 0; nq = 1; }
@@ -852,6 +954,7 @@ __device__ __forceinline__ void refine_output32(const KParams &p, const GroupCtx
 #pragma unroll
     for (int w = 0; w < kWaves; ++w) key = min(key, (uint32_t)L.red[w * kNS + s]);
     if (spec) key = min(key, L.spec[16 + s]);
+    if (fast) key = min(key, L.ctr[s]);   // the centre (exact elimination)
   }
   // candidate j: its window offset, or none
   const int R = g.R, D = 2 * R + 1;
@@ -1088,6 +1191,7 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
   const bool spec = KEY32 && fast && special_on<FFS>(g);
   if (KEY32 && fast) {
     if (spec && wave == 0) special_keys<FFS>(g, L, tid);   // read back after the reduce's barrier
+    if constexpr (KEY32) centre_bounds<FFS>(g, L, lane, ufl(wave));
     if constexpr (KEY32) {
       if (L.wp == kWP32) sweep_v5<kWP32, JMME_SWEEP_P>(L, cs, R, g.rs, best);
       else sweep_v5<0, JMME_SWEEP_P>(L, cs, R, g.rs, best);
@@ -1159,11 +1263,12 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
 #pragma unroll
       for (int w = 0; w < kWaves; ++w) k0 = min(k0, (uint32_t)L.red[w * kNS]);
       if (spec) k0 = min(k0, L.spec[16]);
+      if (fast) k0 = min(k0, L.ctr[0]);
       fb16 = k0 == ~0u;
     }
     STAMP(st.reduce);
 #ifndef JMME_ABL_NOREFINE   // timing ablation only: no refine / output
-    refine_output32<FFS>(p, g, L, spec, fb16, u);
+    refine_output32<FFS>(p, g, L, spec, fast, fb16, u);
 #endif
     if (tick && opaque_tid() == 0) *s_tick = tk;
     STAMP(st.refine);
@@ -1382,6 +1487,17 @@ int resident_grid(Occupancy &o, int dev, int variant, K kernel, int lds_range, s
 }  // namespace
 
 size_t items_lds_bytes(int R) { return lds_plan(R).total; }
+
+#ifdef JMME_ELIM_COUNT
+}  // namespace jmme
+// diagnostic builds: wave-tasks the elimination test saw / skipped since the last call
+extern "C" int jmme_debug_elim(unsigned long long *out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(jmme::g_elim_tasks), 2 * sizeof(unsigned long long)) != hipSuccess) return -1;
+  const unsigned long long z[2] = {0, 0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(jmme::g_elim_tasks), z, sizeof z) == hipSuccess ? 0 : -1;
+}
+namespace jmme {
+#endif
 
 hipError_t launch_search(const KParams &p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
   // occupancy per device: the caller (jmme_capi) has made the context's device current
