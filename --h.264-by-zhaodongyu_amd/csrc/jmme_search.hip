@@ -63,6 +63,7 @@ constexpr int kCostShift = 11;             // key32 = cost << 11 | rank >> 2
 constexpr int kRankDrop = 2;
 constexpr int kCand = 1 << kRankDrop;      // refine candidates per partition
 constexpr int kPlanWaves = 16;             // plan kernel: units per workgroup
+constexpr int kChunk = 16;                 // item kernel: consecutive items dealt to one XCD
 constexpr int kRed1 = (kNS + 3) / 4 * 2;      // reduce: registers after the permlane32 level (22)
 constexpr int kRed2 = kRed1 / 2;              //         ... after the permlane16 level (11)
 
@@ -1342,10 +1343,13 @@ __device__ __forceinline__ Item load_item(const Item *items, unsigned j) {
 }
 
 // Persistent item kernel.  The KEY32 instance drains the 32-bit list, the
-// other the 64-bit list.  XCD x (= blockIdx % 8) serves the contiguous run
-// [x*cnt/8, (x+1)*cnt/8) of the items (neighbouring macroblocks' windows
-// overlap in its L2).  Inside the run the first two items of each workgroup
-// are static (start + lb, start + lb + nbx); the rest are dealt by tickets,
+// other the 64-bit list.  XCD x (= blockIdx % 8) serves every 8th chunk of 16
+// consecutive items (neighbouring macroblocks' windows overlap in its L2; with
+// whole eighths of the list instead, the last eighth -- the bottom rows, whose
+// padded, flat blocks defeat the elimination, and all further groups, which
+// the bottom row holds -- made one XCD end 30 us after the others).  Inside
+// its list the first two items of each workgroup
+// are static (lb, lb + nbx); the rest are dealt by tickets,
 // one atomic per item on the XCD's counter: the workgroups resident on one CU
 // do not progress at the same rate (the oldest wave wins the SIMD's issue
 // arbitration: on MI355X a CU's four workgroups finished equal static shares
@@ -1362,12 +1366,16 @@ __global__ __launch_bounds__(kWG, KEY32 ? JMME_WAVES_PER_EU : 2) void me_items_k
   const unsigned cnt = (unsigned)p.n + p.counts[0];   // first groups, then the further groups
   const Item *items = p.items;
   const int x = blockIdx.x & 7, lb = blockIdx.x >> 3, nbx = (gridDim.x - x + 7) >> 3;
-  const unsigned start = (unsigned)(((unsigned long long)cnt * x) >> 3);
-  const unsigned end = (unsigned)(((unsigned long long)cnt * (x + 1)) >> 3);
-  const unsigned j = start + lb;
+  // XCD x's list: the chunks of kChunk consecutive items c with c % 8 == x
+  // (a chunk's macroblocks are neighbours: their windows overlap in the XCD's
+  // L2); k-th item of the list = list index (k / kChunk * 8 + x) * kChunk + k % kChunk
+  const unsigned rounds = cnt / (8u * kChunk), rest = cnt - rounds * 8u * kChunk;
+  const unsigned end = rounds * kChunk + (unsigned)min(max((int)rest - x * kChunk, 0), kChunk);
+  auto item_at = [&](unsigned k) { return (k / kChunk * 8u + (unsigned)x) * kChunk + k % kChunk; };
+  const unsigned j = (unsigned)lb;
   if (j >= end) return;
   unsigned jn = j + nbx;                                  // the second item (static)
-  const unsigned dyn0 = start + 2u * (unsigned)nbx;       // ticket t serves item dyn0 + t
+  const unsigned dyn0 = 2u * (unsigned)nbx;               // ticket t serves item dyn0 + t
   unsigned *const tick = p.counts + 8 + x;
 
   Lds L = carve(smem, p.lds_range);
@@ -1378,7 +1386,7 @@ __global__ __launch_bounds__(kWG, KEY32 ? JMME_WAVES_PER_EU : 2) void me_items_k
   unsigned long long t_last = __builtin_amdgcn_s_memtime();
 #endif
 
-  Item it = load_item(items, j);
+  Item it = load_item(items, item_at(j));
   prefetch(p, it, L);
 #ifdef JMME_STAMPS
   // per-workgroup record behind the per-unit ones: start / end (s_memrealtime,
@@ -1398,7 +1406,7 @@ __global__ __launch_bounds__(kWG, KEY32 ? JMME_WAVES_PER_EU : 2) void me_items_k
     if (!first) jn = dyn0 + (unsigned)ufl((int)s_tick);
     const bool more = jn < end;
     Item nx;
-    if (more) nx = load_item(items, jn);
+    if (more) nx = load_item(items, item_at(jn));
     STAMP(st.wait);
     const bool fast = it.gmask && item_fast<KEY32, FFS>(p, it);
 #ifndef JMME_ABL_NOEXPAND   // timing ablation only: the window stays as the previous item left it
