@@ -83,6 +83,7 @@ constexpr int kRawExtra = 64;
 
 struct Lds {
   int wp;                   // words per window row
+  int wv;                   // this wave's index in the workgroup (uniform)
   uint32_t *words;          // current item's window, rows x wp
   uint32_t *raw;            // next item as fetched: window rows x nd dwords (dense),
                             // then its current MB (64 dwords)
@@ -126,6 +127,7 @@ __device__ __forceinline__ Lds carve(unsigned char *smem, int R) {
   Lds L;
   const LdsPlan q = lds_plan(R);
   L.wp = words_pitch(R);
+  L.wv = (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   L.words = reinterpret_cast<uint32_t *>(smem + q.words);
   L.raw = reinterpret_cast<uint32_t *>(smem + q.raw);
   L.red = reinterpret_cast<unsigned long long *>(smem + q.red);
@@ -157,13 +159,14 @@ __device__ __forceinline__ unsigned long long ufl64(unsigned long long v) {
   return ((unsigned long long)hi << 32) | lo;
 }
 
-// threadIdx.x through an opaque copy: values derived from it are recomputed in
-// the phase that uses them instead of being hoisted out of the item loop (and
-// kept live -- spilled -- across the sweep)
-__device__ __forceinline__ int opaque_tid() {
-  int t = threadIdx.x;
-  asm volatile("" : "+v"(t));
-  return t;
+// the thread index, rebuilt where it is used from the lane count (an opaque
+// v_mbcnt pair the compiler can neither hoist nor merge) and the wave index,
+// which is uniform and lives in an SGPR: nothing derived from threadIdx.x is
+// hoisted out of the item loop and kept live -- spilled -- across the sweep
+__device__ __forceinline__ int opaque_tid(const Lds &L) {
+  unsigned t;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(t));
+  return (int)(t + ((unsigned)L.wv << 6));
 }
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
@@ -452,7 +455,7 @@ __device__ __forceinline__ void lds_dma_dword(const void *gptr, uint32_t lds) {
 // top of the next item.
 __device__ __forceinline__ void prefetch(const KParams &p, const Item &it, const Lds &L) {
   if (!it.gmask) return;
-  const int tid = opaque_tid(), lane = tid & 63, wave = ufl(tid >> 6);
+  const int tid = opaque_tid(L), lane = tid & 63, wave = ufl(tid >> 6);
   const Win w = win_of(p, it);
   const uint8_t *ref = p.refs[it.ref];
   const int total = w.wrows * w.nd;
@@ -505,7 +508,7 @@ __device__ __forceinline__ void expand_inner(const uint32_t *src, uint32_t *dst,
 }
 
 __device__ __forceinline__ void expand(const KParams &p, const Item &it, const Lds &L) {
-  const int tid = opaque_tid();
+  const int tid = opaque_tid(L);
   const Win w = win_of(p, it);
   const uint32_t *tail = L.raw + w.wrows * w.nd;
   if (tid < 64) L.cur[tid] = tail[tid];
@@ -585,7 +588,7 @@ __device__ __forceinline__ bool item_fast(const KParams &p, const Item &it) {
 // is the pre-seeded (0,0), me_fullfast.c:650-657).
 template <bool FFS>
 __device__ __forceinline__ void build_tabs(const Item &it, const Lds &L) {
-  const int tid = opaque_tid();
+  const int tid = opaque_tid(L);
   const int rs = it.rs, D = 2 * rs + 1;
   for (int i = tid; i < 2 * D; i += kWG) {
     const bool y = i >= D;
@@ -700,7 +703,7 @@ __device__ __forceinline__ void centre_bounds(const GroupCtx &g, const Lds &L, i
 template <int WP, int P>   // WP: words pitch when known at compile time (kWP32), else 0 (L.wp)
 __device__ __forceinline__ void sweep_v5(const Lds &L, const uint32_t (&cs)[64], int R, int rs,
                                          uint32_t (&best)[kNS]) {
-  const int tid = opaque_tid();
+  const int tid = opaque_tid(L);
   const int D = 2 * rs + 1;
   const int DT = (D + P - 1) / P;        // tasks per column (the last one shifted up)
   const int ntask = D * DT;
@@ -872,7 +875,7 @@ __device__ __forceinline__ void special_keys(const GroupCtx &g, const Lds &L, in
 // one barrier per call suffices).
 template <bool FFS>
 __device__ __forceinline__ unsigned long long exact_slot(const GroupCtx &g, const Lds &L, int s) {
-  const int tid = opaque_tid(), lane = tid & 63, wave = tid >> 6;
+  const int tid = opaque_tid(L), lane = tid & 63, wave = tid >> 6;
   const int R = g.R, D = 2 * R + 1;
   const SlotGeom gm = slot_geom(s);
   unsigned long long best = ~0ull;
@@ -941,7 +944,7 @@ __device__ __forceinline__ jmme_block_res block_result(const GroupCtx &g, bool f
 template <bool FFS>
 __device__ __forceinline__ void refine_output32(const KParams &p, const GroupCtx &g, const Lds &L, bool spec,
                                                 bool fast, bool skip0, int u) {
-  const int tid = opaque_tid(), lane = tid & 63, wave = ufl(tid >> 6);
+  const int tid = opaque_tid(L), lane = tid & 63, wave = ufl(tid >> 6);
   int s, j, q, nq;
   if (wave == 0) { s = 25 + (lane >> 2); j = lane & 3; q = 0; nq = 1; }
   else if (wave == 1) { s = 9 + (lane >> 2); j = lane & 3; q = 0; nq = 1; }
@@ -1023,7 +1026,14 @@ __device__ __forceinline__ void refine_output32(const KParams &p, const GroupCtx
     res.mv_y = (int16_t)(g.cqy + 4 * oy);
     res.cost = (int64_t)(key >> kCostShift);
   } else if (j == 0 && key == ~0u) {   // nothing eligible: JM leaves the centre and DISTBLK_MAX
-    res.mv_x = (int16_t)g.cqx; res.mv_y = (int16_t)g.cqy; res.cost = JMME_DISTBLK_MAX;
+    // DISTBLK_MAX built by the asm itself: a plain constant is hoisted out of
+    // the item loop and spilled to scratch
+    static_assert(JMME_DISTBLK_MAX == 0xfffffffe0ll, "DISTBLK_MAX halves below");
+    uint32_t dlo, dhi;
+    asm volatile("v_mov_b32 %0, 0xffffffe0" : "=v"(dlo));
+    asm volatile("v_mov_b32 %0, 15" : "=v"(dhi));
+    const int64_t dmax = (int64_t)(((uint64_t)dhi << 32) | dlo);
+    res.mv_x = (int16_t)g.cqx; res.mv_y = (int16_t)g.cqy; res.cost = dmax;
   } else {
     if (j == 0 && !(M & all)) atomicOr(&p.counts[2], 4u);   // cannot happen: refine lost the winner
     return;
@@ -1045,7 +1055,7 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
 #endif
 ) {
   using Best = typename std::conditional<KEY32, uint32_t, unsigned long long>::type;
-  int tid = opaque_tid();
+  int tid = opaque_tid(L);
   int lane = tid & 63;
   int wave = tid >> 6;
   const uint32_t *curw = L.cur;
@@ -1203,7 +1213,7 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
   STAMP(st.sweep);
 
   // ---- workgroup reduction of this group's per-thread minima
-  tid = opaque_tid();
+  tid = opaque_tid(L);
   lane = tid & 63;
   wave = tid >> 6;
   // the workgroup's next ticket (see me_items_kernel): issued here, written to
@@ -1271,11 +1281,11 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
 #ifndef JMME_ABL_NOREFINE   // timing ablation only: no refine / output
     refine_output32<FFS>(p, g, L, spec, fast, fb16, u);
 #endif
-    if (tick && opaque_tid() == 0) *s_tick = tk;
+    if (tick && opaque_tid(L) == 0) *s_tick = tk;
     STAMP(st.refine);
     if (fb16) {   // search the 16x16 again with exact keys
       const unsigned long long k16 = exact_slot<FFS>(g, L, 0);
-      if (opaque_tid() == 0)
+      if (opaque_tid(L) == 0)
         p.out[(size_t)u * kNS] =
             block_result<FFS>(g, k16 != ~0ull, (uint32_t)(k16 & 0x7fffffffu), (uint32_t)(k16 >> 32));
     }
@@ -1295,7 +1305,7 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
   STAMP(st.refine);
 
   // ---- results of this group (64-bit keys: cost << 32 | rank)
-  tid = opaque_tid();
+  tid = opaque_tid(L);
   if (tick && tid == 0) *s_tick = tk;
   if (tid < kNS && ((gmask >> tid) & 1)) {
     const unsigned long long k = L.red[tid];
@@ -1319,7 +1329,7 @@ __device__ __forceinline__ void search_item_slow64(const KParams &p, const Item 
   for (int s = 0; s < kNS; ++s) {
     if (!((g.gmask >> s) & 1)) continue;
     const unsigned long long k = exact_slot<FFS>(g, L, s);
-    if (opaque_tid() == 0)
+    if (opaque_tid(L) == 0)
       p.out[(size_t)it.u * kNS + s] =
           block_result<FFS>(g, k != ~0ull, (uint32_t)(k & 0x7fffffffu), (uint32_t)(k >> 32));
   }
@@ -1416,7 +1426,7 @@ __global__ __launch_bounds__(kWG, KEY32 ? JMME_WAVES_PER_EU : 2) void me_items_k
     __syncthreads();
     if (p.debug_words && it.u == 0 && (it.gmask & dbg_slot)) {
       const Win w = win_of(p, it);
-      for (int i = opaque_tid(); i < w.wrows * w.wpr; i += kWG) {
+      for (int i = opaque_tid(L); i < w.wrows * w.wpr; i += kWG) {
         const int r = i / w.wpr;
         p.debug_words[i] = L.words[r * L.wp + i - r * w.wpr];
       }
@@ -1450,7 +1460,7 @@ __global__ __launch_bounds__(kWG, KEY32 ? JMME_WAVES_PER_EU : 2) void me_items_k
 #endif
       }
     }
-    if (more && !ticketed && threadIdx.x == 0) s_tick = atomicAdd(tick, 1u);
+    if (more && !ticketed && opaque_tid(L) == 0) s_tick = atomicAdd(tick, 1u);
 #ifdef JMME_STAMPS
     if (p.stamps && threadIdx.x == 0) {
       unsigned long long *o = p.stamps + (size_t)it.u * 8;
