@@ -639,7 +639,7 @@ __device__ __forceinline__ void partition_keys(const uint32_t (&a)[16], uint32_t
 // Exact elimination (fast path).  The keys of the window centre (offset (0,0)
 // of the sweep: FS the search centre, FFS the surface centre -- an eligible
 // candidate of every partition in the fast path) are real candidates' keys;
-// wave 0 writes them to L.ctr and they join the minima where the per-wave
+// the last wave writes them to L.ctr and they join the minima where the per-wave
 // minima are combined.  A task of positions whose every partition key is
 // provably >= the centre's holds no winner -- an equal key shares the centre's
 // (cost, rank >> 2) group, whose ranks the refine re-evaluates exactly -- so its
@@ -683,7 +683,7 @@ __device__ __forceinline__ void centre_bounds(const GroupCtx &g, const Lds &L, i
                                                 : lane == 3 ? bound(m8, 8) : bound(m16, 16);
     L.tmax[wave * 8 + lane] = v;
   }
-  if (wave == 0) {   // the centre's keys for the combine (same form as the sweep's, 16x16 saturating)
+  if (wave == kWaves - 1) {   // the centre's keys for the combine (same form as the sweep's, 16x16 saturating)
     if (lane < 16) L.ctr[kNS + lane] = sad;
     if (lane < kNS) {
       const SlotGeom gm = slot_geom(lane);
@@ -818,7 +818,7 @@ __device__ __forceinline__ void sweep_v5(const Lds &L, const uint32_t (&cs)[64],
 // JM's special (0,0) candidate, once per item instead of per position: FS
 // check_for_00 (slot 0 at (0,0) costs mvcost - 16*lambda, me_fullsearch.c:61,
 // 78-82) and the FFS pre-seed (every partition, rank 0, me_fullfast.c:650-657).
-// Its keys are formed before the sweep (special_keys, wave 0) and join the
+// Its keys are formed before the sweep (special_keys, last wave) and join the
 // reduced minima where the reduce's per-wave minima are combined, so
 // it adds no barrier; the sweep's own key for that position is never below it.
 template <bool FFS>
@@ -849,21 +849,23 @@ __device__ __forceinline__ uint32_t special_key(const GroupCtx &g, const Lds &L,
   return cost < (1u << (32 - kCostShift)) ? (cost << kCostShift) | (rank >> kRankDrop) : ~0u;
 }
 
-// Wave 0, before the sweep: the special candidate's 16 4x4 SADs, then its key
+// The last wave, before the sweep (the one the partial last round of sweep
+// tasks leaves idle, so this work is off the critical path to the reduce's
+// barrier): the special candidate's 16 4x4 SADs, then its key
 // for every slot into L.spec[16 + s] (one wave: its LDS writes land before its
 // own later reads, no barrier); read back after the reduce's barrier.
 template <bool FFS>
-__device__ __forceinline__ void special_keys(const GroupCtx &g, const Lds &L, int tid) {
-  if (tid < 16) {
+__device__ __forceinline__ void special_keys(const GroupCtx &g, const Lds &L, int lane) {
+  if (lane < 16) {
     const int ox = -(g.cqx >> 2), oy = -(g.cqy >> 2);
-    const int bx = tid & 3, by = tid >> 2;
+    const int bx = lane & 3, by = lane >> 2;
     const uint32_t *w = L.words + (oy + g.R + 4 * by) * L.wp + ox + g.R + 4 * bx;
     uint32_t sad = 0;
 #pragma unroll
     for (int r = 0; r < 4; ++r) sad = __builtin_amdgcn_sad_u8(w[r * L.wp], L.cur[(4 * by + r) * 4 + bx], sad);
-    L.spec[tid] = sad;
+    L.spec[lane] = sad;
   }
-  if (tid < kNS) L.spec[16 + tid] = special_key<FFS>(g, L, tid);
+  if (lane < kNS) L.spec[16 + lane] = special_key<FFS>(g, L, lane);
 }
 
 // Exact search of one partition with 64-bit keys (cost << 32 | rank), every
@@ -1201,7 +1203,7 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
   // per-partition masks in the loop)
   const bool spec = KEY32 && fast && special_on<FFS>(g);
   if (KEY32 && fast) {
-    if (spec && wave == 0) special_keys<FFS>(g, L, tid);   // read back after the reduce's barrier
+    if (spec && wave == kWaves - 1) special_keys<FFS>(g, L, lane);   // the wave with the fewest sweep tasks; read back after the reduce's barrier
     if constexpr (KEY32) centre_bounds<FFS>(g, L, lane, ufl(wave));
     if constexpr (KEY32) {
       if (L.wp == kWP32) sweep_v5<kWP32, JMME_SWEEP_P>(L, cs, R, g.rs, best);
