@@ -455,18 +455,16 @@ constexpr size_t align64(size_t v) { return (v + 63) & ~size_t(63); }
 
 int status_words(const unsigned *st, const jmme_ctx *ctx) {
   if (st[2] & 4u) return fail("internal: the refine pass lost a winner");
-  if (st[2] & 1u) return fail("a request's search range exceeds the configured SearchRange %d", ctx->cfg.SearchRange);
+  if (st[2] & 1u) return fail("a request's search range exceeds the configured SearchRange %d (or an FFS block range its surface's)", ctx->cfg.SearchRange);
   if (st[2] & 2u) return fail("a full-search centre is not on the integer grid (EPZSSubPelGrid sub-pel centres are not supported)");
   return 0;
 }
 
-int check_status(jmme_ctx *ctx) {
+int check_status(jmme_ctx *ctx, hipStream_t s) {
   unsigned st[3] = {0, 0, 0};
-  HIPCHK(hipMemcpy(st, ctx->d_counts, sizeof st, hipMemcpyDeviceToHost));
-  if (st[2] & 4u) return fail("internal: the refine pass lost a winner");
-  if (st[2] & 1u) return fail("a request's search range exceeds the configured SearchRange %d", ctx->cfg.SearchRange);
-  if (st[2] & 2u) return fail("a full-search centre is not on the integer grid (EPZSSubPelGrid sub-pel centres are not supported)");
-  return 0;
+  HIPCHK(hipMemcpyAsync(st, ctx->d_counts, sizeof st, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  return status_words(st, ctx);
 }
 
 int validate(const jmme_ctx *ctx, int mode, const jmme_mb_req *req, int n) {
@@ -552,12 +550,23 @@ extern "C" int jmme_search_mbs_planes_async(jmme_ctx *ctx, int mode, const uint8
   if (!ctx) return fail("null ctx");
   if (!d_cur || !d_ref) return fail("null plane");
   if (pitch < w || (pitch & 3) || (w & 15) || (h & 15)) return fail("bad plane geometry %dx%d pitch %d", w, h, pitch);
+  // the item kernel reads MB rows with scalar loads, which ignore the low
+  // address bits: a plane base off a dword boundary would read shifted pels
+  if (((uintptr_t)d_cur | (uintptr_t)d_ref) & 3) return fail("plane base not 4-byte aligned");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   // every (list, ref) of this call reads the one given plane
   std::vector<const uint8_t *> tab(kMaxLists * kMaxRefs, d_ref);
   HIPCHK(hipMemcpyAsync(ctx->d_ref_table, tab.data(), tab.size() * sizeof(void *), hipMemcpyHostToDevice, s));
   ctx->ref_table_dirty = true;
   return launch(ctx, mode, d_cur, ctx->d_ref_table, pitch, w, h, d_req, n, d_out, s);
+}
+
+extern "C" int jmme_search_status(jmme_ctx *ctx, void *stream) {
+  DevGuard dg_(ctx);
+  if (!ctx) return fail("null ctx");
+  // the device-request paths skip validate(): the plan kernel refuses what
+  // would overrun the launch (ranges, sub-pel centres) and flags it here
+  return check_status(ctx, reinterpret_cast<hipStream_t>(stream));
 }
 
 extern "C" float jmme_last_kernel_ms(jmme_ctx *ctx) {

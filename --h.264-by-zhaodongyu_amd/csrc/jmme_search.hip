@@ -118,7 +118,7 @@ __host__ __device__ inline LdsPlan lds_plan(int R) {
   q.spec = take((16 + kNS) * 4);
   q.ctr = take((kNS + 16) * 4);
   q.tmax = take(kWaves * 8 * 4);
-  q.fb = take(kWaves * 8);
+  q.fb = take(2 * kWaves * 8);   // two halves: successive exact_slot calls alternate
   q.total = off;
   return q;
 }
@@ -410,10 +410,13 @@ __global__ __launch_bounds__(64 * kPlanWaves) void me_plan_kernel(KParams p) {
     it.lam = rq_lambda(lq);
     it.ref = rq->list * kMaxRefs + rq->ref_idx;
     it.pad = 0;
-    if (R < 0 || R > p.lds_range || ((cqx | cqy) & 3)) {
+    // FFS: a partition's own range above the surface's would index past the
+    // position tables and the staged window (device requests skip validate())
+    const bool bad_range = R < 0 || R > p.lds_range || it.rs < 0 || it.rs > R;
+    if (bad_range || ((cqx | cqy) & 3)) {
       // outside what this launch was sized for (or a sub-pel-grid centre):
       // refuse loudly instead of overrunning LDS; the host reports it
-      atomicOr(&p.counts[2], (R < 0 || R > p.lds_range) ? 1u : 2u);
+      atomicOr(&p.counts[2], bad_range ? 1u : 2u);
       it.gmask = 0;
     }
     p.items[lane == 0 ? (unsigned)u : (unsigned)p.n + s_off[wave] + lane - 1] = it;
@@ -873,10 +876,11 @@ __device__ __forceinline__ void special_keys(const GroupCtx &g, const Lds &L, in
 // whose every 32-bit key saturated (only when lambda * mvbits > 8160 and its
 // SADs are near 65280), and every partition of a unit whose lambda exceeds the
 // 32-bit keys' range (kItemSlow64; no JM configuration comes near it).  The
-// result is the min over this call's half of L.fb (slots alternate halves, so
-// one barrier per call suffices).
+// result is the min over this call's half of L.fb.  Successive calls of one
+// item must pass alternating halves (a call counter, not the slot: the slots of
+// a sparse group mask need not alternate), so one barrier per call suffices.
 template <bool FFS>
-__device__ __forceinline__ unsigned long long exact_slot(const GroupCtx &g, const Lds &L, int s) {
+__device__ __forceinline__ unsigned long long exact_slot(const GroupCtx &g, const Lds &L, int s, int half) {
   const int tid = opaque_tid(L), lane = tid & 63, wave = tid >> 6;
   const int R = g.R, D = 2 * R + 1;
   const SlotGeom gm = slot_geom(s);
@@ -904,7 +908,7 @@ __device__ __forceinline__ unsigned long long exact_slot(const GroupCtx &g, cons
     const unsigned long long x = ((unsigned long long)hi << 32) | lo;
     best = x < best ? x : best;
   }
-  unsigned long long *fb = L.fb + (s & 1) * kWaves;
+  unsigned long long *fb = L.fb + (half & 1) * kWaves;
   if (lane == 0) fb[wave] = best;
   __syncthreads();
   unsigned long long k = fb[0];
@@ -1286,7 +1290,7 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
     if (tick && opaque_tid(L) == 0) *s_tick = tk;
     STAMP(st.refine);
     if (fb16) {   // search the 16x16 again with exact keys
-      const unsigned long long k16 = exact_slot<FFS>(g, L, 0);
+      const unsigned long long k16 = exact_slot<FFS>(g, L, 0, 0);
       if (opaque_tid(L) == 0)
         p.out[(size_t)u * kNS] =
             block_result<FFS>(g, k16 != ~0ull, (uint32_t)(k16 & 0x7fffffffu), (uint32_t)(k16 >> 32));
@@ -1328,9 +1332,10 @@ __device__ __forceinline__ void search_item_slow64(const KParams &p, const Item 
   g.gmask = it.gmask;
   g.rs = it.rs;
   g.chk00 = !FFS && (it.flags & kItemChk00);
+  int call = 0;
   for (int s = 0; s < kNS; ++s) {
     if (!((g.gmask >> s) & 1)) continue;
-    const unsigned long long k = exact_slot<FFS>(g, L, s);
+    const unsigned long long k = exact_slot<FFS>(g, L, s, call++);
     if (opaque_tid(L) == 0)
       p.out[(size_t)it.u * kNS + s] =
           block_result<FFS>(g, k != ~0ull, (uint32_t)(k & 0x7fffffffu), (uint32_t)(k >> 32));

@@ -108,6 +108,7 @@ def lib() -> ctypes.CDLL:
         "jmme_search_mbs": (I, [P, I, P, I, P]),
         "jmme_search_mbs_async": (I, [P, I, P, I, P, P]),
         "jmme_search_mbs_planes_async": (I, [P, I, P, P, I, I, I, P, I, P, P]),
+        "jmme_search_status": (I, [P, P]),
         "jmme_full_search_block": (ctypes.c_int64, [P, I, I, I, I, I, P, P, ctypes.c_int64, I, I, I]),
         "jmme_fast_full_search_block": (ctypes.c_int64, [P, I, I, I, I, I, P, P, I, I, I, P, ctypes.c_int64, I]),
         "jmme_last_kernel_ms": (ctypes.c_float, [P]),

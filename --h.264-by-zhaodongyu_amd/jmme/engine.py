@@ -115,6 +115,10 @@ class MotionEstimator:
                                                  ctypes.c_void_p(d_req), int(n), ctypes.c_void_p(d_out),
                                                  ctypes.c_void_p(stream)))
 
+    def search_status(self, stream: int = 0) -> None:
+        """Raise if the last device-request search refused a request (synchronises)."""
+        check(lib().jmme_search_status(self._ctx, ctypes.c_void_p(stream)))
+
     def last_kernel_ms(self) -> float:
         return float(lib().jmme_last_kernel_ms(self._ctx))
 

@@ -151,12 +151,20 @@ int jmme_search_mbs_async(jmme_ctx *ctx, int mode, const jmme_mb_req *d_req, int
                           jmme_block_res *d_out, void *stream);
 
 /* Device-plane variant: d_cur/d_ref are 8-bit planes (pitch bytes per row)
- * already in device memory (e.g. from torch), for multi-frame pipelines. */
+ * already in device memory (e.g. from torch), for multi-frame pipelines.
+ * Both base pointers and the pitch must be multiples of 4 bytes. */
 int jmme_search_mbs_planes_async(jmme_ctx *ctx, int mode,
                                  const uint8_t *d_cur, const uint8_t *d_ref, int pitch,
                                  int width, int height,
                                  const jmme_mb_req *d_req, int n, jmme_block_res *d_out,
                                  void *stream);
+
+/* Status of the last search launch of ctx (synchronises `stream`).  The device
+ * request paths above are not validated on the host; the plan kernel refuses
+ * requests that would overrun the launch (range above SearchRange, an FFS block
+ * range above its surface's, a sub-pel centre) and this returns -1 for them,
+ * with jmme_last_error() naming the cause. */
+int jmme_search_status(jmme_ctx *ctx, void *stream);
 
 /* ---- JM IntPelME-signature drop-ins (one partition per call) ------------
  * Same inputs/outputs as full_search_motion_estimation / the FFS pair, in C

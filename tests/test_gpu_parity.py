@@ -374,3 +374,108 @@ def test_staged_window_is_the_clamped_reference(mb, cen, gpu):
         exp |= luma[0][np.ix_(ys, xs)].astype(np.uint32) << np.uint32(8 * b)
     bad = np.argwhere(out[:, :2 * R + 13] != exp)
     assert len(bad) == 0, (len(bad), bad[:5].tolist())
+
+
+def _grouped_units(rng, w, h, n, R, lam):
+    """Units whose 41 partitions share one of 3 (centre, predictor, lambda)
+    triples at random, so the plan kernel's groups have sparse, non-contiguous
+    slot masks (e.g. slots {0, 2, 7, ...} in one group)."""
+    from jmme import MB_REQ
+    req = np.zeros(n, dtype=MB_REQ)
+    req["mb_x"] = rng.integers(0, w // 16, n) * 16
+    req["mb_y"] = rng.integers(0, h // 16, n) * 16
+    req["slot_mask"] = (1 << 41) - 1
+    for u in range(n):
+        trip = []
+        for _ in range(3):
+            cen = rng.integers(-2 * R - 2, 2 * R + 3, size=2) * 4
+            trip.append((cen, cen + rng.integers(-9, 10, size=2), lam + int(rng.integers(0, 500))))
+        pick = rng.integers(0, 3, 41)
+        for s in range(41):
+            cen, pred, lm = trip[pick[s]]
+            b = req["blk"][u, s]
+            b["center_x"], b["center_y"] = cen
+            b["pred_x"], b["pred_y"] = pred
+            b["search_range"] = R
+            b["lambda"] = lm
+            req["blk"][u, s] = b
+    return req
+
+
+@pytest.mark.parametrize("R", [1, 7, 23, 44])
+def test_64bit_path_with_sparse_group_masks(R, gpu):
+    """Lambdas beyond the 32-bit keys send every partition through the exact
+    64-bit search, one partition after another; groups with non-contiguous slot
+    masks make consecutive calls land on slots of equal parity, and the odd
+    halves of the exchange buffer sit at the end of the workgroup's LDS.  Every
+    SearchRange changes where that end falls.  HIP == oracle on every partition."""
+    from jmme import FULL_SEARCH, MotionEstimator, synth
+    w, h = 352, 288
+    rng = np.random.default_rng(40 + R)
+    luma = synth.luma_sequence(w, h, 2, seed=R, gmv=(2, 1))
+    req = _grouped_units(rng, w, h, 8, R, 400000)
+    with MotionEstimator({"SearchRange": R, "SearchMode": -1}) as me:
+        me.upload_cur(luma[1])
+        me.upload_ref(0, 0, luma[0])
+        out = me.search(FULL_SEARCH, req)
+    keys, mv, cost = _oracle_units(luma[1], luma[0], req)
+    got = np.array([(out[u, s]["mv_x"], out[u, s]["mv_y"], out[u, s]["cost"]) for u, s in keys])
+    exp = np.column_stack([mv[:, 0], mv[:, 1], cost])
+    bad = np.nonzero(np.any(got != exp, axis=1))[0]
+    assert len(bad) == 0, [(keys[i], got[i].tolist(), exp[i].tolist()) for i in bad[:5]]
+
+
+def test_device_requests_outside_contract_are_refused(gpu):
+    """The device-request path skips the host validation: the plan kernel must
+    refuse an FFS partition whose own range exceeds its surface's (it would
+    index past the position tables and the staged window) and report it."""
+    import torch
+    from jmme import FAST_FULL_SEARCH, FULL_SEARCH, JmmeError, MB_REQ, NSLOT, BLOCK_RES, MotionEstimator, synth
+    luma = synth.luma_sequence(176, 144, 2, seed=2)
+    req = np.zeros(2, dtype=MB_REQ)
+    req["mb_x"] = [16, 64]
+    req["mb_y"] = [32, 48]
+    req["slot_mask"] = (1 << 41) - 1
+    req["ffs_range"] = 8
+    req["blk"]["search_range"] = 8
+    req["blk"]["lambda"] = 100
+    with MotionEstimator({"SearchRange": 16, "SearchMode": 0}) as me:
+        me.upload_cur(luma[1])
+        me.upload_ref(0, 0, luma[0])
+        dev = torch.device("cuda:0")
+        d_out = torch.zeros(2 * NSLOT * BLOCK_RES.itemsize, dtype=torch.uint8, device=dev)
+
+        def run(r, mode):
+            d_req = torch.from_numpy(r.view(np.uint8).copy()).to(dev)
+            me.search_async(mode, d_req.data_ptr(), len(r), d_out.data_ptr())
+            me.search_status()
+
+        run(req, FAST_FULL_SEARCH)                      # within contract: no error
+        bad = req.copy()
+        bad["blk"][1, 17]["search_range"] = 12           # block range 12 > surface range 8
+        with pytest.raises(JmmeError):
+            run(bad, FAST_FULL_SEARCH)
+        run(req, FAST_FULL_SEARCH)                      # status is per launch
+        fs = req.copy()
+        fs["blk"][0, 3]["center_x"] = 6                  # sub-pel centre on the FS path
+        with pytest.raises(JmmeError):
+            run(fs, FULL_SEARCH)
+
+
+def test_planes_must_be_dword_aligned(gpu):
+    import torch
+    from jmme import FULL_SEARCH, JmmeError, MB_REQ, NSLOT, BLOCK_RES, MotionEstimator
+    dev = torch.device("cuda:0")
+    plane = torch.zeros(144 * 176 + 8, dtype=torch.uint8, device=dev)
+    req = np.zeros(1, dtype=MB_REQ)
+    req["slot_mask"] = 1
+    req["blk"][0, 0]["search_range"] = 4
+    d_req = torch.from_numpy(req.view(np.uint8).copy()).to(dev)
+    d_out = torch.zeros(NSLOT * BLOCK_RES.itemsize, dtype=torch.uint8, device=dev)
+    with MotionEstimator({"SearchRange": 4, "SearchMode": -1}) as me:
+        me.search_planes_async(FULL_SEARCH, plane.data_ptr(), plane.data_ptr(), 176, 176, 144,
+                               d_req.data_ptr(), 1, d_out.data_ptr())
+        me.search_status()
+        with pytest.raises(JmmeError):
+            me.search_planes_async(FULL_SEARCH, plane.data_ptr() + 1, plane.data_ptr(), 176, 176, 144,
+                                   d_req.data_ptr(), 1, d_out.data_ptr())
