@@ -94,6 +94,15 @@ struct jmme_ctx {
   size_t cap_pin = 0;
   uint8_t *d_sp = nullptr;
   size_t cap_sp = 0;
+  // low-latency small batches (launch_search_small): host-built items and the
+  // results in mapped pinned memory, the keys and completion counter on the device
+  int small_max_wg = 4096;                   // largest grid sent down the small path (0: never)
+  SmallItem *h_sitems = nullptr;
+  size_t cap_sitems = 0;
+  jmme_block_res *h_sout = nullptr;
+  size_t cap_sout = 0;
+  unsigned long long *d_skeys = nullptr;     // cap_sitems * JMME_NSLOT, ~0 between launches
+  unsigned *d_sdone = nullptr;
 };
 
 DevGuard::DevGuard(const jmme_ctx *c) {
@@ -288,6 +297,10 @@ extern "C" void jmme_destroy(jmme_ctx *ctx) {
   (void)hipFree(ctx->d_sub_table);
   (void)hipFree(ctx->d_sp);
   if (ctx->h_pin) (void)hipHostFree(ctx->h_pin);
+  if (ctx->h_sitems) (void)hipHostFree(ctx->h_sitems);
+  if (ctx->h_sout) (void)hipHostFree(ctx->h_sout);
+  (void)hipFree(ctx->d_skeys);
+  (void)hipFree(ctx->d_sdone);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
   delete ctx;
@@ -499,7 +512,117 @@ int validate(const jmme_ctx *ctx, int mode, const jmme_mb_req *req, int n) {
   return 0;
 }
 
+// ---- small batches (launch_search_small) -----------------------------------
+// The partitions of a unit that share a window and a predictor/lambda form one
+// item, as the plan kernel groups them (FS: centre, range, predictor, lambda;
+// FFS: the unit's surface + predictor, lambda and own range).
+void small_items(const jmme_ctx *ctx, int mode, const jmme_mb_req *req, int n, std::vector<SmallItem> &items,
+                 int *max_range) {
+  const bool ffs = mode == JMME_FAST_FULL_SEARCH;
+  items.clear();
+  *max_range = 0;
+  for (int u = 0; u < n; ++u) {
+    const jmme_mb_req &r = req[u];
+    uint64_t rem = r.slot_mask & ((1ull << JMME_NSLOT) - 1);
+    while (rem) {
+      const int lead = __builtin_ctzll(rem);
+      const jmme_block_req &a = r.blk[lead];
+      uint64_t gm = 0;
+      for (uint64_t m = rem; m; m &= m - 1) {
+        const int sl = __builtin_ctzll(m);
+        const jmme_block_req &b = r.blk[sl];
+        if (b.pred_x == a.pred_x && b.pred_y == a.pred_y && b.lambda == a.lambda && b.search_range == a.search_range &&
+            (ffs || (b.center_x == a.center_x && b.center_y == a.center_y)))
+          gm |= 1ull << sl;
+      }
+      rem &= ~gm;
+      SmallItem it{};
+      it.ref = ctx->d_refs[r.list * kMaxRefs + r.ref_idx];
+      it.gmask = gm;
+      it.u = u;
+      it.mb_x = r.mb_x;
+      it.mb_y = r.mb_y;
+      it.cqx = ffs ? r.ffs_center_x : a.center_x;
+      it.cqy = ffs ? r.ffs_center_y : a.center_y;
+      it.R = ffs ? r.ffs_range : a.search_range;
+      it.rs = a.search_range;
+      it.px = a.pred_x;
+      it.py = a.pred_y;
+      it.lam = a.lambda;
+      it.flags = (int16_t)(((!ffs && (gm & 1) && (r.blk[0].flags & JMME_BLK_CHECK00)) ? kItemChk00 : 0) |
+                           ((ffs && r.ffs_pos00_valid) ? kItemPreseed : 0));
+      *max_range = std::max(*max_range, (int)it.R);
+      items.push_back(it);
+    }
+  }
+}
+
+// 1 = served (results in out), 0 = too large for the small path, -1 = error
+int search_small(jmme_ctx *ctx, int mode, const jmme_mb_req *req, int n, jmme_block_res *out, hipStream_t s) {
+  if (ctx->small_max_wg <= 0) return 0;
+  std::vector<SmallItem> items;
+  int max_r = 0;
+  small_items(ctx, mode, req, n, items, &max_r);
+  const int tiles = (2 * max_r + 1 + kSmallTile - 1) / kSmallTile;
+  const long long wgs = (long long)items.size() * tiles * tiles;
+  if (items.empty() || wgs > ctx->small_max_wg) return items.empty() ? 1 : 0;
+  if (items.size() > ctx->cap_sitems) {
+    if (ctx->h_sitems) (void)hipHostFree(ctx->h_sitems);
+    (void)hipFree(ctx->d_skeys);
+    ctx->h_sitems = nullptr;
+    ctx->d_skeys = nullptr;
+    ctx->cap_sitems = 0;
+    const size_t cap = std::max<size_t>(256, items.size());
+    HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_sitems), cap * sizeof(SmallItem), hipHostMallocMapped));
+    HIPCHK(hipMalloc(&ctx->d_skeys, cap * JMME_NSLOT * sizeof(unsigned long long)));
+    HIPCHK(hipMemset(ctx->d_skeys, 0xff, cap * JMME_NSLOT * sizeof(unsigned long long)));
+    ctx->cap_sitems = cap;
+  }
+  if ((size_t)n * JMME_NSLOT > ctx->cap_sout) {
+    if (ctx->h_sout) (void)hipHostFree(ctx->h_sout);
+    ctx->h_sout = nullptr;
+    ctx->cap_sout = 0;
+    const size_t cap = std::max<size_t>(64 * JMME_NSLOT, (size_t)n * JMME_NSLOT);
+    HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_sout), cap * sizeof(jmme_block_res), hipHostMallocMapped));
+    ctx->cap_sout = cap;
+  }
+  if (!ctx->d_sdone) {
+    HIPCHK(hipMalloc(&ctx->d_sdone, sizeof(unsigned)));
+    HIPCHK(hipMemset(ctx->d_sdone, 0, sizeof(unsigned)));
+  }
+  std::memcpy(ctx->h_sitems, items.data(), items.size() * sizeof(SmallItem));
+  SmallParams p{};
+  p.cur = ctx->d_cur;
+  p.pitch = ctx->pitch;
+  p.width = ctx->width;
+  p.height = ctx->height;
+  p.mode = mode;
+  p.max_mvd = ctx->max_mvd;
+  void *d_items = nullptr, *d_sout = nullptr;
+  HIPCHK(hipHostGetDevicePointer(&d_items, ctx->h_sitems, 0));
+  HIPCHK(hipHostGetDevicePointer(&d_sout, ctx->h_sout, 0));
+  p.items = static_cast<const SmallItem *>(d_items);
+  p.n_items = (int)items.size();
+  p.tiles = tiles;
+  p.keys = ctx->d_skeys;
+  p.done = ctx->d_sdone;
+  p.out = static_cast<jmme_block_res *>(d_sout);
+  HIPCHK(launch_search_small(p, s));
+  HIPCHK(hipStreamSynchronize(s));
+  ctx->timed = false;
+  for (int i = 0; i < n; ++i)
+    for (int sl = 0; sl < JMME_NSLOT; ++sl)
+      if ((req[i].slot_mask >> sl) & 1) out[(size_t)i * JMME_NSLOT + sl] = ctx->h_sout[(size_t)i * JMME_NSLOT + sl];
+  return 1;
+}
+
 }  // namespace
+
+extern "C" int jmme_set_small_batch_limit(jmme_ctx *ctx, int max_workgroups) {
+  if (!ctx) return fail("null ctx");
+  ctx->small_max_wg = max_workgroups < 0 ? 0 : max_workgroups;
+  return 0;
+}
 
 extern "C" int jmme_search_mbs(jmme_ctx *ctx, int mode, const jmme_mb_req *req, int n, jmme_block_res *out) {
   DevGuard dg_(ctx);
@@ -508,8 +631,13 @@ extern "C" int jmme_search_mbs(jmme_ctx *ctx, int mode, const jmme_mb_req *req, 
   if (n == 0) return 0;
   if (!req || !out) return fail("null request/result array");
   if (validate(ctx, mode, req, n)) return -1;
-  if (ensure_units(ctx, (size_t)n)) return -1;
   hipStream_t s = nullptr;
+  // a batch of a few units: the low-latency path (one launch, no copies)
+  if (mode == JMME_FULL_SEARCH || mode == JMME_FAST_FULL_SEARCH) {
+    const int r = search_small(ctx, mode, req, n, out, s);
+    if (r != 0) return r < 0 ? -1 : 0;
+  }
+  if (ensure_units(ctx, (size_t)n)) return -1;
   if (sync_ref_table(ctx, s)) return -1;
   // pinned staging: [requests | results | status words]
   const size_t rq = align64((size_t)n * sizeof(jmme_mb_req)), rs = align64((size_t)n * JMME_NSLOT * sizeof(jmme_block_res));
@@ -995,20 +1123,23 @@ extern "C" int jmme_epzs_search(jmme_ctx *ctx, const jmme_epzs_req *req, int n, 
 
 // fractal quadtree (encode_one_macroblock): scratch carved from
 // one ctx buffer -- counts, the three id lists, the four levels' results
-extern "C" int jmme_fractal_encode_mbs_async(jmme_ctx *ctx, const uint8_t *d_org, const uint8_t *d_ref0, int pitch,
-                                             const uint32_t *const *d_words, int n_refs, int width, int height,
-                                             int search_range, double tol_16, double tol_8, jmme_fractal_mb *d_out,
-                                             void *stream) {
+extern "C" int jmme_fractal_encode_mb_rows_async(jmme_ctx *ctx, const uint8_t *d_org, const uint8_t *d_ref0,
+                                                 int pitch, const uint32_t *const *d_words, int n_refs, int width,
+                                                 int height, int mb_row0, int mb_row1, int search_range, double tol_16,
+                                                 double tol_8, jmme_fractal_mb *d_out, void *stream) {
   DevGuard dg_(ctx);
   if (!ctx) return fail("null ctx");
   if (fractal_geom_ok(pitch, width, height)) return -1;
   if (width % 16 || height % 16) return fail("fractal macroblock plane %dx%d: need multiples of 16", width, height);
   if (n_refs < 1 || n_refs > JMME_FRACTAL_MAX_VIEWS) return fail("n_refs %d not in 1..%d", n_refs, JMME_FRACTAL_MAX_VIEWS);
   if (search_range < 0) return fail("negative search range");
+  if (mb_row0 < 0 || mb_row1 > height / 16 || mb_row0 > mb_row1)
+    return fail("macroblock rows [%d,%d) outside [0,%d)", mb_row0, mb_row1, height / 16);
   if (!d_org || !d_ref0 || !d_words || !d_out) return fail("null array");
   for (int k = 0; k < n_refs; ++k)
     if (!d_words[k]) return fail("null words image for view %d", k);
-  const int mbs_x = width / 16, n_mb = mbs_x * (height / 16);
+  const int mbs_x = width / 16, n_mb = mbs_x * (mb_row1 - mb_row0);
+  if (n_mb == 0) return 0;
   const size_t res = sizeof(jmme_fractal_res);
   const size_t off_list1 = 256, off_list2 = off_list1 + (size_t)n_mb * 4, off_list3 = off_list2 + (size_t)n_mb * 16;
   const size_t off_res0 = (off_list3 + (size_t)n_mb * 16 + 255) & ~(size_t)255;
@@ -1036,6 +1167,7 @@ extern "C" int jmme_fractal_encode_mbs_async(jmme_ctx *ctx, const uint8_t *d_org
   p.range = search_range;
   p.mbs_x = mbs_x;
   p.n_mb = n_mb;
+  p.mb0 = mb_row0 * mbs_x;
   // `tol*tol*no` as the thesis writes it (block_enc.c:797, 1328, 1584)
   p.thr16 = tol_16 * tol_16 * 256;
   p.thr8 = tol_8 * tol_8 * 64;
@@ -1051,6 +1183,14 @@ extern "C" int jmme_fractal_encode_mbs_async(jmme_ctx *ctx, const uint8_t *d_org
   p.res[3] = reinterpret_cast<jmme_fractal_res *>(base + off_res3);
   HIPCHK(launch_fractal_tree(p, reinterpret_cast<hipStream_t>(stream)));
   return 0;
+}
+
+extern "C" int jmme_fractal_encode_mbs_async(jmme_ctx *ctx, const uint8_t *d_org, const uint8_t *d_ref0, int pitch,
+                                             const uint32_t *const *d_words, int n_refs, int width, int height,
+                                             int search_range, double tol_16, double tol_8, jmme_fractal_mb *d_out,
+                                             void *stream) {
+  return jmme_fractal_encode_mb_rows_async(ctx, d_org, d_ref0, pitch, d_words, n_refs, width, height, 0,
+                                           height > 0 ? height / 16 : 0, search_range, tol_16, tol_8, d_out, stream);
 }
 
 extern "C" int jmme_fractal_encode_mbs(jmme_ctx *ctx, const uint8_t *org, const uint8_t *const *refs, int n_refs,
@@ -1400,3 +1540,52 @@ extern "C" int jmme_subpel_refine(jmme_ctx *ctx, const jmme_subpel_req *req, int
   return 0;
 }
 static_assert(sizeof(jmme_subpel_req) == 48, "sub-pel ABI layout");
+
+// One-time start-up work out of the first search: HIP loads a translation
+// unit's kernels at their first launch and the item kernel's occupancy query is
+// cached on first use, so a tiny search through both search paths (and one
+// sub-image interpolation) on a dummy 64 x 64 plane pays for it here.
+extern "C" int jmme_prepare(jmme_ctx *ctx) {
+  DevGuard dg_(ctx);
+  if (!ctx) return fail("null ctx");
+  constexpr int kW = 64, kH = 64;
+  const auto g = sub_geom(kW, kH);
+  DevBuf plane, table, dreq, dout, subs;
+  HIPCHK(plane.alloc((size_t)kW * kH));
+  HIPCHK(hipMemset(plane.p, 0, (size_t)kW * kH));
+  std::vector<const uint8_t *> tab(kMaxLists * kMaxRefs, static_cast<const uint8_t *>(plane.p));
+  HIPCHK(table.alloc(tab.size() * sizeof(void *)));
+  HIPCHK(hipMemcpy(table.p, tab.data(), tab.size() * sizeof(void *), hipMemcpyHostToDevice));
+  jmme_mb_req r;
+  std::memset(&r, 0, sizeof r);
+  r.mb_x = 16;
+  r.mb_y = 16;
+  r.slot_mask = 1;
+  r.blk[0].search_range = (int16_t)std::min(1, ctx->cfg.SearchRange);
+  HIPCHK(dreq.alloc(sizeof r));
+  HIPCHK(hipMemcpy(dreq.p, &r, sizeof r, hipMemcpyHostToDevice));
+  HIPCHK(dout.alloc(JMME_NSLOT * sizeof(jmme_block_res)));
+  if (launch(ctx, JMME_FULL_SEARCH, static_cast<const uint8_t *>(plane.p), static_cast<const uint8_t *const *>(table.p),
+             kW, kW, kH, static_cast<const jmme_mb_req *>(dreq.p), 1, static_cast<jmme_block_res *>(dout.p), nullptr))
+    return -1;
+  // the small path reads the context's planes: borrow the dummy for one call
+  uint8_t *cur = ctx->d_cur, *ref0 = ctx->d_refs[0];
+  const int w = ctx->width, h = ctx->height, pitch = ctx->pitch;
+  ctx->d_cur = ctx->d_refs[0] = static_cast<uint8_t *>(plane.p);
+  ctx->width = kW;
+  ctx->height = kH;
+  ctx->pitch = kW;
+  jmme_block_res res[JMME_NSLOT];
+  const int rc = search_small(ctx, JMME_FULL_SEARCH, &r, 1, res, nullptr);
+  ctx->d_cur = cur;
+  ctx->d_refs[0] = ref0;
+  ctx->width = w;
+  ctx->height = h;
+  ctx->pitch = pitch;
+  if (rc < 0) return -1;
+  HIPCHK(subs.alloc(16 * g.plane_stride));
+  HIPCHK(launch_sub_images(static_cast<const uint8_t *>(plane.p), kW, kW, kH, static_cast<uint8_t *>(subs.p), g.pitch,
+                           g.plane_stride, nullptr));
+  HIPCHK(hipDeviceSynchronize());
+  return 0;
+}

@@ -208,7 +208,7 @@ __global__ __launch_bounds__(kWG) void tree_init_kernel(FractalTreeParams p) {
   if (valid) {
     uint64_t *rec = reinterpret_cast<uint64_t *>(p.out + mb);
     for (int i = lane; i < (int)(sizeof(jmme_fractal_mb) / 8); i += 64) rec[i] = 0;
-    const int bx = (mb % p.mbs_x) * 16, by = (mb / p.mbs_x) * 16;
+    const int bx = ((p.mb0 + mb) % p.mbs_x) * 16, by = ((p.mb0 + mb) / p.mbs_x) * 16;
     const int x = lane >> 2, y0 = (lane & 3) * 4;     // ii = x*16 + y0 + e
     int rv[4], dv[4], sr = 0, sd = 0;
 #pragma unroll
@@ -272,7 +272,7 @@ __global__ __launch_bounds__(kWG) void tree_search_kernel(FractalTreeParams p) {
     fp.height = p.height;
     fp.range = p.range;
     jmme_fractal_res *o = p.res[LEVEL] + t;
-    const int mb = LEVEL <= 1 ? id : id >> 2;
+    const int mb = p.mb0 + (LEVEL <= 1 ? id : id >> 2);   // ids are band-local, the picture is whole
     int bx = (mb % p.mbs_x) * 16, by = (mb / p.mbs_x) * 16;
     jmme_fractal_req rq;
     if (LEVEL == 0) {

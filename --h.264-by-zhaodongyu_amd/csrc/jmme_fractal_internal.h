@@ -31,6 +31,7 @@ struct FractalTreeParams {
   const uint32_t *words[JMME_FRACTAL_MAX_VIEWS];
   int n_refs, wpitch;
   int width, height, range, mbs_x, n_mb;
+  int mb0;                        // raster index of out[0] (an MB-row band starts there; 0 = whole plane)
   double thr16, thr8, thr_pair;   // tol_16^2*256, tol_8^2*64, tol_8^2*32 (thesis operand order)
   jmme_fractal_mb *out;
   jmme_fractal_res *res[4];

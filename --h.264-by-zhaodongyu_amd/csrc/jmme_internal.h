@@ -61,6 +61,39 @@ struct KParams {
 };
 // status bits (counts[2]): bit 0 range > lds_range, bit 1 sub-pel centre, bit 2 refine lost a winner
 
+// Low-latency form for small batches (a speculative batch after a failed
+// guess is one or two macroblocks): items built on the host, each item's
+// window split into 16x16-position tiles, one workgroup per (item, tile), exact
+// 64-bit keys combined with global atomicMin; the last workgroup to finish
+// writes the results (host-mapped memory) and resets the keys.
+struct SmallItem {
+  const uint8_t *ref;         // the item's 8-bit reference plane
+  unsigned long long gmask;   // partitions (slots) served
+  int u;                      // unit index (result row)
+  int16_t mb_x, mb_y;
+  int16_t cqx, cqy;           // window centre (qpel, integer grid)
+  int16_t R, rs;              // window range; FFS: the members' own range (<= R)
+  int16_t px, py;             // predictor (qpel)
+  int16_t flags, pad;         // kItemChk00 | kItemPreseed
+  int lam;
+  int pad2;
+};
+static_assert(sizeof(SmallItem) == 48, "SmallItem layout");
+
+struct SmallParams {
+  const uint8_t *cur;
+  int pitch, width, height;
+  int mode, max_mvd;
+  const SmallItem *items;             // n_items (device-readable: host-mapped pinned memory)
+  int n_items;
+  int tiles;                          // tiles per item side: ceil((2 * max R + 1) / 16)
+  unsigned long long *keys;           // [n_items * JMME_NSLOT], ~0 between launches (device memory)
+  unsigned *done;                     // workgroups finished, 0 between launches (device memory)
+  jmme_block_res *out;                // [units * JMME_NSLOT] (host-mapped); only searched slots written
+};
+constexpr int kSmallTile = 16;
+hipError_t launch_search_small(const SmallParams &p, hipStream_t s);
+
 size_t items_lds_bytes(int lds_range);
 // plan (unit requests -> items), then the persistent 32-bit and 64-bit item
 // kernels; ev0/ev1 (optional) bracket the main search kernel

@@ -1491,6 +1491,105 @@ __global__ __launch_bounds__(kWG, KEY32 ? JMME_WAVES_PER_EU : 2) void me_items_k
 #endif
 }
 
+// ------------------------------------------------------- small batches --
+// One workgroup per (item, 16x16 tile of window positions).  The tile's
+// reference pels (31 x 31, clamped into the picture as UMVLine4X does) are
+// staged as words (word[y][x] = pels x..x+3), the current MB as 64 dwords;
+// thread (tx, ty) evaluates one position: 16 4x4 SADs, the 41 partition SADs,
+// and for every served partition the exact key cost << 32 | rank, reduced over
+// the wave and folded into the item's global key with atomicMin.  The last
+// workgroup to finish converts the keys to results and resets them.
+template <bool FFS>
+__global__ __launch_bounds__(kWG) void me_small_kernel(SmallParams p) {
+  constexpr int kT = kSmallTile, kRows = kT + 15, kWPs = kT + 12;   // 31 rows x 28 words
+  __shared__ uint32_t s_w[kRows * kWPs];
+  __shared__ uint32_t s_cur[64];
+  __shared__ int s_last;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int tpi = p.tiles * p.tiles;
+  const int ii = blockIdx.x / tpi, t = blockIdx.x - ii * tpi;
+  const SmallItem it = p.items[ii];
+  const int R = it.R;
+  const int ox0 = -R + kT * (t % p.tiles), oy0 = -R + kT * (t / p.tiles);
+  const bool active = ox0 <= R && oy0 <= R;              // uniform over the workgroup
+  if (active) {
+    const int X0 = it.mb_x + (it.cqx >> 2) + ox0, Y0 = it.mb_y + (it.cqy >> 2) + oy0;
+    for (int i = tid; i < kRows * kWPs; i += kWG) {
+      const int r = i / kWPs, c = i - r * kWPs;
+      const uint8_t *row = it.ref + (size_t)clampi(Y0 + r, 0, p.height - 1) * p.pitch;
+      uint32_t w = 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) w |= (uint32_t)row[clampi(X0 + c + b, 0, p.width - 1)] << (8 * b);
+      s_w[i] = w;
+    }
+    if (tid < 64)
+      s_cur[tid] = *reinterpret_cast<const uint32_t *>(p.cur + (size_t)(it.mb_y + (tid >> 2)) * p.pitch + it.mb_x +
+                                                       4 * (tid & 3));
+  }
+  __syncthreads();
+  if (active) {
+    const int tx = tid % kT, ty = tid / kT;
+    const int ox = ox0 + tx, oy = oy0 + ty;
+    uint32_t a[16];
+#pragma unroll
+    for (int by = 0; by < 4; ++by)
+#pragma unroll
+      for (int bx = 0; bx < 4; ++bx) {
+        uint32_t sad = 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          sad = __builtin_amdgcn_sad_u8(s_w[(ty + 4 * by + r) * kWPs + tx + 4 * bx], s_cur[(4 * by + r) * 4 + bx], sad);
+        a[by * 4 + bx] = sad;
+      }
+    uint32_t ps[kNS];
+    partition_sads(a, ps);
+    GroupCtx g;
+    g.R = R; g.cqx = it.cqx; g.cqy = it.cqy; g.px = it.px; g.py = it.py; g.lam = it.lam;
+    g.max_mvd = p.max_mvd; g.preseed = FFS && (it.flags & kItemPreseed); g.gmask = it.gmask; g.rs = it.rs;
+    g.chk00 = !FFS && (it.flags & kItemChk00);
+    const int candx = it.cqx + 4 * ox, candy = it.cqy + 4 * oy;
+    const bool is00 = candx == 0 && candy == 0;
+    const MvCost mc = mv_cost<FFS>(candx, candy, it.px, it.py, it.lam, p.max_mvd);
+    const bool ok = ox <= R && oy <= R && pos_eligible<FFS>(g, mc.ok, max(abs(ox), abs(oy)), is00);
+    const int sidx = spiral_index_bl(ox, oy);
+    const uint32_t rank = FFS ? ((g.preseed && is00) ? 0u : (uint32_t)sidx + 1u) : (uint32_t)sidx;
+#pragma unroll
+    for (int sl = 0; sl < kNS; ++sl) {
+      if (!((it.gmask >> sl) & 1)) continue;
+      const uint32_t mvc = (!FFS && g.chk00 && sl == 0) ? check00_adjust(mc.mvc, it.lam, is00) : mc.mvc;
+      unsigned long long k = ok ? (((unsigned long long)((ps[sl] << 5) + mvc) << 32) | rank) : ~0ull;
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) {
+        const unsigned lo = __shfl_xor((unsigned)k, o, 64), hi = __shfl_xor((unsigned)(k >> 32), o, 64);
+        const unsigned long long x = ((unsigned long long)hi << 32) | lo;
+        k = x < k ? x : k;
+      }
+      if (lane == 0 && k != ~0ull) atomicMin(p.keys + (size_t)ii * kNS + sl, k);
+    }
+  }
+  // the last workgroup to finish writes every result
+  __threadfence();
+  __syncthreads();
+  if (tid == 0)
+    s_last = __hip_atomic_fetch_add(p.done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();
+  for (int i = tid; i < p.n_items * kNS; i += kWG) {
+    const int j = i / kNS, sl = i - j * kNS;
+    const SmallItem q = p.items[j];
+    unsigned long long *kp = p.keys + i;
+    if ((q.gmask >> sl) & 1) {
+      const unsigned long long k = __hip_atomic_load(kp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      GroupCtx g{};
+      g.cqx = q.cqx; g.cqy = q.cqy;
+      p.out[(size_t)q.u * kNS + sl] = block_result<FFS>(g, k != ~0ull, (uint32_t)(k & 0xffffffffu), (uint32_t)(k >> 32));
+      __hip_atomic_store(kp, ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  if (tid == 0) __hip_atomic_store(p.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 struct Occupancy {
   int cus = 0;
   int wg[4][JMME_MAX_RANGE + 1] = {};   // resident workgroups per CU, by kernel variant and lds range
@@ -1554,6 +1653,14 @@ hipError_t launch_search(const KParams &p, hipStream_t s, hipEvent_t ev0, hipEve
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (ev1) (void)hipEventRecord(ev1, s);
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_search_small(const SmallParams &p, hipStream_t s) {
+  if (p.n_items <= 0) return hipSuccess;
+  const dim3 grid((unsigned)(p.n_items * p.tiles * p.tiles));
+  if (p.mode == JMME_FAST_FULL_SEARCH) hipLaunchKernelGGL(me_small_kernel<true>, grid, dim3(kWG), 0, s, p);
+  else hipLaunchKernelGGL(me_small_kernel<false>, grid, dim3(kWG), 0, s, p);
   return hipGetLastError();
 }
 

@@ -109,6 +109,8 @@ def lib() -> ctypes.CDLL:
         "jmme_search_mbs_async": (I, [P, I, P, I, P, P]),
         "jmme_search_mbs_planes_async": (I, [P, I, P, P, I, I, I, P, I, P, P]),
         "jmme_search_status": (I, [P, P]),
+        "jmme_set_small_batch_limit": (I, [P, I]),
+        "jmme_prepare": (I, [P]),
         "jmme_full_search_block": (ctypes.c_int64, [P, I, I, I, I, I, P, P, ctypes.c_int64, I, I, I]),
         "jmme_fast_full_search_block": (ctypes.c_int64, [P, I, I, I, I, I, P, P, I, I, I, P, ctypes.c_int64, I]),
         "jmme_last_kernel_ms": (ctypes.c_float, [P]),
@@ -128,6 +130,7 @@ def lib() -> ctypes.CDLL:
         "jmme_epzs_search": (I, [P, P, I, P, I, P, I, P]),
         "jmme_epzs_search_async": (I, [P, P, I, P, P, P, P]),
         "jmme_fractal_encode_mbs_async": (I, [P, P, P, I, P, I, I, I, I, D, D, P, P]),
+        "jmme_fractal_encode_mb_rows_async": (I, [P, P, P, I, P, I, I, I, I, I, I, D, D, P, P]),
         "jmme_fractal_decode_mbs": (I, [P, P, P, I, I, I, I, I, P]),
         "jmme_fractal_decode_mbs_async": (I, [P, P, P, I, I, I, I, I, P, P, P]),
         "jmme_quant4x4_async": (I, [P, P, P, P, P, P, P, P, I, P]),

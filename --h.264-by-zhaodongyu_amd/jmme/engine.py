@@ -115,6 +115,10 @@ class MotionEstimator:
                                                  ctypes.c_void_p(d_req), int(n), ctypes.c_void_p(d_out),
                                                  ctypes.c_void_p(stream)))
 
+    def set_small_batch_limit(self, max_workgroups: int) -> None:
+        """Largest batch (in 16x16-position workgroups) `search` serves by the low-latency path; 0: never."""
+        check(lib().jmme_set_small_batch_limit(self._ctx, int(max_workgroups)))
+
     def search_status(self, stream: int = 0) -> None:
         """Raise if the last device-request search refused a request (synchronises)."""
         check(lib().jmme_search_status(self._ctx, ctypes.c_void_p(stream)))
@@ -316,6 +320,16 @@ class MotionEstimator:
         ptrs = (ctypes.c_void_p * len(d_words))(*d_words)
         check(lib().jmme_fractal_encode_mbs_async(self._ctx, d_org, d_ref0, pitch, ptrs, len(d_words), width, height,
                                                   int(search_range), float(tol_16), float(tol_8), d_out, stream))
+
+    def fractal_encode_mb_rows_async(self, d_org: int, d_ref0: int, pitch: int, d_words, width: int, height: int,
+                                     mb_row0: int, mb_row1: int, search_range: int, tol_16: float, tol_8: float,
+                                     d_out: int, stream: int = 0) -> None:
+        """fractal_encode_mbs_async for the macroblock rows [mb_row0, mb_row1) only (an MB-row band):
+        d_out receives (width/16)*(mb_row1-mb_row0) FRACTAL_MB records."""
+        ptrs = (ctypes.c_void_p * len(d_words))(*d_words)
+        check(lib().jmme_fractal_encode_mb_rows_async(self._ctx, d_org, d_ref0, pitch, ptrs, len(d_words), width,
+                                                      height, int(mb_row0), int(mb_row1), int(search_range),
+                                                      float(tol_16), float(tol_8), d_out, stream))
 
     def fast_full_search_block(self, list_idx, ref_idx, pos_x, pos_y, blocktype, pred, search_center,
                                surface_range, block_range, rdopt, lambda_factor, min_mcost=_lib.DISTBLK_MAX):

@@ -15,6 +15,15 @@ to use N GPUs, one process per GPU, torch.distributed over RCCL:
   full plane, not a halo).  The per-partition results are all-gathered back
   in band order, which is raster order.
 
+The thesis's fractal P-frame coder shards the same way, without the
+sequential dependency inside a frame: range blocks carry no predictor
+(encode_Oneframe, ZL/src/image.c:1108-1127), so each rank takes a band of
+macroblock (or 4x4 range-block) rows, the src rank broadcasts the range plane
+and the reference (domain) views, every rank builds its own domain images
+(words / box sums) from the received planes, searches its band against the
+whole reference, and the per-macroblock trees (or per-block results) are
+all-gathered in raster order.  `fractal_band_step`.
+
 Nothing here computes a search: the caller passes the engine call, so the
 same bookkeeping runs on RCCL with the HIP engine and on gloo in the CPU
 tests.
@@ -74,12 +83,30 @@ def gather_bands(local: torch.Tensor, counts: Sequence[int], group=None) -> torc
     return torch.cat([parts[r][:counts[r]] for r in range(ws)])
 
 
+def band_exchange(planes: Sequence[torch.Tensor], d_out_band: torch.Tensor, counts: Sequence[int],
+                  work: Callable[[], None], src: int = 0, group=None) -> torch.Tensor:
+    """Broadcast the planes, run this rank's band (`work()` enqueues it on the
+    current stream, writing d_out_band[:counts[rank]]), all-gather every
+    band's rows in rank order."""
+    broadcast_planes(planes, src=src, group=group)
+    work()
+    return gather_bands(d_out_band, counts, group=group)
+
+
+def fractal_band_step(planes: Sequence[torch.Tensor], d_out_band: torch.Tensor, counts: Sequence[int],
+                      encode_band: Callable[[torch.Tensor], None], src: int = 0, group=None) -> torch.Tensor:
+    """One band-sharded fractal P-frame: broadcast [range plane, view 0, view 1, ...],
+    encode this rank's band (`encode_band(d_out_band)` builds the local domain
+    images from the received views and encodes the band's rows), all-gather the
+    bands' records (raster order)."""
+    return band_exchange(planes, d_out_band, counts, lambda: encode_band(d_out_band), src=src, group=group)
+
+
 def band_step(planes: Sequence[torch.Tensor], d_req_band: torch.Tensor, n_band: int, d_out_band: torch.Tensor,
               counts: Sequence[int], search: Callable[[torch.Tensor, int, torch.Tensor], None],
               src: int = 0, group=None) -> torch.Tensor:
     """One band-sharded frame: broadcast the planes, search this rank's band,
     all-gather every band's results (raster order).  `search(d_req, n, d_out)`
     enqueues the engine call on the current stream."""
-    broadcast_planes(planes, src=src, group=group)
-    search(d_req_band, n_band, d_out_band)
-    return gather_bands(d_out_band, counts, group=group)
+    return band_exchange(planes, d_out_band, counts, lambda: search(d_req_band, n_band, d_out_band), src=src,
+                         group=group)

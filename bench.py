@@ -36,6 +36,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(REPO, "--h.264-by-zhaodongyu_amd")
 sys.path.insert(0, PKG)
 sys.path.insert(0, os.path.join(REPO, "tests"))
+sys.path.insert(0, os.path.join(REPO, "tools"))
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -378,6 +379,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-subpel", action="store_true")
     ap.add_argument("--no-uhd", action="store_true")
+    ap.add_argument("--no-fractal", action="store_true", help="skip the configs[2] block (fractal full pool)")
+    ap.add_argument("--no-hybrid", action="store_true", help="skip the configs[4] block (joint codec frame)")
+    ap.add_argument("--no-dropin", action="store_true", help="skip the in-encoder block (lencod vs lencod_jmme)")
     ap.add_argument("--shard", choices=["gop", "band"], default="gop",
                     help="gop: each rank searches its own frames (weak, default); band: rank 0 broadcasts "
                          "each frame's planes over RCCL and every rank searches an MB-row band (strong)")
@@ -490,6 +494,15 @@ def main():
             line["subpel"] = subpel_block(dev, local)
         if not args.no_uhd and ws == 1:
             line["uhd"] = uhd_block(dev, local)
+        if not args.no_fractal and ws == 1:
+            import bench_blocks
+            line["fractal"] = bench_blocks.fractal_block(dev, local)
+        if not args.no_hybrid and ws == 1:
+            import bench_blocks
+            line["hybrid"] = bench_blocks.hybrid_block(dev, local, load_workload)
+        if not args.no_dropin and ws == 1:
+            import bench_blocks
+            line["dropin"] = bench_blocks.dropin_block()
         print(json.dumps(line))
     me.close()
     if ws > 1:

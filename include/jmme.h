@@ -143,6 +143,17 @@ int jmme_slot(int blocktype, int block_x, int block_y);
 /* mode = JMME_FULL_SEARCH or JMME_FAST_FULL_SEARCH.  Host arrays, synchronous.
  * out has n * JMME_NSLOT entries (unsearched slots are left untouched). */
 int jmme_search_mbs(jmme_ctx *ctx, int mode, const jmme_mb_req *req, int n, jmme_block_res *out);
+/* jmme_search_mbs serves a batch whose work items (partition groups sharing a
+ * window and predictor) fit in at most `max_workgroups` workgroups of 16x16
+ * window positions by a single low-latency launch (no device copies, results
+ * written to mapped host memory) -- the speculative batches of the JM drop-in
+ * are mostly one or two macroblocks.  Default 4096; 0 sends everything down the
+ * throughput path.  Results are identical either way. */
+int jmme_set_small_batch_limit(jmme_ctx *ctx, int max_workgroups);
+/* Pay the one-time start-up costs (HIP loads a module's kernels at their first
+ * launch; occupancy queries are cached on first use) with a search on a dummy
+ * plane, so that the first real search is not charged for them.  Optional. */
+int jmme_prepare(jmme_ctx *ctx);
 
 /* Device-resident variant for pipelines and the benchmark: d_req/d_out are
  * device pointers, planes are those already uploaded; enqueued on `stream`
@@ -468,6 +479,15 @@ int jmme_fractal_encode_mbs_async(jmme_ctx *ctx, const uint8_t *d_org, const uin
                                   const uint32_t *const *d_words, int n_refs, int width, int height,
                                   int search_range, double tol_16, double tol_8, jmme_fractal_mb *d_out,
                                   void *stream);
+/* the same for the macroblock rows [mb_row0, mb_row1) of the plane only (an
+ * MB-row band of a multi-GPU split): the searches still see the
+ * whole picture (bound_chk's frame limits, domain blocks outside the band), so
+ * the band's trees are identical to those rows of the whole-plane encode;
+ * d_out[(width/16)*(mb_row1-mb_row0)], raster order from row mb_row0 */
+int jmme_fractal_encode_mb_rows_async(jmme_ctx *ctx, const uint8_t *d_org, const uint8_t *d_ref0, int pitch,
+                                      const uint32_t *const *d_words, int n_refs, int width, int height,
+                                      int mb_row0, int mb_row1, int search_range, double tol_16, double tol_8,
+                                      jmme_fractal_mb *d_out, void *stream);
 
 /* ---- Fractal decoder (reconstruction of a P plane from its trees) -------
  * decode_one_macroblock, decode_block_rect, decode_block_8, decode_block_4

@@ -27,6 +27,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "global.h"
 #include "mbuffer.h"
@@ -39,6 +40,7 @@ extern distblk __real_sub_pel_motion_estimation(Macroblock *, MotionVector *, ME
 extern distblk __real_full_search_motion_estimation(Macroblock *, MotionVector *, MEBlock *, distblk, int);
 extern distblk __real_fast_full_search_motion_estimation(Macroblock *, MotionVector *, MEBlock *, distblk, int);
 extern void __real_setup_fast_full_search(Macroblock *, MEBlock *, int);
+extern void __real_init_motion_search_module(VideoParameters *, InputParameters *);
 
 extern void get_neighbors(Macroblock *currMB, PixelPos *block, int mb_x, int mb_y, int blockshape_x);
 
@@ -103,6 +105,19 @@ static void init_once(VideoParameters *p_Vid, InputParameters *p_Inp)
   c.SourceBitDepthLuma = p_Inp->source.bit_depth[0];
   g_me = jmme_create(&c, -1);
   if (!g_me) fail_jm("jmme_create");
+}
+
+/* init_motion_search_module (mv_search.c:315, called once from init_encoder,
+ * lencod.c:606) builds JM's ME tables; the GPU engine is created there too, and
+ * its one-time start-up (code-object loading, first-launch setup) is paid
+ * before any frame is timed, like JM's own table setup */
+void __wrap_init_motion_search_module(VideoParameters *p_Vid, InputParameters *p_Inp)
+{
+  __real_init_motion_search_module(p_Vid, p_Inp);
+  if (p_Inp->SearchMode[0] == FULL_SEARCH || p_Inp->SearchMode[0] == FAST_FULL_SEARCH) {
+    init_once(p_Vid, p_Inp);
+    if (jmme_prepare(g_me)) fail_jm("jmme_prepare");
+  }
 }
 
 /* planes of the picture being coded and of the reference (list, ref) */
@@ -200,6 +215,19 @@ static spec_ent *g_hyp = NULL;     /* the inputs behind each request's 41 slots 
 static int *g_req_mb = NULL;
 static int g_req_cap = 0;
 
+/* where a frame's batches come from and what they cost (reported at exit):
+ * misses past the batch's end vs inside it (a guess failed), per slot */
+static long long g_miss_past = 0, g_miss_guess = 0, g_miss_slot[JMME_NSLOT], g_units = 0;
+static double g_t_build = 0, g_t_call = 0;
+static FILE *g_trace = NULL;
+
+static double now_us(void)
+{
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec * 1e6 + ts.tv_nsec * 1e-3;
+}
+
 static spec_ent *spec_table(VideoParameters *p_Vid, int list, int ref)
 {
   int i;
@@ -272,6 +300,7 @@ static void spec_batch(int list, int ref, int mb0, const spec_ent *want, int chk
 {
   spec_ent *tab = g_spec[list][ref];
   int n = imin(g_batch, g_n_mb - mb0), nreq = 0, i, s, h, k, mb;
+  double t0 = now_us(), t1, t2;
   if (n * KHYP > g_req_cap) {
     free(g_req);
     free(g_res);
@@ -321,8 +350,14 @@ static void spec_batch(int list, int ref, int mb0, const spec_ent *want, int chk
       g_req_mb[nreq++] = mb;
     }
   }
+  t1 = now_us();
   if (jmme_search_mbs(g_me, want->mode ? JMME_FAST_FULL_SEARCH : JMME_FULL_SEARCH, g_req, nreq, g_res))
     fail_jm("jmme_search_mbs");
+  t2 = now_us();
+  g_t_build += t1 - t0;
+  g_t_call += t2 - t1;
+  g_units += nreq;
+  if (g_trace) fprintf(g_trace, "%d %d %d %.1f %.1f\n", mb0, n, nreq, t1 - t0, t2 - t1);
   for (i = 0; i < nreq; i++) {
     mb = g_req_mb[i];
     k = (i == 0 || g_req_mb[i - 1] != mb) ? 0 : k + 1;       /* guesses of one MB are consecutive */
@@ -345,8 +380,9 @@ static void spec_batch(int list, int ref, int mb0, const spec_ent *want, int chk
 static int speculating(void)
 {
   if (g_speculate < 0) {
-    const char *e = getenv("JMME_SPECULATE");
+    const char *e = getenv("JMME_SPECULATE"), *t = getenv("JMME_TRACE");
     g_speculate = !(e && e[0] == '0');
+    if (t && *t) g_trace = fopen(t, "w");     /* per batch: mb0 n units build_us call_us */
   }
   return g_speculate;
 }
@@ -368,8 +404,14 @@ static const spec_ent *spec_lookup(Macroblock *currMB, MEBlock *mv_block, int li
       ++g_hits;
       return &e[k];
     }
-  if (mb < g_spec_end[list][ref]) g_batch = imax(1, g_batch / 2);         /* every guess failed */
-  else g_batch = imin(2048, g_batch * 2);                                /* ran past the batch */
+  if (mb < g_spec_end[list][ref]) {                                      /* every guess failed */
+    g_batch = imax(1, g_batch / 2);
+    ++g_miss_guess;
+    ++g_miss_slot[s];
+  } else {                                                               /* ran past the batch */
+    g_batch = imin(2048, g_batch * 2);
+    ++g_miss_past;
+  }
   spec_batch(list, ref, mb, want, chk_rule, currMB->p_Inp->rdopt);
   if (!spec_same(&e[0], want)) error("jm_gpu_me: batch lost its own request", 500);
   return &e[0];
@@ -692,6 +734,15 @@ static void report(void)
             g_calls, g_hits + g_batches, g_batches, g_cpu_calls);
     fprintf(stderr, "jm_gpu_me: %lld sub-pel refinements: %lld cached, %lld batches, %lld on the CPU\n",
             g_sp_calls, g_sp_hits, g_sp_batches, g_sp_cpu);
+    if (g_batches) {
+      int s;
+      fprintf(stderr, "jm_gpu_me: integer batches: %lld past the batch, %lld failed guesses; %lld units; "
+                      "%.1f ms building, %.1f ms in jmme_search_mbs; failed guesses by slot:",
+              g_miss_past, g_miss_guess, g_units, g_t_build * 1e-3, g_t_call * 1e-3);
+      for (s = 0; s < JMME_NSLOT; s++) fprintf(stderr, " %lld", g_miss_slot[s]);
+      fprintf(stderr, "\n");
+    }
+    if (g_trace) fclose(g_trace);
     if (g_me) jmme_destroy(g_me);
   }
 }

@@ -216,6 +216,27 @@ def fractal_search_batch(org, ref, R, req):
     return out, xy
 
 
+def host_threads(cap: int = 16) -> int:
+    """CPU threads this process may use, capped (the GPU box's share per GPU is 16)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(cap, n))
+
+
+def fractal_search_batch_par(org, ref, R, req, threads: int | None = None):
+    """fractal_search_batch over `threads` threads (ctypes drops the GIL for the
+    call; the restatement is a pure function of its arguments)."""
+    from concurrent.futures import ThreadPoolExecutor
+    req = np.ascontiguousarray(req, np.int32)
+    threads = threads or host_threads()
+    parts = np.array_split(np.arange(len(req)), threads)
+    with ThreadPoolExecutor(threads) as ex:
+        res = list(ex.map(lambda ix: fractal_search_batch(org, ref, R, req[ix]), parts))
+    return np.concatenate([r[0] for r in res]), np.concatenate([r[1] for r in res])
+
+
 def fractal_box_sums(plane, bsx, bsy):
     lib = load_fractal()
     plane = np.ascontiguousarray(plane, np.uint8)

@@ -179,3 +179,39 @@ def test_pool_mfma_matches_valu_kernel(me):
         mfma = me.fractal_search(org, ref, 4096, req)
         me.fractal_set_pool_min_range(80)
         assert valu.tobytes() == mfma.tobytes()
+
+
+def test_pool_1080p_every_4x4_full_pool(me):
+    """BASELINE configs[2] at full size: every 4x4 range block of a 1080p frame
+    (129,600 blocks) against the full domain pool (2,064,609 positions each).
+    * the matrix-core and the VALU bound tests give identical results on every block;
+    * every winner's rms is <= the windowed R = 4 result (a prefix of the same
+      spiral: the pool minimum cannot be worse);
+    * a seeded sample of 1,024 blocks equals the restatement's brute force."""
+    from jmme import FRACTAL_RES
+    W, H = 1920, 1080
+    org, ref = _frames(H, W, 77, gmv=(3, 2))
+    req = _all_blocks(W, H, 4, 4)
+    assert len(req) == 129600
+    R = max(W, H)
+    me.fractal_set_pool_min_range(0)
+    try:
+        me.fractal_set_pool_mfma(True)
+        mfma = me.fractal_search(org, ref, R, req)
+        me.fractal_set_pool_mfma(False)
+        valu = me.fractal_search(org, ref, R, req)
+        me.fractal_set_pool_mfma(True)
+        me.fractal_set_pool_min_range(NEVER)
+        seed = me.fractal_search(org, ref, 4, req)
+    finally:
+        me.fractal_set_pool_min_range(80)
+        me.fractal_set_pool_mfma(True)
+    assert mfma.dtype == FRACTAL_RES
+    diff = np.nonzero((mfma.view(np.uint8).reshape(len(req), -1) != valu.view(np.uint8).reshape(len(req), -1)).any(1))[0]
+    assert len(diff) == 0, (len(diff), diff[:5].tolist())
+    assert (mfma["rms"] <= seed["rms"]).all()
+    assert (mfma["rms"] < seed["rms"]).sum() > 500         # the pool finds better matches than the window (829 here)
+    sel = np.sort(np.random.default_rng(2024).choice(len(req), 1024, replace=False))
+    rq = np.stack([req["block_x"][sel], req["block_y"][sel], req["bsx"][sel], req["bsy"][sel]], 1).astype(np.int32)
+    exp, xy = ol.fractal_search_batch_par(org, ref, R, rq)
+    _same(mfma[sel], exp, xy, req[sel])

@@ -479,3 +479,79 @@ def test_planes_must_be_dword_aligned(gpu):
         with pytest.raises(JmmeError):
             me.search_planes_async(FULL_SEARCH, plane.data_ptr() + 1, plane.data_ptr(), 176, 176, 144,
                                    d_req.data_ptr(), 1, d_out.data_ptr())
+
+
+# ---- the low-latency small-batch path (jmme_set_small_batch_limit) -------------
+@pytest.mark.parametrize("name", ["c1_foreman_qcif_fs16", "c1_foreman_qcif_fs16_rdo0", "ffs_foreman_qcif_r16",
+                                  "ffs_foreman_qcif_r16_rdo0", "syn_cif_adv_fs32", "syn_cif_ffs32_rdo0_3ref"])
+def test_small_batches_match_jm_golden(name, gpu):
+    """JM's own searches sent three macroblocks at a time, as the drop-in's
+    speculative batches after a failed guess are: every call takes the
+    small-batch kernel, every result equals JM's."""
+    c = g.Case(name)
+    mode = g.manifest()[name]["cfg_overrides"]["SearchMode"]
+    with _engine(c, gpu) as me:
+        me.set_small_batch_limit(1 << 20)
+        n = 0
+        for f, lst, rf, idx in c.groups():
+            me.upload_cur(c.cur[f])
+            me.upload_ref(lst, rf, c.ref[(f, lst, rf)])
+            req, unit_of, slots = c.units(idx, mode)
+            out = np.zeros((len(req), 41), dtype=me.search(mode, req[:1]).dtype)
+            for a in range(0, len(req), 3):
+                out[a:a + 3] = me.search(mode, req[a:a + 3])
+            res = out[unit_of, slots]
+            assert np.array_equal(res["mv_x"], c.r["out_mv_x"][idx]), name
+            assert np.array_equal(res["mv_y"], c.r["out_mv_y"][idx]), name
+            assert np.array_equal(res["cost"], c.r["out_cost"][idx]), name
+            n += len(idx)
+    assert n == c.n
+
+
+@pytest.mark.parametrize("size,R,lam", [((3840, 2160), 32, 400), ((352, 288), 44, 400), ((176, 144), 0, 400),
+                                        ((352, 288), 16, 400000), ((1920, 1088), 64, 400)])
+def test_small_path_equals_throughput_path_fs(size, R, lam, gpu):
+    """Random FS units (centres far outside the picture, mixed windows and
+    predictors per MB, check_for_00, huge lambdas, R up to 64): the small-batch
+    kernel, the throughput kernels and the oracle agree on every partition."""
+    from jmme import FULL_SEARCH, MotionEstimator, synth
+    w, h = size
+    rng = np.random.default_rng(R + w + lam)
+    luma = synth.luma_sequence(w, h, 2, seed=w + R, gmv=(3, -2))
+    req = _random_units(rng, w, h, 6, R, lam_max=lam)
+    with MotionEstimator({"SearchRange": max(R, 1), "SearchMode": -1}) as me:
+        me.upload_cur(luma[1])
+        me.upload_ref(0, 0, luma[0])
+        me.set_small_batch_limit(1 << 20)
+        small = me.search(FULL_SEARCH, req)
+        me.set_small_batch_limit(0)
+        big = me.search(FULL_SEARCH, req)
+    assert small.tobytes() == big.tobytes()
+    keys, mv, cost = _oracle_units(luma[1], luma[0], req)
+    got = np.array([(small[u, s]["mv_x"], small[u, s]["mv_y"], small[u, s]["cost"]) for u, s in keys])
+    exp = np.column_stack([mv[:, 0], mv[:, 1], cost])
+    bad = np.nonzero(np.any(got != exp, axis=1))[0]
+    assert len(bad) == 0, [(keys[i], got[i].tolist(), exp[i].tolist()) for i in bad[:5]]
+
+
+@pytest.mark.parametrize("R,rdopt,far", [(16, 0, 0.0), (16, 1, 0.3), (32, 0, 0.3), (8, 1, 0.5)])
+def test_small_path_equals_throughput_path_ffs(R, rdopt, far, gpu):
+    from jmme import FAST_FULL_SEARCH, MotionEstimator
+    from jmme import synth
+    w, h = 352, 288
+    rng = np.random.default_rng(7 * R + rdopt)
+    luma = synth.luma_sequence(w, h, 2, seed=R + 5, gmv=(3, -2))
+    req, mbs, blk = _ffs_random(rng, w, h, 4, R, rdopt, far)
+    with MotionEstimator({"SearchRange": R, "SearchMode": 0, "RDOptimization": rdopt}) as me:
+        me.upload_cur(luma[1])
+        me.upload_ref(0, 0, luma[0])
+        me.set_small_batch_limit(1 << 20)
+        small = me.search(FAST_FULL_SEARCH, req)
+        me.set_small_batch_limit(0)
+        big = me.search(FAST_FULL_SEARCH, req)
+        max_mvd = me.max_mvd
+    assert small.tobytes() == big.tobytes()
+    mv, cost = ol.ffs_batch(luma[1], luma[0], R, max_mvd, rdopt, mbs, blk)
+    got = np.array([(small[u, s]["mv_x"], small[u, s]["mv_y"], small[u, s]["cost"]) for u in range(len(req))
+                    for s in range(41)])
+    assert np.array_equal(got, np.column_stack([mv[:, 0], mv[:, 1], cost]))

@@ -121,3 +121,60 @@ def test_band_rows_partition():
         sizes = [b - a for a, b in spans]
         assert max(sizes) - min(sizes) <= 1
     assert [shard.gop_owner(g, 4) for g in range(6)] == [0, 1, 2, 3, 0, 1]
+
+
+# ---- fractal P-frame, MB-row bands -----------------------
+FW, FH, FVIEWS = 96, 80, 2
+
+
+def _fractal_worker(rank, ws, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(ws))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        from fractal_scenes import gate_scene
+        from jmme import FRACTAL_MB, shard
+        org, views = gate_scene(FW, FH, 5, FVIEWS, scale=6)
+        rows = [shard.band_rows(FH // 16, r, ws) for r in range(ws)]
+        counts = [(b - a) * (FW // 16) for a, b in rows]
+        # only the owner holds the frame; the others get it from the broadcast
+        planes = [torch.from_numpy(p.copy()) if rank == 0 else torch.zeros((FH, FW), dtype=torch.uint8)
+                  for p in [org] + views]
+        rec = FRACTAL_MB.itemsize
+        t_out = torch.zeros((counts[rank], rec), dtype=torch.uint8)
+
+        def encode_band(d_out):
+            # stand-in for the HIP band encoder: the restatement of the planes this
+            # rank received, restricted to its rows (the GPU test checks that the
+            # HIP band form equals the whole-plane rows)
+            t = ol.fractal_encode_mbs(planes[0].numpy(), [p.numpy() for p in planes[1:]], 7, 8.0, 5.0)
+            a, b = rows[rank]
+            d_out[:] = torch.from_numpy(t[a * (FW // 16):b * (FW // 16)].view(np.uint8).reshape(-1, rec).copy())
+
+        full = shard.fractal_band_step(planes, t_out, counts, encode_band)
+        q.put((rank, counts, full.numpy().tobytes()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("ws", [2, 3])
+def test_fractal_band_shard_equals_single_process(ws):
+    from fractal_scenes import gate_scene
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_fractal_worker, args=(r, ws, port, q)) for r in range(ws)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    org, views = gate_scene(FW, FH, 5, FVIEWS, scale=6)
+    want = ol.fractal_encode_mbs(org, views, 7, 8.0, 5.0)
+    want = np.array(want, copy=True)
+    for rank, counts, got in res:
+        assert sum(counts) == (FW // 16) * (FH // 16)
+        g = np.frombuffer(got, want.dtype).copy()
+        for t in (g, want):
+            t["chun"][np.isnan(t["chun"])] = 0
+        assert g.tobytes() == want.tobytes(), f"rank {rank}: gathered trees differ from the single-process encode"

@@ -1,0 +1,232 @@
+"""bench.py's blocks for the BASELINE configs other than the headline one, each
+measured on rank 0 at N = 1 and printed inside the same JSON line:
+
+* fractal_block -- configs[2]: the thesis's full_search (ZL/src/block_enc.c:
+  1933-1977) of every 4x4 range block of a 1080p frame against the full domain
+  pool, on the pruned MFMA pool search (csrc/jmme_fractal_pool.hip);
+* hybrid_block  -- configs[4]: one frame of the joint fractal + H.264 codec
+  (jmme/hybrid.py): Y/U/V quadtrees over 4 views at the thesis's R = 7, their
+  reconstruction, and JM's FS +-32 ME of the bench frame;
+* dropin_block  -- the drop-in encoder itself: JM 18.5 lencod, stock vs
+  lencod_jmme (integration/), FS and FFS at 1080p, JM's own "Total ME time"
+  per P-frame and byte identity of the outputs.
+
+Each block reports its own parity against the restatement (fractal, parity
+with the thesis unpinned) or JM (ME), and a CPU baseline of the restatement on
+a bounded sample ("port").  The oracle is the checker only, never timed as
+the GPU's work."""
+from __future__ import annotations
+
+import time
+
+import numpy as np
+import torch
+
+MFMA_BF16_PEAK = 2.5e15        # MI355X_MICROARCH.md: dense BF16 MFMA
+FLOPS_PER_PAIR_44 = 64         # bound test of one (domain position, 4x4 range block) pair: 16 MACs x 2 (hi, lo)
+
+
+def _timed(fn, iters, dev):
+    fn()
+    torch.cuda.synchronize(dev)
+    st = torch.cuda.current_stream(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(iters):
+        fn()
+    e1.record(st)
+    torch.cuda.synchronize(dev)
+    return e0.elapsed_time(e1) / iters
+
+
+def fractal_block(dev, local: int, iters: int = 5, sample: int = 256) -> dict:
+    """configs[2]: 1920x1080, 129,600 4x4 range blocks, full domain pool
+    ((W-3)(H-3) = 2,064,609 positions per block).  One step = the reference's
+    words image + the search of every block (seeds, pool images, bound test,
+    exact survivors), inputs resident."""
+    import oracle_lib as ol
+    from jmme import FRACTAL_REQ, FRACTAL_RES, MotionEstimator, synth
+    W, H = 1920, 1080
+    luma = synth.luma_sequence(W, H, 2, seed=77, gmv=(3, 2))
+    org, ref = luma[1].astype(np.uint8), luma[0].astype(np.uint8)
+    ys, xs = np.mgrid[0:H:4, 0:W:4]
+    req = np.zeros(xs.size, FRACTAL_REQ)
+    req["block_x"], req["block_y"], req["bsx"], req["bsy"] = xs.ravel(), ys.ravel(), 4, 4
+    n, R = len(req), max(W, H)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    d_org, d_ref = torch.from_numpy(org).to(dev), torch.from_numpy(ref).to(dev)
+    d_words = torch.empty(W * H, dtype=torch.int32, device=dev)
+    d_req = torch.from_numpy(req.view(np.uint8).copy()).to(dev)
+    d_out = torch.empty(n * FRACTAL_RES.itemsize, dtype=torch.uint8, device=dev)
+    me = MotionEstimator(device=local)
+
+    def step():
+        me.fractal_words_async(d_ref.data_ptr(), W, W, H, d_words.data_ptr(), st)
+        me.fractal_search_async(d_org.data_ptr(), W, d_words.data_ptr(), W, H, R, d_req.data_ptr(), n,
+                                d_out.data_ptr(), st)
+    step()
+    torch.cuda.synchronize(dev)
+    me.fractal_pool_survivors()
+    ms = _timed(step, iters, dev)
+    surv = me.fractal_pool_survivors() / (iters + 1)
+    got = d_out.cpu().numpy().view(FRACTAL_RES)
+    me.close()
+    # parity + CPU baseline: the restatement's brute force on a seeded sample,
+    # over the host threads this process may use
+    threads = ol.host_threads()
+    sel = np.sort(np.random.default_rng(7).choice(n, sample, replace=False))
+    rq = np.stack([req["block_x"][sel], req["block_y"][sel], req["bsx"][sel], req["bsy"][sel]], 1).astype(np.int32)
+    t0 = time.time()
+    exp, xy = ol.fractal_search_batch_par(org, ref, R, rq, threads)
+    cpu_s = time.time() - t0
+    g = got[sel]
+    exact = int(np.sum((g["rms"] == exp[:, 0]) & (g["scale"] == exp[:, 1]) & (g["offset"] == exp[:, 2]) &
+                       (g["x"] == xy[:, 0]) & (g["y"] == xy[:, 1])))
+    pairs = n * (W - 3) * (H - 3)
+    flops = pairs * FLOPS_PER_PAIR_44
+    return {"workload": "configs[2]: 1080p (1920x1080) fractal full_search, every 4x4 range block (129,600) vs the "
+                        "full domain pool (2,064,609 positions each), thesis compute_rms / QUAN_A, pruned exact "
+                        "search (MFMA bound test)",
+            "range_blocks": n, "ms_per_frame": round(ms, 3), "range_blocks_per_s": round(n / (ms * 1e-3), 1),
+            "pairs_per_s": round(pairs / (ms * 1e-3), 1),
+            "exact_evals_per_block": round(surv / n, 3),
+            "roofline": {"bound": "mfma", "achieved": round(flops / (ms * 1e-3) / 1e12, 1),
+                         "peak": MFMA_BF16_PEAK / 1e12, "unit": "TFLOP/s",
+                         "frac": round(flops / (ms * 1e-3) / MFMA_BF16_PEAK, 4),
+                         "note": "algorithmic bound-test flops (64 per pair, bf16 hi/lo split) over the whole "
+                                 "frame time (words image, seeds and exact survivors included)"},
+            "parity": {"reference": "oracle/fractal_oracle.c (parity with the thesis unpinned)",
+                       "sample": int(sample), "bit_exact": exact},
+            "cpu_baseline": {"value": round(sample / cpu_s, 2), "unit": "range blocks/sec", "cores": threads,
+                             "kind": "port",
+                             "sample": f"{sample} seeded blocks of the same frame, thesis full_search restated "
+                                       f"(oracle/fractal_oracle.c), brute force over the full pool, {threads} "
+                                       f"threads: {cpu_s:.2f} s"}}
+
+
+def hybrid_block(dev, local: int, load_workload, iters: int = 10) -> dict:
+    """configs[4] per GPU: one 1080p frame of the joint codec (jmme/hybrid.py)."""
+    import oracle_lib as ol
+    from fractal_scenes import gate_scene
+    from jmme.hybrid import HybridFrameCoder
+    W, H = 1920, 1088
+    scene = [gate_scene(W, H, 11, 4, scale=6), gate_scene(W // 2, H // 2, 12, 4, scale=6),
+             gate_scene(W // 2, H // 2, 13, 4, scale=6)]
+    cur, ref, req, unit_of, slots, expect, meta = load_workload()
+    st = torch.cuda.current_stream(dev).cuda_stream
+    with HybridFrameCoder(W, H, n_views=4, fractal_range=7, tol_16=8.0, tol_8=5.0, device=local) as hc:
+        hc.load_fractal(scene)
+        hc.load_me(cur, ref, req)
+        ms_enc = _timed(lambda: hc.fractal_encode(st), iters, dev)
+        ms_dec = _timed(lambda: hc.fractal_decode(st), iters, dev)
+        ms_me = _timed(lambda: hc.motion_search(st), iters, dev)
+        ms = _timed(lambda: hc.step(st), iters, dev)
+        res = hc.me_results()[unit_of, slots]
+        me_exact = int(np.sum((res["mv_x"] == expect[0]) & (res["mv_y"] == expect[1]) & (res["cost"] == expect[2])))
+        pu = hc.planes[1]
+        got = np.array(pu.trees_host(), copy=True)
+        rec = pu.rec.cpu().numpy()
+        split = [int((p.trees_host()["mb"]["partition"] == 3).sum()) for p in hc.planes]
+    org_u, views_u = scene[1]
+    t0 = time.time()
+    exp = np.array(ol.fractal_encode_mbs(org_u, views_u, 7, 8.0, 5.0), copy=True)
+    cpu_s = time.time() - t0
+    for t in (got, exp):
+        t["chun"][np.isnan(t["chun"])] = 0
+    tree_exact = int((got.view(np.uint8).reshape(len(got), -1) == exp.view(np.uint8).reshape(len(exp), -1))
+                     .all(1).sum())
+    rc, rec_exp = ol.fractal_decode_mbs(exp, views_u, 2)
+    n_mb = sum(p.n_mb for p in hc.planes)
+    return {"workload": "configs[4] per GPU: one 1080p frame of the joint fractal + H.264 codec -- Y 1920x1088 and "
+                        "U, V 960x544 quadtrees (4 views, R 7, tol 8/5), their reconstruction, JM FS +-32 ME of "
+                        "8160 MB x ref",
+            "frames_per_s": round(1e3 / ms, 1), "ms_per_frame": round(ms, 4),
+            "stages_ms": {"fractal_encode_YUV": round(ms_enc, 4), "fractal_decode_YUV": round(ms_dec, 4),
+                          "h264_fs32_me": round(ms_me, 4)},
+            "fractal_macroblocks": n_mb, "split_macroblocks_YUV": split,
+            "parity": {"h264_me_vs_jm": {"searches": int(len(expect[0])), "bit_exact": me_exact},
+                       "u_trees_vs_restatement": {"macroblocks": len(exp), "bit_exact": tree_exact},
+                       "u_reconstruction_vs_restatement": bool(rc == 0 and np.array_equal(rec, rec_exp))},
+            "cpu_baseline": {"value": round(len(exp) / cpu_s, 1), "unit": "fractal macroblocks/sec", "cores": 1,
+                             "kind": "port", "sample": f"the U plane's quadtree ({len(exp)} MBs, 4 views), "
+                                                       f"oracle/fractal_oracle.c: {cpu_s:.2f} s"},
+            "scaling": "GOP replicas: a frame's P-frame refers to the previous reconstruction"}
+
+
+# ---- the drop-in encoder (JM 18.5 lencod with libjmme behind IntPelME) -----------
+def _lencod(binary, d, tag, yuv, w, h, frames, params, cfg_text, env=None):
+    import hashlib
+    import os
+    import re
+    import subprocess
+    cfg = os.path.join(d, "enc.cfg")
+    open(cfg, "w").write(cfg_text)
+    out, rec = os.path.join(d, f"{tag}.264"), os.path.join(d, f"{tag}_rec.yuv")
+    args = [binary, "-d", cfg, "-p", f"InputFile={yuv}", "-p", f"SourceWidth={w}", "-p", f"SourceHeight={h}",
+            "-p", f"OutputWidth={w}", "-p", f"OutputHeight={h}", "-p", f"FramesToBeEncoded={frames}",
+            "-p", f"OutputFile={out}", "-p", f"ReconFile={rec}"]
+    for k, v in params.items():
+        args += ["-p", f"{k}={v}"]
+    t0 = time.time()
+    r = subprocess.run(args, cwd=d, capture_output=True, text=True, timeout=900, env=dict(os.environ, **(env or {})))
+    wall = time.time() - t0
+    if r.returncode != 0:
+        raise RuntimeError(r.stdout[-1500:] + r.stderr[-1500:])
+    me = re.search(r"Total ME time for sequence\s*:\s*([0-9.]+) sec", r.stdout)
+    calls = re.search(r"jm_gpu_me: (\d+) integer-pel searches on the GPU \(libjmme\): (\d+) from (\d+) speculative",
+                      r.stderr)
+    stats = re.search(r"integer batches: (\d+) past the batch, (\d+) failed guesses; (\d+) units; ([0-9.]+) ms building, "
+                      r"([0-9.]+) ms in jmme_search_mbs", r.stderr)
+    sp = re.search(r"(\d+) sub-pel refinements: (\d+) cached, (\d+) batches, (\d+) on the CPU", r.stderr)
+    res = dict(wall_s=round(wall, 3), me_s=float(me.group(1)) if me else None,
+               md5=(hashlib.md5(open(out, "rb").read()).hexdigest(), hashlib.md5(open(rec, "rb").read()).hexdigest()))
+    if calls:
+        res.update(gpu_searches=int(calls.group(1)), batches=int(calls.group(3)),
+                   searches_from_cache=int(calls.group(2)) - int(calls.group(3)))
+    if stats:
+        res.update(batches_past_end=int(stats.group(1)), batches_failed_guess=int(stats.group(2)),
+                   batch_units=int(stats.group(3)), host_build_ms=float(stats.group(4)),
+                   engine_call_ms=float(stats.group(5)))
+    if sp:
+        res["subpel"] = dict(zip(("calls", "cached", "batches", "cpu"), map(int, sp.groups())))
+    return res
+
+
+def dropin_block(modes=((-1, "FS"), (0, "FFS")), size=(1920, 1080), frames=3, search_range=32) -> dict | None:
+    """JM 18.5 lencod, stock (CPU) and lencod_jmme (the same JM objects, integer-pel
+    ME through libjmme) on the same seeded clip: JM's own 'Total ME time' per
+    P-frame, and byte identity of bitstream and reconstruction.  The GPU engine is
+    created and warmed in init_motion_search_module (encoder start-up, before any
+    frame is timed)."""
+    import os
+    import tempfile
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    stock = os.path.join(repo, "oracle", "_ref", "lencod")
+    gpu = os.path.join(repo, "integration", "_build", "lencod_jmme")
+    if not (os.path.exists(stock) and os.path.exists(gpu)):
+        return None
+    from jmme import synth
+    from test_jm_dropin_gpu import CFG
+    w, h = size
+    out = {"workload": f"JM 18.5 lencod encoding a seeded {w}x{h} clip, {frames} frames (1 I + {frames - 1} P), "
+                       f"+-{search_range}, 1 ref, RDO off, sub-pel off: stock (1 core) vs the drop-in "
+                       f"(integer-pel ME on the GPU, one speculative batch per miss)",
+           "p_frames": frames - 1, "p_frame_macroblocks": (w // 16) * ((h + 15) // 16)}
+    with tempfile.TemporaryDirectory() as d:
+        yuv = os.path.join(d, "in.yuv")
+        synth.write_yuv420(yuv, synth.luma_sequence(w, h, frames, seed=2024, gmv=(5, 3)))
+        for mode, tag in modes:
+            params = {"SearchMode": mode, "SearchRange": search_range, "RDOptimization": 0,
+                      "NumberReferenceFrames": 1}
+            cpu = _lencod(stock, d, f"cpu{mode}", yuv, w, h, frames, params, CFG)
+            g = _lencod(gpu, d, f"gpu{mode}", yuv, w, h, frames, params, CFG)
+            p = frames - 1
+            out[tag] = {
+                "stock_me_ms_per_p_frame": round(cpu["me_s"] * 1e3 / p, 2),
+                "dropin_me_ms_per_p_frame": round(g["me_s"] * 1e3 / p, 2),
+                "me_speedup": round(cpu["me_s"] / g["me_s"], 2) if g["me_s"] else None,
+                "dropin_mb_per_s": round(out["p_frame_macroblocks"] * p / g["me_s"], 1) if g["me_s"] else None,
+                "byte_identical": cpu["md5"] == g["md5"],
+                "stock_wall_s": cpu["wall_s"], "dropin_wall_s": g["wall_s"],
+                "dropin": {k: v for k, v in g.items() if k not in ("md5", "me_s", "wall_s")}}
+    return out
