@@ -101,8 +101,8 @@ struct jmme_ctx {
   size_t cap_sitems = 0;
   jmme_block_res *h_sout = nullptr;
   size_t cap_sout = 0;
-  unsigned long long *d_skeys = nullptr;     // cap_sitems * JMME_NSLOT, ~0 between launches
-  unsigned *d_sdone = nullptr;
+  unsigned long long *d_skeys = nullptr;     // per (item, tile) keys, cap_skeys * JMME_NSLOT
+  size_t cap_skeys = 0;
 };
 
 DevGuard::DevGuard(const jmme_ctx *c) {
@@ -300,7 +300,6 @@ extern "C" void jmme_destroy(jmme_ctx *ctx) {
   if (ctx->h_sitems) (void)hipHostFree(ctx->h_sitems);
   if (ctx->h_sout) (void)hipHostFree(ctx->h_sout);
   (void)hipFree(ctx->d_skeys);
-  (void)hipFree(ctx->d_sdone);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
   delete ctx;
@@ -366,6 +365,13 @@ extern "C" void jmme_spiral_offset(int idx, int *ox, int *oy) { spiral_offset(id
 extern "C" int jmme_mvbits(int v) { return mvbits(v); }
 
 namespace {
+
+// host-array convenience: stage through device buffers owned by this call
+struct DevBuf {
+  void *p = nullptr;
+  ~DevBuf() { (void)hipFree(p); }
+  hipError_t alloc(size_t bytes) { return hipMalloc(&p, bytes ? bytes : 4); }
+};
 
 int ensure_units(jmme_ctx *ctx, size_t n) {
   if (n <= ctx->cap_units) return 0;
@@ -551,6 +557,12 @@ void small_items(const jmme_ctx *ctx, int mode, const jmme_mb_req *req, int n, s
       it.lam = a.lambda;
       it.flags = (int16_t)(((!ffs && (gm & 1) && (r.blk[0].flags & JMME_BLK_CHECK00)) ? kItemChk00 : 0) |
                            ((ffs && r.ffs_pos00_valid) ? kItemPreseed : 0));
+      it.bmask = 0;
+      for (uint64_t m = gm; m; m &= m - 1) {
+        const SlotGeom sg = slot_geom(__builtin_ctzll(m));
+        for (int y = 0; y < sg.h; ++y)
+          for (int x = 0; x < sg.w; ++x) it.bmask |= (uint16_t)(1u << ((sg.by + y) * 4 + sg.bx + x));
+      }
       *max_range = std::max(*max_range, (int)it.R);
       items.push_back(it);
     }
@@ -568,15 +580,19 @@ int search_small(jmme_ctx *ctx, int mode, const jmme_mb_req *req, int n, jmme_bl
   if (items.empty() || wgs > ctx->small_max_wg) return items.empty() ? 1 : 0;
   if (items.size() > ctx->cap_sitems) {
     if (ctx->h_sitems) (void)hipHostFree(ctx->h_sitems);
-    (void)hipFree(ctx->d_skeys);
     ctx->h_sitems = nullptr;
-    ctx->d_skeys = nullptr;
     ctx->cap_sitems = 0;
     const size_t cap = std::max<size_t>(256, items.size());
     HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_sitems), cap * sizeof(SmallItem), hipHostMallocMapped));
-    HIPCHK(hipMalloc(&ctx->d_skeys, cap * JMME_NSLOT * sizeof(unsigned long long)));
-    HIPCHK(hipMemset(ctx->d_skeys, 0xff, cap * JMME_NSLOT * sizeof(unsigned long long)));
     ctx->cap_sitems = cap;
+  }
+  if ((size_t)wgs > ctx->cap_skeys) {              // one key per (item, tile, partition)
+    (void)hipFree(ctx->d_skeys);
+    ctx->d_skeys = nullptr;
+    ctx->cap_skeys = 0;
+    const size_t cap = std::max<size_t>(4096, (size_t)wgs);
+    HIPCHK(hipMalloc(&ctx->d_skeys, cap * JMME_NSLOT * sizeof(unsigned long long) + cap * sizeof(int4)));
+    ctx->cap_skeys = cap;
   }
   if ((size_t)n * JMME_NSLOT > ctx->cap_sout) {
     if (ctx->h_sout) (void)hipHostFree(ctx->h_sout);
@@ -585,10 +601,6 @@ int search_small(jmme_ctx *ctx, int mode, const jmme_mb_req *req, int n, jmme_bl
     const size_t cap = std::max<size_t>(64 * JMME_NSLOT, (size_t)n * JMME_NSLOT);
     HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_sout), cap * sizeof(jmme_block_res), hipHostMallocMapped));
     ctx->cap_sout = cap;
-  }
-  if (!ctx->d_sdone) {
-    HIPCHK(hipMalloc(&ctx->d_sdone, sizeof(unsigned)));
-    HIPCHK(hipMemset(ctx->d_sdone, 0, sizeof(unsigned)));
   }
   std::memcpy(ctx->h_sitems, items.data(), items.size() * sizeof(SmallItem));
   SmallParams p{};
@@ -605,7 +617,7 @@ int search_small(jmme_ctx *ctx, int mode, const jmme_mb_req *req, int n, jmme_bl
   p.n_items = (int)items.size();
   p.tiles = tiles;
   p.keys = ctx->d_skeys;
-  p.done = ctx->d_sdone;
+  p.info = reinterpret_cast<int4 *>(ctx->d_skeys + ctx->cap_skeys * JMME_NSLOT);   // items <= workgroups <= cap
   p.out = static_cast<jmme_block_res *>(d_sout);
   HIPCHK(launch_search_small(p, s));
   HIPCHK(hipStreamSynchronize(s));
@@ -744,16 +756,6 @@ extern "C" jmme_distblk jmme_full_search_block(jmme_ctx *ctx, int list, int ref_
 }
 
 // ------------------------------------------------- transforms / quant / SATD --
-namespace {
-
-// host-array convenience: stage through device buffers owned by this call
-struct DevBuf {
-  void *p = nullptr;
-  ~DevBuf() { (void)hipFree(p); }
-  hipError_t alloc(size_t bytes) { return hipMalloc(&p, bytes ? bytes : 4); }
-};
-
-}  // namespace
 
 extern "C" int jmme_transform_async(jmme_ctx *ctx, int op, const int32_t *d_in, int32_t *d_out, int n, void *stream) {
   DevGuard dg_(ctx);

@@ -63,9 +63,9 @@ struct KParams {
 
 // Low-latency form for small batches (a speculative batch after a failed
 // guess is one or two macroblocks): items built on the host, each item's
-// window split into 16x16-position tiles, one workgroup per (item, tile), exact
-// 64-bit keys combined with global atomicMin; the last workgroup to finish
-// writes the results (host-mapped memory) and resets the keys.
+// window split into 16x16-position tiles, one workgroup per (item, tile)
+// storing its exact per-partition keys; a second launch takes the minimum over
+// tiles and writes the results (mapped host memory).
 struct SmallItem {
   const uint8_t *ref;         // the item's 8-bit reference plane
   unsigned long long gmask;   // partitions (slots) served
@@ -74,7 +74,8 @@ struct SmallItem {
   int16_t cqx, cqy;           // window centre (qpel, integer grid)
   int16_t R, rs;              // window range; FFS: the members' own range (<= R)
   int16_t px, py;             // predictor (qpel)
-  int16_t flags, pad;         // kItemChk00 | kItemPreseed
+  int16_t flags;              // kItemChk00 | kItemPreseed
+  uint16_t bmask;             // 4x4 blocks the served partitions cover (bit by*4+bx)
   int lam;
   int pad2;
 };
@@ -87,8 +88,8 @@ struct SmallParams {
   const SmallItem *items;             // n_items (device-readable: host-mapped pinned memory)
   int n_items;
   int tiles;                          // tiles per item side: ceil((2 * max R + 1) / 16)
-  unsigned long long *keys;           // [n_items * JMME_NSLOT], ~0 between launches (device memory)
-  unsigned *done;                     // workgroups finished, 0 between launches (device memory)
+  unsigned long long *keys;           // [n_items][tiles^2][JMME_NSLOT] per-tile keys (device memory)
+  int4 *info;                         // [n_items] gmask lo/hi, centre, unit, for the finish launch (device memory)
   jmme_block_res *out;                // [units * JMME_NSLOT] (host-mapped); only searched slots written
 };
 constexpr int kSmallTile = 16;

@@ -1492,102 +1492,153 @@ __global__ __launch_bounds__(kWG, KEY32 ? JMME_WAVES_PER_EU : 2) void me_items_k
 }
 
 // ------------------------------------------------------- small batches --
-// One workgroup per (item, 16x16 tile of window positions).  The tile's
-// reference pels (31 x 31, clamped into the picture as UMVLine4X does) are
-// staged as words (word[y][x] = pels x..x+3), the current MB as 64 dwords;
-// thread (tx, ty) evaluates one position: 16 4x4 SADs, the 41 partition SADs,
-// and for every served partition the exact key cost << 32 | rank, reduced over
-// the wave and folded into the item's global key with atomicMin.  The last
-// workgroup to finish converts the keys to results and resets them.
+// Latency form (the drop-in's speculative batches after a failed guess are one
+// or two macroblocks; a launch + sync round trip costs ~10 us and a lightly
+// loaded GPU runs at a low clock, so the critical path is what counts):
+//   * search launch: one workgroup per (item, 16x16 tile of window
+//     positions), one position per thread.  The tile's reference pels are
+//     staged as aligned dwords (clamped into the picture as UMVLine4X does),
+//     expanded to words (word[y][x] = pels x..x+3); per position only the 4x4
+//     SADs the item's partitions use are formed.  Per served partition the
+//     wave's minimum cost comes from 4 DPP steps + 4 readlanes, the smallest
+//     rank among the lanes holding it from a ballot (and, on a tie, one more
+//     such reduction); the 4 waves meet in LDS and the tile's exact key
+//     cost << 32 | rank is stored (no atomics, no fences);
+//   * finish launch: one thread per (item, partition) takes the minimum over
+//     the item's tiles and writes the result (mapped host memory).
+__host__ __device__ inline int small_rows() { return kSmallTile + 15; }
+constexpr int kSmallWP = kSmallTile + 12;   // words per staged row
+constexpr int kSmallRaw = 9;                // raw dwords per staged row (36 pels >= 3 + 28 + 3)
+
+// wave minimum of a u32, the same in every lane (scalar)
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+  v = dpp_min<0xB1>(v);    // quad_perm [1,0,3,2]
+  v = dpp_min<0x4E>(v);    // quad_perm [2,3,0,1]
+  v = dpp_min<0x141>(v);   // row_half_mirror
+  v = dpp_min<0x140>(v);   // row_mirror: every lane of a row of 16 holds the row's minimum
+  const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)v, 0), r1 = (uint32_t)__builtin_amdgcn_readlane((int)v, 16);
+  const uint32_t r2 = (uint32_t)__builtin_amdgcn_readlane((int)v, 32), r3 = (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
+  return min(min(r0, r1), min(r2, r3));
+}
+
 template <bool FFS>
 __global__ __launch_bounds__(kWG) void me_small_kernel(SmallParams p) {
-  constexpr int kT = kSmallTile, kRows = kT + 15, kWPs = kT + 12;   // 31 rows x 28 words
-  __shared__ uint32_t s_w[kRows * kWPs];
+  constexpr int kRows = kSmallTile + 15;
+  __shared__ uint32_t s_w[kRows * kSmallWP];
+  __shared__ uint32_t s_raw[kRows * kSmallRaw];
   __shared__ uint32_t s_cur[64];
-  __shared__ int s_last;
-  const int tid = threadIdx.x, lane = tid & 63;
+  __shared__ uint32_t s_cost[kWaves][kNS], s_rank[kWaves][kNS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int tpi = p.tiles * p.tiles;
   const int ii = blockIdx.x / tpi, t = blockIdx.x - ii * tpi;
   const SmallItem it = p.items[ii];
   const int R = it.R;
-  const int ox0 = -R + kT * (t % p.tiles), oy0 = -R + kT * (t / p.tiles);
-  const bool active = ox0 <= R && oy0 <= R;              // uniform over the workgroup
-  if (active) {
+  const int ox0 = -R + kSmallTile * (t % p.tiles), oy0 = -R + kSmallTile * (t / p.tiles);
+  unsigned long long *part = p.keys + ((size_t)ii * tpi + t) * kNS;
+  // what the finish launch needs of the item, in device memory (it would
+  // otherwise read the mapped host copy again)
+  if (t == 0 && tid == 0) p.info[ii] = make_int4((int)(unsigned)it.gmask, (int)(unsigned)(it.gmask >> 32),
+                                                 (int)(unsigned short)it.cqx | ((int)it.cqy << 16), it.u);
+  if (ox0 > R || oy0 > R) {                              // a tile past this item's window
+    if (tid < kNS && ((it.gmask >> tid) & 1)) part[tid] = ~0ull;
+    return;
+  }
+  {
     const int X0 = it.mb_x + (it.cqx >> 2) + ox0, Y0 = it.mb_y + (it.cqy >> 2) + oy0;
-    for (int i = tid; i < kRows * kWPs; i += kWG) {
-      const int r = i / kWPs, c = i - r * kWPs;
+    const int xa = X0 & ~3, sh = X0 - xa;
+    for (int i = tid; i < kRows * kSmallRaw; i += kWG) {
+      const int r = i / kSmallRaw, k = i - r * kSmallRaw;
       const uint8_t *row = it.ref + (size_t)clampi(Y0 + r, 0, p.height - 1) * p.pitch;
-      uint32_t w = 0;
+      const int x = xa + 4 * k;
+      uint32_t w;
+      if (x >= 0 && x + 3 < p.width) {
+        w = *reinterpret_cast<const uint32_t *>(row + x);
+      } else {
+        w = 0;
 #pragma unroll
-      for (int b = 0; b < 4; ++b) w |= (uint32_t)row[clampi(X0 + c + b, 0, p.width - 1)] << (8 * b);
-      s_w[i] = w;
+        for (int b = 0; b < 4; ++b) w |= (uint32_t)row[clampi(x + b, 0, p.width - 1)] << (8 * b);
+      }
+      s_raw[i] = w;
     }
     if (tid < 64)
       s_cur[tid] = *reinterpret_cast<const uint32_t *>(p.cur + (size_t)(it.mb_y + (tid >> 2)) * p.pitch + it.mb_x +
                                                        4 * (tid & 3));
+    __syncthreads();
+    for (int i = tid; i < kRows * kSmallWP; i += kWG) {
+      const int r = i / kSmallWP, c = i - r * kSmallWP, q = (sh + c) >> 2;
+      s_w[i] = __builtin_amdgcn_alignbyte(s_raw[r * kSmallRaw + q + 1], s_raw[r * kSmallRaw + q], (sh + c) & 3);
+    }
+    __syncthreads();
   }
-  __syncthreads();
-  if (active) {
-    const int tx = tid % kT, ty = tid / kT;
-    const int ox = ox0 + tx, oy = oy0 + ty;
-    uint32_t a[16];
+  const int tx = tid % kSmallTile, ty = tid / kSmallTile;
+  const int ox = ox0 + tx, oy = oy0 + ty;
+  uint32_t a[16];
 #pragma unroll
-    for (int by = 0; by < 4; ++by)
+  for (int b = 0; b < 16; ++b) {
+    a[b] = 0;
+    if ((it.bmask >> b) & 1) {
+      const int by = b >> 2, bx = b & 3;
 #pragma unroll
-      for (int bx = 0; bx < 4; ++bx) {
-        uint32_t sad = 0;
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          sad = __builtin_amdgcn_sad_u8(s_w[(ty + 4 * by + r) * kWPs + tx + 4 * bx], s_cur[(4 * by + r) * 4 + bx], sad);
-        a[by * 4 + bx] = sad;
-      }
-    uint32_t ps[kNS];
-    partition_sads(a, ps);
-    GroupCtx g;
-    g.R = R; g.cqx = it.cqx; g.cqy = it.cqy; g.px = it.px; g.py = it.py; g.lam = it.lam;
-    g.max_mvd = p.max_mvd; g.preseed = FFS && (it.flags & kItemPreseed); g.gmask = it.gmask; g.rs = it.rs;
-    g.chk00 = !FFS && (it.flags & kItemChk00);
-    const int candx = it.cqx + 4 * ox, candy = it.cqy + 4 * oy;
-    const bool is00 = candx == 0 && candy == 0;
-    const MvCost mc = mv_cost<FFS>(candx, candy, it.px, it.py, it.lam, p.max_mvd);
-    const bool ok = ox <= R && oy <= R && pos_eligible<FFS>(g, mc.ok, max(abs(ox), abs(oy)), is00);
-    const int sidx = spiral_index_bl(ox, oy);
-    const uint32_t rank = FFS ? ((g.preseed && is00) ? 0u : (uint32_t)sidx + 1u) : (uint32_t)sidx;
-#pragma unroll
-    for (int sl = 0; sl < kNS; ++sl) {
-      if (!((it.gmask >> sl) & 1)) continue;
-      const uint32_t mvc = (!FFS && g.chk00 && sl == 0) ? check00_adjust(mc.mvc, it.lam, is00) : mc.mvc;
-      unsigned long long k = ok ? (((unsigned long long)((ps[sl] << 5) + mvc) << 32) | rank) : ~0ull;
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) {
-        const unsigned lo = __shfl_xor((unsigned)k, o, 64), hi = __shfl_xor((unsigned)(k >> 32), o, 64);
-        const unsigned long long x = ((unsigned long long)hi << 32) | lo;
-        k = x < k ? x : k;
-      }
-      if (lane == 0 && k != ~0ull) atomicMin(p.keys + (size_t)ii * kNS + sl, k);
+      for (int r = 0; r < 4; ++r)
+        a[b] = __builtin_amdgcn_sad_u8(s_w[(ty + 4 * by + r) * kSmallWP + tx + 4 * bx], s_cur[(4 * by + r) * 4 + bx], a[b]);
     }
   }
-  // the last workgroup to finish writes every result
-  __threadfence();
-  __syncthreads();
-  if (tid == 0)
-    s_last = __hip_atomic_fetch_add(p.done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
-  __syncthreads();
-  if (!s_last) return;
-  __threadfence();
-  for (int i = tid; i < p.n_items * kNS; i += kWG) {
-    const int j = i / kNS, sl = i - j * kNS;
-    const SmallItem q = p.items[j];
-    unsigned long long *kp = p.keys + i;
-    if ((q.gmask >> sl) & 1) {
-      const unsigned long long k = __hip_atomic_load(kp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      GroupCtx g{};
-      g.cqx = q.cqx; g.cqy = q.cqy;
-      p.out[(size_t)q.u * kNS + sl] = block_result<FFS>(g, k != ~0ull, (uint32_t)(k & 0xffffffffu), (uint32_t)(k >> 32));
-      __hip_atomic_store(kp, ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+  uint32_t ps[kNS];
+  partition_sads(a, ps);
+  GroupCtx g;
+  g.R = R; g.cqx = it.cqx; g.cqy = it.cqy; g.px = it.px; g.py = it.py; g.lam = it.lam;
+  g.max_mvd = p.max_mvd; g.preseed = FFS && (it.flags & kItemPreseed); g.gmask = it.gmask; g.rs = it.rs;
+  g.chk00 = !FFS && (it.flags & kItemChk00);
+  const int candx = it.cqx + 4 * ox, candy = it.cqy + 4 * oy;
+  const bool is00 = candx == 0 && candy == 0;
+  const MvCost mc = mv_cost<FFS>(candx, candy, it.px, it.py, it.lam, p.max_mvd);
+  const bool ok = ox <= R && oy <= R && pos_eligible<FFS>(g, mc.ok, max(abs(ox), abs(oy)), is00);
+  const int sidx = spiral_index_bl(ox, oy);
+  const uint32_t rank = FFS ? ((g.preseed && is00) ? 0u : (uint32_t)sidx + 1u) : (uint32_t)sidx;
+#pragma unroll
+  for (int sl = 0; sl < kNS; ++sl) {
+    if (!((it.gmask >> sl) & 1)) continue;
+    const uint32_t mvc = (!FFS && g.chk00 && sl == 0) ? check00_adjust(mc.mvc, it.lam, is00) : mc.mvc;
+    const uint32_t cost = ok ? (ps[sl] << 5) + mvc : ~0u;
+    const uint32_t cmin = wave_min_u32(cost);
+    const unsigned long long at = __builtin_amdgcn_ballot_w64(cost == cmin);
+    uint32_t rmin = (uint32_t)__builtin_amdgcn_readlane((int)rank, __builtin_ctzll(at));
+    if (at & (at - 1)) rmin = wave_min_u32(cost == cmin ? rank : ~0u);   // a tie: the first in spiral order
+    if (lane == 0) { s_cost[wave][sl] = cmin; s_rank[wave][sl] = rmin; }
   }
-  if (tid == 0) __hip_atomic_store(p.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  if (tid < kNS && ((it.gmask >> tid) & 1)) {
+    unsigned long long k = ~0ull;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) {
+      const uint32_t c = s_cost[w][tid];
+      const unsigned long long kw = c == ~0u ? ~0ull : (((unsigned long long)c << 32) | s_rank[w][tid]);
+      k = kw < k ? kw : k;
+    }
+    part[tid] = k;
+  }
+}
+
+// the results of a small batch: one thread per (item, partition), the minimum
+// over the item's tiles (the kernel boundary orders it after the search launch)
+template <bool FFS>
+__global__ __launch_bounds__(kWG) void small_finish_kernel(SmallParams p) {
+  const int i = blockIdx.x * kWG + threadIdx.x;
+  if (i >= p.n_items * kNS) return;
+  const int j = i / kNS, sl = i - j * kNS;
+  const int4 q = p.info[j];
+  const unsigned long long gmask = (unsigned)q.x | ((unsigned long long)(unsigned)q.y << 32);
+  if (!((gmask >> sl) & 1)) return;
+  const int tpi = p.tiles * p.tiles;
+  const unsigned long long *part = p.keys + (size_t)j * tpi * kNS + sl;
+  unsigned long long k = ~0ull;
+  for (int t = 0; t < tpi; ++t) {
+    const unsigned long long v = part[(size_t)t * kNS];
+    k = v < k ? v : k;
+  }
+  GroupCtx g{};
+  g.cqx = (int16_t)(q.z & 0xffff); g.cqy = (int16_t)((unsigned)q.z >> 16);
+  p.out[(size_t)q.w * kNS + sl] = block_result<FFS>(g, k != ~0ull, (uint32_t)(k & 0xffffffffu), (uint32_t)(k >> 32));
 }
 
 struct Occupancy {
@@ -1658,9 +1709,14 @@ hipError_t launch_search(const KParams &p, hipStream_t s, hipEvent_t ev0, hipEve
 
 hipError_t launch_search_small(const SmallParams &p, hipStream_t s) {
   if (p.n_items <= 0) return hipSuccess;
-  const dim3 grid((unsigned)(p.n_items * p.tiles * p.tiles));
-  if (p.mode == JMME_FAST_FULL_SEARCH) hipLaunchKernelGGL(me_small_kernel<true>, grid, dim3(kWG), 0, s, p);
-  else hipLaunchKernelGGL(me_small_kernel<false>, grid, dim3(kWG), 0, s, p);
+  const dim3 grid((unsigned)(p.n_items * p.tiles * p.tiles)), g2((unsigned)((p.n_items * kNS + kWG - 1) / kWG));
+  if (p.mode == JMME_FAST_FULL_SEARCH) {
+    hipLaunchKernelGGL(me_small_kernel<true>, grid, dim3(kWG), 0, s, p);
+    hipLaunchKernelGGL(small_finish_kernel<true>, g2, dim3(kWG), 0, s, p);
+  } else {
+    hipLaunchKernelGGL(me_small_kernel<false>, grid, dim3(kWG), 0, s, p);
+    hipLaunchKernelGGL(small_finish_kernel<false>, g2, dim3(kWG), 0, s, p);
+  }
   return hipGetLastError();
 }
 

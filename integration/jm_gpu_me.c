@@ -218,7 +218,7 @@ static int g_req_cap = 0;
 /* where a frame's batches come from and what they cost (reported at exit):
  * misses past the batch's end vs inside it (a guess failed), per slot */
 static long long g_miss_past = 0, g_miss_guess = 0, g_miss_slot[JMME_NSLOT], g_units = 0;
-static double g_t_build = 0, g_t_call = 0;
+static double g_t_build = 0, g_t_call = 0, g_t_wrap = 0;
 static FILE *g_trace = NULL;
 
 static double now_us(void)
@@ -430,6 +430,7 @@ distblk __wrap_full_search_motion_estimation(Macroblock *currMB, MotionVector *p
   jmme_mv pred = {pred_mv->mv_x, pred_mv->mv_y};
   jmme_mv mv = {mv_block->mv[list].mv_x, mv_block->mv[list].mv_y};   /* centre in */
   distblk cost;
+  const double t_in = g_trace ? now_us() : 0;
   if (fs_on_cpu(mv_block)) {
     ++g_cpu_calls;
     return __real_full_search_motion_estimation(currMB, pred_mv, mv_block, min_mcost, lambda_factor);
@@ -444,6 +445,7 @@ distblk __wrap_full_search_motion_estimation(Macroblock *currMB, MotionVector *p
     want.sr = (int16_t)search_range; want.chk = (int16_t)check_for_00; want.lambda = lambda_factor;
     e = spec_lookup(currMB, mv_block, list, ref, &want, chk_rule);
     cost = e->cost;
+    if (g_trace) g_t_wrap += now_us() - t_in;
     if (cost >= min_mcost) return min_mcost;
     mv_block->mv[list].mv_x = e->mvx;
     mv_block->mv[list].mv_y = e->mvy;
@@ -739,6 +741,7 @@ static void report(void)
       fprintf(stderr, "jm_gpu_me: integer batches: %lld past the batch, %lld failed guesses; %lld units; "
                       "%.1f ms building, %.1f ms in jmme_search_mbs; failed guesses by slot:",
               g_miss_past, g_miss_guess, g_units, g_t_build * 1e-3, g_t_call * 1e-3);
+      if (g_trace) fprintf(stderr, " [%.1f ms inside the FS wrapper]", g_t_wrap * 1e-3);
       for (s = 0; s < JMME_NSLOT; s++) fprintf(stderr, " %lld", g_miss_slot[s]);
       fprintf(stderr, "\n");
     }

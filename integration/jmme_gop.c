@@ -1,0 +1,224 @@
+/*
+ * jmme_gop.c -- closed-GOP multi-GPU launcher for the drop-in encoder
+ * (JM's motion estimation is sequential inside a GOP --
+ * frame t searches the reconstruction of t-1, store_picture_in_dpb,
+ * JM/lencod/src/mbuffer.c:1905 -- so N GPUs encode N closed GOPs at once).
+ *
+ * The sequence [0, frames) is cut into GOPs of `gop` frames.  GOP k is encoded
+ * by a fresh encoder process (lencod_jmme, or the stock lencod for a CPU
+ * rehearsal) started with JM's own keys
+ *     -p StartFrame=k*gop -p FramesToBeEncoded=<gop or the rest>
+ *     -p OutputFile=<prefix>_gopK.264 -p ReconFile=<prefix>_gopK_rec.yuv
+ * (StartFrame / FramesToBeEncoded: JM/lencod/inc/configfile.h:39,47), so each
+ * GOP starts with an IDR picture and references nothing outside itself.  Its
+ * GPU is chosen in the child's environment (HIP_VISIBLE_DEVICES) between fork
+ * and exec -- this process never touches the GPU.  Up to `per_gpu` children
+ * run on each GPU; a GPU whose child exits takes the next GOP.
+ *
+ * The GOP reconstructions, concatenated in order, equal the reconstruction of
+ * one encoder run over the whole sequence with IntraPeriod = IDRPeriod = gop
+ * (tests/test_gop_launch.py checks this on the CPU with the stock encoder and
+ * on the GPU with lencod_jmme); the bitstreams differ only in their headers
+ * (each GOP carries its own parameter sets and idr_pic_id).
+ *
+ * Usage:
+ *   jmme_gop --encoder PATH --gpus N [--per-gpu K] --gop G --frames F
+ *            --prefix OUTPREFIX [--concat] -- <encoder arguments>
+ * Prints one JSON line: GOPs, their GPU, wall time and JM's "Total ME time".
+ */
+#define _GNU_SOURCE
+#include <errno.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/time.h>
+#include <sys/types.h>
+#include <sys/wait.h>
+#include <unistd.h>
+
+typedef struct gop_run {
+  int gop, gpu, first, count;
+  pid_t pid;
+  double t0, t1, me_s;
+  int status;
+} gop_run;
+
+static double now_s(void)
+{
+  struct timeval tv;
+  gettimeofday(&tv, NULL);
+  return tv.tv_sec + tv.tv_usec * 1e-6;
+}
+
+static void die(const char *msg)
+{
+  fprintf(stderr, "jmme_gop: %s\n", msg);
+  exit(2);
+}
+
+static const char *g_encoder, *g_prefix;
+static char **g_enc_args;
+static int g_n_enc_args;
+
+static void gop_path(char *buf, size_t n, int gop, const char *suffix)
+{
+  snprintf(buf, n, "%s_gop%03d%s", g_prefix, gop, suffix);
+}
+
+/* fork + exec one GOP's encoder on `gpu`; the child's stdout goes to its log */
+static pid_t start_gop(gop_run *r)
+{
+  char start[64], count[64], out[4096], rec[4096], log[4096], dev[32];
+  char outp[4200], recp[4200];
+  pid_t pid;
+  int i, k = 0;
+  char **argv = (char **)calloc((size_t)g_n_enc_args + 16, sizeof(char *));
+  if (!argv) die("out of memory");
+  snprintf(start, sizeof start, "StartFrame=%d", r->first);
+  snprintf(count, sizeof count, "FramesToBeEncoded=%d", r->count);
+  gop_path(out, sizeof out, r->gop, ".264");
+  gop_path(rec, sizeof rec, r->gop, "_rec.yuv");
+  gop_path(log, sizeof log, r->gop, ".log");
+  snprintf(outp, sizeof outp, "OutputFile=%s", out);
+  snprintf(recp, sizeof recp, "ReconFile=%s", rec);
+  snprintf(dev, sizeof dev, "%d", r->gpu);
+  argv[k++] = (char *)g_encoder;
+  for (i = 0; i < g_n_enc_args; i++) argv[k++] = g_enc_args[i];
+  argv[k++] = "-p"; argv[k++] = start;
+  argv[k++] = "-p"; argv[k++] = count;
+  argv[k++] = "-p"; argv[k++] = outp;
+  argv[k++] = "-p"; argv[k++] = recp;
+  argv[k] = NULL;
+  pid = fork();
+  if (pid < 0) die("fork failed");
+  if (pid == 0) {
+    FILE *f = freopen(log, "w", stdout);
+    if (!f) _exit(127);
+    /* the device is fixed before the encoder (and the HIP runtime in it) starts */
+    setenv("HIP_VISIBLE_DEVICES", dev, 1);
+    execv(g_encoder, argv);
+    fprintf(stderr, "jmme_gop: exec %s: %s\n", g_encoder, strerror(errno));
+    _exit(127);
+  }
+  free(argv);
+  r->pid = pid;
+  r->t0 = now_s();
+  return pid;
+}
+
+/* JM's own "Total ME time for sequence : x sec" (report.c:803) from the GOP's log */
+static double me_time(int gop)
+{
+  char path[4096], line[512];
+  double v = -1;
+  FILE *f;
+  gop_path(path, sizeof path, gop, ".log");
+  f = fopen(path, "r");
+  if (!f) return -1;
+  while (fgets(line, sizeof line, f)) {
+    const char *p = strstr(line, "Total ME time for sequence");
+    if (p && (p = strchr(p, ':'))) v = atof(p + 1);
+  }
+  fclose(f);
+  return v;
+}
+
+static int append_file(FILE *dst, const char *src)
+{
+  char buf[1 << 16];
+  size_t n;
+  FILE *f = fopen(src, "rb");
+  if (!f) return -1;
+  while ((n = fread(buf, 1, sizeof buf, f)) > 0)
+    if (fwrite(buf, 1, n, dst) != n) { fclose(f); return -1; }
+  fclose(f);
+  return 0;
+}
+
+int main(int argc, char **argv)
+{
+  int gpus = 1, per_gpu = 1, gop = 0, frames = 0, concat = 0, i, n_gops, next = 0, done = 0, failed = 0;
+  int *busy;
+  gop_run *runs;
+  double t_start;
+  for (i = 1; i < argc; i++) {
+    if (!strcmp(argv[i], "--")) { i++; break; }
+    if (!strcmp(argv[i], "--concat")) { concat = 1; continue; }
+    if (i + 1 >= argc) die("missing value");
+    if (!strcmp(argv[i], "--encoder")) g_encoder = argv[++i];
+    else if (!strcmp(argv[i], "--gpus")) gpus = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "--per-gpu")) per_gpu = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "--gop")) gop = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "--frames")) frames = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "--prefix")) g_prefix = argv[++i];
+    else die("unknown option (see the usage in jmme_gop.c)");
+  }
+  if (!g_encoder || !g_prefix || gpus < 1 || per_gpu < 1 || gop < 1 || frames < 1)
+    die("need --encoder, --prefix, --gpus >= 1, --gop >= 1, --frames >= 1");
+  g_enc_args = argv + i;
+  g_n_enc_args = argc - i;
+  n_gops = (frames + gop - 1) / gop;
+  runs = (gop_run *)calloc((size_t)n_gops, sizeof(gop_run));
+  busy = (int *)calloc((size_t)gpus, sizeof(int));
+  if (!runs || !busy) die("out of memory");
+  for (i = 0; i < n_gops; i++) {
+    runs[i].gop = i;
+    runs[i].first = i * gop;
+    runs[i].count = frames - i * gop < gop ? frames - i * gop : gop;
+    runs[i].gpu = -1;
+  }
+  t_start = now_s();
+  while (done < n_gops) {
+    /* fill every free slot, GPU by GPU */
+    int g;
+    for (g = 0; g < gpus && next < n_gops; g++)
+      while (busy[g] < per_gpu && next < n_gops) {
+        runs[next].gpu = g;
+        start_gop(&runs[next]);
+        busy[g]++;
+        next++;
+      }
+    {
+      int st = 0;
+      pid_t pid = wait(&st);
+      if (pid < 0) die("wait failed");
+      for (i = 0; i < n_gops; i++)
+        if (runs[i].pid == pid && runs[i].t1 == 0) {
+          runs[i].t1 = now_s();
+          runs[i].status = WIFEXITED(st) ? WEXITSTATUS(st) : 128 + (WIFSIGNALED(st) ? WTERMSIG(st) : 0);
+          runs[i].me_s = me_time(i);
+          busy[runs[i].gpu]--;
+          if (runs[i].status) failed++;
+          done++;
+          break;
+        }
+    }
+  }
+  if (concat && !failed) {
+    char path[4096], src[4096];
+    FILE *fo, *fr;
+    snprintf(path, sizeof path, "%s.264", g_prefix);
+    fo = fopen(path, "wb");
+    snprintf(path, sizeof path, "%s_rec.yuv", g_prefix);
+    fr = fopen(path, "wb");
+    if (!fo || !fr) die("cannot write the concatenated outputs");
+    for (i = 0; i < n_gops; i++) {
+      gop_path(src, sizeof src, i, ".264");
+      if (append_file(fo, src)) die("cannot read a GOP bitstream");
+      gop_path(src, sizeof src, i, "_rec.yuv");
+      if (append_file(fr, src)) die("cannot read a GOP reconstruction");
+    }
+    fclose(fo);
+    fclose(fr);
+  }
+  printf("{\"gops\": %d, \"gop\": %d, \"frames\": %d, \"gpus\": %d, \"per_gpu\": %d, \"wall_s\": %.3f, \"failed\": %d, "
+         "\"runs\": [", n_gops, gop, frames, gpus, per_gpu, now_s() - t_start, failed);
+  for (i = 0; i < n_gops; i++)
+    printf("%s{\"gop\": %d, \"gpu\": %d, \"first\": %d, \"frames\": %d, \"wall_s\": %.3f, \"me_s\": %.3f, "
+           "\"status\": %d}", i ? ", " : "", i, runs[i].gpu, runs[i].first, runs[i].count, runs[i].t1 - runs[i].t0,
+           runs[i].me_s, runs[i].status);
+  printf("]}\n");
+  free(runs);
+  free(busy);
+  return failed ? 1 : 0;
+}

@@ -1,0 +1,81 @@
+"""Closed-GOP sharding of the encoder (integration/jmme_gop.c, SURVEY §8(e)
+row 1): a sequence cut into GOPs, one fresh encoder process per GOP, its GPU
+fixed in the child's environment before it starts.  The concatenated GOP
+reconstructions must equal one encoder run over the whole sequence with
+IntraPeriod = IDRPeriod = the GOP length (JM/lencod/inc/configfile.h:39-47).
+
+CPU rehearsal: the stock JM 18.5 lencod (oracle/_ref/lencod) under the
+launcher with 2 "GPUs" (concurrent processes).  GPU: lencod_jmme under the
+launcher (2 encoders sharing the box's GPU) against the stock single run."""
+import hashlib
+import json
+import os
+import subprocess
+import tempfile
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+STOCK = os.path.join(REPO, "oracle", "_ref", "lencod")
+GPU_ENC = os.path.join(REPO, "integration", "_build", "lencod_jmme")
+LAUNCHER = os.path.join(REPO, "integration", "_build", "jmme_gop")
+W, H, FRAMES, GOP = 352, 288, 7, 3
+
+
+def _clip(d):
+    from jmme import synth
+    from test_jm_dropin_gpu import CFG
+    yuv = os.path.join(d, "in.yuv")
+    synth.write_yuv420(yuv, synth.luma_sequence(W, H, FRAMES, seed=21, gmv=(3, -1)))
+    cfg = os.path.join(d, "enc.cfg")
+    open(cfg, "w").write(CFG)
+    return ["-d", cfg, "-p", f"InputFile={yuv}", "-p", f"SourceWidth={W}", "-p", f"SourceHeight={H}",
+            "-p", f"OutputWidth={W}", "-p", f"OutputHeight={H}", "-p", "SearchMode=-1", "-p", "SearchRange=16",
+            "-p", "NumberReferenceFrames=2", "-p", "RDOptimization=0"]
+
+
+def _md5(p):
+    return hashlib.md5(open(p, "rb").read()).hexdigest()
+
+
+def _single(d, args):
+    rec = os.path.join(d, "single_rec.yuv")
+    r = subprocess.run([STOCK] + args + ["-p", f"FramesToBeEncoded={FRAMES}", "-p", f"IntraPeriod={GOP}",
+                                         "-p", f"IDRPeriod={GOP}", "-p", f"OutputFile={os.path.join(d, 'single.264')}",
+                                         "-p", f"ReconFile={rec}"], cwd=d, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-1000:]
+    return rec
+
+
+def _sharded(d, encoder, gpus, per_gpu):
+    prefix = os.path.join(d, "shard")
+    r = subprocess.run([LAUNCHER, "--encoder", encoder, "--gpus", str(gpus), "--per-gpu", str(per_gpu), "--gop",
+                        str(GOP), "--frames", str(FRAMES), "--prefix", prefix, "--concat", "--"] + _clip(d),
+                       cwd=d, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, (r.stdout[-1500:], r.stderr[-1500:])
+    return json.loads(r.stdout.strip().splitlines()[-1]), prefix + "_rec.yuv"
+
+
+@pytest.mark.skipif(not (os.path.exists(STOCK) and os.path.exists(LAUNCHER)), reason="JM build / launcher absent")
+def test_gop_launcher_cpu_rehearsal():
+    with tempfile.TemporaryDirectory() as d:
+        rep, rec = _sharded(d, STOCK, gpus=2, per_gpu=1)
+        want = _single(d, _clip(d))
+        assert rep["gops"] == 3 and rep["failed"] == 0
+        assert [r["frames"] for r in rep["runs"]] == [3, 3, 1]
+        assert sorted({r["gpu"] for r in rep["runs"]}) == [0, 1]
+        assert all(r["me_s"] >= 0 for r in rep["runs"])
+        assert _md5(rec) == _md5(want)
+
+
+@pytest.mark.gpu
+def test_gop_launcher_gpu_dropin_matches_single_cpu_run(gpu):
+    """lencod_jmme per GOP (two encoders sharing the one GPU) == stock single run."""
+    with tempfile.TemporaryDirectory() as d:
+        rep, rec = _sharded(d, GPU_ENC, gpus=1, per_gpu=2)
+        want = _single(d, _clip(d))
+        assert rep["failed"] == 0
+        assert _md5(rec) == _md5(want)
+        for r in rep["runs"]:
+            log = open(os.path.join(d, f"shard_gop{r['gop']:03d}.log")).read()
+            assert "Total ME time" in log

@@ -1,9 +1,9 @@
 #!/bin/bash
 # rocprofv3 kernel + runtime trace of the drop-in encoder itself (1080p, 2 frames,
-# sub-pel on): where a speculative batch's time goes.  GPU box.
+# sub-pel on unless SUBPEL=0): where a speculative batch's time goes.  GPU box.
 set -e
 cd "$(dirname "$0")/.."
-out=gpurun_out/prof_dropin
+out=gpurun_out/${OUT:-prof_dropin}
 mkdir -p $out
 export TMPDIR=/tmp
 d=$(mktemp -d)
@@ -18,8 +18,8 @@ open(os.path.join(d, "enc.cfg"), "w").write(CFG)
 PY
 args="-d $d/enc.cfg -p InputFile=$d/in.yuv -p SourceWidth=1920 -p SourceHeight=1080 -p OutputWidth=1920
  -p OutputHeight=1080 -p FramesToBeEncoded=2 -p OutputFile=$d/o.264 -p ReconFile=$d/r.yuv -p SearchMode=${MODE:--1}
- -p SearchRange=32 -p RDOptimization=0 -p NumberReferenceFrames=1 -p DisableSubpelME=0 -p MEDistortionQPel=2
- -p MDDistortion=2"
-timeout -k 10 300 rocprofv3 --kernel-trace --runtime-trace --stats -d $out -o run -- \
+ -p SearchRange=32 -p RDOptimization=0 -p NumberReferenceFrames=1"
+if [ "${SUBPEL:-1}" = 1 ]; then args="$args -p DisableSubpelME=0 -p MEDistortionQPel=2 -p MDDistortion=2"; fi
+timeout -k 10 300 rocprofv3 --kernel-trace --runtime-trace --stats --output-format csv -d $out -o run -- \
   "$PWD/integration/_build/lencod_jmme" $args > $out/lencod.log 2>&1
 find $out -name "*stats.csv" | head
