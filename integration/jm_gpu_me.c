@@ -430,11 +430,12 @@ distblk __wrap_full_search_motion_estimation(Macroblock *currMB, MotionVector *p
   jmme_mv pred = {pred_mv->mv_x, pred_mv->mv_y};
   jmme_mv mv = {mv_block->mv[list].mv_x, mv_block->mv[list].mv_y};   /* centre in */
   distblk cost;
-  const double t_in = g_trace ? now_us() : 0;
+  double t_in;
   if (fs_on_cpu(mv_block)) {
     ++g_cpu_calls;
     return __real_full_search_motion_estimation(currMB, pred_mv, mv_block, min_mcost, lambda_factor);
   }
+  t_in = (speculating() && g_trace) ? now_us() : 0;
   ensure_planes(currMB, list, ref);
   ++g_calls;
   if (speculating()) {
