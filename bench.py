@@ -244,16 +244,20 @@ def subpel_block(dev, local: int, iters: int = 20) -> dict | None:
 
 
 UHD_CASE = "c2_syn_4k_fs32"
+ADV_CASE = "c2_syn_1080p_adv_fs32"
 
 
-def uhd_block(dev, local: int, iters: int = 10) -> dict | None:
-    """The same full search at 4K (3840x2160: 32,400 MB x ref per P-frame), measured
-    on rank 0 with JM 18.5's own requests for a seeded 4K clip, parity vs JM."""
+def case_block(dev, local: int, case: str, workload: str, iters: int = 10) -> dict | None:
+    """The same full search on another captured frame, measured on rank 0 with
+    JM 18.5's own requests for it, parity vs JM: the 4K frame (3840x2160, 32,400
+    MB x ref) and the adversarial 1080p frame (every macroblock moved by its own
+    random vector: the window centre is no good bound, so the exact elimination
+    prunes little -- SURVEY §8(d)'s adversarial variant)."""
     import golden_io as g
     from jmme import BLOCK_RES, FULL_SEARCH, MotionEstimator, NSLOT
-    if UHD_CASE not in g.manifest():
+    if case not in g.manifest():
         return None
-    cur, ref, req, unit_of, slots, expect, meta = load_workload(UHD_CASE)
+    cur, ref, req, unit_of, slots, expect, meta = load_workload(case)
     n = len(req)
     me = MotionEstimator({"SearchRange": 32, "SearchMode": -1, "RDOptimization": 0}, device=local)
     me.upload_cur(cur)
@@ -276,14 +280,23 @@ def uhd_block(dev, local: int, iters: int = 10) -> dict | None:
     exact = int(np.sum((out["mv_x"] == expect[0]) & (out["mv_y"] == expect[1]) & (out["cost"] == expect[2])))
     me.close()
     kernel_ms = float(np.mean(kms))
-    return {"workload": "4K (3840x2160) FS +-32 SAD integer-pel, 1 ref, 32,400 MB x ref per frame, "
-                        "JM 18.5's own requests", "mb_per_step": n, "ms_per_frame": round(ms, 4),
+    return {"workload": workload, "mb_per_step": n, "ms_per_frame": round(ms, 4),
             "kernel_ms": round(kernel_ms, 4), "mb_per_s": round(n / (ms * 1e-3), 1),
             "valu_frac": round(ABSDIFF_PER_UNIT * n / (kernel_ms * 1e-3) / VSAD_PEAK, 4),
             "hbm_frac": round(ALG_BYTES_PER_UNIT * n / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6),
             "parity": {"reference": "JM 18.5 lencod (captured)", "searches": int(len(expect[0])),
                        "bit_exact": exact},
             "jm_me_time_at_capture": meta.get("jm_me_time")}
+
+
+def uhd_block(dev, local: int, iters: int = 10) -> dict | None:
+    return case_block(dev, local, UHD_CASE, "4K (3840x2160) FS +-32 SAD integer-pel, 1 ref, 32,400 MB x ref per "
+                                            "frame, JM 18.5's own requests", iters)
+
+
+def adversarial_block(dev, local: int, iters: int = 10) -> dict | None:
+    return case_block(dev, local, ADV_CASE, "1080p FS +-32, adversarial content (per-MB random motion, no global "
+                                            "motion), 8160 MB x ref, JM 18.5's own requests", iters)
 
 
 def reduce_over_ranks(wall: float, exact: int, ws: int, dev) -> tuple[float, int]:
@@ -379,6 +392,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-subpel", action="store_true")
     ap.add_argument("--no-uhd", action="store_true")
+    ap.add_argument("--no-adversarial", action="store_true")
     ap.add_argument("--no-fractal", action="store_true", help="skip the configs[2] block (fractal full pool)")
     ap.add_argument("--no-hybrid", action="store_true", help="skip the configs[4] block (joint codec frame)")
     ap.add_argument("--no-dropin", action="store_true", help="skip the in-encoder block (lencod vs lencod_jmme)")
@@ -494,6 +508,8 @@ def main():
             line["subpel"] = subpel_block(dev, local)
         if not args.no_uhd and ws == 1:
             line["uhd"] = uhd_block(dev, local)
+        if not args.no_adversarial and ws == 1:
+            line["adversarial"] = adversarial_block(dev, local)
         if not args.no_fractal and ws == 1:
             import bench_blocks
             line["fractal"] = bench_blocks.fractal_block(dev, local)

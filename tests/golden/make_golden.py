@@ -73,6 +73,13 @@ CASES = {
                               p={"SearchMode": -1, "SearchRange": 32, "NumberReferenceFrames": 1,
                                  "RDOptimization": 0, "MDDistortion": 0, **INT_PEL},
                               keep="compact"),
+    # the headline configuration on adversarial content: every 16x16 macroblock of the
+    # P-frame moves by its own random vector within +-32 (no global motion for the
+    # window centre to ride on; the GPU's exact elimination prunes little)
+    "c2_syn_1080p_adv_fs32": dict(src="synth", w=1920, h=1080, frames=2, seed=2025, gmv=(0, 0), adversarial=True,
+                                  p={"SearchMode": -1, "SearchRange": 32, "NumberReferenceFrames": 1,
+                                     "RDOptimization": 0, "MDDistortion": 0, **INT_PEL},
+                                  keep="compact"),
     # the same configuration at 4K (3840x2160, 32,400 MB x ref per P-frame): the bench's UHD block
     "c2_syn_4k_fs32": dict(src="synth", w=3840, h=2160, frames=2, seed=4096, gmv=(5, 3),
                            p={"LevelIDC": 51, "SearchMode": -1, "SearchRange": 32, "NumberReferenceFrames": 1,
