@@ -715,9 +715,23 @@ __device__ __forceinline__ void sweep_v5(const Lds &L, const uint32_t (&cs)[64],
   // tid / D by a multiply: exact for tid * D < 2^16 (tid < 256, D <= 89)
   const unsigned dm = (65536u + (unsigned)D - 1u) / (unsigned)D;
   int tq = (int)(((unsigned)tid * dm) >> 16), tx = tid - tq * D;   // task column, task row
+  // Windows of at least 64 columns: lane l takes column l of whole task rows
+  // (a wave streams one row of tasks; task row = wave + 4k), so the 64 lanes
+  // of an LDS read hit 64 consecutive words -- no bank conflicts.  Dealing
+  // tasks in raster order instead wraps a wave across two task rows (P rows x
+  // pitch apart), which put two lanes on one bank in most reads.  The columns
+  // past 63 follow as extra tasks after the 64 * DT row tasks.
+  const bool rows64 = D >= 64;
+  const int nrow64 = 64 * DT;
+  if (rows64) { tq = tid >> 6; tx = tid & 63; }
   const int wp = WP ? WP : L.wp;
   const uint32_t tb = lds_addr(L.tmax) + 32u * (uint32_t)ufl(tid >> 6);   // this wave's elimination bounds
   for (int t = tid; t < ntask; t += kWG) {
+    if (rows64 && t >= nrow64) {                       // a column past 63
+      const int e = t - nrow64;
+      tq = e / (D - 64);
+      tx = 64 + e - tq * (D - 64);
+    }
     const int y0 = min(P * tq, D - P);
     uint32_t K[P];
     {
@@ -812,9 +826,13 @@ __device__ __forceinline__ void sweep_v5(const Lds &L, const uint32_t (&cs)[64],
     }
     }
 #endif
-    tx += rstep;
-    tq += qstep;
-    if (tx >= D) { tx -= D; ++tq; }
+    if (rows64) {
+      tq += kWaves;
+    } else {
+      tx += rstep;
+      tq += qstep;
+      if (tx >= D) { tx -= D; ++tq; }
+    }
   }
 }
 

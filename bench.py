@@ -396,10 +396,15 @@ def main():
     ap.add_argument("--no-fractal", action="store_true", help="skip the configs[2] block (fractal full pool)")
     ap.add_argument("--no-hybrid", action="store_true", help="skip the configs[4] block (joint codec frame)")
     ap.add_argument("--no-dropin", action="store_true", help="skip the in-encoder block (lencod vs lencod_jmme)")
+    ap.add_argument("--headline-only", action="store_true", help="the headline line alone (no CPU baseline, no "
+                                                                  "side blocks): profiling runs")
     ap.add_argument("--shard", choices=["gop", "band"], default="gop",
                     help="gop: each rank searches its own frames (weak, default); band: rank 0 broadcasts "
                          "each frame's planes over RCCL and every rank searches an MB-row band (strong)")
     args = ap.parse_args()
+    if args.headline_only:
+        for k in ("no_cpu_baseline", "no_subpel", "no_uhd", "no_adversarial", "no_fractal", "no_hybrid", "no_dropin"):
+            setattr(args, k, True)
 
     ws, rank, local = dist_env()
     if ws > 1:

@@ -15,6 +15,6 @@ G[tcc1]="FETCH_SIZE"
 G[tcc2]="WRITE_SIZE"
 for g in $GROUPS_; do
   timeout -k 10 240 rocprofv3 --kernel-trace --pmc ${G[$g]} --output-format csv -d "$OUT/$g" -o p -- \
-    python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-subpel --no-uhd > "$OUT/$g.log" 2>&1
+    python3 bench.py --steps 5 --warmup 1 --headline-only > "$OUT/$g.log" 2>&1
 done
 echo pmc done
