@@ -101,6 +101,8 @@ struct jmme_ctx {
   size_t cap_sitems = 0;
   jmme_block_res *h_sout = nullptr;
   size_t cap_sout = 0;
+  uint8_t *h_emap = nullptr;                 // jmme_epzs_search_ex: mapped pinned request / result block
+  size_t cap_emap = 0;
   unsigned long long *d_skeys = nullptr;     // per (item, tile) keys, cap_skeys * JMME_NSLOT
   size_t cap_skeys = 0;
 };
@@ -299,6 +301,7 @@ extern "C" void jmme_destroy(jmme_ctx *ctx) {
   if (ctx->h_pin) (void)hipHostFree(ctx->h_pin);
   if (ctx->h_sitems) (void)hipHostFree(ctx->h_sitems);
   if (ctx->h_sout) (void)hipHostFree(ctx->h_sout);
+  if (ctx->h_emap) (void)hipHostFree(ctx->h_emap);
   (void)hipFree(ctx->d_skeys);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
@@ -596,6 +599,7 @@ int search_small(jmme_ctx *ctx, int mode, const jmme_mb_req *req, int n, jmme_bl
   }
   if ((size_t)n * JMME_NSLOT > ctx->cap_sout) {
     if (ctx->h_sout) (void)hipHostFree(ctx->h_sout);
+  if (ctx->h_emap) (void)hipHostFree(ctx->h_emap);
     ctx->h_sout = nullptr;
     ctx->cap_sout = 0;
     const size_t cap = std::max<size_t>(64 * JMME_NSLOT, (size_t)n * JMME_NSLOT);
@@ -1027,21 +1031,15 @@ extern "C" int jmme_fractal_box_sums(jmme_ctx *ctx, const uint8_t *plane, int pi
 }
 
 // -------------------------------------------------------------------- EPZS --
-static_assert(sizeof(jmme_epzs_req) == 80 && sizeof(jmme_epzs_res) == 24, "EPZS ABI layout");
+static_assert(sizeof(jmme_epzs_req) == 80 && sizeof(jmme_epzs_res) == 32, "EPZS ABI layout");
 
 namespace {
 int prepare_subs(jmme_ctx *ctx, hipStream_t s);   // sub-pel section below
 }  // namespace
 
-extern "C" int jmme_epzs_search_async(jmme_ctx *ctx, const jmme_epzs_req *d_req, int n, const int16_t *d_preds,
-                                      const int16_t *d_stale, jmme_epzs_res *d_out, void *stream) {
-  DevGuard dg_(ctx);
-  if (!ctx) return fail("null ctx");
-  if (n < 0) return fail("negative request count");
-  if (n == 0) return 0;
-  if (!ctx->d_cur) return fail("no current frame uploaded");
-  if (!d_req || !d_out || !d_preds || !d_stale) return fail("null array");
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+namespace {
+int launch_epzs_ex(jmme_ctx *ctx, const jmme_epzs_req *d_req, int n, const int16_t *d_preds, const uint8_t *d_cond,
+                   const int16_t *d_stale, jmme_epzs_res *d_out, int16_t *d_vis, int max_visited, hipStream_t s) {
   if (sync_ref_table(ctx, s)) return -1;
   EpzsParams p{};
   p.cur = ctx->d_cur;
@@ -1067,17 +1065,29 @@ extern "C" int jmme_epzs_search_async(jmme_ctx *ctx, const jmme_epzs_req *d_req,
     p.max_qpel = kEpzsMaxQpel;
   }
   p.map_words = (int)epzs_map_words(p.grid, p.max_qpel);
+  p.pred_cond = d_cond;
+  p.visited = d_vis;
+  p.max_visited = max_visited;
   HIPCHK(launch_epzs(p, s));
   return 0;
 }
+}  // namespace
 
-extern "C" int jmme_epzs_search(jmme_ctx *ctx, const jmme_epzs_req *req, int n, const int16_t *preds, int n_preds,
-                                const int16_t *stale, int n_stale, jmme_epzs_res *out) {
+extern "C" int jmme_epzs_search_async(jmme_ctx *ctx, const jmme_epzs_req *d_req, int n, const int16_t *d_preds,
+                                      const int16_t *d_stale, jmme_epzs_res *d_out, void *stream) {
   DevGuard dg_(ctx);
   if (!ctx) return fail("null ctx");
-  if (n <= 0) return n < 0 ? fail("negative request count") : 0;
-  if (!req || !out || (n_preds && !preds) || (n_stale && !stale)) return fail("null array");
+  if (n < 0) return fail("negative request count");
+  if (n == 0) return 0;
   if (!ctx->d_cur) return fail("no current frame uploaded");
+  if (!d_req || !d_out || !d_preds || !d_stale) return fail("null array");
+  return launch_epzs_ex(ctx, d_req, n, d_preds, nullptr, d_stale, d_out, nullptr, 0,
+                        reinterpret_cast<hipStream_t>(stream));
+}
+
+namespace {
+// the checks of the host-array EPZS entry points
+int epzs_validate(const jmme_ctx *ctx, const jmme_epzs_req *req, int n, int n_preds, int n_stale) {
   for (int i = 0; i < n; ++i) {
     const jmme_epzs_req &q = req[i];
     const bool size_ok = (q.bsx == 16 || q.bsx == 8 || q.bsx == 4) && (q.bsy == 16 || q.bsy == 8 || q.bsy == 4) &&
@@ -1108,6 +1118,18 @@ extern "C" int jmme_epzs_search(jmme_ctx *ctx, const jmme_epzs_req *req, int n, 
     if (q.ref_slot < 0 || q.ref_slot >= kMaxLists * kMaxRefs || !ctx->d_refs[q.ref_slot])
       return fail("request %d: reference slot %d not uploaded", i, q.ref_slot);
   }
+  return 0;
+}
+}  // namespace
+
+extern "C" int jmme_epzs_search(jmme_ctx *ctx, const jmme_epzs_req *req, int n, const int16_t *preds, int n_preds,
+                                const int16_t *stale, int n_stale, jmme_epzs_res *out) {
+  DevGuard dg_(ctx);
+  if (!ctx) return fail("null ctx");
+  if (n <= 0) return n < 0 ? fail("negative request count") : 0;
+  if (!req || !out || (n_preds && !preds) || (n_stale && !stale)) return fail("null array");
+  if (!ctx->d_cur) return fail("no current frame uploaded");
+  if (epzs_validate(ctx, req, n, n_preds, n_stale)) return -1;
   DevBuf dq, dp, ds, dout;
   HIPCHK(dq.alloc((size_t)n * sizeof(jmme_epzs_req)));
   HIPCHK(dp.alloc((size_t)(n_preds ? n_preds : 1) * 4));
@@ -1120,6 +1142,69 @@ extern "C" int jmme_epzs_search(jmme_ctx *ctx, const jmme_epzs_req *req, int n, 
                              (jmme_epzs_res *)dout.p, nullptr))
     return -1;
   HIPCHK(hipMemcpy(out, dout.p, (size_t)n * sizeof(jmme_epzs_res), hipMemcpyDeviceToHost));
+  return 0;
+}
+
+extern "C" int jmme_epzs_search_ex(jmme_ctx *ctx, const jmme_epzs_req *req, int n, const int16_t *preds,
+                                   const uint8_t *pred_cond, int n_preds, const int16_t *stale, int n_stale,
+                                   jmme_epzs_res *out, int16_t *visited, int max_visited) {
+  DevGuard dg_(ctx);
+  if (!ctx) return fail("null ctx");
+  if (n <= 0) return n < 0 ? fail("negative request count") : 0;
+  if (!req || !out || (n_preds && !preds) || (n_stale && !stale)) return fail("null array");
+  if (!ctx->d_cur) return fail("no current frame uploaded");
+  if (visited && max_visited <= 0) return fail("max_visited must be positive");
+  if (epzs_validate(ctx, req, n, n_preds, n_stale)) return -1;
+  if (pred_cond)
+    for (int i = 0; i < n_preds; ++i)
+      if (pred_cond[i] > JMME_EPZS_PRED_GT_3STOP) return fail("predictor %d: condition %d", i, pred_cond[i]);
+  // one mapped pinned block: [req | preds | stale | cond | out | visited]
+  const size_t b_req = align64((size_t)n * sizeof(jmme_epzs_req)), b_pred = align64((size_t)n_preds * 4 + 4);
+  const size_t b_stale = align64((size_t)n_stale * 4 + 4), b_cond = align64((size_t)n_preds + 1);
+  const size_t b_out = align64((size_t)n * sizeof(jmme_epzs_res));
+  const size_t b_vis = visited ? align64((size_t)n * max_visited * 4) : 0;
+  const size_t need = b_req + b_pred + b_stale + b_cond + b_out + b_vis;
+  if (need > ctx->cap_emap) {
+    if (ctx->h_emap) (void)hipHostFree(ctx->h_emap);
+    ctx->h_emap = nullptr;
+    ctx->cap_emap = 0;
+    const size_t cap = std::max<size_t>(1u << 20, need + need / 2);
+    HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_emap), cap, hipHostMallocMapped));
+    ctx->cap_emap = cap;
+  }
+  uint8_t *h = ctx->h_emap;
+  void *dh = nullptr;
+  HIPCHK(hipHostGetDevicePointer(&dh, h, 0));
+  uint8_t *d = static_cast<uint8_t *>(dh);
+  size_t o = 0;
+  std::memcpy(h + o, req, (size_t)n * sizeof(jmme_epzs_req));
+  const jmme_epzs_req *d_req = reinterpret_cast<const jmme_epzs_req *>(d + o);
+  o += b_req;
+  if (n_preds) std::memcpy(h + o, preds, (size_t)n_preds * 4);
+  const int16_t *d_preds = reinterpret_cast<const int16_t *>(d + o);
+  o += b_pred;
+  if (n_stale) std::memcpy(h + o, stale, (size_t)n_stale * 4);
+  const int16_t *d_stale = reinterpret_cast<const int16_t *>(d + o);
+  o += b_stale;
+  if (pred_cond && n_preds) std::memcpy(h + o, pred_cond, (size_t)n_preds);
+  const uint8_t *d_cond = pred_cond ? d + o : nullptr;
+  o += b_cond;
+  jmme_epzs_res *h_out = reinterpret_cast<jmme_epzs_res *>(h + o), *d_out = reinterpret_cast<jmme_epzs_res *>(d + o);
+  o += b_out;
+  int16_t *h_vis = visited ? reinterpret_cast<int16_t *>(h + o) : nullptr;
+  int16_t *d_vis = visited ? reinterpret_cast<int16_t *>(d + o) : nullptr;
+  hipStream_t s = nullptr;
+  if (launch_epzs_ex(ctx, d_req, n, d_preds, d_cond, d_stale, d_out, d_vis, max_visited, s)) return -1;
+  HIPCHK(hipStreamSynchronize(s));
+  std::memcpy(out, h_out, (size_t)n * sizeof(jmme_epzs_res));
+  for (int i = 0; i < n; ++i)
+    if (visited && out[i].n_visited > max_visited)
+      return fail("request %d: the search stamped %d map cells, more than max_visited %d", i, out[i].n_visited,
+                  max_visited);
+  if (visited)   // only the pairs each search wrote
+    for (int i = 0; i < n; ++i)
+      std::memcpy(visited + 2 * (size_t)max_visited * i, h_vis + 2 * (size_t)max_visited * i,
+                  (size_t)out[i].n_visited * 4);
   return 0;
 }
 

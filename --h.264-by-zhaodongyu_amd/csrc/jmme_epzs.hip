@@ -290,6 +290,10 @@ __device__ void search_one(const EpzsParams &p, const jmme_epzs_req &q, WaveLds 
     bool check_median = false, done = false;
     int tmp2x = 0, tmp2y = 0;
     stop = q.stop_crit;
+    // the predictor list is JM's as generated with min_mcost = the centre's
+    // cost: conditional entries (temporal neighbours, window, block-type
+    // predictors, me_epzs_common.c:1528, 1654, 1224) join on that value
+    const int64_t gen_min = best;
     if (best < (stop >> 1)) {
       path = 2;
       update = GRID && !variant;   // EPZS_integer_motion_estimation keeps the value (me_epzs_int.c:118-120)
@@ -298,7 +302,12 @@ __device__ void search_one(const EpzsParams &p, const jmme_epzs_req &q, WaveLds 
     // predictors, 64 at a time; JM's order is restored in the fold
     for (int base = 0; !done && base < q.n_pred; base += 64) {
       const int i = base + lane;
-      const bool valid = i < q.n_pred;
+      bool valid = i < q.n_pred;
+      if (valid && p.pred_cond) {
+        const int c = p.pred_cond[q.pred_off + i];
+        valid = c == JMME_EPZS_PRED_ALWAYS || (c == JMME_EPZS_PRED_GT_STOP && gen_min > stop) ||
+                (c == JMME_EPZS_PRED_GT_2STOP && gen_min > 2 * stop) || (c == JMME_EPZS_PRED_GT_3STOP && gen_min > 3 * stop);
+      }
       int mx = 0, my = 0;
       if (valid) {
         mx = p.preds[2 * (q.pred_off + i)];
@@ -465,9 +474,40 @@ __device__ void search_one(const EpzsParams &p, const jmme_epzs_req &q, WaveLds 
     }
   }
   if (update && (refi == 0 || prev > best)) prev = best;
+  const int motx = tmpx, moty = tmpy;   // JM's tmp: what every return path stores to p_motion
   if (path <= 2 || path == 6) {   // returned before touching *mv
     tmpx = s.cx;
     tmpy = s.cy;
+  }
+  // the drop-in keeps JM's never-cleared EPZSMap: every cell this search
+  // stamped (the centre, evaluated predictors and pattern points, and the
+  // cells that already held its BlkCount), as (dx, dy) qpel from the centre
+  int nv = 0;
+  if (p.visited) {
+    int16_t *const vout = p.visited + 2 * (size_t)p.max_visited * (size_t)(out - p.out);
+    const int words = (s.side_x * side_y + 31) >> 5;
+    for (int base = 0; base < words; base += 64) {
+      const int wi = base + lane;
+      uint32_t bits = wi < words ? s.map[wi] : 0u;
+      int cnt = __popc(bits), pre = cnt;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {   // inclusive prefix sum over the wave
+        const int v = __shfl_up(pre, o, 64);
+        if (lane >= o) pre += v;
+      }
+      int at = nv + pre - cnt;
+      while (bits) {
+        const int b = __builtin_ctz(bits);
+        bits &= bits - 1;
+        const int c = wi * 32 + b, cyi = c / s.side_x, cxi = c - cyi * s.side_x;
+        if (at < p.max_visited) {
+          vout[2 * at] = (int16_t)(GRID ? cxi - s.max_x : 4 * cxi - s.max_x);
+          vout[2 * at + 1] = (int16_t)(GRID ? cyi - s.max_y : 4 * cyi - s.max_y);
+        }
+        ++at;
+      }
+      nv += __shfl(pre, 63, 64);
+    }
   }
   if (lane == 0) {
     jmme_epzs_res r;
@@ -476,6 +516,9 @@ __device__ void search_one(const EpzsParams &p, const jmme_epzs_req &q, WaveLds 
     r.path = path;
     r.cost = best;
     r.prev_sad = prev;
+    r.motion_x = (int16_t)motx;
+    r.motion_y = (int16_t)moty;
+    r.n_visited = nv;
     *out = r;
   }
   wave_sync();

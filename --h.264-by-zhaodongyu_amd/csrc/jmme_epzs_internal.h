@@ -24,6 +24,12 @@ struct EpzsParams {
   size_t plane_stride;
   int max_qpel;                        // largest searchRange.max_x / max_y the map is sized for
   int map_words;                       // epzs_map_words(grid, max_qpel)
+  // drop-in extras (jmme_epzs_search_ex): predictor conditions parallel to
+  // preds (JMME_EPZS_PRED_*; null: all unconditional) and the visited cells of
+  // each search, (dx, dy) qpel from the centre, max_visited per search (null: not written)
+  const uint8_t *pred_cond;
+  int16_t *visited;
+  int max_visited;
 };
 
 size_t epzs_map_words(bool grid, int max_qpel);

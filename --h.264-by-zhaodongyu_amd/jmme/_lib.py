@@ -42,7 +42,8 @@ EPZS_REQ = np.dtype([("pos_x", "<i2"), ("pos_y", "<i2"), ("bsx", "<i2"), ("bsy",
                      ("n_pred", "<i4"), ("pred_off", "<i4"), ("n_stale", "<i4"), ("stale_off", "<i4"),
                      ("ref_slot", "<i4"), ("reserved", "<i4"),
                      ("prev_sad", "<i8"), ("medthres", "<i8"), ("stop_crit", "<i8")])
-EPZS_RES = np.dtype([("mv_x", "<i2"), ("mv_y", "<i2"), ("path", "<i4"), ("cost", "<i8"), ("prev_sad", "<i8")])
+EPZS_RES = np.dtype([("mv_x", "<i2"), ("mv_y", "<i2"), ("path", "<i4"), ("cost", "<i8"), ("prev_sad", "<i8"),
+                     ("motion_x", "<i2"), ("motion_y", "<i2"), ("n_visited", "<i4")])
 EPZS_FRAME, EPZS_PSLICE = 1, 2
 SUBPEL_REQ = np.dtype([("pos_x", "<i2"), ("pos_y", "<i2"), ("blocktype", "<i2"), ("ref_slot", "<i2"),
                        ("pred_x", "<i2"), ("pred_y", "<i2"), ("mv_x", "<i2"), ("mv_y", "<i2"),
@@ -60,7 +61,7 @@ TRANSFORM_OPS = {"forward4x4": (0, 16, 16), "inverse4x4": (1, 16, 16), "hadamard
 assert BLOCK_REQ.itemsize == 16 and MB_REQ.itemsize == 688 and BLOCK_RES.itemsize == 16
 assert QUANT4x4_PARAMS.itemsize == 248 and FRACTAL_REQ.itemsize == 8 and FRACTAL_RES.itemsize == 32
 assert FRACTAL_NODE.itemsize == 40 and FRACTAL_MB.itemsize == 848
-assert EPZS_REQ.itemsize == 80 and EPZS_RES.itemsize == 24 and SUBPEL_REQ.itemsize == 48
+assert EPZS_REQ.itemsize == 80 and EPZS_RES.itemsize == 32 and SUBPEL_REQ.itemsize == 48
 
 CONFIG_FIELDS = ["SourceWidth", "SourceHeight", "SearchMode", "SearchRange", "NumberReferenceFrames",
                  "DisableSubpelME", "RDOptimization", "MEDistortionFPel", "MDDistortion", "EPZSSubPelGrid",
@@ -129,6 +130,7 @@ def lib() -> ctypes.CDLL:
         "jmme_fractal_encode_mbs": (I, [P, P, P, I, I, I, I, I, D, D, P]),
         "jmme_epzs_search": (I, [P, P, I, P, I, P, I, P]),
         "jmme_epzs_search_async": (I, [P, P, I, P, P, P, P]),
+        "jmme_epzs_search_ex": (I, [P, P, I, P, P, I, P, I, P, P, I]),
         "jmme_fractal_encode_mbs_async": (I, [P, P, P, I, P, I, I, I, I, D, D, P, P]),
         "jmme_fractal_encode_mb_rows_async": (I, [P, P, P, I, P, I, I, I, I, I, I, D, D, P, P]),
         "jmme_fractal_decode_mbs": (I, [P, P, P, I, I, I, I, I, P]),

@@ -296,7 +296,21 @@ typedef struct jmme_epzs_res {
   int32_t path;                /* 1..7: which return of the JM function was taken (-1: refused) */
   int64_t cost;                /* return value (min_mcost) */
   int64_t prev_sad;            /* *prevSad on return */
-} jmme_epzs_res;               /* 24 bytes */
+  int16_t motion_x, motion_y;  /* JM's tmp at return: what EPZSSpatialMem stores to p_motion */
+  int32_t n_visited;           /* EPZSMap cells the search stamped (jmme_epzs_search_ex) */
+} jmme_epzs_res;               /* 32 bytes */
+
+/* Predictor conditions (jmme_epzs_search_ex's pred_cond, one per predictor):
+ * JM generates part of the list only when the centre's cost min_mcost passes a
+ * bound on the stop criterion (me_epzs.c:170-212, me_epzs_int.c:163-212):
+ * temporal neighbours (min_mcost > stop, EPZS_temporal_predictors), window
+ * predictors (> 3 stop), block-type predictors for ref > 0 (> 2 stop).  The
+ * caller generates the whole list with JM's own routines; the search keeps the
+ * entries whose condition holds for the centre cost it computes. */
+#define JMME_EPZS_PRED_ALWAYS   0
+#define JMME_EPZS_PRED_GT_STOP  1
+#define JMME_EPZS_PRED_GT_2STOP 2
+#define JMME_EPZS_PRED_GT_3STOP 3
 
 /* against the uploaded current frame and reference slots; host arrays */
 int jmme_epzs_search(jmme_ctx *ctx, const jmme_epzs_req *req, int n, const int16_t *preds, int n_preds,
@@ -304,6 +318,16 @@ int jmme_epzs_search(jmme_ctx *ctx, const jmme_epzs_req *req, int n, const int16
 /* device arrays on `stream` (requests validated by the caller) */
 int jmme_epzs_search_async(jmme_ctx *ctx, const jmme_epzs_req *d_req, int n, const int16_t *d_preds,
                            const int16_t *d_stale, jmme_epzs_res *d_out, void *stream);
+/* The drop-in's form (integration/jm_gpu_me.c wraps JM's four EPZS functions
+ * with it, one call per search): as jmme_epzs_search, plus pred_cond (may be
+ * NULL) and, when visited is not NULL, the EPZSMap cells each search stamped
+ * -- (dx, dy) qpel from its centre, max_visited pairs per request at
+ * visited[2 * max_visited * i] -- so the caller can keep JM's map.  Fails when a
+ * search stamps more than max_visited cells.  Host arrays; no device copies (the
+ * kernel reads and writes mapped host memory), one launch and one sync. */
+int jmme_epzs_search_ex(jmme_ctx *ctx, const jmme_epzs_req *req, int n, const int16_t *preds,
+                        const uint8_t *pred_cond, int n_preds, const int16_t *stale, int n_stale,
+                        jmme_epzs_res *out, int16_t *visited, int max_visited);
 
 /* ---- Quarter-pel reference planes and sub-pel refinement -----------------
  * SURVEY.md §8(f) rank 1.

@@ -32,6 +32,7 @@
 #include "global.h"
 #include "mbuffer.h"
 #include "me_distortion.h"
+#include "me_epzs_common.h"
 #include "me_fullfast.h"
 #include "mv_search.h"
 #include "jmme.h"
@@ -114,7 +115,7 @@ static void init_once(VideoParameters *p_Vid, InputParameters *p_Inp)
 void __wrap_init_motion_search_module(VideoParameters *p_Vid, InputParameters *p_Inp)
 {
   __real_init_motion_search_module(p_Vid, p_Inp);
-  if (p_Inp->SearchMode[0] == FULL_SEARCH || p_Inp->SearchMode[0] == FAST_FULL_SEARCH) {
+  if (p_Inp->SearchMode[0] == FULL_SEARCH || p_Inp->SearchMode[0] == FAST_FULL_SEARCH || p_Inp->SearchMode[0] == EPZS) {
     init_once(p_Vid, p_Inp);
     if (jmme_prepare(g_me)) fail_jm("jmme_prepare");
   }
@@ -727,11 +728,402 @@ distblk __wrap_sub_pel_motion_estimation(Macroblock *currMB, MotionVector *pred_
   return (distblk)e->cost;
 }
 
+/* ---- EPZS (SearchMode = 3) ---------------------------------------------------
+ * JM's four EPZS integer searches (me_epzs.c:54-407, 417-780; EPZSSubPelGrid:
+ * me_epzs_int.c:41-420, 431-780) and EPZS_sub_pel_motion_estimation
+ * (me_epzs_sub.c:30-222), one GPU call per search.  The caller's half stays
+ * JM's: the predictor list is built here with JM's own routines
+ * (EPZS_spatial_predictors, _spatial_memory_, _temporal_, EPZSWindowPredictors,
+ * EPZSBlockTypePredictors(MB), me_epzs_common.c:1224-1764) and its stop
+ * criterion with EPZSDetermineStopCriterion (:1764).  The parts JM generates
+ * only when the centre's cost passes a bound are tagged with that bound
+ * (JMME_EPZS_PRED_*) -- the GPU computes the centre's cost and keeps the entries
+ * whose bound holds, so the list it searches is JM's.
+ *
+ * JM's state around a search is kept exactly:
+ *   BlkCount   ++, skipping 0 (me_epzs.c:92-94);
+ *   EPZSMap    never cleared: every cell the search stamps (the GPU returns
+ *              them) gets this BlkCount, and the cells that already hold the
+ *              new BlkCount (stamped 65535 searches ago, uint16 wrap) are
+ *              passed in as visited.  They are found through a ring of
+ *              per-BlkCount cell lists (g_ring[c]: every cell holding c), so no
+ *              search scans the map.  A search JM ran itself (a metric the GPU
+ *              does not serve, or the bipred searches that share the map) leaves
+ *              stamps the ring does not know: from then to the next slice the
+ *              cells are found by scanning the search window instead;
+ *   prevSad    p_EPZS->distortion[...] (the value the GPU returns);
+ *   p_motion   EPZSSpatialMem's memory (EPZSREF = 1, defines.h:56): JM's tmp at
+ *              every return;
+ *   mv         mv_block->mv[list]. */
+extern distblk __real_EPZS_motion_estimation(Macroblock *, MotionVector *, MEBlock *, distblk, int);
+extern distblk __real_EPZS_subMB_motion_estimation(Macroblock *, MotionVector *, MEBlock *, distblk, int);
+extern distblk __real_EPZS_integer_motion_estimation(Macroblock *, MotionVector *, MEBlock *, distblk, int);
+extern distblk __real_EPZS_integer_subMB_motion_estimation(Macroblock *, MotionVector *, MEBlock *, distblk, int);
+extern distblk __real_EPZS_sub_pel_motion_estimation(Macroblock *, MotionVector *, MEBlock *, distblk, int *);
+
+typedef struct cell_list {
+  uint32_t *c;
+  int n, cap;
+} cell_list;
+
+static cell_list *g_ring = NULL;                 /* [65536]: the map cells holding each BlkCount */
+static EPZSParameters *g_ring_owner = NULL;
+static int g_ring_count = -1, g_ring_foreign = 0, g_ring_side = 0, g_epzs_check = -1;
+static long long g_epzs_calls = 0, g_epzs_cpu = 0, g_epzs_foreign = 0, g_epzs_stale = 0, g_epzs_preds = 0;
+static long long g_epzs_sp_calls = 0, g_epzs_sp_cpu = 0;
+static double g_t_epzs = 0, g_t_epzs_gpu = 0;
+static int16_t *g_ep_pred = NULL, *g_ep_stale = NULL, *g_ep_vis = NULL;
+static uint8_t *g_ep_cond = NULL;
+static int g_ep_pred_cap = 0, g_ep_stale_cap = 0, g_ep_vis_cap = 0;
+
+static void cell_push(cell_list *l, uint32_t c)
+{
+  if (l->n == l->cap) {
+    int cap = l->cap ? 2 * l->cap : 16;
+    uint32_t *p = (uint32_t *)realloc(l->c, (size_t)cap * sizeof(uint32_t));
+    if (!p) error("jm_gpu_me: out of memory", 500);
+    l->c = p;
+    l->cap = cap;
+  }
+  l->c[l->n++] = c;
+}
+
+static void grow16(int16_t **p, int *cap, int need)
+{
+  if (need <= *cap) return;
+  *cap = imax(need, 2 * *cap);
+  free(*p);
+  *p = (int16_t *)malloc((size_t)*cap * 2 * sizeof(int16_t));
+  if (!*p) error("jm_gpu_me: out of memory", 500);
+}
+
+/* EPZSMap's side (searcharray, me_epzs_common.c:428-431) */
+static int epzs_map_side(Macroblock *currMB)
+{
+  InputParameters *p_Inp = currMB->p_Inp;
+  VideoParameters *p_Vid = currMB->p_Vid;
+  int sr = p_Inp->search_range[p_Vid->view_id];
+  if (p_Inp->BiPredMotionEstimation && p_Inp->BiPredMESearchRange[p_Vid->view_id] > sr)
+    sr = p_Inp->BiPredMESearchRange[p_Vid->view_id];
+  return (2 * sr + 1) << 2;
+}
+
+/* Is the ring still the whole truth about the map?  A fresh EPZS structure
+ * (EPZSStructInit per slice, slice.c:1661-1665: BlkCount 1, a zeroed map)
+ * restarts it; a BlkCount that moved without us means JM searched itself. */
+static void epzs_ring_sync(EPZSParameters *p_EPZS, int side)
+{
+  int i, j, fresh;
+  if (!g_ring) {
+    g_ring = (cell_list *)calloc(65536, sizeof(cell_list));
+    if (!g_ring) error("jm_gpu_me: out of memory", 500);
+  }
+  if (p_EPZS == g_ring_owner && (int)p_EPZS->BlkCount == g_ring_count && side == g_ring_side) return;
+  fresh = p_EPZS->BlkCount == 1;
+  for (i = 0; i < side && fresh; i++)
+    for (j = 0; j < side && fresh; j++) fresh = p_EPZS->EPZSMap[i][j] == 0;
+  if (fresh) {
+    for (i = 0; i < 65536; i++) g_ring[i].n = 0;
+    g_ring_foreign = 0;
+  } else if (!g_ring_foreign) {
+    g_ring_foreign = 1;
+    ++g_epzs_foreign;
+  }
+  g_ring_owner = p_EPZS;
+  g_ring_side = side;
+  g_ring_count = (int)p_EPZS->BlkCount;
+}
+
+/* the predictor list JM would build for this search, every conditional part
+ * included and tagged; returns the count (pool: g_ep_pred / g_ep_cond) */
+static int epzs_predictors(int variant, Macroblock *currMB, MEBlock *mv_block, distblk stop)
+{
+  Slice *currSlice = currMB->p_Slice;
+  VideoParameters *p_Vid = currMB->p_Vid;
+  InputParameters *p_Inp = currMB->p_Inp;
+  EPZSParameters *p_EPZS = currSlice->p_EPZS;
+  SPoint *pt = p_EPZS->predictor->point;
+  int list = mv_block->list, cur_list = list + currMB->list_offset, ref = mv_block->ref_idx;
+  int bt = mv_block->blocktype, sub = variant & 1, grid = variant >= 2;
+  int field_or_mbaff = currSlice->structure != FRAME || currMB->list_offset;
+  StorablePicture *ref_picture = currSlice->listX[cur_list][ref];
+  int n = 5, n1, i, w;
+  uint8_t cond[2048];
+  short invalid_refs;
+  (void)stop;
+  invalid_refs = EPZS_spatial_predictors(p_EPZS, mv_block, list, currMB->list_offset, (short)ref,
+                                         p_Vid->enc_picture->mv_info);
+  if (p_Inp->EPZSSpatialMem) EPZS_spatial_memory_predictors(p_EPZS, mv_block, cur_list, &n, ref_picture->size_x >> 2);
+  for (i = 0; i < n; i++) cond[i] = JMME_EPZS_PRED_ALWAYS;
+#if (MVC_EXTENSION_ENABLE)
+  if (!sub && p_Inp->EPZSTemporal[currSlice->view_id] && (grid || bt < 5))
+#else
+  if (!sub && p_Inp->EPZSTemporal && (grid || bt < 5))
+#endif
+  {
+    /* the co-located vector always; its neighbours when min_mcost > stop (me_epzs_common.c:1550) */
+    int start = n;
+    EPZS_temporal_predictors(currMB, ref_picture, p_EPZS, mv_block, &n, 1, 0);
+    n1 = n;
+    n = start;
+    EPZS_temporal_predictors(currMB, ref_picture, p_EPZS, mv_block, &n, 0, 1);
+    for (i = start; i < n; i++) cond[i] = (uint8_t)(i < n1 ? JMME_EPZS_PRED_ALWAYS : JMME_EPZS_PRED_GT_STOP);
+  }
+  if (!sub) {   /* window predictors (me_epzs.c:181-191, me_epzs_int.c:181-191) */
+    int always = p_Inp->EPZSFixed == 3 && (currMB->mb_x == 0 || currMB->mb_y == 0);
+    int gated = ((ref < 2 && bt < 4) || (ref < 1 && bt == 4) || (field_or_mbaff && ref < 3)) &&
+                (p_Inp->EPZSFixed > 1 || (p_Inp->EPZSFixed && currSlice->slice_type == P_SLICE));
+    if (always || gated) {
+      int ext = (grid || bt < 5) && invalid_refs > 2 && ref < 1 + field_or_mbaff;
+      int start = n;
+      EPZSWindowPredictors(&mv_block->mv[list], p_EPZS->predictor, &n,
+                           ext ? p_EPZS->window_predictor_ext : p_EPZS->window_predictor);
+      if (n > (int)sizeof cond) error("jm_gpu_me: EPZS predictor list too long", 500);
+      for (i = start; i < n; i++) cond[i] = (uint8_t)(always ? JMME_EPZS_PRED_ALWAYS : JMME_EPZS_PRED_GT_3STOP);
+    }
+  }
+  if (currMB->mbAddrX != 0 && p_Inp->EPZSBlockType) {   /* ref == 0 || min_mcost > 2 * stop */
+    int start = n;
+    if (sub)
+      EPZSBlockTypePredictors(currSlice, mv_block, pt, &n);
+    else
+      EPZSBlockTypePredictorsMB(currSlice, mv_block, pt, &n);
+    for (i = start; i < n; i++) cond[i] = (uint8_t)(ref == 0 ? JMME_EPZS_PRED_ALWAYS : JMME_EPZS_PRED_GT_2STOP);
+  }
+  if (n > (int)sizeof cond) error("jm_gpu_me: EPZS predictor list too long", 500);
+  if (n > g_ep_pred_cap) {
+    g_ep_pred_cap = imax(n, 2 * g_ep_pred_cap);
+    free(g_ep_pred);
+    free(g_ep_cond);
+    g_ep_pred = (int16_t *)malloc((size_t)g_ep_pred_cap * 2 * sizeof(int16_t));
+    g_ep_cond = (uint8_t *)malloc((size_t)g_ep_pred_cap);
+    if (!g_ep_pred || !g_ep_cond) error("jm_gpu_me: out of memory", 500);
+  }
+  for (w = 0; w < n; w++) {
+    g_ep_pred[2 * w] = pt[w].motion.mv_x;
+    g_ep_pred[2 * w + 1] = pt[w].motion.mv_y;
+    g_ep_cond[w] = cond[w];
+  }
+  return n;
+}
+
+static distblk real_epzs(int variant, Macroblock *currMB, MotionVector *pred_mv, MEBlock *mv_block, distblk min_mcost,
+                         int lambda_factor)
+{
+  switch (variant) {
+    case 0: return __real_EPZS_motion_estimation(currMB, pred_mv, mv_block, min_mcost, lambda_factor);
+    case 1: return __real_EPZS_subMB_motion_estimation(currMB, pred_mv, mv_block, min_mcost, lambda_factor);
+    case 2: return __real_EPZS_integer_motion_estimation(currMB, pred_mv, mv_block, min_mcost, lambda_factor);
+    default: return __real_EPZS_integer_subMB_motion_estimation(currMB, pred_mv, mv_block, min_mcost, lambda_factor);
+  }
+}
+
+static distblk epzs_gpu(int variant, Macroblock *currMB, MotionVector *pred_mv, MEBlock *mv_block, distblk min_mcost,
+                        int lambda_factor)
+{
+  Slice *currSlice = currMB->p_Slice;
+  InputParameters *p_Inp = currMB->p_Inp;
+  EPZSParameters *p_EPZS = currSlice->p_EPZS;
+  int list = mv_block->list, cur_list = list + currMB->list_offset, ref = mv_block->ref_idx;
+  int bt = mv_block->blocktype, grid = variant >= 2;
+  int max_x = mv_block->searchRange.max_x, max_y = mv_block->searchRange.max_y;
+  MotionVector *mv = &mv_block->mv[list];
+  distblk lambda_dist = weighted_cost(lambda_factor, (variant & 1) ? 3 : 2);
+  distblk *prevSad = &p_EPZS->distortion[cur_list][bt - 1][mv_block->pos_x2];
+  int side = epzs_map_side(currMB), n_pred, n_stale = 0, i, max_vis;
+  uint16 cnt;
+  jmme_epzs_req q;
+  jmme_epzs_res res;
+  double t0, t1;
+  if (fs_on_cpu(mv_block) || 2 * max_x + 1 > side || 2 * max_y + 1 > side) {
+    ++g_epzs_cpu;
+    return real_epzs(variant, currMB, pred_mv, mv_block, min_mcost, lambda_factor);
+  }
+  t0 = now_us();
+  ensure_planes(currMB, list, ref);
+  ++g_epzs_calls;
+  epzs_ring_sync(p_EPZS, side);
+  cnt = (uint16)(p_EPZS->BlkCount + 1);
+  if (cnt == 0) cnt = 1;
+
+  /* cells already holding cnt inside this search's window, (dx, dy) from the centre */
+  if (!g_ring_foreign) {
+    cell_list *l = &g_ring[cnt];
+    int k = 0;
+    grow16(&g_ep_stale, &g_ep_stale_cap, l->n + 1);
+    for (i = 0; i < l->n; i++) {
+      uint32_t c = l->c[i];
+      int r = (int)(c / (uint32_t)side), col = (int)(c % (uint32_t)side);
+      if (p_EPZS->EPZSMap[r][col] != cnt) continue;       /* overwritten since */
+      l->c[k++] = c;
+      if (r <= 2 * max_y && col <= 2 * max_x) {
+        g_ep_stale[2 * n_stale] = (int16_t)(col - max_x);
+        g_ep_stale[2 * n_stale + 1] = (int16_t)(r - max_y);
+        ++n_stale;
+      }
+    }
+    l->n = k;
+  } else {
+    int step = grid ? 1 : 4, r, col;
+    for (r = 0; r <= 2 * max_y; r += step)
+      for (col = 0; col <= 2 * max_x; col += step)
+        if (p_EPZS->EPZSMap[r][col] == cnt) {
+          grow16(&g_ep_stale, &g_ep_stale_cap, n_stale + 1);
+          g_ep_stale[2 * n_stale] = (int16_t)(col - max_x);
+          g_ep_stale[2 * n_stale + 1] = (int16_t)(r - max_y);
+          ++n_stale;
+        }
+  }
+  g_epzs_stale += n_stale;
+  if (g_epzs_check < 0) {
+    const char *e = getenv("JMME_EPZS_CHECK");
+    g_epzs_check = e && e[0] == '1';
+  }
+  if (g_epzs_check && !g_ring_foreign) {   /* the ring against a scan of the window */
+    int step = grid ? 1 : 4, r, col, found = 0, k;
+    for (r = 0; r <= 2 * max_y; r += step)
+      for (col = 0; col <= 2 * max_x; col += step)
+        if (p_EPZS->EPZSMap[r][col] == cnt) {
+          for (k = 0; k < n_stale; k++)
+            if (g_ep_stale[2 * k] == col - max_x && g_ep_stale[2 * k + 1] == r - max_y) break;
+          if (k == n_stale) error("jm_gpu_me: JMME_EPZS_CHECK: a map cell holding the next BlkCount is not in the ring", 500);
+          ++found;
+        }
+    if (found != n_stale) error("jm_gpu_me: JMME_EPZS_CHECK: the ring lists cells the window scan does not find", 500);
+  }
+
+  memset(&q, 0, sizeof q);
+  q.stop_crit = (int64_t)EPZSDetermineStopCriterion(p_EPZS, prevSad, mv_block, lambda_dist);
+  n_pred = epzs_predictors(variant, currMB, mv_block, (distblk)q.stop_crit);
+  g_epzs_preds += n_pred;
+  q.pos_x = mv_block->pos_x;
+  q.pos_y = mv_block->pos_y;
+  q.bsx = mv_block->blocksize_x;
+  q.bsy = mv_block->blocksize_y;
+  q.blocktype = (int16_t)bt;
+  q.ref_idx = (int16_t)ref;
+  q.pred_x = pred_mv->mv_x;
+  q.pred_y = pred_mv->mv_y;
+  q.center_x = mv->mv_x;
+  q.center_y = mv->mv_y;
+  q.max_x = (int16_t)max_x;
+  q.max_y = (int16_t)max_y;
+  q.lambda = lambda_factor;
+  q.variant = (uint8_t)variant;
+  q.flags = (uint8_t)((currSlice->structure == FRAME ? JMME_EPZS_FRAME : 0) |
+                      (currSlice->slice_type == P_SLICE ? JMME_EPZS_PSLICE : 0));
+  q.pattern = (uint8_t)p_Inp->EPZSPattern;
+  q.dual = (uint8_t)p_Inp->EPZSDual;
+  q.n_pred = n_pred;
+  q.n_stale = n_stale;
+  q.ref_slot = list * 32 + ref;
+  q.prev_sad = (int64_t)*prevSad;
+  q.medthres = (int64_t)p_EPZS->medthres[bt];
+  /* every cell a search can stamp lies in its window */
+  max_vis = grid ? (2 * max_x + 1) * (2 * max_y + 1) : ((max_x >> 1) + 1) * ((max_y >> 1) + 1);
+  grow16(&g_ep_vis, &g_ep_vis_cap, max_vis);
+  t1 = now_us();
+  if (jmme_epzs_search_ex(g_me, &q, 1, g_ep_pred, g_ep_cond, n_pred, g_ep_stale, n_stale, &res, g_ep_vis, max_vis))
+    fail_jm("jmme_epzs_search_ex");
+  g_t_epzs_gpu += now_us() - t1;
+
+  /* JM's side effects */
+  for (i = 0; i < res.n_visited; i++) {
+    int r = max_y + g_ep_vis[2 * i + 1], col = max_x + g_ep_vis[2 * i];
+    if (p_EPZS->EPZSMap[r][col] != cnt) {
+      p_EPZS->EPZSMap[r][col] = cnt;
+      if (!g_ring_foreign) cell_push(&g_ring[cnt], (uint32_t)(r * side + col));
+    }
+  }
+  p_EPZS->BlkCount = cnt;
+  g_ring_count = cnt;
+  *prevSad = (distblk)res.prev_sad;
+  if (p_Inp->EPZSSpatialMem) {
+    MotionVector *m = &p_EPZS->p_motion[cur_list][ref][bt - 1][mv_block->block_y][mv_block->pos_x2];
+    m->mv_x = res.motion_x;
+    m->mv_y = res.motion_y;
+  }
+  mv->mv_x = res.mv_x;
+  mv->mv_y = res.mv_y;
+  g_t_epzs += now_us() - t0;
+  return (distblk)res.cost;
+}
+
+distblk __wrap_EPZS_motion_estimation(Macroblock *currMB, MotionVector *pred_mv, MEBlock *mv_block, distblk min_mcost,
+                                      int lambda_factor)
+{
+  return epzs_gpu(0, currMB, pred_mv, mv_block, min_mcost, lambda_factor);
+}
+
+distblk __wrap_EPZS_subMB_motion_estimation(Macroblock *currMB, MotionVector *pred_mv, MEBlock *mv_block,
+                                            distblk min_mcost, int lambda_factor)
+{
+  return epzs_gpu(1, currMB, pred_mv, mv_block, min_mcost, lambda_factor);
+}
+
+distblk __wrap_EPZS_integer_motion_estimation(Macroblock *currMB, MotionVector *pred_mv, MEBlock *mv_block,
+                                              distblk min_mcost, int lambda_factor)
+{
+  return epzs_gpu(2, currMB, pred_mv, mv_block, min_mcost, lambda_factor);
+}
+
+distblk __wrap_EPZS_integer_subMB_motion_estimation(Macroblock *currMB, MotionVector *pred_mv, MEBlock *mv_block,
+                                                    distblk min_mcost, int lambda_factor)
+{
+  return epzs_gpu(3, currMB, pred_mv, mv_block, min_mcost, lambda_factor);
+}
+
+/* EPZS_sub_pel_motion_estimation's contract (me_epzs_sub.c:30-222): variant 1
+ * of jmme_subpel_refine, its early-exit threshold p_EPZS->subthres[blocktype] */
+distblk __wrap_EPZS_sub_pel_motion_estimation(Macroblock *currMB, MotionVector *pred_mv, MEBlock *mv_block,
+                                              distblk min_mcost, int *lambda_factor)
+{
+  VideoParameters *p_Vid = currMB->p_Vid;
+  Slice *currSlice = currMB->p_Slice;
+  int list = mv_block->list, ref = mv_block->ref_idx;
+  int mh = metric_id(mv_block->computePredHPel), mq = metric_id(mv_block->computePredQPel);
+  jmme_subpel_req q;
+  jmme_block_res r;
+  if (mh < 0 || mq < 0 || mv_block->ChromaMEEnable || mv_block->search_pos2 > 9 || mv_block->search_pos4 > 9 ||
+      (mv_block->test8x8 && mv_block->blocktype > 4)) {
+    ++g_epzs_sp_cpu;
+    return __real_EPZS_sub_pel_motion_estimation(currMB, pred_mv, mv_block, min_mcost, lambda_factor);
+  }
+  ++g_epzs_sp_calls;
+  ensure_planes(currMB, list, ref);
+  memset(&q, 0, sizeof q);
+  q.pos_x = mv_block->pos_x;
+  q.pos_y = mv_block->pos_y;
+  q.blocktype = (int16_t)mv_block->blocktype;
+  q.ref_slot = (int16_t)(list * 32 + ref);
+  q.pred_x = pred_mv->mv_x;
+  q.pred_y = pred_mv->mv_y;
+  q.mv_x = mv_block->mv[list].mv_x;
+  q.mv_y = mv_block->mv[list].mv_y;
+  q.lambda_h = lambda_factor[H_PEL];
+  q.lambda_q = lambda_factor[Q_PEL];
+  q.min_mcost = (int64_t)min_mcost;
+  q.subthres = (int64_t)currSlice->p_EPZS->subthres[mv_block->blocktype];
+  q.variant = 1;
+  q.flags = (uint8_t)((mv_block->test8x8 ? JMME_SP_TEST8x8 : 0) |
+                      ((!currMB->p_Inp->rdopt && currSlice->slice_type != B_SLICE) ? JMME_SP_CHECK0 : 0));
+  q.metric_h = (uint8_t)mh;
+  q.metric_q = (uint8_t)mq;
+  q.start_hp = (uint8_t)(p_Vid->start_me_refinement_hp != 0);
+  q.start_qp = (uint8_t)(p_Vid->start_me_refinement_qp != 0);
+  q.search_pos2 = (uint8_t)mv_block->search_pos2;
+  q.search_pos4 = (uint8_t)mv_block->search_pos4;
+  if (jmme_subpel_refine(g_me, &q, 1, &r)) fail_jm("jmme_subpel_refine");
+  mv_block->mv[list].mv_x = r.mv_x;
+  mv_block->mv[list].mv_y = r.mv_y;
+  return (distblk)r.cost;
+}
+
 /* reported at exit, so a run shows the searches really went to the GPU */
 static void report(void) __attribute__((destructor));
 static void report(void)
 {
-  if (g_me || g_cpu_calls) {
+  if (g_me || g_cpu_calls || g_epzs_cpu) {
     fprintf(stderr, "jm_gpu_me: %lld integer-pel searches on the GPU (libjmme): %lld from %lld speculative "
                     "batches, the rest one call each; %lld on the CPU (non-SAD or weighted metric)\n",
             g_calls, g_hits + g_batches, g_batches, g_cpu_calls);
@@ -746,6 +1138,15 @@ static void report(void)
       for (s = 0; s < JMME_NSLOT; s++) fprintf(stderr, " %lld", g_miss_slot[s]);
       fprintf(stderr, "\n");
     }
+    if (g_epzs_calls || g_epzs_cpu)
+      fprintf(stderr, "jm_gpu_me: %lld EPZS searches on the GPU (libjmme), one call each; %lld on the CPU; "
+                      "%lld predictors, %lld pre-stamped map cells, %lld switches to window scans; "
+                      "%.1f ms in the EPZS wrapper, %.1f ms in jmme_epzs_search_ex\n",
+              g_epzs_calls, g_epzs_cpu, g_epzs_preds, g_epzs_stale, g_epzs_foreign, g_t_epzs * 1e-3,
+              g_t_epzs_gpu * 1e-3);
+    if (g_epzs_sp_calls || g_epzs_sp_cpu)
+      fprintf(stderr, "jm_gpu_me: %lld EPZS sub-pel refinements on the GPU, %lld on the CPU\n", g_epzs_sp_calls,
+              g_epzs_sp_cpu);
     if (g_trace) fclose(g_trace);
     if (g_me) jmme_destroy(g_me);
   }

@@ -1,0 +1,112 @@
+"""GPU: EPZS (SearchMode = 3) in the drop-in.  lencod_jmme wraps JM's four EPZS
+integer searches (JM/lencod/src/me_epzs.c:54,417; me_epzs_int.c:41,431) and
+EPZS_sub_pel_motion_estimation (me_epzs_sub.c:30): the predictor lists are
+built host-side with JM's own routines and every search runs in
+jmme_epzs_search_ex, JM's never-cleared EPZSMap, BlkCount, prevSad and
+spatial-memory vectors kept from the GPU's answers (integration/jm_gpu_me.c).
+The stock lencod (oracle/_ref/lencod) is the oracle: bitstream and
+reconstruction must be byte-identical, with no EPZS search left on the CPU.
+
+BASELINE_EPZS restates the motion-estimation keys of the reference's
+encoder_baseline.cfg (JM/bin/encoder_baseline.cfg: SATD sub-pel, RDO on,
+SearchRange 32, the EPZS section) with SearchMode = 3 -- the file itself is not
+read at run time."""
+import os
+import re
+import tempfile
+
+import pytest
+
+from test_jm_dropin_gpu import GPU, STOCK, _encode
+
+pytestmark = pytest.mark.gpu
+
+BASELINE_EPZS = {
+    "ProfileIDC": 66, "SearchMode": 3, "SearchRange": 32, "DisableSubpelME": 0, "MEDistortionFPel": 0,
+    "MEDistortionHPel": 2, "MEDistortionQPel": 2, "MDDistortion": 2, "RestrictSearchRange": 2, "RDOptimization": 1,
+    "AdaptiveRounding": 1, "EPZSPattern": 2, "EPZSDualRefinement": 3, "EPZSFixedPredictors": 2, "EPZSTemporal": 1,
+    "EPZSSpatialMem": 1, "EPZSBlockType": 1, "EPZSMinThresScale": 0, "EPZSMedThresScale": 1,
+    "EPZSMaxThresScale": 2, "EPZSSubPelME": 1, "EPZSSubPelMEBiPred": 1, "EPZSSubPelThresScale": 2,
+    "EPZSSubPelGrid": 1,
+}
+
+_EPZS_LINE = re.compile(r"(\d+) EPZS searches on the GPU \(libjmme\), one call each; (\d+) on the CPU; (\d+) predictors, "
+                        r"(\d+) pre-stamped map cells, (\d+) switches to window scans; ([\d.]+) ms in the EPZS wrapper, "
+                        r"([\d.]+) ms in jmme_epzs_search_ex")
+_SP_LINE = re.compile(r"(\d+) EPZS sub-pel refinements on the GPU, (\d+) on the CPU")
+
+
+def epzs_stats(stderr):
+    m = _EPZS_LINE.search(stderr)
+    assert m, stderr[-800:]
+    k = ("gpu", "cpu", "preds", "stale", "scans", "wrap_ms", "call_ms")
+    return {a: (float(b) if a.endswith("_ms") else int(b)) for a, b in zip(k, m.groups())}
+
+
+def _run(w, h, frames, over, seed=5, gmv=(3, -2), adversarial=False, env=None):
+    if not (os.path.exists(STOCK) and os.path.exists(GPU)):
+        pytest.fail("lencod builds missing: run `make -C oracle ref && make -C integration` in the build container")
+    from jmme import synth
+    params = dict(BASELINE_EPZS, **over)
+    with tempfile.TemporaryDirectory() as d:
+        yuv = os.path.join(d, "in.yuv")
+        synth.write_yuv420(yuv, synth.luma_sequence(w, h, frames, seed=seed, gmv=gmv, adversarial=adversarial))
+        ref264, refrec, _ = _encode(STOCK, d, "cpu", yuv, w, h, frames, params)
+        gpu264, gpurec, r = _encode(GPU, d, "gpu", yuv, w, h, frames, params, env)
+        st = epzs_stats(r.stderr)
+        assert (gpu264, gpurec) == (ref264, refrec), r.stderr[-800:]
+        return st, r.stderr
+
+
+@pytest.mark.parametrize("w,h,frames,over", [
+    # encoder_baseline.cfg itself (EPZSSubPelGrid 1: the quarter-pel grid searches, no SubPelME)
+    (176, 144, 4, {"NumberReferenceFrames": 1}),
+    (176, 144, 4, {"NumberReferenceFrames": 3}),
+    # EPZSSubPelGrid 0: integer-grid searches + EPZS_sub_pel_motion_estimation on the GPU
+    (176, 144, 4, {"NumberReferenceFrames": 2, "EPZSSubPelGrid": 0}),
+    (352, 288, 3, {"NumberReferenceFrames": 3, "EPZSSubPelGrid": 0}),
+    (352, 288, 3, {"NumberReferenceFrames": 2}),
+    # RDO off; the other refinement patterns (0 small diamond, 1 square, 3 extended diamond,
+    # 5 PMVFAST; the SBP large diamond 4 needs the grid) and dual refinements; window
+    # predictors on every picture-border macroblock (EPZSFixedPredictors 3)
+    (176, 144, 3, {"NumberReferenceFrames": 2, "RDOptimization": 0, "EPZSSubPelGrid": 0, "EPZSPattern": 0,
+                   "EPZSDualRefinement": 1, "EPZSFixedPredictors": 3}),
+    (176, 144, 3, {"NumberReferenceFrames": 2, "RDOptimization": 0, "EPZSPattern": 4, "EPZSDualRefinement": 5,
+                   "EPZSFixedPredictors": 3}),
+    (176, 144, 3, {"NumberReferenceFrames": 1, "EPZSSubPelGrid": 0, "EPZSPattern": 3, "EPZSDualRefinement": 6,
+                   "EPZSSpatialMem": 0, "EPZSTemporal": 0}),
+    (176, 144, 3, {"NumberReferenceFrames": 2, "EPZSPattern": 5, "EPZSDualRefinement": 2, "EPZSBlockType": 0,
+                   "Transform8x8Mode": 1, "ProfileIDC": 100}),
+    (176, 144, 3, {"NumberReferenceFrames": 1, "EPZSPattern": 1, "EPZSDualRefinement": 0, "SearchRange": 16}),
+])
+def test_lencod_epzs_is_byte_identical(gpu, w, h, frames, over):
+    st, err = _run(w, h, frames, over, seed=w + frames + len(over))
+    assert st["gpu"] > 0 and st["cpu"] == 0 and st["scans"] == 0, err[-800:]
+    if not over.get("EPZSSubPelGrid", 1):
+        m = _SP_LINE.search(err)
+        assert m and int(m.group(1)) > 0 and int(m.group(2)) == 0, err[-800:]
+
+
+def test_lencod_epzs_blkcount_wraps(gpu):
+    """a 1080p P picture runs 334,560 searches in one slice: BlkCount wraps five times
+    (me_epzs.c:92-94) and map cells stamped 65535 searches earlier count as visited.
+    JMME_EPZS_CHECK=1 has the adapter check its ring of stamped cells against a scan
+    of every search window (integer grid: EPZSSubPelGrid 0, sub-pel on the GPU)"""
+    st, err = _run(1920, 1080, 2, {"NumberReferenceFrames": 1, "EPZSSubPelGrid": 0}, seed=77,
+                   env={"JMME_EPZS_CHECK": "1"})
+    assert st["gpu"] == 8160 * 41 and st["cpu"] == 0 and st["scans"] == 0 and st["stale"] > 0, err[-800:]
+
+
+def test_lencod_epzs_b_pictures_with_cpu_bipred(gpu):
+    """B pictures with bi-predictive ME: JM's own EPZS_bipred_motion_estimation shares
+    EPZSMap and BlkCount with the GPU searches, so the adapter falls back to scanning the
+    search window for cells holding the next BlkCount -- still byte-identical"""
+    st, err = _run(176, 144, 5, {"NumberReferenceFrames": 2, "EPZSSubPelGrid": 0, "ProfileIDC": 77,
+                                 "NumberBFrames": 1, "BiPredMotionEstimation": 1}, seed=9)
+    assert st["gpu"] > 0 and st["cpu"] == 0 and st["scans"] > 0, err[-800:]
+
+
+def test_lencod_epzs_1080p_frame(gpu):
+    """one 1080p P picture (8160 macroblocks, every partition of the baseline config)"""
+    st, err = _run(1920, 1080, 2, {"NumberReferenceFrames": 1}, seed=31)
+    assert st["gpu"] == 8160 * 41 and st["cpu"] == 0 and st["stale"] > 0, err[-800:]
