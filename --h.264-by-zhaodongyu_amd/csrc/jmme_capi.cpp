@@ -61,12 +61,15 @@ struct jmme_ctx {
   jmme_config cfg;
   int device = 0;
   int max_mvd = 0;
-  int width = 0, height = 0, pitch = 0;
+  int width = 0, height = 0, pitch = 0;      // pitch in pels
+  bool hbd = false;                          // SourceBitDepthLuma > 8: 16-bit planes, small-kernel search only
+  int max_pel = 255;
   uint8_t *d_cur = nullptr;
   uint8_t *d_refs[kMaxLists * kMaxRefs] = {};
   const uint8_t **d_ref_table = nullptr;     // device copy of d_refs
   bool ref_table_dirty = true;
-  std::vector<uint8_t> h_stage;              // u16 -> u8 conversion buffer
+  uint8_t *h_stage = nullptr;                // u16 -> u8 conversion buffer (pinned: one DMA per plane)
+  size_t cap_stage = 0;
   jmme_mb_req *d_req = nullptr;
   jmme_block_res *d_out = nullptr;
   size_t cap_units = 0;
@@ -243,7 +246,11 @@ extern "C" const char *jmme_version(void) { return "jmme 0.1 (gfx950)"; }
 extern "C" jmme_ctx *jmme_create(const jmme_config *cfg, int device) {
   if (!cfg) { fail("null config"); return nullptr; }
   if (cfg->ChromaMEEnable) { fail("ChromaMEEnable != 0 is not supported"); return nullptr; }
-  if (cfg->SourceBitDepthLuma != 8) { fail("only 8-bit luma is supported"); return nullptr; }
+  // JM's imgpel holds 8..14-bit luma (defines.h:37, configfile.h SourceBitDepthLuma)
+  if (cfg->SourceBitDepthLuma < 8 || cfg->SourceBitDepthLuma > 14) {
+    fail("SourceBitDepthLuma %d outside 8..14", cfg->SourceBitDepthLuma);
+    return nullptr;
+  }
   // the integer-pel kernels compute JM's computeSAD (me_distortion.c:349); SSE /
   // SATD full-pel metrics (MEDistortionFPel 1/2, lencod.c:782-796) would give
   // different vectors, so they are refused rather than silently searched with SAD
@@ -257,6 +264,8 @@ extern "C" jmme_ctx *jmme_create(const jmme_config *cfg, int device) {
   }
   auto *ctx = new jmme_ctx;
   ctx->cfg = *cfg;
+  ctx->hbd = cfg->SourceBitDepthLuma > 8;
+  ctx->max_pel = (1 << cfg->SourceBitDepthLuma) - 1;
   ctx->max_mvd = jmme_max_mvd(cfg);
   hipError_t e;
   int caller_dev = -1;
@@ -299,6 +308,7 @@ extern "C" void jmme_destroy(jmme_ctx *ctx) {
   (void)hipFree(ctx->d_sub_table);
   (void)hipFree(ctx->d_sp);
   if (ctx->h_pin) (void)hipHostFree(ctx->h_pin);
+  if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
   if (ctx->h_sitems) (void)hipHostFree(ctx->h_sitems);
   if (ctx->h_sout) (void)hipHostFree(ctx->h_sout);
   if (ctx->h_emap) (void)hipHostFree(ctx->h_emap);
@@ -321,22 +331,38 @@ int set_geometry(jmme_ctx *ctx, int w, int h) {
   return 0;
 }
 
-// JM get_mem2Dpel(_pad) planes: rows[y] equally spaced.  Converted to 8-bit.
+// JM get_mem2Dpel(_pad) planes: rows[y] equally spaced.  Converted to 8-bit
+// (or kept 16-bit when the context is high bit depth).
 int upload_plane(jmme_ctx *ctx, uint8_t **dst, const jmme_imgpel *const *rows, int w, int h) {
   if (!rows || !rows[0]) return fail("null plane");
   if (set_geometry(ctx, w, h)) return -1;
   ptrdiff_t stride = h > 1 ? rows[1] - rows[0] : w;
-  ctx->h_stage.resize((size_t)ctx->pitch * h);
+  const size_t es = ctx->hbd ? 2 : 1, bytes = (size_t)ctx->pitch * h * es;
+  if (bytes > ctx->cap_stage) {
+    if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
+    ctx->h_stage = nullptr;
+    ctx->cap_stage = 0;
+    HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_stage), bytes, hipHostMallocDefault));
+    ctx->cap_stage = bytes;
+  }
   for (int y = 0; y < h; ++y) {
     const jmme_imgpel *src = rows[0] + (ptrdiff_t)y * stride;
     if (rows[y] != src) return fail("plane rows are not equally spaced (row %d)", y);
-    uint8_t *d = &ctx->h_stage[(size_t)y * ctx->pitch];
     unsigned m = 0;
-    for (int x = 0; x < w; ++x) { m |= src[x]; d[x] = (uint8_t)src[x]; }
-    if (m > 255) return fail("sample > 255 in row %d: only 8-bit luma is supported", y);
+    if (ctx->hbd) {
+      uint16_t *d = reinterpret_cast<uint16_t *>(ctx->h_stage) + (size_t)y * ctx->pitch;
+      for (int x = 0; x < w; ++x) { m |= src[x]; d[x] = src[x]; }
+    } else {
+      uint8_t *d = ctx->h_stage + (size_t)y * ctx->pitch;
+      for (int x = 0; x < w; ++x) { m |= src[x]; d[x] = (uint8_t)src[x]; }
+    }
+    if (m > (unsigned)ctx->max_pel)
+      return fail("sample above %d in row %d (SourceBitDepthLuma %d)", ctx->max_pel, y, ctx->cfg.SourceBitDepthLuma);
   }
-  if (!*dst) HIPCHK(hipMalloc(dst, (size_t)ctx->pitch * h));
-  HIPCHK(hipMemcpy(*dst, ctx->h_stage.data(), (size_t)ctx->pitch * h, hipMemcpyHostToDevice));
+  if (!*dst) HIPCHK(hipMalloc(dst, bytes));
+  // complete before the staging buffer is refilled by the next upload
+  HIPCHK(hipMemcpyAsync(*dst, ctx->h_stage, bytes, hipMemcpyHostToDevice, nullptr));
+  HIPCHK(hipStreamSynchronize(nullptr));
   return 0;
 }
 
@@ -410,7 +436,10 @@ int sync_ref_table(jmme_ctx *ctx, hipStream_t s) {
 
 int launch(jmme_ctx *ctx, int mode, const uint8_t *d_cur, const uint8_t *const *d_ref_table, int pitch,
            int w, int h, const jmme_mb_req *d_req, int n, jmme_block_res *d_out, hipStream_t s,
-           uint32_t *debug_words = nullptr) {
+           uint32_t *debug_words = nullptr, bool planes_8bit = false) {
+  if (ctx->hbd && !planes_8bit)
+    return fail("SourceBitDepthLuma %d: the batched item kernel reads 8-bit planes; high bit depth is served by "
+                "jmme_search_mbs (host arrays)", ctx->cfg.SourceBitDepthLuma);
   if (mode != JMME_FULL_SEARCH && mode != JMME_FAST_FULL_SEARCH)
     return fail("search mode %d not supported by the batched engine (FS=-1, FFS=0)", mode);
   if (n < 0) return fail("negative unit count");
@@ -573,14 +602,19 @@ void small_items(const jmme_ctx *ctx, int mode, const jmme_mb_req *req, int n, s
 }
 
 // 1 = served (results in out), 0 = too large for the small path, -1 = error
-int search_small(jmme_ctx *ctx, int mode, const jmme_mb_req *req, int n, jmme_block_res *out, hipStream_t s) {
-  if (ctx->small_max_wg <= 0) return 0;
+int search_small(jmme_ctx *ctx, int mode, const jmme_mb_req *req, int n, jmme_block_res *out, hipStream_t s,
+                 bool force = false) {
+  if (ctx->small_max_wg <= 0 && !force) return 0;
   std::vector<SmallItem> items;
   int max_r = 0;
   small_items(ctx, mode, req, n, items, &max_r);
   const int tiles = (2 * max_r + 1 + kSmallTile - 1) / kSmallTile;
   const long long wgs = (long long)items.size() * tiles * tiles;
-  if (items.empty() || wgs > ctx->small_max_wg) return items.empty() ? 1 : 0;
+  if (items.empty() || (wgs > ctx->small_max_wg && !force)) return items.empty() ? 1 : 0;
+  if (ctx->hbd)   // 32-bit costs: (SAD << 5) + lambda * mvbits must not wrap
+    for (const SmallItem &it : items)
+      if ((uint64_t)it.lam * 64u + ((uint64_t)256 * ctx->max_pel << 5) >= (1ull << 32))
+        return fail("lambda %d too large for the high-bit-depth search", it.lam);
   if (items.size() > ctx->cap_sitems) {
     if (ctx->h_sitems) (void)hipHostFree(ctx->h_sitems);
     ctx->h_sitems = nullptr;
@@ -599,7 +633,6 @@ int search_small(jmme_ctx *ctx, int mode, const jmme_mb_req *req, int n, jmme_bl
   }
   if ((size_t)n * JMME_NSLOT > ctx->cap_sout) {
     if (ctx->h_sout) (void)hipHostFree(ctx->h_sout);
-  if (ctx->h_emap) (void)hipHostFree(ctx->h_emap);
     ctx->h_sout = nullptr;
     ctx->cap_sout = 0;
     const size_t cap = std::max<size_t>(64 * JMME_NSLOT, (size_t)n * JMME_NSLOT);
@@ -614,6 +647,7 @@ int search_small(jmme_ctx *ctx, int mode, const jmme_mb_req *req, int n, jmme_bl
   p.height = ctx->height;
   p.mode = mode;
   p.max_mvd = ctx->max_mvd;
+  p.hbd = ctx->hbd ? 1 : 0;
   void *d_items = nullptr, *d_sout = nullptr;
   HIPCHK(hipHostGetDevicePointer(&d_items, ctx->h_sitems, 0));
   HIPCHK(hipHostGetDevicePointer(&d_sout, ctx->h_sout, 0));
@@ -650,7 +684,8 @@ extern "C" int jmme_search_mbs(jmme_ctx *ctx, int mode, const jmme_mb_req *req, 
   hipStream_t s = nullptr;
   // a batch of a few units: the low-latency path (one launch, no copies)
   if (mode == JMME_FULL_SEARCH || mode == JMME_FAST_FULL_SEARCH) {
-    const int r = search_small(ctx, mode, req, n, out, s);
+    // high bit depth: every batch on the 16-bit small kernel
+    const int r = search_small(ctx, mode, req, n, out, s, ctx->hbd);
     if (r != 0) return r < 0 ? -1 : 0;
   }
   if (ensure_units(ctx, (size_t)n)) return -1;
@@ -702,7 +737,7 @@ extern "C" int jmme_search_mbs_planes_async(jmme_ctx *ctx, int mode, const uint8
   std::vector<const uint8_t *> tab(kMaxLists * kMaxRefs, d_ref);
   HIPCHK(hipMemcpyAsync(ctx->d_ref_table, tab.data(), tab.size() * sizeof(void *), hipMemcpyHostToDevice, s));
   ctx->ref_table_dirty = true;
-  return launch(ctx, mode, d_cur, ctx->d_ref_table, pitch, w, h, d_req, n, d_out, s);
+  return launch(ctx, mode, d_cur, ctx->d_ref_table, pitch, w, h, d_req, n, d_out, s, nullptr, true);
 }
 
 extern "C" int jmme_search_status(jmme_ctx *ctx, void *stream) {
@@ -1040,6 +1075,7 @@ int prepare_subs(jmme_ctx *ctx, hipStream_t s);   // sub-pel section below
 namespace {
 int launch_epzs_ex(jmme_ctx *ctx, const jmme_epzs_req *d_req, int n, const int16_t *d_preds, const uint8_t *d_cond,
                    const int16_t *d_stale, jmme_epzs_res *d_out, int16_t *d_vis, int max_visited, hipStream_t s) {
+  if (ctx->hbd) return fail("SourceBitDepthLuma %d: the EPZS search is 8-bit only", ctx->cfg.SourceBitDepthLuma);
   if (sync_ref_table(ctx, s)) return -1;
   EpzsParams p{};
   p.cur = ctx->d_cur;
@@ -1468,6 +1504,7 @@ extern "C" int jmme_debug_stamps(jmme_ctx *ctx, uint64_t *out, int max_units) {
 namespace {
 
 int build_sub_images(jmme_ctx *ctx, int slot, hipStream_t s) {
+  if (ctx->hbd) return fail("SourceBitDepthLuma %d: quarter-pel planes are 8-bit only", ctx->cfg.SourceBitDepthLuma);
   if (!ctx->d_refs[slot]) return fail("reference slot %d not uploaded", slot);
   const SubGeom g = sub_geom(ctx->width, ctx->height);
   if (!ctx->d_subs[slot]) {
@@ -1548,6 +1585,7 @@ extern "C" int jmme_sub_images_async(jmme_ctx *ctx, const uint8_t *d_src, int sr
 extern "C" int jmme_subpel_validate(jmme_ctx *ctx, const jmme_subpel_req *req, int n) {
   DevGuard dg_(ctx);
   if (!ctx) return fail("null ctx");
+  if (ctx->hbd) return fail("SourceBitDepthLuma %d: sub-pel refinement is 8-bit only", ctx->cfg.SourceBitDepthLuma);
   if (n < 0) return fail("negative request count");
   if (n && !req) return fail("null request array");
   if (!ctx->d_cur) return fail("no current frame uploaded");
@@ -1638,8 +1676,8 @@ extern "C" int jmme_prepare(jmme_ctx *ctx) {
   constexpr int kW = 64, kH = 64;
   const auto g = sub_geom(kW, kH);
   DevBuf plane, table, dreq, dout, subs;
-  HIPCHK(plane.alloc((size_t)kW * kH));
-  HIPCHK(hipMemset(plane.p, 0, (size_t)kW * kH));
+  HIPCHK(plane.alloc((size_t)kW * kH * 2));   // 16-bit pels for a high-bit-depth context
+  HIPCHK(hipMemset(plane.p, 0, (size_t)kW * kH * 2));
   std::vector<const uint8_t *> tab(kMaxLists * kMaxRefs, static_cast<const uint8_t *>(plane.p));
   HIPCHK(table.alloc(tab.size() * sizeof(void *)));
   HIPCHK(hipMemcpy(table.p, tab.data(), tab.size() * sizeof(void *), hipMemcpyHostToDevice));
@@ -1653,7 +1691,8 @@ extern "C" int jmme_prepare(jmme_ctx *ctx) {
   HIPCHK(hipMemcpy(dreq.p, &r, sizeof r, hipMemcpyHostToDevice));
   HIPCHK(dout.alloc(JMME_NSLOT * sizeof(jmme_block_res)));
   if (launch(ctx, JMME_FULL_SEARCH, static_cast<const uint8_t *>(plane.p), static_cast<const uint8_t *const *>(table.p),
-             kW, kW, kH, static_cast<const jmme_mb_req *>(dreq.p), 1, static_cast<jmme_block_res *>(dout.p), nullptr))
+             kW, kW, kH, static_cast<const jmme_mb_req *>(dreq.p), 1, static_cast<jmme_block_res *>(dout.p), nullptr,
+             nullptr, true))
     return -1;
   // the small path reads the context's planes: borrow the dummy for one call
   uint8_t *cur = ctx->d_cur, *ref0 = ctx->d_refs[0];
@@ -1663,13 +1702,14 @@ extern "C" int jmme_prepare(jmme_ctx *ctx) {
   ctx->height = kH;
   ctx->pitch = kW;
   jmme_block_res res[JMME_NSLOT];
-  const int rc = search_small(ctx, JMME_FULL_SEARCH, &r, 1, res, nullptr);
+  const int rc = search_small(ctx, JMME_FULL_SEARCH, &r, 1, res, nullptr, true);
   ctx->d_cur = cur;
   ctx->d_refs[0] = ref0;
   ctx->width = w;
   ctx->height = h;
   ctx->pitch = pitch;
   if (rc < 0) return -1;
+  if (ctx->hbd) return 0;   // no quarter-pel planes at high bit depth
   HIPCHK(subs.alloc(16 * g.plane_stride));
   HIPCHK(launch_sub_images(static_cast<const uint8_t *>(plane.p), kW, kW, kH, static_cast<uint8_t *>(subs.p), g.pitch,
                            g.plane_stride, nullptr));

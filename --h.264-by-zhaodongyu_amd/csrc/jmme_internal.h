@@ -83,8 +83,9 @@ static_assert(sizeof(SmallItem) == 48, "SmallItem layout");
 
 struct SmallParams {
   const uint8_t *cur;
-  int pitch, width, height;
+  int pitch, width, height;           // pitch in pels (16-bit pels when hbd)
   int mode, max_mvd;
+  int hbd;                            // SourceBitDepthLuma > 8: 16-bit planes (v_sad_u16)
   const SmallItem *items;             // n_items (device-readable: host-mapped pinned memory)
   int n_items;
   int tiles;                          // tiles per item side: ceil((2 * max R + 1) / 16)

@@ -1539,12 +1539,19 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
   return min(min(r0, r1), min(r2, r3));
 }
 
-template <bool FFS>
+// High bit depth (SourceBitDepthLuma > 8: JM's imgpel holds up to 14 bits,
+// JM/lencod/inc/defines.h:37): the planes are 16-bit and the staged words hold
+// two pels, so a 4x4 row is two v_sad_u16 (|a.lo - b.lo| + |a.hi - b.hi|).
+constexpr int kSmallWP16 = kSmallTile + 14;   // 2-pel words per staged row (c = tx + 4 bx + {0, 2})
+constexpr int kSmallRaw16 = 16;               // raw dwords per staged row (32 pels >= 1 + 31)
+
+template <bool FFS, bool HBD>
 __global__ __launch_bounds__(kWG) void me_small_kernel(SmallParams p) {
   constexpr int kRows = kSmallTile + 15;
-  __shared__ uint32_t s_w[kRows * kSmallWP];
-  __shared__ uint32_t s_raw[kRows * kSmallRaw];
-  __shared__ uint32_t s_cur[64];
+  constexpr int kWP = HBD ? kSmallWP16 : kSmallWP, kRaw = HBD ? kSmallRaw16 : kSmallRaw;
+  __shared__ uint32_t s_w[kRows * kWP];
+  __shared__ uint32_t s_raw[kRows * kRaw];
+  __shared__ uint32_t s_cur[HBD ? 128 : 64];
   __shared__ uint32_t s_cost[kWaves][kNS], s_rank[kWaves][kNS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int tpi = p.tiles * p.tiles;
@@ -1561,7 +1568,7 @@ __global__ __launch_bounds__(kWG) void me_small_kernel(SmallParams p) {
     if (tid < kNS && ((it.gmask >> tid) & 1)) part[tid] = ~0ull;
     return;
   }
-  {
+  if constexpr (!HBD) {
     const int X0 = it.mb_x + (it.cqx >> 2) + ox0, Y0 = it.mb_y + (it.cqy >> 2) + oy0;
     const int xa = X0 & ~3, sh = X0 - xa;
     for (int i = tid; i < kRows * kSmallRaw; i += kWG) {
@@ -1587,6 +1594,33 @@ __global__ __launch_bounds__(kWG) void me_small_kernel(SmallParams p) {
       s_w[i] = __builtin_amdgcn_alignbyte(s_raw[r * kSmallRaw + q + 1], s_raw[r * kSmallRaw + q], (sh + c) & 3);
     }
     __syncthreads();
+  } else {
+    // pitch in pels; word c of a staged row = pels (X0 + c, X0 + c + 1)
+    const int X0 = it.mb_x + (it.cqx >> 2) + ox0, Y0 = it.mb_y + (it.cqy >> 2) + oy0;
+    const int xa = X0 & ~1, sh = X0 - xa;
+    const uint16_t *ref16 = reinterpret_cast<const uint16_t *>(it.ref);
+    const uint16_t *cur16 = reinterpret_cast<const uint16_t *>(p.cur);
+    for (int i = tid; i < kRows * kSmallRaw16; i += kWG) {
+      const int r = i / kSmallRaw16, k = i - r * kSmallRaw16;
+      const uint16_t *row = ref16 + (size_t)clampi(Y0 + r, 0, p.height - 1) * p.pitch;
+      const int x = xa + 2 * k;
+      uint32_t w;
+      if (x >= 0 && x + 1 < p.width)
+        w = *reinterpret_cast<const uint32_t *>(row + x);
+      else
+        w = (uint32_t)row[clampi(x, 0, p.width - 1)] | ((uint32_t)row[clampi(x + 1, 0, p.width - 1)] << 16);
+      s_raw[i] = w;
+    }
+    if (tid < 128)
+      s_cur[tid] = *reinterpret_cast<const uint32_t *>(cur16 + (size_t)(it.mb_y + (tid >> 3)) * p.pitch + it.mb_x +
+                                                       2 * (tid & 7));
+    __syncthreads();
+    for (int i = tid; i < kRows * kSmallWP16; i += kWG) {
+      const int r = i / kSmallWP16, c = i - r * kSmallWP16, q = (sh + c) >> 1;
+      const uint32_t lo = s_raw[r * kSmallRaw16 + q];
+      s_w[i] = ((sh + c) & 1) ? __builtin_amdgcn_alignbyte(s_raw[r * kSmallRaw16 + q + 1], lo, 2) : lo;
+    }
+    __syncthreads();
   }
   const int tx = tid % kSmallTile, ty = tid / kSmallTile;
   const int ox = ox0 + tx, oy = oy0 + ty;
@@ -1597,8 +1631,16 @@ __global__ __launch_bounds__(kWG) void me_small_kernel(SmallParams p) {
     if ((it.bmask >> b) & 1) {
       const int by = b >> 2, bx = b & 3;
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        a[b] = __builtin_amdgcn_sad_u8(s_w[(ty + 4 * by + r) * kSmallWP + tx + 4 * bx], s_cur[(4 * by + r) * 4 + bx], a[b]);
+      for (int r = 0; r < 4; ++r) {
+        if constexpr (!HBD) {
+          a[b] = __builtin_amdgcn_sad_u8(s_w[(ty + 4 * by + r) * kSmallWP + tx + 4 * bx], s_cur[(4 * by + r) * 4 + bx],
+                                         a[b]);
+        } else {
+          const uint32_t *w = &s_w[(ty + 4 * by + r) * kSmallWP16 + tx + 4 * bx];
+          a[b] = __builtin_amdgcn_sad_u16(w[0], s_cur[(4 * by + r) * 8 + 2 * bx], a[b]);
+          a[b] = __builtin_amdgcn_sad_u16(w[2], s_cur[(4 * by + r) * 8 + 2 * bx + 1], a[b]);
+        }
+      }
     }
   }
   uint32_t ps[kNS];
@@ -1728,13 +1770,12 @@ hipError_t launch_search(const KParams &p, hipStream_t s, hipEvent_t ev0, hipEve
 hipError_t launch_search_small(const SmallParams &p, hipStream_t s) {
   if (p.n_items <= 0) return hipSuccess;
   const dim3 grid((unsigned)(p.n_items * p.tiles * p.tiles)), g2((unsigned)((p.n_items * kNS + kWG - 1) / kWG));
-  if (p.mode == JMME_FAST_FULL_SEARCH) {
-    hipLaunchKernelGGL(me_small_kernel<true>, grid, dim3(kWG), 0, s, p);
-    hipLaunchKernelGGL(small_finish_kernel<true>, g2, dim3(kWG), 0, s, p);
-  } else {
-    hipLaunchKernelGGL(me_small_kernel<false>, grid, dim3(kWG), 0, s, p);
-    hipLaunchKernelGGL(small_finish_kernel<false>, g2, dim3(kWG), 0, s, p);
-  }
+  const bool ffs = p.mode == JMME_FAST_FULL_SEARCH;
+  void (*search)(SmallParams) = p.hbd ? (ffs ? me_small_kernel<true, true> : me_small_kernel<false, true>)
+                                      : (ffs ? me_small_kernel<true, false> : me_small_kernel<false, false>);
+  void (*finish)(SmallParams) = ffs ? small_finish_kernel<true> : small_finish_kernel<false>;
+  hipLaunchKernelGGL(search, grid, dim3(kWG), 0, s, p);
+  hipLaunchKernelGGL(finish, g2, dim3(kWG), 0, s, p);
   return hipGetLastError();
 }
 

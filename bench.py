@@ -614,6 +614,12 @@ def main():
         if not args.no_dropin and ws == 1:
             import bench_blocks
             line["dropin"] = bench_blocks.dropin_block()
+            # EPZS (encoder_baseline.cfg's ME keys): one call per search, latency bound -- one P-frame
+            ep = bench_blocks.dropin_block(modes=((3, "EPZS"),), frames=2)
+            if line["dropin"] is not None and ep is not None:
+                line["dropin"]["EPZS"] = dict(ep["EPZS"], p_frames=1, note="one GPU call per EPZS search and per "
+                                              "EPZS sub-pel refinement (JM's predictor lists need the previous "
+                                              "search's answer); parity path, not a throughput path")
         print(json.dumps(line))
     me.close()
     if ws > 1:

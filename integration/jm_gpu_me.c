@@ -46,7 +46,9 @@ extern void __real_init_motion_search_module(VideoParameters *, InputParameters 
 extern void get_neighbors(Macroblock *currMB, PixelPos *block, int mb_x, int mb_y, int blockshape_x);
 
 static jmme_ctx *g_me = NULL;
+static int g_hbd = 0;   /* luma above 8 bits: sub-pel and EPZS stay on JM's CPU code (8-bit kernels) */
 static long long g_calls = 0, g_cpu_calls = 0;
+static FILE *g_trace = NULL, *g_trace_miss = NULL;   /* JMME_TRACE / JMME_TRACE_MISS */
 
 /* What the uploaded planes and every cached answer belong to.  frame_no alone
  * does not identify a coded picture: MVC view 1 shares view 0's frame_no with
@@ -103,7 +105,10 @@ static void init_once(VideoParameters *p_Vid, InputParameters *p_Inp)
   c.SetMVXLimit = p_Inp->SetMVXLimit;
   c.SetMVYLimit = p_Inp->SetMVYLimit;
   c.ChromaMEEnable = p_Inp->ChromaMEEnable;
-  c.SourceBitDepthLuma = p_Inp->source.bit_depth[0];
+  /* the luma depth of JM's imgpel planes (init_img, lencod.c:1115): above 8 the
+   * context keeps 16-bit planes and searches with v_sad_u16 */
+  c.SourceBitDepthLuma = p_Vid->bitdepth_luma > 0 ? p_Vid->bitdepth_luma : p_Inp->source.bit_depth[0];
+  g_hbd = c.SourceBitDepthLuma > 8;
   g_me = jmme_create(&c, -1);
   if (!g_me) fail_jm("jmme_create");
 }
@@ -112,6 +117,8 @@ static void init_once(VideoParameters *p_Vid, InputParameters *p_Inp)
  * lencod.c:606) builds JM's ME tables; the GPU engine is created there too, and
  * its one-time start-up (code-object loading, first-launch setup) is paid
  * before any frame is timed, like JM's own table setup */
+static void prefault_tables(VideoParameters *p_Vid, InputParameters *p_Inp);
+
 void __wrap_init_motion_search_module(VideoParameters *p_Vid, InputParameters *p_Inp)
 {
   __real_init_motion_search_module(p_Vid, p_Inp);
@@ -119,9 +126,12 @@ void __wrap_init_motion_search_module(VideoParameters *p_Vid, InputParameters *p
     init_once(p_Vid, p_Inp);
     if (jmme_prepare(g_me)) fail_jm("jmme_prepare");
   }
+  if (p_Inp->SearchMode[0] == FULL_SEARCH || p_Inp->SearchMode[0] == FAST_FULL_SEARCH) prefault_tables(p_Vid, p_Inp);
 }
 
 /* planes of the picture being coded and of the reference (list, ref) */
+static double g_t_planes = 0;   /* in jmme_upload_cur / _ref (reported when tracing) */
+static double now_us(void);
 static void ensure_planes(Macroblock *currMB, int list, int ref)
 {
   VideoParameters *p_Vid = currMB->p_Vid;
@@ -138,17 +148,21 @@ static void ensure_planes(Macroblock *currMB, int list, int ref)
       k.rd_pass != g_pic.rd_pass || k.cur != g_pic.cur) {   /* another coded picture: every slot is stale */
     g_pic = k;
     memset(g_ref_pic, 0, sizeof g_ref_pic);
+    double t0 = now_us();
     ++g_gen;
     if (jmme_upload_cur(g_me, (const jmme_imgpel *const *)p_Vid->pCurImg, p_Vid->width, p_Vid->height))
       fail_jm("jmme_upload_cur");
+    g_t_planes += now_us() - t0;
   }
   if (list < 0 || list > 1 || ref < 0 || ref >= 32) error("jm_gpu_me: reference index out of range", 500);
   pic = currSlice->listX[list + currMB->list_offset][ref];
   if (g_ref_pic[list][ref] != pic) {           /* first use, or the slot now names another picture */
+    double t0 = now_us();
     if (jmme_upload_ref(g_me, list, ref, (const jmme_imgpel *const *)pic->imgY, pic->size_x, pic->size_y))
       fail_jm("jmme_upload_ref");
     g_ref_pic[list][ref] = pic;
     g_slot_gen[list][ref] = ++g_gen;
+    g_t_planes += now_us() - t0;
   }
 }
 
@@ -200,7 +214,7 @@ typedef struct spec_ent {
   int32_t lambda;
   int16_t mvx, mvy;
   int64_t cost;
-  int8_t valid;
+  uint32_t valid;                        /* the g_slot_gen it was cached in (0: none) */
 } spec_ent;
 
 #define KHYP 4                     /* guesses per (macroblock, partition) */
@@ -220,7 +234,6 @@ static int g_req_cap = 0;
  * misses past the batch's end vs inside it (a guess failed), per slot */
 static long long g_miss_past = 0, g_miss_guess = 0, g_miss_slot[JMME_NSLOT], g_units = 0;
 static double g_t_build = 0, g_t_call = 0, g_t_wrap = 0;
-static FILE *g_trace = NULL;
 
 static double now_us(void)
 {
@@ -231,7 +244,6 @@ static double now_us(void)
 
 static spec_ent *spec_table(VideoParameters *p_Vid, int list, int ref)
 {
-  int i;
   if (!g_n_mb) {
     g_mbs_x = p_Vid->width / 16;
     g_n_mb = g_mbs_x * (p_Vid->height / 16);
@@ -242,9 +254,7 @@ static spec_ent *spec_table(VideoParameters *p_Vid, int list, int ref)
     if (!g_spec[list][ref] || !g_seen[list][ref]) error("jm_gpu_me: out of memory", 500);
     g_spec_gen[list][ref] = 0;
   }
-  if (g_spec_gen[list][ref] != g_slot_gen[list][ref]) {   /* other planes: forget every guess */
-    for (i = 0; i < g_n_mb * JMME_NSLOT * KHYP; i++) g_spec[list][ref][i].valid = 0;
-    for (i = 0; i < g_n_mb * JMME_NSLOT; i++) g_seen[list][ref][i].valid = 0;
+  if (g_spec_gen[list][ref] != g_slot_gen[list][ref]) {   /* other planes: every guess is stale (its stamp) */
     g_spec_gen[list][ref] = g_slot_gen[list][ref];
     g_spec_end[list][ref] = 0;
   }
@@ -258,7 +268,7 @@ static int spec_key_eq(const spec_ent *e, const spec_ent *w)
          e->lambda == w->lambda;
 }
 
-static int spec_same(const spec_ent *e, const spec_ent *w) { return e->valid && spec_key_eq(e, w); }
+static int spec_same(const spec_ent *e, const spec_ent *w, unsigned gen) { return e->valid == gen && spec_key_eq(e, w); }
 
 /* Guess h for the 41 partitions of macroblock mb, the search having missed at
  * macroblock mb0 (mb >= mb0) with inputs `want`:
@@ -278,7 +288,7 @@ static int spec_hyp(int list, int ref, int h, int mb0, int mb, const spec_ent *w
   if (h == 3 && mb > mb0) fmb = mb0;
   for (s = 0; s < JMME_NSLOT; s++) {
     src = fmb >= 0 ? &seen[(size_t)fmb * JMME_NSLOT + s] : NULL;
-    if (src && src->valid && src->mode == want->mode) {
+    if (src && src->valid == g_slot_gen[list][ref] && src->mode == want->mode) {
       out[s] = *src;
       any = 1;
     } else {
@@ -368,7 +378,7 @@ static void spec_batch(int list, int ref, int mb0, const spec_ent *want, int chk
       e->mvx = g_res[i * JMME_NSLOT + s].mv_x;
       e->mvy = g_res[i * JMME_NSLOT + s].mv_y;
       e->cost = g_res[i * JMME_NSLOT + s].cost;
-      e->valid = 1;
+      e->valid = g_slot_gen[list][ref];
     }
     if (i + 1 == nreq || g_req_mb[i + 1] != mb)               /* drop older guesses of this MB */
       for (s = 0; s < JMME_NSLOT; s++)
@@ -384,6 +394,8 @@ static int speculating(void)
     const char *e = getenv("JMME_SPECULATE"), *t = getenv("JMME_TRACE");
     g_speculate = !(e && e[0] == '0');
     if (t && *t) g_trace = fopen(t, "w");     /* per batch: mb0 n units build_us call_us */
+    t = getenv("JMME_TRACE_MISS");
+    if (t && *t) g_trace_miss = fopen(t, "w");
   }
   return g_speculate;
 }
@@ -398,10 +410,10 @@ static const spec_ent *spec_lookup(Macroblock *currMB, MEBlock *mv_block, int li
   spec_ent *tab = spec_table(p_Vid, list, ref), *e;
   if (s < 0 || mb < 0 || mb >= g_n_mb) error("jm_gpu_me: block outside the picture", 500);
   g_seen[list][ref][(size_t)mb * JMME_NSLOT + s] = *want;
-  g_seen[list][ref][(size_t)mb * JMME_NSLOT + s].valid = 1;
+  g_seen[list][ref][(size_t)mb * JMME_NSLOT + s].valid = g_slot_gen[list][ref];
   e = &tab[((size_t)mb * JMME_NSLOT + s) * KHYP];
   for (k = 0; k < KHYP; k++)
-    if (spec_same(&e[k], want)) {
+    if (spec_same(&e[k], want, g_slot_gen[list][ref])) {
       ++g_hits;
       return &e[k];
     }
@@ -409,12 +421,21 @@ static const spec_ent *spec_lookup(Macroblock *currMB, MEBlock *mv_block, int li
     g_batch = imax(1, g_batch / 2);
     ++g_miss_guess;
     ++g_miss_slot[s];
+    if (g_trace_miss) {   /* JMME_TRACE_MISS: the inputs that missed and the guesses held for them */
+      fprintf(g_trace_miss, "miss mb %d slot %d want c(%d,%d) p(%d,%d) sr %d chk %d lam %d |", mb, s, want->cx, want->cy,
+              want->px, want->py, want->sr, want->chk, want->lambda);
+      for (k = 0; k < KHYP; k++)
+        if (e[k].valid == g_slot_gen[list][ref])
+          fprintf(g_trace_miss, " g%d c(%d,%d) p(%d,%d) sr %d chk %d lam %d", k, e[k].cx, e[k].cy, e[k].px, e[k].py,
+                  e[k].sr, e[k].chk, e[k].lambda);
+      fprintf(g_trace_miss, "\n");
+    }
   } else {                                                               /* ran past the batch */
     g_batch = imin(2048, g_batch * 2);
     ++g_miss_past;
   }
   spec_batch(list, ref, mb, want, chk_rule, currMB->p_Inp->rdopt);
-  if (!spec_same(&e[0], want)) error("jm_gpu_me: batch lost its own request", 500);
+  if (!spec_same(&e[0], want, g_slot_gen[list][ref])) error("jm_gpu_me: batch lost its own request", 500);
   return &e[0];
 }
 
@@ -547,7 +568,8 @@ typedef struct sp_ent {
   int16_t px, py, mx, my;
   int64_t min_mcost;
   int32_t lam_h, lam_q;
-  uint8_t metric_h, metric_q, start_hp, start_qp, pos2, pos4, flags, valid;
+  uint8_t metric_h, metric_q, start_hp, start_qp, pos2, pos4, flags;
+  uint32_t valid;                             /* the g_slot_gen it was cached in (0: none) */
   int16_t omx, omy;
   int64_t cost;
 } sp_ent;
@@ -568,9 +590,9 @@ static int metric_id(distblk (*f)(StorablePicture *, MEBlock *, distblk, MotionV
   return -1;                                  /* weighted / on-the-fly: stays on the CPU */
 }
 
-static int sp_same(const sp_ent *e, const sp_ent *w)
+static int sp_same(const sp_ent *e, const sp_ent *w, unsigned gen)
 {
-  return e->valid && e->px == w->px && e->py == w->py && e->mx == w->mx && e->my == w->my &&
+  return e->valid == gen && e->px == w->px && e->py == w->py && e->mx == w->mx && e->my == w->my &&
          e->min_mcost == w->min_mcost && e->lam_h == w->lam_h && e->lam_q == w->lam_q &&
          e->metric_h == w->metric_h && e->metric_q == w->metric_q && e->start_hp == w->start_hp &&
          e->start_qp == w->start_qp && e->pos2 == w->pos2 && e->pos4 == w->pos4 && e->flags == w->flags;
@@ -642,7 +664,7 @@ static void sp_batch(int list, int ref, int mb0, int s0, const sp_ent *w, int t8
       for (k = 0; k < KHYP; k++) {
         const spec_ent *ie = &itab[((size_t)mb * JMME_NSLOT + s) * KHYP + k];
         sp_ent g = *w;
-        if (!ie->valid) continue;
+        if (ie->valid != g_slot_gen[list][ref]) continue;
         g.px = ie->px;
         g.py = ie->py;
         g.mx = ie->mvx;
@@ -662,9 +684,36 @@ static void sp_batch(int list, int ref, int mb0, int s0, const sp_ent *w, int t8
     e->metric_h = q->metric_h; e->metric_q = q->metric_q; e->start_hp = q->start_hp; e->start_qp = q->start_qp;
     e->pos2 = q->search_pos2; e->pos4 = q->search_pos4; e->flags = q->flags;
     e->omx = g_sres[i].mv_x; e->omy = g_sres[i].mv_y; e->cost = g_sres[i].cost;
-    e->valid = 1;
+    e->valid = g_slot_gen[list][ref];
   }
   ++g_sp_batches;
+}
+
+static sp_ent *sp_table(VideoParameters *p_Vid, int list, int ref)
+{
+  spec_table(p_Vid, list, ref);                       /* sizes and per-picture reset of the integer table */
+  if (!g_sp[list][ref]) {
+    size_t n = (size_t)g_n_mb * JMME_NSLOT * SPK;
+    g_sp[list][ref] = (sp_ent *)malloc(n * sizeof(sp_ent));
+    if (!g_sp[list][ref]) error("jm_gpu_me: out of memory", 500);
+    memset(g_sp[list][ref], 0, n * sizeof(sp_ent));
+    g_sp_gen[list][ref] = 0;
+  }
+  if (g_sp_gen[list][ref] != g_slot_gen[list][ref])   /* other planes: every entry is stale (its stamp) */
+    g_sp_gen[list][ref] = g_slot_gen[list][ref];
+  return g_sp[list][ref];
+}
+
+/* The speculative caches of (list 0, ref 0) -- tens of MB at 1080p -- are
+ * allocated and touched at encoder start-up, so the first P picture does not
+ * pay their page faults inside JM's ME timer. */
+static void prefault_tables(VideoParameters *p_Vid, InputParameters *p_Inp)
+{
+  if (p_Vid->width <= 0 || p_Vid->height <= 0) return;
+  spec_table(p_Vid, 0, 0);
+  memset(g_spec[0][0], 0, (size_t)g_n_mb * JMME_NSLOT * KHYP * sizeof(spec_ent));
+  memset(g_seen[0][0], 0, (size_t)g_n_mb * JMME_NSLOT * sizeof(spec_ent));
+  if (!p_Inp->DisableSubpelME[0]) sp_table(p_Vid, 0, 0);
 }
 
 /* sub_pel_motion_estimation's contract (me_fullsearch.c:186-289) */
@@ -681,7 +730,7 @@ distblk __wrap_sub_pel_motion_estimation(Macroblock *currMB, MotionVector *pred_
   int mode = currMB->p_Inp->SearchMode[p_Vid->view_id];
   /* GPU sub-pel follows a GPU integer search (FS / FFS); UMHEX's direct calls and
    * weighted / chroma metrics stay on the CPU */
-  if (!speculating() || (mode != FULL_SEARCH && mode != FAST_FULL_SEARCH) || mh < 0 || mq < 0 ||
+  if (!speculating() || g_hbd || (mode != FULL_SEARCH && mode != FAST_FULL_SEARCH) || mh < 0 || mq < 0 ||
       mv_block->ChromaMEEnable || mv_block->search_pos2 > 9 || mv_block->search_pos4 > 9 ||
       (mv_block->test8x8 && mv_block->blocktype > 4)) {
     ++g_sp_cpu;
@@ -699,29 +748,19 @@ distblk __wrap_sub_pel_motion_estimation(Macroblock *currMB, MotionVector *pred_
   want.pos2 = (uint8_t)mv_block->search_pos2; want.pos4 = (uint8_t)mv_block->search_pos4;
   want.flags = (uint8_t)((mv_block->test8x8 ? JMME_SP_TEST8x8 : 0) |
                          ((!currMB->p_Inp->rdopt && currSlice->slice_type != B_SLICE) ? JMME_SP_CHECK0 : 0));
-  spec_table(p_Vid, list, ref);                       /* sizes and per-picture reset of the integer table */
-  if (!g_sp[list][ref]) {
-    g_sp[list][ref] = (sp_ent *)calloc((size_t)g_n_mb * JMME_NSLOT * SPK, sizeof(sp_ent));
-    if (!g_sp[list][ref]) error("jm_gpu_me: out of memory", 500);
-    g_sp_gen[list][ref] = 0;
-  }
-  tab = g_sp[list][ref];
-  if (g_sp_gen[list][ref] != g_slot_gen[list][ref]) {
-    for (i = 0; i < g_n_mb * JMME_NSLOT * SPK; i++) tab[i].valid = 0;
-    g_sp_gen[list][ref] = g_slot_gen[list][ref];
-  }
+  tab = sp_table(p_Vid, list, ref);
   mb = (mv_block->pos_y >> 4) * g_mbs_x + (mv_block->pos_x >> 4);
   s = jmme_slot(mv_block->blocktype, (mv_block->pos_x & 15) >> 2, (mv_block->pos_y & 15) >> 2);
   if (s < 0 || mb < 0 || mb >= g_n_mb) error("jm_gpu_me: block outside the picture", 500);
   e = &tab[((size_t)mb * JMME_NSLOT + s) * SPK];
-  for (i = 0; i < SPK && !sp_same(&e[i], &want); i++) {}
+  for (i = 0; i < SPK && !sp_same(&e[i], &want, g_slot_gen[list][ref]); i++) {}
   if (i < SPK) {
     ++g_sp_hits;
     e += i;
   } else {
     sp_batch(list, ref, mb, s, &want, currMB->p_Inp->Transform8x8Mode != 0);
     e += KHYP;
-    if (!sp_same(e, &want)) error("jm_gpu_me: sub-pel batch lost its own request", 500);
+    if (!sp_same(e, &want, g_slot_gen[list][ref])) error("jm_gpu_me: sub-pel batch lost its own request", 500);
   }
   mv_block->mv[list].mv_x = e->omx;
   mv_block->mv[list].mv_y = e->omy;
@@ -935,7 +974,8 @@ static distblk epzs_gpu(int variant, Macroblock *currMB, MotionVector *pred_mv, 
   jmme_epzs_req q;
   jmme_epzs_res res;
   double t0, t1;
-  if (fs_on_cpu(mv_block) || 2 * max_x + 1 > side || 2 * max_y + 1 > side) {
+  init_once(currMB->p_Vid, p_Inp);
+  if (g_hbd || fs_on_cpu(mv_block) || 2 * max_x + 1 > side || 2 * max_y + 1 > side) {
     ++g_epzs_cpu;
     return real_epzs(variant, currMB, pred_mv, mv_block, min_mcost, lambda_factor);
   }
@@ -1084,7 +1124,8 @@ distblk __wrap_EPZS_sub_pel_motion_estimation(Macroblock *currMB, MotionVector *
   int mh = metric_id(mv_block->computePredHPel), mq = metric_id(mv_block->computePredQPel);
   jmme_subpel_req q;
   jmme_block_res r;
-  if (mh < 0 || mq < 0 || mv_block->ChromaMEEnable || mv_block->search_pos2 > 9 || mv_block->search_pos4 > 9 ||
+  init_once(p_Vid, currMB->p_Inp);
+  if (g_hbd || mh < 0 || mq < 0 || mv_block->ChromaMEEnable || mv_block->search_pos2 > 9 || mv_block->search_pos4 > 9 ||
       (mv_block->test8x8 && mv_block->blocktype > 4)) {
     ++g_epzs_sp_cpu;
     return __real_EPZS_sub_pel_motion_estimation(currMB, pred_mv, mv_block, min_mcost, lambda_factor);
@@ -1134,7 +1175,9 @@ static void report(void)
       fprintf(stderr, "jm_gpu_me: integer batches: %lld past the batch, %lld failed guesses; %lld units; "
                       "%.1f ms building, %.1f ms in jmme_search_mbs; failed guesses by slot:",
               g_miss_past, g_miss_guess, g_units, g_t_build * 1e-3, g_t_call * 1e-3);
-      if (g_trace) fprintf(stderr, " [%.1f ms inside the FS wrapper]", g_t_wrap * 1e-3);
+      if (g_trace)
+        fprintf(stderr, " [%.1f ms inside the FS wrapper, %.1f ms uploading planes]", g_t_wrap * 1e-3,
+                g_t_planes * 1e-3);
       for (s = 0; s < JMME_NSLOT; s++) fprintf(stderr, " %lld", g_miss_slot[s]);
       fprintf(stderr, "\n");
     }
@@ -1148,6 +1191,7 @@ static void report(void)
       fprintf(stderr, "jm_gpu_me: %lld EPZS sub-pel refinements on the GPU, %lld on the CPU\n", g_epzs_sp_calls,
               g_epzs_sp_cpu);
     if (g_trace) fclose(g_trace);
+    if (g_trace_miss) fclose(g_trace_miss);
     if (g_me) jmme_destroy(g_me);
   }
 }

@@ -1,0 +1,54 @@
+"""GPU: the drop-in at high bit depth.  A 10-bit High 10 encode (ProfileIDC 110,
+SourceBitDepthLuma / OutputBitDepthLuma 10: JM keeps 10-bit samples in its
+uint16 imgpel planes, JM/lencod/inc/defines.h:37) through lencod_jmme -- the
+integer-pel full / fast full searches on the GPU's 16-bit path (v_sad_u16),
+sub-pel refinement on JM's own code -- must be byte-identical to the stock
+lencod, with no integer-pel search left on the CPU."""
+import os
+import re
+import tempfile
+
+import numpy as np
+import pytest
+
+from test_jm_dropin_gpu import GPU, STOCK, _encode
+
+pytestmark = pytest.mark.gpu
+
+
+def write_yuv420_16(path, luma, bits):
+    """planar I420, 16-bit little-endian samples (JM reads 2 bytes per sample
+    when the source depth is above 8); chroma mid-grey"""
+    f, h, w = luma.shape
+    grey = np.full((h // 2, w // 2), 1 << (bits - 1), np.uint16)
+    with open(path, "wb") as fp:
+        for t in range(f):
+            fp.write(luma[t].astype("<u2").tobytes())
+            fp.write(grey.astype("<u2").tobytes())
+            fp.write(grey.astype("<u2").tobytes())
+
+
+@pytest.mark.parametrize("w,h,frames,params", [
+    (176, 144, 3, {"SearchMode": -1, "SearchRange": 16, "RDOptimization": 0, "NumberReferenceFrames": 1}),
+    (176, 144, 4, {"SearchMode": 0, "SearchRange": 16, "RDOptimization": 1, "NumberReferenceFrames": 2}),
+    (352, 288, 3, {"SearchMode": -1, "SearchRange": 32, "RDOptimization": 1, "NumberReferenceFrames": 2,
+                   "DisableSubpelME": 0, "MEDistortionQPel": 2, "MDDistortion": 2}),
+])
+def test_lencod_10bit_is_byte_identical(gpu, w, h, frames, params):
+    if not (os.path.exists(STOCK) and os.path.exists(GPU)):
+        pytest.fail("lencod builds missing: run `make -C oracle ref && make -C integration` in the build container")
+    from jmme import synth
+    bits = 10
+    p = dict(params, ProfileIDC=110, SourceBitDepthLuma=bits, SourceBitDepthChroma=bits, OutputBitDepthLuma=bits,
+             OutputBitDepthChroma=bits)
+    with tempfile.TemporaryDirectory() as d:
+        yuv = os.path.join(d, "in.yuv")
+        luma = synth.luma_sequence(w, h, frames, seed=w + 3 * frames, gmv=(3, -2)).astype(np.int32)
+        rng = np.random.default_rng(frames)
+        luma10 = np.clip((luma << 2) + rng.integers(0, 4, size=luma.shape), 0, 1023).astype(np.uint16)
+        write_yuv420_16(yuv, luma10, bits)
+        ref264, refrec, _ = _encode(STOCK, d, "cpu", yuv, w, h, frames, p)
+        gpu264, gpurec, r = _encode(GPU, d, "gpu", yuv, w, h, frames, p)
+        assert (gpu264, gpurec) == (ref264, refrec), r.stderr[-800:]
+        m = re.search(r"(\d+) integer-pel searches on the GPU .*; (\d+) on the CPU", r.stderr)
+        assert m and int(m.group(1)) > 0 and int(m.group(2)) == 0, r.stderr[-800:]

@@ -178,6 +178,10 @@ def _lencod(binary, d, tag, yuv, w, h, frames, params, cfg_text, env=None):
     stats = re.search(r"integer batches: (\d+) past the batch, (\d+) failed guesses; (\d+) units; ([0-9.]+) ms building, "
                       r"([0-9.]+) ms in jmme_search_mbs", r.stderr)
     sp = re.search(r"(\d+) sub-pel refinements: (\d+) cached, (\d+) batches, (\d+) on the CPU", r.stderr)
+    ep = re.search(r"(\d+) EPZS searches on the GPU \(libjmme\), one call each; (\d+) on the CPU; (\d+) predictors, "
+                   r"(\d+) pre-stamped map cells, (\d+) switches to window scans; ([\d.]+) ms in the EPZS wrapper, "
+                   r"([\d.]+) ms in jmme_epzs_search_ex", r.stderr)
+    esp = re.search(r"(\d+) EPZS sub-pel refinements on the GPU, (\d+) on the CPU", r.stderr)
     res = dict(wall_s=round(wall, 3), me_s=float(me.group(1)) if me else None,
                md5=(hashlib.md5(open(out, "rb").read()).hexdigest(), hashlib.md5(open(rec, "rb").read()).hexdigest()))
     if calls:
@@ -189,6 +193,14 @@ def _lencod(binary, d, tag, yuv, w, h, frames, params, cfg_text, env=None):
                    engine_call_ms=float(stats.group(5)))
     if sp:
         res["subpel"] = dict(zip(("calls", "cached", "batches", "cpu"), map(int, sp.groups())))
+    if ep:
+        g = ep.groups()
+        res["epzs"] = dict(gpu_searches=int(g[0]), cpu_searches=int(g[1]), predictors=int(g[2]),
+                           pre_stamped_cells=int(g[3]), window_scan_switches=int(g[4]), wrapper_ms=float(g[5]),
+                           engine_call_ms=float(g[6]),
+                           us_per_search=round(float(g[5]) * 1e3 / max(1, int(g[0])), 2))
+    if esp:
+        res["epzs_subpel"] = dict(gpu=int(esp.group(1)), cpu=int(esp.group(2)))
     return res
 
 
@@ -203,6 +215,7 @@ def dropin_block(modes=((-1, "FS"), (0, "FFS")), size=(1920, 1080), frames=3, se
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     stock = os.path.join(repo, "oracle", "_ref", "lencod")
     gpu = os.path.join(repo, "integration", "_build", "lencod_jmme")
+    floor = os.path.join(repo, "integration", "_build", "lencod_noop_me")
     if not (os.path.exists(stock) and os.path.exists(gpu)):
         return None
     from jmme import synth
@@ -218,15 +231,22 @@ def dropin_block(modes=((-1, "FS"), (0, "FFS")), size=(1920, 1080), frames=3, se
         for mode, tag in modes:
             params = {"SearchMode": mode, "SearchRange": search_range, "RDOptimization": 0,
                       "NumberReferenceFrames": 1}
+            if mode == 3:   # EPZS: encoder_baseline.cfg's ME keys (RDO on, SATD sub-pel, EPZSSubPelGrid 1)
+                from test_jm_dropin_epzs_gpu import BASELINE_EPZS
+                params = dict(BASELINE_EPZS, SearchRange=search_range, NumberReferenceFrames=1)
             cpu = _lencod(stock, d, f"cpu{mode}", yuv, w, h, frames, params, CFG)
             g = _lencod(gpu, d, f"gpu{mode}", yuv, w, h, frames, params, CFG)
             p = frames - 1
+            # JM's own loop around the search (integration/jm_noop_me.c: a zero-cost IntPelME)
+            fl = _lencod(floor, d, f"floor{mode}", yuv, w, h, frames, params, CFG) \
+                if mode in (-1, 0) and os.path.exists(floor) else None
             out[tag] = {
                 "stock_me_ms_per_p_frame": round(cpu["me_s"] * 1e3 / p, 2),
                 "dropin_me_ms_per_p_frame": round(g["me_s"] * 1e3 / p, 2),
                 "me_speedup": round(cpu["me_s"] / g["me_s"], 2) if g["me_s"] else None,
                 "dropin_mb_per_s": round(out["p_frame_macroblocks"] * p / g["me_s"], 1) if g["me_s"] else None,
-                "byte_identical": cpu["md5"] == g["md5"],
+                "byte_identical": cpu["md5"] == g["md5"], "params": params,
+                "jm_loop_floor_ms_per_p_frame": round(fl["me_s"] * 1e3 / p, 2) if fl and fl["me_s"] else None,
                 "stock_wall_s": cpu["wall_s"], "dropin_wall_s": g["wall_s"],
                 "dropin": {k: v for k, v in g.items() if k not in ("md5", "me_s", "wall_s")}}
     return out

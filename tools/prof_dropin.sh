@@ -20,6 +20,15 @@ args="-d $d/enc.cfg -p InputFile=$d/in.yuv -p SourceWidth=1920 -p SourceHeight=1
  -p OutputHeight=1080 -p FramesToBeEncoded=2 -p OutputFile=$d/o.264 -p ReconFile=$d/r.yuv -p SearchMode=${MODE:--1}
  -p SearchRange=32 -p RDOptimization=0 -p NumberReferenceFrames=1"
 if [ "${SUBPEL:-1}" = 1 ]; then args="$args -p DisableSubpelME=0 -p MEDistortionQPel=2 -p MDDistortion=2"; fi
+# MODE=3: EPZS with encoder_baseline.cfg's ME keys (tests/test_jm_dropin_epzs_gpu.py BASELINE_EPZS)
+if [ "${MODE:--1}" = 3 ]; then
+  args="$args $(python3 -c 'import sys; sys.path.insert(0, "tests"); sys.path.insert(0, "--h.264-by-zhaodongyu_amd")
+from test_jm_dropin_epzs_gpu import BASELINE_EPZS as b
+print(" ".join(f"-p {k}={v}" for k, v in b.items() if k not in ("SearchRange",)))')"
+fi
+args="$args ${EXTRA:-}"
 timeout -k 10 300 rocprofv3 --kernel-trace --runtime-trace --stats --output-format csv -d $out -o run -- \
   "$PWD/integration/_build/lencod_jmme" $args > $out/lencod.log 2>&1
+# keep the summaries (the per-dispatch traces of a 1080p encode run to hundreds of MB)
+find $out -name "*.csv" ! -name "*stats.csv" -delete
 find $out -name "*stats.csv" | head

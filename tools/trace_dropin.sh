@@ -1,0 +1,23 @@
+#!/bin/bash
+# The drop-in encoder (1080p, 2 frames, FS by default: MODE) with its speculation
+# traced: per batch (JMME_TRACE) and per failed guess (JMME_TRACE_MISS).  GPU box.
+set -e
+cd "$(dirname "$0")/.."
+out=gpurun_out/${OUT:-trace_dropin}
+mkdir -p $out
+d=$(mktemp -d)
+python3 - "$d" <<'PY'
+import os, sys
+sys.path.insert(0, "--h.264-by-zhaodongyu_amd"); sys.path.insert(0, "tests")
+from jmme import synth
+from test_jm_dropin_gpu import CFG
+d = sys.argv[1]
+synth.write_yuv420(os.path.join(d, "in.yuv"), synth.luma_sequence(1920, 1080, 2, seed=2024, gmv=(5, 3)))
+open(os.path.join(d, "enc.cfg"), "w").write(CFG)
+PY
+JMME_TRACE=$PWD/$out/batches.txt JMME_TRACE_MISS=$PWD/$out/misses.txt timeout -k 10 300 \
+  "$PWD/integration/_build/lencod_jmme" -d $d/enc.cfg -p InputFile=$d/in.yuv -p SourceWidth=1920 -p SourceHeight=1080 \
+  -p OutputWidth=1920 -p OutputHeight=1080 -p FramesToBeEncoded=2 -p OutputFile=$d/o.264 -p ReconFile=$d/r.yuv \
+  -p SearchMode=${MODE:--1} -p SearchRange=32 -p RDOptimization=0 -p NumberReferenceFrames=1 ${EXTRA:-} \
+  > $out/lencod.log 2>&1
+rm -rf "$d"
