@@ -104,6 +104,8 @@ struct jmme_ctx {
   size_t cap_sitems = 0;
   jmme_block_res *h_sout = nullptr;
   size_t cap_sout = 0;
+  unsigned long long *h_hkeys = nullptr;    // small latency form: per-tile keys (mapped pinned)
+  size_t cap_hkeys = 0;
   uint8_t *h_emap = nullptr;                 // jmme_epzs_search_ex: mapped pinned request / result block
   size_t cap_emap = 0;
   unsigned long long *d_skeys = nullptr;     // per (item, tile) keys, cap_skeys * JMME_NSLOT
@@ -312,6 +314,7 @@ extern "C" void jmme_destroy(jmme_ctx *ctx) {
   if (ctx->h_sitems) (void)hipHostFree(ctx->h_sitems);
   if (ctx->h_sout) (void)hipHostFree(ctx->h_sout);
   if (ctx->h_emap) (void)hipHostFree(ctx->h_emap);
+  if (ctx->h_hkeys) (void)hipHostFree(ctx->h_hkeys);
   (void)hipFree(ctx->d_skeys);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
@@ -639,7 +642,6 @@ int search_small(jmme_ctx *ctx, int mode, const jmme_mb_req *req, int n, jmme_bl
     HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_sout), cap * sizeof(jmme_block_res), hipHostMallocMapped));
     ctx->cap_sout = cap;
   }
-  std::memcpy(ctx->h_sitems, items.data(), items.size() * sizeof(SmallItem));
   SmallParams p{};
   p.cur = ctx->d_cur;
   p.pitch = ctx->pitch;
@@ -648,12 +650,67 @@ int search_small(jmme_ctx *ctx, int mode, const jmme_mb_req *req, int n, jmme_bl
   p.mode = mode;
   p.max_mvd = ctx->max_mvd;
   p.hbd = ctx->hbd ? 1 : 0;
-  void *d_items = nullptr, *d_sout = nullptr;
+  p.n_items = (int)items.size();
+  p.tiles = tiles;
+  const int tpi = tiles * tiles;
+  // Up to kSmallInline items travel in the kernel arguments (no read of host
+  // memory before the first load).  Latency form for a few items: the per-tile
+  // keys go to mapped host memory and the minimum over tiles is taken here (one
+  // launch); past kHostFinishItems the host's reads of those keys cost more
+  // than the finish launch (tools/ubench_small.py: 1 unit 35.1 -> 30.2 us,
+  // 8 units 37.6 -> 48.6 us).
+  constexpr size_t kHostFinishItems = 4;
+  const bool lat = items.size() <= kHostFinishItems;
+  p.n_inline = (int)std::min(items.size(), (size_t)kSmallInline);
+  std::memcpy(p.inl, items.data(), (size_t)p.n_inline * sizeof(SmallItem));
+  void *d_items = nullptr, *d_sout = nullptr, *d_hkeys = nullptr;
+  if (lat) {
+    const size_t nk = (size_t)wgs * JMME_NSLOT;
+    if (nk > ctx->cap_hkeys) {
+      if (ctx->h_hkeys) (void)hipHostFree(ctx->h_hkeys);
+      ctx->h_hkeys = nullptr;
+      ctx->cap_hkeys = 0;
+      const size_t cap = std::max<size_t>(64 * 1024, nk);
+      HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_hkeys), cap * sizeof(unsigned long long),
+                           hipHostMallocMapped));
+      ctx->cap_hkeys = cap;
+    }
+    HIPCHK(hipHostGetDevicePointer(&d_hkeys, ctx->h_hkeys, 0));
+    p.host_finish = 1;
+    p.keys = static_cast<unsigned long long *>(d_hkeys);
+    HIPCHK(launch_search_small(p, s));
+    HIPCHK(hipStreamSynchronize(s));
+    ctx->timed = false;
+    const bool ffs = mode == JMME_FAST_FULL_SEARCH;
+    for (size_t ii = 0; ii < items.size(); ++ii) {
+      const SmallItem &it = items[ii];
+      const unsigned long long *k0 = ctx->h_hkeys + ii * tpi * JMME_NSLOT;
+      for (uint64_t m = it.gmask; m; m &= m - 1) {
+        const int sl = __builtin_ctzll(m);
+        unsigned long long k = ~0ull;
+        for (int t = 0; t < tpi; ++t) k = std::min(k, k0[(size_t)t * JMME_NSLOT + sl]);
+        // block_result (jmme_search.hip): the winning spiral rank -> vector
+        jmme_block_res &r = out[(size_t)it.u * JMME_NSLOT + sl];
+        r.reserved = 0;
+        if (k == ~0ull) {
+          r.mv_x = it.cqx; r.mv_y = it.cqy; r.cost = JMME_DISTBLK_MAX;
+          continue;
+        }
+        const int rank = (int)(uint32_t)(k & 0xffffffffu);
+        int ox, oy;
+        if (ffs && rank == 0) { ox = -(it.cqx >> 2); oy = -(it.cqy >> 2); }   // the pre-seeded (0,0)
+        else spiral_offset(ffs ? rank - 1 : rank, &ox, &oy);
+        r.mv_x = (int16_t)(it.cqx + 4 * ox);
+        r.mv_y = (int16_t)(it.cqy + 4 * oy);
+        r.cost = (int64_t)(k >> 32);
+      }
+    }
+    return 1;
+  }
+  std::memcpy(ctx->h_sitems, items.data(), items.size() * sizeof(SmallItem));
   HIPCHK(hipHostGetDevicePointer(&d_items, ctx->h_sitems, 0));
   HIPCHK(hipHostGetDevicePointer(&d_sout, ctx->h_sout, 0));
   p.items = static_cast<const SmallItem *>(d_items);
-  p.n_items = (int)items.size();
-  p.tiles = tiles;
   p.keys = ctx->d_skeys;
   p.info = reinterpret_cast<int4 *>(ctx->d_skeys + ctx->cap_skeys * JMME_NSLOT);   // items <= workgroups <= cap
   p.out = static_cast<jmme_block_res *>(d_sout);

@@ -81,6 +81,8 @@ struct SmallItem {
 };
 static_assert(sizeof(SmallItem) == 48, "SmallItem layout");
 
+constexpr int kSmallInline = 32;   // items a small launch carries in its kernel arguments
+
 struct SmallParams {
   const uint8_t *cur;
   int pitch, width, height;           // pitch in pels (16-bit pels when hbd)
@@ -89,9 +91,15 @@ struct SmallParams {
   const SmallItem *items;             // n_items (device-readable: host-mapped pinned memory)
   int n_items;
   int tiles;                          // tiles per item side: ceil((2 * max R + 1) / 16)
-  unsigned long long *keys;           // [n_items][tiles^2][JMME_NSLOT] per-tile keys (device memory)
+  unsigned long long *keys;           // [n_items][tiles^2][JMME_NSLOT] per-tile keys
   int4 *info;                         // [n_items] gmask lo/hi, centre, unit, for the finish launch (device memory)
   jmme_block_res *out;                // [units * JMME_NSLOT] (host-mapped); only searched slots written
+  // latency form: the first n_inline items travel in the kernel arguments (no
+  // read of host memory before the first load), the per-tile keys go straight
+  // to host-mapped memory and the host takes the minimum over tiles (no finish launch)
+  int host_finish;
+  int n_inline;
+  SmallItem inl[kSmallInline];
 };
 constexpr int kSmallTile = 16;
 hipError_t launch_search_small(const SmallParams &p, hipStream_t s);

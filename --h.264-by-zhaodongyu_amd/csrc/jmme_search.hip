@@ -1556,13 +1556,13 @@ __global__ __launch_bounds__(kWG) void me_small_kernel(SmallParams p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int tpi = p.tiles * p.tiles;
   const int ii = blockIdx.x / tpi, t = blockIdx.x - ii * tpi;
-  const SmallItem it = p.items[ii];
+  const SmallItem it = ii < p.n_inline ? p.inl[ii] : p.items[ii];
   const int R = it.R;
   const int ox0 = -R + kSmallTile * (t % p.tiles), oy0 = -R + kSmallTile * (t / p.tiles);
   unsigned long long *part = p.keys + ((size_t)ii * tpi + t) * kNS;
   // what the finish launch needs of the item, in device memory (it would
   // otherwise read the mapped host copy again)
-  if (t == 0 && tid == 0) p.info[ii] = make_int4((int)(unsigned)it.gmask, (int)(unsigned)(it.gmask >> 32),
+  if (!p.host_finish && t == 0 && tid == 0) p.info[ii] = make_int4((int)(unsigned)it.gmask, (int)(unsigned)(it.gmask >> 32),
                                                  (int)(unsigned short)it.cqx | ((int)it.cqy << 16), it.u);
   if (ox0 > R || oy0 > R) {                              // a tile past this item's window
     if (tid < kNS && ((it.gmask >> tid) & 1)) part[tid] = ~0ull;
@@ -1775,7 +1775,7 @@ hipError_t launch_search_small(const SmallParams &p, hipStream_t s) {
                                       : (ffs ? me_small_kernel<true, false> : me_small_kernel<false, false>);
   void (*finish)(SmallParams) = ffs ? small_finish_kernel<true> : small_finish_kernel<false>;
   hipLaunchKernelGGL(search, grid, dim3(kWG), 0, s, p);
-  hipLaunchKernelGGL(finish, g2, dim3(kWG), 0, s, p);
+  if (!p.host_finish) hipLaunchKernelGGL(finish, g2, dim3(kWG), 0, s, p);
   return hipGetLastError();
 }
 

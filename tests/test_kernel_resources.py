@@ -47,3 +47,13 @@ def test_item_kernels_fit_four_waves_without_scratch(tmp_path):
         k = kernels[name]
         assert k[".private_segment_fixed_size"] == 0, f"{what}: {k['.private_segment_fixed_size']} B/lane scratch"
         assert k[".vgpr_count"] <= 128, f"{what}: {k['.vgpr_count']} VGPRs (4 waves/SIMD needs <= 128)"
+
+
+def test_small_kernels_read_inline_items_without_scratch(tmp_path):
+    """the latency-form small launch indexes its items inside the kernel
+    arguments (SmallParams::inl); that must stay scalar loads, not a private copy"""
+    kernels = _kernel_metadata(tmp_path)
+    small = {k: v for k, v in kernels.items() if "me_small_kernel" in k}
+    assert len(small) == 4, sorted(small)   # FS / FFS x 8-bit / 16-bit pels
+    for name, k in small.items():
+        assert k[".private_segment_fixed_size"] == 0, f"{name}: {k['.private_segment_fixed_size']} B/lane scratch"
