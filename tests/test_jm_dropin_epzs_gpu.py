@@ -78,6 +78,11 @@ def _run(w, h, frames, over, seed=5, gmv=(3, -2), adversarial=False, env=None):
     (176, 144, 3, {"NumberReferenceFrames": 2, "EPZSPattern": 5, "EPZSDualRefinement": 2, "EPZSBlockType": 0,
                    "Transform8x8Mode": 1, "ProfileIDC": 100}),
     (176, 144, 3, {"NumberReferenceFrames": 1, "EPZSPattern": 1, "EPZSDualRefinement": 0, "SearchRange": 16}),
+    # several slices per picture: each slice allocates a fresh EPZS structure (slice.c:1661-1665,
+    # BlkCount 1 and a zeroed map), which the adapter must recognise
+    (352, 288, 3, {"NumberReferenceFrames": 2, "SliceMode": 1, "SliceArgument": 50}),
+    (176, 144, 4, {"NumberReferenceFrames": 2, "EPZSSubPelGrid": 0, "SliceMode": 1, "SliceArgument": 20,
+                   "RDOptimization": 0}),
 ])
 def test_lencod_epzs_is_byte_identical(gpu, w, h, frames, over):
     st, err = _run(w, h, frames, over, seed=w + frames + len(over))

@@ -77,6 +77,9 @@ def _encode(binary, d, tag, yuv, w, h, frames, params, env=None):
                    "NumberBFrames": 1, "ProfileIDC": 77, "DisableSubpelME": 0, "MEDistortionQPel": 0}),
     (176, 144, 5, {"SearchMode": 0, "SearchRange": 16, "RDOptimization": 1, "NumberReferenceFrames": 2,
                    "NumberBFrames": 1, "ProfileIDC": 77, "DisableSubpelME": 0, "MEDistortionQPel": 0}),
+    # slices (neighbours across a slice border are unavailable: other predictors, same pure search)
+    (352, 288, 3, {"SearchMode": -1, "SearchRange": 16, "RDOptimization": 0, "NumberReferenceFrames": 2,
+                   "SliceMode": 1, "SliceArgument": 33, "DisableSubpelME": 0, "MEDistortionQPel": 0}),
 ])
 def test_lencod_with_gpu_me_is_byte_identical(gpu, w, h, frames, params, speculate):
     """speculate=1: full-search calls answered from speculative batches (jm_gpu_me.c);
