@@ -104,6 +104,8 @@ struct jmme_ctx {
   size_t cap_sitems = 0;
   jmme_block_res *h_sout = nullptr;
   size_t cap_sout = 0;
+  jmme_chain_res *h_chres = nullptr;         // jmme_search_mbs_chains results (mapped pinned)
+  hipStream_t chain_stream = nullptr;        // chains run beside the batch of the same call (non-blocking)
   unsigned long long *h_hkeys = nullptr;    // small latency form: per-tile keys (mapped pinned)
   size_t cap_hkeys = 0;
   uint8_t *h_emap = nullptr;                 // jmme_epzs_search_ex: mapped pinned request / result block
@@ -315,6 +317,8 @@ extern "C" void jmme_destroy(jmme_ctx *ctx) {
   if (ctx->h_sout) (void)hipHostFree(ctx->h_sout);
   if (ctx->h_emap) (void)hipHostFree(ctx->h_emap);
   if (ctx->h_hkeys) (void)hipHostFree(ctx->h_hkeys);
+  if (ctx->h_chres) (void)hipHostFree(ctx->h_chres);
+  if (ctx->chain_stream) (void)hipStreamDestroy(ctx->chain_stream);
   (void)hipFree(ctx->d_skeys);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
@@ -769,6 +773,82 @@ extern "C" int jmme_search_mbs(jmme_ctx *ctx, int mode, const jmme_mb_req *req, 
   return 0;
 }
 
+// chained searches: validated and launched (asynchronously, on stream s)
+// before the batch of the same call, so the batch's stream sync covers them
+namespace {
+int launch_chains(jmme_ctx *ctx, int mode, const jmme_chain *chains, int n, hipStream_t s) {
+  if (n <= 0) return 0;
+  if (n > kChainInline) return fail("%d chains in one call (at most %d)", n, kChainInline);
+  if (mode != JMME_FULL_SEARCH && mode != JMME_FAST_FULL_SEARCH) return fail("chains: mode %d", mode);
+  if (ctx->hbd) return fail("chains: 8-bit planes only");
+  ChainParams p{};
+  int max_r = 0;
+  for (int i = 0; i < n; ++i) {
+    const jmme_chain &c = chains[i];
+    if (c.n_steps < 1 || c.n_steps > JMME_CHAIN_MAX_STEPS) return fail("chain %d: %d steps", i, c.n_steps);
+    if (c.mb_x < 0 || c.mb_y < 0 || (c.mb_x & 15) || (c.mb_y & 15) || c.mb_x + 16 > ctx->width ||
+        c.mb_y + 16 > ctx->height)
+      return fail("chain %d: macroblock (%d,%d) outside the picture", i, c.mb_x, c.mb_y);
+    if (c.list < 0 || c.list >= kMaxLists || c.ref_idx < 0 || c.ref_idx >= kMaxRefs ||
+        !ctx->d_refs[c.list * kMaxRefs + c.ref_idx])
+      return fail("chain %d: reference (%d,%d) not uploaded", i, c.list, c.ref_idx);
+    if (c.lambda < 0) return fail("chain %d: negative lambda", i);
+    if (mode == JMME_FAST_FULL_SEARCH && (c.ffs_range < 0 || c.ffs_range > kChainMaxR || (c.ffs_center_x & 3) ||
+                                          (c.ffs_center_y & 3)))
+      return fail("chain %d: FFS surface range %d / centre", i, c.ffs_range);
+    for (int k = 0; k < c.n_steps; ++k) {
+      const jmme_chain_step &st = c.steps[k];
+      if (st.slot < 0 || st.slot >= JMME_NSLOT) return fail("chain %d step %d: slot %d", i, k, st.slot);
+      for (int j = 0; j < 3; ++j)
+        if (st.nb[j].src < JMME_NB_FIXED || st.nb[j].src >= k)
+          return fail("chain %d step %d: neighbour source %d", i, k, st.nb[j].src);
+      if (st.sr_min_x > 0 || st.sr_max_x < 0 || st.sr_min_y > 0 || st.sr_max_y < 0)
+        return fail("chain %d step %d: search window", i, k);
+    }
+  }
+  max_r = kChainMaxR;
+  const size_t nres = (size_t)n * JMME_CHAIN_MAX_STEPS;
+  if (!ctx->h_chres) {
+    HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_chres), kChainInline * JMME_CHAIN_MAX_STEPS *
+                                                                      sizeof(jmme_chain_res), hipHostMallocMapped));
+  }
+  std::memset(ctx->h_chres, 0, nres * sizeof(jmme_chain_res));
+  void *d_res = nullptr;
+  HIPCHK(hipHostGetDevicePointer(&d_res, ctx->h_chres, 0));
+  if (sync_ref_table(ctx, s)) return -1;
+  p.cur = ctx->d_cur;
+  p.refs = ctx->d_ref_table;
+  p.pitch = ctx->pitch;
+  p.width = ctx->width;
+  p.height = ctx->height;
+  p.mode = mode;
+  p.max_mvd = ctx->max_mvd;
+  p.n = n;
+  p.max_r = max_r;
+  p.res = static_cast<jmme_chain_res *>(d_res);
+  std::memcpy(p.chains, chains, (size_t)n * sizeof(jmme_chain));
+  HIPCHK(launch_search_chains(p, s));
+  return 0;
+}
+}  // namespace
+
+extern "C" int jmme_search_mbs_chains(jmme_ctx *ctx, int mode, const jmme_mb_req *req, int n, jmme_block_res *out,
+                                      const jmme_chain *chains, int n_chains, jmme_chain_res *res) {
+  DevGuard dg_(ctx);
+  if (!ctx) return fail("null ctx");
+  if (!ctx->d_cur) return fail("current picture not uploaded");
+  if (n_chains < 0 || (n_chains && (!chains || !res))) return fail("null chain array");
+  if (n_chains == 0) return jmme_search_mbs(ctx, mode, req, n, out);
+  if (!ctx->chain_stream) HIPCHK(hipStreamCreateWithFlags(&ctx->chain_stream, hipStreamNonBlocking));
+  // the chains run on their own stream beside the batch (which syncs the null stream)
+  if (launch_chains(ctx, mode, chains, n_chains, ctx->chain_stream)) return -1;
+  const int rc = n ? jmme_search_mbs(ctx, mode, req, n, out) : 0;
+  HIPCHK(hipStreamSynchronize(ctx->chain_stream));
+  if (rc) return rc;
+  std::memcpy(res, ctx->h_chres, (size_t)n_chains * JMME_CHAIN_MAX_STEPS * sizeof(jmme_chain_res));
+  return 0;
+}
+
 extern "C" int jmme_search_mbs_async(jmme_ctx *ctx, int mode, const jmme_mb_req *d_req, int n,
                                      jmme_block_res *d_out, void *stream) {
   DevGuard dg_(ctx);
@@ -1124,6 +1204,8 @@ extern "C" int jmme_fractal_box_sums(jmme_ctx *ctx, const uint8_t *plane, int pi
 
 // -------------------------------------------------------------------- EPZS --
 static_assert(sizeof(jmme_epzs_req) == 80 && sizeof(jmme_epzs_res) == 32, "EPZS ABI layout");
+static_assert(sizeof(jmme_chain) == 176 && sizeof(jmme_chain_step) == 36 && sizeof(jmme_chain_res) == 24,
+              "chain ABI layout");
 
 namespace {
 int prepare_subs(jmme_ctx *ctx, hipStream_t s);   // sub-pel section below

@@ -103,6 +103,19 @@ struct SmallParams {
 };
 constexpr int kSmallTile = 16;
 hipError_t launch_search_small(const SmallParams &p, hipStream_t s);
+// chained partition searches (jmme_search_mbs_chains): one workgroup per chain
+constexpr int kChainInline = 8;     // chains per launch (kernel arguments)
+constexpr int kChainMaxR = 44;      // largest window range the staged LDS window holds
+struct ChainParams {
+  const uint8_t *cur;
+  const uint8_t *const *refs;       // device reference table
+  int pitch, width, height;
+  int mode, max_mvd, n, max_r;      // max_r: largest window range of the launch (LDS sizing)
+  jmme_chain_res *res;              // [n][JMME_CHAIN_MAX_STEPS] (host-mapped)
+  jmme_chain chains[kChainInline];
+};
+size_t chain_lds_bytes(int max_r);
+hipError_t launch_search_chains(const ChainParams &p, hipStream_t s);
 
 size_t items_lds_bytes(int lds_range);
 // plan (unit requests -> items), then the persistent 32-bit and 64-bit item

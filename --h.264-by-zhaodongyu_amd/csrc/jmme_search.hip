@@ -1701,6 +1701,204 @@ __global__ __launch_bounds__(kWG) void small_finish_kernel(SmallParams p) {
   p.out[(size_t)q.w * kNS + sl] = block_result<FFS>(g, k != ~0ull, (uint32_t)(k & 0xffffffffu), (uint32_t)(k >> 32));
 }
 
+// ------------------------------------------------------ chained searches --
+// One workgroup per chain (jmme.h, jmme_search_mbs_chains).  Per step, thread 0
+// derives the step's predictor and centre as JM would from the chain's
+// neighbours (GetMotionVectorPredictorNormal, JM/lcommon/src/mv_prediction.c:
+// 192-300; BlockMotionSearch, mv_search.c:930-956; CheckSearchRange :822-848;
+// clip_mv_range, conformance.c:463-469), the window around it is staged in LDS
+// (clamped as UMVLine4X does), every position's SAD over the partition is
+// formed from the staged words, and the (cost, spiral rank) minimum wins, as
+// in full_search_motion_estimation / fast_full_search_motion_estimation.  The
+// step's answer, clipped as BlockMotionSearch clips it after the search
+// (mv_search.c:983), is what the next steps read as that partition's vector.
+constexpr int kChainWG = 1024, kChainWaves = kChainWG / 64;
+
+__host__ __device__ inline int chain_wpr(int R) { return 2 * R + 13; }          // words per staged row (w = 4)
+__host__ __device__ inline int chain_raw(int R) { return (2 * R + 19 + 3) / 4 + 1; }   // raw dwords per row
+
+__device__ __forceinline__ int imedian3(int a, int b, int c) {
+  return a > b ? (b > c ? b : (a > c ? c : a)) : (a > c ? a : (b > c ? c : b));
+}
+
+template <bool FFS>
+__global__ __launch_bounds__(kChainWG) void chain_kernel(ChainParams p) {
+  extern __shared__ uint32_t dyn[];
+  __shared__ uint32_t s_cur[64];
+  __shared__ int s_d[8];                          // px, py, cqx, cqy, R, rs, ok
+  __shared__ int s_mv[JMME_CHAIN_MAX_STEPS][2];   // the steps' vectors as the next steps read them
+  __shared__ uint32_t s_minc[kChainWaves], s_minr[kChainWaves];
+  const jmme_chain &c = p.chains[blockIdx.x];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint8_t *ref = p.refs[c.list * kMaxRefs + c.ref_idx];
+  jmme_chain_res *out = p.res + (size_t)blockIdx.x * JMME_CHAIN_MAX_STEPS;
+  if (tid < 64)
+    s_cur[tid] = *reinterpret_cast<const uint32_t *>(p.cur + (size_t)(c.mb_y + (tid >> 2)) * p.pitch + c.mb_x +
+                                                     4 * (tid & 3));
+  bool alive = true;
+  int staged_x = -0x40000000, staged_y = 0, staged_r = -1;   // the window in LDS (centre, range)
+  for (int k = 0; k < c.n_steps; ++k) {
+    const jmme_chain_step &st = c.steps[k];
+    const SlotGeom sg = slot_geom(st.slot);
+    const int bsx = 4 * sg.w, bsy = 4 * sg.h;
+    if (tid == 0) {
+      // neighbours: (available, ref_idx, mv)
+      int av[3], rf[3], mx[3], my[3];
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const jmme_chain_nb nb = st.nb[j];
+        av[j] = nb.src != JMME_NB_UNAVAILABLE;
+        if (nb.src >= 0) { rf[j] = c.ref_idx; mx[j] = s_mv[nb.src][0]; my[j] = s_mv[nb.src][1]; }
+        else { rf[j] = nb.ref_idx; mx[j] = nb.mv_x; my[j] = nb.mv_y; }
+      }
+      const int r = c.ref_idx;
+      const int rL = av[0] ? rf[0] : -1, rU = av[1] ? rf[1] : -1, rUR = av[2] ? rf[2] : -1;
+      int type = 0;   // 0 median, 1 L, 2 U, 3 UR
+      if (rL == r && rU != r && rUR != r) type = 1;
+      else if (rL != r && rU == r && rUR != r) type = 2;
+      else if (rL != r && rU != r && rUR == r) type = 3;
+      if (bsx == 8 && bsy == 16) {
+        if (sg.bx == 0) { if (rL == r) type = 1; }
+        else { if (rUR == r) type = 3; }
+      } else if (bsx == 16 && bsy == 8) {
+        if (sg.by == 0) { if (rU == r) type = 2; }
+        else { if (rL == r) type = 1; }
+      }
+      int px = 0, py = 0;
+      if (type == 0) {
+        if (!(av[1] || av[2])) {
+          if (av[0]) { px = mx[0]; py = my[0]; }
+        } else {
+          px = imedian3(av[0] ? mx[0] : 0, av[1] ? mx[1] : 0, av[2] ? mx[2] : 0);
+          py = imedian3(av[0] ? my[0] : 0, av[1] ? my[1] : 0, av[2] ? my[2] : 0);
+        }
+      } else {
+        const int j = type - 1;
+        if (av[j]) { px = mx[j]; py = my[j]; }
+      }
+      px = (int16_t)px; py = (int16_t)py;
+      // BlockMotionSearch's centre: JM_INT_DIVIDE rounding, the (0,0)-inside clip
+      // with CheckSearchRange when RDO is off, then the level's vector range
+      int cx = (int16_t)(((px + 2) >> 2) * 4), cy = (int16_t)(((py + 2) >> 2) * 4);
+      int mnx = st.sr_min_x, mxx = st.sr_max_x, mny = st.sr_min_y, mxy = st.sr_max_y;
+      if (!c.rdopt) {
+        const int ccx = cx, ccy = cy;
+        cx = clampi(cx, mnx, mxx);
+        cy = clampi(cy, mny, mxy);
+        if (cx != ccx || cy != ccy) {
+          const int md = p.max_mvd - 2;
+          int left = cx + mnx, right = cx + mxx, top = cy + mny, down = cy + mxy;
+          left = clampi(left, ccx - md, ccx + md);
+          right = clampi(right, ccx - md, ccx + md);
+          top = clampi(top, ccy - md, ccy + md);
+          down = clampi(down, ccy - md, ccy + md);
+          if (left < right && top < down) {
+            cx = (int16_t)((left + right) >> 1);
+            cy = (int16_t)((top + down) >> 1);
+            mnx = left - cx; mxx = min(cx - left, right - cx);
+            mny = top - cy; mxy = min(cy - top, down - cy);
+          } else {
+            cx = ccx; cy = ccy;
+          }
+        }
+      }
+      cx = clampi(cx, c.mv_lim_x0, c.mv_lim_x1);
+      cy = clampi(cy, c.mv_lim_y0, c.mv_lim_y1);
+      const int rmin = min(mxx, mxy) >> 2, rmax = max(mxx, mxy) >> 2;
+      out[k].pred_x = (int16_t)px; out[k].pred_y = (int16_t)py;
+      out[k].center_x = (int16_t)cx; out[k].center_y = (int16_t)cy;
+      out[k].range_min = (int16_t)rmin; out[k].range_max = (int16_t)rmax;
+      s_d[0] = px; s_d[1] = py;
+      s_d[2] = FFS ? c.ffs_center_x : cx;
+      s_d[3] = FFS ? c.ffs_center_y : cy;
+      s_d[4] = FFS ? c.ffs_range : rmin;
+      s_d[5] = FFS ? rmax : rmin;
+      // the window must fit the staged LDS and (FS) start on an integer vector
+      s_d[6] = s_d[4] >= 0 && s_d[4] <= p.max_r && s_d[5] >= 0 && !((s_d[2] | s_d[3]) & 3);
+    }
+    __syncthreads();
+    const int px = s_d[0], py = s_d[1], cqx = s_d[2], cqy = s_d[3], R = s_d[4], rs = s_d[5];
+    alive = alive && s_d[6];
+    if (!alive) {   // this step and the rest: no answer
+      if (tid == 0) { out[k].cost = -1; s_mv[k][0] = cqx; s_mv[k][1] = cqy; }
+      __syncthreads();
+      continue;
+    }
+    // stage the window of the whole macroblock: words[y][x] = pels x..x+3 of
+    // window row y, window origin (macroblock origin + centre - R), clamped into
+    // the picture; restaged only when the centre or range moves (FFS: once per chain)
+    const int wpr = chain_wpr(R), nraw = chain_raw(R), rows = 2 * R + 16;
+    uint32_t *words = dyn, *raw = dyn + (size_t)rows * wpr;
+    if (cqx != staged_x || cqy != staged_y || R != staged_r) {
+      staged_x = cqx; staged_y = cqy; staged_r = R;
+      const int X0 = c.mb_x + (cqx >> 2) - R, Y0 = c.mb_y + (cqy >> 2) - R;
+      const int xa = X0 & ~3, sh = X0 - xa;
+      for (int i = tid; i < rows * nraw; i += kChainWG) {
+        const int r = i / nraw, q = i - r * nraw;
+        const uint8_t *row = ref + (size_t)clampi(Y0 + r, 0, p.height - 1) * p.pitch;
+        const int x = xa + 4 * q;
+        uint32_t w;
+        if (x >= 0 && x + 3 < p.width) {
+          w = *reinterpret_cast<const uint32_t *>(row + x);
+        } else {
+          w = 0;
+#pragma unroll
+          for (int b = 0; b < 4; ++b) w |= (uint32_t)row[clampi(x + b, 0, p.width - 1)] << (8 * b);
+        }
+        raw[i] = w;
+      }
+      __syncthreads();
+      for (int i = tid; i < rows * wpr; i += kChainWG) {
+        const int r = i / wpr, x = i - r * wpr, q = (sh + x) >> 2;
+        words[i] = __builtin_amdgcn_alignbyte(raw[r * nraw + q + 1], raw[r * nraw + q], (sh + x) & 3);
+      }
+      __syncthreads();
+    }
+    // every position of the window: (cost << 32 | rank), eligible ones only
+    GroupCtx g{};
+    g.R = R; g.rs = rs; g.cqx = cqx; g.cqy = cqy; g.px = px; g.py = py; g.lam = c.lambda; g.max_mvd = p.max_mvd;
+    g.preseed = FFS && c.ffs_pos00_valid;
+    const int D = 2 * R + 1;
+    uint32_t bc = ~0u, br = ~0u;   // this thread's best (cost, rank)
+    for (int i = tid; i < D * D; i += kChainWG) {
+      const int oy = i / D - R, ox = i - (oy + R) * D - R;
+      const int candx = cqx + 4 * ox, candy = cqy + 4 * oy;
+      const bool is00 = candx == 0 && candy == 0;
+      const MvCost mc = mv_cost<FFS>(candx, candy, px, py, c.lambda, p.max_mvd);
+      if (!pos_eligible<FFS>(g, mc.ok, max(abs(ox), abs(oy)), is00)) continue;
+      uint32_t sad = 0;
+      const uint32_t *wb = words + (oy + R + 4 * sg.by) * wpr + (ox + R + 4 * sg.bx);
+      for (int r = 0; r < bsy; ++r)
+        for (int wc = 0; wc < sg.w; ++wc)
+          sad = __builtin_amdgcn_sad_u8(wb[r * wpr + 4 * wc], s_cur[(4 * sg.by + r) * 4 + sg.bx + wc], sad);
+      const int sidx = spiral_index_bl(ox, oy);
+      const uint32_t rank = FFS ? ((g.preseed && is00) ? 0u : (uint32_t)sidx + 1u) : (uint32_t)sidx;
+      const uint32_t cost = (sad << 5) + mc.mvc;
+      if (cost < bc || (cost == bc && rank < br)) { bc = cost; br = rank; }
+    }
+    // wave minimum of the cost (DPP), then the smallest rank among its holders
+    {
+      const uint32_t cmin = wave_min_u32(bc);
+      const uint32_t rmin = wave_min_u32(bc == cmin ? br : ~0u);
+      if (lane == 0) { s_minc[wave] = cmin; s_minr[wave] = rmin; }
+    }
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t bcost = s_minc[0], brank = s_minr[0];
+#pragma unroll
+      for (int w = 1; w < kChainWaves; ++w)
+        if (s_minc[w] < bcost || (s_minc[w] == bcost && s_minr[w] < brank)) { bcost = s_minc[w]; brank = s_minr[w]; }
+      const jmme_block_res r = block_result<FFS>(g, brank != ~0u, brank, bcost);
+      out[k].mv_x = r.mv_x; out[k].mv_y = r.mv_y; out[k].cost = r.cost;
+      // as BlockMotionSearch leaves it for the next partitions' predictors (mv_search.c:983)
+      s_mv[k][0] = clampi(r.mv_x, c.mv_lim_x0, c.mv_lim_x1);
+      s_mv[k][1] = clampi(r.mv_y, c.mv_lim_y0, c.mv_lim_y1);
+    }
+    __syncthreads();
+  }
+}
+
+
 struct Occupancy {
   int cus = 0;
   int wg[4][JMME_MAX_RANGE + 1] = {};   // resident workgroups per CU, by kernel variant and lds range
@@ -1764,6 +1962,19 @@ hipError_t launch_search(const KParams &p, hipStream_t s, hipEvent_t ev0, hipEve
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (ev1) (void)hipEventRecord(ev1, s);
   }
+  return hipGetLastError();
+}
+
+size_t chain_lds_bytes(int max_r) {
+  const int rows = 2 * max_r + 16;
+  return (size_t)rows * (chain_wpr(max_r) + chain_raw(max_r)) * 4;
+}
+
+hipError_t launch_search_chains(const ChainParams &p, hipStream_t s) {
+  if (p.n <= 0) return hipSuccess;
+  const size_t lds = chain_lds_bytes(p.max_r);
+  if (p.mode == JMME_FAST_FULL_SEARCH) hipLaunchKernelGGL(chain_kernel<true>, dim3(p.n), dim3(kChainWG), lds, s, p);
+  else hipLaunchKernelGGL(chain_kernel<false>, dim3(p.n), dim3(kChainWG), lds, s, p);
   return hipGetLastError();
 }
 

@@ -28,6 +28,16 @@ MB_REQ = np.dtype([("mb_x", "<i2"), ("mb_y", "<i2"), ("list", "<i2"), ("ref_idx"
                    ("ffs_pos00_valid", "<i2"), ("reserved", "<i2", (4,)),
                    ("blk", BLOCK_REQ, (NSLOT,))])
 BLOCK_RES = np.dtype([("mv_x", "<i2"), ("mv_y", "<i2"), ("reserved", "<i4"), ("cost", "<i8")])
+CHAIN_MAX_STEPS, NB_UNAVAILABLE, NB_FIXED = 4, -1, -2
+CHAIN_NB = np.dtype([("src", "<i2"), ("ref_idx", "<i2"), ("mv_x", "<i2"), ("mv_y", "<i2")])
+CHAIN_STEP = np.dtype([("slot", "<i2"), ("reserved", "<i2"), ("nb", CHAIN_NB, (3,)), ("sr_min_x", "<i2"),
+                       ("sr_max_x", "<i2"), ("sr_min_y", "<i2"), ("sr_max_y", "<i2")])
+CHAIN = np.dtype([("mb_x", "<i2"), ("mb_y", "<i2"), ("list", "<i2"), ("ref_idx", "<i2"), ("n_steps", "<i2"),
+                  ("rdopt", "<i2"), ("ffs_center_x", "<i2"), ("ffs_center_y", "<i2"), ("ffs_range", "<i2"),
+                  ("ffs_pos00_valid", "<i2"), ("mv_lim_x0", "<i2"), ("mv_lim_x1", "<i2"), ("mv_lim_y0", "<i2"),
+                  ("mv_lim_y1", "<i2"), ("lambda", "<i4"), ("steps", CHAIN_STEP, (4,))])
+CHAIN_RES = np.dtype([("pred_x", "<i2"), ("pred_y", "<i2"), ("center_x", "<i2"), ("center_y", "<i2"),
+                      ("range_min", "<i2"), ("range_max", "<i2"), ("mv_x", "<i2"), ("mv_y", "<i2"), ("cost", "<i8")])
 FRACTAL_REQ = np.dtype([("block_x", "<i2"), ("block_y", "<i2"), ("bsx", "<i2"), ("bsy", "<i2")])
 FRACTAL_RES = np.dtype([("rms", "<f8"), ("scale", "<f8"), ("offset", "<f8"), ("x", "<i4"), ("y", "<i4")])
 FRACTAL_NODE = np.dtype([("rms", "<f8"), ("scale", "<f8"), ("offset", "<f8"), ("x", "<i4"), ("y", "<i4"),
@@ -62,6 +72,7 @@ assert BLOCK_REQ.itemsize == 16 and MB_REQ.itemsize == 688 and BLOCK_RES.itemsiz
 assert QUANT4x4_PARAMS.itemsize == 248 and FRACTAL_REQ.itemsize == 8 and FRACTAL_RES.itemsize == 32
 assert FRACTAL_NODE.itemsize == 40 and FRACTAL_MB.itemsize == 848
 assert EPZS_REQ.itemsize == 80 and EPZS_RES.itemsize == 32 and SUBPEL_REQ.itemsize == 48
+assert CHAIN_NB.itemsize == 8 and CHAIN_STEP.itemsize == 36 and CHAIN.itemsize == 176 and CHAIN_RES.itemsize == 24
 
 CONFIG_FIELDS = ["SourceWidth", "SourceHeight", "SearchMode", "SearchRange", "NumberReferenceFrames",
                  "DisableSubpelME", "RDOptimization", "MEDistortionFPel", "MDDistortion", "EPZSSubPelGrid",
@@ -107,6 +118,7 @@ def lib() -> ctypes.CDLL:
         "jmme_upload_ref": (I, [P, I, I, P, I, I]),
         "jmme_slot": (I, [I, I, I]),
         "jmme_search_mbs": (I, [P, I, P, I, P]),
+        "jmme_search_mbs_chains": (I, [P, I, P, I, P, P, I, P]),
         "jmme_search_mbs_async": (I, [P, I, P, I, P, P]),
         "jmme_search_mbs_planes_async": (I, [P, I, P, P, I, I, I, P, I, P, P]),
         "jmme_search_status": (I, [P, P]),

@@ -103,6 +103,17 @@ class MotionEstimator:
         check(lib().jmme_search_mbs(self._ctx, int(mode), ptr(req), req.shape[0], ptr(out)))
         return out
 
+    def search_chains(self, mode: int, req: np.ndarray, chains: np.ndarray):
+        """jmme_search_mbs_chains: the batch (BLOCK_RES [n, 41]) and the chains'
+        steps (CHAIN_RES [n_chains, 4]) in one round trip."""
+        req = np.ascontiguousarray(req, dtype=MB_REQ)
+        chains = np.ascontiguousarray(chains, dtype=_lib.CHAIN)
+        out = np.zeros((req.shape[0], NSLOT), dtype=BLOCK_RES)
+        res = np.zeros((len(chains), _lib.CHAIN_MAX_STEPS), dtype=_lib.CHAIN_RES)
+        check(lib().jmme_search_mbs_chains(self._ctx, int(mode), ptr(req), req.shape[0], ptr(out), ptr(chains),
+                                           len(chains), ptr(res)))
+        return out, res
+
     def search_async(self, mode: int, d_req: int, n: int, d_out: int, stream: int = 0) -> None:
         """Device-resident variant: d_req/d_out are device addresses (e.g. torch data_ptr())."""
         check(lib().jmme_search_mbs_async(self._ctx, int(mode), ctypes.c_void_p(d_req), int(n),

@@ -143,6 +143,61 @@ int jmme_slot(int blocktype, int block_x, int block_y);
 /* mode = JMME_FULL_SEARCH or JMME_FAST_FULL_SEARCH.  Host arrays, synchronous.
  * out has n * JMME_NSLOT entries (unsearched slots are left untouched). */
 int jmme_search_mbs(jmme_ctx *ctx, int mode, const jmme_mb_req *req, int n, jmme_block_res *out);
+/* ---- Chained partition searches (the drop-in's guesses inside one macroblock)
+ * JM searches a macroblock's partitions one at a time, and a partition's MV
+ * predictor (GetMotionVectorPredictorNormal, JM/lcommon/src/mv_prediction.c:192)
+ * reads the vectors its neighbours inside the macroblock were just given
+ * (set_me_parameters after each search, mv_search.c:1614,1705-1720).  A chain
+ * is such a run of partitions -- the rest of a 16x8 / 8x16 pair, or one
+ * sub-mode of one 8x8 quadrant -- whose neighbours are either fixed (decided
+ * before the chain starts: neighbouring macroblocks, earlier quadrants) or an
+ * earlier step of the same chain.  The GPU derives each step's predictor and
+ * centre exactly as BlockMotionSearch does (mv_search.c:896-956) from those
+ * neighbours and the previous steps' results, and searches it.  Single
+ * reference, integer-pel only (the neighbours' vectors are integer results);
+ * the caller uses a result only when JM's real call carries the same inputs. */
+#define JMME_CHAIN_MAX_STEPS 4
+#define JMME_NB_UNAVAILABLE (-1)
+#define JMME_NB_FIXED (-2)
+
+typedef struct jmme_chain_nb {
+  int16_t src;                 /* JMME_NB_UNAVAILABLE, JMME_NB_FIXED, or k >= 0: step k's result */
+  int16_t ref_idx;             /* JMME_NB_FIXED: mv_info[y][x].ref_idx[list] */
+  int16_t mv_x, mv_y;          /* JMME_NB_FIXED: mv_info[y][x].mv[list] (qpel) */
+} jmme_chain_nb;               /* 8 bytes */
+
+typedef struct jmme_chain_step {
+  int16_t slot;                /* partition (jmme_slot) */
+  int16_t reserved;
+  jmme_chain_nb nb[3];         /* get_neighbors' block[0] (left), [1] (up), [2] (up-right, else up-left) */
+  int16_t sr_min_x, sr_max_x;  /* mv_block->searchRange after get_search_range (qpel) */
+  int16_t sr_min_y, sr_max_y;
+} jmme_chain_step;             /* 36 bytes */
+
+typedef struct jmme_chain {
+  int16_t mb_x, mb_y;          /* macroblock origin (luma pels) */
+  int16_t list, ref_idx;       /* the uploaded reference; also the in-chain neighbours' ref_idx */
+  int16_t n_steps;             /* 1..JMME_CHAIN_MAX_STEPS */
+  int16_t rdopt;               /* p_Inp->rdopt (the centre clip of mv_search.c:939-955 runs when 0) */
+  int16_t ffs_center_x, ffs_center_y, ffs_range, ffs_pos00_valid;   /* FFS: the macroblock's surface */
+  int16_t mv_lim_x0, mv_lim_x1;   /* p_Vid->MaxHmvR[4], [5] (clip_mv_range, Q_PEL) */
+  int16_t mv_lim_y0, mv_lim_y1;   /* p_Vid->MaxVmvR[4], [5] */
+  int32_t lambda;              /* lambda_factor[F_PEL] */
+  jmme_chain_step steps[JMME_CHAIN_MAX_STEPS];
+} jmme_chain;                  /* 32 + 4 * 36 = 176 bytes */
+
+typedef struct jmme_chain_res {
+  int16_t pred_x, pred_y;      /* the step's derived predictor (qpel) */
+  int16_t center_x, center_y;  /* FS: mv_block->mv[list] on entry to IntPelME */
+  int16_t range_min, range_max;   /* min / max(searchRange.max_x, .max_y) >> 2 after CheckSearchRange */
+  int16_t mv_x, mv_y;          /* the search's answer (before JM's clip_mv_range) */
+  int64_t cost;
+} jmme_chain_res;              /* 24 bytes */
+
+/* jmme_search_mbs plus chains, one launch round trip: res[i * JMME_CHAIN_MAX_STEPS + k] is step k of chain i. */
+int jmme_search_mbs_chains(jmme_ctx *ctx, int mode, const jmme_mb_req *req, int n, jmme_block_res *out,
+                           const jmme_chain *chains, int n_chains, jmme_chain_res *res);
+
 /* jmme_search_mbs serves a batch whose work items (partition groups sharing a
  * window and predictor) fit in at most `max_workgroups` workgroups of 16x16
  * window positions by a single low-latency launch (no device copies, results

@@ -218,6 +218,7 @@ typedef struct spec_ent {
 } spec_ent;
 
 #define KHYP 4                     /* guesses per (macroblock, partition) */
+#define KWAYS (KHYP + 1)           /* cache ways: the KHYP guesses + the chained search's answer (way KHYP) */
 static spec_ent *g_spec[2][32];    /* KHYP cached (inputs -> result) per (macroblock, slot) */
 static spec_ent *g_seen[2][32];    /* the inputs each (macroblock, slot) was really searched with */
 static unsigned g_spec_gen[2][32]; /* g_slot_gen the cached guesses belong to */
@@ -249,7 +250,7 @@ static spec_ent *spec_table(VideoParameters *p_Vid, int list, int ref)
     g_n_mb = g_mbs_x * (p_Vid->height / 16);
   }
   if (!g_spec[list][ref]) {
-    g_spec[list][ref] = (spec_ent *)calloc((size_t)g_n_mb * JMME_NSLOT * KHYP, sizeof(spec_ent));
+    g_spec[list][ref] = (spec_ent *)calloc((size_t)g_n_mb * JMME_NSLOT * KWAYS, sizeof(spec_ent));
     g_seen[list][ref] = (spec_ent *)calloc((size_t)g_n_mb * JMME_NSLOT, sizeof(spec_ent));
     if (!g_spec[list][ref] || !g_seen[list][ref]) error("jm_gpu_me: out of memory", 500);
     g_spec_gen[list][ref] = 0;
@@ -304,6 +305,182 @@ static int spec_hyp(int list, int ref, int h, int mb0, int mb, const spec_ent *w
       out[s].frange = out[0].frange;
     }
   return any;
+}
+
+/* ---- chained guesses inside the missing macroblock ---------------------------
+ * A partition's predictor reads the vectors JM just gave its neighbours inside
+ * the macroblock (set_me_parameters after each search, mv_search.c:1614,1720),
+ * so a guess taken from other macroblocks fails wherever the vectors of one
+ * macroblock differ (the padding rows of a 1080-line picture; any non-uniform
+ * motion).  On a miss the adapter therefore also sends the partitions of the
+ * same macroblock whose neighbours are decided by now as chains
+ * (jmme_search_mbs_chains): the rest of the missing partition's group (a
+ * 16x8 / 8x16 pair, or one sub-mode of one 8x8 quadrant) and the groups JM
+ * searches after it before the next mode decision -- the other pairs and
+ * quadrant 0 after a 16x16 / 16x8 / 8x16 miss, the quadrant's later sub-modes
+ * after a quadrant miss.  Each neighbour is taken from JM's get_neighbors and
+ * is either a vector JM's mv_info already holds for good (neighbouring
+ * macroblocks, earlier quadrants, read now) or an earlier step of the chain;
+ * the GPU derives predictor and centre from them as BlockMotionSearch does and
+ * searches.  The answers land in cache way KHYP and, like every guess, are used
+ * only when JM's real call carries the derived inputs.  Single reference, P
+ * slices, integer-pel results only (sub-pel refinement would change the
+ * neighbours' vectors), no 8x8 transform (its second pass over the quadrants),
+ * JMME_CHAINS=0 turns it off. */
+static jmme_chain g_chains[8];
+static jmme_chain_res g_chres[8 * JMME_CHAIN_MAX_STEPS];
+static int g_n_chains = 0, g_chain_on = -1, g_chain_head = -1;
+static int8_t g_slot_bt[JMME_NSLOT], g_slot_bx[JMME_NSLOT], g_slot_by[JMME_NSLOT];   /* slot_geometry() */
+static void slot_geometry(void);
+static long long g_chain_sent = 0, g_chain_steps = 0, g_chain_hits = 0, g_chain_head_bad = 0;
+static int8_t g_grp[19][4], g_grp_n[19], g_slot_grp[JMME_NSLOT], g_slot_idx[JMME_NSLOT];
+
+/* JM's search order of a macroblock's partitions as groups whose members chain:
+ * 16x16; 16x8; 8x16; then per quadrant q: 8x8, 8x4, 4x8, 4x4 (md_low.c:185-304,
+ * mode_decision_P8x8.c:101-135, mv_search.c:1686-1760) */
+static void chain_groups(void)
+{
+  int g = 0, q, i;
+  g_grp[g][0] = 0; g_grp_n[g++] = 1;
+  g_grp[g][0] = 1; g_grp[g][1] = 2; g_grp_n[g++] = 2;
+  g_grp[g][0] = 3; g_grp[g][1] = 4; g_grp_n[g++] = 2;
+  for (q = 0; q < 4; q++) {
+    const int bx = 2 * (q & 1), by = 2 * (q >> 1);
+    g_grp[g][0] = (int8_t)jmme_slot(4, bx, by); g_grp_n[g++] = 1;
+    g_grp[g][0] = (int8_t)jmme_slot(5, bx, by); g_grp[g][1] = (int8_t)jmme_slot(5, bx, by + 1); g_grp_n[g++] = 2;
+    g_grp[g][0] = (int8_t)jmme_slot(6, bx, by); g_grp[g][1] = (int8_t)jmme_slot(6, bx + 1, by); g_grp_n[g++] = 2;
+    g_grp[g][0] = (int8_t)jmme_slot(7, bx, by); g_grp[g][1] = (int8_t)jmme_slot(7, bx + 1, by);
+    g_grp[g][2] = (int8_t)jmme_slot(7, bx, by + 1); g_grp[g][3] = (int8_t)jmme_slot(7, bx + 1, by + 1);
+    g_grp_n[g++] = 4;
+  }
+  for (g = 0; g < 19; g++)
+    for (i = 0; i < g_grp_n[g]; i++) { g_slot_grp[g_grp[g][i]] = (int8_t)g; g_slot_idx[g_grp[g][i]] = (int8_t)i; }
+}
+
+static int chains_on(Macroblock *currMB, int list, int ref)
+{
+  VideoParameters *p_Vid = currMB->p_Vid;
+  InputParameters *p_Inp = currMB->p_Inp;
+  Slice *currSlice = currMB->p_Slice;
+  if (g_chain_on < 0) {
+    const char *e = getenv("JMME_CHAINS");
+    g_chain_on = !(e && e[0] == '0');
+    chain_groups();
+    if (!g_slot_bt[0]) slot_geometry();
+  }
+  return g_chain_on && !g_hbd && currSlice->slice_type == P_SLICE && currSlice->structure == FRAME &&
+         currMB->list_offset == 0 && list == 0 && ref == 0 && currSlice->listXsize[0] == 1 &&
+         p_Inp->DisableSubpelME[p_Vid->view_id] && !p_Inp->Transform8x8Mode;
+}
+
+/* one chain: group g's partitions from index i0, in JM's order */
+static void chain_fill(jmme_chain *c, Macroblock *currMB, int list, int ref, int g, int i0, const spec_ent *want)
+{
+  static const int bw[8] = {0, 16, 16, 8, 8, 8, 4, 4}, bh[8] = {0, 16, 8, 16, 8, 4, 8, 4};
+  VideoParameters *p_Vid = currMB->p_Vid;
+  InputParameters *p_Inp = currMB->p_Inp;
+  PicMotionParams **mvi = p_Vid->enc_picture->mv_info;
+  MEFullFast *ff = p_Vid->p_ffast_me;
+  MEBlock tmp;
+  int k, j, kk;
+  memset(c, 0, sizeof *c);
+  c->mb_x = (int16_t)currMB->pix_x;
+  c->mb_y = (int16_t)currMB->pix_y;
+  c->list = (int16_t)list;
+  c->ref_idx = (int16_t)ref;
+  c->rdopt = (int16_t)p_Inp->rdopt;
+  c->lambda = want->lambda;
+  c->mv_lim_x0 = (int16_t)p_Vid->MaxHmvR[4]; c->mv_lim_x1 = (int16_t)p_Vid->MaxHmvR[5];
+  c->mv_lim_y0 = (int16_t)p_Vid->MaxVmvR[4]; c->mv_lim_y1 = (int16_t)p_Vid->MaxVmvR[5];
+  if (want->mode) {
+    c->ffs_center_x = ff->search_center[list][ref].mv_x;
+    c->ffs_center_y = ff->search_center[list][ref].mv_y;
+    c->ffs_range = (int16_t)ff->max_search_range[list][ref];
+    c->ffs_pos00_valid = (int16_t)(p_Inp->rdopt == 0);
+  }
+  memset(&tmp, 0, sizeof tmp);
+  tmp.p_Vid = p_Vid;
+  for (k = 0; k < g_grp_n[g] - i0; k++) {
+    const int sl = g_grp[g][i0 + k], bt = g_slot_bt[sl];
+    jmme_chain_step *st = &c->steps[k];
+    PixelPos block[4];
+    st->slot = (int16_t)sl;
+    get_neighbors(currMB, block, g_slot_bx[sl], g_slot_by[sl], bw[bt]);
+    for (j = 0; j < 3; j++) {
+      jmme_chain_nb *nb = &st->nb[j];
+      const int lx = block[j].pos_x - currMB->block_x, ly = block[j].pos_y - currMB->block_y;
+      nb->src = JMME_NB_UNAVAILABLE;
+      if (!block[j].available) continue;
+      if (lx >= 0 && lx < 4 && ly >= 0 && ly < 4)   /* inside: an earlier step of this chain? */
+        for (kk = 0; kk < k; kk++) {
+          const int o = c->steps[kk].slot, ox = g_slot_bx[o] >> 2, oy = g_slot_by[o] >> 2;
+          if (lx >= ox && lx < ox + (bw[g_slot_bt[o]] >> 2) && ly >= oy && ly < oy + (bh[g_slot_bt[o]] >> 2))
+            nb->src = (int16_t)kk;
+        }
+      if (nb->src == JMME_NB_UNAVAILABLE) {       /* decided by now: JM's mv_info */
+        nb->src = JMME_NB_FIXED;
+        nb->ref_idx = mvi[block[j].pos_y][block[j].pos_x].ref_idx[list];
+        nb->mv_x = mvi[block[j].pos_y][block[j].pos_x].mv[list].mv_x;
+        nb->mv_y = mvi[block[j].pos_y][block[j].pos_x].mv[list].mv_y;
+      }
+    }
+    get_search_range(&tmp, p_Inp, (short)ref, bt);
+    st->sr_min_x = (int16_t)tmp.searchRange.min_x; st->sr_max_x = (int16_t)tmp.searchRange.max_x;
+    st->sr_min_y = (int16_t)tmp.searchRange.min_y; st->sr_max_y = (int16_t)tmp.searchRange.max_y;
+  }
+  c->n_steps = (int16_t)k;
+}
+
+/* the chains that are decided at a miss of slot s of macroblock mb (the current one) */
+static int build_chains(Macroblock *currMB, int list, int ref, int mb, int s, const spec_ent *want)
+{
+  const int g0 = g_slot_grp[s], i0 = g_slot_idx[s];
+  int n = 0, g, g1;
+  (void)mb;
+  g_chain_head = -1;
+  if (i0 + 1 < g_grp_n[g0]) {                       /* the rest of s's group, s first */
+    chain_fill(&g_chains[n++], currMB, list, ref, g0, i0, want);
+    g_chain_head = s;
+  }
+  g1 = g0 <= 2 ? 6 : 3 + 4 * ((g0 - 3) / 4) + 3;   /* through quadrant 0 / through s's quadrant */
+  for (g = g0 + 1; g <= g1 && n < 8; g++)
+    if (g_grp_n[g] > 1 || g0 <= 2) chain_fill(&g_chains[n++], currMB, list, ref, g, 0, want);
+  return n;
+}
+
+/* the chains' answers -> way KHYP of their (macroblock, slot) */
+static void store_chains(int list, int ref, const spec_ent *want)
+{
+  spec_ent *tab = g_spec[list][ref];
+  int i, k;
+  for (i = 0; i < g_n_chains; i++) {
+    const jmme_chain *c = &g_chains[i];
+    const int mb = (c->mb_y >> 4) * g_mbs_x + (c->mb_x >> 4);
+    ++g_chain_sent;
+    for (k = 0; k < c->n_steps; k++) {
+      const jmme_chain_res *r = &g_chres[i * JMME_CHAIN_MAX_STEPS + k];
+      const int sl = c->steps[k].slot;
+      spec_ent *e = &tab[((size_t)mb * JMME_NSLOT + sl) * KWAYS + KHYP];
+      if (r->cost < 0) break;
+      memset(e, 0, sizeof *e);
+      e->mode = want->mode;
+      e->px = r->pred_x; e->py = r->pred_y;
+      e->lambda = want->lambda;
+      if (want->mode) {
+        e->sr = r->range_max;
+        e->fcx = c->ffs_center_x; e->fcy = c->ffs_center_y; e->frange = c->ffs_range;
+      } else {
+        e->cx = r->center_x; e->cy = r->center_y;
+        e->sr = r->range_min;
+      }
+      e->mvx = r->mv_x; e->mvy = r->mv_y; e->cost = r->cost;
+      e->valid = g_slot_gen[list][ref];
+      ++g_chain_steps;
+      /* the chain's first step is the missing call itself: its derived inputs must be the real ones */
+      if (i == 0 && k == 0 && sl == g_chain_head && !spec_key_eq(e, want)) ++g_chain_head_bad;
+    }
+  }
+  g_n_chains = 0;
 }
 
 /* one batched search: all 41 partitions of macroblocks mb0.., under every distinct guess */
@@ -362,8 +539,9 @@ static void spec_batch(int list, int ref, int mb0, const spec_ent *want, int chk
     }
   }
   t1 = now_us();
-  if (jmme_search_mbs(g_me, want->mode ? JMME_FAST_FULL_SEARCH : JMME_FULL_SEARCH, g_req, nreq, g_res))
-    fail_jm("jmme_search_mbs");
+  if (jmme_search_mbs_chains(g_me, want->mode ? JMME_FAST_FULL_SEARCH : JMME_FULL_SEARCH, g_req, nreq, g_res,
+                             g_chains, g_n_chains, g_chres))
+    fail_jm("jmme_search_mbs_chains");
   t2 = now_us();
   g_t_build += t1 - t0;
   g_t_call += t2 - t1;
@@ -373,7 +551,7 @@ static void spec_batch(int list, int ref, int mb0, const spec_ent *want, int chk
     mb = g_req_mb[i];
     k = (i == 0 || g_req_mb[i - 1] != mb) ? 0 : k + 1;       /* guesses of one MB are consecutive */
     for (s = 0; s < JMME_NSLOT; s++) {
-      spec_ent *e = &tab[((size_t)mb * JMME_NSLOT + s) * KHYP + k];
+      spec_ent *e = &tab[((size_t)mb * JMME_NSLOT + s) * KWAYS + k];
       *e = g_hyp[(size_t)i * JMME_NSLOT + s];
       e->mvx = g_res[i * JMME_NSLOT + s].mv_x;
       e->mvy = g_res[i * JMME_NSLOT + s].mv_y;
@@ -382,10 +560,11 @@ static void spec_batch(int list, int ref, int mb0, const spec_ent *want, int chk
     }
     if (i + 1 == nreq || g_req_mb[i + 1] != mb)               /* drop older guesses of this MB */
       for (s = 0; s < JMME_NSLOT; s++)
-        for (h = k + 1; h < KHYP; h++) tab[((size_t)mb * JMME_NSLOT + s) * KHYP + h].valid = 0;
+        for (h = k + 1; h < KHYP; h++) tab[((size_t)mb * JMME_NSLOT + s) * KWAYS + h].valid = 0;
   }
   g_spec_end[list][ref] = mb0 + n;
   ++g_batches;
+  store_chains(list, ref, want);
 }
 
 static int speculating(void)
@@ -411,10 +590,11 @@ static const spec_ent *spec_lookup(Macroblock *currMB, MEBlock *mv_block, int li
   if (s < 0 || mb < 0 || mb >= g_n_mb) error("jm_gpu_me: block outside the picture", 500);
   g_seen[list][ref][(size_t)mb * JMME_NSLOT + s] = *want;
   g_seen[list][ref][(size_t)mb * JMME_NSLOT + s].valid = g_slot_gen[list][ref];
-  e = &tab[((size_t)mb * JMME_NSLOT + s) * KHYP];
-  for (k = 0; k < KHYP; k++)
+  e = &tab[((size_t)mb * JMME_NSLOT + s) * KWAYS];
+  for (k = 0; k < KWAYS; k++)
     if (spec_same(&e[k], want, g_slot_gen[list][ref])) {
       ++g_hits;
+      if (k == KHYP) ++g_chain_hits;
       return &e[k];
     }
   if (mb < g_spec_end[list][ref]) {                                      /* every guess failed */
@@ -424,7 +604,7 @@ static const spec_ent *spec_lookup(Macroblock *currMB, MEBlock *mv_block, int li
     if (g_trace_miss) {   /* JMME_TRACE_MISS: the inputs that missed and the guesses held for them */
       fprintf(g_trace_miss, "miss mb %d slot %d want c(%d,%d) p(%d,%d) sr %d chk %d lam %d |", mb, s, want->cx, want->cy,
               want->px, want->py, want->sr, want->chk, want->lambda);
-      for (k = 0; k < KHYP; k++)
+      for (k = 0; k < KWAYS; k++)
         if (e[k].valid == g_slot_gen[list][ref])
           fprintf(g_trace_miss, " g%d c(%d,%d) p(%d,%d) sr %d chk %d lam %d", k, e[k].cx, e[k].cy, e[k].px, e[k].py,
                   e[k].sr, e[k].chk, e[k].lambda);
@@ -434,6 +614,7 @@ static const spec_ent *spec_lookup(Macroblock *currMB, MEBlock *mv_block, int li
     g_batch = imin(2048, g_batch * 2);
     ++g_miss_past;
   }
+  g_n_chains = chains_on(currMB, list, ref) ? build_chains(currMB, list, ref, mb, s, want) : 0;
   spec_batch(list, ref, mb, want, chk_rule, currMB->p_Inp->rdopt);
   if (!spec_same(&e[0], want, g_slot_gen[list][ref])) error("jm_gpu_me: batch lost its own request", 500);
   return &e[0];
@@ -662,7 +843,7 @@ static void sp_batch(int list, int ref, int mb0, int s0, const sp_ent *w, int t8
   for (mb = mb0; mb < mb1; mb++)
     for (s = 0; s < JMME_NSLOT; s++)
       for (k = 0; k < KHYP; k++) {
-        const spec_ent *ie = &itab[((size_t)mb * JMME_NSLOT + s) * KHYP + k];
+        const spec_ent *ie = &itab[((size_t)mb * JMME_NSLOT + s) * KWAYS + k];
         sp_ent g = *w;
         if (ie->valid != g_slot_gen[list][ref]) continue;
         g.px = ie->px;
@@ -711,7 +892,7 @@ static void prefault_tables(VideoParameters *p_Vid, InputParameters *p_Inp)
 {
   if (p_Vid->width <= 0 || p_Vid->height <= 0) return;
   spec_table(p_Vid, 0, 0);
-  memset(g_spec[0][0], 0, (size_t)g_n_mb * JMME_NSLOT * KHYP * sizeof(spec_ent));
+  memset(g_spec[0][0], 0, (size_t)g_n_mb * JMME_NSLOT * KWAYS * sizeof(spec_ent));
   memset(g_seen[0][0], 0, (size_t)g_n_mb * JMME_NSLOT * sizeof(spec_ent));
   if (!p_Inp->DisableSubpelME[0]) sp_table(p_Vid, 0, 0);
 }
@@ -1181,6 +1362,9 @@ static void report(void)
       for (s = 0; s < JMME_NSLOT; s++) fprintf(stderr, " %lld", g_miss_slot[s]);
       fprintf(stderr, "\n");
     }
+    if (g_chain_sent)
+      fprintf(stderr, "jm_gpu_me: chained guesses: %lld chains, %lld steps, %lld calls answered, %lld head mismatches\n",
+              g_chain_sent, g_chain_steps, g_chain_hits, g_chain_head_bad);
     if (g_epzs_calls || g_epzs_cpu)
       fprintf(stderr, "jm_gpu_me: %lld EPZS searches on the GPU (libjmme), one call each; %lld on the CPU; "
                       "%lld predictors, %lld pre-stamped map cells, %lld switches to window scans; "

@@ -13,7 +13,9 @@ sys.path.insert(0, "--h.264-by-zhaodongyu_amd"); sys.path.insert(0, "tests")
 from jmme import synth
 from test_jm_dropin_gpu import CFG
 d = sys.argv[1]
-synth.write_yuv420(os.path.join(d, "in.yuv"), synth.luma_sequence(1920, 1080, 2, seed=2024, gmv=(5, 3)))
+adv = os.environ.get("ADV") == "1"   # per-macroblock random motion
+synth.write_yuv420(os.path.join(d, "in.yuv"), synth.luma_sequence(1920, 1080, 2, seed=2024, gmv=(0, 0) if adv else (5, 3),
+                                                                  adversarial=adv))
 open(os.path.join(d, "enc.cfg"), "w").write(CFG)
 PY
 args="-d $d/enc.cfg -p InputFile=$d/in.yuv -p SourceWidth=1920 -p SourceHeight=1080 -p OutputWidth=1920

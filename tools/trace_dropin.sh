@@ -1,5 +1,5 @@
 #!/bin/bash
-# The drop-in encoder (1080p, 2 frames, FS by default: MODE) with its speculation
+# The drop-in encoder (1080p, 2 frames, FS by default: MODE; ADV=1 adversarial motion) with its speculation
 # traced: per batch (JMME_TRACE) and per failed guess (JMME_TRACE_MISS).  GPU box.
 set -e
 cd "$(dirname "$0")/.."
@@ -12,7 +12,9 @@ sys.path.insert(0, "--h.264-by-zhaodongyu_amd"); sys.path.insert(0, "tests")
 from jmme import synth
 from test_jm_dropin_gpu import CFG
 d = sys.argv[1]
-synth.write_yuv420(os.path.join(d, "in.yuv"), synth.luma_sequence(1920, 1080, 2, seed=2024, gmv=(5, 3)))
+adv = os.environ.get("ADV") == "1"   # per-macroblock random motion (SURVEY §8(d) adversarial variant)
+synth.write_yuv420(os.path.join(d, "in.yuv"), synth.luma_sequence(1920, 1080, 2, seed=2024, gmv=(0, 0) if adv else (5, 3),
+                                                                  adversarial=adv))
 open(os.path.join(d, "enc.cfg"), "w").write(CFG)
 PY
 JMME_TRACE=$PWD/$out/batches.txt JMME_TRACE_MISS=$PWD/$out/misses.txt timeout -k 10 300 \
