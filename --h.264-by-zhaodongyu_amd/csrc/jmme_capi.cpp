@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -105,14 +106,35 @@ struct jmme_ctx {
   jmme_block_res *h_sout = nullptr;
   size_t cap_sout = 0;
   jmme_chain_res *h_chres = nullptr;         // jmme_search_mbs_chains results (mapped pinned)
-  hipStream_t chain_stream = nullptr;        // chains run beside the batch of the same call (non-blocking)
   unsigned long long *h_hkeys = nullptr;    // small latency form: per-tile keys (mapped pinned)
   size_t cap_hkeys = 0;
   uint8_t *h_emap = nullptr;                 // jmme_epzs_search_ex: mapped pinned request / result block
   size_t cap_emap = 0;
   unsigned long long *d_skeys = nullptr;     // per (item, tile) keys, cap_skeys * JMME_NSLOT
   size_t cap_skeys = 0;
+  hipStream_t chain_stream = nullptr;        // chains run beside the batch of the same call (non-blocking)
+  std::vector<SmallItem> small_scratch;      // search_small's items (kept: no allocation per call)
+  void *dv_hkeys = nullptr, *dv_chres = nullptr, *dv_sitems = nullptr, *dv_sout = nullptr;   // device views
+  std::vector<uint8_t *> spare_planes;       // jmme_reserve: plane buffers the first uploads take
+  size_t spare_bytes = 0;                    // their size (taken only by uploads of that size)
+  // JMME_PHASES=1: host-side phase times of the latency calls, printed at jmme_destroy
+  bool phases = false;
+  double ph_us[12] = {};
+  long long ph_calls = 0, ph_big = 0;
 };
+
+namespace {
+double now_us() {
+  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+// adds the time since *t to ctx->ph_us[i] and restarts *t (JMME_PHASES only)
+inline void phase(jmme_ctx *ctx, int i, double *t) {
+  if (!ctx->phases) return;
+  const double n = now_us();
+  ctx->ph_us[i] += n - *t;
+  *t = n;
+}
+}  // namespace
 
 DevGuard::DevGuard(const jmme_ctx *c) {
   int cur = 0;
@@ -279,6 +301,10 @@ extern "C" jmme_ctx *jmme_create(const jmme_config *cfg, int device) {
     if (e != hipSuccess) { fail("hipSetDevice(%d): %s", device, hipGetErrorString(e)); delete ctx; return nullptr; }
   }
   (void)hipGetDevice(&ctx->device);
+  {
+    const char *ph = getenv("JMME_PHASES");
+    ctx->phases = ph && *ph && *ph != '0';
+  }
   // allocations below go to ctx->device; the caller's current device is restored on return
   struct Restore {
     int d, was;
@@ -298,8 +324,21 @@ extern "C" jmme_ctx *jmme_create(const jmme_config *cfg, int device) {
 extern "C" void jmme_destroy(jmme_ctx *ctx) {
   DevGuard dg_(ctx);
   if (!ctx) return;
+  if (ctx->phases && ctx->ph_calls) {
+    static const char *names[12] = {"chains: validate+launch", "small: items", "small: launch", "small: sync",
+                                    "small: host finish", "chains: sync+copy", "big: validate", "big: stage+launch",
+                                    "big: sync", "big: scatter", "", ""};
+    fprintf(stderr, "jmme phases over %lld chained calls (us per call):", ctx->ph_calls);
+    for (int i = 0; i < 6; ++i)
+      if (ctx->ph_us[i] > 0) fprintf(stderr, " %s %.2f;", names[i], ctx->ph_us[i] / ctx->ph_calls);
+    fprintf(stderr, "\njmme phases over %lld throughput-path calls (us per call):", ctx->ph_big);
+    for (int i = 6; i < 10; ++i)
+      if (ctx->ph_us[i] > 0) fprintf(stderr, " %s %.2f;", names[i], ctx->ph_us[i] / std::max(1ll, ctx->ph_big));
+    fprintf(stderr, "\n");
+  }
   (void)hipFree(ctx->d_cur);
   for (auto *p : ctx->d_refs) (void)hipFree(p);
+  for (auto *p : ctx->spare_planes) (void)hipFree(p);
   (void)hipFree(ctx->d_ref_table);
   (void)hipFree(ctx->d_req);
   (void)hipFree(ctx->d_out);
@@ -366,6 +405,10 @@ int upload_plane(jmme_ctx *ctx, uint8_t **dst, const jmme_imgpel *const *rows, i
     if (m > (unsigned)ctx->max_pel)
       return fail("sample above %d in row %d (SourceBitDepthLuma %d)", ctx->max_pel, y, ctx->cfg.SourceBitDepthLuma);
   }
+  if (!*dst && !ctx->spare_planes.empty() && ctx->spare_bytes == bytes) {   // the size jmme_reserve expected
+    *dst = ctx->spare_planes.back();
+    ctx->spare_planes.pop_back();
+  }
   if (!*dst) HIPCHK(hipMalloc(dst, bytes));
   // complete before the staging buffer is refilled by the next upload
   HIPCHK(hipMemcpyAsync(*dst, ctx->h_stage, bytes, hipMemcpyHostToDevice, nullptr));
@@ -415,7 +458,7 @@ int ensure_units(jmme_ctx *ctx, size_t n) {
   (void)hipFree(ctx->d_out);
   ctx->d_req = nullptr;
   ctx->d_out = nullptr;
-  size_t cap = n < 1024 ? 1024 : n;
+  size_t cap = std::max<size_t>({n, 1024, 2 * ctx->cap_units});   // geometric: few reallocations while batches grow
   HIPCHK(hipMalloc(&ctx->d_req, cap * sizeof(jmme_mb_req)));
   HIPCHK(hipMalloc(&ctx->d_out, cap * JMME_NSLOT * sizeof(jmme_block_res)));
   ctx->cap_units = cap;
@@ -427,7 +470,7 @@ int ensure_items(jmme_ctx *ctx, size_t n) {
   if (n <= ctx->cap_items) return 0;
   (void)hipFree(ctx->d_items);
   ctx->d_items = nullptr;
-  size_t cap = n < 4096 ? 4096 : n;
+  size_t cap = std::max<size_t>({n, 4096, 2 * ctx->cap_items});
   HIPCHK(hipMalloc(&ctx->d_items, cap * sizeof(Item)));
   ctx->cap_items = cap;
   return 0;
@@ -612,7 +655,8 @@ void small_items(const jmme_ctx *ctx, int mode, const jmme_mb_req *req, int n, s
 int search_small(jmme_ctx *ctx, int mode, const jmme_mb_req *req, int n, jmme_block_res *out, hipStream_t s,
                  bool force = false) {
   if (ctx->small_max_wg <= 0 && !force) return 0;
-  std::vector<SmallItem> items;
+  double t_ph = ctx->phases ? now_us() : 0;
+  std::vector<SmallItem> &items = ctx->small_scratch;
   int max_r = 0;
   small_items(ctx, mode, req, n, items, &max_r);
   const int tiles = (2 * max_r + 1 + kSmallTile - 1) / kSmallTile;
@@ -628,6 +672,7 @@ int search_small(jmme_ctx *ctx, int mode, const jmme_mb_req *req, int n, jmme_bl
     ctx->cap_sitems = 0;
     const size_t cap = std::max<size_t>(256, items.size());
     HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_sitems), cap * sizeof(SmallItem), hipHostMallocMapped));
+    HIPCHK(hipHostGetDevicePointer(&ctx->dv_sitems, ctx->h_sitems, 0));
     ctx->cap_sitems = cap;
   }
   if ((size_t)wgs > ctx->cap_skeys) {              // one key per (item, tile, partition)
@@ -644,6 +689,7 @@ int search_small(jmme_ctx *ctx, int mode, const jmme_mb_req *req, int n, jmme_bl
     ctx->cap_sout = 0;
     const size_t cap = std::max<size_t>(64 * JMME_NSLOT, (size_t)n * JMME_NSLOT);
     HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_sout), cap * sizeof(jmme_block_res), hipHostMallocMapped));
+    HIPCHK(hipHostGetDevicePointer(&ctx->dv_sout, ctx->h_sout, 0));
     ctx->cap_sout = cap;
   }
   SmallParams p{};
@@ -677,13 +723,17 @@ int search_small(jmme_ctx *ctx, int mode, const jmme_mb_req *req, int n, jmme_bl
       const size_t cap = std::max<size_t>(64 * 1024, nk);
       HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_hkeys), cap * sizeof(unsigned long long),
                            hipHostMallocMapped));
+      HIPCHK(hipHostGetDevicePointer(&ctx->dv_hkeys, ctx->h_hkeys, 0));
       ctx->cap_hkeys = cap;
     }
-    HIPCHK(hipHostGetDevicePointer(&d_hkeys, ctx->h_hkeys, 0));
+    d_hkeys = ctx->dv_hkeys;
     p.host_finish = 1;
     p.keys = static_cast<unsigned long long *>(d_hkeys);
+    phase(ctx, 1, &t_ph);
     HIPCHK(launch_search_small(p, s));
+    phase(ctx, 2, &t_ph);
     HIPCHK(hipStreamSynchronize(s));
+    phase(ctx, 3, &t_ph);
     ctx->timed = false;
     const bool ffs = mode == JMME_FAST_FULL_SEARCH;
     for (size_t ii = 0; ii < items.size(); ++ii) {
@@ -709,21 +759,26 @@ int search_small(jmme_ctx *ctx, int mode, const jmme_mb_req *req, int n, jmme_bl
         r.cost = (int64_t)(k >> 32);
       }
     }
+    phase(ctx, 4, &t_ph);
     return 1;
   }
   std::memcpy(ctx->h_sitems, items.data(), items.size() * sizeof(SmallItem));
-  HIPCHK(hipHostGetDevicePointer(&d_items, ctx->h_sitems, 0));
-  HIPCHK(hipHostGetDevicePointer(&d_sout, ctx->h_sout, 0));
+  d_items = ctx->dv_sitems;
+  d_sout = ctx->dv_sout;
   p.items = static_cast<const SmallItem *>(d_items);
   p.keys = ctx->d_skeys;
   p.info = reinterpret_cast<int4 *>(ctx->d_skeys + ctx->cap_skeys * JMME_NSLOT);   // items <= workgroups <= cap
   p.out = static_cast<jmme_block_res *>(d_sout);
+  phase(ctx, 1, &t_ph);
   HIPCHK(launch_search_small(p, s));
+  phase(ctx, 2, &t_ph);
   HIPCHK(hipStreamSynchronize(s));
+  phase(ctx, 3, &t_ph);
   ctx->timed = false;
   for (int i = 0; i < n; ++i)
     for (int sl = 0; sl < JMME_NSLOT; ++sl)
       if ((req[i].slot_mask >> sl) & 1) out[(size_t)i * JMME_NSLOT + sl] = ctx->h_sout[(size_t)i * JMME_NSLOT + sl];
+  phase(ctx, 4, &t_ph);
   return 1;
 }
 
@@ -741,6 +796,7 @@ extern "C" int jmme_search_mbs(jmme_ctx *ctx, int mode, const jmme_mb_req *req, 
   if (!ctx->d_cur) return fail("current picture not uploaded");
   if (n == 0) return 0;
   if (!req || !out) return fail("null request/result array");
+  double t_ph = ctx->phases ? now_us() : 0;
   if (validate(ctx, mode, req, n)) return -1;
   hipStream_t s = nullptr;
   // a batch of a few units: the low-latency path (one launch, no copies)
@@ -749,6 +805,8 @@ extern "C" int jmme_search_mbs(jmme_ctx *ctx, int mode, const jmme_mb_req *req, 
     const int r = search_small(ctx, mode, req, n, out, s, ctx->hbd);
     if (r != 0) return r < 0 ? -1 : 0;
   }
+  if (ctx->phases) ++ctx->ph_big;
+  phase(ctx, 6, &t_ph);
   if (ensure_units(ctx, (size_t)n)) return -1;
   if (sync_ref_table(ctx, s)) return -1;
   // pinned staging: [requests | results | status words]
@@ -765,11 +823,14 @@ extern "C" int jmme_search_mbs(jmme_ctx *ctx, int mode, const jmme_mb_req *req, 
   HIPCHK(hipMemcpyAsync(ctx->h_pin + rq, ctx->d_out, (size_t)n * JMME_NSLOT * sizeof(jmme_block_res),
                         hipMemcpyDeviceToHost, s));
   HIPCHK(hipMemcpyAsync(ctx->h_pin + rq + rs, ctx->d_counts, 3 * sizeof(unsigned), hipMemcpyDeviceToHost, s));
+  phase(ctx, 7, &t_ph);
   HIPCHK(hipStreamSynchronize(s));
+  phase(ctx, 8, &t_ph);
   if (status_words(st, ctx)) return -1;
   for (int i = 0; i < n; ++i)
     for (int sl = 0; sl < JMME_NSLOT; ++sl)
       if ((req[i].slot_mask >> sl) & 1) out[(size_t)i * JMME_NSLOT + sl] = tmp[(size_t)i * JMME_NSLOT + sl];
+  phase(ctx, 9, &t_ph);
   return 0;
 }
 
@@ -811,10 +872,10 @@ int launch_chains(jmme_ctx *ctx, int mode, const jmme_chain *chains, int n, hipS
   if (!ctx->h_chres) {
     HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_chres), kChainInline * JMME_CHAIN_MAX_STEPS *
                                                                       sizeof(jmme_chain_res), hipHostMallocMapped));
+    HIPCHK(hipHostGetDevicePointer(&ctx->dv_chres, ctx->h_chres, 0));
   }
   std::memset(ctx->h_chres, 0, nres * sizeof(jmme_chain_res));
-  void *d_res = nullptr;
-  HIPCHK(hipHostGetDevicePointer(&d_res, ctx->h_chres, 0));
+  void *d_res = ctx->dv_chres;
   if (sync_ref_table(ctx, s)) return -1;
   p.cur = ctx->d_cur;
   p.refs = ctx->d_ref_table;
@@ -840,12 +901,19 @@ extern "C" int jmme_search_mbs_chains(jmme_ctx *ctx, int mode, const jmme_mb_req
   if (n_chains < 0 || (n_chains && (!chains || !res))) return fail("null chain array");
   if (n_chains == 0) return jmme_search_mbs(ctx, mode, req, n, out);
   if (!ctx->chain_stream) HIPCHK(hipStreamCreateWithFlags(&ctx->chain_stream, hipStreamNonBlocking));
-  // the chains run on their own stream beside the batch (which syncs the null stream)
+  double t_ph = ctx->phases ? now_us() : 0;
+  if (ctx->phases) ++ctx->ph_calls;
+  // the chains run on their own stream beside the batch (which syncs the null
+  // stream).  On one stream, one after the other, the call took longer
+  // (JMME_PHASES, 1080p drop-in: 51 us waiting, against 29 + 12 on two streams)
   if (launch_chains(ctx, mode, chains, n_chains, ctx->chain_stream)) return -1;
+  phase(ctx, 0, &t_ph);
   const int rc = n ? jmme_search_mbs(ctx, mode, req, n, out) : 0;
+  if (ctx->phases) t_ph = now_us();
   HIPCHK(hipStreamSynchronize(ctx->chain_stream));
   if (rc) return rc;
   std::memcpy(res, ctx->h_chres, (size_t)n_chains * JMME_CHAIN_MAX_STEPS * sizeof(jmme_chain_res));
+  phase(ctx, 5, &t_ph);
   return 0;
 }
 
@@ -1826,13 +1894,15 @@ extern "C" int jmme_prepare(jmme_ctx *ctx) {
   r.mb_y = 16;
   r.slot_mask = 1;
   r.blk[0].search_range = (int16_t)std::min(1, ctx->cfg.SearchRange);
+  r.ffs_range = r.blk[0].search_range;
   HIPCHK(dreq.alloc(sizeof r));
   HIPCHK(hipMemcpy(dreq.p, &r, sizeof r, hipMemcpyHostToDevice));
   HIPCHK(dout.alloc(JMME_NSLOT * sizeof(jmme_block_res)));
-  if (launch(ctx, JMME_FULL_SEARCH, static_cast<const uint8_t *>(plane.p), static_cast<const uint8_t *const *>(table.p),
-             kW, kW, kH, static_cast<const jmme_mb_req *>(dreq.p), 1, static_cast<jmme_block_res *>(dout.p), nullptr,
-             nullptr, true))
-    return -1;
+  for (int mode : {JMME_FULL_SEARCH, JMME_FAST_FULL_SEARCH})
+    if (launch(ctx, mode, static_cast<const uint8_t *>(plane.p), static_cast<const uint8_t *const *>(table.p), kW, kW,
+               kH, static_cast<const jmme_mb_req *>(dreq.p), 1, static_cast<jmme_block_res *>(dout.p), nullptr, nullptr,
+               true))
+      return -1;
   // the small path reads the context's planes: borrow the dummy for one call
   uint8_t *cur = ctx->d_cur, *ref0 = ctx->d_refs[0];
   const int w = ctx->width, h = ctx->height, pitch = ctx->pitch;
@@ -1841,7 +1911,32 @@ extern "C" int jmme_prepare(jmme_ctx *ctx) {
   ctx->height = kH;
   ctx->pitch = kW;
   jmme_block_res res[JMME_NSLOT];
-  const int rc = search_small(ctx, JMME_FULL_SEARCH, &r, 1, res, nullptr, true);
+  int rc = 0;
+  for (int mode : {JMME_FULL_SEARCH, JMME_FAST_FULL_SEARCH})
+    if (rc >= 0) rc = search_small(ctx, mode, &r, 1, res, nullptr, true);
+  // the chain kernels, their stream and result block (jmme_search_mbs_chains)
+  if (rc >= 0 && !ctx->hbd) {
+    jmme_chain c;
+    std::memset(&c, 0, sizeof c);
+    c.mb_x = c.mb_y = 16;
+    c.n_steps = 1;
+    c.mv_lim_x0 = c.mv_lim_y0 = -512;
+    c.mv_lim_x1 = c.mv_lim_y1 = 511;
+    c.ffs_range = 1;
+    c.steps[0].slot = 0;
+    for (int j = 0; j < 3; ++j) c.steps[0].nb[j].src = JMME_NB_UNAVAILABLE;
+    c.steps[0].sr_min_x = c.steps[0].sr_min_y = -4;
+    c.steps[0].sr_max_x = c.steps[0].sr_max_y = 4;
+    const bool dirty = ctx->ref_table_dirty;
+    const uint8_t **rt = ctx->d_ref_table;
+    ctx->d_ref_table = static_cast<const uint8_t **>(table.p);
+    ctx->ref_table_dirty = false;
+    jmme_chain_res cres[JMME_CHAIN_MAX_STEPS];
+    for (int mode : {JMME_FULL_SEARCH, JMME_FAST_FULL_SEARCH})
+      if (rc >= 0 && jmme_search_mbs_chains(ctx, mode, &r, 0, res, &c, 1, cres)) rc = -1;
+    ctx->d_ref_table = rt;
+    ctx->ref_table_dirty = dirty;
+  }
   ctx->d_cur = cur;
   ctx->d_refs[0] = ref0;
   ctx->width = w;
@@ -1853,5 +1948,45 @@ extern "C" int jmme_prepare(jmme_ctx *ctx) {
   HIPCHK(launch_sub_images(static_cast<const uint8_t *>(plane.p), kW, kW, kH, static_cast<uint8_t *>(subs.p), g.pitch,
                            g.plane_stride, nullptr));
   HIPCHK(hipDeviceSynchronize());
+  return 0;
+}
+
+extern "C" int jmme_reserve(jmme_ctx *ctx, int max_units) {
+  DevGuard dg_(ctx);
+  if (!ctx) return fail("null ctx");
+  if (max_units < 0) return fail("negative unit count");
+  const size_t n = (size_t)max_units;
+  if (ensure_units(ctx, n) || ensure_items(ctx, n * JMME_NSLOT)) return -1;
+  const size_t rq = align64(n * sizeof(jmme_mb_req)), rs = align64(n * JMME_NSLOT * sizeof(jmme_block_res));
+  if (ensure_pin(ctx, rq + rs + 64)) return -1;
+  // the configured picture's planes: the staging buffer and device planes for
+  // the current picture and every reference of list 0, taken by the first uploads
+  const int w = ctx->cfg.SourceWidth, h = ctx->cfg.SourceHeight;
+  if (w > 0 && h > 0 && !(w & 15) && !(h & 15) && (!ctx->width || (ctx->width == w && ctx->height == h))) {
+    const size_t bytes = (size_t)((w + 63) & ~63) * h * (ctx->hbd ? 2 : 1);   // set_geometry's pitch
+    if (bytes > ctx->cap_stage) {
+      if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
+      ctx->h_stage = nullptr;
+      ctx->cap_stage = 0;
+      HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_stage), bytes, hipHostMallocDefault));
+      ctx->cap_stage = bytes;
+    }
+    const int planes = 1 + std::min(std::max(ctx->cfg.NumberReferenceFrames, 1), kMaxRefs);
+    if (ctx->spare_bytes != bytes) {
+      for (auto *p : ctx->spare_planes) (void)hipFree(p);
+      ctx->spare_planes.clear();
+      ctx->spare_bytes = bytes;
+    }
+    while ((int)ctx->spare_planes.size() < planes) {
+      uint8_t *d = nullptr;
+      HIPCHK(hipMalloc(&d, bytes));
+      ctx->spare_planes.push_back(d);
+    }
+    // one plane-sized copy: the first large host-to-device copy of a process
+    // sets up its DMA path (~8 ms measured inside the first P picture's ME time)
+    std::memset(ctx->h_stage, 0, bytes);
+    HIPCHK(hipMemcpyAsync(ctx->spare_planes.back(), ctx->h_stage, bytes, hipMemcpyHostToDevice, nullptr));
+    HIPCHK(hipStreamSynchronize(nullptr));
+  }
   return 0;
 }

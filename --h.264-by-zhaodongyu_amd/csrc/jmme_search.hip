@@ -1721,6 +1721,15 @@ __device__ __forceinline__ int imedian3(int a, int b, int c) {
   return a > b ? (b > c ? b : (a > c ? c : a)) : (a > c ? a : (b > c ? c : b));
 }
 
+#ifdef JMME_CHAIN_PROF
+// diagnostic builds: block 0's phase times (100 MHz realtime; [30], [31] shader
+// clocks at start / end), read with jmme_debug_chain_prof
+__device__ unsigned long long g_chain_prof[32];
+#define CPROF(i) do { if (blockIdx.x == 0 && tid == 0) g_chain_prof[i] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define CPROF(i) do { } while (0)
+#endif
+
 template <bool FFS>
 __global__ __launch_bounds__(kChainWG) void chain_kernel(ChainParams p) {
   extern __shared__ uint32_t dyn[];
@@ -1728,10 +1737,26 @@ __global__ __launch_bounds__(kChainWG) void chain_kernel(ChainParams p) {
   __shared__ int s_d[8];                          // px, py, cqx, cqy, R, rs, ok
   __shared__ int s_mv[JMME_CHAIN_MAX_STEPS][2];   // the steps' vectors as the next steps read them
   __shared__ uint32_t s_minc[kChainWaves], s_minr[kChainWaves];
-  const jmme_chain &c = p.chains[blockIdx.x];
+  __shared__ jmme_chain s_chain;                          // this chain, copied out of the kernel arguments once
+  __shared__ jmme_chain_res s_out[JMME_CHAIN_MAX_STEPS];  // written to the caller's mapped memory at the end
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#ifdef JMME_CHAIN_PROF
+  if (blockIdx.x == 0 && tid == 0) g_chain_prof[30] = __builtin_amdgcn_s_memtime();
+#endif
+  CPROF(0);
+  {
+    // one parallel round of dword loads instead of a dependent scalar load per
+    // field (the kernel arguments may sit in host memory)
+    constexpr int kWords = sizeof(jmme_chain) / 4;
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(&p.chains[blockIdx.x]);
+    uint32_t *dst = reinterpret_cast<uint32_t *>(&s_chain);
+    if (tid >= 64 && tid < 64 + kWords) dst[tid - 64] = src[tid - 64];
+  }
+  __syncthreads();
+  CPROF(1);
+  const jmme_chain &c = s_chain;
   const uint8_t *ref = p.refs[c.list * kMaxRefs + c.ref_idx];
-  jmme_chain_res *out = p.res + (size_t)blockIdx.x * JMME_CHAIN_MAX_STEPS;
+  jmme_chain_res *out = s_out;
   if (tid < 64)
     s_cur[tid] = *reinterpret_cast<const uint32_t *>(p.cur + (size_t)(c.mb_y + (tid >> 2)) * p.pitch + c.mb_x +
                                                      4 * (tid & 3));
@@ -1817,6 +1842,7 @@ __global__ __launch_bounds__(kChainWG) void chain_kernel(ChainParams p) {
       s_d[6] = s_d[4] >= 0 && s_d[4] <= p.max_r && s_d[5] >= 0 && !((s_d[2] | s_d[3]) & 3);
     }
     __syncthreads();
+    CPROF(2 + 4 * k);
     const int px = s_d[0], py = s_d[1], cqx = s_d[2], cqy = s_d[3], R = s_d[4], rs = s_d[5];
     alive = alive && s_d[6];
     if (!alive) {   // this step and the rest: no answer
@@ -1854,6 +1880,7 @@ __global__ __launch_bounds__(kChainWG) void chain_kernel(ChainParams p) {
       }
       __syncthreads();
     }
+    CPROF(3 + 4 * k);
     // every position of the window: (cost << 32 | rank), eligible ones only
     GroupCtx g{};
     g.R = R; g.rs = rs; g.cqx = cqx; g.cqy = cqy; g.px = px; g.py = py; g.lam = c.lambda; g.max_mvd = p.max_mvd;
@@ -1883,6 +1910,7 @@ __global__ __launch_bounds__(kChainWG) void chain_kernel(ChainParams p) {
       if (lane == 0) { s_minc[wave] = cmin; s_minr[wave] = rmin; }
     }
     __syncthreads();
+    CPROF(4 + 4 * k);
     if (tid == 0) {
       uint32_t bcost = s_minc[0], brank = s_minr[0];
 #pragma unroll
@@ -1895,7 +1923,13 @@ __global__ __launch_bounds__(kChainWG) void chain_kernel(ChainParams p) {
       s_mv[k][1] = clampi(r.mv_y, c.mv_lim_y0, c.mv_lim_y1);
     }
     __syncthreads();
+    CPROF(5 + 4 * k);
   }
+  if (tid < c.n_steps) p.res[(size_t)blockIdx.x * JMME_CHAIN_MAX_STEPS + tid] = s_out[tid];
+  CPROF(18);
+#ifdef JMME_CHAIN_PROF
+  if (blockIdx.x == 0 && tid == 0) g_chain_prof[31] = __builtin_amdgcn_s_memtime();
+#endif
 }
 
 
@@ -1920,6 +1954,14 @@ int resident_grid(Occupancy &o, int dev, int variant, K kernel, int lds_range, s
 }  // namespace
 
 size_t items_lds_bytes(int R) { return lds_plan(R).total; }
+
+#ifdef JMME_CHAIN_PROF
+}  // namespace jmme
+extern "C" int jmme_debug_chain_prof(unsigned long long *out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(jmme::g_chain_prof), sizeof jmme::g_chain_prof) == hipSuccess ? 0 : -1;
+}
+namespace jmme {
+#endif
 
 #ifdef JMME_ELIM_COUNT
 }  // namespace jmme

@@ -209,6 +209,10 @@ int jmme_set_small_batch_limit(jmme_ctx *ctx, int max_workgroups);
  * launch; occupancy queries are cached on first use) with a search on a dummy
  * plane, so that the first real search is not charged for them.  Optional. */
 int jmme_prepare(jmme_ctx *ctx);
+/* Size the synchronous batch path's device and pinned host buffers for batches
+ * of up to `max_units` units now (they otherwise grow on demand, each growth a
+ * device allocation inside some search call).  Optional. */
+int jmme_reserve(jmme_ctx *ctx, int max_units);
 
 /* Device-resident variant for pipelines and the benchmark: d_req/d_out are
  * device pointers, planes are those already uploaded; enqueued on `stream`

@@ -14,36 +14,49 @@ sys.path.insert(0, os.path.join(REPO, "--h.264-by-zhaodongyu_amd"))
 sys.path.insert(0, os.path.join(REPO, "tests"))
 
 
-def main():
-    from jmme import FULL_SEARCH, MB_REQ, MotionEstimator, synth
-    from jmme._lib import CHAIN
+W, H, R = 1920, 1088, 32
+SLOTS = {1: [5], 2: [9, 11], 4: [25, 26, 29, 30]}
+
+
+def setup():
+    from jmme import MotionEstimator, synth
     from test_gpu_parity import _random_units
-    w, h, R = 1920, 1088, 32
-    luma = synth.luma_sequence(w, h, 2, seed=5, gmv=(0, 0), adversarial=True)
-    rng = np.random.default_rng(1)
-    slots = {1: [5], 2: [9, 11], 4: [25, 26, 29, 30]}
+    luma = synth.luma_sequence(W, H, 2, seed=5, gmv=(0, 0), adversarial=True)
+    me = MotionEstimator({"SearchRange": R, "SearchMode": -1, "RDOptimization": 0})
+    me.upload_cur(luma[1])
+    me.upload_ref(0, 0, luma[0])
+    return me, _random_units(np.random.default_rng(1), W, H, 1, R)
+
+
+def make_chains(steps, n_chains, r=R):
+    """n_chains chains of `steps` steps (slots SLOTS[steps]) with fixed neighbours, range r"""
+    from jmme._lib import CHAIN
+    ch = np.zeros(n_chains, CHAIN)
+    for i in range(n_chains):
+        ch[i]["mb_x"], ch[i]["mb_y"] = 16 * (5 + i), 16 * 7
+        ch[i]["n_steps"] = steps
+        ch[i]["lambda"] = 100
+        ch[i]["mv_lim_x0"], ch[i]["mv_lim_x1"], ch[i]["mv_lim_y0"], ch[i]["mv_lim_y1"] = -2048, 2047, -512, 511
+        for k, s in enumerate(SLOTS[steps]):
+            st = ch[i]["steps"][k]
+            st["slot"] = s
+            for j in range(3):
+                st["nb"][j]["src"] = k - 1 if (k and j == 0) else -2
+                st["nb"][j]["mv_x"], st["nb"][j]["mv_y"] = 4 * (3 * j - 2), 4 * (j - 1)
+            st["sr_min_x"] = st["sr_min_y"] = -4 * r
+            st["sr_max_x"] = st["sr_max_y"] = 4 * r
+            ch[i]["steps"][k] = st
+    return ch
+
+
+def main():
+    from jmme import FULL_SEARCH, MB_REQ
     out = []
-    with MotionEstimator({"SearchRange": R, "SearchMode": -1, "RDOptimization": 0}) as me:
-        me.upload_cur(luma[1])
-        me.upload_ref(0, 0, luma[0])
-        unit = _random_units(rng, w, h, 1, R)
-        for steps, sl in slots.items():
+    me, unit = setup()
+    with me:
+        for steps in SLOTS:
             for n_chains in (1, 4):
-                ch = np.zeros(n_chains, CHAIN)
-                for i in range(n_chains):
-                    ch[i]["mb_x"], ch[i]["mb_y"] = 16 * (5 + i), 16 * 7
-                    ch[i]["n_steps"] = steps
-                    ch[i]["lambda"] = 100
-                    ch[i]["mv_lim_x0"], ch[i]["mv_lim_x1"], ch[i]["mv_lim_y0"], ch[i]["mv_lim_y1"] = -2048, 2047, -512, 511
-                    for k, s in enumerate(sl):
-                        st = ch[i]["steps"][k]
-                        st["slot"] = s
-                        for j in range(3):
-                            st["nb"][j]["src"] = k - 1 if (k and j == 0) else -2
-                            st["nb"][j]["mv_x"], st["nb"][j]["mv_y"] = 4 * (3 * j - 2), 4 * (j - 1)
-                        st["sr_min_x"] = st["sr_min_y"] = -4 * R
-                        st["sr_max_x"] = st["sr_max_y"] = 4 * R
-                        ch[i]["steps"][k] = st
+                ch = make_chains(steps, n_chains)
                 for batch in (False, True):
                     req = unit if batch else np.zeros(0, MB_REQ)
                     for _ in range(20):
@@ -54,6 +67,14 @@ def main():
                         me.search_chains(FULL_SEARCH, req, ch)
                     us = (time.perf_counter() - t0) / n * 1e6
                     out.append({"steps": steps, "chains": n_chains, "with_batch": batch, "us_per_call": round(us, 1)})
+        # fixed costs: one step at range 1 (a 3x3 window)
+        ch = make_chains(1, 1, r=1)
+        for _ in range(20):
+            me.search_chains(FULL_SEARCH, np.zeros(0, MB_REQ), ch)
+        t0 = time.perf_counter()
+        for _ in range(300):
+            me.search_chains(FULL_SEARCH, np.zeros(0, MB_REQ), ch)
+        out.append({"steps": 1, "chains": 1, "range": 1, "us_per_call": round((time.perf_counter() - t0) / 300 * 1e6, 1)})
         # the batch alone, for reference
         for _ in range(20):
             me.search(FULL_SEARCH, unit)
