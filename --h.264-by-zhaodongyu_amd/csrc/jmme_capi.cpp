@@ -655,6 +655,10 @@ void small_items(const jmme_ctx *ctx, int mode, const jmme_mb_req *req, int n, s
 int search_small(jmme_ctx *ctx, int mode, const jmme_mb_req *req, int n, jmme_block_res *out, hipStream_t s,
                  bool force = false) {
   if (ctx->small_max_wg <= 0 && !force) return 0;
+  // the latency form is for a few units (the drop-in's re-batches): larger
+  // batches go to the throughput path without building their items here
+  constexpr int kSmallMaxUnits = 32;
+  if (n > kSmallMaxUnits && !force) return 0;
   double t_ph = ctx->phases ? now_us() : 0;
   std::vector<SmallItem> &items = ctx->small_scratch;
   int max_r = 0;
@@ -827,9 +831,15 @@ extern "C" int jmme_search_mbs(jmme_ctx *ctx, int mode, const jmme_mb_req *req, 
   HIPCHK(hipStreamSynchronize(s));
   phase(ctx, 8, &t_ph);
   if (status_words(st, ctx)) return -1;
-  for (int i = 0; i < n; ++i)
+  constexpr uint64_t kAll = (1ull << JMME_NSLOT) - 1;
+  for (int i = 0; i < n; ++i) {
+    if ((req[i].slot_mask & kAll) == kAll) {
+      std::memcpy(&out[(size_t)i * JMME_NSLOT], &tmp[(size_t)i * JMME_NSLOT], JMME_NSLOT * sizeof(jmme_block_res));
+      continue;
+    }
     for (int sl = 0; sl < JMME_NSLOT; ++sl)
       if ((req[i].slot_mask >> sl) & 1) out[(size_t)i * JMME_NSLOT + sl] = tmp[(size_t)i * JMME_NSLOT + sl];
+  }
   phase(ctx, 9, &t_ph);
   return 0;
 }
@@ -860,6 +870,8 @@ int launch_chains(jmme_ctx *ctx, int mode, const jmme_chain *chains, int n, hipS
     for (int k = 0; k < c.n_steps; ++k) {
       const jmme_chain_step &st = c.steps[k];
       if (st.slot < 0 || st.slot >= JMME_NSLOT) return fail("chain %d step %d: slot %d", i, k, st.slot);
+      if ((st.flags & ~JMME_CHAIN_CHECK00) || ((st.flags & JMME_CHAIN_CHECK00) && st.slot != 0))
+        return fail("chain %d step %d: flags %d (check_for_00 is a 16x16 step's)", i, k, st.flags);
       for (int j = 0; j < 3; ++j)
         if (st.nb[j].src < JMME_NB_FIXED || st.nb[j].src >= k)
           return fail("chain %d step %d: neighbour source %d", i, k, st.nb[j].src);

@@ -1730,23 +1730,136 @@ __device__ unsigned long long g_chain_prof[32];
 #define CPROF(i) do { } while (0)
 #endif
 
+// a step's predictor, centre and ranges from its neighbours and the earlier
+// steps' vectors (mv[j] for j < k): computed by every thread (uniform values,
+// no barrier to hand them out)
+struct ChainStepIn {
+  int px, py, cx, cy, rmin, rmax;
+};
+
+__device__ __forceinline__ ChainStepIn chain_derive(const jmme_chain &c, const jmme_chain_step &st, const int (&mvx)[4],
+                                                    const int (&mvy)[4], int max_mvd) {
+  const SlotGeom sg = slot_geom(st.slot);
+  const int bsx = 4 * sg.w, bsy = 4 * sg.h;
+  // neighbours: (available, ref_idx, mv)
+  int av[3], rf[3], mx[3], my[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const jmme_chain_nb nb = st.nb[j];
+    av[j] = nb.src != JMME_NB_UNAVAILABLE;
+    if (nb.src >= 0) {
+      const int q = nb.src;   // < k <= 3
+      rf[j] = c.ref_idx;
+      mx[j] = q == 0 ? mvx[0] : q == 1 ? mvx[1] : mvx[2];
+      my[j] = q == 0 ? mvy[0] : q == 1 ? mvy[1] : mvy[2];
+    } else {
+      rf[j] = nb.ref_idx; mx[j] = nb.mv_x; my[j] = nb.mv_y;
+    }
+  }
+  const int r = c.ref_idx;
+  const int rL = av[0] ? rf[0] : -1, rU = av[1] ? rf[1] : -1, rUR = av[2] ? rf[2] : -1;
+  int type = 0;   // 0 median, 1 L, 2 U, 3 UR
+  if (rL == r && rU != r && rUR != r) type = 1;
+  else if (rL != r && rU == r && rUR != r) type = 2;
+  else if (rL != r && rU != r && rUR == r) type = 3;
+  if (bsx == 8 && bsy == 16) {
+    if (sg.bx == 0) { if (rL == r) type = 1; }
+    else { if (rUR == r) type = 3; }
+  } else if (bsx == 16 && bsy == 8) {
+    if (sg.by == 0) { if (rU == r) type = 2; }
+    else { if (rL == r) type = 1; }
+  }
+  int px = 0, py = 0;
+  if (type == 0) {
+    if (!(av[1] || av[2])) {
+      if (av[0]) { px = mx[0]; py = my[0]; }
+    } else {
+      px = imedian3(av[0] ? mx[0] : 0, av[1] ? mx[1] : 0, av[2] ? mx[2] : 0);
+      py = imedian3(av[0] ? my[0] : 0, av[1] ? my[1] : 0, av[2] ? my[2] : 0);
+    }
+  } else {
+    const int j = type - 1;
+    if (av[j]) { px = mx[j]; py = my[j]; }
+  }
+  px = (int16_t)px; py = (int16_t)py;
+  // BlockMotionSearch's centre: JM_INT_DIVIDE rounding, the (0,0)-inside clip
+  // with CheckSearchRange when RDO is off, then the level's vector range
+  int cx = (int16_t)(((px + 2) >> 2) * 4), cy = (int16_t)(((py + 2) >> 2) * 4);
+  int mnx = st.sr_min_x, mxx = st.sr_max_x, mny = st.sr_min_y, mxy = st.sr_max_y;
+  if (!c.rdopt) {
+    const int ccx = cx, ccy = cy;
+    cx = clampi(cx, mnx, mxx);
+    cy = clampi(cy, mny, mxy);
+    if (cx != ccx || cy != ccy) {
+      const int md = max_mvd - 2;
+      int left = cx + mnx, right = cx + mxx, top = cy + mny, down = cy + mxy;
+      left = clampi(left, ccx - md, ccx + md);
+      right = clampi(right, ccx - md, ccx + md);
+      top = clampi(top, ccy - md, ccy + md);
+      down = clampi(down, ccy - md, ccy + md);
+      if (left < right && top < down) {
+        cx = (int16_t)((left + right) >> 1);
+        cy = (int16_t)((top + down) >> 1);
+        mnx = left - cx; mxx = min(cx - left, right - cx);
+        mny = top - cy; mxy = min(cy - top, down - cy);
+      } else {
+        cx = ccx; cy = ccy;
+      }
+    }
+  }
+  ChainStepIn o;
+  o.px = px; o.py = py;
+  o.cx = clampi(cx, c.mv_lim_x0, c.mv_lim_x1);
+  o.cy = clampi(cy, c.mv_lim_y0, c.mv_lim_y1);
+  o.rmin = min(mxx, mxy) >> 2;
+  o.rmax = max(mxx, mxy) >> 2;
+  return o;
+}
+
+// every position of the (2R+1)^2 window for a W x H (4x4 units) partition at
+// (BX, BY): this thread's best (cost, rank)
+template <bool FFS, int W, int H>
+__device__ __forceinline__ void chain_sweep(const GroupCtx &g, const uint32_t *words, int wpr, const uint32_t *s_cur,
+                                            int bx, int by, int tid, uint32_t &bc, uint32_t &br) {
+  const int R = g.R, D = 2 * R + 1;
+  const float inv = 1.0f / (float)D;
+  for (int i = tid; i < D * D; i += kChainWG) {
+    int iy = (int)((float)i * inv);               // i / D, corrected (exact for i < 2^22)
+    iy -= iy * D > i;
+    iy += (iy + 1) * D <= i;
+    const int oy = iy - R, ox = i - iy * D - R;
+    const int candx = g.cqx + 4 * ox, candy = g.cqy + 4 * oy;
+    const bool is00 = candx == 0 && candy == 0;
+    const MvCost mc = mv_cost<FFS>(candx, candy, g.px, g.py, g.lam, g.max_mvd);
+    if (!pos_eligible<FFS>(g, mc.ok, max(abs(ox), abs(oy)), is00)) continue;
+    const uint32_t mvc = g.chk00 ? check00_adjust(mc.mvc, g.lam, is00) : mc.mvc;
+    uint32_t sad = 0;
+    const uint32_t *wb = words + (oy + R + 4 * by) * wpr + (ox + R + 4 * bx);
+#pragma unroll
+    for (int r = 0; r < 4 * H; ++r)
+#pragma unroll
+      for (int wc = 0; wc < W; ++wc)
+        sad = __builtin_amdgcn_sad_u8(wb[r * wpr + 4 * wc], s_cur[(4 * by + r) * 4 + bx + wc], sad);
+    const int sidx = spiral_index_bl(ox, oy);
+    const uint32_t rank = FFS ? ((g.preseed && is00) ? 0u : (uint32_t)sidx + 1u) : (uint32_t)sidx;
+    const uint32_t cost = (sad << 5) + mvc;
+    if (cost < bc || (cost == bc && rank < br)) { bc = cost; br = rank; }
+  }
+}
+
 template <bool FFS>
 __global__ __launch_bounds__(kChainWG) void chain_kernel(ChainParams p) {
   extern __shared__ uint32_t dyn[];
   __shared__ uint32_t s_cur[64];
-  __shared__ int s_d[8];                          // px, py, cqx, cqy, R, rs, ok
-  __shared__ int s_mv[JMME_CHAIN_MAX_STEPS][2];   // the steps' vectors as the next steps read them
-  __shared__ uint32_t s_minc[kChainWaves], s_minr[kChainWaves];
-  __shared__ jmme_chain s_chain;                          // this chain, copied out of the kernel arguments once
-  __shared__ jmme_chain_res s_out[JMME_CHAIN_MAX_STEPS];  // written to the caller's mapped memory at the end
+  __shared__ uint32_t s_minc[2][kChainWaves], s_minr[2][kChainWaves];   // by step parity: one barrier per step
+  __shared__ jmme_chain s_chain;                                         // out of the kernel arguments once
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 #ifdef JMME_CHAIN_PROF
   if (blockIdx.x == 0 && tid == 0) g_chain_prof[30] = __builtin_amdgcn_s_memtime();
 #endif
   CPROF(0);
   {
-    // one parallel round of dword loads instead of a dependent scalar load per
-    // field (the kernel arguments may sit in host memory)
+    // one parallel round of dword loads instead of a dependent scalar load per field
     constexpr int kWords = sizeof(jmme_chain) / 4;
     const uint32_t *src = reinterpret_cast<const uint32_t *>(&p.chains[blockIdx.x]);
     uint32_t *dst = reinterpret_cast<uint32_t *>(&s_chain);
@@ -1755,99 +1868,34 @@ __global__ __launch_bounds__(kChainWG) void chain_kernel(ChainParams p) {
   __syncthreads();
   CPROF(1);
   const jmme_chain &c = s_chain;
+  const int n_steps = c.n_steps;
   const uint8_t *ref = p.refs[c.list * kMaxRefs + c.ref_idx];
-  jmme_chain_res *out = s_out;
   if (tid < 64)
     s_cur[tid] = *reinterpret_cast<const uint32_t *>(p.cur + (size_t)(c.mb_y + (tid >> 2)) * p.pitch + c.mb_x +
                                                      4 * (tid & 3));
+  // every thread holds the steps' vectors (as the next steps read them) and,
+  // for thread 0's final write, their results
+  int mvx[4] = {0, 0, 0, 0}, mvy[4] = {0, 0, 0, 0};
+  jmme_chain_res res[4];
   bool alive = true;
   int staged_x = -0x40000000, staged_y = 0, staged_r = -1;   // the window in LDS (centre, range)
-  for (int k = 0; k < c.n_steps; ++k) {
-    const jmme_chain_step &st = c.steps[k];
-    const SlotGeom sg = slot_geom(st.slot);
-    const int bsx = 4 * sg.w, bsy = 4 * sg.h;
-    if (tid == 0) {
-      // neighbours: (available, ref_idx, mv)
-      int av[3], rf[3], mx[3], my[3];
 #pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        const jmme_chain_nb nb = st.nb[j];
-        av[j] = nb.src != JMME_NB_UNAVAILABLE;
-        if (nb.src >= 0) { rf[j] = c.ref_idx; mx[j] = s_mv[nb.src][0]; my[j] = s_mv[nb.src][1]; }
-        else { rf[j] = nb.ref_idx; mx[j] = nb.mv_x; my[j] = nb.mv_y; }
-      }
-      const int r = c.ref_idx;
-      const int rL = av[0] ? rf[0] : -1, rU = av[1] ? rf[1] : -1, rUR = av[2] ? rf[2] : -1;
-      int type = 0;   // 0 median, 1 L, 2 U, 3 UR
-      if (rL == r && rU != r && rUR != r) type = 1;
-      else if (rL != r && rU == r && rUR != r) type = 2;
-      else if (rL != r && rU != r && rUR == r) type = 3;
-      if (bsx == 8 && bsy == 16) {
-        if (sg.bx == 0) { if (rL == r) type = 1; }
-        else { if (rUR == r) type = 3; }
-      } else if (bsx == 16 && bsy == 8) {
-        if (sg.by == 0) { if (rU == r) type = 2; }
-        else { if (rL == r) type = 1; }
-      }
-      int px = 0, py = 0;
-      if (type == 0) {
-        if (!(av[1] || av[2])) {
-          if (av[0]) { px = mx[0]; py = my[0]; }
-        } else {
-          px = imedian3(av[0] ? mx[0] : 0, av[1] ? mx[1] : 0, av[2] ? mx[2] : 0);
-          py = imedian3(av[0] ? my[0] : 0, av[1] ? my[1] : 0, av[2] ? my[2] : 0);
-        }
-      } else {
-        const int j = type - 1;
-        if (av[j]) { px = mx[j]; py = my[j]; }
-      }
-      px = (int16_t)px; py = (int16_t)py;
-      // BlockMotionSearch's centre: JM_INT_DIVIDE rounding, the (0,0)-inside clip
-      // with CheckSearchRange when RDO is off, then the level's vector range
-      int cx = (int16_t)(((px + 2) >> 2) * 4), cy = (int16_t)(((py + 2) >> 2) * 4);
-      int mnx = st.sr_min_x, mxx = st.sr_max_x, mny = st.sr_min_y, mxy = st.sr_max_y;
-      if (!c.rdopt) {
-        const int ccx = cx, ccy = cy;
-        cx = clampi(cx, mnx, mxx);
-        cy = clampi(cy, mny, mxy);
-        if (cx != ccx || cy != ccy) {
-          const int md = p.max_mvd - 2;
-          int left = cx + mnx, right = cx + mxx, top = cy + mny, down = cy + mxy;
-          left = clampi(left, ccx - md, ccx + md);
-          right = clampi(right, ccx - md, ccx + md);
-          top = clampi(top, ccy - md, ccy + md);
-          down = clampi(down, ccy - md, ccy + md);
-          if (left < right && top < down) {
-            cx = (int16_t)((left + right) >> 1);
-            cy = (int16_t)((top + down) >> 1);
-            mnx = left - cx; mxx = min(cx - left, right - cx);
-            mny = top - cy; mxy = min(cy - top, down - cy);
-          } else {
-            cx = ccx; cy = ccy;
-          }
-        }
-      }
-      cx = clampi(cx, c.mv_lim_x0, c.mv_lim_x1);
-      cy = clampi(cy, c.mv_lim_y0, c.mv_lim_y1);
-      const int rmin = min(mxx, mxy) >> 2, rmax = max(mxx, mxy) >> 2;
-      out[k].pred_x = (int16_t)px; out[k].pred_y = (int16_t)py;
-      out[k].center_x = (int16_t)cx; out[k].center_y = (int16_t)cy;
-      out[k].range_min = (int16_t)rmin; out[k].range_max = (int16_t)rmax;
-      s_d[0] = px; s_d[1] = py;
-      s_d[2] = FFS ? c.ffs_center_x : cx;
-      s_d[3] = FFS ? c.ffs_center_y : cy;
-      s_d[4] = FFS ? c.ffs_range : rmin;
-      s_d[5] = FFS ? rmax : rmin;
-      // the window must fit the staged LDS and (FS) start on an integer vector
-      s_d[6] = s_d[4] >= 0 && s_d[4] <= p.max_r && s_d[5] >= 0 && !((s_d[2] | s_d[3]) & 3);
-    }
-    __syncthreads();
+  for (int k = 0; k < JMME_CHAIN_MAX_STEPS; ++k) {
+    if (k >= n_steps) break;
+    const jmme_chain_step &st = c.steps[k];
+    const ChainStepIn in = chain_derive(c, st, mvx, mvy, p.max_mvd);
+    const int cqx = FFS ? c.ffs_center_x : in.cx, cqy = FFS ? c.ffs_center_y : in.cy;
+    const int R = FFS ? c.ffs_range : in.rmin, rs = FFS ? in.rmax : in.rmin;
+    res[k].pred_x = (int16_t)in.px; res[k].pred_y = (int16_t)in.py;
+    res[k].center_x = (int16_t)in.cx; res[k].center_y = (int16_t)in.cy;
+    res[k].range_min = (int16_t)in.rmin; res[k].range_max = (int16_t)in.rmax;
+    res[k].mv_x = res[k].mv_y = 0;
     CPROF(2 + 4 * k);
-    const int px = s_d[0], py = s_d[1], cqx = s_d[2], cqy = s_d[3], R = s_d[4], rs = s_d[5];
-    alive = alive && s_d[6];
+    // the window must fit the staged LDS and (FS) start on an integer vector
+    alive = alive && R >= 0 && R <= p.max_r && rs >= 0 && !((cqx | cqy) & 3);
     if (!alive) {   // this step and the rest: no answer
-      if (tid == 0) { out[k].cost = -1; s_mv[k][0] = cqx; s_mv[k][1] = cqy; }
-      __syncthreads();
+      res[k].cost = -1;
+      mvx[k] = cqx; mvy[k] = cqy;
       continue;
     }
     // stage the window of the whole macroblock: words[y][x] = pels x..x+3 of
@@ -1881,51 +1929,49 @@ __global__ __launch_bounds__(kChainWG) void chain_kernel(ChainParams p) {
       __syncthreads();
     }
     CPROF(3 + 4 * k);
-    // every position of the window: (cost << 32 | rank), eligible ones only
     GroupCtx g{};
-    g.R = R; g.rs = rs; g.cqx = cqx; g.cqy = cqy; g.px = px; g.py = py; g.lam = c.lambda; g.max_mvd = p.max_mvd;
+    g.R = R; g.rs = rs; g.cqx = cqx; g.cqy = cqy; g.px = in.px; g.py = in.py; g.lam = c.lambda; g.max_mvd = p.max_mvd;
     g.preseed = FFS && c.ffs_pos00_valid;
-    const int D = 2 * R + 1;
+    g.chk00 = !FFS && st.slot == 0 && (st.flags & JMME_CHAIN_CHECK00);
+    const SlotGeom sg = slot_geom(st.slot);
     uint32_t bc = ~0u, br = ~0u;   // this thread's best (cost, rank)
-    for (int i = tid; i < D * D; i += kChainWG) {
-      const int oy = i / D - R, ox = i - (oy + R) * D - R;
-      const int candx = cqx + 4 * ox, candy = cqy + 4 * oy;
-      const bool is00 = candx == 0 && candy == 0;
-      const MvCost mc = mv_cost<FFS>(candx, candy, px, py, c.lambda, p.max_mvd);
-      if (!pos_eligible<FFS>(g, mc.ok, max(abs(ox), abs(oy)), is00)) continue;
-      uint32_t sad = 0;
-      const uint32_t *wb = words + (oy + R + 4 * sg.by) * wpr + (ox + R + 4 * sg.bx);
-      for (int r = 0; r < bsy; ++r)
-        for (int wc = 0; wc < sg.w; ++wc)
-          sad = __builtin_amdgcn_sad_u8(wb[r * wpr + 4 * wc], s_cur[(4 * sg.by + r) * 4 + sg.bx + wc], sad);
-      const int sidx = spiral_index_bl(ox, oy);
-      const uint32_t rank = FFS ? ((g.preseed && is00) ? 0u : (uint32_t)sidx + 1u) : (uint32_t)sidx;
-      const uint32_t cost = (sad << 5) + mc.mvc;
-      if (cost < bc || (cost == bc && rank < br)) { bc = cost; br = rank; }
+    switch (sg.bt) {
+      case 1: chain_sweep<FFS, 4, 4>(g, words, wpr, s_cur, sg.bx, sg.by, tid, bc, br); break;
+      case 2: chain_sweep<FFS, 4, 2>(g, words, wpr, s_cur, sg.bx, sg.by, tid, bc, br); break;
+      case 3: chain_sweep<FFS, 2, 4>(g, words, wpr, s_cur, sg.bx, sg.by, tid, bc, br); break;
+      case 4: chain_sweep<FFS, 2, 2>(g, words, wpr, s_cur, sg.bx, sg.by, tid, bc, br); break;
+      case 5: chain_sweep<FFS, 2, 1>(g, words, wpr, s_cur, sg.bx, sg.by, tid, bc, br); break;
+      case 6: chain_sweep<FFS, 1, 2>(g, words, wpr, s_cur, sg.bx, sg.by, tid, bc, br); break;
+      default: chain_sweep<FFS, 1, 1>(g, words, wpr, s_cur, sg.bx, sg.by, tid, bc, br); break;
     }
-    // wave minimum of the cost (DPP), then the smallest rank among its holders
+    // wave minimum of the cost (DPP), then the smallest rank among its holders;
+    // after the one barrier every thread combines the 16 waves itself
     {
       const uint32_t cmin = wave_min_u32(bc);
       const uint32_t rmin = wave_min_u32(bc == cmin ? br : ~0u);
-      if (lane == 0) { s_minc[wave] = cmin; s_minr[wave] = rmin; }
+      if (lane == 0) { s_minc[k & 1][wave] = cmin; s_minr[k & 1][wave] = rmin; }
     }
     __syncthreads();
     CPROF(4 + 4 * k);
-    if (tid == 0) {
-      uint32_t bcost = s_minc[0], brank = s_minr[0];
+    uint32_t bcost = s_minc[k & 1][0], brank = s_minr[k & 1][0];
 #pragma unroll
-      for (int w = 1; w < kChainWaves; ++w)
-        if (s_minc[w] < bcost || (s_minc[w] == bcost && s_minr[w] < brank)) { bcost = s_minc[w]; brank = s_minr[w]; }
-      const jmme_block_res r = block_result<FFS>(g, brank != ~0u, brank, bcost);
-      out[k].mv_x = r.mv_x; out[k].mv_y = r.mv_y; out[k].cost = r.cost;
-      // as BlockMotionSearch leaves it for the next partitions' predictors (mv_search.c:983)
-      s_mv[k][0] = clampi(r.mv_x, c.mv_lim_x0, c.mv_lim_x1);
-      s_mv[k][1] = clampi(r.mv_y, c.mv_lim_y0, c.mv_lim_y1);
+    for (int w = 1; w < kChainWaves; ++w) {
+      const uint32_t cw = s_minc[k & 1][w], rw = s_minr[k & 1][w];
+      if (cw < bcost || (cw == bcost && rw < brank)) { bcost = cw; brank = rw; }
     }
-    __syncthreads();
+    const jmme_block_res r = block_result<FFS>(g, brank != ~0u, brank, bcost);
+    res[k].mv_x = r.mv_x; res[k].mv_y = r.mv_y; res[k].cost = r.cost;
+    // as BlockMotionSearch leaves it for the next partitions' predictors (mv_search.c:983)
+    mvx[k] = clampi(r.mv_x, c.mv_lim_x0, c.mv_lim_x1);
+    mvy[k] = clampi(r.mv_y, c.mv_lim_y0, c.mv_lim_y1);
     CPROF(5 + 4 * k);
   }
-  if (tid < c.n_steps) p.res[(size_t)blockIdx.x * JMME_CHAIN_MAX_STEPS + tid] = s_out[tid];
+  if (tid == 0) {
+    jmme_chain_res *out = p.res + (size_t)blockIdx.x * JMME_CHAIN_MAX_STEPS;
+#pragma unroll
+    for (int k = 0; k < JMME_CHAIN_MAX_STEPS; ++k)
+      if (k < n_steps) out[k] = res[k];
+  }
   CPROF(18);
 #ifdef JMME_CHAIN_PROF
   if (blockIdx.x == 0 && tid == 0) g_chain_prof[31] = __builtin_amdgcn_s_memtime();

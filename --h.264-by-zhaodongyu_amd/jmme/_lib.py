@@ -30,7 +30,7 @@ MB_REQ = np.dtype([("mb_x", "<i2"), ("mb_y", "<i2"), ("list", "<i2"), ("ref_idx"
 BLOCK_RES = np.dtype([("mv_x", "<i2"), ("mv_y", "<i2"), ("reserved", "<i4"), ("cost", "<i8")])
 CHAIN_MAX_STEPS, NB_UNAVAILABLE, NB_FIXED = 4, -1, -2
 CHAIN_NB = np.dtype([("src", "<i2"), ("ref_idx", "<i2"), ("mv_x", "<i2"), ("mv_y", "<i2")])
-CHAIN_STEP = np.dtype([("slot", "<i2"), ("reserved", "<i2"), ("nb", CHAIN_NB, (3,)), ("sr_min_x", "<i2"),
+CHAIN_STEP = np.dtype([("slot", "<i2"), ("flags", "<i2"), ("nb", CHAIN_NB, (3,)), ("sr_min_x", "<i2"),
                        ("sr_max_x", "<i2"), ("sr_min_y", "<i2"), ("sr_max_y", "<i2")])
 CHAIN = np.dtype([("mb_x", "<i2"), ("mb_y", "<i2"), ("list", "<i2"), ("ref_idx", "<i2"), ("n_steps", "<i2"),
                   ("rdopt", "<i2"), ("ffs_center_x", "<i2"), ("ffs_center_y", "<i2"), ("ffs_range", "<i2"),

@@ -159,6 +159,7 @@ int jmme_search_mbs(jmme_ctx *ctx, int mode, const jmme_mb_req *req, int n, jmme
 #define JMME_CHAIN_MAX_STEPS 4
 #define JMME_NB_UNAVAILABLE (-1)
 #define JMME_NB_FIXED (-2)
+#define JMME_CHAIN_CHECK00 1   /* jmme_chain_step.flags: check_for_00 (a 16x16 step, FS, me_fullsearch.c:61) */
 
 typedef struct jmme_chain_nb {
   int16_t src;                 /* JMME_NB_UNAVAILABLE, JMME_NB_FIXED, or k >= 0: step k's result */
@@ -168,7 +169,7 @@ typedef struct jmme_chain_nb {
 
 typedef struct jmme_chain_step {
   int16_t slot;                /* partition (jmme_slot) */
-  int16_t reserved;
+  int16_t flags;               /* JMME_CHAIN_CHECK00 */
   jmme_chain_nb nb[3];         /* get_neighbors' block[0] (left), [1] (up), [2] (up-right, else up-left) */
   int16_t sr_min_x, sr_max_x;  /* mv_block->searchRange after get_search_range (qpel) */
   int16_t sr_min_y, sr_max_y;
@@ -198,8 +199,8 @@ typedef struct jmme_chain_res {
 int jmme_search_mbs_chains(jmme_ctx *ctx, int mode, const jmme_mb_req *req, int n, jmme_block_res *out,
                            const jmme_chain *chains, int n_chains, jmme_chain_res *res);
 
-/* jmme_search_mbs serves a batch whose work items (partition groups sharing a
- * window and predictor) fit in at most `max_workgroups` workgroups of 16x16
+/* jmme_search_mbs serves a batch of at most 32 units whose work items (partition
+ * groups sharing a window and predictor) fit in at most `max_workgroups` workgroups of 16x16
  * window positions by a single low-latency launch (no device copies, results
  * written to mapped host memory) -- the speculative batches of the JM drop-in
  * are mostly one or two macroblocks.  Default 4096; 0 sends everything down the

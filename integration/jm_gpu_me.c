@@ -244,7 +244,8 @@ static int g_batch = 64, g_speculate = -1, g_mbs_x = 0, g_n_mb = 0;
 static long long g_hits = 0, g_batches = 0;
 static jmme_mb_req *g_req = NULL;
 static jmme_block_res *g_res = NULL;
-static spec_ent *g_hyp = NULL;     /* the inputs behind each request's 41 slots */
+static spec_ent *g_hyp = NULL;     /* the upper-neighbour guesses (per macroblock) */
+static const spec_ent **g_req_row = NULL;   /* the inputs behind each request's 41 slots */
 static int *g_req_mb = NULL;
 static int g_req_cap = 0;
 
@@ -350,6 +351,8 @@ static int g_n_chains = 0, g_chain_on = -1, g_chain_head = -1;
 static int8_t g_slot_bt[JMME_NSLOT], g_slot_bx[JMME_NSLOT], g_slot_by[JMME_NSLOT];   /* slot_geometry() */
 static void slot_geometry(void);
 static long long g_chain_sent = 0, g_chain_steps = 0, g_chain_hits = 0, g_chain_head_bad = 0;
+static long long g_chain_calls = 0, g_chain_call_fail = 0;
+static int g_chain_only = -1;   /* JMME_CHAIN_ONLY=0: a failed guess always re-batches */
 static int8_t g_grp[19][4], g_grp_n[19], g_slot_grp[JMME_NSLOT], g_slot_idx[JMME_NSLOT];
 
 /* JM's search order of a macroblock's partitions as groups whose members chain:
@@ -422,6 +425,8 @@ static void chain_fill(jmme_chain *c, Macroblock *currMB, int list, int ref, int
     jmme_chain_step *st = &c->steps[k];
     PixelPos block[4];
     st->slot = (int16_t)sl;
+    /* check_for_00 as me_fullsearch.c:61 (chains: P slices, reference 0) */
+    st->flags = (int16_t)(!want->mode && sl == 0 && !p_Inp->rdopt ? JMME_CHAIN_CHECK00 : 0);
     get_neighbors(currMB, block, g_slot_bx[sl], g_slot_by[sl], bw[bt]);
     for (j = 0; j < 3; j++) {
       jmme_chain_nb *nb = &st->nb[j];
@@ -449,13 +454,13 @@ static void chain_fill(jmme_chain *c, Macroblock *currMB, int list, int ref, int
 }
 
 /* the chains that are decided at a miss of slot s of macroblock mb (the current one) */
-static int build_chains(Macroblock *currMB, int list, int ref, int mb, int s, const spec_ent *want)
+static int build_chains(Macroblock *currMB, int list, int ref, int mb, int s, const spec_ent *want, int with_s)
 {
   const int g0 = g_slot_grp[s], i0 = g_slot_idx[s];
   int n = 0, g, g1;
   (void)mb;
   g_chain_head = -1;
-  if (i0 + 1 < g_grp_n[g0]) {                       /* the rest of s's group, s first */
+  if (with_s || i0 + 1 < g_grp_n[g0]) {             /* the rest of s's group, s first */
     chain_fill(&g_chains[n++], currMB, list, ref, g0, i0, want);
     g_chain_head = s;
   }
@@ -489,6 +494,7 @@ static void store_chains(int list, int ref, const spec_ent *want)
       } else {
         e->cx = r->center_x; e->cy = r->center_y;
         e->sr = r->range_min;
+        e->chk = (int16_t)((c->steps[k].flags & JMME_CHAIN_CHECK00) != 0);
       }
       e->mvx = r->mv_x; e->mvy = r->mv_y; e->cost = r->cost;
       e->valid = g_slot_gen[list][ref];
@@ -507,35 +513,57 @@ static void reserve_batches(void)
 }
 
 /* one batched search: all 41 partitions of macroblocks mb0.., under every distinct guess */
+static int rows_eq(const spec_ent *a, const spec_ent *b)
+{
+  int s;
+  for (s = 0; s < JMME_NSLOT; s++)
+    if (!spec_key_eq(&a[s], &b[s])) return 0;
+  return 1;
+}
+
 static void spec_batch(int list, int ref, int mb0, const spec_ent *want, int chk00_slot0, int rdopt)
 {
+  static spec_ent hc[4][JMME_NSLOT];
+  int ok[4] = {0, 0, 0, 0};
   spec_ent *tab = g_spec[list][ref];
-  int n = imin(g_batch, g_n_mb - mb0), nreq = 0, i, s, h, k, mb;
+  int n = imin(g_batch, g_n_mb - mb0), nreq = 0, i, s, k, mb;
   double t0 = now_us(), t1, t2;
   if (n * KHYP > g_req_cap) {
     free(g_req);
     free(g_res);
     free(g_hyp);
     free(g_req_mb);
+    free(g_req_row);
     g_req_cap = n * KHYP;
     g_req = (jmme_mb_req *)malloc((size_t)g_req_cap * sizeof(jmme_mb_req));
     g_res = (jmme_block_res *)malloc((size_t)g_req_cap * JMME_NSLOT * sizeof(jmme_block_res));
     g_hyp = (spec_ent *)malloc((size_t)g_req_cap * JMME_NSLOT * sizeof(spec_ent));
     g_req_mb = (int *)malloc((size_t)g_req_cap * sizeof(int));
-    if (!g_req || !g_res || !g_hyp || !g_req_mb) error("jm_gpu_me: out of memory", 500);
+    g_req_row = (const spec_ent **)malloc((size_t)g_req_cap * sizeof(*g_req_row));
+    if (!g_req || !g_res || !g_hyp || !g_req_mb || !g_req_row) error("jm_gpu_me: out of memory", 500);
   }
+  /* guesses 0, 1 and 3 are the same rows for every macroblock of the batch
+   * (want; mb0's left neighbour; mb0 itself): built and compared once */
+  ok[0] = spec_hyp(list, ref, 0, mb0, mb0, want, chk00_slot0, hc[0]);
+  ok[1] = spec_hyp(list, ref, 1, mb0, mb0, want, chk00_slot0, hc[1]);
+  ok[3] = mb0 + 1 < g_n_mb && spec_hyp(list, ref, 3, mb0, mb0 + 1, want, chk00_slot0, hc[3]);
+  ok[1] = ok[1] && !rows_eq(hc[1], hc[0]);
+  ok[3] = ok[3] && !rows_eq(hc[3], hc[0]) && !(ok[1] && rows_eq(hc[3], hc[1]));
   for (mb = mb0; mb < mb0 + n; mb++) {
-    int first = nreq;
-    for (h = 0; h < KHYP; h++) {
-      spec_ent *hy = &g_hyp[(size_t)nreq * JMME_NSLOT];
-      jmme_mb_req *r = &g_req[nreq];
+    const spec_ent *rows[KHYP];
+    spec_ent *h2 = &g_hyp[(size_t)(mb - mb0) * JMME_NSLOT];
+    int nr = 0, j;
+    rows[nr++] = hc[0];
+    if (ok[1]) rows[nr++] = hc[1];
+    if (spec_hyp(list, ref, 2, mb0, mb, want, chk00_slot0, h2)) {
       int dup = 0;
-      if (!spec_hyp(list, ref, h, mb0, mb, want, chk00_slot0, hy)) continue;
-      for (k = first; k < nreq && !dup; k++) {
-        const spec_ent *o = &g_hyp[(size_t)k * JMME_NSLOT];
-        for (dup = 1, s = 0; s < JMME_NSLOT && dup; s++) dup = spec_key_eq(&o[s], &hy[s]);
-      }
-      if (dup) continue;
+      for (j = 0; j < nr && !dup; j++) dup = rows_eq(rows[j], h2);
+      if (!dup) rows[nr++] = h2;
+    }
+    if (mb > mb0 && ok[3] && !(nr > 1 && rows[nr - 1] == h2 && rows_eq(hc[3], h2))) rows[nr++] = hc[3];
+    for (j = 0; j < nr; j++) {
+      const spec_ent *hy = rows[j];
+      jmme_mb_req *r = &g_req[nreq];
       memset(r, 0, sizeof *r);
       r->mb_x = (int16_t)((mb % g_mbs_x) * 16);
       r->mb_y = (int16_t)((mb / g_mbs_x) * 16);
@@ -558,6 +586,7 @@ static void spec_batch(int list, int ref, int mb0, const spec_ent *want, int chk
         b->flags = (int16_t)(hy[s].chk ? JMME_BLK_CHECK00 : 0);
         b->lambda = hy[s].lambda;
       }
+      g_req_row[nreq] = hy;
       g_req_mb[nreq++] = mb;
     }
   }
@@ -577,7 +606,7 @@ static void spec_batch(int list, int ref, int mb0, const spec_ent *want, int chk
      * inputs on these planes, whichever batch searched it) */
     for (s = 0; s < JMME_NSLOT; s++) {
       spec_ent *e = &tab[spec_idx(mb, s, k)];
-      *e = g_hyp[(size_t)i * JMME_NSLOT + s];
+      *e = g_req_row[i][s];
       e->mvx = g_res[i * JMME_NSLOT + s].mv_x;
       e->mvy = g_res[i * JMME_NSLOT + s].mv_y;
       e->cost = g_res[i * JMME_NSLOT + s].cost;
@@ -628,8 +657,8 @@ static const spec_ent *spec_lookup(Macroblock *currMB, MEBlock *mv_block, int li
       return e;
     }
   }
-  if (mb < g_spec_end[list][ref]) {                                      /* every guess failed */
-    g_batch = imax(1, g_batch / 2);
+  const int failed = mb < g_spec_end[list][ref];
+  if (failed) {                                                          /* every guess failed */
     ++g_miss_guess;
     ++g_miss_slot[s];
     if (g_trace_miss) {   /* JMME_TRACE_MISS: the inputs that missed and the guesses held for them */
@@ -647,7 +676,27 @@ static const spec_ent *spec_lookup(Macroblock *currMB, MEBlock *mv_block, int li
     g_batch = imin(MAX_BATCH, g_batch * 2);
     ++g_miss_past;
   }
-  g_n_chains = chains_on(currMB, list, ref) ? build_chains(currMB, list, ref, mb, s, want) : 0;
+  if (g_chain_only < 0) {
+    const char *c = getenv("JMME_CHAIN_ONLY");
+    g_chain_only = !(c && c[0] == '0');
+  }
+  if (g_chain_only && failed && s != 0 && chains_on(currMB, list, ref)) {
+    /* a failed guess inside a macroblock whose 16x16 search hit: the
+     * macroblock's decided partitions as chains, the missing call first, and no
+     * batch (the guesses for the macroblocks after this one stand).  A 16x16
+     * miss says the guesses themselves are off: that one re-batches. */
+    g_n_chains = build_chains(currMB, list, ref, mb, s, want, 1);
+    if (jmme_search_mbs_chains(g_me, want->mode ? JMME_FAST_FULL_SEARCH : JMME_FULL_SEARCH, g_req, 0, g_res, g_chains,
+                               g_n_chains, g_chres))
+      fail_jm("jmme_search_mbs_chains");
+    ++g_chain_calls;
+    store_chains(list, ref, want);
+    e = &tab[spec_idx(mb, s, KHYP)];
+    if (spec_same(e, want, g_slot_gen[list][ref])) return e;
+    ++g_chain_call_fail;   /* (the chain stopped before it: a half-way centre or an oversized range) */
+  }
+  if (failed) g_batch = imax(1, g_batch / 2);   /* a re-batch after a failed guess: shorter */
+  g_n_chains = chains_on(currMB, list, ref) ? build_chains(currMB, list, ref, mb, s, want, 0) : 0;
   spec_batch(list, ref, mb, want, chk_rule, currMB->p_Inp->rdopt);
   e = &tab[spec_idx(mb, s, 0)];
   if (!spec_same(e, want, g_slot_gen[list][ref])) error("jm_gpu_me: batch lost its own request", 500);
@@ -1382,7 +1431,7 @@ static void report(void)
   if (g_me || g_cpu_calls || g_epzs_cpu) {
     fprintf(stderr, "jm_gpu_me: %lld integer-pel searches on the GPU (libjmme): %lld from %lld speculative "
                     "batches, the rest one call each; %lld on the CPU (non-SAD or weighted metric)\n",
-            g_calls, g_hits + g_batches, g_batches, g_cpu_calls);
+            g_calls, g_hits + g_batches + g_chain_calls - g_chain_call_fail, g_batches, g_cpu_calls);
     fprintf(stderr, "jm_gpu_me: %lld sub-pel refinements: %lld cached, %lld batches, %lld on the CPU\n",
             g_sp_calls, g_sp_hits, g_sp_batches, g_sp_cpu);
     if (g_batches) {
@@ -1397,8 +1446,9 @@ static void report(void)
       fprintf(stderr, "\n");
     }
     if (g_chain_sent)
-      fprintf(stderr, "jm_gpu_me: chained guesses: %lld chains, %lld steps, %lld calls answered, %lld head mismatches\n",
-              g_chain_sent, g_chain_steps, g_chain_hits, g_chain_head_bad);
+      fprintf(stderr, "jm_gpu_me: chained guesses: %lld chains, %lld steps, %lld calls answered, %lld head mismatches; "
+                      "%lld chain-only calls (%lld fell back to a batch)\n",
+              g_chain_sent, g_chain_steps, g_chain_hits, g_chain_head_bad, g_chain_calls, g_chain_call_fail);
     if (g_epzs_calls || g_epzs_cpu)
       fprintf(stderr, "jm_gpu_me: %lld EPZS searches on the GPU (libjmme), one call each; %lld on the CPU; "
                       "%lld predictors, %lld pre-stamped map cells, %lld switches to window scans; "

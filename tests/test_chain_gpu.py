@@ -96,7 +96,7 @@ def _random_chains(rng, w, h, n, R, rdopt, ffs):
     from jmme._lib import CHAIN
     ch = np.zeros(n, CHAIN)
     groups = [[2], [4], [5], [9, 11], [17, 18], [25, 26, 29, 30], [27, 28, 31, 32], [13, 15], [21, 22],
-              [33, 34, 37, 38], [6], [35, 36, 39, 40]]
+              [33, 34, 37, 38], [6], [35, 36, 39, 40], [0], [0, 1, 2]]
     for i in range(n):
         c = ch[i]
         c["mb_x"] = rng.integers(0, w // 16) * 16
@@ -114,6 +114,8 @@ def _random_chains(rng, w, h, n, R, rdopt, ffs):
         for k, slot in enumerate(g):
             st = c["steps"][k]
             st["slot"] = slot
+            if slot == 0 and not ffs and rng.random() < 0.7:
+                st["flags"] = 1   # JMME_CHAIN_CHECK00: check_for_00 (me_fullsearch.c:61)
             for j in range(3):
                 u = rng.random()
                 if k and u < 0.45:
@@ -140,6 +142,9 @@ def _step_req(chain, k, pred, centre, rng_min, rng_max, ffs):
     b = q["blk"][0, s]
     b["pred_x"], b["pred_y"] = pred
     b["lambda"] = chain["lambda"]
+    if chain["steps"][k]["flags"] & 1:
+        from jmme import BLK_CHECK00
+        b["flags"] = BLK_CHECK00
     if ffs:
         q["ffs_center_x"], q["ffs_center_y"] = chain["ffs_center_x"], chain["ffs_center_y"]
         q["ffs_range"], q["ffs_pos00_valid"] = chain["ffs_range"], chain["ffs_pos00_valid"]
@@ -226,6 +231,10 @@ def test_chain_requests_outside_contract_are_refused(gpu):
             bad[field] = val
             with pytest.raises(JmmeError):
                 me.search_chains(FULL_SEARCH, empty, bad)
+        bad = good.copy()
+        bad["steps"][0, 0]["flags"] = 1              # check_for_00 on a step that is not 16x16
+        with pytest.raises(JmmeError):
+            me.search_chains(FULL_SEARCH, empty, bad)
         bad = good.copy()
         bad["steps"][0, 0]["nb"][1]["src"] = 0      # a step cannot read itself
         with pytest.raises(JmmeError):

@@ -182,6 +182,8 @@ def _lencod(binary, d, tag, yuv, w, h, frames, params, cfg_text, env=None):
                    r"(\d+) pre-stamped map cells, (\d+) switches to window scans; ([\d.]+) ms in the EPZS wrapper, "
                    r"([\d.]+) ms in jmme_epzs_search_ex", r.stderr)
     esp = re.search(r"(\d+) EPZS sub-pel refinements on the GPU, (\d+) on the CPU", r.stderr)
+    ch = re.search(r"chained guesses: (\d+) chains, (\d+) steps, (\d+) calls answered, (\d+) head mismatches; "
+                   r"(\d+) chain-only calls \((\d+) fell back", r.stderr)
     res = dict(wall_s=round(wall, 3), me_s=float(me.group(1)) if me else None,
                md5=(hashlib.md5(open(out, "rb").read()).hexdigest(), hashlib.md5(open(rec, "rb").read()).hexdigest()))
     if calls:
@@ -191,6 +193,9 @@ def _lencod(binary, d, tag, yuv, w, h, frames, params, cfg_text, env=None):
         res.update(batches_past_end=int(stats.group(1)), batches_failed_guess=int(stats.group(2)),
                    batch_units=int(stats.group(3)), host_build_ms=float(stats.group(4)),
                    engine_call_ms=float(stats.group(5)))
+    if ch:
+        res["chains"] = dict(zip(("chains", "steps", "calls_answered", "head_mismatches", "chain_only_calls",
+                                  "chain_only_fallbacks"), map(int, ch.groups())))
     if sp:
         res["subpel"] = dict(zip(("calls", "cached", "batches", "cpu"), map(int, sp.groups())))
     if ep:

@@ -31,6 +31,24 @@ fi
 args="$args ${EXTRA:-}"
 timeout -k 10 300 rocprofv3 --kernel-trace --runtime-trace --stats --output-format csv -d $out -o run -- \
   "$PWD/integration/_build/lencod_jmme" $args > $out/lencod.log 2>&1
+# per-dispatch durations of the latency kernels (chain / small), summarised before the traces go
+python3 - $out <<'PY'
+import csv, glob, sys, collections
+import numpy as np
+out = sys.argv[1]
+for f in glob.glob(f"{out}/**/*kernel_trace.csv", recursive=True):
+    d = collections.defaultdict(list)
+    for r in csv.DictReader(open(f)):
+        n = r["Kernel_Name"]
+        k = "chain_kernel" if "chain_kernel" in n else "me_small_kernel" if "me_small_kernel" in n else None
+        if k:
+            d[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    with open(f"{out}/latency_kernels.txt", "w") as o:
+        for k, v in d.items():
+            v = np.array(v)
+            o.write(f"{k}: n {len(v)} mean {v.mean():.2f} us p50 {np.median(v):.2f} p90 {np.percentile(v, 90):.2f} "
+                    f"max {v.max():.2f}\n")
+PY
 # keep the summaries (the per-dispatch traces of a 1080p encode run to hundreds of MB)
 find $out -name "*.csv" ! -name "*stats.csv" -delete
 find $out -name "*stats.csv" | head
