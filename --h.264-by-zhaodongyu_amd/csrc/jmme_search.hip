@@ -1714,8 +1714,15 @@ __global__ __launch_bounds__(kWG) void small_finish_kernel(SmallParams p) {
 // (mv_search.c:983), is what the next steps read as that partition's vector.
 constexpr int kChainWG = 1024, kChainWaves = kChainWG / 64;
 
-__host__ __device__ inline int chain_wpr(int R) { return 2 * R + 13; }          // words per staged row (w = 4)
-__host__ __device__ inline int chain_raw(int R) { return (2 * R + 19 + 3) / 4 + 1; }   // raw dwords per row
+// The staged window may carry a margin of kChainMargin pels on every side, so
+// that a later step whose centre moved by up to that much searches the same
+// staging.  Measured in the 1080p drop-in: a 12-pel margin left the chain
+// kernel at 26.5 us (26.2 without) -- the larger first staging costs what the
+// avoided restagings save -- so none.
+constexpr int kChainMargin = 0;
+__host__ __device__ inline int chain_wpr(int R) { return 2 * R + 13 + 2 * kChainMargin; }   // words per staged row
+__host__ __device__ inline int chain_rows(int R) { return 2 * R + 16 + 2 * kChainMargin; }
+__host__ __device__ inline int chain_raw(int R) { return (chain_wpr(R) + 9) / 4 + 1; }   // raw dwords per row
 
 __device__ __forceinline__ int imedian3(int a, int b, int c) {
   return a > b ? (b > c ? b : (a > c ? c : a)) : (a > c ? a : (b > c ? c : b));
@@ -1817,33 +1824,41 @@ __device__ __forceinline__ ChainStepIn chain_derive(const jmme_chain &c, const j
 }
 
 // every position of the (2R+1)^2 window for a W x H (4x4 units) partition at
-// (BX, BY): this thread's best (cost, rank)
+// (BX, BY): this thread's best (cost, rank).  Thread t owns window column
+// t % D and every G-th row from t / D (G = 1024 / D row groups), so the column
+// part of the vector cost is formed once; the spiral rank -- which only breaks
+// ties -- is formed when a position ties the thread's best, and for the winner
+// at the end.
 template <bool FFS, int W, int H>
 __device__ __forceinline__ void chain_sweep(const GroupCtx &g, const uint32_t *words, int wpr, const uint32_t *s_cur,
                                             int bx, int by, int tid, uint32_t &bc, uint32_t &br) {
   const int R = g.R, D = 2 * R + 1;
-  const float inv = 1.0f / (float)D;
-  for (int i = tid; i < D * D; i += kChainWG) {
-    int iy = (int)((float)i * inv);               // i / D, corrected (exact for i < 2^22)
-    iy -= iy * D > i;
-    iy += (iy + 1) * D <= i;
-    const int oy = iy - R, ox = i - iy * D - R;
-    const int candx = g.cqx + 4 * ox, candy = g.cqy + 4 * oy;
+  const int G = kChainWG / D;                      // D <= 2 * kChainMaxR + 1 = 89 < 1024: G >= 11
+  const int col = tid % D, grp = tid / D;
+  if (grp >= G) return;
+  const int ox = col - R, candx = g.cqx + 4 * ox, dx = candx - g.px;
+  const uint32_t bits_x = (uint32_t)mvbits(dx);
+  for (int iy = grp; iy < D; iy += G) {
+    const int oy = iy - R, candy = g.cqy + 4 * oy, dy = candy - g.py;
     const bool is00 = candx == 0 && candy == 0;
-    const MvCost mc = mv_cost<FFS>(candx, candy, g.px, g.py, g.lam, g.max_mvd);
-    if (!pos_eligible<FFS>(g, mc.ok, max(abs(ox), abs(oy)), is00)) continue;
-    const uint32_t mvc = g.chk00 ? check00_adjust(mc.mvc, g.lam, is00) : mc.mvc;
+    if (FFS) {
+      const bool gate = max(abs(dx), abs(dy)) < g.max_mvd - 1;   // me_fullfast.c:663
+      if (!pos_eligible<FFS>(g, gate, max(abs(ox), abs(oy)), is00)) continue;
+    }
+    uint32_t mvc = (uint32_t)g.lam * (bits_x + (uint32_t)mvbits(dy));
+    if (g.chk00) mvc = check00_adjust(mvc, g.lam, is00);
     uint32_t sad = 0;
-    const uint32_t *wb = words + (oy + R + 4 * by) * wpr + (ox + R + 4 * bx);
+    const uint32_t *wb = words + (iy + 4 * by) * wpr + (col + 4 * bx);
 #pragma unroll
     for (int r = 0; r < 4 * H; ++r)
 #pragma unroll
       for (int wc = 0; wc < W; ++wc)
         sad = __builtin_amdgcn_sad_u8(wb[r * wpr + 4 * wc], s_cur[(4 * by + r) * 4 + bx + wc], sad);
+    const uint32_t cost = (sad << 5) + mvc;
+    if (cost > bc) continue;
     const int sidx = spiral_index_bl(ox, oy);
     const uint32_t rank = FFS ? ((g.preseed && is00) ? 0u : (uint32_t)sidx + 1u) : (uint32_t)sidx;
-    const uint32_t cost = (sad << 5) + mvc;
-    if (cost < bc || (cost == bc && rank < br)) { bc = cost; br = rank; }
+    if (cost < bc || rank < br) { bc = cost; br = rank; }
   }
 }
 
@@ -1878,7 +1893,7 @@ __global__ __launch_bounds__(kChainWG) void chain_kernel(ChainParams p) {
   int mvx[4] = {0, 0, 0, 0}, mvy[4] = {0, 0, 0, 0};
   jmme_chain_res res[4];
   bool alive = true;
-  int staged_x = -0x40000000, staged_y = 0, staged_r = -1;   // the window in LDS (centre, range)
+  int st_x = 0, st_y = 0, st_w = 0, st_h = 0;   // the staged window in LDS (origin, words per row, rows)
 #pragma unroll
   for (int k = 0; k < JMME_CHAIN_MAX_STEPS; ++k) {
     if (k >= n_steps) break;
@@ -1899,17 +1914,18 @@ __global__ __launch_bounds__(kChainWG) void chain_kernel(ChainParams p) {
       continue;
     }
     // stage the window of the whole macroblock: words[y][x] = pels x..x+3 of
-    // window row y, window origin (macroblock origin + centre - R), clamped into
-    // the picture; restaged only when the centre or range moves (FFS: once per chain)
-    const int wpr = chain_wpr(R), nraw = chain_raw(R), rows = 2 * R + 16;
-    uint32_t *words = dyn, *raw = dyn + (size_t)rows * wpr;
-    if (cqx != staged_x || cqy != staged_y || R != staged_r) {
-      staged_x = cqx; staged_y = cqy; staged_r = R;
-      const int X0 = c.mb_x + (cqx >> 2) - R, Y0 = c.mb_y + (cqy >> 2) - R;
-      const int xa = X0 & ~3, sh = X0 - xa;
+    // window row y, clamped into the picture (UMVLine4X), with a margin; a step
+    // whose window (origin: macroblock origin + centre - R) lies inside the
+    // staged one searches it in place (FFS: one staging per chain)
+    const int X0 = c.mb_x + (cqx >> 2) - R, Y0 = c.mb_y + (cqy >> 2) - R;
+    if (!(X0 >= st_x && Y0 >= st_y && X0 + 2 * R + 13 <= st_x + st_w && Y0 + 2 * R + 16 <= st_y + st_h)) {
+      st_x = X0 - kChainMargin; st_y = Y0 - kChainMargin; st_w = chain_wpr(R); st_h = chain_rows(R);
+      const int wpr = st_w, nraw = chain_raw(R), rows = st_h;
+      uint32_t *words = dyn, *raw = dyn + (size_t)rows * wpr;
+      const int xa = st_x & ~3, sh = st_x - xa, Y0s = st_y;
       for (int i = tid; i < rows * nraw; i += kChainWG) {
         const int r = i / nraw, q = i - r * nraw;
-        const uint8_t *row = ref + (size_t)clampi(Y0 + r, 0, p.height - 1) * p.pitch;
+        const uint8_t *row = ref + (size_t)clampi(Y0s + r, 0, p.height - 1) * p.pitch;
         const int x = xa + 4 * q;
         uint32_t w;
         if (x >= 0 && x + 3 < p.width) {
@@ -1928,6 +1944,8 @@ __global__ __launch_bounds__(kChainWG) void chain_kernel(ChainParams p) {
       }
       __syncthreads();
     }
+    const int wpr = st_w;
+    const uint32_t *words = dyn + (size_t)(Y0 - st_y) * wpr + (X0 - st_x);   // this step's window in the staging
     CPROF(3 + 4 * k);
     GroupCtx g{};
     g.R = R; g.rs = rs; g.cqx = cqx; g.cqy = cqy; g.px = in.px; g.py = in.py; g.lam = c.lambda; g.max_mvd = p.max_mvd;
@@ -2054,8 +2072,7 @@ hipError_t launch_search(const KParams &p, hipStream_t s, hipEvent_t ev0, hipEve
 }
 
 size_t chain_lds_bytes(int max_r) {
-  const int rows = 2 * max_r + 16;
-  return (size_t)rows * (chain_wpr(max_r) + chain_raw(max_r)) * 4;
+  return (size_t)chain_rows(max_r) * (chain_wpr(max_r) + chain_raw(max_r)) * 4;
 }
 
 hipError_t launch_search_chains(const ChainParams &p, hipStream_t s) {
