@@ -124,6 +124,7 @@ def lib() -> ctypes.CDLL:
         "jmme_search_status": (I, [P, P]),
         "jmme_set_small_batch_limit": (I, [P, I]),
         "jmme_prepare": (I, [P]),
+        "jmme_reserve": (I, [P, I]),
         "jmme_full_search_block": (ctypes.c_int64, [P, I, I, I, I, I, P, P, ctypes.c_int64, I, I, I]),
         "jmme_fast_full_search_block": (ctypes.c_int64, [P, I, I, I, I, I, P, P, I, I, I, P, ctypes.c_int64, I]),
         "jmme_last_kernel_ms": (ctypes.c_float, [P]),

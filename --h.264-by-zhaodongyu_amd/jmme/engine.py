@@ -130,6 +130,13 @@ class MotionEstimator:
         """Largest batch (in 16x16-position workgroups) `search` serves by the low-latency path; 0: never."""
         check(lib().jmme_set_small_batch_limit(self._ctx, int(max_workgroups)))
 
+    def prepare(self, max_units: int = 0) -> None:
+        """Pay start-up costs now (jmme_prepare: every kernel launched once) and, with
+        max_units, size the batch / staging / plane buffers (jmme_reserve)."""
+        check(lib().jmme_prepare(self._ctx))
+        if max_units:
+            check(lib().jmme_reserve(self._ctx, int(max_units)))
+
     def search_status(self, stream: int = 0) -> None:
         """Raise if the last device-request search refused a request (synchronises)."""
         check(lib().jmme_search_status(self._ctx, ctypes.c_void_p(stream)))

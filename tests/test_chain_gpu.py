@@ -241,3 +241,25 @@ def test_chain_requests_outside_contract_are_refused(gpu):
             me.search_chains(FULL_SEARCH, empty, bad)
         with pytest.raises(JmmeError):
             me.search_chains(FULL_SEARCH, empty, np.repeat(good, 9))
+
+
+def test_prepare_and_reserve_then_search(gpu):
+    """jmme_prepare (every kernel variant, chains included, on a dummy plane) and
+    jmme_reserve (buffers for the largest batch, plane buffers of the configured
+    size) leave the context as fresh: the first searches equal a plain context's"""
+    from jmme import FULL_SEARCH, MotionEstimator, synth
+    from test_gpu_parity import _random_units
+    w, h, R = 352, 288, 16
+    luma = synth.luma_sequence(w, h, 2, seed=11, gmv=(1, 2))
+    req = _random_units(np.random.default_rng(3), w, h, 40, R)
+    chains = _random_chains(np.random.default_rng(4), w, h, 4, R, 0, False)
+    res = []
+    for warm in (False, True):
+        with MotionEstimator({"SearchRange": R, "SearchMode": -1, "SourceWidth": w, "SourceHeight": h}) as me:
+            if warm:
+                me.prepare(max_units=256)
+            me.upload_cur(luma[1])
+            me.upload_ref(0, 0, luma[0])
+            res.append((me.search(FULL_SEARCH, req), *me.search_chains(FULL_SEARCH, req[:2], chains)))
+    for a, b in zip(*res):
+        assert np.array_equal(a, b)
