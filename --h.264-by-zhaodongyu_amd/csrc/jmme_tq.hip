@@ -200,6 +200,125 @@ __global__ __launch_bounds__(kTB) void transform_kernel(const int32_t *__restric
   }
 }
 
+// ---- 8x8 blocks: a row per lane ----------------------------------------------
+// A lane per row keeps a lane's state at one row (8 values) instead of a whole
+// block (64 + 64 + 64: 170 VGPRs, 2 waves/SIMD -- 57-59 % of HBM): the 8 lanes
+// of a block load its 256 B as two lane-contiguous 16-B chunks each (fully
+// coalesced, no staging), run JM's row butterflies, transpose through a padded
+// per-wave LDS tile, run the column butterflies and transpose back.  Same
+// integer operations in the same order as transform.c:365-506.
+constexpr int kT8 = 9;     // LDS row stride (dwords) of the 8x8 tiles
+constexpr int kWG8 = 256;  // 4 waves per workgroup: one-wave workgroups left too few waves per CU
+constexpr int kU8 = 4;     // 8x8 transforms: block groups per loop iteration (loads in flight)
+constexpr int kUQ = 8;     // quant: blocks per 16-lane group per loop iteration
+
+template <int OP>
+__global__ __launch_bounds__(kWG8) void transform8_kernel(const int32_t *__restrict__ in, int32_t *__restrict__ out,
+                                                          int n) {
+  // kU8 groups of 32 blocks per iteration: all their loads are issued before
+  // the first is used (HBM wants ~100+ KB in flight per CU)
+  __shared__ int32_t tile[kWG8 / 8 * 8 * kT8];
+  const int b = threadIdx.x >> 3, r = threadIdx.x & 7;   // block of a group of 32, row
+  int32_t *t = tile + b * 8 * kT8;
+  constexpr int kG = kWG8 / 8;
+  for (int base = blockIdx.x * kG * kU8; base < n; base += gridDim.x * kG * kU8) {
+    v4i q[kU8][2];
+#pragma unroll
+    for (int u = 0; u < kU8; ++u) {
+      const int blk = base + u * kG + b;
+      if (blk < n) {
+        const v4i *src = reinterpret_cast<const v4i *>(in + ((size_t)blk * 64 + r * 8));
+        q[u][0] = __builtin_nontemporal_load(src);
+        q[u][1] = __builtin_nontemporal_load(src + 1);
+      } else {
+        q[u][0] = q[u][1] = v4i{0, 0, 0, 0};
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kU8; ++u) {
+      const int blk = base + u * kG + b;
+      int x[8] = {q[u][0].x, q[u][0].y, q[u][0].z, q[u][0].w, q[u][1].x, q[u][1].y, q[u][1].z, q[u][1].w}, y[8];
+      if (OP == JMME_TF_FORWARD8x8) fwd8(x, 1, y, 1); else inv8(x, 1, y, 1);   // rows
+#pragma unroll
+      for (int k = 0; k < 8; ++k) t[r * kT8 + k] = y[k];
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < 8; ++k) x[k] = t[k * kT8 + r];                      // column r
+      if (OP == JMME_TF_FORWARD8x8) fwd8(x, 1, y, 1); else inv8(x, 1, y, 1);   // columns
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < 8; ++k) t[k * kT8 + r] = y[k];
+      __syncthreads();
+      if (blk < n) {
+        // store j writes 16-B chunk 8j + r of the block: the 8 lanes of a block
+        // cover one whole 128-B line per store instruction (rows 4j .. 4j+3)
+        v4i *dst = reinterpret_cast<v4i *>(out + (size_t)blk * 64);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int *src = t + (4 * j + (r >> 1)) * kT8 + 4 * (r & 1);
+          __builtin_nontemporal_store(v4i{src[0], src[1], src[2], src[3]}, dst + 8 * j + r);
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// 8-point Walsh-Hadamard butterflies in place (the order of wht_abs_sum)
+__device__ __forceinline__ void wht8(int *v) {
+#pragma unroll
+  for (int len = 1; len < 8; len <<= 1)
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (!(j & len)) {
+        const int a = v[j], c = v[j + len];
+        v[j] = a + c;
+        v[j + len] = a - c;
+      }
+}
+
+// HadamardSAD8x8 (me_distortion.c:261-341) a row per lane: one 16-B load of 8
+// int16 differences, row WHT, transpose, column WHT, |.| summed over the 8
+// lanes of the block by cross-lane adds
+__global__ __launch_bounds__(kWG8) void satd8_kernel(const int16_t *__restrict__ diff, int32_t *__restrict__ out, int n) {
+  __shared__ int32_t tile[kWG8 / 8 * 8 * kT8];
+  const int b = threadIdx.x >> 3, r = threadIdx.x & 7;
+  int32_t *t = tile + b * 8 * kT8;
+  constexpr int kG = kWG8 / 8;
+  for (int base = blockIdx.x * kG * kU8; base < n; base += gridDim.x * kG * kU8) {
+    v4i q[kU8];
+#pragma unroll
+    for (int u = 0; u < kU8; ++u) {   // every group's row loaded before the first is used
+      const int blk = base + u * kG + b;
+      q[u] = blk < n ? __builtin_nontemporal_load(reinterpret_cast<const v4i *>(diff + ((size_t)blk * 64 + r * 8)))
+                     : v4i{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int u = 0; u < kU8; ++u) {
+      const int blk = base + u * kG + b;
+      const int w[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
+      int v[8];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { v[2 * k] = (int)(int16_t)(w[k] & 0xffff); v[2 * k + 1] = w[k] >> 16; }
+      wht8(v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) t[r * kT8 + k] = v[k];
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = t[k * kT8 + r];
+      __syncthreads();
+      wht8(v);
+      int sum = 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) sum += abs(v[k]);
+      sum += __shfl_xor(sum, 1, 64);
+      sum += __shfl_xor(sum, 2, 64);
+      sum += __shfl_xor(sum, 4, 64);
+      if (blk < n && r == 0) out[blk] = (sum + 2) >> 2;   // me_distortion.c:339
+    }
+  }
+}
+
 // ---- SATD ------------------------------------------------------------------
 // Sum of |Walsh-Hadamard(d)|: every output of JM's HadamardSAD4x4/8x8 is a +-1
 // combination of the inputs with a distinct sign pattern, so the sum of
@@ -255,70 +374,90 @@ __global__ __launch_bounds__(kTB) void satd_kernel(const int16_t *__restrict__ d
 }
 
 // ---- quant_4x4_normal --------------------------------------------------------
-__global__ __launch_bounds__(kTB) void quant4x4_kernel(const jmme_quant4x4_params *__restrict__ params,
-                                                       const int32_t *__restrict__ param_idx,
-                                                       int32_t *__restrict__ coef, int32_t *__restrict__ levels,
-                                                       int32_t *__restrict__ runs,
-                                                       int32_t *__restrict__ coeff_cost,
-                                                       int32_t *__restrict__ nonzero, int n) {
-  // per-lane scratch for the scan-order walk (coefficient, level and run
-  // arrays indexed by the runtime scan position; stride 17 dwords keeps the
-  // 64 lanes on distinct banks).  The staging slab aliases it: the workgroup
-  // is one wave, and the slab is only live inside wave_load / wave_store.
-  __shared__ __attribute__((aligned(16))) int32_t lds[3 * 64 * 17];
-  static_assert(64 * slab_stride<17>() <= 3 * 64 * 17, "slab fits the scratch");
-  int32_t *slab = lds, *sc = lds, *sl = lds + 64 * 17, *sr = lds + 2 * 64 * 17;
-  const int lane = threadIdx.x;
-  int32_t *my_c = sc + lane * 17, *my_l = sl + lane * 17, *my_r = sr + lane * 17;
-  for (int base = blockIdx.x * 64; base < n; base += gridDim.x * 64) {
-    const int nb = min(64, n - base);
-    const int b = base + lane;
-    const bool live = lane < nb;
-    const jmme_quant4x4_params &q = params[(param_idx && live) ? param_idx[b] : 0];
-    int c[16];
-    wave_load<16>(coef + (size_t)base * 16, nb, slab, lane, c);
+// A lane per scan position, 16 lanes per block, 4 blocks per wave.  JM's loop
+// (quant4x4_normal.c:59-104) is sequential only through `run` and the output
+// index; both are functions of which earlier scan positions quantise to a
+// nonzero level, i.e. of the block's 16-bit slice of one ballot: the output
+// index is the popcount of the nonzero positions below, the run the distance
+// to the highest one.  The cost is a sum over the nonzero positions (a 16-lane
+// cross-lane reduction), and the level / run lists are compacted through a
+// small LDS table.  (The earlier lane-per-block form walked the scan in
+// per-lane LDS arrays: 120 VGPRs, 13 KB LDS per wave, 34 % of HBM.)
+__global__ __launch_bounds__(kWG8) void quant4x4_kernel(const jmme_quant4x4_params *__restrict__ params,
+                                                        const int32_t *__restrict__ param_idx,
+                                                        int32_t *__restrict__ coef, int32_t *__restrict__ levels,
+                                                        int32_t *__restrict__ runs,
+                                                        int32_t *__restrict__ coeff_cost,
+                                                        int32_t *__restrict__ nonzero, int n) {
+  constexpr int kB = kWG8 / 16;   // blocks per workgroup per round; kUQ rounds' loads issued together
+  __shared__ int32_t s_l[kB][17], s_r[kB][16];
+  const int g = threadIdx.x >> 4, k = threadIdx.x & 15, gw = g & 3;   // block, scan position, block in the wave
+  for (int base = blockIdx.x * kB * kUQ; base < n; base += gridDim.x * kB * kUQ) {
+    int pq[kUQ], x[kUQ], sc[kUQ], of[kUQ], iv[kUQ], cc[kUQ];
+    const jmme_quant4x4_params *qp[kUQ];
 #pragma unroll
-    for (int e = 0; e < 16; ++e) { my_c[e] = c[e]; my_l[e] = 0; my_r[e] = 0; }
-    my_l[16] = 0;
-    const int q_bits = 15 + q.qp_per;                 // Q_BITS, defines.h:311
-    int run = 0, nout = 0, nz = 0, cost = live ? coeff_cost[b] : 0;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const int pq = q.scan[k][1] * 4 + q.scan[k][0];   // (horizontal, vertical)
-      const int x = my_c[pq];
-      if (x == 0) { ++run; continue; }
-      int level = (abs(x) * q.scale[pq] + q.offset[pq]) >> q_bits;
-      if (level == 0) {
-        my_c[pq] = 0;
-        ++run;
-        continue;
-      }
-      if (q.is_cavlc && level > 2063) level = 2063;    // CAVLC_LEVEL_LIMIT, defines.h:99
-      cost += level > 1 ? 999999 : (int)q.c_cost[run];   // MAX_VALUE, defines.h:123
-      if (x < 0) level = -level;
-      my_c[pq] = ((level * q.inv_scale[pq] << q.qp_per) + 8) >> 4;   // rshift_rnd_sf(.,4)
-      my_l[nout] = level;
-      my_r[nout] = run;
-      ++nout;
-      run = 0;
-      nz = 1;
+    for (int u = 0; u < kUQ; ++u) {
+      const int b = base + u * kB + g;
+      qp[u] = params + ((param_idx && b < n) ? param_idx[b] : 0);
     }
-    int lv[17], rn[16];
 #pragma unroll
-    for (int e = 0; e < 16; ++e) { c[e] = my_c[e]; lv[e] = my_l[e]; rn[e] = my_r[e]; }
-    lv[16] = my_l[16];
-    wave_store<16>(coef + (size_t)base * 16, nb, slab, lane, c);
-    wave_store<17>(levels + (size_t)base * 17, nb, slab, lane, lv);
-    wave_store<16>(runs + (size_t)base * 16, nb, slab, lane, rn);
-    if (live) {
-      coeff_cost[b] = cost;
-      nonzero[b] = nz;
+    for (int u = 0; u < kUQ; ++u) pq[u] = qp[u]->scan[k][1] * 4 + qp[u]->scan[k][0];   // (horizontal, vertical)
+#pragma unroll
+    for (int u = 0; u < kUQ; ++u) {
+      const int b = base + u * kB + g;
+      x[u] = b < n ? coef[(size_t)b * 16 + pq[u]] : 0;
+      sc[u] = qp[u]->scale[pq[u]];
+      of[u] = qp[u]->offset[pq[u]];
+      iv[u] = qp[u]->inv_scale[pq[u]];
+      cc[u] = (k == 0 && b < n) ? coeff_cost[b] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < kUQ; ++u) {
+      const int b = base + u * kB + g;
+      const bool live = b < n;
+      const jmme_quant4x4_params &q = *qp[u];
+      const int q_bits = 15 + q.qp_per;                 // Q_BITS, defines.h:311
+      const int p = pq[u], xv = x[u];
+      int level = xv == 0 ? 0 : (abs(xv) * sc[u] + of[u]) >> q_bits;
+      if (q.is_cavlc && level > 2063) level = 2063;     // CAVLC_LEVEL_LIMIT, defines.h:99
+      const unsigned mg = (unsigned)(__builtin_amdgcn_ballot_w64(level != 0) >> (16 * gw)) & 0xffffu;
+      const unsigned below = mg & ((1u << k) - 1u);
+      const int idx = __builtin_popcount(below);
+      const int run = below ? k - (32 - __builtin_clz(below)) : k;   // positions since the previous nonzero
+      s_l[g][k] = 0;
+      s_r[g][k] = 0;
+      if (k == 0) s_l[g][16] = 0;
+      __syncthreads();
+      int term = 0, deq = 0;
+      if (level) {
+        term = level > 1 ? 999999 : (int)q.c_cost[run];   // MAX_VALUE, defines.h:123
+        const int sl = xv < 0 ? -level : level;
+        deq = ((sl * iv[u] << q.qp_per) + 8) >> 4;   // rshift_rnd_sf(., 4)
+        s_l[g][idx] = sl;
+        s_r[g][idx] = run;
+      }
+      term += __shfl_xor(term, 8, 64);
+      term += __shfl_xor(term, 4, 64);
+      term += __shfl_xor(term, 2, 64);
+      term += __shfl_xor(term, 1, 64);
+      __syncthreads();
+      if (live) {
+        if (xv != 0) coef[(size_t)b * 16 + p] = deq;
+        levels[(size_t)b * 17 + k] = s_l[g][k];
+        runs[(size_t)b * 16 + k] = s_r[g][k];
+        if (k == 0) {
+          levels[(size_t)b * 17 + 16] = s_l[g][16];
+          coeff_cost[b] = cc[u] + term;
+          nonzero[b] = mg != 0;
+        }
+      }
+      __syncthreads();
     }
   }
 }
 
-int grid_for(int n) {
-  const int g = (n + 63) / 64;
+int grid_for(int n, int per_wg = 64) {
+  const int g = (n + per_wg - 1) / per_wg;
   return g < 1 ? 1 : (g > 8192 ? 8192 : g);
 }
 
@@ -326,12 +465,17 @@ int grid_for(int n) {
 
 hipError_t launch_transform(int op, const int32_t *in, int32_t *out, int n, hipStream_t s) {
   const int g = grid_for(n);
+  if (op == JMME_TF_FORWARD8x8 || op == JMME_TF_INVERSE8x8) {
+    const int g8 = grid_for(n, kWG8 / 8 * kU8);
+    if (op == JMME_TF_FORWARD8x8) hipLaunchKernelGGL(transform8_kernel<JMME_TF_FORWARD8x8>, dim3(g8), dim3(kWG8), 0, s, in, out, n);
+    else hipLaunchKernelGGL(transform8_kernel<JMME_TF_INVERSE8x8>, dim3(g8), dim3(kWG8), 0, s, in, out, n);
+    return hipGetLastError();
+  }
   switch (op) {
 #define JMME_TF(OP) case OP: hipLaunchKernelGGL(transform_kernel<OP>, dim3(g), dim3(kTB), 0, s, in, out, n); break;
     JMME_TF(JMME_TF_FORWARD4x4) JMME_TF(JMME_TF_INVERSE4x4) JMME_TF(JMME_TF_HADAMARD4x4)
     JMME_TF(JMME_TF_IHADAMARD4x4) JMME_TF(JMME_TF_HADAMARD4x2) JMME_TF(JMME_TF_IHADAMARD4x2)
-    JMME_TF(JMME_TF_HADAMARD2x2) JMME_TF(JMME_TF_IHADAMARD2x2) JMME_TF(JMME_TF_FORWARD8x8)
-    JMME_TF(JMME_TF_INVERSE8x8)
+    JMME_TF(JMME_TF_HADAMARD2x2) JMME_TF(JMME_TF_IHADAMARD2x2)
 #undef JMME_TF
     default: return hipErrorInvalidValue;
   }
@@ -343,14 +487,14 @@ int transform_elems(int op) { return (op < 0 || op > JMME_TF_INVERSE8x8) ? 0 : t
 hipError_t launch_satd(int size, const int16_t *diff, int32_t *out, int n, hipStream_t s) {
   const int g = grid_for(n);
   if (size == 4) hipLaunchKernelGGL(satd_kernel<4>, dim3(g), dim3(kTB), 0, s, diff, out, n);
-  else if (size == 8) hipLaunchKernelGGL(satd_kernel<8>, dim3(g), dim3(kTB), 0, s, diff, out, n);
+  else if (size == 8) hipLaunchKernelGGL(satd8_kernel, dim3(grid_for(n, kWG8 / 8 * kU8)), dim3(kWG8), 0, s, diff, out, n);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }
 
 hipError_t launch_quant4x4(const jmme_quant4x4_params *params, const int32_t *param_idx, int32_t *coef, int32_t *levels,
                            int32_t *runs, int32_t *coeff_cost, int32_t *nonzero, int n, hipStream_t s) {
-  hipLaunchKernelGGL(quant4x4_kernel, dim3(grid_for(n)), dim3(kTB), 0, s, params, param_idx, coef, levels, runs,
+  hipLaunchKernelGGL(quant4x4_kernel, dim3(grid_for(n, kWG8 / 16 * kUQ)), dim3(kWG8), 0, s, params, param_idx, coef, levels, runs,
                      coeff_cost, nonzero, n);
   return hipGetLastError();
 }
