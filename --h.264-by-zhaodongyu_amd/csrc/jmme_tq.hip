@@ -442,13 +442,21 @@ __global__ __launch_bounds__(kWG8) void quant4x4_kernel(const jmme_quant4x4_para
       term += __shfl_xor(term, 1, 64);
       __syncthreads();
       if (live) {
-        if (xv != 0) coef[(size_t)b * 16 + p] = deq;
-        levels[(size_t)b * 17 + k] = s_l[g][k];
+        coef[(size_t)b * 16 + p] = deq;   // (0 where x was 0: every lane stores, whole lines)
         runs[(size_t)b * 16 + k] = s_r[g][k];
         if (k == 0) {
-          levels[(size_t)b * 17 + 16] = s_l[g][16];
           coeff_cost[b] = cc[u] + term;
           nonzero[b] = mg != 0;
+        }
+      }
+      {
+        // the wave's 4 blocks' level lists are one contiguous run of 68
+        // dwords: lane l stores dword l, lanes 0-3 dwords 64-67
+        const int wl = threadIdx.x & 63, w4 = g & ~3, b0 = base + u * kB + w4;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int d = h * 64 + wl, j = d / 17;
+          if (d < 68 && b0 + j < n) levels[(size_t)b0 * 17 + d] = s_l[w4 + j][d - 17 * j];
         }
       }
       __syncthreads();
