@@ -82,7 +82,9 @@ struct jmme_ctx {
   int pool_min_range = 80;                   // jmme_fractal_search: pruned pool search from this radius up
   int pool_mfma = 1;                         // 4x4 full pool: matrix-core bound test (0: VALU)
   size_t cap_stamps = 0;
-  unsigned *d_counts = nullptr;              // kCountWords: [0] further groups, [2] status, [8..15] XCD tickets
+  unsigned *d_counts = nullptr;              // 2 x kCountWords: [0] further groups, [2] status, [8..15] XCD tickets
+  int counts_half = 0;                       // the set the next launch uses (the plan kernel zeroes the other)
+  unsigned *last_counts = nullptr;           // the set of the last launch (status)
   Item *d_items = nullptr;                   // work items (one per unit x partition group)
   size_t cap_items = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -311,7 +313,8 @@ extern "C" jmme_ctx *jmme_create(const jmme_config *cfg, int device) {
     ~Restore() { if (d >= 0 && d != was) (void)hipSetDevice(d); }
   } restore_{caller_dev, ctx->device};
   if ((e = hipMalloc(&ctx->d_ref_table, sizeof(uint8_t *) * kMaxLists * kMaxRefs)) != hipSuccess ||
-      (e = hipMalloc(&ctx->d_counts, kCountWords * sizeof(unsigned))) != hipSuccess ||
+      (e = hipMalloc(&ctx->d_counts, 2 * kCountWords * sizeof(unsigned))) != hipSuccess ||
+      (e = hipMemset(ctx->d_counts, 0, 2 * kCountWords * sizeof(unsigned))) != hipSuccess ||
       (e = hipMalloc(&ctx->d_sub_table, sizeof(uint8_t *) * kMaxLists * kMaxRefs)) != hipSuccess ||
       (e = hipEventCreate(&ctx->ev0)) != hipSuccess || (e = hipEventCreate(&ctx->ev1)) != hipSuccess) {
     fail("jmme_create: %s", hipGetErrorString(e));
@@ -510,7 +513,8 @@ int launch(jmme_ctx *ctx, int mode, const uint8_t *d_cur, const uint8_t *const *
   p.key32 = p.lds_range <= kKey32MaxRange;
   p.items = ctx->d_items;
   p.item_cap = (unsigned)ctx->cap_items;
-  p.counts = ctx->d_counts;
+  p.counts = ctx->d_counts + ctx->counts_half * kCountWords;
+  p.counts_next = ctx->d_counts + (ctx->counts_half ^ 1) * kCountWords;
   p.debug_words = debug_words;
 #ifdef JMME_STAMPS
   // n units x 8 words, then 4 words per workgroup (up to kStampWGs)
@@ -523,9 +527,10 @@ int launch(jmme_ctx *ctx, int mode, const uint8_t *d_cur, const uint8_t *const *
   p.stamps = ctx->d_stamps;
   HIPCHK(hipMemsetAsync(ctx->d_stamps, 0, words * sizeof(unsigned long long), s));
 #endif
-  HIPCHK(hipMemsetAsync(ctx->d_counts, 0, kCountWords * sizeof(unsigned), s));
   // jmme_last_kernel_ms: the main item kernel alone (ev0 .. ev1)
   HIPCHK(launch_search(p, s, ctx->ev0, ctx->ev1));
+  ctx->last_counts = p.counts;
+  ctx->counts_half ^= 1;
   ctx->timed = true;
   return 0;
 }
@@ -563,7 +568,8 @@ int status_words(const unsigned *st, const jmme_ctx *ctx) {
 
 int check_status(jmme_ctx *ctx, hipStream_t s) {
   unsigned st[3] = {0, 0, 0};
-  HIPCHK(hipMemcpyAsync(st, ctx->d_counts, sizeof st, hipMemcpyDeviceToHost, s));
+  if (!ctx->last_counts) return 0;   // no batched launch yet
+  HIPCHK(hipMemcpyAsync(st, ctx->last_counts, sizeof st, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   return status_words(st, ctx);
 }
@@ -826,7 +832,7 @@ extern "C" int jmme_search_mbs(jmme_ctx *ctx, int mode, const jmme_mb_req *req, 
   const unsigned *st = reinterpret_cast<const unsigned *>(ctx->h_pin + rq + rs);
   HIPCHK(hipMemcpyAsync(ctx->h_pin + rq, ctx->d_out, (size_t)n * JMME_NSLOT * sizeof(jmme_block_res),
                         hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(ctx->h_pin + rq + rs, ctx->d_counts, 3 * sizeof(unsigned), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(ctx->h_pin + rq + rs, ctx->last_counts, 3 * sizeof(unsigned), hipMemcpyDeviceToHost, s));
   phase(ctx, 7, &t_ph);
   HIPCHK(hipStreamSynchronize(s));
   phase(ctx, 8, &t_ph);
@@ -1294,10 +1300,10 @@ int prepare_subs(jmme_ctx *ctx, hipStream_t s);   // sub-pel section below
 namespace {
 int launch_epzs_ex(jmme_ctx *ctx, const jmme_epzs_req *d_req, int n, const int16_t *d_preds, const uint8_t *d_cond,
                    const int16_t *d_stale, jmme_epzs_res *d_out, int16_t *d_vis, int max_visited, hipStream_t s) {
-  if (ctx->hbd) return fail("SourceBitDepthLuma %d: the EPZS search is 8-bit only", ctx->cfg.SourceBitDepthLuma);
   if (sync_ref_table(ctx, s)) return -1;
   EpzsParams p{};
   p.cur = ctx->d_cur;
+  p.hbd = ctx->hbd ? 1 : 0;   // 16-bit planes / sub-images: the v_sad_u16 instantiation
   p.refs = ctx->d_ref_table;
   p.pitch = ctx->pitch;
   p.width = ctx->width;
@@ -1722,16 +1728,17 @@ extern "C" int jmme_debug_stamps(jmme_ctx *ctx, uint64_t *out, int max_units) {
 // EPZS_sub_pel_motion_estimation (me_fullsearch.c:186-289, me_epzs_sub.c:30-222)
 namespace {
 
+// high bit depth: 16-bit sub-images clipped to max_imgpel_value (the same
+// sample type as the context's planes)
 int build_sub_images(jmme_ctx *ctx, int slot, hipStream_t s) {
-  if (ctx->hbd) return fail("SourceBitDepthLuma %d: quarter-pel planes are 8-bit only", ctx->cfg.SourceBitDepthLuma);
   if (!ctx->d_refs[slot]) return fail("reference slot %d not uploaded", slot);
   const SubGeom g = sub_geom(ctx->width, ctx->height);
   if (!ctx->d_subs[slot]) {
-    HIPCHK(hipMalloc(&ctx->d_subs[slot], 16 * g.plane_stride));
+    HIPCHK(hipMalloc(&ctx->d_subs[slot], 16 * g.plane_stride * (ctx->hbd ? 2 : 1)));
     ctx->sub_table_dirty = true;
   }
   HIPCHK(launch_sub_images(ctx->d_refs[slot], ctx->pitch, ctx->width, ctx->height, ctx->d_subs[slot], g.pitch,
-                           g.plane_stride, s));
+                           g.plane_stride, s, ctx->hbd ? ctx->cfg.SourceBitDepthLuma : 8));
   ctx->sub_stale[slot] = false;
   return 0;
 }
@@ -1769,7 +1776,8 @@ extern "C" int jmme_get_sub_images(jmme_ctx *ctx, int list, int ref_idx, jmme_im
   if (!ctx->d_refs[slot]) return fail("reference slot %d not uploaded", slot);
   if ((ctx->sub_stale[slot] || !ctx->d_subs[slot]) && build_sub_images(ctx, slot, nullptr)) return -1;
   const SubGeom g = sub_geom(ctx->width, ctx->height);
-  std::vector<uint8_t> h(16 * g.plane_stride);
+  const size_t es = ctx->hbd ? 2 : 1;
+  std::vector<uint8_t> h(16 * g.plane_stride * es);
   HIPCHK(hipMemcpy(h.data(), ctx->d_subs[slot], h.size(), hipMemcpyDeviceToHost));
   for (int k = 0; k < 16; ++k) {
     jmme_imgpel **rows = sub[k >> 2][k & 3];
@@ -1778,8 +1786,14 @@ extern "C" int jmme_get_sub_images(jmme_ctx *ctx, int list, int ref_idx, jmme_im
       jmme_imgpel *d = rows[j - JMME_SUBPEL_PAD_Y];
       if (!d) return fail("null row %d of sub-image [%d][%d]", j - JMME_SUBPEL_PAD_Y, k >> 2, k & 3);
       d -= JMME_SUBPEL_PAD_X;
-      const uint8_t *srow = &h[(size_t)k * g.plane_stride + (size_t)j * g.pitch];
-      for (int i = 0; i < g.pw; ++i) d[i] = srow[i];
+      const size_t o = (size_t)k * g.plane_stride + (size_t)j * g.pitch;
+      if (ctx->hbd) {
+        const uint16_t *srow = reinterpret_cast<const uint16_t *>(h.data()) + o;
+        for (int i = 0; i < g.pw; ++i) d[i] = srow[i];
+      } else {
+        const uint8_t *srow = &h[o];
+        for (int i = 0; i < g.pw; ++i) d[i] = srow[i];
+      }
     }
   }
   return 0;
@@ -1804,7 +1818,6 @@ extern "C" int jmme_sub_images_async(jmme_ctx *ctx, const uint8_t *d_src, int sr
 extern "C" int jmme_subpel_validate(jmme_ctx *ctx, const jmme_subpel_req *req, int n) {
   DevGuard dg_(ctx);
   if (!ctx) return fail("null ctx");
-  if (ctx->hbd) return fail("SourceBitDepthLuma %d: sub-pel refinement is 8-bit only", ctx->cfg.SourceBitDepthLuma);
   if (n < 0) return fail("negative request count");
   if (n && !req) return fail("null request array");
   if (!ctx->d_cur) return fail("no current frame uploaded");
@@ -1823,6 +1836,11 @@ extern "C" int jmme_subpel_validate(jmme_ctx *ctx, const jmme_subpel_req *req, i
       return fail("request %d: reference slot %d not uploaded", i, q.ref_slot);
     if (q.variant > 1) return fail("request %d: variant %d", i, q.variant);
     if (q.metric_h > 2 || q.metric_q > 2) return fail("request %d: metric %d/%d", i, q.metric_h, q.metric_q);
+    // computeSSE sums into an int (me_distortion.c:1197): above 11 bits a 16x16
+    // block's sum can pass 2^31, where JM's row-wise early exit meets a wrapped sum
+    if ((q.metric_h == 1 || q.metric_q == 1) && ctx->cfg.SourceBitDepthLuma > 11)
+      return fail("request %d: SSE sub-pel metric at SourceBitDepthLuma %d (int sums may wrap)", i,
+                  ctx->cfg.SourceBitDepthLuma);
     if (q.start_hp > 1 || q.start_qp > 1) return fail("request %d: start_hp/qp", i);
     if (q.search_pos2 > 9 || q.search_pos4 > 9)
       return fail("request %d: search_pos2/4 %d/%d beyond JM's 9-point rings", i, q.search_pos2, q.search_pos4);
@@ -1852,6 +1870,7 @@ extern "C" int jmme_subpel_refine_async(jmme_ctx *ctx, const jmme_subpel_req *d_
   p.cur_pitch = ctx->pitch;
   p.width = ctx->width;
   p.height = ctx->height;
+  p.hbd = ctx->hbd ? 1 : 0;
   p.subs = ctx->d_sub_table;
   p.sub_pitch = g.pitch;
   p.plane_stride = g.plane_stride;
@@ -1955,10 +1974,9 @@ extern "C" int jmme_prepare(jmme_ctx *ctx) {
   ctx->height = h;
   ctx->pitch = pitch;
   if (rc < 0) return -1;
-  if (ctx->hbd) return 0;   // no quarter-pel planes at high bit depth
-  HIPCHK(subs.alloc(16 * g.plane_stride));
+  HIPCHK(subs.alloc(16 * g.plane_stride * 2));
   HIPCHK(launch_sub_images(static_cast<const uint8_t *>(plane.p), kW, kW, kH, static_cast<uint8_t *>(subs.p), g.pitch,
-                           g.plane_stride, nullptr));
+                           g.plane_stride, nullptr, ctx->hbd ? ctx->cfg.SourceBitDepthLuma : 8));
   HIPCHK(hipDeviceSynchronize());
   return 0;
 }

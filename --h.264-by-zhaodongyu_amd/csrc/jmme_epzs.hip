@@ -71,7 +71,7 @@ __device__ __forceinline__ int dual_pattern(int v) {
 __device__ __forceinline__ void wave_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 struct WaveLds {
-  uint32_t cur[64];
+  uint32_t cur[128];      // the current block: 4 (8-bit) or 2 (16-bit) samples per dword
   int pk[64][3];          // compacted candidates (x, y, source index)
 };
 // the visited-position bitmap (EPZSMap) lives in dynamic LDS, map_words per wave:
@@ -80,19 +80,22 @@ struct WaveLds {
 struct Search {
   const uint8_t *ref;    // integer grid: the reference plane; sub-pel grid: its 16 sub-images
   int pitch, W, H;       // pitch: of the plane, or of the sub-images
-  size_t ps;             // sub-pel grid: bytes per sub-image
+  size_t ps;             // sub-pel grid: samples per sub-image (pitch too: in samples)
   int pos_x, pos_y, bsx, bsy;
   int pred_x, pred_y, cx, cy, max_x, max_y, side_x;
   int lambda;
-  const uint32_t *cur;   // LDS, bsx/4 dwords per row
+  const uint32_t *cur;   // LDS, bsx/4 (16-bit: bsx/2) dwords per row
   uint32_t *map;
 };
 
 // SAD of row r of the block at (ox, oy) against the current block's row r
 // (LDS).  UMVLine4X semantics: the row index and, off the picture's sides,
 // every sample are clamped into the picture.
+template <int NQ, bool HBD>
+__device__ __forceinline__ unsigned row_sad(const Search &s, int ox, int oy, int r);
+// 8-bit samples: NQ dwords of 4 samples, v_sad_u8
 template <int NQ>
-__device__ __forceinline__ unsigned row_sad(const Search &s, int ox, int oy, int r) {
+__device__ __forceinline__ unsigned row_sad8(const Search &s, int ox, int oy, int r) {
   const uint8_t *row = s.ref + (size_t)min(max(oy + r, 0), s.H - 1) * s.pitch;
   const uint32_t *cur = s.cur + r * NQ;
   unsigned sad = 0;
@@ -116,17 +119,47 @@ __device__ __forceinline__ unsigned row_sad(const Search &s, int ox, int oy, int
   }
   return sad;
 }
+// 16-bit samples (SourceBitDepthLuma 9..14): NQ dwords of 2 samples, v_sad_u16
+template <int NQ>
+__device__ __forceinline__ unsigned row_sad16(const Search &s, int ox, int oy, int r) {
+  const uint16_t *row = reinterpret_cast<const uint16_t *>(s.ref) + (size_t)min(max(oy + r, 0), s.H - 1) * s.pitch;
+  const uint32_t *cur = s.cur + r * NQ;
+  unsigned sad = 0;
+  if (ox >= 0 && ox + 2 * NQ <= s.W) {
+    const uint32_t *base = reinterpret_cast<const uint32_t *>(row + (ox & ~1));
+    const uint32_t sh = (uint32_t)(ox & 1) * 2;
+    uint32_t w[NQ + 1];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) w[q] = base[q];
+    w[NQ] = base[sh ? NQ : NQ - 1];   // stays inside the row
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) sad = __builtin_amdgcn_sad_u16(__builtin_amdgcn_alignbyte(w[q + 1], w[q], sh), cur[q], sad);
+  } else {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const uint32_t d = (uint32_t)row[min(max(ox + 2 * q, 0), s.W - 1)] |
+                         ((uint32_t)row[min(max(ox + 2 * q + 1, 0), s.W - 1)] << 16);
+      sad = __builtin_amdgcn_sad_u16(d, cur[q], sad);
+    }
+  }
+  return sad;
+}
+template <int NQ, bool HBD>
+__device__ __forceinline__ unsigned row_sad(const Search &s, int ox, int oy, int r) {
+  if constexpr (HBD) return row_sad16<NQ>(s, ox, oy, r);
+  else return row_sad8<NQ>(s, ox, oy, r);
+}
 
 // Sub-pel grid: SAD of row r of the block at padded quarter-pel position
 // (cx, cy): UMVLine4X picks sub-image (cy & 3, cx & 3) and clamps the origin
 // to [-20, H+3] x [-32, W+15] (refbuf.h:22-26, mbuffer.c:549-550); the padded
 // sub-image holds every sample the block then reads.
-template <int NQ>
+template <int NQ, bool HBD>
 __device__ __forceinline__ unsigned row_sad_grid(const Search &s, int cx, int cy, int r) {
   const int pl = ((cy & 3) << 2) | (cx & 3);
   const int yy = min(max(cy >> 2, -20), s.H + 3), xx = min(max(cx >> 2, -32), s.W + 15);
-  const uint8_t *a = s.ref + (size_t)pl * s.ps + (size_t)(yy + 20 + r) * s.pitch + (xx + 32);
-  const uintptr_t u = reinterpret_cast<uintptr_t>(a);
+  const size_t off = (size_t)pl * s.ps + (size_t)(yy + 20 + r) * s.pitch + (xx + 32);
+  const uintptr_t u = reinterpret_cast<uintptr_t>(HBD ? s.ref + 2 * off : s.ref + off);
   const uint32_t *w = reinterpret_cast<const uint32_t *>(u & ~(uintptr_t)3);
   const uint32_t sh = (uint32_t)(u & 3);
   const uint32_t *cur = s.cur + r * NQ;
@@ -135,14 +168,17 @@ __device__ __forceinline__ unsigned row_sad_grid(const Search &s, int cx, int cy
   for (int q = 0; q <= NQ; ++q) v[q] = w[q];
   unsigned sad = 0;
 #pragma unroll
-  for (int q = 0; q < NQ; ++q) sad = __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(v[q + 1], v[q], sh), cur[q], sad);
+  for (int q = 0; q < NQ; ++q) {
+    const uint32_t d = __builtin_amdgcn_alignbyte(v[q + 1], v[q], sh);
+    sad = HBD ? __builtin_amdgcn_sad_u16(d, cur[q], sad) : __builtin_amdgcn_sad_u8(d, cur[q], sad);
+  }
   return sad;
 }
 
 // Costs (mv_cost + SAD << 5) of the candidates held by lanes 0..K-1 (qpel
 // (mx, my)), returned in the same lanes.  One lane per (candidate, row):
 // 64/bsy candidates per pass, row sums reduced inside aligned lane groups.
-template <int NQ, int LOGR, bool GRID>
+template <int NQ, int LOGR, bool GRID, bool HBD>
 __device__ __forceinline__ int64_t eval_t(const Search &s, int lane, int K, int mx, int my) {
   constexpr int R = 1 << LOGR, C = 64 >> LOGR;
   const int grp = lane >> LOGR, r = lane & (R - 1);
@@ -152,8 +188,8 @@ __device__ __forceinline__ int64_t eval_t(const Search &s, int lane, int K, int 
     const int cmx = __shfl(mx, c & 63, 64), cmy = __shfl(my, c & 63, 64);
     unsigned sad = 0u;
     if (c < K)
-      sad = GRID ? row_sad_grid<NQ>(s, (s.pos_x << 2) + cmx, (s.pos_y << 2) + cmy, r)
-                 : row_sad<NQ>(s, s.pos_x + (cmx >> 2), s.pos_y + (cmy >> 2), r);
+      sad = GRID ? row_sad_grid<NQ, HBD>(s, (s.pos_x << 2) + cmx, (s.pos_y << 2) + cmy, r)
+                 : row_sad<NQ, HBD>(s, s.pos_x + (cmx >> 2), s.pos_y + (cmy >> 2), r);
 #pragma unroll
     for (int m = 1; m < R; m <<= 1) sad += __shfl_xor(sad, m, 64);
     const int j = lane - base;
@@ -164,7 +200,7 @@ __device__ __forceinline__ int64_t eval_t(const Search &s, int lane, int K, int 
   return mvc + ((int64_t)mine << 5);
 }
 
-template <bool GRID>
+template <bool GRID, bool HBD>
 __device__ __noinline__ int64_t eval_costs_v(const uint8_t *ref, int pitch, size_t ps, int W, int H, const uint32_t *cur,
                                               int pos_x, int pos_y, int bsx, int bsy, int pred_x, int pred_y,
                                               int lambda, int lane, int K, int mx, int my) {
@@ -182,21 +218,22 @@ __device__ __noinline__ int64_t eval_costs_v(const uint8_t *ref, int pitch, size
   s.pred_x = pred_x;
   s.pred_y = pred_y;
   s.lambda = lambda;
+  constexpr int M = HBD ? 2 : 1;   // dwords per 4 samples
   switch ((bsx << 8) | bsy) {
-    case (16 << 8) | 16: return eval_t<4, 4, GRID>(s, lane, K, mx, my);
-    case (16 << 8) | 8: return eval_t<4, 3, GRID>(s, lane, K, mx, my);
-    case (8 << 8) | 16: return eval_t<2, 4, GRID>(s, lane, K, mx, my);
-    case (8 << 8) | 8: return eval_t<2, 3, GRID>(s, lane, K, mx, my);
-    case (8 << 8) | 4: return eval_t<2, 2, GRID>(s, lane, K, mx, my);
-    case (4 << 8) | 8: return eval_t<1, 3, GRID>(s, lane, K, mx, my);
-    default: return eval_t<1, 2, GRID>(s, lane, K, mx, my);
+    case (16 << 8) | 16: return eval_t<4 * M, 4, GRID, HBD>(s, lane, K, mx, my);
+    case (16 << 8) | 8: return eval_t<4 * M, 3, GRID, HBD>(s, lane, K, mx, my);
+    case (8 << 8) | 16: return eval_t<2 * M, 4, GRID, HBD>(s, lane, K, mx, my);
+    case (8 << 8) | 8: return eval_t<2 * M, 3, GRID, HBD>(s, lane, K, mx, my);
+    case (8 << 8) | 4: return eval_t<2 * M, 2, GRID, HBD>(s, lane, K, mx, my);
+    case (4 << 8) | 8: return eval_t<1 * M, 3, GRID, HBD>(s, lane, K, mx, my);
+    default: return eval_t<1 * M, 2, GRID, HBD>(s, lane, K, mx, my);
   }
 }
 
 // scalar arguments keep the out-of-line call's context in registers
-template <bool GRID>
+template <bool GRID, bool HBD>
 __device__ __forceinline__ int64_t eval_costs(const Search &s, int lane, int K, int mx, int my) {
-  return eval_costs_v<GRID>(s.ref, s.pitch, s.ps, s.W, s.H, s.cur, s.pos_x, s.pos_y, s.bsx, s.bsy, s.pred_x, s.pred_y,
+  return eval_costs_v<GRID, HBD>(s.ref, s.pitch, s.ps, s.W, s.H, s.cur, s.pos_x, s.pos_y, s.bsx, s.bsy, s.pred_x, s.pred_y,
                             s.lambda, lane, K, mx, my);
 }
 
@@ -230,7 +267,7 @@ __device__ __forceinline__ int64_t rl64(int64_t v, int j) {
 
 __device__ __forceinline__ int16_t int_mv(int v) { return (int16_t)(v & 0xFFFC); }   // set_integer_mv
 
-template <bool GRID>
+template <bool GRID, bool HBD>
 __device__ void search_one(const EpzsParams &p, const jmme_epzs_req &q, WaveLds &w, uint32_t *map, int lane,
                            jmme_epzs_res *out) {
   Search s;
@@ -256,7 +293,14 @@ __device__ void search_one(const EpzsParams &p, const jmme_epzs_req &q, WaveLds 
   const int side_y = GRID ? 2 * q.max_y + 1 : (2 * q.max_y >> 2) + 1;
   const int nq = q.bsx >> 2;
 
-  if (lane < nq * q.bsy) {
+  if constexpr (HBD) {   // 16-bit: bsx/2 dwords a row, up to 128
+    const int nd = q.bsx >> 1;
+    const uint16_t *cur16 = reinterpret_cast<const uint16_t *>(p.cur);
+    for (int i = lane; i < nd * q.bsy; i += 64) {
+      const int r = i / nd, c = i - r * nd;
+      w.cur[i] = *reinterpret_cast<const uint32_t *>(cur16 + (size_t)(q.pos_y + r) * p.pitch + q.pos_x + 2 * c);
+    }
+  } else if (lane < nq * q.bsy) {
     const int r = lane / nq, c = lane - r * nq;
     w.cur[lane] = *reinterpret_cast<const uint32_t *>(p.cur + (size_t)(q.pos_y + r) * p.pitch + q.pos_x + 4 * c);
   }
@@ -277,7 +321,7 @@ __device__ void search_one(const EpzsParams &p, const jmme_epzs_req &q, WaveLds 
   const int64_t lambda_dist = (int64_t)q.lambda * (variant ? 3 : 2);
   const int mv_range = variant ? 12 : 10;
   int64_t stop = q.medthres + lambda_dist, prev = q.prev_sad;
-  int64_t best = rl64(eval_costs<GRID>(s, lane, 1, s.cx, s.cy), 0);
+  int64_t best = rl64(eval_costs<GRID, HBD>(s, lane, 1, s.cx, s.cy), 0);
   int tmpx = s.cx, tmpy = s.cy, path = 5;
   bool update = true;
 
@@ -336,7 +380,7 @@ __device__ void search_one(const EpzsParams &p, const jmme_epzs_req &q, WaveLds 
       wave_sync();
       const int px = lane < ke ? w.pk[lane][0] : 0, py = lane < ke ? w.pk[lane][1] : 0;
       wave_sync();
-      const int64_t cost = eval_costs<GRID>(s, lane, ke, px, py);
+      const int64_t cost = eval_costs<GRID, HBD>(s, lane, ke, px, py);
       const int64_t thr3 = (3 * stop) >> 2;
       // sub-pel grid subMB: before the 3/4 check, the ref > 0 prevSad exit that
       // returns without touching *mv (me_epzs_int.c:590-600)
@@ -423,7 +467,7 @@ __device__ void search_one(const EpzsParams &p, const jmme_epzs_req &q, WaveLds 
           const int px = lane < ke ? w.pk[lane][0] : 0, py = lane < ke ? w.pk[lane][1] : 0;
           const int pi = lane < ke ? w.pk[lane][2] : 0;
           wave_sync();
-          const int64_t cost = eval_costs<GRID>(s, lane, ke, px, py);
+          const int64_t cost = eval_costs<GRID, HBD>(s, lane, ke, px, py);
           for (int j = 0; j < ke; ++j) {
             const int64_t c = rl64(cost, j);
             if (c < best) {
@@ -529,7 +573,7 @@ __device__ void search_one(const EpzsParams &p, const jmme_epzs_req &q, WaveLds 
 #endif
 // the search is latency-bound (a few dependent cache-resident fetch rounds
 // per search): waves in flight matter more than a few spilled registers
-template <bool GRID>
+template <bool GRID, bool HBD>
 __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(JMME_EPZS_WAVES_PER_EU))) void epzs_kernel(
     EpzsParams p) {
   __shared__ WaveLds s_w[kWaves];
@@ -541,7 +585,7 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(JMME_EPZS_W
     // requests of the other grid, or with a window the map was not sized for, are refused
     const bool ok = (GRID ? q.variant >= 2 : q.variant <= 1) && q.max_x <= p.max_qpel && q.max_y <= p.max_qpel;
     if (ok) {
-      search_one<GRID>(p, q, s_w[wave], map, lane, p.out + t);
+      search_one<GRID, HBD>(p, q, s_w[wave], map, lane, p.out + t);
     } else if (lane == 0) {
       jmme_epzs_res r{};
       r.path = -1;
@@ -562,15 +606,14 @@ hipError_t launch_epzs(const EpzsParams &p, hipStream_t s) {
   if (grid > 8192) grid = 8192;
   if (grid < 1) grid = 1;
   const size_t lds = (size_t)kWaves * p.map_words * sizeof(uint32_t);
+  auto k = p.grid ? (p.hbd ? epzs_kernel<true, true> : epzs_kernel<true, false>)
+                  : (p.hbd ? epzs_kernel<false, true> : epzs_kernel<false, false>);
   if (lds > 65536) {   // sub-pel grid beyond R = 45: one workgroup may take up to 160 KiB
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(p.grid ? epzs_kernel<true> : epzs_kernel<false>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds);
     if (e != hipSuccess) return e;
   }
-  if (p.grid)
-    hipLaunchKernelGGL(epzs_kernel<true>, dim3(grid), dim3(kWG), lds, s, p);
-  else
-    hipLaunchKernelGGL(epzs_kernel<false>, dim3(grid), dim3(kWG), lds, s, p);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(kWG), lds, s, p);
   return hipGetLastError();
 }
 

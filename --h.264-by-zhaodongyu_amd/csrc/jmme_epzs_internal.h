@@ -10,9 +10,10 @@ namespace jmme {
 constexpr int kEpzsMaxQpel = 4 * JMME_MAX_RANGE;   // largest searchRange.max_x / max_y (qpel)
 
 struct EpzsParams {
-  const uint8_t *cur;                  // current frame, 8-bit
+  const uint8_t *cur;                  // current frame: 8-bit, or 16-bit when hbd
   const uint8_t *const *refs;          // device table of reference planes (list * 32 + ref_idx)
-  int pitch, width, height;
+  int pitch, width, height;            // pitch in samples
+  int hbd;                             // 16-bit planes and sub-images (SourceBitDepthLuma 9..14)
   const jmme_epzs_req *req;
   const int16_t *preds, *stale;        // (x, y) pools
   jmme_epzs_res *out;

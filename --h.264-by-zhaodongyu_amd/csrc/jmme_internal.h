@@ -11,7 +11,7 @@ constexpr int kMaxRefs = 32;
 constexpr int kKey32MaxRange = 44;   // (2R+1)^2 < 2^13 spiral ranks fit the 32-bit key
 constexpr int kWG = 256;             // 4 waves of 64
 constexpr int kStampWGs = 4096;      // diagnostic builds: per-workgroup records
-constexpr int kCountWords = 16;      // KParams::counts, zeroed before every search launch
+constexpr int kCountWords = 16;      // KParams::counts; two sets, each launch's plan kernel zeroes the other
 
 // One work item of the search kernels: the partitions of one MB x ref unit
 // that share a search window AND a predictor/lambda (one SAD sweep serves all
@@ -56,6 +56,8 @@ struct KParams {
   unsigned item_cap;
   unsigned *counts;                   // kCountWords: [0] further groups, [1] unused, [2] status,
                                       // [8 + x] XCD x's item tickets (item kernel)
+  unsigned *counts_next;              // the other set: zeroed by the plan kernel for the next launch
+                                      // (no memset launch per search)
   uint32_t *debug_words;              // debug: unit 0's first staged window (rows x wp words)
   unsigned long long *stamps;         // diagnostic builds (JMME_STAMPS): per-unit phase clocks
 };

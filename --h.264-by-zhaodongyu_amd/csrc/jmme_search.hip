@@ -343,6 +343,9 @@ __global__ __launch_bounds__(64 * kPlanWaves) void me_plan_kernel(KParams p) {
   __shared__ unsigned s_n[kPlanWaves], s_off[kPlanWaves];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int u = blockIdx.x * kPlanWaves + wave;
+  // the next launch's counters (this launch's item kernel uses p.counts; stream
+  // order puts the next launch after it)
+  if (blockIdx.x == 0 && tid < kCountWords) p.counts_next[tid] = 0u;
   int ng = 0;
   bool slow = false;            // a lambda beyond the 32-bit keys: kItemSlow64 items
   unsigned long long my_gm = 0;

@@ -43,7 +43,7 @@ namespace {
 constexpr int64_t kDistMax = ((int64_t)0x7fffffff) << 5;   // DISTBLK_MAX, JM/lencod/inc/defines.h:135
 constexpr int kPadY = JMME_SUBPEL_PAD_Y, kPadX = JMME_SUBPEL_PAD_X;
 
-__device__ __forceinline__ int clip255(int v) { return min(max(v, 0), 255); }
+__device__ __forceinline__ int clipv(int v, int maxv) { return min(max(v, 0), maxv); }   // iClip1(max_imgpel_value)
 __device__ __forceinline__ int avg2(int a, int b) { return (a + b + 1) >> 1; }   // rshift_rnd_sf(a + b, 1)
 __device__ __forceinline__ int six(int c, int d, int b, int e, int a, int f) {   // ONE_FOURTH_TAP {20, -5, 1}
   return 20 * (c + d) - 5 * (b + e) + (a + f);
@@ -55,10 +55,26 @@ __device__ __forceinline__ uint32_t pack4(int a, int b, int c, int d) {
 // ------------------------------------------------------------ sub-images --
 constexpr int kTileW = 256, kTileH = 4, kSW = kTileW + 16, kSH = kTileH + 6;
 
-__global__ __launch_bounds__(256) void sub_images_kernel(const uint8_t *__restrict__ src, int src_pitch, int W, int H,
-                                                         uint8_t *__restrict__ dst, int dst_pitch, size_t plane_stride,
-                                                         int pw, int ph) {
-  __shared__ uint8_t S[kSH][kSW];
+// four samples of one row as written to a sub-image: one dword (8-bit) or two
+// (16-bit samples, SourceBitDepthLuma 9..14)
+template <typename T> struct Pack4;
+template <> struct Pack4<uint8_t> {
+  using V = uint32_t;
+  __device__ static V make(int a, int b, int c, int d) { return pack4(a, b, c, d); }
+};
+template <> struct Pack4<uint16_t> {
+  using V = uint2;
+  __device__ static V make(int a, int b, int c, int d) {
+    return make_uint2((uint32_t)a | ((uint32_t)b << 16), (uint32_t)c | ((uint32_t)d << 16));
+  }
+};
+
+// T = sample type; pitches and the plane stride in samples; maxv = max_imgpel_value
+template <typename T>
+__global__ __launch_bounds__(256) void sub_images_kernel(const T *__restrict__ src, int src_pitch, int W, int H,
+                                                         T *__restrict__ dst, int dst_pitch, size_t plane_stride,
+                                                         int pw, int ph, int maxv) {
+  __shared__ T S[kSH][kSW];
   const int X0 = blockIdx.x * kTileW, Y0 = blockIdx.y * kTileH;   // padded output coordinates
   // S[r][c] = picture sample (Y0 - kPadY - 2 + r, X0 - kPadX - 2 + c), clamped
   for (int k = threadIdx.x; k < kSH * kSW; k += 256) {
@@ -89,20 +105,21 @@ __global__ __launch_bounds__(256) void sub_images_kernel(const uint8_t *__restri
     s00[0][k] = I[2][k + 2];
     s00[1][k] = I[3][k + 2];
     // getVerSubImageSixTap
-    s20[k] = clip255((six(I[2][k + 2], I[3][k + 2], I[1][k + 2], I[4][k + 2], I[0][k + 2], I[5][k + 2]) + 16) >> 5);
+    s20[k] = clipv((six(I[2][k + 2], I[3][k + 2], I[1][k + 2], I[4][k + 2], I[0][k + 2], I[5][k + 2]) + 16) >> 5, maxv);
   }
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    s02[0][k] = clip255((h[2][k] + 16) >> 5);
-    s02[1][k] = clip255((h[3][k] + 16) >> 5);
+    s02[0][k] = clipv((h[2][k] + 16) >> 5, maxv);
+    s02[1][k] = clipv((h[3][k] + 16) >> 5, maxv);
     // getVerSubImageSixTapTmp
-    s22[k] = clip255((six(h[2][k], h[3][k], h[1][k], h[4][k], h[0][k], h[5][k]) + 512) >> 10);
+    s22[k] = clipv((six(h[2][k], h[3][k], h[1][k], h[4][k], h[0][k], h[5][k]) + 512) >> 10, maxv);
   }
-  uint32_t o[16];
-  o[0] = pack4(s00[0][0], s00[0][1], s00[0][2], s00[0][3]);
-  o[2] = pack4(s02[0][0], s02[0][1], s02[0][2], s02[0][3]);
-  o[8] = pack4(s20[0], s20[1], s20[2], s20[3]);
-  o[10] = pack4(s22[0], s22[1], s22[2], s22[3]);
+  using PK = Pack4<T>;
+  typename PK::V o[16];
+  o[0] = PK::make(s00[0][0], s00[0][1], s00[0][2], s00[0][3]);
+  o[2] = PK::make(s02[0][0], s02[0][1], s02[0][2], s02[0][3]);
+  o[8] = PK::make(s20[0], s20[1], s20[2], s20[3]);
+  o[10] = PK::make(s22[0], s22[1], s22[2], s22[3]);
   int q[12][4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -121,10 +138,10 @@ __global__ __launch_bounds__(256) void sub_images_kernel(const uint8_t *__restri
   }
   const int qi[12] = {1, 4, 5, 6, 9, 3, 7, 11, 12, 13, 14, 15};
 #pragma unroll
-  for (int j = 0; j < 12; ++j) o[qi[j]] = pack4(q[j][0], q[j][1], q[j][2], q[j][3]);
-  uint8_t *d = dst + (size_t)row * dst_pitch + col;
+  for (int j = 0; j < 12; ++j) o[qi[j]] = PK::make(q[j][0], q[j][1], q[j][2], q[j][3]);
+  T *d = dst + (size_t)row * dst_pitch + col;
 #pragma unroll
-  for (int k = 0; k < 16; ++k) *reinterpret_cast<uint32_t *>(d + (size_t)k * plane_stride) = o[k];
+  for (int k = 0; k < 16; ++k) *reinterpret_cast<typename PK::V *>(d + (size_t)k * plane_stride) = o[k];
 }
 
 // ------------------------------------------------------------- refinement --
@@ -148,6 +165,22 @@ __device__ __forceinline__ uint32_t ref4(const uint8_t *plane, int sp, int y, in
   const uintptr_t u = reinterpret_cast<uintptr_t>(a);
   const uint32_t *w = reinterpret_cast<const uint32_t *>(u & ~(uintptr_t)3);
   return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(u & 3));
+}
+
+// 4 samples of a row as ints: v[k] = p[k] (8-bit: one dword, any alignment)
+__device__ __forceinline__ void row4(const uint8_t *p, int (&v)[4]) {
+  const uintptr_t u = reinterpret_cast<uintptr_t>(p);
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(u & ~(uintptr_t)3);
+  const uint32_t d = __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(u & 3));
+#pragma unroll
+  for (int k = 0; k < 4; ++k) v[k] = (int)((d >> (8 * k)) & 255);
+}
+__device__ __forceinline__ void row4(const uint16_t *p, int (&v)[4]) {   // 16-bit samples, 2-byte aligned
+  const uintptr_t u = reinterpret_cast<uintptr_t>(p);
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(u & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)(u & 2);
+  const uint32_t d0 = __builtin_amdgcn_alignbyte(w[1], w[0], sh), d1 = __builtin_amdgcn_alignbyte(w[2], w[1], sh);
+  v[0] = (int)(d0 & 0xffff); v[1] = (int)(d0 >> 16); v[2] = (int)(d1 & 0xffff); v[3] = (int)(d1 >> 16);
 }
 
 __device__ __forceinline__ int had4_sum(const int *d) {   // HadamardSAD4x4 before its (s+1)>>1
@@ -225,15 +258,18 @@ constexpr int kMaxCand = 10;  // candidates of one phase (search_point tables: 1
 
 // One phase's job description of request k, as the cooperating lanes read it.
 // code: p0 [0,4) | lg_nb [4,7) | lg_nbx [8,10) | metric [12,14) | big 14 | sc [15,17) | tab 17
+template <typename T>
 struct WaveLds {
   int sums[kK][kMaxCand];
   int4 job[kK];                  // (mx, my, code, pos_x | pos_y << 16)
-  const uint8_t *sub[kK];
+  const T *sub[kK];
 };
 
 // The distortion sum of one transform / 4x4 block of one candidate
 // (computeSAD / computeSSE / computeSATD restated per block; their per-row or
 // per-block early exits are reproduced by dist() in the fold).
+// 8-bit samples: v_sad_u8 for SAD, bytes unpacked for SSE / SATD.  16-bit
+// samples (job_sum below): the same sums over unpacked samples.
 __device__ __forceinline__ int job_sum(const uint8_t *sub, size_t ps, int sp, const uint8_t *org, int cp, int ymax,
                                        int xmax, int metric, bool big, int cx, int cy, int bxo, int byo) {
   const int pl = ((cy & 3) << 2) | (cx & 3);
@@ -288,17 +324,75 @@ __device__ __forceinline__ int job_sum(const uint8_t *sub, size_t ps, int sp, co
   return s;
 }
 
+__device__ __forceinline__ int job_sum(const uint16_t *sub, size_t ps, int sp, const uint16_t *org, int cp, int ymax,
+                                       int xmax, int metric, bool big, int cx, int cy, int bxo, int byo) {
+  const int pl = ((cy & 3) << 2) | (cx & 3);
+  const uint16_t *plane = sub + (size_t)pl * ps;
+  int yy, xx;
+  if (metric == 2) {
+    yy = min(max((cy + (byo << 2)) >> 2, -kPadY), ymax);
+    xx = min(max((cx + (bxo << 2)) >> 2, -kPadX), xmax);
+  } else {
+    yy = min(max(cy >> 2, -kPadY), ymax) + byo;
+    xx = min(max(cx >> 2, -kPadX), xmax) + bxo;
+  }
+  org += (size_t)byo * cp + bxo;
+  auto ref = [&](int r, int c, int (&v)[4]) { row4(plane + (size_t)(yy + r + kPadY) * sp + (xx + c + kPadX), v); };
+  int s = 0;
+  if (metric <= 1) {   // computeSAD / computeSSE (int sums, as JM's mcost)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      int a[4], w[4];
+      row4(org + r * cp, a);
+      ref(r, 0, w);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int d = a[k] - w[k];
+        s += metric == 0 ? abs(d) : d * d;
+      }
+    }
+  } else if (!big) {
+    int d[16];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      int a[4], w[4];
+      row4(org + r * cp, a);
+      ref(r, 0, w);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) d[4 * r + k] = a[k] - w[k];
+    }
+    s = (had4_sum(d) + 1) >> 1;
+  } else {
+    int d[64];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        int a[4], w[4];
+        row4(org + r * cp + 4 * h, a);
+        ref(r, 4 * h, w);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) d[8 * r + 4 * h + k] = a[k] - w[k];
+      }
+    }
+    s = (had8_sum(d) + 2) >> 2;
+  }
+  return s;
+}
+
 // Per-request geometry the owner lane keeps.
+template <typename T>
 struct Own {
   int bsy, lg_nbx, pos_x, pos_y;
-  const uint8_t *sub;
+  const T *sub;
 };
 
 // One phase for the whole wave: owner lane k asks for the candidates at table
 // positions [p0, p1) of table `tab` scaled by `sc` around padded (mx, my) with
 // its metric; all 64 lanes share the (candidate, block) jobs of the 16
 // requests, pass after pass, and add the block sums into sums[k][c].
-__device__ void run_phase(const SubpelParams &p, WaveLds &L, int lane, const Own &o, int p0, int p1, int metric,
+template <typename T>
+__device__ void run_phase(const SubpelParams &p, WaveLds<T> &L, int lane, const Own<T> &o, int p0, int p1, int metric,
                           bool t8, int sc, int tab, int mx, int my) {
   const bool big = metric == 2 && t8;
   const int lg_nbx = big ? o.lg_nbx - 1 : o.lg_nbx;
@@ -343,7 +437,7 @@ __device__ void run_phase(const SubpelParams &p, WaveLds &L, int lane, const Own
       const int oy = ((jb.z >> 17) & 1) ? kEpzsPt[pos][1] : kSpiral9[pos][1];
       const int bs = jbig ? 8 : 4;
       const int bxo = (b & ((1 << jl_nbx) - 1)) * bs, byo = (b >> jl_nbx) * bs;
-      const uint8_t *org = p.cur + (size_t)(jb.w >> 16) * p.cur_pitch + (jb.w & 0xffff);
+      const T *org = reinterpret_cast<const T *>(p.cur) + (size_t)(jb.w >> 16) * p.cur_pitch + (jb.w & 0xffff);
       const int s = job_sum(L.sub[k], p.plane_stride, p.sub_pitch, org, p.cur_pitch, ymax, xmax, jm, jbig,
                             jb.x + jsc * ox, jb.y + jsc * oy, bxo, byo);
       atomicAdd(&L.sums[k][c], s);
@@ -352,13 +446,14 @@ __device__ void run_phase(const SubpelParams &p, WaveLds &L, int lane, const Own
   wave_sync();
 }
 
+template <typename T>
 __global__ __launch_bounds__(256) void subpel_kernel(SubpelParams p) {
-  __shared__ WaveLds lds[kWaves];
+  __shared__ WaveLds<T> lds[kWaves];
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int i0 = __builtin_amdgcn_readfirstlane((blockIdx.x * kWaves + wv) * p.per_wave);
   if (i0 >= p.n) return;
-  WaveLds &L = lds[wv];
+  WaveLds<T> &L = lds[wv];
   const int i = i0 + lane;
   // owner lanes: lane k < 16 holds request i0 + k; inactive owners ask for nothing
   jmme_subpel_req q{};
@@ -375,14 +470,14 @@ __global__ __launch_bounds__(256) void subpel_kernel(SubpelParams p) {
     mvy = ir.mv_y;
     min_mcost = q.start_hp ? (int64_t)ir.cost : kDistMax;
   }
-  Own o;
+  Own<T> o;
   int bsx = 4;
   o.bsy = 4;
   if (act) blk_size(q.blocktype, bsx, o.bsy);
   o.lg_nbx = bsx == 16 ? 2 : bsx == 8 ? 1 : 0;
   o.pos_x = q.pos_x;
   o.pos_y = q.pos_y;
-  o.sub = act ? p.subs[q.ref_slot] : p.subs[0];
+  o.sub = reinterpret_cast<const T *>(act ? p.subs[q.ref_slot] : p.subs[0]);
   const bool t8 = q.flags & JMME_SP_TEST8x8;
   const int pxp = q.pos_x << 2, pyp = q.pos_y << 2;   // pos_x_padded (mv_search.c:685-686)
   const int px = q.pred_x, py = q.pred_y;
@@ -526,11 +621,16 @@ __global__ __launch_bounds__(256) void subpel_kernel(SubpelParams p) {
 }  // namespace
 
 hipError_t launch_sub_images(const uint8_t *src, int src_pitch, int w, int h, uint8_t *dst, int dst_pitch,
-                             size_t plane_stride, hipStream_t s) {
+                             size_t plane_stride, hipStream_t s, int bits) {
   const int pw = w + 2 * kPadX, ph = h + 2 * kPadY;
   dim3 grid((pw + kTileW - 1) / kTileW, (ph + kTileH - 1) / kTileH);
-  hipLaunchKernelGGL(sub_images_kernel, grid, dim3(256), 0, s, src, src_pitch, w, h, dst, dst_pitch, plane_stride,
-                     pw, ph);
+  if (bits > 8)
+    hipLaunchKernelGGL(sub_images_kernel<uint16_t>, grid, dim3(256), 0, s, reinterpret_cast<const uint16_t *>(src),
+                       src_pitch, w, h, reinterpret_cast<uint16_t *>(dst), dst_pitch, plane_stride, pw, ph,
+                       (1 << bits) - 1);
+  else
+    hipLaunchKernelGGL(sub_images_kernel<uint8_t>, grid, dim3(256), 0, s, src, src_pitch, w, h, dst, dst_pitch,
+                       plane_stride, pw, ph, 255);
   return hipGetLastError();
 }
 
@@ -543,7 +643,10 @@ hipError_t launch_subpel(const SubpelParams &p, hipStream_t s) {
   const int waves_wanted = 256 * 4 * 2;   // two waves per SIMD over 256 CUs
   q.per_wave = std::min(kK, std::max(1, (p.n + waves_wanted - 1) / waves_wanted));
   const int per_wg = kWaves * q.per_wave;
-  hipLaunchKernelGGL(subpel_kernel, dim3((p.n + per_wg - 1) / per_wg), dim3(256), 0, s, q);
+  if (p.hbd)
+    hipLaunchKernelGGL(subpel_kernel<uint16_t>, dim3((p.n + per_wg - 1) / per_wg), dim3(256), 0, s, q);
+  else
+    hipLaunchKernelGGL(subpel_kernel<uint8_t>, dim3((p.n + per_wg - 1) / per_wg), dim3(256), 0, s, q);
   return hipGetLastError();
 }
 

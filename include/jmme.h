@@ -399,7 +399,10 @@ int jmme_epzs_search_ex(jmme_ctx *ctx, const jmme_epzs_req *req, int n, const in
  * IMG_PAD_SIZE_X = 32 columns (JM/lencod/inc/defines.h) exactly as
  * get_mem4Dpel_pad lays them out (memalloc.c:881-904).  Built on the device
  * for each uploaded reference slot when first needed (jmme_upload_ref marks a
- * slot's sub-images stale). */
+ * slot's sub-images stale).  A context with SourceBitDepthLuma 9..14 keeps
+ * 16-bit sub-images, the six-tap results clipped to (1 << bits) - 1
+ * (max_imgpel_value), and refines on them; the SSE metric is refused above 11
+ * bits, where JM's int sum (computeSSE, me_distortion.c:1197) can wrap. */
 #define JMME_SUBPEL_PAD_Y 20
 #define JMME_SUBPEL_PAD_X 32
 
@@ -410,7 +413,7 @@ int jmme_interpolate_ref(jmme_ctx *ctx, int list, int ref_idx, void *stream);
  * UnifiedOneForthPix, image.c:2148-2164); row pointers as get_mem4Dpel_pad
  * makes them (sub[dy][dx][j] points at column 0 of padded row j). */
 int jmme_get_sub_images(jmme_ctx *ctx, int list, int ref_idx, jmme_imgpel ****sub);
-/* device form over caller planes: d_src = 8-bit W x H plane (src_pitch bytes
+/* device form over caller planes (8-bit only): d_src = 8-bit W x H plane (src_pitch bytes
  * a row); d_dst = 16 planes, plane k = dy*4+dx at d_dst + k*plane_stride,
  * (H+40) rows of dst_pitch >= W+64 bytes, padded row 0 = picture row -20 */
 int jmme_sub_images_async(jmme_ctx *ctx, const uint8_t *d_src, int src_pitch, int width, int height,

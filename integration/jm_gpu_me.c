@@ -46,7 +46,8 @@ extern void __real_init_motion_search_module(VideoParameters *, InputParameters 
 extern void get_neighbors(Macroblock *currMB, PixelPos *block, int mb_x, int mb_y, int blockshape_x);
 
 static jmme_ctx *g_me = NULL;
-static int g_hbd = 0;   /* luma above 8 bits: sub-pel and EPZS stay on JM's CPU code (8-bit kernels) */
+static int g_hbd = 0;   /* luma above 8 bits: 16-bit planes (no chained guesses) */
+static int g_bits = 8;  /* SourceBitDepthLuma */
 static long long g_calls = 0, g_cpu_calls = 0;
 static FILE *g_trace = NULL, *g_trace_miss = NULL;   /* JMME_TRACE / JMME_TRACE_MISS */
 
@@ -109,6 +110,7 @@ static void init_once(VideoParameters *p_Vid, InputParameters *p_Inp)
    * context keeps 16-bit planes and searches with v_sad_u16 */
   c.SourceBitDepthLuma = p_Vid->bitdepth_luma > 0 ? p_Vid->bitdepth_luma : p_Inp->source.bit_depth[0];
   g_hbd = c.SourceBitDepthLuma > 8;
+  g_bits = c.SourceBitDepthLuma;
   g_me = jmme_create(&c, -1);
   if (!g_me) fail_jm("jmme_create");
 }
@@ -992,9 +994,11 @@ distblk __wrap_sub_pel_motion_estimation(Macroblock *currMB, MotionVector *pred_
   sp_ent want, *e, *tab;
   ++g_sp_calls;
   int mode = currMB->p_Inp->SearchMode[p_Vid->view_id];
-  /* GPU sub-pel follows a GPU integer search (FS / FFS); UMHEX's direct calls and
-   * weighted / chroma metrics stay on the CPU */
-  if (!speculating() || g_hbd || (mode != FULL_SEARCH && mode != FAST_FULL_SEARCH) || mh < 0 || mq < 0 ||
+  /* GPU sub-pel follows a GPU integer search (FS / FFS); UMHEX's direct calls,
+   * weighted / chroma metrics and SSE above 11 bits (libjmme refuses it: JM's int
+   * sum can wrap) stay on the CPU */
+  if (!speculating() || (mode != FULL_SEARCH && mode != FAST_FULL_SEARCH) || mh < 0 || mq < 0 ||
+      (g_bits > 11 && (mh == 1 || mq == 1)) ||
       mv_block->ChromaMEEnable || mv_block->search_pos2 > 9 || mv_block->search_pos4 > 9 ||
       (mv_block->test8x8 && mv_block->blocktype > 4)) {
     ++g_sp_cpu;
@@ -1239,7 +1243,7 @@ static distblk epzs_gpu(int variant, Macroblock *currMB, MotionVector *pred_mv, 
   jmme_epzs_res res;
   double t0, t1;
   init_once(currMB->p_Vid, p_Inp);
-  if (g_hbd || fs_on_cpu(mv_block) || 2 * max_x + 1 > side || 2 * max_y + 1 > side) {
+  if (fs_on_cpu(mv_block) || 2 * max_x + 1 > side || 2 * max_y + 1 > side) {
     ++g_epzs_cpu;
     return real_epzs(variant, currMB, pred_mv, mv_block, min_mcost, lambda_factor);
   }
@@ -1389,7 +1393,8 @@ distblk __wrap_EPZS_sub_pel_motion_estimation(Macroblock *currMB, MotionVector *
   jmme_subpel_req q;
   jmme_block_res r;
   init_once(p_Vid, currMB->p_Inp);
-  if (g_hbd || mh < 0 || mq < 0 || mv_block->ChromaMEEnable || mv_block->search_pos2 > 9 || mv_block->search_pos4 > 9 ||
+  if (mh < 0 || mq < 0 || (g_bits > 11 && (mh == 1 || mq == 1)) || mv_block->ChromaMEEnable ||
+      mv_block->search_pos2 > 9 || mv_block->search_pos4 > 9 ||
       (mv_block->test8x8 && mv_block->blocktype > 4)) {
     ++g_epzs_sp_cpu;
     return __real_EPZS_sub_pel_motion_estimation(currMB, pred_mv, mv_block, min_mcost, lambda_factor);

@@ -71,7 +71,7 @@ static int mvbits(int v)   /* JM/lencod/src/mv_search.c:366-374 */
 
 typedef struct ctx {
   const eo_req *q;
-  const uint8_t *cur, *ref;
+  const eo_pel *cur, *ref;
   int pitch, W, H;
   /* EPZSMap restated as the set of visited integer offsets from the centre */
   int side_x, side_y;
@@ -89,8 +89,8 @@ static int64_t cost_of(const ctx *c, int mx, int my)
   int x, y, sad = 0;
   const int ox = q->pos_x + (mx >> 2), oy = q->pos_y + (my >> 2);
   for (y = 0; y < q->bsy; y++) {
-    const uint8_t *rrow = c->ref + (size_t)clampi(oy + y, 0, c->H - 1) * c->pitch;
-    const uint8_t *crow = c->cur + (size_t)(q->pos_y + y) * c->pitch + q->pos_x;
+    const eo_pel *rrow = c->ref + (size_t)clampi(oy + y, 0, c->H - 1) * c->pitch;
+    const eo_pel *crow = c->cur + (size_t)(q->pos_y + y) * c->pitch + q->pos_x;
     for (x = 0; x < q->bsx; x++) {
       int d = crow[x] - rrow[clampi(ox + x, 0, c->W - 1)];
       sad += d < 0 ? -d : d;
@@ -117,7 +117,7 @@ static int visit(ctx *c, int mx, int my)
 
 static int16_t int_mv(int16_t v) { return (int16_t)(v & 0xFFFC); }   /* set_integer_mv, me_epzs.c:39-43 */
 
-void eo_epzs(const eo_req *q, const int16_t *preds, const int16_t *stale, const uint8_t *cur, const uint8_t *ref,
+void eo_epzs(const eo_req *q, const int16_t *preds, const int16_t *stale, const eo_pel *cur, const eo_pel *ref,
              int pitch, int W, int H, eo_res *out)
 {
   ctx c;
@@ -263,8 +263,8 @@ done_noupdate:
   free(c.map);
 }
 
-void eo_epzs_batch(const eo_req *q, int n, const int16_t *preds, const int16_t *stale, const uint8_t *cur,
-                   const uint8_t *const *refs, int pitch, int W, int H, eo_res *out)
+void eo_epzs_batch(const eo_req *q, int n, const int16_t *preds, const int16_t *stale, const eo_pel *cur,
+                   const eo_pel *const *refs, int pitch, int W, int H, eo_res *out)
 {
   int i;
   for (i = 0; i < n; i++)
@@ -285,7 +285,7 @@ void eo_epzs_batch(const eo_req *q, int n, const int16_t *preds, const int16_t *
  * padded row 0 = picture row -20 (getSubImagesLuma layout). */
 typedef struct gctx {
   const eo_req *q;
-  const uint8_t *cur, *subs;
+  const eo_pel *cur, *subs;
   int pitch, W, H, sp, sh;   /* cur pitch; sub-image pitch / rows */
   int side_x;
   unsigned char *map;
@@ -299,11 +299,11 @@ static int64_t gcost_of(const gctx *c, int mx, int my)
   const int cx = mx + (q->pos_x << 2), cy = my + (q->pos_y << 2);   /* pad_MVs */
   /* UMVLine4X (refbuf.h:22-26): size_y_pad = H+3, size_x_pad = W+15 (mbuffer.c:549-550) */
   const int yy = clampi(cy >> 2, -20, c->H + 3), xx = clampi(cx >> 2, -32, c->W + 15);
-  const uint8_t *plane = c->subs + (size_t)((cy & 3) * 4 + (cx & 3)) * c->sp * c->sh;
+  const eo_pel *plane = c->subs + (size_t)((cy & 3) * 4 + (cx & 3)) * c->sp * c->sh;
   int x, y, sad = 0;
   for (y = 0; y < q->bsy; y++) {
-    const uint8_t *rrow = plane + (size_t)(yy + 20 + y) * c->sp + (xx + 32);
-    const uint8_t *crow = c->cur + (size_t)(q->pos_y + y) * c->pitch + q->pos_x;
+    const eo_pel *rrow = plane + (size_t)(yy + 20 + y) * c->sp + (xx + 32);
+    const eo_pel *crow = c->cur + (size_t)(q->pos_y + y) * c->pitch + q->pos_x;
     for (x = 0; x < q->bsx; x++) {
       int d = crow[x] - rrow[x];
       sad += d < 0 ? -d : d;
@@ -327,8 +327,8 @@ static int gvisit(gctx *c, int mx, int my)
   return 1;
 }
 
-void eo_epzs_grid(const eo_req *q, const int16_t *preds, const int16_t *stale, const uint8_t *cur, int pitch,
-                  const uint8_t *subs, int W, int H, eo_res *out)
+void eo_epzs_grid(const eo_req *q, const int16_t *preds, const int16_t *stale, const eo_pel *cur, int pitch,
+                  const eo_pel *subs, int W, int H, eo_res *out)
 {
   gctx c;
   const int frame = q->flags & 1, pslice = (q->flags >> 1) & 1, bt = q->blocktype, refi = q->ref_idx;
@@ -496,8 +496,8 @@ done_noupdate:
   free(c.map);
 }
 
-void eo_epzs_grid_batch(const eo_req *q, int n, const int16_t *preds, const int16_t *stale, const uint8_t *cur,
-                        int pitch, const uint8_t *const *subs, int W, int H, eo_res *out)
+void eo_epzs_grid_batch(const eo_req *q, int n, const int16_t *preds, const int16_t *stale, const eo_pel *cur,
+                        int pitch, const eo_pel *const *subs, int W, int H, eo_res *out)
 {
   int i;
   for (i = 0; i < n; i++)

@@ -24,6 +24,14 @@
 extern "C" {
 #endif
 
+/* Sample type of the planes: 8-bit, or JM's 16-bit imgpel for SourceBitDepthLuma
+ * 9..14 (build/libepzs_oracle16.so is this file compiled with -DEO_PEL16). */
+#ifdef EO_PEL16
+typedef uint16_t eo_pel;
+#else
+typedef uint8_t eo_pel;
+#endif
+
 typedef struct eo_req {
   int16_t pos_x, pos_y, bsx, bsy;
   int16_t blocktype, ref_idx;
@@ -46,12 +54,12 @@ typedef struct eo_res {
 
 /* one search; cur / ref 8-bit W x H planes with `pitch`; preds / stale are
  * (x, y) int16 pairs (stale: qpel offsets from the centre) */
-void eo_epzs(const eo_req *q, const int16_t *preds, const int16_t *stale, const uint8_t *cur, const uint8_t *ref,
+void eo_epzs(const eo_req *q, const int16_t *preds, const int16_t *stale, const eo_pel *cur, const eo_pel *ref,
              int pitch, int W, int H, eo_res *out);
 
 /* batch: request i searches ref plane refs[q.plane] */
-void eo_epzs_batch(const eo_req *q, int n, const int16_t *preds, const int16_t *stale, const uint8_t *cur,
-                   const uint8_t *const *refs, int pitch, int W, int H, eo_res *out);
+void eo_epzs_batch(const eo_req *q, int n, const int16_t *preds, const int16_t *stale, const eo_pel *cur,
+                   const eo_pel *const *refs, int pitch, int W, int H, eo_res *out);
 
 /* EPZSSubPelGrid = 1 (variants 2 EPZS_integer_motion_estimation, 3
  * EPZS_integer_subMB_motion_estimation, JM/lencod/src/me_epzs_int.c:41-782):
@@ -59,10 +67,10 @@ void eo_epzs_batch(const eo_req *q, int n, const int16_t *preds, const int16_t *
  * 8-bit, getSubImagesLuma layout, subpel_oracle.h).  Extra paths: 6 = the
  * subMB predictor-loop prevSad exit (mv untouched), 7 = the post-predictor
  * prevSad exit of variant 2 (mv = best). */
-void eo_epzs_grid(const eo_req *q, const int16_t *preds, const int16_t *stale, const uint8_t *cur, int pitch,
-                  const uint8_t *subs, int W, int H, eo_res *out);
-void eo_epzs_grid_batch(const eo_req *q, int n, const int16_t *preds, const int16_t *stale, const uint8_t *cur,
-                        int pitch, const uint8_t *const *subs, int W, int H, eo_res *out);
+void eo_epzs_grid(const eo_req *q, const int16_t *preds, const int16_t *stale, const eo_pel *cur, int pitch,
+                  const eo_pel *subs, int W, int H, eo_res *out);
+void eo_epzs_grid_batch(const eo_req *q, int n, const int16_t *preds, const int16_t *stale, const eo_pel *cur,
+                        int pitch, const eo_pel *const *subs, int W, int H, eo_res *out);
 
 #ifdef __cplusplus
 }

@@ -9,7 +9,10 @@
 
 #define DISTBLK_MAX (((int64_t)0x7fffffff) << 5)   /* JM/lencod/inc/defines.h:135 */
 
-static inline int clip255(int v) { return v < 0 ? 0 : (v > 255 ? 255 : v); }   /* iClip1(max_imgpel_value) */
+/* p_Vid->max_imgpel_value = (1 << bitdepth_luma) - 1 (image.c init_img); 255 unless set */
+static int g_max_pel = 255;
+void spo_set_bitdepth(int bits) { g_max_pel = (1 << bits) - 1; }
+static inline int clip255(int v) { return v < 0 ? 0 : (v > g_max_pel ? g_max_pel : v); }   /* iClip1(max_imgpel_value) */
 static inline int rnd_sf(int x, int a) { return (x + (1 << (a - 1))) >> a; }    /* rshift_rnd_sf, ifunctions.h */
 static inline int imin_(int a, int b) { return a < b ? a : b; }
 static inline int imax_(int a, int b) { return a > b ? a : b; }

@@ -24,6 +24,10 @@ extern "C" {
  * column (i+SPO_PAD_X) holding JM's p_curr_img_sub[dy][dx][j][i]. */
 void spo_sub_images(const uint16_t *src, int W, int H, uint16_t *out);
 
+/* The interpolation's clip bound, JM's max_imgpel_value = (1 << bits) - 1
+ * (SourceBitDepthLuma); 8 unless set.  Process-wide. */
+void spo_set_bitdepth(int bits);
+
 /* One sub-pel refinement with JM's inputs.  sub = spo_sub_images() output of
  * the reference; cur = W x H current picture.  Metrics: 0 SAD (computeSAD,
  * me_distortion.c:349-426), 1 SSE (computeSSE :1189-1240), 2 SATD

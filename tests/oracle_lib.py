@@ -280,26 +280,30 @@ EPZS_REQ = np.dtype([("pos_x", "<i2"), ("pos_y", "<i2"), ("bsx", "<i2"), ("bsy",
 EPZS_RES = np.dtype([("mv_x", "<i2"), ("mv_y", "<i2"), ("path", "<i4"), ("cost", "<i8"), ("prev_sad", "<i8")])
 assert EPZS_REQ.itemsize == 80 and EPZS_RES.itemsize == 24
 EP_SO = os.path.join(ORACLE_DIR, "build", "libepzs_oracle.so")
-_ep = None
+EP16_SO = os.path.join(ORACLE_DIR, "build", "libepzs_oracle16.so")   # 16-bit samples (-DEO_PEL16)
+_ep = {}
 
 
-def load_epzs() -> ctypes.CDLL:
-    global _ep
-    if _ep is not None:
-        return _ep
+def load_epzs(wide: bool = False) -> ctypes.CDLL:
+    if wide in _ep:
+        return _ep[wide]
+    so = EP16_SO if wide else EP_SO
     src = os.path.join(ORACLE_DIR, "epzs_oracle.c")
-    if not os.path.exists(EP_SO) or os.path.getmtime(EP_SO) < os.path.getmtime(src):
+    if not os.path.exists(so) or os.path.getmtime(so) < os.path.getmtime(src):
         subprocess.run(["make", "-s", "-C", ORACLE_DIR, "port"], check=True)
-    lib = ctypes.CDLL(EP_SO)
+    lib = ctypes.CDLL(so)
     P, I = ctypes.c_void_p, ctypes.c_int
     lib.eo_epzs_batch.argtypes = [P, I, P, P, P, P, I, I, I, P]
-    _ep = lib
+    _ep[wide] = lib
     return lib
 
 
 def epzs_batch(req, preds, stale, cur, refs):
-    """req EPZS_REQ[n]; preds/stale int16 [k, 2] pools; cur / refs[plane] uint8 HxW -> EPZS_RES[n]"""
-    lib = load_epzs()
+    """req EPZS_REQ[n]; preds/stale int16 [k, 2] pools; cur / refs[plane] HxW -> EPZS_RES[n];
+    uint16 planes (SourceBitDepthLuma 9..14) go to the 16-bit build of the restatement"""
+    wide = np.asarray(cur).dtype == np.uint16
+    pel = np.uint16 if wide else np.uint8
+    lib = load_epzs(wide)
     req = np.ascontiguousarray(req, EPZS_REQ)
     preds = np.ascontiguousarray(preds, np.int16).reshape(-1, 2)
     stale = np.ascontiguousarray(stale, np.int16).reshape(-1, 2)
@@ -307,8 +311,8 @@ def epzs_batch(req, preds, stale, cur, refs):
         preds = np.zeros((1, 2), np.int16)
     if len(stale) == 0:
         stale = np.zeros((1, 2), np.int16)
-    cur = np.ascontiguousarray(cur, np.uint8)
-    refs = [np.ascontiguousarray(r, np.uint8) for r in refs]
+    cur = np.ascontiguousarray(cur, pel)
+    refs = [np.ascontiguousarray(r, pel) for r in refs]
     h, w = cur.shape
     ptrs = (ctypes.c_void_p * len(refs))(*[r.ctypes.data for r in refs])
     out = np.zeros(len(req), EPZS_RES)
@@ -338,18 +342,24 @@ def load_subpel() -> ctypes.CDLL:
     lib = ctypes.CDLL(SP_SO)
     P, I = ctypes.c_void_p, ctypes.c_int
     lib.spo_sub_images.argtypes = [P, I, I, P]
+    lib.spo_set_bitdepth.argtypes = [I]
     lib.spo_sub_pel_batch.argtypes = [P, P, I, I, P, I, I, P, P]
     _sp = lib
     return lib
 
 
-def sub_images(plane: np.ndarray) -> np.ndarray:
-    """getSubImagesLuma of an HxW plane -> uint16 [16, H+40, W+64] (JM's padded sub-images)"""
+def sub_images(plane: np.ndarray, bits: int = 8) -> np.ndarray:
+    """getSubImagesLuma of an HxW plane -> uint16 [16, H+40, W+64] (JM's padded sub-images);
+    bits = SourceBitDepthLuma (the six-tap clip bound)"""
     lib = load_subpel()
     src = np.ascontiguousarray(plane, np.uint16)
     h, w = src.shape
     out = np.zeros((16, h + 40, w + 64), np.uint16)
-    lib.spo_sub_images(src.ctypes.data, w, h, out.ctypes.data)
+    lib.spo_set_bitdepth(int(bits))
+    try:
+        lib.spo_sub_images(src.ctypes.data, w, h, out.ctypes.data)
+    finally:
+        lib.spo_set_bitdepth(8)
     return out
 
 
@@ -367,9 +377,12 @@ def sub_pel_batch(cur: np.ndarray, sub: np.ndarray, req: np.ndarray, epzs: bool)
     return mv, cost
 
 
-def epzs_grid_batch(req, preds, stale, cur, refs):
-    """EPZSSubPelGrid = 1 searches (variants 2 / 3) against the sub-images of refs[plane] -> EPZS_RES[n]"""
-    lib = load_epzs()
+def epzs_grid_batch(req, preds, stale, cur, refs, bits=8):
+    """EPZSSubPelGrid = 1 searches (variants 2 / 3) against the sub-images of refs[plane] -> EPZS_RES[n];
+    bits > 8: uint16 planes and 16-bit sub-images clipped to (1 << bits) - 1"""
+    wide = bits > 8
+    pel = np.uint16 if wide else np.uint8
+    lib = load_epzs(wide)
     if not hasattr(lib, "_grid_sig"):
         P, I = ctypes.c_void_p, ctypes.c_int
         lib.eo_epzs_grid_batch.argtypes = [P, I, P, P, P, I, P, I, I, P]
@@ -381,8 +394,8 @@ def epzs_grid_batch(req, preds, stale, cur, refs):
         preds = np.zeros((1, 2), np.int16)
     if len(stale) == 0:
         stale = np.zeros((1, 2), np.int16)
-    cur = np.ascontiguousarray(cur, np.uint8)
-    subs = [np.ascontiguousarray(sub_images(r).astype(np.uint8)) for r in refs]
+    cur = np.ascontiguousarray(cur, pel)
+    subs = [np.ascontiguousarray(sub_images(r, bits).astype(pel)) for r in refs]
     h, w = cur.shape
     ptrs = (ctypes.c_void_p * len(subs))(*[s.ctypes.data for s in subs])
     out = np.zeros(len(req), EPZS_RES)

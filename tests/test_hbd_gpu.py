@@ -99,9 +99,9 @@ def test_hbd_extremes_14bit(gpu):
 
 
 def test_hbd_refusals(gpu):
-    """samples above the declared depth are refused at upload; the 8-bit-only
-    paths (sub-pel planes / refinement, EPZS) refuse a high-bit-depth context"""
-    from jmme import EPZS_REQ, SUBPEL_REQ, JmmeError, MotionEstimator
+    """samples above the declared depth are refused at upload; SSE sub-pel
+    refinement is refused above 11 bits (JM's int sum can wrap there)"""
+    from jmme import SUBPEL_REQ, JmmeError, MotionEstimator
     plane = np.full((32, 32), 1023, np.uint16)
     with MotionEstimator({"SourceBitDepthLuma": 10}) as me:
         me.upload_cur(plane)
@@ -110,12 +110,127 @@ def test_hbd_refusals(gpu):
             me.upload_cur(np.full((32, 32), 1024, np.uint16))
         q = np.zeros(1, SUBPEL_REQ)
         q["blocktype"] = 1
-        with pytest.raises(JmmeError):
-            me.subpel_refine(q)
-        e = np.zeros(1, EPZS_REQ)
-        e["bsx"] = e["bsy"] = 16
-        e["blocktype"] = 1
-        with pytest.raises(JmmeError):
-            me.epzs_search(e, np.zeros((0, 2), np.int16))
+        q["metric_h"] = q["metric_q"] = 1
+        q["search_pos2"] = q["search_pos4"] = 9
+        me.subpel_validate(q)                       # SSE at 10 bits: served
     with pytest.raises(JmmeError):
         MotionEstimator({"SourceBitDepthLuma": 15})
+    with MotionEstimator({"SourceBitDepthLuma": 12}) as me:
+        p12 = np.full((32, 32), 4095, np.uint16)
+        me.upload_cur(p12)
+        me.upload_ref(0, 0, p12)
+        q["metric_q"] = 2
+        with pytest.raises(JmmeError):               # SSE half-pel at 12 bits
+            me.subpel_refine(q)
+        q["metric_h"] = 0
+        me.subpel_validate(q)
+
+
+# ---- sub-pel at high bit depth: 16-bit sub-images (getSubImagesLuma with
+# max_imgpel_value = (1 << bits) - 1, img_luma.c:184-329) and the refinement on
+# them (me_fullsearch.c:186-289, me_epzs_sub.c:30-222), vs the restatement
+
+@pytest.mark.parametrize("bits,hw", [(10, (144, 176)), (12, (64, 96)), (14, (48, 32))])
+def test_hbd_sub_images_vs_oracle(gpu, bits, hw):
+    from jmme import MotionEstimator
+    h, w = hw
+    rng = np.random.default_rng(bits)
+    top = (1 << bits) - 1
+    # extremes exercise the six-tap clip at 0 and max_imgpel_value
+    plane = np.where(rng.random((h, w)) < 0.3, rng.choice(np.array([0, top, 1, top - 1]), size=(h, w)),
+                     rng.integers(0, top + 1, size=(h, w))).astype(np.uint16)
+    with MotionEstimator({"SourceBitDepthLuma": bits}) as me:
+        me.upload_cur(plane)
+        me.upload_ref(0, 2, plane)
+        got = me.sub_images(0, 2)
+    exp = ol.sub_images(plane, bits)
+    bad = [k for k in range(16) if not np.array_equal(got[k], exp[k])]
+    assert not bad, (bits, bad)
+    assert got.max() == top   # the clip bound is reached (not 255)
+
+
+@pytest.mark.parametrize("bits,seed", [(10, 1), (10, 2), (11, 3), (12, 4), (14, 5)])
+def test_hbd_refinement_random_vs_oracle(gpu, bits, seed):
+    """both refinement functions, SAD / SSE / SATD 4x4 / 8x8 (SSE up to 11 bits),
+    finite bounds, vectors outside the picture"""
+    from jmme import MotionEstimator
+    from test_subpel_gpu import random_requests, to_oracle
+    rng = np.random.default_rng(100 + seed)
+    h, w = (144, 176) if seed != 2 else (288, 352)
+    cur, ref = _planes(w, h, bits, seed=seed)[::-1]
+    q = random_requests(rng, 4000, w, h)
+    if bits > 11:   # SSE is refused there
+        q["metric_h"] = np.where(q["metric_h"] == 1, 2, q["metric_h"])
+        q["metric_q"] = np.where(q["metric_q"] == 1, 0, q["metric_q"])
+    # bounds on the scale of these samples (the 8-bit generator's are too small to bind)
+    big = rng.random(len(q)) < 0.3
+    q["min_mcost"] = np.where(big, rng.integers(0, 60000, len(q)) * 32 << (bits - 8), q["min_mcost"])
+    with MotionEstimator({"SourceBitDepthLuma": bits}) as me:
+        me.upload_cur(cur)
+        me.upload_ref(0, 0, ref)
+        got = me.subpel_refine(q)
+    sub = ol.sub_images(ref, bits)
+    mv = np.zeros((len(q), 2), np.int16)
+    cost = np.zeros(len(q), np.int64)
+    o = to_oracle(q)
+    for v in (0, 1):
+        k = q["variant"] == v
+        mv[k], cost[k] = ol.sub_pel_batch(cur, sub, o[k], bool(v))
+    bad = np.nonzero((got["mv_x"] != mv[:, 0]) | (got["mv_y"] != mv[:, 1]) | (got["cost"] != cost))[0]
+    assert len(bad) == 0, (bits, len(bad), q[bad[:3]], got[bad[:3]], mv[bad[:3]], cost[bad[:3]])
+
+
+
+# ---- EPZS at high bit depth: the v_sad_u16 instantiation of the EPZS kernel on
+# 16-bit planes (integer grid) and 16-bit sub-images (EPZSSubPelGrid = 1), vs
+# the 16-bit build of the restatement (oracle/epzs_oracle.c -DEO_PEL16)
+
+@pytest.mark.parametrize("bits,grid,seed", [(10, 0, 0), (10, 1, 1), (12, 0, 2), (14, 1, 3)])
+def test_hbd_epzs_random_vs_restatement(gpu, bits, grid, seed):
+    from jmme import MotionEstimator
+    from test_epzs_gpu import _random_requests, _run_frame
+    rng = np.random.default_rng(200 + seed)
+    w, h = 96, 64
+    cur, r1 = _planes(w, h, bits, seed=seed)[::-1]
+    r0 = _planes(w, h, bits, seed=seed + 50, gmv=(-1, 2))[0]
+    refs = [r1, r0]
+    req, preds, stale = _random_requests(rng, w, h, 1500)
+    sc = 1 << (bits - 8)   # thresholds on the scale of these SADs
+    for k in ("medthres", "stop_crit"):
+        req[k] = req[k] * sc
+    if grid:
+        req["variant"] += 2
+        req["center_x"] += rng.integers(-3, 4, len(req))
+        req["center_y"] += rng.integers(-3, 4, len(req))
+        req["max_x"] = np.minimum(req["max_x"], 128)
+        req["pattern"] = rng.choice([0, 1, 2, 3, 4, 5], len(req))
+        exp = ol.epzs_grid_batch(req, preds, stale, cur, refs, bits)
+    else:
+        exp = ol.epzs_batch(req, preds, stale, cur, refs)
+    cfg = {"SourceBitDepthLuma": bits, "SearchMode": 3, "EPZSSubPelGrid": grid, "SearchRange": 32}
+    with MotionEstimator(cfg) as me:
+        got = _run_frame(me, cur, refs, req, preds, stale)
+    for k in ("mv_x", "mv_y", "path", "cost", "prev_sad"):
+        bad = np.nonzero(got[k] != exp[k])[0]
+        assert len(bad) == 0, (k, len(bad), req[bad[:2]], got[bad[:2]], exp[bad[:2]])
+    assert len(set(np.unique(exp["path"]))) >= 4
+
+
+@pytest.mark.parametrize("grid", [0])   # (sub-images differ: the six-tap clip is max_imgpel_value)
+def test_hbd_epzs_equals_8bit_on_8bit_content(gpu, grid):
+    from jmme import MotionEstimator, synth
+    from test_epzs_gpu import _random_requests, _run_frame
+    rng = np.random.default_rng(7 + grid)
+    w, h = 96, 64
+    luma = synth.luma_sequence(w, h, 3, seed=4, gmv=(2, -1))
+    cur, refs = luma[2], [luma[1], luma[0]]
+    req, preds, stale = _random_requests(rng, w, h, 1500)
+    if grid:
+        req["variant"] += 2
+        req["max_x"] = np.minimum(req["max_x"], 128)
+    res = []
+    for bits in (8, 10):
+        cfg = {"SourceBitDepthLuma": bits, "SearchMode": 3, "EPZSSubPelGrid": grid, "SearchRange": 32}
+        with MotionEstimator(cfg) as me:
+            res.append(_run_frame(me, cur, refs, req, preds, stale))
+    assert np.array_equal(res[0], res[1])
