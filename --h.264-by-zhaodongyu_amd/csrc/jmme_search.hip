@@ -730,7 +730,11 @@ __device__ __forceinline__ void sweep_v5(const Lds &L, const uint32_t (&cs)[64],
   const int wp = WP ? WP : L.wp;
   const uint32_t tb = lds_addr(L.tmax) + 32u * (uint32_t)ufl(tid >> 6);   // this wave's elimination bounds
   for (int t = tid; t < ntask; t += kWG) {
-    if (rows64 && t >= nrow64) {                       // a column past 63
+    // a column past 63.  nrow64 is a multiple of 64, so the test is the same for
+    // every lane of the wave: tested on the first lane it is a scalar branch, and
+    // the division stays out of the row tasks (as a per-lane test the compiler
+    // selected its result into every task: ~20 VALU a task)
+    if (rows64 && ufl(t) >= nrow64) {
       const int e = t - nrow64;
       tq = e / (D - 64);
       tx = 64 + e - tq * (D - 64);
