@@ -12,12 +12,13 @@
 //
 // Interpolation.  Every JM sub-image, including its padding, equals the
 // filter evaluated on the edge-replicated picture (JM clamps each tap into
-// the padded plane, whose border is itself a replica), so a 4 x 256 output
-// tile needs only a 10 x 265 integer tile with clamped reads.  One thread
-// makes 4 columns of one row for all 16 sub-images: 24 horizontal and 5
-// vertical six-tap sums, the (+512)>>10 centre sample, then the 12 bilinear
-// averages, written as one dword per sub-image.  The kernel is a one-pass
-// stream: 1 B read, 16 B written per padded sample (HBM roofline).
+// the padded plane, whose border is itself a replica), so an 8 x 256 output
+// tile needs only a 14 x 262 integer tile with clamped reads.  One thread
+// makes 4 columns of two rows for all 16 sub-images: 28 horizontal six-tap
+// sums shared by the two rows, 5 vertical ones and the (+512)>>10 centre
+// sample per row, then the 12 bilinear averages, written as one dword (8-bit)
+// or two (16-bit) per sub-image.  The kernel is a one-pass stream: 1 sample
+// read, 16 written per padded sample (HBM roofline).
 //
 // Refinement.  One wave per 16 refinements; lane k < 16 owns refinement k and
 // runs JM's control flow for it.  Each phase of JM's loop (the half-pel ring,
@@ -53,7 +54,10 @@ __device__ __forceinline__ uint32_t pack4(int a, int b, int c, int d) {
 }
 
 // ------------------------------------------------------------ sub-images --
-constexpr int kTileW = 256, kTileH = 4, kSW = kTileW + 16, kSH = kTileH + 6;
+// A workgroup makes a 256 x 8 tile of every sub-image; a thread makes 4 columns
+// of two consecutive rows, sharing the 7 rows of horizontal six-tap sums the two
+// need (a 4-row tile with one row a thread needed 6 per row).
+constexpr int kTileW = 256, kTileH = 8, kSW = kTileW + 16, kSH = kTileH + 6;
 
 // four samples of one row as written to a sub-image: one dword (8-bit) or two
 // (16-bit samples, SourceBitDepthLuma 9..14)
@@ -83,65 +87,70 @@ __global__ __launch_bounds__(256) void sub_images_kernel(const T *__restrict__ s
     S[r][c] = src[(size_t)y * src_pitch + x];
   }
   __syncthreads();
-  const int ty = threadIdx.x >> 6, tx = threadIdx.x & 63;   // a wave writes 256 contiguous bytes per sub-image
-  const int row = Y0 + ty, col = X0 + 4 * tx;
-  if (row >= ph || col >= pw) return;
-  int I[6][9];   // I[dr + 2][dc + 2] = sample at (row + dr, col + dc)
+  const int ty = threadIdx.x >> 6, tx = threadIdx.x & 63;   // a wave writes 256 contiguous samples per sub-image
+  const int row0 = Y0 + 2 * ty, col = X0 + 4 * tx;
+  if (row0 >= ph || col >= pw) return;
+  int I[7][9];   // I[dr + 2][dc + 2] = sample at (row0 + dr, col + dc)
 #pragma unroll
-  for (int r = 0; r < 6; ++r)
+  for (int r = 0; r < 7; ++r)
 #pragma unroll
-    for (int c = 0; c < 9; ++c) I[r][c] = S[ty + r][4 * tx + c];
-  // horizontal six-tap (getHorSubImageSixTap) at rows -2..3, columns 0..3: the
+    for (int c = 0; c < 9; ++c) I[r][c] = S[2 * ty + r][4 * tx + c];
+  // horizontal six-tap (getHorSubImageSixTap) at rows -2..4, columns 0..3: the
   // unrounded sums are p_Vid->imgY_sub_tmp
-  int h[6][4];
+  int h[7][4];
 #pragma unroll
-  for (int r = 0; r < 6; ++r)
+  for (int r = 0; r < 7; ++r)
 #pragma unroll
     for (int k = 0; k < 4; ++k)
       h[r][k] = six(I[r][k + 2], I[r][k + 3], I[r][k + 1], I[r][k + 4], I[r][k], I[r][k + 5]);
-  int s00[2][5], s02[2][4], s20[5], s22[4];
-#pragma unroll
-  for (int k = 0; k < 5; ++k) {
-    s00[0][k] = I[2][k + 2];
-    s00[1][k] = I[3][k + 2];
-    // getVerSubImageSixTap
-    s20[k] = clipv((six(I[2][k + 2], I[3][k + 2], I[1][k + 2], I[4][k + 2], I[0][k + 2], I[5][k + 2]) + 16) >> 5, maxv);
-  }
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    s02[0][k] = clipv((h[2][k] + 16) >> 5, maxv);
-    s02[1][k] = clipv((h[3][k] + 16) >> 5, maxv);
-    // getVerSubImageSixTapTmp
-    s22[k] = clipv((six(h[2][k], h[3][k], h[1][k], h[4][k], h[0][k], h[5][k]) + 512) >> 10, maxv);
-  }
   using PK = Pack4<T>;
-  typename PK::V o[16];
-  o[0] = PK::make(s00[0][0], s00[0][1], s00[0][2], s00[0][3]);
-  o[2] = PK::make(s02[0][0], s02[0][1], s02[0][2], s02[0][3]);
-  o[8] = PK::make(s20[0], s20[1], s20[2], s20[3]);
-  o[10] = PK::make(s22[0], s22[1], s22[2], s22[3]);
-  int q[12][4];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    q[0][k] = avg2(s00[0][k], s02[0][k]);       // [0][1] getSubImageBiLinear
-    q[1][k] = avg2(s00[0][k], s20[k]);          // [1][0]
-    q[2][k] = avg2(s02[0][k], s20[k]);          // [1][1]
-    q[3][k] = avg2(s02[0][k], s22[k]);          // [1][2]
-    q[4][k] = avg2(s20[k], s22[k]);             // [2][1]
-    q[5][k] = avg2(s02[0][k], s00[0][k + 1]);   // [0][3] getHorSubImageBiLinear
-    q[6][k] = avg2(s02[0][k], s20[k + 1]);      // [1][3]
-    q[7][k] = avg2(s22[k], s20[k + 1]);         // [2][3]
-    q[8][k] = avg2(s20[k], s00[1][k]);          // [3][0] getVerSubImageBiLinear
-    q[9][k] = avg2(s20[k], s02[1][k]);          // [3][1]
-    q[10][k] = avg2(s22[k], s02[1][k]);         // [3][2]
-    q[11][k] = avg2(s02[1][k], s20[k + 1]);     // [3][3] getDiagSubImageBiLinear
+  for (int m = 0; m < 2; ++m) {   // output row row0 + m: input rows m .. m + 5
+    if (row0 + m >= ph) break;
+    int s00[2][5], s02[2][4], s20[5], s22[4];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      s00[0][k] = I[m + 2][k + 2];
+      s00[1][k] = I[m + 3][k + 2];
+      // getVerSubImageSixTap
+      s20[k] = clipv((six(I[m + 2][k + 2], I[m + 3][k + 2], I[m + 1][k + 2], I[m + 4][k + 2], I[m][k + 2],
+                          I[m + 5][k + 2]) + 16) >> 5, maxv);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      s02[0][k] = clipv((h[m + 2][k] + 16) >> 5, maxv);
+      s02[1][k] = clipv((h[m + 3][k] + 16) >> 5, maxv);
+      // getVerSubImageSixTapTmp
+      s22[k] = clipv((six(h[m + 2][k], h[m + 3][k], h[m + 1][k], h[m + 4][k], h[m][k], h[m + 5][k]) + 512) >> 10, maxv);
+    }
+    typename PK::V o[16];
+    o[0] = PK::make(s00[0][0], s00[0][1], s00[0][2], s00[0][3]);
+    o[2] = PK::make(s02[0][0], s02[0][1], s02[0][2], s02[0][3]);
+    o[8] = PK::make(s20[0], s20[1], s20[2], s20[3]);
+    o[10] = PK::make(s22[0], s22[1], s22[2], s22[3]);
+    int q[12][4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      q[0][k] = avg2(s00[0][k], s02[0][k]);       // [0][1] getSubImageBiLinear
+      q[1][k] = avg2(s00[0][k], s20[k]);          // [1][0]
+      q[2][k] = avg2(s02[0][k], s20[k]);          // [1][1]
+      q[3][k] = avg2(s02[0][k], s22[k]);          // [1][2]
+      q[4][k] = avg2(s20[k], s22[k]);             // [2][1]
+      q[5][k] = avg2(s02[0][k], s00[0][k + 1]);   // [0][3] getHorSubImageBiLinear
+      q[6][k] = avg2(s02[0][k], s20[k + 1]);      // [1][3]
+      q[7][k] = avg2(s22[k], s20[k + 1]);         // [2][3]
+      q[8][k] = avg2(s20[k], s00[1][k]);          // [3][0] getVerSubImageBiLinear
+      q[9][k] = avg2(s20[k], s02[1][k]);          // [3][1]
+      q[10][k] = avg2(s22[k], s02[1][k]);         // [3][2]
+      q[11][k] = avg2(s02[1][k], s20[k + 1]);     // [3][3] getDiagSubImageBiLinear
+    }
+    const int qi[12] = {1, 4, 5, 6, 9, 3, 7, 11, 12, 13, 14, 15};
+#pragma unroll
+    for (int j = 0; j < 12; ++j) o[qi[j]] = PK::make(q[j][0], q[j][1], q[j][2], q[j][3]);
+    T *d = dst + (size_t)(row0 + m) * dst_pitch + col;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) *reinterpret_cast<typename PK::V *>(d + (size_t)k * plane_stride) = o[k];
   }
-  const int qi[12] = {1, 4, 5, 6, 9, 3, 7, 11, 12, 13, 14, 15};
-#pragma unroll
-  for (int j = 0; j < 12; ++j) o[qi[j]] = PK::make(q[j][0], q[j][1], q[j][2], q[j][3]);
-  T *d = dst + (size_t)row * dst_pitch + col;
-#pragma unroll
-  for (int k = 0; k < 16; ++k) *reinterpret_cast<typename PK::V *>(d + (size_t)k * plane_stride) = o[k];
 }
 
 // ------------------------------------------------------------- refinement --
