@@ -61,3 +61,21 @@ def test_grid_fixtures_cover_the_search_paths():
     assert variants == {2, 3}
     assert (4, 5) in pats and frac > 0
     assert (paths[[1, 2, 3, 5, 6, 7]] > 0).all(), paths
+
+
+def test_16bit_restatement_equals_8bit_on_8bit_content():
+    """build/libepzs_oracle16.so (the restatement over JM's 16-bit imgpel, the checker of
+    the high-bit-depth EPZS kernel) answers like the 8-bit build on 8-bit samples; with
+    the planes scaled to 10 bits it still runs every search path"""
+    from test_epzs_gpu import _random_requests
+    rng = np.random.default_rng(11)
+    w, h = 96, 64
+    cur = rng.integers(0, 256, size=(h, w), dtype=np.uint8)
+    refs = [np.clip(np.roll(cur, (2, -3), (0, 1)).astype(np.int32) + rng.integers(-5, 6, size=(h, w)), 0, 255)
+            .astype(np.uint8), rng.integers(0, 256, size=(h, w), dtype=np.uint8)]
+    req, preds, stale = _random_requests(rng, w, h, 600)
+    a = ol.epzs_batch(req, preds, stale, cur, refs)
+    b = ol.epzs_batch(req, preds, stale, cur.astype(np.uint16), [r.astype(np.uint16) for r in refs])
+    assert np.array_equal(a, b)
+    c = ol.epzs_batch(req, preds, stale, cur.astype(np.uint16) << 2, [r.astype(np.uint16) << 2 for r in refs])
+    assert len(np.unique(c["path"])) >= 4
