@@ -57,22 +57,35 @@ def main():
     ap.add_argument("--subpel", action="store_true",
                     help="sub-pel refinement on (JM default), SATD quarter-pel = mode-decision metric")
     ap.add_argument("--per-call", action="store_true", help="also time JMME_SPECULATE=0 (one GPU call per search)")
+    ap.add_argument("--bits", type=int, default=8,
+                    help="SourceBitDepthLuma (9..14: 16-bit planes, High 10 / High 4:4:4 profile)")
     a = ap.parse_args()
     from jmme import synth
     w, h = (int(v) for v in a.size.split("x"))
     params = {"SearchMode": a.mode, "SearchRange": a.range, "RDOptimization": 0, "NumberReferenceFrames": 1}
     if a.subpel:
         params.update(DisableSubpelME=0, MEDistortionQPel=2, MDDistortion=2)
+    if a.bits > 8:
+        params.update(ProfileIDC=110 if a.bits <= 10 else 244, SourceBitDepthLuma=a.bits, SourceBitDepthChroma=a.bits,
+                      OutputBitDepthLuma=a.bits, OutputBitDepthChroma=a.bits)
     with tempfile.TemporaryDirectory() as d:
         yuv = os.path.join(d, "in.yuv")
-        synth.write_yuv420(yuv, synth.luma_sequence(w, h, a.frames, seed=2024, gmv=(5, 3)))
+        luma = synth.luma_sequence(w, h, a.frames, seed=2024, gmv=(5, 3))
+        if a.bits > 8:   # the 8-bit texture scaled, plus low-order noise (tests/test_jm_dropin_hbd_gpu.py)
+            import numpy as np
+            from test_jm_dropin_hbd_gpu import write_yuv420_16
+            sh = a.bits - 8
+            l16 = (luma.astype(np.int32) << sh) + np.random.default_rng(a.bits).integers(0, 1 << sh, size=luma.shape)
+            write_yuv420_16(yuv, np.clip(l16, 0, (1 << a.bits) - 1).astype(np.uint16), a.bits)
+        else:
+            synth.write_yuv420(yuv, luma)
         cpu = run(STOCK, d, "cpu", yuv, w, h, a.frames, params)
         gpu = run(GPU, d, "gpu", yuv, w, h, a.frames, params)
         percall = run(GPU, d, "gpu1", yuv, w, h, a.frames, params, {"JMME_SPECULATE": "0"}) if a.per_call else None
     mbs = (w // 16) * ((h + 15) // 16) * (a.frames - 1)
     print(json.dumps({
         "metric": "end-to-end JM 18.5 encode with the drop-in integer-pel ME (lencod_jmme vs stock lencod)",
-        "size": a.size, "frames": a.frames, "params": params, "p_frame_macroblocks": mbs,
+        "size": a.size, "frames": a.frames, "bits": a.bits, "params": params, "p_frame_macroblocks": mbs,
         "stock_cpu": {k: v for k, v in cpu.items() if k != "md5"},
         "dropin_gpu": {k: v for k, v in gpu.items() if k != "md5"},
         "dropin_gpu_per_call": {k: v for k, v in percall.items() if k != "md5"} if percall else None,
