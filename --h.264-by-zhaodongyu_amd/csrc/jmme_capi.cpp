@@ -857,7 +857,6 @@ int launch_chains(jmme_ctx *ctx, int mode, const jmme_chain *chains, int n, hipS
   if (n <= 0) return 0;
   if (n > kChainInline) return fail("%d chains in one call (at most %d)", n, kChainInline);
   if (mode != JMME_FULL_SEARCH && mode != JMME_FAST_FULL_SEARCH) return fail("chains: mode %d", mode);
-  if (ctx->hbd) return fail("chains: 8-bit planes only");
   ChainParams p{};
   int max_r = 0;
   for (int i = 0; i < n; ++i) {
@@ -870,6 +869,9 @@ int launch_chains(jmme_ctx *ctx, int mode, const jmme_chain *chains, int n, hipS
         !ctx->d_refs[c.list * kMaxRefs + c.ref_idx])
       return fail("chain %d: reference (%d,%d) not uploaded", i, c.list, c.ref_idx);
     if (c.lambda < 0) return fail("chain %d: negative lambda", i);
+    // 32-bit costs: (SAD << 5) + lambda * mvbits must not wrap (16-bit planes: SAD up to 256 * max_pel)
+    if ((uint64_t)c.lambda * 64u + ((uint64_t)256 * ctx->max_pel << 5) >= (1ull << 32))
+      return fail("chain %d: lambda %d too large for 32-bit costs", i, c.lambda);
     if (mode == JMME_FAST_FULL_SEARCH && (c.ffs_range < 0 || c.ffs_range > kChainMaxR || (c.ffs_center_x & 3) ||
                                           (c.ffs_center_y & 3)))
       return fail("chain %d: FFS surface range %d / centre", i, c.ffs_range);
@@ -904,6 +906,7 @@ int launch_chains(jmme_ctx *ctx, int mode, const jmme_chain *chains, int n, hipS
   p.max_mvd = ctx->max_mvd;
   p.n = n;
   p.max_r = max_r;
+  p.hbd = ctx->hbd ? 1 : 0;
   p.res = static_cast<jmme_chain_res *>(d_res);
   std::memcpy(p.chains, chains, (size_t)n * sizeof(jmme_chain));
   HIPCHK(launch_search_chains(p, s));
@@ -1946,7 +1949,7 @@ extern "C" int jmme_prepare(jmme_ctx *ctx) {
   for (int mode : {JMME_FULL_SEARCH, JMME_FAST_FULL_SEARCH})
     if (rc >= 0) rc = search_small(ctx, mode, &r, 1, res, nullptr, true);
   // the chain kernels, their stream and result block (jmme_search_mbs_chains)
-  if (rc >= 0 && !ctx->hbd) {
+  if (rc >= 0) {   // (16-bit contexts: the v_sad_u16 instantiation on the 16-bit dummy plane)
     jmme_chain c;
     std::memset(&c, 0, sizeof c);
     c.mb_x = c.mb_y = 16;

@@ -113,10 +113,11 @@ struct ChainParams {
   const uint8_t *const *refs;       // device reference table
   int pitch, width, height;
   int mode, max_mvd, n, max_r;      // max_r: largest window range of the launch (LDS sizing)
+  int hbd;                          // 16-bit planes (SourceBitDepthLuma 9..14): v_sad_u16 instantiation
   jmme_chain_res *res;              // [n][JMME_CHAIN_MAX_STEPS] (host-mapped)
   jmme_chain chains[kChainInline];
 };
-size_t chain_lds_bytes(int max_r);
+size_t chain_lds_bytes(int max_r, bool hbd = false);
 hipError_t launch_search_chains(const ChainParams &p, hipStream_t s);
 
 size_t items_lds_bytes(int lds_range);

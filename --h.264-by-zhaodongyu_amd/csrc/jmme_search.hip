@@ -1730,6 +1730,10 @@ constexpr int kChainMargin = 0;
 __host__ __device__ inline int chain_wpr(int R) { return 2 * R + 13 + 2 * kChainMargin; }   // words per staged row
 __host__ __device__ inline int chain_rows(int R) { return 2 * R + 16 + 2 * kChainMargin; }
 __host__ __device__ inline int chain_raw(int R) { return (chain_wpr(R) + 9) / 4 + 1; }   // raw dwords per row
+// 16-bit planes (SourceBitDepthLuma 9..14): words[x] = pels x, x+1, two more
+// words a row (a 4-pel chunk is words x and x+2), two samples per raw dword
+__host__ __device__ inline int chain_wpr16(int R) { return chain_wpr(R) + 2; }
+__host__ __device__ inline int chain_raw16(int R) { return (chain_wpr16(R) + 5) / 2 + 1; }
 
 __device__ __forceinline__ int imedian3(int a, int b, int c) {
   return a > b ? (b > c ? b : (a > c ? c : a)) : (a > c ? a : (b > c ? c : b));
@@ -1836,7 +1840,7 @@ __device__ __forceinline__ ChainStepIn chain_derive(const jmme_chain &c, const j
 // part of the vector cost is formed once; the spiral rank -- which only breaks
 // ties -- is formed when a position ties the thread's best, and for the winner
 // at the end.
-template <bool FFS, int W, int H>
+template <bool FFS, int W, int H, bool HBD>
 __device__ __forceinline__ void chain_sweep(const GroupCtx &g, const uint32_t *words, int wpr, const uint32_t *s_cur,
                                             int bx, int by, int tid, uint32_t &bc, uint32_t &br) {
   const int R = g.R, D = 2 * R + 1;
@@ -1859,8 +1863,15 @@ __device__ __forceinline__ void chain_sweep(const GroupCtx &g, const uint32_t *w
 #pragma unroll
     for (int r = 0; r < 4 * H; ++r)
 #pragma unroll
-      for (int wc = 0; wc < W; ++wc)
-        sad = __builtin_amdgcn_sad_u8(wb[r * wpr + 4 * wc], s_cur[(4 * by + r) * 4 + bx + wc], sad);
+      for (int wc = 0; wc < W; ++wc) {
+        if constexpr (HBD) {   // a 4-pel chunk: words x and x+2 against two current dwords (v_sad_u16)
+          const uint32_t *cr = s_cur + (4 * by + r) * 8 + 2 * (bx + wc);
+          sad = __builtin_amdgcn_sad_u16(wb[r * wpr + 4 * wc], cr[0], sad);
+          sad = __builtin_amdgcn_sad_u16(wb[r * wpr + 4 * wc + 2], cr[1], sad);
+        } else {
+          sad = __builtin_amdgcn_sad_u8(wb[r * wpr + 4 * wc], s_cur[(4 * by + r) * 4 + bx + wc], sad);
+        }
+      }
     const uint32_t cost = (sad << 5) + mvc;
     if (cost > bc) continue;
     const int sidx = spiral_index_bl(ox, oy);
@@ -1869,10 +1880,10 @@ __device__ __forceinline__ void chain_sweep(const GroupCtx &g, const uint32_t *w
   }
 }
 
-template <bool FFS>
+template <bool FFS, bool HBD>
 __global__ __launch_bounds__(kChainWG) void chain_kernel(ChainParams p) {
   extern __shared__ uint32_t dyn[];
-  __shared__ uint32_t s_cur[64];
+  __shared__ uint32_t s_cur[HBD ? 128 : 64];
   __shared__ uint32_t s_minc[2][kChainWaves], s_minr[2][kChainWaves];   // by step parity: one barrier per step
   __shared__ jmme_chain s_chain;                                         // out of the kernel arguments once
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1892,9 +1903,14 @@ __global__ __launch_bounds__(kChainWG) void chain_kernel(ChainParams p) {
   const jmme_chain &c = s_chain;
   const int n_steps = c.n_steps;
   const uint8_t *ref = p.refs[c.list * kMaxRefs + c.ref_idx];
-  if (tid < 64)
+  if constexpr (HBD) {
+    if (tid < 128)
+      s_cur[tid] = *reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint16_t *>(p.cur) +
+                                                       (size_t)(c.mb_y + (tid >> 3)) * p.pitch + c.mb_x + 2 * (tid & 7));
+  } else if (tid < 64) {
     s_cur[tid] = *reinterpret_cast<const uint32_t *>(p.cur + (size_t)(c.mb_y + (tid >> 2)) * p.pitch + c.mb_x +
                                                      4 * (tid & 3));
+  }
   // every thread holds the steps' vectors (as the next steps read them) and,
   // for thread 0's final write, their results
   int mvx[4] = {0, 0, 0, 0}, mvy[4] = {0, 0, 0, 0};
@@ -1925,8 +1941,28 @@ __global__ __launch_bounds__(kChainWG) void chain_kernel(ChainParams p) {
     // whose window (origin: macroblock origin + centre - R) lies inside the
     // staged one searches it in place (FFS: one staging per chain)
     const int X0 = c.mb_x + (cqx >> 2) - R, Y0 = c.mb_y + (cqy >> 2) - R;
-    if (!(X0 >= st_x && Y0 >= st_y && X0 + 2 * R + 13 <= st_x + st_w && Y0 + 2 * R + 16 <= st_y + st_h)) {
-      st_x = X0 - kChainMargin; st_y = Y0 - kChainMargin; st_w = chain_wpr(R); st_h = chain_rows(R);
+    if (!(X0 >= st_x && Y0 >= st_y && X0 + 2 * R + (HBD ? 15 : 13) <= st_x + st_w && Y0 + 2 * R + 16 <= st_y + st_h)) {
+      st_x = X0 - kChainMargin; st_y = Y0 - kChainMargin; st_w = HBD ? chain_wpr16(R) : chain_wpr(R);
+      st_h = chain_rows(R);
+      if constexpr (HBD) {   // raw[r][q] = samples xa + 2q, +1 (clamped); words[x] = samples x, x + 1
+        const int wpr = st_w, nraw = chain_raw16(R), rows = st_h;
+        uint32_t *words = dyn, *raw = dyn + (size_t)rows * wpr;
+        const int xa = st_x & ~1, sh = st_x - xa, Y0s = st_y;
+        for (int i = tid; i < rows * nraw; i += kChainWG) {
+          const int r = i / nraw, q = i - r * nraw;
+          const uint16_t *row = reinterpret_cast<const uint16_t *>(ref) + (size_t)clampi(Y0s + r, 0, p.height - 1) * p.pitch;
+          const int x = xa + 2 * q;
+          raw[i] = (x >= 0 && x + 1 < p.width)
+                       ? *reinterpret_cast<const uint32_t *>(row + x)
+                       : (uint32_t)row[clampi(x, 0, p.width - 1)] | ((uint32_t)row[clampi(x + 1, 0, p.width - 1)] << 16);
+        }
+        __syncthreads();
+        for (int i = tid; i < rows * wpr; i += kChainWG) {
+          const int r = i / wpr, x = i - r * wpr, q = (sh + x) >> 1;
+          words[i] = __builtin_amdgcn_alignbyte(raw[r * nraw + q + 1], raw[r * nraw + q], 2 * ((sh + x) & 1));
+        }
+        __syncthreads();
+      } else {
       const int wpr = st_w, nraw = chain_raw(R), rows = st_h;
       uint32_t *words = dyn, *raw = dyn + (size_t)rows * wpr;
       const int xa = st_x & ~3, sh = st_x - xa, Y0s = st_y;
@@ -1950,6 +1986,7 @@ __global__ __launch_bounds__(kChainWG) void chain_kernel(ChainParams p) {
         words[i] = __builtin_amdgcn_alignbyte(raw[r * nraw + q + 1], raw[r * nraw + q], (sh + x) & 3);
       }
       __syncthreads();
+      }
     }
     const int wpr = st_w;
     const uint32_t *words = dyn + (size_t)(Y0 - st_y) * wpr + (X0 - st_x);   // this step's window in the staging
@@ -1961,13 +1998,13 @@ __global__ __launch_bounds__(kChainWG) void chain_kernel(ChainParams p) {
     const SlotGeom sg = slot_geom(st.slot);
     uint32_t bc = ~0u, br = ~0u;   // this thread's best (cost, rank)
     switch (sg.bt) {
-      case 1: chain_sweep<FFS, 4, 4>(g, words, wpr, s_cur, sg.bx, sg.by, tid, bc, br); break;
-      case 2: chain_sweep<FFS, 4, 2>(g, words, wpr, s_cur, sg.bx, sg.by, tid, bc, br); break;
-      case 3: chain_sweep<FFS, 2, 4>(g, words, wpr, s_cur, sg.bx, sg.by, tid, bc, br); break;
-      case 4: chain_sweep<FFS, 2, 2>(g, words, wpr, s_cur, sg.bx, sg.by, tid, bc, br); break;
-      case 5: chain_sweep<FFS, 2, 1>(g, words, wpr, s_cur, sg.bx, sg.by, tid, bc, br); break;
-      case 6: chain_sweep<FFS, 1, 2>(g, words, wpr, s_cur, sg.bx, sg.by, tid, bc, br); break;
-      default: chain_sweep<FFS, 1, 1>(g, words, wpr, s_cur, sg.bx, sg.by, tid, bc, br); break;
+      case 1: chain_sweep<FFS, 4, 4, HBD>(g, words, wpr, s_cur, sg.bx, sg.by, tid, bc, br); break;
+      case 2: chain_sweep<FFS, 4, 2, HBD>(g, words, wpr, s_cur, sg.bx, sg.by, tid, bc, br); break;
+      case 3: chain_sweep<FFS, 2, 4, HBD>(g, words, wpr, s_cur, sg.bx, sg.by, tid, bc, br); break;
+      case 4: chain_sweep<FFS, 2, 2, HBD>(g, words, wpr, s_cur, sg.bx, sg.by, tid, bc, br); break;
+      case 5: chain_sweep<FFS, 2, 1, HBD>(g, words, wpr, s_cur, sg.bx, sg.by, tid, bc, br); break;
+      case 6: chain_sweep<FFS, 1, 2, HBD>(g, words, wpr, s_cur, sg.bx, sg.by, tid, bc, br); break;
+      default: chain_sweep<FFS, 1, 1, HBD>(g, words, wpr, s_cur, sg.bx, sg.by, tid, bc, br); break;
     }
     // wave minimum of the cost (DPP), then the smallest rank among its holders;
     // after the one barrier every thread combines the 16 waves itself
@@ -2078,15 +2115,27 @@ hipError_t launch_search(const KParams &p, hipStream_t s, hipEvent_t ev0, hipEve
   return hipGetLastError();
 }
 
-size_t chain_lds_bytes(int max_r) {
-  return (size_t)chain_rows(max_r) * (chain_wpr(max_r) + chain_raw(max_r)) * 4;
+size_t chain_lds_bytes(int max_r, bool hbd) {
+  return hbd ? (size_t)chain_rows(max_r) * (chain_wpr16(max_r) + chain_raw16(max_r)) * 4
+             : (size_t)chain_rows(max_r) * (chain_wpr(max_r) + chain_raw(max_r)) * 4;
 }
 
 hipError_t launch_search_chains(const ChainParams &p, hipStream_t s) {
   if (p.n <= 0) return hipSuccess;
-  const size_t lds = chain_lds_bytes(p.max_r);
-  if (p.mode == JMME_FAST_FULL_SEARCH) hipLaunchKernelGGL(chain_kernel<true>, dim3(p.n), dim3(kChainWG), lds, s, p);
-  else hipLaunchKernelGGL(chain_kernel<false>, dim3(p.n), dim3(kChainWG), lds, s, p);
+  const size_t lds = chain_lds_bytes(p.max_r, p.hbd);
+  const bool ffs = p.mode == JMME_FAST_FULL_SEARCH;
+  auto k = p.hbd ? (ffs ? chain_kernel<true, true> : chain_kernel<false, true>)
+                 : (ffs ? chain_kernel<true, false> : chain_kernel<false, false>);
+  if (lds > 65536) {   // 16-bit staging at R = 44: 65,728 B of the CU's 160 KiB (once per kernel and thread)
+    static thread_local bool raised[2] = {false, false};
+    if (!raised[ffs]) {
+      const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (e != hipSuccess) return e;
+      raised[ffs] = true;
+    }
+  }
+  hipLaunchKernelGGL(k, dim3(p.n), dim3(kChainWG), lds, s, p);
   return hipGetLastError();
 }
 

@@ -46,7 +46,6 @@ extern void __real_init_motion_search_module(VideoParameters *, InputParameters 
 extern void get_neighbors(Macroblock *currMB, PixelPos *block, int mb_x, int mb_y, int blockshape_x);
 
 static jmme_ctx *g_me = NULL;
-static int g_hbd = 0;   /* luma above 8 bits: 16-bit planes (no chained guesses) */
 static int g_bits = 8;  /* SourceBitDepthLuma */
 static long long g_calls = 0, g_cpu_calls = 0;
 static FILE *g_trace = NULL, *g_trace_miss = NULL;   /* JMME_TRACE / JMME_TRACE_MISS */
@@ -109,7 +108,6 @@ static void init_once(VideoParameters *p_Vid, InputParameters *p_Inp)
   /* the luma depth of JM's imgpel planes (init_img, lencod.c:1115): above 8 the
    * context keeps 16-bit planes and searches with v_sad_u16 */
   c.SourceBitDepthLuma = p_Vid->bitdepth_luma > 0 ? p_Vid->bitdepth_luma : p_Inp->source.bit_depth[0];
-  g_hbd = c.SourceBitDepthLuma > 8;
   g_bits = c.SourceBitDepthLuma;
   g_me = jmme_create(&c, -1);
   if (!g_me) fail_jm("jmme_create");
@@ -390,7 +388,7 @@ static int chains_on(Macroblock *currMB, int list, int ref)
     chain_groups();
     if (!g_slot_bt[0]) slot_geometry();
   }
-  return g_chain_on && !g_hbd && currSlice->slice_type == P_SLICE && currSlice->structure == FRAME &&
+  return g_chain_on && currSlice->slice_type == P_SLICE && currSlice->structure == FRAME &&
          currMB->list_offset == 0 && list == 0 && ref == 0 && currSlice->listXsize[0] == 1 &&
          p_Inp->DisableSubpelME[p_Vid->view_id] && !p_Inp->Transform8x8Mode;
 }

@@ -156,16 +156,23 @@ def _step_req(chain, k, pred, centre, rng_min, rng_max, ffs):
     return q, s
 
 
-@pytest.mark.parametrize("ffs,rdopt,R", [(False, 0, 16), (False, 1, 32), (True, 0, 16), (True, 1, 32)])
-def test_chains_match_step_by_step_searches(gpu, ffs, rdopt, R):
+@pytest.mark.parametrize("ffs,rdopt,R,bits", [(False, 0, 16, 8), (False, 1, 32, 8), (True, 0, 16, 8), (True, 1, 32, 8),
+                                              # 16-bit planes: the v_sad_u16 chain kernel against the
+                                              # small kernel's 16-bit searches
+                                              (False, 0, 16, 10), (True, 1, 32, 12), (False, 1, 32, 14)])
+def test_chains_match_step_by_step_searches(gpu, ffs, rdopt, R, bits):
     from jmme import FAST_FULL_SEARCH, FULL_SEARCH, MB_REQ, MotionEstimator, synth
     w, h = 352, 288
-    rng = np.random.default_rng(10 * R + rdopt + 100 * ffs)
+    rng = np.random.default_rng(10 * R + rdopt + 100 * ffs + bits)
     luma = synth.luma_sequence(w, h, 2, seed=R + rdopt, gmv=(3, -2), adversarial=True, adv_range=R)
+    if bits > 8:   # the texture scaled, plus low-order noise only a 16-bit search sees
+        sh = bits - 8
+        luma = ((luma.astype(np.int32) << sh) + rng.integers(0, 1 << sh, size=luma.shape)).astype(np.uint16)
     chains = _random_chains(rng, w, h, 8, R, rdopt, ffs)
     mode = FAST_FULL_SEARCH if ffs else FULL_SEARCH
     n_steps = 0
-    with MotionEstimator({"SearchRange": R, "SearchMode": 0 if ffs else -1, "RDOptimization": rdopt}) as me:
+    cfg = {"SearchRange": R, "SearchMode": 0 if ffs else -1, "RDOptimization": rdopt, "SourceBitDepthLuma": bits}
+    with MotionEstimator(cfg) as me:
         me.upload_cur(luma[1])
         me.upload_ref(0, 0, luma[0])
         _, res = me.search_chains(mode, np.zeros(0, MB_REQ), chains)
