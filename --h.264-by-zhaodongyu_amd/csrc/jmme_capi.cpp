@@ -528,7 +528,13 @@ int launch(jmme_ctx *ctx, int mode, const uint8_t *d_cur, const uint8_t *const *
   HIPCHK(hipMemsetAsync(ctx->d_stamps, 0, words * sizeof(unsigned long long), s));
 #endif
   // jmme_last_kernel_ms: the main item kernel alone (ev0 .. ev1)
-  HIPCHK(launch_search(p, s, ctx->ev0, ctx->ev1));
+  if (launch_search(p, s, ctx->ev0, ctx->ev1) != hipSuccess) {
+    // the plan kernel may have launched and counted into this set (and zeroed
+    // only the other one): leave both clean for the next launch
+    (void)hipMemsetAsync(ctx->d_counts, 0, 2 * kCountWords * sizeof(*ctx->d_counts), s);
+    ctx->counts_half = 0;
+    return fail("launch_search: the item-kernel launch failed");
+  }
   ctx->last_counts = p.counts;
   ctx->counts_half ^= 1;
   ctx->timed = true;
@@ -672,10 +678,14 @@ int search_small(jmme_ctx *ctx, int mode, const jmme_mb_req *req, int n, jmme_bl
   const int tiles = (2 * max_r + 1 + kSmallTile - 1) / kSmallTile;
   const long long wgs = (long long)items.size() * tiles * tiles;
   if (items.empty() || (wgs > ctx->small_max_wg && !force)) return items.empty() ? 1 : 0;
-  if (ctx->hbd)   // 32-bit costs: (SAD << 5) + lambda * mvbits must not wrap
-    for (const SmallItem &it : items)
-      if ((uint64_t)it.lam * 64u + ((uint64_t)256 * ctx->max_pel << 5) >= (1ull << 32))
-        return fail("lambda %d too large for the high-bit-depth search", it.lam);
+  // 32-bit costs: (SAD << 5) + lambda * mvbits must not wrap.  An 8-bit batch
+  // with such a lambda goes to the item kernel, whose 64-bit keys serve it
+  // exactly; high bit depth has no other path, so it fails loudly.
+  for (const SmallItem &it : items)
+    if ((uint64_t)it.lam * 64u + ((uint64_t)256 * ctx->max_pel << 5) >= (1ull << 32)) {
+      if (ctx->hbd) return fail("lambda %d too large for the high-bit-depth search", it.lam);
+      return 0;
+    }
   if (items.size() > ctx->cap_sitems) {
     if (ctx->h_sitems) (void)hipHostFree(ctx->h_sitems);
     ctx->h_sitems = nullptr;

@@ -18,8 +18,10 @@ the GPU box's share per GPU) and as one process alone; JM's own "Total ME
 time" gives MB/s.  Falls back to the C restatement (oracle/) on a sample when
 the JM build is absent.
 
-Multi-GPU (torchrun): frames/GOPs shard across ranks (weak scaling), no
-collective on the data path; barrier + max-over-ranks timing.
+Multi-GPU (torchrun): GOPs shard across ranks (weak scaling): rank r searches
+the P-frame of its own seeded GOP (rank 0 the captured one), no collective on
+the data path; barrier + max-over-ranks timing; every rank's parity is gathered
+and reported (rank 0 against JM, the others against the oracle on a sample).
 """
 from __future__ import annotations
 
@@ -312,6 +314,48 @@ def reduce_over_ranks(wall: float, exact: int, ws: int, dev) -> tuple[float, int
     return float(t.item()), int(e.item())
 
 
+def gather_rank_parity(info: list[int], ws: int, dev) -> list[list[int]]:
+    """Every rank's own parity record ([frame seed, searches checked, bit-exact,
+    reference: 0 JM / 1 oracle]) on every rank, in rank order: with GOP
+    sharding each rank searches different frames, so each is checked on its own."""
+    if ws == 1:
+        return [list(info)]
+    import torch.distributed as dist
+    t = torch.tensor(info, dtype=torch.int64, device=dev)
+    out = [torch.zeros_like(t) for _ in range(ws)]
+    dist.all_gather(out, t)
+    return [[int(v) for v in x.tolist()] for x in out]
+
+
+def rank_frames(rank: int, cur, ref, meta):
+    """GOP sharding: the frames rank `rank` searches.  Rank 0 takes the captured
+    P-frame (JM 18.5's own results for it are checked on every search); rank r > 0
+    the P-frame of its own seeded GOP (clip seed + 1000 r, the same global
+    motion), searched with the same requests and checked against the oracle on a
+    sample.  Returns (cur, ref, clip seed)."""
+    if rank == 0:
+        return cur, ref, int(meta["seed"])
+    from jmme import synth
+    H, W = cur.shape
+    seed = int(meta["seed"]) + 1000 * rank
+    luma = synth.luma_sequence(W, H, 2, seed=seed, gmv=tuple(meta["gmv"]))
+    return luma[1], luma[0], seed
+
+
+def oracle_parity(cur, ref, req, out, sample: int = 96, seed: int = 5) -> tuple[int, int]:
+    """(searches checked, bit-exact) of a seeded sample of units against the C
+    restatement (oracle/me_oracle.c, itself pinned to JM 18.5's captures)."""
+    import oracle_lib as ol
+    from jmme import NSLOT
+    sel = np.sort(np.random.default_rng(seed).choice(len(req), min(sample, len(req)), replace=False))
+    mv, cost = ol.full_search_batch(cur, ref, _oracle_rows(req[sel]))
+    got = [(out[u, s]["mv_x"], out[u, s]["mv_y"], out[u, s]["cost"]) for u in sel for s in range(NSLOT)
+           if (int(req[u]["slot_mask"]) >> s) & 1]
+    got = np.array(got, np.int64).reshape(-1, 3)
+    exp = np.column_stack([mv[:, 0], mv[:, 1], cost]).astype(np.int64)
+    return len(exp), int(np.sum(np.all(got == exp, axis=1)))
+
+
 def job_value(units_per_rank_step: int, steps: int, ws: int, wall: float) -> float:
     """Whole-job throughput: every rank's units over the max-over-ranks time."""
     return units_per_rank_step * steps * ws / wall
@@ -513,6 +557,7 @@ def main():
     from jmme import BLOCK_RES, FULL_SEARCH, MotionEstimator, NSLOT
     cur, ref, req, unit_of, slots, expect, meta = load_workload()
     n = len(req)
+    cur, ref, clip_seed = rank_frames(rank, cur, ref, meta)
     me = MotionEstimator({"SearchRange": 32, "SearchMode": -1, "RDOptimization": 0}, device=local)
     me.upload_cur(cur)
     me.upload_ref(0, 0, ref)
@@ -527,9 +572,16 @@ def main():
         step()
     torch.cuda.synchronize(dev)
 
-    # parity of this rank's output against JM 18.5's own results
-    out = d_out.cpu().numpy().view(BLOCK_RES).reshape(n, NSLOT)[unit_of, slots]
-    exact = int(np.sum((out["mv_x"] == expect[0]) & (out["mv_y"] == expect[1]) & (out["cost"] == expect[2])))
+    # parity of this rank's output: JM 18.5's own results (rank 0, the captured
+    # frame) or the oracle on a sample (its own GOP's frame)
+    full = d_out.cpu().numpy().view(BLOCK_RES).reshape(n, NSLOT)
+    if rank == 0:
+        out = full[unit_of, slots]
+        checked = len(expect[0])
+        exact = int(np.sum((out["mv_x"] == expect[0]) & (out["mv_y"] == expect[1]) & (out["cost"] == expect[2])))
+    else:
+        checked, exact = oracle_parity(cur, ref, req, full)
+    per_rank = gather_rank_parity([clip_seed, checked, exact, int(rank != 0)], ws, dev)
 
     # kernel duration: HIP events around the unit kernel, on its stream
     kms = []
@@ -552,7 +604,7 @@ def main():
         torch.distributed.barrier()
     wall = time.perf_counter() - t0
     ev_ms = ev0.elapsed_time(ev1)
-    wall, exact = reduce_over_ranks(wall, exact, ws, dev)
+    wall, _ = reduce_over_ranks(wall, exact, ws, dev)
 
     if rank == 0:
         value = job_value(n, args.steps, ws, wall)
@@ -585,7 +637,8 @@ def main():
             "config": {"workload": "1080p FS +-32 SAD integer-pel, 1 ref, 8160 MB x ref per step (configs[1])",
                        "search_range": 32, "mb_per_step": n,
                        "partition_searches_per_step": int(sum(bin(int(m)).count("1") for m in req["slot_mask"])),
-                       "parallelism": f"frame-shard x{ws}"},
+                       "parallelism": f"frame-shard x{ws}" + ("" if ws == 1 else
+                                                                  ": rank r searches the P-frame of its own GOP")},
             "parity": {"reference": "JM 18.5 lencod (captured)", "searches": int(len(expect[0])),
                        "bit_exact": exact},
             "roofline": {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -597,6 +650,10 @@ def main():
                      "peak_source": "measured v_sad_u8 rate (tools/ubench_valu.hip) x 4 abs-diffs",
                      "frac": round(ABSDIFF_PER_UNIT * n / (kernel_ms * 1e-3) / VSAD_PEAK, 4)},
             "event_ms_per_step": round(ev_ms / args.steps, 4),
+            "per_rank": [{"rank": r, "clip_seed": sd, "searches_checked": ck, "bit_exact": ex,
+                          "reference": "JM 18.5 lencod (captured)" if kind == 0 else
+                          "oracle/me_oracle.c (pinned to JM), seeded sample of 96 units"}
+                         for r, (sd, ck, ex, kind) in enumerate(per_rank)],
             "cpu_baseline": cpu,
         }
         if not args.no_subpel and ws == 1:
@@ -613,13 +670,10 @@ def main():
             line["hybrid"] = bench_blocks.hybrid_block(dev, local, load_workload)
         if not args.no_dropin and ws == 1:
             import bench_blocks
+            # FS / FFS (configs[1] settings), FS / FFS with encoder_baseline.cfg's
+            # sub-pel keys, EPZS (configs[3]'s algorithm, the same file's EPZS keys);
+            # each against one core and against host_cores() concurrent encoders
             line["dropin"] = bench_blocks.dropin_block()
-            # EPZS (encoder_baseline.cfg's ME keys): one call per search, latency bound -- one P-frame
-            ep = bench_blocks.dropin_block(modes=((3, "EPZS"),), frames=2)
-            if line["dropin"] is not None and ep is not None:
-                line["dropin"]["EPZS"] = dict(ep["EPZS"], p_frames=1, note="one GPU call per EPZS search and per "
-                                              "EPZS sub-pel refinement (JM's predictor lists need the previous "
-                                              "search's answer); parity path, not a throughput path")
         print(json.dumps(line))
     me.close()
     if ws > 1:

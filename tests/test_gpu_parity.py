@@ -274,9 +274,12 @@ def test_ffs_random_requests_vs_oracle(R, rdopt, far, gpu):
     assert len(bad) == 0, [(divmod(int(i), 41), got[i].tolist(), exp[i].tolist()) for i in bad[:5]]
 
 
-def test_saturated_32bit_keys_take_the_64bit_path(gpu):
+@pytest.mark.parametrize("path", ["items", "small"])
+def test_saturated_32bit_keys_take_the_64bit_path(path, gpu):
     """Huge lambdas push every candidate of the small partitions past the
-    32-bit key's cost field; the deferred 64-bit pass must keep results exact."""
+    32-bit key's cost field; the deferred 64-bit pass must keep results exact.
+    `items` forces the throughput kernel (small-batch limit 0), whose 64-bit
+    keys and exact re-search this guards; `small` is the latency path."""
     from jmme import FULL_SEARCH, MotionEstimator, synth
     w, h, R = 352, 288, 16
     rng = np.random.default_rng(9)
@@ -284,6 +287,7 @@ def test_saturated_32bit_keys_take_the_64bit_path(gpu):
     req = _random_units(rng, w, h, 6, R)
     req["blk"]["lambda"] = 400000
     with MotionEstimator({"SearchRange": R, "SearchMode": -1}) as me:
+        me.set_small_batch_limit(0 if path == "items" else 1 << 20)
         me.upload_cur(luma[1])
         me.upload_ref(0, 0, luma[0])
         out = me.search(FULL_SEARCH, req)
@@ -292,8 +296,9 @@ def test_saturated_32bit_keys_take_the_64bit_path(gpu):
         assert (out[u, s]["mv_x"], out[u, s]["mv_y"], out[u, s]["cost"]) == (mv[i, 0], mv[i, 1], cost[i])
 
 
+@pytest.mark.parametrize("path", ["items", "small"])
 @pytest.mark.parametrize("scene", ["flat", "inverted"])
-def test_saturated_16x16_keys_are_searched_exactly(scene, gpu):
+def test_saturated_16x16_keys_are_searched_exactly(scene, path, gpu):
     """Lambdas just inside the 32-bit key range on pictures whose 16x16 SADs
     reach (flat: equal) 65280: every 16x16 key of the sweep saturates, so the
     16x16 result comes from the exact 64-bit re-search; the other partitions
@@ -311,6 +316,7 @@ def test_saturated_16x16_keys_are_searched_exactly(scene, gpu):
     req = _random_units(rng, w, h, 8, R)
     req["blk"]["lambda"] = rng.integers(13000, 14226, size=req["blk"]["lambda"].shape)
     with MotionEstimator({"SearchRange": R, "SearchMode": -1}) as me:
+        me.set_small_batch_limit(0 if path == "items" else 1 << 20)
         me.upload_cur(cur)
         me.upload_ref(0, 0, ref)
         out = me.search(FULL_SEARCH, req)
@@ -402,19 +408,44 @@ def _grouped_units(rng, w, h, n, R, lam):
     return req
 
 
+@pytest.mark.parametrize("path", ["items", "small"])
 @pytest.mark.parametrize("R", [1, 7, 23, 44])
-def test_64bit_path_with_sparse_group_masks(R, gpu):
+def test_64bit_path_with_sparse_group_masks(R, path, gpu):
     """Lambdas beyond the 32-bit keys send every partition through the exact
     64-bit search, one partition after another; groups with non-contiguous slot
     masks make consecutive calls land on slots of equal parity, and the odd
     halves of the exchange buffer sit at the end of the workgroup's LDS.  Every
-    SearchRange changes where that end falls.  HIP == oracle on every partition."""
+    SearchRange changes where that end falls.  HIP == oracle on every partition,
+    on the item kernel (`items`: small-batch limit 0) and the latency path."""
     from jmme import FULL_SEARCH, MotionEstimator, synth
     w, h = 352, 288
     rng = np.random.default_rng(40 + R)
     luma = synth.luma_sequence(w, h, 2, seed=R, gmv=(2, 1))
     req = _grouped_units(rng, w, h, 8, R, 400000)
     with MotionEstimator({"SearchRange": R, "SearchMode": -1}) as me:
+        me.set_small_batch_limit(0 if path == "items" else 1 << 20)
+        me.upload_cur(luma[1])
+        me.upload_ref(0, 0, luma[0])
+        out = me.search(FULL_SEARCH, req)
+    keys, mv, cost = _oracle_units(luma[1], luma[0], req)
+    got = np.array([(out[u, s]["mv_x"], out[u, s]["mv_y"], out[u, s]["cost"]) for u, s in keys])
+    exp = np.column_stack([mv[:, 0], mv[:, 1], cost])
+    bad = np.nonzero(np.any(got != exp, axis=1))[0]
+    assert len(bad) == 0, [(keys[i], got[i].tolist(), exp[i].tolist()) for i in bad[:5]]
+
+
+def test_small_batch_with_wrapping_lambda_goes_to_the_item_kernel(gpu):
+    """A few units (the small path's size) with lambda ~7e7: the small kernel's
+    exact 32-bit cost (SAD << 5) + lambda * mvbits would wrap, so the batch must
+    go to the item kernel's 64-bit keys.  HIP == oracle."""
+    from jmme import FULL_SEARCH, MotionEstimator, synth
+    w, h, R = 176, 144, 8
+    rng = np.random.default_rng(77)
+    luma = synth.luma_sequence(w, h, 2, seed=12, gmv=(1, 2))
+    req = _random_units(rng, w, h, 3, R)
+    req["blk"]["lambda"] = rng.integers(67_200_000, 90_000_000, size=req["blk"]["lambda"].shape)
+    with MotionEstimator({"SearchRange": R, "SearchMode": -1}) as me:
+        me.set_small_batch_limit(1 << 20)
         me.upload_cur(luma[1])
         me.upload_ref(0, 0, luma[0])
         out = me.search(FULL_SEARCH, req)

@@ -154,11 +154,8 @@ def hybrid_block(dev, local: int, load_workload, iters: int = 10) -> dict:
 
 
 # ---- the drop-in encoder (JM 18.5 lencod with libjmme behind IntPelME) -----------
-def _lencod(binary, d, tag, yuv, w, h, frames, params, cfg_text, env=None):
-    import hashlib
+def _lencod_args(binary, d, tag, yuv, w, h, frames, params, cfg_text):
     import os
-    import re
-    import subprocess
     cfg = os.path.join(d, "enc.cfg")
     open(cfg, "w").write(cfg_text)
     out, rec = os.path.join(d, f"{tag}.264"), os.path.join(d, f"{tag}_rec.yuv")
@@ -167,6 +164,38 @@ def _lencod(binary, d, tag, yuv, w, h, frames, params, cfg_text, env=None):
             "-p", f"OutputFile={out}", "-p", f"ReconFile={rec}"]
     for k, v in params.items():
         args += ["-p", f"{k}={v}"]
+    return args, out, rec
+
+
+def _lencod_host(binary, d, yuv, w, h, frames, params, cfg_text, procs):
+    """`procs` stock encoders at once, each in its own directory on the same clip
+    (JM is single-threaded: N concurrent encodes are how the host spends N cores,
+    SURVEY §8(d)).  Returns every process's own 'Total ME time' (s)."""
+    import os
+    import re
+    import subprocess
+    runs = []
+    for i in range(procs):
+        wd = os.path.join(d, f"host{i}")
+        os.makedirs(wd, exist_ok=True)
+        args, _, _ = _lencod_args(binary, wd, "h", yuv, w, h, frames, params, cfg_text)
+        runs.append(subprocess.Popen(args, cwd=wd, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True))
+    me = []
+    for r in runs:
+        out, _ = r.communicate(timeout=900)
+        m = re.search(r"Total ME time for sequence\s*:\s*([0-9.]+) sec", out)
+        if r.returncode != 0 or not m:
+            raise RuntimeError("host encoder failed: " + out[-800:])
+        me.append(float(m.group(1)))
+    return me
+
+
+def _lencod(binary, d, tag, yuv, w, h, frames, params, cfg_text, env=None):
+    import hashlib
+    import os
+    import re
+    import subprocess
+    args, out, rec = _lencod_args(binary, d, tag, yuv, w, h, frames, params, cfg_text)
     t0 = time.time()
     r = subprocess.run(args, cwd=d, capture_output=True, text=True, timeout=900, env=dict(os.environ, **(env or {})))
     wall = time.time() - t0
@@ -209,15 +238,34 @@ def _lencod(binary, d, tag, yuv, w, h, frames, params, cfg_text, env=None):
     return res
 
 
-def dropin_block(modes=((-1, "FS"), (0, "FFS")), size=(1920, 1080), frames=3, search_range=32,
-                 reps=3) -> dict | None:
-    """JM 18.5 lencod, stock (CPU) and lencod_jmme (the same JM objects, integer-pel
-    ME through libjmme) on the same seeded clip: JM's own 'Total ME time' per
+# the drop-in rows of bench.py: (tag, JM parameters, frames).  FS / FFS with
+# sub-pel off and RDO off are configs[1]'s settings; the "_subpel" rows are
+# JM/bin/encoder_baseline.cfg's ME keys (sub-pel on, SATD half/quarter-pel and
+# mode decision, RDO on, adaptive rounding) with FS / FFS and one reference; EPZS
+# is configs[3]'s algorithm with the same file's EPZS section.
+BASELINE_SUBPEL = {"DisableSubpelME": 0, "MEDistortionFPel": 0, "MEDistortionHPel": 2, "MEDistortionQPel": 2,
+                   "MDDistortion": 2, "RestrictSearchRange": 2, "RDOptimization": 1, "AdaptiveRounding": 1}
+
+
+def dropin_modes():
+    from test_jm_dropin_epzs_gpu import BASELINE_EPZS
+    return (("FS", {"SearchMode": -1, "RDOptimization": 0}, 3),
+            ("FFS", {"SearchMode": 0, "RDOptimization": 0}, 3),
+            ("FS_subpel", dict(BASELINE_SUBPEL, SearchMode=-1), 2),
+            ("FFS_subpel", dict(BASELINE_SUBPEL, SearchMode=0), 2),
+            ("EPZS", dict(BASELINE_EPZS), 2))
+
+
+def dropin_block(modes=None, size=(1920, 1080), search_range=32, reps=2, host_procs=None) -> dict | None:
+    """JM 18.5 lencod, stock (CPU) and lencod_jmme (the same JM objects, the ME
+    through libjmme) on the same seeded clip: JM's own 'Total ME time' per
     P-frame, and byte identity of bitstream and reconstruction.  The GPU engine is
     created and warmed in init_motion_search_module (encoder start-up, before any
-    frame is timed).  The drop-in and the floor run `reps` times (the median ME
-    time is reported, the spread beside it: the host's load moves JM's own time);
-    the stock encoder once."""
+    frame is timed).  The drop-in runs `reps` times (median ME time reported, the
+    spread beside it); the stock encoder runs once alone (one core) and as
+    `host_procs` concurrent encoders (the host's cores, default the headline
+    baseline's host_cores()), so every row states its speed against one core and
+    against the whole host."""
     import os
     import tempfile
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -226,40 +274,49 @@ def dropin_block(modes=((-1, "FS"), (0, "FFS")), size=(1920, 1080), frames=3, se
     floor = os.path.join(repo, "integration", "_build", "lencod_noop_me")
     if not (os.path.exists(stock) and os.path.exists(gpu)):
         return None
+    if host_procs is None:
+        from bench import host_cores, cpu_model
+        host_procs, cpu = host_cores(), cpu_model()
+    else:
+        cpu = None
     from jmme import synth
     from test_jm_dropin_gpu import CFG
     w, h = size
-    out = {"workload": f"JM 18.5 lencod encoding a seeded {w}x{h} clip, {frames} frames (1 I + {frames - 1} P), "
-                       f"+-{search_range}, 1 ref, RDO off, sub-pel off: stock (1 core) vs the drop-in "
-                       f"(integer-pel ME on the GPU, one speculative batch per miss)",
-           "p_frames": frames - 1, "p_frame_macroblocks": (w // 16) * ((h + 15) // 16)}
+    mbs = (w // 16) * ((h + 15) // 16)
+    out = {"workload": f"JM 18.5 lencod encoding a seeded {w}x{h} clip (1 I + P frames), +-{search_range}, 1 ref: "
+                       f"stock (CPU) vs the drop-in (ME on the GPU)",
+           "p_frame_macroblocks": mbs, "host_procs": host_procs, "host_cpu": cpu}
     with tempfile.TemporaryDirectory() as d:
-        yuv = os.path.join(d, "in.yuv")
-        synth.write_yuv420(yuv, synth.luma_sequence(w, h, frames, seed=2024, gmv=(5, 3)))
-        for mode, tag in modes:
-            params = {"SearchMode": mode, "SearchRange": search_range, "RDOptimization": 0,
-                      "NumberReferenceFrames": 1}
-            if mode == 3:   # EPZS: encoder_baseline.cfg's ME keys (RDO on, SATD sub-pel, EPZSSubPelGrid 1)
-                from test_jm_dropin_epzs_gpu import BASELINE_EPZS
-                params = dict(BASELINE_EPZS, SearchRange=search_range, NumberReferenceFrames=1)
-            cpu = _lencod(stock, d, f"cpu{mode}", yuv, w, h, frames, params, CFG)
-            gs = sorted((_lencod(gpu, d, f"gpu{mode}_{r}", yuv, w, h, frames, params, CFG) for r in range(reps)),
+        for tag, mparams, frames in (modes or dropin_modes()):
+            yuv = os.path.join(d, f"in{frames}.yuv")
+            if not os.path.exists(yuv):
+                synth.write_yuv420(yuv, synth.luma_sequence(w, h, frames, seed=2024, gmv=(5, 3)))
+            params = dict(mparams, SearchRange=search_range, NumberReferenceFrames=1)
+            mode = params["SearchMode"]
+            p = frames - 1
+            cpu = _lencod(stock, d, f"cpu_{tag}", yuv, w, h, frames, params, CFG)
+            host = _lencod_host(stock, d, yuv, w, h, frames, params, CFG, host_procs) if host_procs > 1 else None
+            gs = sorted((_lencod(gpu, d, f"gpu_{tag}_{r}", yuv, w, h, frames, params, CFG) for r in range(reps)),
                         key=lambda x: x["me_s"])
             g = gs[len(gs) // 2]
-            p = frames - 1
             # JM's own loop around the search (integration/jm_noop_me.c: a zero-cost IntPelME)
-            fls = sorted((_lencod(floor, d, f"floor{mode}_{r}", yuv, w, h, frames, params, CFG) for r in range(reps)),
-                         key=lambda x: x["me_s"]) if mode in (-1, 0) and os.path.exists(floor) else []
-            fl = fls[len(fls) // 2] if fls else None
-            out[tag] = {
+            fl = _lencod(floor, d, f"floor_{tag}", yuv, w, h, frames, params, CFG) \
+                if mode in (-1, 0) and params.get("DisableSubpelME", 1) and os.path.exists(floor) else None
+            row = {
                 "stock_me_ms_per_p_frame": round(cpu["me_s"] * 1e3 / p, 2),
                 "dropin_me_ms_per_p_frame": round(g["me_s"] * 1e3 / p, 2),
                 "me_speedup": round(cpu["me_s"] / g["me_s"], 2) if g["me_s"] else None,
-                "dropin_mb_per_s": round(out["p_frame_macroblocks"] * p / g["me_s"], 1) if g["me_s"] else None,
-                "byte_identical": all(cpu["md5"] == x["md5"] for x in gs), "params": params,
+                "dropin_mb_per_s": round(mbs * p / g["me_s"], 1) if g["me_s"] else None,
+                "byte_identical": all(cpu["md5"] == x["md5"] for x in gs), "params": params, "p_frames": p,
                 "dropin_me_ms_per_p_frame_runs": [round(x["me_s"] * 1e3 / p, 2) for x in gs],
                 "jm_loop_floor_ms_per_p_frame": round(fl["me_s"] * 1e3 / p, 2) if fl and fl["me_s"] else None,
-                "jm_loop_floor_ms_per_p_frame_runs": [round(x["me_s"] * 1e3 / p, 2) for x in fls],
                 "stock_wall_s": cpu["wall_s"], "dropin_wall_s": g["wall_s"],
                 "dropin": {k: v for k, v in g.items() if k not in ("md5", "me_s", "wall_s")}}
+            if host:
+                # the host's rate: every encoder's P-frame macroblocks over the slowest one's ME time
+                host_rate = host_procs * mbs * p / max(host)
+                row.update(host_mb_per_s=round(host_rate, 1),
+                           host_me_ms_per_p_frame_slowest=round(max(host) * 1e3 / p, 2),
+                           me_speedup_vs_host=round(row["dropin_mb_per_s"] / host_rate, 3) if g["me_s"] else None)
+            out[tag] = row
     return out

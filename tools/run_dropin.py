@@ -1,6 +1,9 @@
 #!/usr/bin/env python3
-"""The bench's in-encoder block alone (stock lencod vs lencod_jmme, 1080p FS and
-FFS; add EPZS with --epzs), one JSON line.  GPU box."""
+"""The bench's in-encoder block alone (stock lencod vs lencod_jmme on the 1080p
+clip), one JSON line.  GPU box.
+Usage: python3 tools/run_dropin.py [TAG ...] [--reps N] [--host N]
+TAG: FS FFS FS_subpel FFS_subpel EPZS (default: all of bench_blocks.dropin_modes())."""
+import argparse
 import json
 import os
 import sys
@@ -11,5 +14,10 @@ for p in (REPO, os.path.join(REPO, "tools"), os.path.join(REPO, "tests"), os.pat
 
 import bench_blocks  # noqa: E402
 
-modes = [(-1, "FS"), (0, "FFS")] + ([(3, "EPZS")] if "--epzs" in sys.argv else [])
-print(json.dumps(bench_blocks.dropin_block(modes=tuple(modes))))
+ap = argparse.ArgumentParser()
+ap.add_argument("tags", nargs="*")
+ap.add_argument("--reps", type=int, default=2)
+ap.add_argument("--host", type=int, default=None, help="concurrent stock encoders (default: host_cores())")
+a = ap.parse_args()
+modes = [m for m in bench_blocks.dropin_modes() if not a.tags or m[0] in a.tags]
+print(json.dumps(bench_blocks.dropin_block(modes=tuple(modes), reps=a.reps, host_procs=a.host)))
