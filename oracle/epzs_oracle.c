@@ -6,6 +6,7 @@
  */
 #include "epzs_oracle.h"
 
+#include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -117,15 +118,60 @@ static int visit(ctx *c, int mx, int my)
 
 static int16_t int_mv(int16_t v) { return (int16_t)(v & 0xFFFC); }   /* set_integer_mv, me_epzs.c:39-43 */
 
-void eo_epzs(const eo_req *q, const int16_t *preds, const int16_t *stale, const eo_pel *cur, const eo_pel *ref,
-             int pitch, int W, int H, eo_res *out)
+/* ---- validity intervals (the drop-in's speculative searches) -------------
+ * Every comparison the search makes with the stop criterion S or the prevSad
+ * value P is monotone in that value, so it reads "x >= t" for a threshold t
+ * formed from the other operands.  ge() returns the outcome and narrows [lo, hi]
+ * to the values that give the same outcome; the search's result is then the
+ * same for every (S, P) inside the two intervals. */
+typedef struct iv {
+  int64_t lo, hi;
+} iv;
+static int ge(int64_t x, int64_t t, iv *v)
+{
+  if (x >= t) {
+    if (t > v->lo) v->lo = t;
+    return 1;
+  }
+  if (t - 1 < v->hi) v->hi = t - 1;
+  return 0;
+}
+static int64_t fdiv(int64_t a, int64_t b) { return a / b - ((a % b) != 0 && a < 0); }   /* floor, b > 0 */
+static int64_t cdiv(int64_t a, int64_t b) { return -fdiv(-a, b); }
+/* P <= S with both inputs: pinned on the guessed P so each interval stands alone */
+static int le2(int64_t p, int64_t s, iv *pv, iv *sv)
+{
+  if (p <= s) {
+    if (p < pv->hi) pv->hi = p;
+    if (p > sv->lo) sv->lo = p;
+    return 1;
+  }
+  if (p > pv->lo) pv->lo = p;
+  if (p - 1 < sv->hi) sv->hi = p - 1;
+  return 0;
+}
+/* whether a JMME_EPZS_PRED_* entry joins the list for centre cost g and stop S
+ * (me_epzs_common.c:1550 temporal, me_epzs.c:184-199 window, :205 block type) */
+static int cond_ok(int c, int64_t g, int64_t S, iv *sv)
+{
+  switch (c) {
+    case 1: return !ge(S, g, sv);                    /* g > S */
+    case 2: return !ge(S, fdiv(g - 1, 2) + 1, sv);   /* g > 2 S */
+    case 3: return !ge(S, fdiv(g - 1, 3) + 1, sv);   /* g > 3 S */
+    default: return 1;
+  }
+}
+
+void eo_epzs_ex(const eo_req *q, const int16_t *preds, const uint8_t *cond, const int16_t *stale, const eo_pel *cur,
+                const eo_pel *ref, int pitch, int W, int H, eo_res *out, eo_bounds *bnd, int16_t *vis, int max_vis)
 {
   ctx c;
   const int frame = q->flags & 1, pslice = (q->flags >> 1) & 1, bt = q->blocktype, refi = q->ref_idx;
   const int64_t lambda_dist = (int64_t)q->lambda * (q->variant ? 3 : 2);
   const int mv_range = q->variant ? 12 : 10;
   int64_t stop = q->medthres + lambda_dist, prev = q->prev_sad, min;
-  int tmpx = q->center_x, tmpy = q->center_y, i;
+  int tmpx = q->center_x, tmpy = q->center_y, i, written = 0;
+  iv sv = {INT64_MIN, INT64_MAX}, pv = {INT64_MIN, INT64_MAX};
   memset(out, 0, sizeof(*out));
   c.q = q;
   c.cur = cur;
@@ -144,20 +190,25 @@ void eo_epzs(const eo_req *q, const int16_t *preds, const int16_t *stale, const 
   visit(&c, q->center_x, q->center_y);
   min = cost_of(&c, q->center_x, q->center_y);
 
-  if (refi > 0 && frame && prev < (stop < min ? stop : min)) {
+  if (refi > 0 && frame && !ge(prev, stop < min ? stop : min, &pv)) {   /* prev < min(stop, min) */
     out->path = 1;
     goto done_noupdate;
   }
   if (min > stop) {
     int64_t second = DMAX;
-    int check_median = 0, tmp2x = 0, tmp2y = 0, P;
+    int check_median = 0, tmp2x = 0, tmp2y = 0, P, ok[4] = {1, 1, 1, 1};
+    const int64_t gen_min = min;
     stop = q->stop_crit;
-    if (min < (stop >> 1)) {
+    if (ge(stop, 2 * min + 2, &sv)) {      /* min < (stop >> 1) */
       out->path = 2;
       goto done_noupdate;
     }
+    if (cond)   /* the conditional parts of the list, generated with min_mcost = the centre's cost */
+      for (i = 0; i < q->n_pred; i++)
+        if (cond[i] && ok[cond[i]] == 1) ok[cond[i]] = 2 + cond_ok(cond[i], gen_min, stop, &sv);
     for (i = 0; i < q->n_pred; i++) {
       const int mx = int_mv(preds[2 * i]), my = int_mv(preds[2 * i + 1]);
+      if (cond && cond[i] && ok[cond[i]] != 3) continue;   /* not in JM's list */
       if (in_range(&c, mx, my) && visit(&c, mx, my)) {
         const int64_t mc = cost_of(&c, mx, my);
         if (mc < min) {
@@ -175,16 +226,16 @@ void eo_epzs(const eo_req *q, const int16_t *preds, const int16_t *stale, const 
           check_median = 1;
         }
       }
-      if (q->variant && min < ((3 * stop) >> 2)) {     /* me_epzs.c:583-596 */
+      if (q->variant && ge(stop, cdiv(4 * min + 4, 3), &sv)) {     /* min < (3 stop) >> 2, me_epzs.c:583-596 */
         out->path = 3;
         goto done_mv_noupdate;
       }
     }
-    if (min > stop) {
+    if (!ge(stop, min, &sv)) {             /* min > stop */
       int cenx, ceny, point = 0, pstop = 0, next_last = 0, total, dir = 0;
       P = primary_pattern(q->pattern);
       if (q->pattern != 0) {
-        if (min < stop + ((3 * q->medthres) >> 1)) {
+        if (ge(stop, min - ((3 * q->medthres) >> 1) + 1, &sv)) {   /* min < stop + 3 medthres / 2 */
           const int dx = abs(tmpx - q->center_x), dy = abs(tmpy - q->center_y);
           P = ((tmpx == 0 && tmpy == 0) || (dx < mv_range && dy < mv_range)) ? P_SDIAMOND : P_SQUARE;
         } else if (q->variant || bt > 4 || (refi > 0 && bt != 1)) {
@@ -225,11 +276,13 @@ void eo_epzs(const eo_req *q, const int16_t *preds, const int16_t *stale, const 
           }
         } while (pstop != 1);
 
-        if (refi > 0 && frame && (4 * prev < min || (3 * prev < min && prev <= stop))) {
+        /* 4 prev < min || (3 prev < min && prev <= stop) */
+        if (refi > 0 && frame &&
+            (!ge(prev, fdiv(min - 1, 4) + 1, &pv) || (!ge(prev, fdiv(min - 1, 3) + 1, &pv) && le2(prev, stop, &pv, &sv)))) {
           out->path = 4;
           goto done_mv_noupdate;
         }
-        if (!(check_median && (pslice || (!q->variant && bt < 5)) && min > stop && q->dual > 0)) break;
+        if (!(check_median && (pslice || (!q->variant && bt < 5)) && !ge(stop, min, &sv) && q->dual > 0)) break;
         point = 0;
         pstop = 0;
         dir = 0;
@@ -247,20 +300,43 @@ void eo_epzs(const eo_req *q, const int16_t *preds, const int16_t *stale, const 
     }
   }
   out->path = out->path ? out->path : 5;
-  if (refi == 0 || prev > min) prev = min;
+  if (refi == 0 || ge(prev, min + 1, &pv)) {   /* prev > min */
+    prev = min;
+    written = 1;
+  }
 done_mv_noupdate:
   out->mv_x = (int16_t)tmpx;
   out->mv_y = (int16_t)tmpy;
-  out->cost = min;
-  out->prev_sad = prev;
-  free(c.map);
-  return;
+  goto finish;
 done_noupdate:
   out->mv_x = q->center_x;
   out->mv_y = q->center_y;
+finish:
   out->cost = min;
   out->prev_sad = prev;
+  if (bnd) {
+    bnd->stop_lo = sv.lo;
+    bnd->stop_hi = sv.hi;
+    bnd->prev_lo = pv.lo;
+    bnd->prev_hi = pv.hi;
+    bnd->prev_written = written;
+    bnd->n_visited = 0;
+    for (i = 0; i < c.side_x * c.side_y; i++)   /* every stamped cell, (dx, dy) qpel from the centre, in cell order */
+      if (c.map[i]) {
+        if (vis && bnd->n_visited < max_vis) {
+          vis[2 * bnd->n_visited] = (int16_t)(4 * (i % c.side_x) - q->max_x);
+          vis[2 * bnd->n_visited + 1] = (int16_t)(4 * (i / c.side_x) - q->max_y);
+        }
+        bnd->n_visited++;
+      }
+  }
   free(c.map);
+}
+
+void eo_epzs(const eo_req *q, const int16_t *preds, const int16_t *stale, const eo_pel *cur, const eo_pel *ref,
+             int pitch, int W, int H, eo_res *out)
+{
+  eo_epzs_ex(q, preds, NULL, stale, cur, ref, pitch, W, H, out, NULL, NULL, 0);
 }
 
 void eo_epzs_batch(const eo_req *q, int n, const int16_t *preds, const int16_t *stale, const eo_pel *cur,
@@ -327,8 +403,9 @@ static int gvisit(gctx *c, int mx, int my)
   return 1;
 }
 
-void eo_epzs_grid(const eo_req *q, const int16_t *preds, const int16_t *stale, const eo_pel *cur, int pitch,
-                  const eo_pel *subs, int W, int H, eo_res *out)
+void eo_epzs_grid_ex(const eo_req *q, const int16_t *preds, const uint8_t *cond, const int16_t *stale,
+                     const eo_pel *cur, int pitch, const eo_pel *subs, int W, int H, eo_res *out, eo_bounds *bnd,
+                     int16_t *vis, int max_vis)
 {
   gctx c;
   const int frame = q->flags & 1, pslice = (q->flags >> 1) & 1, bt = q->blocktype, refi = q->ref_idx;
@@ -336,7 +413,8 @@ void eo_epzs_grid(const eo_req *q, const int16_t *preds, const int16_t *stale, c
   const int64_t lambda_dist = (int64_t)q->lambda * (sub ? 3 : 2);
   const int mv_range = sub ? 12 : 10;
   int64_t stop = q->medthres + lambda_dist, prev = q->prev_sad, min;
-  int tmpx = q->center_x, tmpy = q->center_y, i;
+  int tmpx = q->center_x, tmpy = q->center_y, i, written = 0;
+  iv sv = {INT64_MIN, INT64_MAX}, pv = {INT64_MIN, INT64_MAX};
   memset(out, 0, sizeof(*out));
   c.q = q;
   c.cur = cur;
@@ -356,21 +434,30 @@ void eo_epzs_grid(const eo_req *q, const int16_t *preds, const int16_t *stale, c
   min = gcost_of(&c, q->center_x, q->center_y);
 
   /* :67-80 / :496-507: the ref > 0 early exit also fires when prevSad * 8 (6 for subMB) < min */
-  if (refi > 0 && frame && (prev < (stop < min ? stop : min) || prev * (sub ? 6 : 8) < min)) {
+  if (refi > 0 && frame &&
+      (!ge(prev, stop < min ? stop : min, &pv) || !ge(prev, fdiv(min - 1, sub ? 6 : 8) + 1, &pv))) {
     out->path = 1;
     goto done_noupdate;
   }
   if (min > stop) {
     int64_t second = DMAX;
-    int check_median = 0, tmp2x = 0, tmp2y = 0, P;
+    int check_median = 0, tmp2x = 0, tmp2y = 0, P, ok[4] = {1, 1, 1, 1};
+    const int64_t gen_min = min;
     stop = q->stop_crit;
-    if (min < (stop >> 1)) {               /* :112-124 (variant 2 updates prevSad) / :525-536 */
+    if (ge(stop, 2 * min + 2, &sv)) {      /* min < (stop >> 1): :112-124 (variant 2 updates prevSad) / :525-536 */
       out->path = 2;
-      if (!sub && (refi == 0 || prev > min)) prev = min;
+      if (!sub && (refi == 0 || ge(prev, min + 1, &pv))) {
+        prev = min;
+        written = 1;
+      }
       goto done_noupdate;
     }
+    if (cond)   /* the conditional parts of the list, generated with min_mcost = the centre's cost */
+      for (i = 0; i < q->n_pred; i++)
+        if (cond[i] && ok[cond[i]] == 1) ok[cond[i]] = 2 + cond_ok(cond[i], gen_min, stop, &sv);
     for (i = 0; i < q->n_pred; i++) {
       const int mx = preds[2 * i], my = preds[2 * i + 1];   /* no set_integer_mv */
+      if (cond && cond[i] && ok[cond[i]] != 3) continue;   /* not in JM's list */
       if (gin_range(&c, mx, my) && gvisit(&c, mx, my)) {
         int64_t mc = (int64_t)q->lambda * (mvbits(mx - q->pred_x) + mvbits(my - q->pred_y));
         if (mc < second) {   /* :224-226: the SAD of a candidate whose mv cost reaches second is skipped */
@@ -392,25 +479,25 @@ void eo_epzs_grid(const eo_req *q, const int16_t *preds, const int16_t *stale, c
         }
       }
       if (sub) {
-        if (refi > 0 && frame && prev * 3 < min) {   /* :590-600: returns without touching *mv */
+        if (refi > 0 && frame && !ge(prev, fdiv(min - 1, 3) + 1, &pv)) {   /* prev * 3 < min, :590-600 */
           out->path = 6;
           goto done_noupdate;
         }
-        if (min < ((3 * stop) >> 2)) {                /* :604-615 */
+        if (ge(stop, cdiv(4 * min + 4, 3), &sv)) {                          /* min < (3 stop) >> 2, :604-615 */
           out->path = 3;
           goto done_mv_noupdate;
         }
       }
     }
-    if (!sub && refi > 0 && frame && prev * 3 < min) {   /* :249-265 */
+    if (!sub && refi > 0 && frame && !ge(prev, fdiv(min - 1, 3) + 1, &pv)) {   /* prev * 3 < min, :249-265 */
       out->path = 7;
       goto done_mv_noupdate;
     }
-    if (min > stop) {
+    if (!ge(stop, min, &sv)) {             /* min > stop */
       int cenx, ceny, point = 0, pstop = 0, next_last = 0, total, dir = 0;
       P = primary_pattern(q->pattern);
       if (q->pattern != 0) {
-        if (min < stop + ((3 * q->medthres) >> 1)) {
+        if (ge(stop, min - ((3 * q->medthres) >> 1) + 1, &sv)) {   /* min < stop + 3 medthres / 2 */
           const int dx = abs(tmpx - q->center_x), dy = abs(tmpy - q->center_y);
           P = ((sub && bt == 7) || (tmpx == 0 && tmpy == 0) || (dx < mv_range && dy < mv_range)) ? P_SDIAMOND
                                                                                                   : P_SQUARE;
@@ -455,13 +542,15 @@ void eo_epzs_grid(const eo_req *q, const int16_t *preds, const int16_t *stale, c
           }
         } while (pstop != 1);
 
-        if (refi > 0 && frame && (4 * prev < min || (3 * prev < min && prev <= stop))) {
+        /* 4 prev < min || (3 prev < min && prev <= stop) */
+        if (refi > 0 && frame &&
+            (!ge(prev, fdiv(min - 1, 4) + 1, &pv) || (!ge(prev, fdiv(min - 1, 3) + 1, &pv) && le2(prev, stop, &pv, &sv)))) {
           out->path = 4;
           goto done_mv_noupdate;
         }
-        /* second-best refinement, :337-340 / :298-301 */
-        if (!(check_median && (!sub || bt != 7) && (refi == 0 || min < 2 * prev) && (!sub || pslice) &&
-              min > ((3 * stop) >> 1) && q->dual > 0))
+        /* second-best refinement, :337-340 / :298-301: min < 2 prev; min > (3 stop) >> 1 */
+        if (!(check_median && (!sub || bt != 7) && (refi == 0 || ge(prev, cdiv(min + 1, 2), &pv)) && (!sub || pslice) &&
+              !ge(stop, fdiv(2 * min - 1, 3) + 1, &sv) && q->dual > 0))
           break;
         point = 0;
         pstop = 0;
@@ -480,20 +569,44 @@ void eo_epzs_grid(const eo_req *q, const int16_t *preds, const int16_t *stale, c
     }
   }
   out->path = out->path ? out->path : 5;
-  if (refi == 0 || prev > min) prev = min;
+  if (refi == 0 || ge(prev, min + 1, &pv)) {   /* prev > min */
+    prev = min;
+    written = 1;
+  }
 done_mv_noupdate:
   out->mv_x = (int16_t)tmpx;
   out->mv_y = (int16_t)tmpy;
-  out->cost = min;
-  out->prev_sad = prev;
-  free(c.map);
-  return;
+  goto finish;
 done_noupdate:
   out->mv_x = q->center_x;
   out->mv_y = q->center_y;
+finish:
   out->cost = min;
   out->prev_sad = prev;
+  if (bnd) {
+    const int side_y = 2 * q->max_y + 1;
+    bnd->stop_lo = sv.lo;
+    bnd->stop_hi = sv.hi;
+    bnd->prev_lo = pv.lo;
+    bnd->prev_hi = pv.hi;
+    bnd->prev_written = written;
+    bnd->n_visited = 0;
+    for (i = 0; i < c.side_x * side_y; i++)     /* every stamped cell, (dx, dy) qpel from the centre, in cell order */
+      if (c.map[i]) {
+        if (vis && bnd->n_visited < max_vis) {
+          vis[2 * bnd->n_visited] = (int16_t)(i % c.side_x - q->max_x);
+          vis[2 * bnd->n_visited + 1] = (int16_t)(i / c.side_x - q->max_y);
+        }
+        bnd->n_visited++;
+      }
+  }
   free(c.map);
+}
+
+void eo_epzs_grid(const eo_req *q, const int16_t *preds, const int16_t *stale, const eo_pel *cur, int pitch,
+                  const eo_pel *subs, int W, int H, eo_res *out)
+{
+  eo_epzs_grid_ex(q, preds, NULL, stale, cur, pitch, subs, W, H, out, NULL, NULL, 0);
 }
 
 void eo_epzs_grid_batch(const eo_req *q, int n, const int16_t *preds, const int16_t *stale, const eo_pel *cur,
@@ -503,4 +616,26 @@ void eo_epzs_grid_batch(const eo_req *q, int n, const int16_t *preds, const int1
   for (i = 0; i < n; i++)
     eo_epzs_grid(&q[i], preds + 2 * (size_t)q[i].pred_off, stale + 2 * (size_t)q[i].stale_off, cur, pitch,
                  subs[q[i].plane], W, H, &out[i]);
+}
+
+void eo_epzs_ex_batch(const eo_req *q, int n, const int16_t *preds, const uint8_t *cond, const int16_t *stale,
+                      const eo_pel *cur, const eo_pel *const *refs, int pitch, int W, int H, eo_res *out,
+                      eo_bounds *bnd, int16_t *vis, int max_vis)
+{
+  int i;
+  for (i = 0; i < n; i++)
+    eo_epzs_ex(&q[i], preds + 2 * (size_t)q[i].pred_off, cond ? cond + q[i].pred_off : NULL,
+               stale + 2 * (size_t)q[i].stale_off, cur, refs[q[i].plane], pitch, W, H, &out[i], &bnd[i],
+               vis ? vis + 2 * (size_t)max_vis * i : NULL, max_vis);
+}
+
+void eo_epzs_grid_ex_batch(const eo_req *q, int n, const int16_t *preds, const uint8_t *cond, const int16_t *stale,
+                           const eo_pel *cur, int pitch, const eo_pel *const *subs, int W, int H, eo_res *out,
+                           eo_bounds *bnd, int16_t *vis, int max_vis)
+{
+  int i;
+  for (i = 0; i < n; i++)
+    eo_epzs_grid_ex(&q[i], preds + 2 * (size_t)q[i].pred_off, cond ? cond + q[i].pred_off : NULL,
+                    stale + 2 * (size_t)q[i].stale_off, cur, pitch, subs[q[i].plane], W, H, &out[i], &bnd[i],
+                    vis ? vis + 2 * (size_t)max_vis * i : NULL, max_vis);
 }

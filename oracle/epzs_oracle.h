@@ -72,6 +72,35 @@ void eo_epzs_grid(const eo_req *q, const int16_t *preds, const int16_t *stale, c
 void eo_epzs_grid_batch(const eo_req *q, int n, const int16_t *preds, const int16_t *stale, const eo_pel *cur,
                         int pitch, const eo_pel *const *subs, int W, int H, eo_res *out);
 
+/* Speculative searches (the drop-in's EPZS batches): with the predictor
+ * conditions of jmme_epzs_search_ex (cond[i] = JMME_EPZS_PRED_*, NULL: all
+ * unconditional; the list JM searches is the entries whose condition holds for
+ * the centre's cost) and the validity intervals of the result: the same result
+ * (mv, cost, visited cells, p_motion) for every stop criterion in
+ * [stop_lo, stop_hi] and prevSad in [prev_lo, prev_hi] (each comparison with
+ * either value is monotone in it; P <= S, which holds both, is pinned on the
+ * given P).  prev_written: JM stores *prevSad = cost at this return (else it
+ * leaves *prevSad alone).  n_visited and vis (may be NULL; up to max_vis pairs):
+ * the EPZSMap cells the search stamped, (dx, dy) qpel from the centre, in cell
+ * (row-major) order.  Layout = jmme_epzs_bounds. */
+typedef struct eo_bounds {
+  int64_t stop_lo, stop_hi, prev_lo, prev_hi;
+  int32_t prev_written, n_visited;
+} eo_bounds;                    /* 40 bytes */
+
+void eo_epzs_ex(const eo_req *q, const int16_t *preds, const uint8_t *cond, const int16_t *stale, const eo_pel *cur,
+                const eo_pel *ref, int pitch, int W, int H, eo_res *out, eo_bounds *bnd, int16_t *vis, int max_vis);
+void eo_epzs_grid_ex(const eo_req *q, const int16_t *preds, const uint8_t *cond, const int16_t *stale,
+                     const eo_pel *cur, int pitch, const eo_pel *subs, int W, int H, eo_res *out, eo_bounds *bnd,
+                     int16_t *vis, int max_vis);
+/* batches: cond (may be NULL) parallel to preds, indexed by pred_off like them; vis: max_vis pairs per request */
+void eo_epzs_ex_batch(const eo_req *q, int n, const int16_t *preds, const uint8_t *cond, const int16_t *stale,
+                      const eo_pel *cur, const eo_pel *const *refs, int pitch, int W, int H, eo_res *out,
+                      eo_bounds *bnd, int16_t *vis, int max_vis);
+void eo_epzs_grid_ex_batch(const eo_req *q, int n, const int16_t *preds, const uint8_t *cond, const int16_t *stale,
+                           const eo_pel *cur, int pitch, const eo_pel *const *subs, int W, int H, eo_res *out,
+                           eo_bounds *bnd, int16_t *vis, int max_vis);
+
 #ifdef __cplusplus
 }
 #endif

@@ -404,6 +404,55 @@ def epzs_grid_batch(req, preds, stale, cur, refs, bits=8):
     return out
 
 
+EPZS_BOUNDS = np.dtype([("stop_lo", "<i8"), ("stop_hi", "<i8"), ("prev_lo", "<i8"), ("prev_hi", "<i8"),
+                        ("prev_written", "<i4"), ("n_visited", "<i4")])
+assert EPZS_BOUNDS.itemsize == 40
+
+
+def epzs_spec_batch(req, preds, cond, stale, cur, refs, grid: bool, bits=8, max_vis=64, subs=None):
+    """eo_epzs_ex / eo_epzs_grid_ex: the searches with predictor conditions (cond
+    uint8 parallel to preds, or None) and their validity intervals -> (EPZS_RES[n],
+    EPZS_BOUNDS[n], visited int16 [n, max_vis, 2]); subs: prebuilt sub-images per
+    ref (grid), else built here"""
+    wide = bits > 8
+    pel = np.uint16 if wide else np.uint8
+    lib = load_epzs(wide)
+    if not hasattr(lib, "_ex_sig"):
+        P, I = ctypes.c_void_p, ctypes.c_int
+        lib.eo_epzs_ex_batch.argtypes = [P, I, P, P, P, P, P, I, I, I, P, P, P, I]
+        lib.eo_epzs_grid_ex_batch.argtypes = [P, I, P, P, P, P, I, P, I, I, P, P, P, I]
+        lib._ex_sig = True
+    req = np.ascontiguousarray(req, EPZS_REQ)
+    preds = np.ascontiguousarray(preds, np.int16).reshape(-1, 2)
+    stale = np.ascontiguousarray(stale, np.int16).reshape(-1, 2)
+    if len(preds) == 0:
+        preds = np.zeros((1, 2), np.int16)
+    if len(stale) == 0:
+        stale = np.zeros((1, 2), np.int16)
+    cnd = None if cond is None else np.ascontiguousarray(cond, np.uint8)
+    if cnd is not None and len(cnd) == 0:
+        cnd = np.zeros(1, np.uint8)
+    cur = np.ascontiguousarray(cur, pel)
+    h, w = cur.shape
+    out = np.zeros(len(req), EPZS_RES)
+    bnd = np.zeros(len(req), EPZS_BOUNDS)
+    vis = np.zeros((len(req), max_vis, 2), np.int16)
+    cptr = None if cnd is None else cnd.ctypes.data
+    if grid:
+        if subs is None:
+            subs = [np.ascontiguousarray(sub_images(r, bits).astype(pel)) for r in refs]
+        ptrs = (ctypes.c_void_p * len(subs))(*[x.ctypes.data for x in subs])
+        lib.eo_epzs_grid_ex_batch(req.ctypes.data, len(req), preds.ctypes.data, cptr, stale.ctypes.data,
+                                  cur.ctypes.data, w, ptrs, w, h, out.ctypes.data, bnd.ctypes.data, vis.ctypes.data,
+                                  max_vis)
+    else:
+        refs = [np.ascontiguousarray(r, pel) for r in refs]
+        ptrs = (ctypes.c_void_p * len(refs))(*[r.ctypes.data for r in refs])
+        lib.eo_epzs_ex_batch(req.ctypes.data, len(req), preds.ctypes.data, cptr, stale.ctypes.data, cur.ctypes.data,
+                             ptrs, w, w, h, out.ctypes.data, bnd.ctypes.data, vis.ctypes.data, max_vis)
+    return out, bnd, vis
+
+
 def fractal_decode_mbs(mbs, views, component=1):
     """fro_decode_mbs: the thesis decoder (block_dec.c) -> (rc, rec H x W uint8)"""
     lib = load_fractal()
