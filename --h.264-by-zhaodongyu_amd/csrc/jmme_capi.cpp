@@ -1312,7 +1312,8 @@ int prepare_subs(jmme_ctx *ctx, hipStream_t s);   // sub-pel section below
 
 namespace {
 int launch_epzs_ex(jmme_ctx *ctx, const jmme_epzs_req *d_req, int n, const int16_t *d_preds, const uint8_t *d_cond,
-                   const int16_t *d_stale, jmme_epzs_res *d_out, int16_t *d_vis, int max_visited, hipStream_t s) {
+                   const int16_t *d_stale, jmme_epzs_res *d_out, int16_t *d_vis, int max_visited, hipStream_t s,
+                   jmme_epzs_bounds *d_bounds = nullptr, jmme_block_res *d_int = nullptr) {
   if (sync_ref_table(ctx, s)) return -1;
   EpzsParams p{};
   p.cur = ctx->d_cur;
@@ -1342,6 +1343,8 @@ int launch_epzs_ex(jmme_ctx *ctx, const jmme_epzs_req *d_req, int n, const int16
   p.pred_cond = d_cond;
   p.visited = d_vis;
   p.max_visited = max_visited;
+  p.bounds = d_bounds;
+  p.int_out = d_int;
   HIPCHK(launch_epzs(p, s));
   return 0;
 }
@@ -1479,6 +1482,89 @@ extern "C" int jmme_epzs_search_ex(jmme_ctx *ctx, const jmme_epzs_req *req, int 
     for (int i = 0; i < n; ++i)
       std::memcpy(visited + 2 * (size_t)max_visited * i, h_vis + 2 * (size_t)max_visited * i,
                   (size_t)out[i].n_visited * 4);
+  return 0;
+}
+
+static_assert(sizeof(jmme_epzs_bounds) == 40, "EPZS bounds ABI layout");
+
+extern "C" int jmme_epzs_speculate(jmme_ctx *ctx, const jmme_epzs_req *req, int n, const int16_t *preds,
+                                   const uint8_t *pred_cond, int n_preds, const int16_t *stale, int n_stale,
+                                   jmme_epzs_res *out, jmme_epzs_bounds *bounds, int16_t *visited, int max_visited,
+                                   const jmme_subpel_req *sp_req, jmme_block_res *sp_out) {
+  DevGuard dg_(ctx);
+  if (!ctx) return fail("null ctx");
+  if (n <= 0) return n < 0 ? fail("negative request count") : 0;
+  if (!req || !out || !bounds || !visited || (n_preds && !preds) || (n_stale && !stale)) return fail("null array");
+  if (sp_req && !sp_out) return fail("sub-pel requests without an output array");
+  if (!ctx->d_cur) return fail("no current frame uploaded");
+  if (max_visited <= 0) return fail("max_visited must be positive");
+  if (epzs_validate(ctx, req, n, n_preds, n_stale)) return -1;
+  if (pred_cond)
+    for (int i = 0; i < n_preds; ++i)
+      if (pred_cond[i] > JMME_EPZS_PRED_GT_3STOP) return fail("predictor %d: condition %d", i, pred_cond[i]);
+  if (sp_req && jmme_subpel_validate(ctx, sp_req, n)) return -1;
+  // one mapped pinned block: [req | preds | stale | cond | out | bounds | visited | sp_req | int | sp_out]
+  const size_t b_req = align64((size_t)n * sizeof(jmme_epzs_req)), b_pred = align64((size_t)n_preds * 4 + 4);
+  const size_t b_stale = align64((size_t)n_stale * 4 + 4), b_cond = align64((size_t)n_preds + 1);
+  const size_t b_out = align64((size_t)n * sizeof(jmme_epzs_res)), b_bnd = align64((size_t)n * sizeof(jmme_epzs_bounds));
+  const size_t b_vis = align64((size_t)n * max_visited * 4);
+  const size_t b_sp = sp_req ? align64((size_t)n * sizeof(jmme_subpel_req)) : 0;
+  const size_t b_res = sp_req ? align64((size_t)n * sizeof(jmme_block_res)) : 0;
+  const size_t need = b_req + b_pred + b_stale + b_cond + b_out + b_bnd + b_vis + b_sp + 2 * b_res;
+  if (need > ctx->cap_emap) {
+    if (ctx->h_emap) (void)hipHostFree(ctx->h_emap);
+    ctx->h_emap = nullptr;
+    ctx->cap_emap = 0;
+    const size_t cap = std::max<size_t>(1u << 20, need + need / 2);
+    HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_emap), cap, hipHostMallocMapped));
+    ctx->cap_emap = cap;
+  }
+  uint8_t *h = ctx->h_emap;
+  void *dh = nullptr;
+  HIPCHK(hipHostGetDevicePointer(&dh, h, 0));
+  uint8_t *d = static_cast<uint8_t *>(dh);
+  size_t o = 0;
+  std::memcpy(h + o, req, (size_t)n * sizeof(jmme_epzs_req));
+  const jmme_epzs_req *d_req = reinterpret_cast<const jmme_epzs_req *>(d + o);
+  o += b_req;
+  if (n_preds) std::memcpy(h + o, preds, (size_t)n_preds * 4);
+  const int16_t *d_preds = reinterpret_cast<const int16_t *>(d + o);
+  o += b_pred;
+  if (n_stale) std::memcpy(h + o, stale, (size_t)n_stale * 4);
+  const int16_t *d_stale = reinterpret_cast<const int16_t *>(d + o);
+  o += b_stale;
+  if (pred_cond && n_preds) std::memcpy(h + o, pred_cond, (size_t)n_preds);
+  const uint8_t *d_cond = pred_cond ? d + o : nullptr;
+  o += b_cond;
+  jmme_epzs_res *h_out = reinterpret_cast<jmme_epzs_res *>(h + o), *d_out = reinterpret_cast<jmme_epzs_res *>(d + o);
+  o += b_out;
+  jmme_epzs_bounds *h_bnd = reinterpret_cast<jmme_epzs_bounds *>(h + o);
+  jmme_epzs_bounds *d_bnd = reinterpret_cast<jmme_epzs_bounds *>(d + o);
+  o += b_bnd;
+  int16_t *h_vis = reinterpret_cast<int16_t *>(h + o), *d_vis = reinterpret_cast<int16_t *>(d + o);
+  o += b_vis;
+  const jmme_subpel_req *d_spq = nullptr;
+  jmme_block_res *d_int = nullptr, *d_spo = nullptr, *h_spo = nullptr;
+  if (sp_req) {
+    std::memcpy(h + o, sp_req, (size_t)n * sizeof(jmme_subpel_req));
+    d_spq = reinterpret_cast<const jmme_subpel_req *>(d + o);
+    o += b_sp;
+    d_int = reinterpret_cast<jmme_block_res *>(d + o);
+    o += b_res;
+    std::memcpy(h + o, sp_out, (size_t)n * sizeof(jmme_block_res));   // blocktype-0 entries keep theirs
+    d_spo = reinterpret_cast<jmme_block_res *>(d + o);
+    h_spo = reinterpret_cast<jmme_block_res *>(h + o);
+  }
+  hipStream_t s = nullptr;
+  if (launch_epzs_ex(ctx, d_req, n, d_preds, d_cond, d_stale, d_out, d_vis, max_visited, s, d_bnd, d_int)) return -1;
+  if (sp_req && jmme_subpel_refine_async(ctx, d_spq, n, d_int, d_spo, s)) return -1;
+  HIPCHK(hipStreamSynchronize(s));
+  std::memcpy(out, h_out, (size_t)n * sizeof(jmme_epzs_res));
+  std::memcpy(bounds, h_bnd, (size_t)n * sizeof(jmme_epzs_bounds));
+  for (int i = 0; i < n; ++i)   // only the pairs each search wrote
+    std::memcpy(visited + 2 * (size_t)max_visited * i, h_vis + 2 * (size_t)max_visited * i,
+                (size_t)std::min(out[i].n_visited, max_visited) * 4);
+  if (sp_req) std::memcpy(sp_out, h_spo, (size_t)n * sizeof(jmme_block_res));
   return 0;
 }
 

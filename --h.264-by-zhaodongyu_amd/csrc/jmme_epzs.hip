@@ -267,6 +267,36 @@ __device__ __forceinline__ int64_t rl64(int64_t v, int j) {
 
 __device__ __forceinline__ int16_t int_mv(int v) { return (int16_t)(v & 0xFFFC); }   // set_integer_mv
 
+// Validity intervals (the drop-in's speculative searches, jmme_epzs_bounds):
+// every comparison with the stop criterion S or the prevSad value P is monotone
+// in it and reads "x >= t"; ge() returns the outcome and narrows [lo, hi] to the
+// values that give the same one (restated in oracle/epzs_oracle.c).  The values
+// are wave-uniform, so this is scalar bookkeeping.
+struct Iv {
+  int64_t lo, hi;
+};
+__device__ __forceinline__ bool ge(int64_t x, int64_t t, Iv &v) {
+  if (x >= t) {
+    v.lo = t > v.lo ? t : v.lo;
+    return true;
+  }
+  v.hi = t - 1 < v.hi ? t - 1 : v.hi;
+  return false;
+}
+__device__ __forceinline__ int64_t fdiv(int64_t a, int64_t b) { return a / b - ((a % b) != 0 && a < 0); }
+__device__ __forceinline__ int64_t cdiv(int64_t a, int64_t b) { return -fdiv(-a, b); }
+// P <= S with both inputs: pinned on the given P so each interval stands alone
+__device__ __forceinline__ bool le2(int64_t pr, int64_t st, Iv &pv, Iv &sv) {
+  if (pr <= st) {
+    pv.hi = pr < pv.hi ? pr : pv.hi;
+    sv.lo = pr > sv.lo ? pr : sv.lo;
+    return true;
+  }
+  pv.lo = pr > pv.lo ? pr : pv.lo;
+  sv.hi = pr - 1 < sv.hi ? pr - 1 : sv.hi;
+  return false;
+}
+
 template <bool GRID, bool HBD>
 __device__ void search_one(const EpzsParams &p, const jmme_epzs_req &q, WaveLds &w, uint32_t *map, int lane,
                            jmme_epzs_res *out) {
@@ -324,34 +354,44 @@ __device__ void search_one(const EpzsParams &p, const jmme_epzs_req &q, WaveLds 
   int64_t best = rl64(eval_costs<GRID, HBD>(s, lane, 1, s.cx, s.cy), 0);
   int tmpx = s.cx, tmpy = s.cy, path = 5;
   bool update = true;
+  Iv sv{INT64_MIN, INT64_MAX}, pv{INT64_MIN, INT64_MAX};
 
   // me_epzs_int.c:67-80 / 496-507 add prevSad * 8 (subMB: 6) < min to the ref > 0 early exit
-  if (refi > 0 && frame && (prev < (stop < best ? stop : best) || (GRID && prev * (variant ? 6 : 8) < best))) {
+  if (refi > 0 && frame &&
+      (!ge(prev, stop < best ? stop : best, pv) || (GRID && !ge(prev, fdiv(best - 1, variant ? 6 : 8) + 1, pv)))) {
     path = 1;
     update = false;
   } else if (best > stop) {
     int64_t second = kDistMax;
-    bool check_median = false, done = false;
+    bool check_median = false, done = false, first_seen = false;
     int tmp2x = 0, tmp2y = 0;
     stop = q.stop_crit;
     // the predictor list is JM's as generated with min_mcost = the centre's
     // cost: conditional entries (temporal neighbours, window, block-type
     // predictors, me_epzs_common.c:1528, 1654, 1224) join on that value
     const int64_t gen_min = best;
-    if (best < (stop >> 1)) {
+    bool cok[4] = {true, true, true, true};
+    if (ge(stop, 2 * best + 2, sv)) {   // best < (stop >> 1)
       path = 2;
       update = GRID && !variant;   // EPZS_integer_motion_estimation keeps the value (me_epzs_int.c:118-120)
       done = true;
+    } else if (p.pred_cond) {
+      // which conditions the list holds: each is one comparison with S
+      unsigned present = 0;
+      for (int base = 0; base < q.n_pred; base += 64) {
+        const int i = base + lane;
+        const int c = i < q.n_pred ? p.pred_cond[q.pred_off + i] : 0;
+        present |= (__ballot(c == 1) ? 2u : 0u) | (__ballot(c == 2) ? 4u : 0u) | (__ballot(c == 3) ? 8u : 0u);
+      }
+      if (present & 2u) cok[1] = !ge(stop, gen_min, sv);                    // gen_min > S
+      if (present & 4u) cok[2] = !ge(stop, fdiv(gen_min - 1, 2) + 1, sv);   // gen_min > 2 S
+      if (present & 8u) cok[3] = !ge(stop, fdiv(gen_min - 1, 3) + 1, sv);   // gen_min > 3 S
     }
     // predictors, 64 at a time; JM's order is restored in the fold
     for (int base = 0; !done && base < q.n_pred; base += 64) {
       const int i = base + lane;
       bool valid = i < q.n_pred;
-      if (valid && p.pred_cond) {
-        const int c = p.pred_cond[q.pred_off + i];
-        valid = c == JMME_EPZS_PRED_ALWAYS || (c == JMME_EPZS_PRED_GT_STOP && gen_min > stop) ||
-                (c == JMME_EPZS_PRED_GT_2STOP && gen_min > 2 * stop) || (c == JMME_EPZS_PRED_GT_3STOP && gen_min > 3 * stop);
-      }
+      if (valid && p.pred_cond) valid = cok[p.pred_cond[q.pred_off + i] & 3];
       int mx = 0, my = 0;
       if (valid) {
         mx = p.preds[2 * (q.pred_off + i)];
@@ -381,22 +421,26 @@ __device__ void search_one(const EpzsParams &p, const jmme_epzs_req &q, WaveLds 
       const int px = lane < ke ? w.pk[lane][0] : 0, py = lane < ke ? w.pk[lane][1] : 0;
       wave_sync();
       const int64_t cost = eval_costs<GRID, HBD>(s, lane, ke, px, py);
-      const int64_t thr3 = (3 * stop) >> 2;
       // sub-pel grid subMB: before the 3/4 check, the ref > 0 prevSad exit that
       // returns without touching *mv (me_epzs_int.c:590-600)
       const bool pexit = GRID && variant && refi > 0 && frame;
-      // me_epzs.c:583-596 checks after every predictor; between updates the
-      // minimum is unchanged, so checking after index 0 and after each
-      // evaluated one is the same
-      if (variant && base == 0 && !(__ballot(eval) & 1ull)) {
-        if (pexit && prev * 3 < best) {
-          path = 6;
-          update = false;
-          done = true;
-        } else if (best < thr3) {
-          path = 3;
-          update = false;
-          done = true;
+      // me_epzs.c:583-596 checks after every entry of JM's list; between updates
+      // the minimum is unchanged, so checking after its first entry and after
+      // each evaluated one is the same.  JM's first entry is the first valid
+      // one (the entries whose condition failed are not in JM's list).
+      const unsigned long long vm = __ballot(valid);
+      if (variant && !first_seen && vm) {
+        first_seen = true;
+        if (!((__ballot(eval) >> __builtin_ctzll(vm)) & 1ull)) {
+          if (pexit && !ge(prev, fdiv(best - 1, 3) + 1, pv)) {          // prev * 3 < best
+            path = 6;
+            update = false;
+            done = true;
+          } else if (ge(stop, cdiv(4 * best + 4, 3), sv)) {           // best < (3 stop) >> 2
+            path = 3;
+            update = false;
+            done = true;
+          }
         }
       }
       for (int j = 0; !done && j < ke; ++j) {
@@ -416,26 +460,27 @@ __device__ void search_one(const EpzsParams &p, const jmme_epzs_req &q, WaveLds 
           second = c;
           check_median = true;
         }
-        if (variant && pexit && prev * 3 < best) {
+        if (variant && pexit && !ge(prev, fdiv(best - 1, 3) + 1, pv)) {   // prev * 3 < best
           path = 6;
           update = false;
           done = true;
-        } else if (variant && best < thr3) {
+        } else if (variant && ge(stop, cdiv(4 * best + 4, 3), sv)) {       // best < (3 stop) >> 2
           path = 3;
           update = false;
           done = true;
         }
       }
     }
-    if (GRID && !done && !variant && refi > 0 && frame && prev * 3 < best) {   // me_epzs_int.c:249-265
+    // me_epzs_int.c:249-265: prev * 3 < best
+    if (GRID && !done && !variant && refi > 0 && frame && !ge(prev, fdiv(best - 1, 3) + 1, pv)) {
       path = 7;
       update = false;
       done = true;
     }
-    if (!done && best > stop) {
+    if (!done && !ge(stop, best, sv)) {   // best > stop
       int P = primary_pattern(q.pattern);
       if (q.pattern != 0) {
-        if (best < stop + ((3 * q.medthres) >> 1)) {
+        if (ge(stop, best - ((3 * q.medthres) >> 1) + 1, sv)) {   // best < stop + 3 medthres / 2
           P = ((GRID && variant && bt == 7) || (tmpx == 0 && tmpy == 0) ||
                (abs(tmpx - s.cx) < mv_range && abs(tmpy - s.cy) < mv_range))
                   ? P_SDIAMOND : P_SQUARE;
@@ -492,15 +537,18 @@ __device__ void search_one(const EpzsParams &p, const jmme_epzs_req &q, WaveLds 
           }
         } while (pstop != 1);
 
-        if (refi > 0 && frame && (4 * prev < best || (3 * prev < best && prev <= stop))) {
+        // 4 prev < best || (3 prev < best && prev <= stop)
+        if (refi > 0 && frame &&
+            (!ge(prev, fdiv(best - 1, 4) + 1, pv) || (!ge(prev, fdiv(best - 1, 3) + 1, pv) && le2(prev, stop, pv, sv)))) {
           path = 4;
           update = false;
           break;
         }
+        // me_epzs_int.c:337-340 / 298-301: best < 2 prev; best > (3 stop) >> 1 (integer grid: best > stop)
         const bool dual_ok =
-            GRID ? check_median && !(variant && bt == 7) && (refi == 0 || best < 2 * prev) && (!variant || pslice) &&
-                       best > ((3 * stop) >> 1) && q.dual > 0   // me_epzs_int.c:337-340 / 298-301
-                 : check_median && (pslice || (!variant && bt < 5)) && best > stop && q.dual > 0;
+            GRID ? check_median && !(variant && bt == 7) && (refi == 0 || ge(prev, cdiv(best + 1, 2), pv)) &&
+                       (!variant || pslice) && !ge(stop, fdiv(2 * best - 1, 3) + 1, sv) && q.dual > 0
+                 : check_median && (pslice || (!variant && bt < 5)) && !ge(stop, best, sv) && q.dual > 0;
         if (!dual_ok) break;
         point = 0;
         pstop = 0;
@@ -517,7 +565,11 @@ __device__ void search_one(const EpzsParams &p, const jmme_epzs_req &q, WaveLds 
       }
     }
   }
-  if (update && (refi == 0 || prev > best)) prev = best;
+  bool written = false;
+  if (update && (refi == 0 || ge(prev, best + 1, pv))) {   // prev > best
+    prev = best;
+    written = true;
+  }
   const int motx = tmpx, moty = tmpy;   // JM's tmp: what every return path stores to p_motion
   if (path <= 2 || path == 6) {   // returned before touching *mv
     tmpx = s.cx;
@@ -564,6 +616,25 @@ __device__ void search_one(const EpzsParams &p, const jmme_epzs_req &q, WaveLds 
     r.motion_y = (int16_t)moty;
     r.n_visited = nv;
     *out = r;
+    const size_t t = (size_t)(out - p.out);
+    if (p.bounds) {
+      jmme_epzs_bounds b;
+      b.stop_lo = sv.lo;
+      b.stop_hi = sv.hi;
+      b.prev_lo = pv.lo;
+      b.prev_hi = pv.hi;
+      b.prev_written = written ? 1 : 0;
+      b.n_visited = nv;
+      p.bounds[t] = b;
+    }
+    if (p.int_out) {   // the integer result as jmme_subpel_refine_async's d_int reads it
+      jmme_block_res br;
+      br.mv_x = (int16_t)tmpx;
+      br.mv_y = (int16_t)tmpy;
+      br.reserved = 0;
+      br.cost = best;
+      p.int_out[t] = br;
+    }
   }
   wave_sync();
 }

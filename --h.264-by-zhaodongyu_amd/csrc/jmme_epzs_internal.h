@@ -31,6 +31,11 @@ struct EpzsParams {
   const uint8_t *pred_cond;
   int16_t *visited;
   int max_visited;
+  // speculative batches (jmme_epzs_speculate): each search's validity
+  // intervals, and its result as a jmme_block_res for the chained sub-pel
+  // refinement (null: not written)
+  jmme_epzs_bounds *bounds;
+  jmme_block_res *int_out;
 };
 
 size_t epzs_map_words(bool grid, int max_qpel);

@@ -55,6 +55,8 @@ EPZS_REQ = np.dtype([("pos_x", "<i2"), ("pos_y", "<i2"), ("bsx", "<i2"), ("bsy",
 EPZS_RES = np.dtype([("mv_x", "<i2"), ("mv_y", "<i2"), ("path", "<i4"), ("cost", "<i8"), ("prev_sad", "<i8"),
                      ("motion_x", "<i2"), ("motion_y", "<i2"), ("n_visited", "<i4")])
 EPZS_FRAME, EPZS_PSLICE = 1, 2
+EPZS_BOUNDS = np.dtype([("stop_lo", "<i8"), ("stop_hi", "<i8"), ("prev_lo", "<i8"), ("prev_hi", "<i8"),
+                        ("prev_written", "<i4"), ("n_visited", "<i4")])
 SUBPEL_REQ = np.dtype([("pos_x", "<i2"), ("pos_y", "<i2"), ("blocktype", "<i2"), ("ref_slot", "<i2"),
                        ("pred_x", "<i2"), ("pred_y", "<i2"), ("mv_x", "<i2"), ("mv_y", "<i2"),
                        ("lambda_h", "<i4"), ("lambda_q", "<i4"), ("min_mcost", "<i8"), ("subthres", "<i8"),
@@ -144,6 +146,7 @@ def lib() -> ctypes.CDLL:
         "jmme_epzs_search": (I, [P, P, I, P, I, P, I, P]),
         "jmme_epzs_search_async": (I, [P, P, I, P, P, P, P]),
         "jmme_epzs_search_ex": (I, [P, P, I, P, P, I, P, I, P, P, I]),
+        "jmme_epzs_speculate": (I, [P, P, I, P, P, I, P, I, P, P, P, I, P, P]),
         "jmme_fractal_encode_mbs_async": (I, [P, P, P, I, P, I, I, I, I, D, D, P, P]),
         "jmme_fractal_encode_mb_rows_async": (I, [P, P, P, I, P, I, I, I, I, I, I, D, D, P, P]),
         "jmme_fractal_decode_mbs": (I, [P, P, P, I, I, I, I, I, P]),

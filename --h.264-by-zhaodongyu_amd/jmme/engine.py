@@ -251,6 +251,28 @@ class MotionEstimator:
                                      ptr(out)))
         return out
 
+    def epzs_speculate(self, req: np.ndarray, preds: np.ndarray, cond: np.ndarray | None = None,
+                       stale: np.ndarray | None = None, max_visited: int = 64, sp_req: np.ndarray | None = None):
+        """jmme_epzs_speculate: the searches with their predictor conditions, validity
+        intervals and stamped cells, and (sp_req) a chained EPZS sub-pel refinement
+        of each result -> (EPZS_RES[n], EPZS_BOUNDS[n], visited int16 [n, max_visited, 2],
+        BLOCK_RES[n] or None)."""
+        req = np.ascontiguousarray(req, _lib.EPZS_REQ)
+        preds = np.ascontiguousarray(preds, np.int16).reshape(-1, 2)
+        stale = np.zeros((0, 2), np.int16) if stale is None else np.ascontiguousarray(stale, np.int16).reshape(-1, 2)
+        cnd = None if cond is None else np.ascontiguousarray(cond, np.uint8)
+        n = len(req)
+        out = np.zeros(n, _lib.EPZS_RES)
+        bnd = np.zeros(n, _lib.EPZS_BOUNDS)
+        vis = np.zeros((n, max_visited, 2), np.int16)
+        spq = None if sp_req is None else np.ascontiguousarray(sp_req, _lib.SUBPEL_REQ)
+        spo = None if sp_req is None else np.zeros(n, _lib.BLOCK_RES)
+        check(lib().jmme_epzs_speculate(self._ctx, ptr(req), n, ptr(preds), None if cnd is None else ptr(cnd),
+                                        len(preds), ptr(stale), len(stale), ptr(out), ptr(bnd), ptr(vis),
+                                        int(max_visited), None if spq is None else ptr(spq),
+                                        None if spo is None else ptr(spo)))
+        return out, bnd, vis, spo
+
     def epzs_search_async(self, d_req: int, n: int, d_preds: int, d_stale: int, d_out: int, stream: int = 0) -> None:
         check(lib().jmme_epzs_search_async(self._ctx, d_req, int(n), d_preds, d_stale, d_out, stream))
 

@@ -389,6 +389,22 @@ int jmme_epzs_search_ex(jmme_ctx *ctx, const jmme_epzs_req *req, int n, const in
                         const uint8_t *pred_cond, int n_preds, const int16_t *stale, int n_stale,
                         jmme_epzs_res *out, int16_t *visited, int max_visited);
 
+/* ---- Speculative EPZS batches (the drop-in's throughput form) -------------
+ * A search reads the stop criterion (EPZSDetermineStopCriterion,
+ * me_epzs_common.c:1764) and *prevSad only through comparisons, each monotone
+ * in that value (JM/lencod/src/me_epzs.c:54-407, me_epzs_int.c:41-782), so a
+ * search run with guessed values returns the intervals within which its whole
+ * execution -- (mv, cost, the cells it stamps, p_motion, whether it writes
+ * *prevSad) -- is unchanged.  The drop-in serves a cached answer to JM's call
+ * when the call's other inputs equal the guessed ones and its real stop
+ * criterion and prevSad lie inside. */
+typedef struct jmme_epzs_bounds {
+  int64_t stop_lo, stop_hi;    /* the result holds for every stop criterion in [stop_lo, stop_hi] */
+  int64_t prev_lo, prev_hi;    /* ... and every *prevSad on entry in [prev_lo, prev_hi] */
+  int32_t prev_written;        /* 1: the search stores *prevSad = cost; 0: it leaves *prevSad alone */
+  int32_t n_visited;           /* = jmme_epzs_res.n_visited */
+} jmme_epzs_bounds;            /* 40 bytes */
+
 /* ---- Quarter-pel reference planes and sub-pel refinement -----------------
  * SURVEY.md §8(f) rank 1.
  *
@@ -450,6 +466,19 @@ typedef struct jmme_subpel_req {
 
 /* host arrays, synchronous; out[i] = (mv, cost) SubPelME returns */
 int jmme_subpel_refine(jmme_ctx *ctx, const jmme_subpel_req *req, int n, jmme_block_res *out);
+
+/* EPZS speculative batch with its chained sub-pel refinements (jmme_epzs_bounds above). */
+/* One launch over n searches, as jmme_epzs_search_ex (host arrays, one sync),
+ * plus bounds[i] and, when sp_req is not NULL, one sub-pel refinement per search
+ * chained on the device: sp_req[i] (blocktype 0: none; its mv and min_mcost are
+ * ignored) refines search i's result -- mv = its mv, min_mcost = start_hp ? its
+ * cost : DISTBLK_MAX, as BlockMotionSearch hands SubPelME (mv_search.c:960-976)
+ * -- into sp_out[i].  A search that stamps more than max_visited cells is not
+ * an error here: only max_visited pairs are written and n_visited tells. */
+int jmme_epzs_speculate(jmme_ctx *ctx, const jmme_epzs_req *req, int n, const int16_t *preds,
+                        const uint8_t *pred_cond, int n_preds, const int16_t *stale, int n_stale,
+                        jmme_epzs_res *out, jmme_epzs_bounds *bounds, int16_t *visited, int max_visited,
+                        const jmme_subpel_req *sp_req, jmme_block_res *sp_out);
 /* device arrays on `stream`.  d_int (may be NULL): integer-pel results aligned
  * with the requests (e.g. the jmme_search_mbs_async output with requests in
  * unit x slot order); when given, entry i takes mv = d_int[i].mv and

@@ -1223,6 +1223,365 @@ static distblk real_epzs(int variant, Macroblock *currMB, MotionVector *pred_mv,
   }
 }
 
+/* ---- speculative EPZS batches ---------------------------------------------
+ * JM's EPZS calls depend on each other (the predictor list holds the final
+ * vectors of the neighbours and of the macroblock's other block types, the stop
+ * criterion the neighbours' SADs), so one call cannot wait for a GPU round trip
+ * each.  Instead a batch searches, in one launch, every partition of the next
+ * macroblocks under the inputs the same partition had in already-searched
+ * macroblocks (left of the batch, and the row above), and JM's real call is
+ * answered from the batch when its inputs equal a guess:
+ *   - block, centre, predictor, lambda, range, variant, pattern, thresholds and
+ *     the predictor list with its conditions: equal;
+ *   - the stop criterion and *prevSad: inside the intervals the search reports
+ *     (jmme_epzs_bounds: each comparison with them is monotone, so inside the
+ *     intervals the search runs exactly as it ran);
+ *   - EPZSMap: the guess ran with no pre-stamped cells; JM's cells that already
+ *     hold this BlkCount must not include any the search evaluated (it would
+ *     have skipped them), which the stamped-cell list it returns tells.
+ * Every answer is JM's exactly.  The EPZS sub-pel refinement of each guess is
+ * chained on the device in the same launch and answered the same way.  A call
+ * no guess fits is searched alone (with its chained refinement), or starts the
+ * next batch when it lies past the current one.  JMME_EPZS_SPECULATE=0: one
+ * call per search. */
+#define EP_MAXP 128                /* predictors of a list the cache keeps (longer lists: one call each) */
+#define EP_MAXV 64                 /* stamped cells kept per cached answer */
+#define EP_WAYS 4                  /* guesses per (macroblock, partition, reference) */
+#define EP_REFS 4                  /* references speculated (list 0) */
+#define EP_BATCH_MAX 512
+
+typedef struct ep_in {             /* one search's inputs */
+  jmme_epzs_req q;                 /* pred_off / n_stale / stale_off / reserved: not compared */
+  int32_t pred[EP_MAXP];           /* (x, y) pairs as int16 */
+  uint8_t cond[EP_MAXP];
+  int32_t mb;                      /* the macroblock (seen ring: which one the entry holds) */
+  uint32_t gen;                    /* g_slot_gen of its reference when stored (0: empty) */
+} ep_in;
+
+typedef struct ep_ans {            /* a searched guess: inputs, result, validity, chained refinement */
+  ep_in in;
+  jmme_epzs_res res;
+  jmme_epzs_bounds bnd;
+  int16_t vis[EP_MAXV][2];
+  jmme_subpel_req spq;             /* the refinement's inputs (mv / min_mcost from res); blocktype 0: none */
+  jmme_block_res sp_res;
+} ep_ans;
+
+typedef struct ep_spp {            /* EPZS sub-pel parameters of this encode, from JM's last real call */
+  int valid, lam_h, lam_q, metric_h, metric_q, start_hp, start_qp, pos2, pos4, check0, t8;
+} ep_spp;
+
+static int g_ep_spec = -1, g_ep_batch = 64, g_ep_ring_n = 0;
+static ep_in *g_ep_seen = NULL;    /* [ring of macroblocks][41 slots][EP_REFS]: the inputs JM really searched with */
+static ep_ans *g_ep_ans = NULL;    /* the current batch's searched guesses */
+static int *g_ep_idx = NULL;       /* [batch macroblock][41][EP_REFS][EP_WAYS] -> g_ep_ans index (-1: none) */
+static int g_ep_cap = 0, g_ep_n = 0, g_ep_mb0 = 0, g_ep_mb1 = 0;
+static unsigned g_ep_gen = 0;      /* g_slot_gen the batch belongs to (0: none) */
+static const ep_ans *g_ep_served = NULL;   /* the answer the last EPZS call was served from (its refinement) */
+static ep_spp g_ep_spp;
+static jmme_epzs_req *g_ep_q = NULL;
+static int16_t *g_ep_ppool = NULL;
+static uint8_t *g_ep_cpool = NULL;
+static jmme_epzs_res *g_ep_res = NULL;
+static jmme_epzs_bounds *g_ep_bnd = NULL;
+static int16_t *g_ep_vbuf = NULL;
+static jmme_subpel_req *g_ep_spq = NULL;
+static jmme_block_res *g_ep_spo = NULL;
+static int g_ep_pcap = 0;
+static long long g_ep_hits = 0, g_ep_batches = 0, g_ep_singles = 0, g_ep_guesses = 0, g_ep_direct = 0;
+static long long g_ep_fail_bounds = 0, g_ep_fail_stale = 0, g_ep_fail_inputs = 0, g_ep_sp_hits = 0;
+static double g_t_ep_build = 0;
+
+static int ep_speculating(Macroblock *currMB, int cur_list, int ref, int n_pred)
+{
+  if (g_ep_spec < 0) {
+    const char *e = getenv("JMME_EPZS_SPECULATE"), *b = getenv("JMME_EPZS_BATCH");
+    g_ep_spec = !(e && e[0] == '0');
+    if (b && atoi(b) > 0) g_ep_batch = imin(atoi(b), EP_BATCH_MAX);
+  }
+  if (!g_n_mb) {
+    g_mbs_x = currMB->p_Vid->width / 16;
+    g_n_mb = g_mbs_x * (currMB->p_Vid->height / 16);
+  }
+  if (!g_slot_bt[0]) slot_geometry();
+  if (!g_ep_spec || cur_list != 0 || ref >= EP_REFS || n_pred > EP_MAXP ||
+      currMB->p_Slice->slice_type != P_SLICE || currMB->p_Slice->structure != FRAME) {
+    if (g_ep_spec) ++g_ep_direct;
+    return 0;
+  }
+  return 1;
+}
+
+static int ep_slot_of(const jmme_epzs_req *q)
+{
+  return jmme_slot(q->blocktype, (q->pos_x & 15) >> 2, (q->pos_y & 15) >> 2);
+}
+
+/* equal inputs, the stop criterion, prevSad and the pre-stamped cells aside */
+static int ep_same(const ep_in *a, const jmme_epzs_req *q, const int16_t *pred, const uint8_t *cond)
+{
+  const jmme_epzs_req *b = &a->q;
+  return b->pos_x == q->pos_x && b->pos_y == q->pos_y && b->blocktype == q->blocktype && b->ref_idx == q->ref_idx &&
+         b->pred_x == q->pred_x && b->pred_y == q->pred_y && b->center_x == q->center_x &&
+         b->center_y == q->center_y && b->max_x == q->max_x && b->max_y == q->max_y && b->lambda == q->lambda &&
+         b->variant == q->variant && b->flags == q->flags && b->pattern == q->pattern && b->dual == q->dual &&
+         b->medthres == q->medthres && b->ref_slot == q->ref_slot && b->n_pred == q->n_pred &&
+         b->bsx == q->bsx && b->bsy == q->bsy &&
+         !memcmp(a->pred, pred, (size_t)q->n_pred * 4) && !memcmp(a->cond, cond, (size_t)q->n_pred);
+}
+
+/* the same search at another block position (guess -> guess dedup) */
+static int ep_same_moved(const ep_in *a, const ep_in *b)
+{
+  jmme_epzs_req q = b->q;
+  q.pos_x = a->q.pos_x;
+  q.pos_y = a->q.pos_y;
+  return ep_same(a, &q, (const int16_t *)b->pred, b->cond);
+}
+
+static void ep_fill_in(ep_in *e, const jmme_epzs_req *q, const int16_t *pred, const uint8_t *cond, int mb, unsigned gen)
+{
+  e->q = *q;
+  e->q.pred_off = 0;
+  e->q.n_stale = 0;
+  e->q.stale_off = 0;
+  e->q.reserved = 0;
+  memcpy(e->pred, pred, (size_t)q->n_pred * 4);
+  memcpy(e->cond, cond, (size_t)q->n_pred);
+  e->mb = mb;
+  e->gen = gen;
+}
+
+static ep_in *ep_seen_at(int mb, int slot, int ref)
+{
+  return &g_ep_seen[((size_t)(mb % g_ep_ring_n) * JMME_NSLOT + slot) * EP_REFS + ref];
+}
+
+/* the cached answer for this call, or NULL */
+static const ep_ans *ep_lookup(Macroblock *currMB, MEBlock *mv_block, const jmme_epzs_req *q, const int16_t *pred,
+                               const uint8_t *cond, const int16_t *stale, int n_stale)
+{
+  const int mb = (mv_block->pos_y >> 4) * g_mbs_x + (mv_block->pos_x >> 4), slot = ep_slot_of(q), ref = q->ref_idx;
+  const unsigned gen = g_slot_gen[0][ref];
+  int w, i, j;
+  (void)currMB;
+  if (!g_ep_seen || g_ep_ring_n != g_mbs_x + 4) {
+    free(g_ep_seen);
+    g_ep_ring_n = g_mbs_x + 4;
+    g_ep_seen = (ep_in *)calloc((size_t)g_ep_ring_n * JMME_NSLOT * EP_REFS, sizeof(ep_in));
+    if (!g_ep_seen) error("jm_gpu_me: out of memory", 500);
+  }
+  ep_fill_in(ep_seen_at(mb, slot, ref), q, pred, cond, mb, gen);
+  if (g_ep_gen != gen || mb < g_ep_mb0 || mb >= g_ep_mb1) return NULL;
+  for (w = 0; w < EP_WAYS; w++) {
+    const int k = g_ep_idx[(((size_t)(mb - g_ep_mb0) * JMME_NSLOT + slot) * EP_REFS + ref) * EP_WAYS + w];
+    const ep_ans *a;
+    if (k < 0) break;
+    a = &g_ep_ans[k];
+    if (!ep_same(&a->in, q, pred, cond)) continue;
+    if (q->stop_crit < a->bnd.stop_lo || q->stop_crit > a->bnd.stop_hi || q->prev_sad < a->bnd.prev_lo ||
+        q->prev_sad > a->bnd.prev_hi || a->res.n_visited > EP_MAXV) {
+      ++g_ep_fail_bounds;
+      continue;
+    }
+    for (i = 0; i < n_stale; i++) {   /* a cell JM already holds at this BlkCount: did the guess evaluate it? */
+      if (!stale[2 * i] && !stale[2 * i + 1]) continue;   /* the centre is searched first whatever the map holds */
+      for (j = 0; j < a->res.n_visited; j++)
+        if (a->vis[j][0] == stale[2 * i] && a->vis[j][1] == stale[2 * i + 1]) break;
+      if (j < a->res.n_visited) break;
+    }
+    if (i < n_stale) {
+      ++g_ep_fail_stale;
+      continue;
+    }
+    ++g_ep_hits;
+    return a;
+  }
+  ++g_ep_fail_inputs;
+  return NULL;
+}
+
+static void ep_grow(int n, int n_pred)
+{
+  if (n > g_ep_cap) {
+    g_ep_cap = imax(n, 2 * g_ep_cap);
+    free(g_ep_ans); free(g_ep_q); free(g_ep_res); free(g_ep_bnd); free(g_ep_vbuf); free(g_ep_spq); free(g_ep_spo);
+    g_ep_ans = (ep_ans *)malloc((size_t)g_ep_cap * sizeof(ep_ans));
+    g_ep_q = (jmme_epzs_req *)malloc((size_t)g_ep_cap * sizeof(jmme_epzs_req));
+    g_ep_res = (jmme_epzs_res *)malloc((size_t)g_ep_cap * sizeof(jmme_epzs_res));
+    g_ep_bnd = (jmme_epzs_bounds *)malloc((size_t)g_ep_cap * sizeof(jmme_epzs_bounds));
+    g_ep_vbuf = (int16_t *)malloc((size_t)g_ep_cap * EP_MAXV * 4);
+    g_ep_spq = (jmme_subpel_req *)malloc((size_t)g_ep_cap * sizeof(jmme_subpel_req));
+    g_ep_spo = (jmme_block_res *)malloc((size_t)g_ep_cap * sizeof(jmme_block_res));
+    if (!g_ep_ans || !g_ep_q || !g_ep_res || !g_ep_bnd || !g_ep_vbuf || !g_ep_spq || !g_ep_spo)
+      error("jm_gpu_me: out of memory", 500);
+  }
+  if (n_pred > g_ep_pcap) {
+    g_ep_pcap = imax(n_pred, 2 * g_ep_pcap);
+    free(g_ep_ppool); free(g_ep_cpool);
+    g_ep_ppool = (int16_t *)malloc((size_t)g_ep_pcap * 4);
+    g_ep_cpool = (uint8_t *)malloc((size_t)g_ep_pcap);
+    if (!g_ep_ppool || !g_ep_cpool) error("jm_gpu_me: out of memory", 500);
+  }
+}
+
+/* request k of the batch: the search with inputs e at its own block; its refinement */
+static int g_ep_np = 0;
+static void ep_add(int k, const ep_in *e, int pos_x, int pos_y, EPZSParameters *p_EPZS)
+{
+  jmme_epzs_req *q = &g_ep_q[k];
+  jmme_subpel_req *sp = &g_ep_spq[k];
+  *q = e->q;
+  q->pos_x = (int16_t)pos_x;
+  q->pos_y = (int16_t)pos_y;
+  q->pred_off = g_ep_np;
+  q->n_stale = 0;
+  q->stale_off = 0;
+  memcpy(g_ep_ppool + 2 * (size_t)g_ep_np, e->pred, (size_t)e->q.n_pred * 4);
+  memcpy(g_ep_cpool + g_ep_np, e->cond, (size_t)e->q.n_pred);
+  g_ep_np += e->q.n_pred;
+  memset(sp, 0, sizeof *sp);
+  if (g_ep_spp.valid) {   /* EPZS_sub_pel_motion_estimation of the result (mv_search.c:966-976) */
+    sp->pos_x = (int16_t)pos_x;
+    sp->pos_y = (int16_t)pos_y;
+    sp->blocktype = q->blocktype;
+    sp->ref_slot = (int16_t)q->ref_slot;
+    sp->pred_x = q->pred_x;
+    sp->pred_y = q->pred_y;
+    sp->lambda_h = g_ep_spp.lam_h;
+    sp->lambda_q = g_ep_spp.lam_q;
+    sp->subthres = (int64_t)p_EPZS->subthres[q->blocktype];
+    sp->variant = 1;
+    sp->flags = (uint8_t)((g_ep_spp.t8 && q->blocktype <= 4 ? JMME_SP_TEST8x8 : 0) | (g_ep_spp.check0 ? JMME_SP_CHECK0 : 0));
+    sp->metric_h = (uint8_t)g_ep_spp.metric_h;
+    sp->metric_q = (uint8_t)g_ep_spp.metric_q;
+    sp->start_hp = (uint8_t)g_ep_spp.start_hp;
+    sp->start_qp = (uint8_t)g_ep_spp.start_qp;
+    sp->search_pos2 = (uint8_t)g_ep_spp.pos2;
+    sp->search_pos4 = (uint8_t)g_ep_spp.pos4;
+  }
+}
+
+/* search requests 0..n-1 (the real call first, with its pre-stamped cells) and keep the answers */
+static void ep_run(int n, const int16_t *stale, int n_stale, unsigned gen)
+{
+  int k;
+  g_ep_q[0].n_stale = n_stale;
+  for (k = 0; k < n; k++) g_ep_spo[k].mv_x = g_ep_spo[k].mv_y = 0, g_ep_spo[k].cost = 0, g_ep_spo[k].reserved = 0;
+  if (jmme_epzs_speculate(g_me, g_ep_q, n, g_ep_ppool, g_ep_cpool, g_ep_np, stale, n_stale, g_ep_res, g_ep_bnd,
+                          g_ep_vbuf, EP_MAXV, g_ep_spq, g_ep_spo))
+    fail_jm("jmme_epzs_speculate");
+  for (k = 0; k < n; k++) {
+    ep_ans *a = &g_ep_ans[k];
+    const int16_t *pp = g_ep_ppool + 2 * (size_t)g_ep_q[k].pred_off;
+    ep_fill_in(&a->in, &g_ep_q[k], pp, g_ep_cpool + g_ep_q[k].pred_off, -1, gen);
+    a->res = g_ep_res[k];
+    a->bnd = g_ep_bnd[k];
+    memcpy(a->vis, g_ep_vbuf + 2 * (size_t)EP_MAXV * k, (size_t)imin(a->res.n_visited, EP_MAXV) * 4);
+    a->spq = g_ep_spq[k];
+    if (a->spq.blocktype) {   /* what the chained refinement was handed */
+      a->spq.mv_x = a->res.mv_x;
+      a->spq.mv_y = a->res.mv_y;
+      a->spq.min_mcost = a->spq.start_hp ? a->res.cost : JMME_DISTBLK_MAX;
+    }
+    a->sp_res = g_ep_spo[k];
+  }
+}
+
+/* no guess fits: search the call alone, or start the next batch when it lies past the current one */
+static const ep_ans *ep_miss(Macroblock *currMB, MEBlock *mv_block, const jmme_epzs_req *q, const int16_t *pred,
+                             const uint8_t *cond, const int16_t *stale, int n_stale)
+{
+  EPZSParameters *p_EPZS = currMB->p_Slice->p_EPZS;
+  const int mb = (mv_block->pos_y >> 4) * g_mbs_x + (mv_block->pos_x >> 4), ref = q->ref_idx;
+  const unsigned gen = g_slot_gen[0][ref];
+  const int inside = g_ep_gen == gen && mb >= g_ep_mb0 && mb < g_ep_mb1;
+  ep_in want;
+  int n = 1, x, t, r, w, nmb;
+  double t0 = now_us();
+  ep_fill_in(&want, q, pred, cond, mb, gen);
+  if (inside) {   /* a guess failed: this call alone; the batch's other guesses stand */
+    ep_grow(1, q->n_pred);
+    g_ep_np = 0;
+    ep_add(0, &want, q->pos_x, q->pos_y, p_EPZS);
+    g_t_ep_build += now_us() - t0;
+    ep_run(1, stale, n_stale, gen);
+    ++g_ep_singles;
+    /* (request 0 of the batch was a call already served: the batch's other guesses stand) */
+    return &g_ep_ans[0];
+  }
+  /* a new batch from this macroblock: the call itself (way 0 of its slot), and
+   * for every partition of the next macroblocks the inputs the same partition
+   * had left of the batch and in the row above (distinct ones only) */
+  nmb = imin(g_ep_batch, g_n_mb - mb);
+  {
+    int need = 1 + nmb * JMME_NSLOT * EP_REFS * (EP_WAYS - 1);
+    ep_grow(need + 1, (need + 1) * EP_MAXP);
+    free(g_ep_idx);
+    g_ep_idx = (int *)malloc((size_t)nmb * JMME_NSLOT * EP_REFS * EP_WAYS * sizeof(int));
+    if (!g_ep_idx) error("jm_gpu_me: out of memory", 500);
+    memset(g_ep_idx, 0xff, (size_t)nmb * JMME_NSLOT * EP_REFS * EP_WAYS * sizeof(int));
+  }
+  g_ep_np = 0;
+  ep_add(0, &want, q->pos_x, q->pos_y, p_EPZS);
+  g_ep_idx[(((size_t)0 * JMME_NSLOT + ep_slot_of(q)) * EP_REFS + ref) * EP_WAYS] = 0;
+  for (x = mb; x < mb + nmb; x++) {
+    const int col = x % g_mbs_x;
+    int src[4], ns = 0, i;
+    if (mb % g_mbs_x) src[ns++] = mb - 1;                         /* left of the batch, this row */
+    if (x - g_mbs_x >= 0 && x - g_mbs_x < mb) src[ns++] = x - g_mbs_x;
+    if (col + 1 < g_mbs_x && x - g_mbs_x + 1 >= 0 && x - g_mbs_x + 1 < mb) src[ns++] = x - g_mbs_x + 1;
+    if (col > 0 && x - g_mbs_x - 1 >= 0 && x - g_mbs_x - 1 < mb) src[ns++] = x - g_mbs_x - 1;
+    for (t = 0; t < JMME_NSLOT; t++) {
+      const int px = col * 16 + g_slot_bx[t], py = (x / g_mbs_x) * 16 + g_slot_by[t];
+      for (r = 0; r < EP_REFS; r++) {
+        int *idx = &g_ep_idx[(((size_t)(x - mb) * JMME_NSLOT + t) * EP_REFS + r) * EP_WAYS];
+        w = 0;
+        while (w < EP_WAYS && idx[w] >= 0) w++;
+        for (i = 0; i < ns && w < EP_WAYS; i++) {
+          const ep_in *e = ep_seen_at(src[i], t, r);
+          int d;
+          if (e->mb != src[i] || e->gen != g_slot_gen[0][r] || !g_slot_gen[0][r]) continue;
+          for (d = 0; d < w; d++) {   /* a guess already made for this partition */
+            const ep_in *o = idx[d] == 0 ? &want : &g_ep_ans[idx[d]].in;
+            if (ep_same_moved(o, e) && o->q.pos_x == px && o->q.pos_y == py) break;
+          }
+          if (d < w) continue;
+          ep_add(n, e, px, py, p_EPZS);
+          g_ep_ans[n].in.q = g_ep_q[n];   /* (dedup reads the guess's inputs before the run) */
+          g_ep_ans[n].in.q.pos_x = (int16_t)px;
+          g_ep_ans[n].in.q.pos_y = (int16_t)py;
+          memcpy(g_ep_ans[n].in.pred, e->pred, (size_t)e->q.n_pred * 4);
+          memcpy(g_ep_ans[n].in.cond, e->cond, (size_t)e->q.n_pred);
+          idx[w++] = n++;
+        }
+      }
+    }
+  }
+  g_t_ep_build += now_us() - t0;
+  ep_run(n, stale, n_stale, gen);
+  g_ep_n = n;
+  g_ep_mb0 = mb;
+  g_ep_mb1 = mb + nmb;
+  g_ep_gen = gen;
+  g_ep_guesses += n - 1;
+  ++g_ep_batches;
+  return &g_ep_ans[0];
+}
+
+/* JM's EPZSMap after the search: every cell it stamped gets BlkCount cnt */
+static void ep_apply(EPZSParameters *p_EPZS, const int16_t *vis, int n_vis, uint16 cnt, int side, int max_x, int max_y)
+{
+  int i;
+  for (i = 0; i < n_vis; i++) {
+    int r = max_y + vis[2 * i + 1], col = max_x + vis[2 * i];
+    if (p_EPZS->EPZSMap[r][col] != cnt) {
+      p_EPZS->EPZSMap[r][col] = cnt;
+      if (!g_ring_foreign) cell_push(&g_ring[cnt], (uint32_t)(r * side + col));
+    }
+  }
+}
+
 static distblk epzs_gpu(int variant, Macroblock *currMB, MotionVector *pred_mv, MEBlock *mv_block, distblk min_mcost,
                         int lambda_factor)
 {
@@ -1325,25 +1684,33 @@ static distblk epzs_gpu(int variant, Macroblock *currMB, MotionVector *pred_mv, 
   q.ref_slot = list * 32 + ref;
   q.prev_sad = (int64_t)*prevSad;
   q.medthres = (int64_t)p_EPZS->medthres[bt];
-  /* every cell a search can stamp lies in its window */
-  max_vis = grid ? (2 * max_x + 1) * (2 * max_y + 1) : ((max_x >> 1) + 1) * ((max_y >> 1) + 1);
-  grow16(&g_ep_vis, &g_ep_vis_cap, max_vis);
-  t1 = now_us();
-  if (jmme_epzs_search_ex(g_me, &q, 1, g_ep_pred, g_ep_cond, n_pred, g_ep_stale, n_stale, &res, g_ep_vis, max_vis))
-    fail_jm("jmme_epzs_search_ex");
-  g_t_epzs_gpu += now_us() - t1;
+
+  if (ep_speculating(currMB, cur_list, ref, n_pred)) {
+    /* the speculative path: a cached answer whose inputs are this call's, or a batch */
+    const ep_ans *a = ep_lookup(currMB, mv_block, &q, g_ep_pred, g_ep_cond, g_ep_stale, n_stale);
+    t1 = now_us();
+    if (!a) a = ep_miss(currMB, mv_block, &q, g_ep_pred, g_ep_cond, g_ep_stale, n_stale);
+    g_t_epzs_gpu += now_us() - t1;
+    res = a->res;
+    ep_apply(p_EPZS, &a->vis[0][0], res.n_visited, cnt, side, max_x, max_y);
+    g_ep_served = a;
+    if (a->bnd.prev_written) *prevSad = (distblk)res.cost;
+  } else {
+    /* one search per call: its whole window can be stamped */
+    max_vis = grid ? (2 * max_x + 1) * (2 * max_y + 1) : ((max_x >> 1) + 1) * ((max_y >> 1) + 1);
+    grow16(&g_ep_vis, &g_ep_vis_cap, max_vis);
+    t1 = now_us();
+    if (jmme_epzs_search_ex(g_me, &q, 1, g_ep_pred, g_ep_cond, n_pred, g_ep_stale, n_stale, &res, g_ep_vis, max_vis))
+      fail_jm("jmme_epzs_search_ex");
+    g_t_epzs_gpu += now_us() - t1;
+    ep_apply(p_EPZS, g_ep_vis, res.n_visited, cnt, side, max_x, max_y);
+    g_ep_served = NULL;
+    *prevSad = (distblk)res.prev_sad;
+  }
 
   /* JM's side effects */
-  for (i = 0; i < res.n_visited; i++) {
-    int r = max_y + g_ep_vis[2 * i + 1], col = max_x + g_ep_vis[2 * i];
-    if (p_EPZS->EPZSMap[r][col] != cnt) {
-      p_EPZS->EPZSMap[r][col] = cnt;
-      if (!g_ring_foreign) cell_push(&g_ring[cnt], (uint32_t)(r * side + col));
-    }
-  }
   p_EPZS->BlkCount = cnt;
   g_ring_count = cnt;
-  *prevSad = (distblk)res.prev_sad;
   if (p_Inp->EPZSSpatialMem) {
     MotionVector *m = &p_EPZS->p_motion[cur_list][ref][bt - 1][mv_block->block_y][mv_block->pos_x2];
     m->mv_x = res.motion_x;
@@ -1421,7 +1788,26 @@ distblk __wrap_EPZS_sub_pel_motion_estimation(Macroblock *currMB, MotionVector *
   q.start_qp = (uint8_t)(p_Vid->start_me_refinement_qp != 0);
   q.search_pos2 = (uint8_t)mv_block->search_pos2;
   q.search_pos4 = (uint8_t)mv_block->search_pos4;
-  if (jmme_subpel_refine(g_me, &q, 1, &r)) fail_jm("jmme_subpel_refine");
+  /* the parameters the next batches chain their refinements with */
+  g_ep_spp.lam_h = q.lambda_h;
+  g_ep_spp.lam_q = q.lambda_q;
+  g_ep_spp.metric_h = q.metric_h;
+  g_ep_spp.metric_q = q.metric_q;
+  g_ep_spp.start_hp = q.start_hp;
+  g_ep_spp.start_qp = q.start_qp;
+  g_ep_spp.pos2 = q.search_pos2;
+  g_ep_spp.pos4 = q.search_pos4;
+  g_ep_spp.check0 = (q.flags & JMME_SP_CHECK0) != 0;
+  g_ep_spp.t8 = currMB->p_Inp->Transform8x8Mode != 0;
+  g_ep_spp.valid = 1;
+  if (g_ep_served && g_ep_served->spq.blocktype && !memcmp(&g_ep_served->spq, &q, sizeof q)) {
+    /* refined on the device right after the integer search this call follows */
+    r = g_ep_served->sp_res;
+    ++g_ep_sp_hits;
+  } else if (jmme_subpel_refine(g_me, &q, 1, &r)) {
+    fail_jm("jmme_subpel_refine");
+  }
+  g_ep_served = NULL;
   mv_block->mv[list].mv_x = r.mv_x;
   mv_block->mv[list].mv_y = r.mv_y;
   return (distblk)r.cost;
@@ -1453,14 +1839,20 @@ static void report(void)
                       "%lld chain-only calls (%lld fell back to a batch)\n",
               g_chain_sent, g_chain_steps, g_chain_hits, g_chain_head_bad, g_chain_calls, g_chain_call_fail);
     if (g_epzs_calls || g_epzs_cpu)
-      fprintf(stderr, "jm_gpu_me: %lld EPZS searches on the GPU (libjmme), one call each; %lld on the CPU; "
+      fprintf(stderr, "jm_gpu_me: %lld EPZS searches on the GPU (libjmme); %lld on the CPU; "
                       "%lld predictors, %lld pre-stamped map cells, %lld switches to window scans; "
-                      "%.1f ms in the EPZS wrapper, %.1f ms in jmme_epzs_search_ex\n",
+                      "%.1f ms in the EPZS wrapper, %.1f ms in the engine\n",
               g_epzs_calls, g_epzs_cpu, g_epzs_preds, g_epzs_stale, g_epzs_foreign, g_t_epzs * 1e-3,
               g_t_epzs_gpu * 1e-3);
+    if (g_epzs_calls && g_ep_spec > 0)
+      fprintf(stderr, "jm_gpu_me: EPZS speculation: %lld searches answered from %lld batches (%lld guesses), "
+                      "%lld searched alone; %lld not speculated; guesses refused: %lld inputs, %lld bounds, "
+                      "%lld map cells; %.1f ms building batches\n",
+              g_ep_hits, g_ep_batches, g_ep_guesses, g_ep_singles, g_ep_direct, g_ep_fail_inputs, g_ep_fail_bounds,
+              g_ep_fail_stale, g_t_ep_build * 1e-3);
     if (g_epzs_sp_calls || g_epzs_sp_cpu)
-      fprintf(stderr, "jm_gpu_me: %lld EPZS sub-pel refinements on the GPU, %lld on the CPU\n", g_epzs_sp_calls,
-              g_epzs_sp_cpu);
+      fprintf(stderr, "jm_gpu_me: %lld EPZS sub-pel refinements on the GPU (%lld chained in the search's launch), "
+                      "%lld on the CPU\n", g_epzs_sp_calls, g_ep_sp_hits, g_epzs_sp_cpu);
     if (g_trace) fclose(g_trace);
     if (g_trace_miss) fclose(g_trace_miss);
     if (g_me) jmme_destroy(g_me);

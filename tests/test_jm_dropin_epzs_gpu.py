@@ -30,17 +30,33 @@ BASELINE_EPZS = {
     "EPZSSubPelGrid": 1,
 }
 
-_EPZS_LINE = re.compile(r"(\d+) EPZS searches on the GPU \(libjmme\), one call each; (\d+) on the CPU; (\d+) predictors, "
+_EPZS_LINE = re.compile(r"(\d+) EPZS searches on the GPU \(libjmme\); (\d+) on the CPU; (\d+) predictors, "
                         r"(\d+) pre-stamped map cells, (\d+) switches to window scans; ([\d.]+) ms in the EPZS wrapper, "
-                        r"([\d.]+) ms in jmme_epzs_search_ex")
-_SP_LINE = re.compile(r"(\d+) EPZS sub-pel refinements on the GPU, (\d+) on the CPU")
+                        r"([\d.]+) ms in the engine")
+_SP_LINE = re.compile(r"(\d+) EPZS sub-pel refinements on the GPU \((\d+) chained[^)]*\), (\d+) on the CPU")
+
+
+_SPEC_LINE = re.compile(r"EPZS speculation: (\d+) searches answered from (\d+) batches \((\d+) guesses\), (\d+) searched "
+                        r"alone; (\d+) not speculated; guesses refused: (\d+) inputs, (\d+) bounds, (\d+) map cells; "
+                        r"([\d.]+) ms building batches")
 
 
 def epzs_stats(stderr):
     m = _EPZS_LINE.search(stderr)
     assert m, stderr[-800:]
     k = ("gpu", "cpu", "preds", "stale", "scans", "wrap_ms", "call_ms")
-    return {a: (float(b) if a.endswith("_ms") else int(b)) for a, b in zip(k, m.groups())}
+    st = {a: (float(b) if a.endswith("_ms") else int(b)) for a, b in zip(k, m.groups())}
+    sp = _SPEC_LINE.search(stderr)
+    if sp:
+        k = ("hits", "batches", "guesses", "alone", "direct", "refused_inputs", "refused_bounds", "refused_cells",
+             "build_ms")
+        st.update({a: (float(b) if a.endswith("_ms") else int(b)) for a, b in zip(k, sp.groups())})
+        # every GPU search is answered from a batch, starts one, runs alone, or was not speculated
+        assert st["hits"] + st["batches"] + st["alone"] + st["direct"] == st["gpu"], stderr[-800:]
+    m = _SP_LINE.search(stderr)
+    if m:
+        st.update(sp_gpu=int(m.group(1)), sp_chained=int(m.group(2)), sp_cpu=int(m.group(3)))
+    return st
 
 
 def _run(w, h, frames, over, seed=5, gmv=(3, -2), adversarial=False, env=None):
@@ -89,7 +105,7 @@ def test_lencod_epzs_is_byte_identical(gpu, w, h, frames, over):
     assert st["gpu"] > 0 and st["cpu"] == 0 and st["scans"] == 0, err[-800:]
     if not over.get("EPZSSubPelGrid", 1):
         m = _SP_LINE.search(err)
-        assert m and int(m.group(1)) > 0 and int(m.group(2)) == 0, err[-800:]
+        assert m and int(m.group(1)) > 0 and int(m.group(3)) == 0, err[-800:]
 
 
 def test_lencod_epzs_blkcount_wraps(gpu):

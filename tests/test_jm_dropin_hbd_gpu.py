@@ -64,7 +64,7 @@ def test_lencod_10bit_is_byte_identical(gpu, w, h, frames, params):
         assert m and int(m.group(1)) > 0 and int(m.group(2)) == 0, r.stderr[-800:]
         if not p.get("DisableSubpelME", 1):   # sub-pel on: every refinement on the GPU
             m = re.search(r"(\d+) sub-pel refinements: .*, (\d+) on the CPU", r.stderr)
-            assert m and int(m.group(1)) > 0 and int(m.group(2)) == 0, r.stderr[-800:]
+            assert m and int(m.group(1)) > 0 and int(m.group(3)) == 0, r.stderr[-800:]
 
 
 @pytest.mark.parametrize("bits,over", [
@@ -97,4 +97,4 @@ def test_lencod_epzs_high_bit_depth_is_byte_identical(gpu, bits, over):
         assert st["gpu"] > 0 and st["cpu"] == 0 and st["scans"] == 0, r.stderr[-800:]
         if not p.get("EPZSSubPelGrid", 1):
             m = _SP_LINE.search(r.stderr)
-            assert m and int(m.group(1)) > 0 and int(m.group(2)) == 0, r.stderr[-800:]
+            assert m and int(m.group(1)) > 0 and int(m.group(3)) == 0, r.stderr[-800:]

@@ -154,6 +154,12 @@ def hybrid_block(dev, local: int, load_workload, iters: int = 10) -> dict:
 
 
 # ---- the drop-in encoder (JM 18.5 lencod with libjmme behind IntPelME) -----------
+def _progress(msg):
+    """a line on stderr per encode: long blocks keep showing signs of life"""
+    import sys
+    print(msg, file=sys.stderr, flush=True)
+
+
 def _lencod_args(binary, d, tag, yuv, w, h, frames, params, cfg_text):
     import os
     cfg = os.path.join(d, "enc.cfg")
@@ -207,10 +213,10 @@ def _lencod(binary, d, tag, yuv, w, h, frames, params, cfg_text, env=None):
     stats = re.search(r"integer batches: (\d+) past the batch, (\d+) failed guesses; (\d+) units; ([0-9.]+) ms building, "
                       r"([0-9.]+) ms in jmme_search_mbs", r.stderr)
     sp = re.search(r"(\d+) sub-pel refinements: (\d+) cached, (\d+) batches, (\d+) on the CPU", r.stderr)
-    ep = re.search(r"(\d+) EPZS searches on the GPU \(libjmme\), one call each; (\d+) on the CPU; (\d+) predictors, "
+    ep = re.search(r"(\d+) EPZS searches on the GPU \(libjmme\); (\d+) on the CPU; (\d+) predictors, "
                    r"(\d+) pre-stamped map cells, (\d+) switches to window scans; ([\d.]+) ms in the EPZS wrapper, "
-                   r"([\d.]+) ms in jmme_epzs_search_ex", r.stderr)
-    esp = re.search(r"(\d+) EPZS sub-pel refinements on the GPU, (\d+) on the CPU", r.stderr)
+                   r"([\d.]+) ms in the engine", r.stderr)
+    esp = re.search(r"(\d+) EPZS sub-pel refinements on the GPU \((\d+) chained[^)]*\), (\d+) on the CPU", r.stderr)
     ch = re.search(r"chained guesses: (\d+) chains, (\d+) steps, (\d+) calls answered, (\d+) head mismatches; "
                    r"(\d+) chain-only calls \((\d+) fell back", r.stderr)
     res = dict(wall_s=round(wall, 3), me_s=float(me.group(1)) if me else None,
@@ -234,7 +240,14 @@ def _lencod(binary, d, tag, yuv, w, h, frames, params, cfg_text, env=None):
                            engine_call_ms=float(g[6]),
                            us_per_search=round(float(g[5]) * 1e3 / max(1, int(g[0])), 2))
     if esp:
-        res["epzs_subpel"] = dict(gpu=int(esp.group(1)), cpu=int(esp.group(2)))
+        res["epzs_subpel"] = dict(gpu=int(esp.group(1)), chained=int(esp.group(2)), cpu=int(esp.group(3)))
+    spec = re.search(r"EPZS speculation: (\d+) searches answered from (\d+) batches \((\d+) guesses\), (\d+) searched "
+                     r"alone; (\d+) not speculated; guesses refused: (\d+) inputs, (\d+) bounds, (\d+) map cells; "
+                     r"([\d.]+) ms building batches", r.stderr)
+    if spec:
+        res["epzs_speculation"] = dict(zip(("answered_from_batches", "batches", "guesses", "searched_alone",
+                                            "not_speculated", "refused_inputs", "refused_bounds", "refused_cells"),
+                                           map(int, spec.groups()[:8])), build_ms=float(spec.group(9)))
     return res
 
 
@@ -295,9 +308,15 @@ def dropin_block(modes=None, size=(1920, 1080), search_range=32, reps=2, host_pr
             mode = params["SearchMode"]
             p = frames - 1
             cpu = _lencod(stock, d, f"cpu_{tag}", yuv, w, h, frames, params, CFG)
+            _progress(f"dropin {tag}: stock {cpu['me_s']:.3f} s of ME")
             host = _lencod_host(stock, d, yuv, w, h, frames, params, CFG, host_procs) if host_procs > 1 else None
-            gs = sorted((_lencod(gpu, d, f"gpu_{tag}_{r}", yuv, w, h, frames, params, CFG) for r in range(reps)),
-                        key=lambda x: x["me_s"])
+            if host:
+                _progress(f"dropin {tag}: {host_procs} concurrent stock encoders, slowest {max(host):.3f} s of ME")
+            gs = []
+            for r in range(reps):
+                gs.append(_lencod(gpu, d, f"gpu_{tag}_{r}", yuv, w, h, frames, params, CFG))
+                _progress(f"dropin {tag}: drop-in run {r}: {gs[-1]['me_s']:.3f} s of ME")
+            gs.sort(key=lambda x: x["me_s"])
             g = gs[len(gs) // 2]
             # JM's own loop around the search (integration/jm_noop_me.c: a zero-cost IntPelME)
             fl = _lencod(floor, d, f"floor_{tag}", yuv, w, h, frames, params, CFG) \
