@@ -429,9 +429,11 @@ __device__ void search_one(const EpzsParams &p, const jmme_epzs_req &q, WaveLds 
       // each evaluated one is the same.  JM's first entry is the first valid
       // one (the entries whose condition failed are not in JM's list).
       const unsigned long long vm = __ballot(valid);
+      int jexit = ke;   // an exit after packed entry jexit: JM never reaches (or stamps) the ones after it
       if (variant && !first_seen && vm) {
         first_seen = true;
         if (!((__ballot(eval) >> __builtin_ctzll(vm)) & 1ull)) {
+          jexit = -1;
           if (pexit && !ge(prev, fdiv(best - 1, 3) + 1, pv)) {          // prev * 3 < best
             path = 6;
             update = false;
@@ -443,8 +445,10 @@ __device__ void search_one(const EpzsParams &p, const jmme_epzs_req &q, WaveLds 
           }
         }
       }
+      if (!done) jexit = ke;
       for (int j = 0; !done && j < ke; ++j) {
         const int64_t c = rl64(cost, j);
+        jexit = j;
         const int jx = rl(px, j), jy = rl(py, j);
         if (c < best) {
           tmp2x = tmpx;
@@ -469,6 +473,10 @@ __device__ void search_one(const EpzsParams &p, const jmme_epzs_req &q, WaveLds 
           update = false;
           done = true;
         }
+      }
+      if (done && jexit < ke - 1) {   // un-stamp the chunk's entries past the exit
+        if (eval && k > jexit) atomicAnd(&s.map[cell >> 5], ~(1u << (cell & 31)));
+        wave_sync();
       }
     }
     // me_epzs_int.c:249-265: prev * 3 < best
