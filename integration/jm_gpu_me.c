@@ -1515,7 +1515,7 @@ static const ep_ans *ep_miss(Macroblock *currMB, MEBlock *mv_block, const jmme_e
    * had left of the batch and in the row above (distinct ones only) */
   nmb = imin(g_ep_batch, g_n_mb - mb);
   {
-    int need = 1 + nmb * JMME_NSLOT * EP_REFS * (EP_WAYS - 1);
+    int need = 1 + nmb * JMME_NSLOT * EP_REFS * EP_WAYS;   /* at most EP_WAYS guesses per partition and reference */
     ep_grow(need + 1, (need + 1) * EP_MAXP);
     free(g_ep_idx);
     g_ep_idx = (int *)malloc((size_t)nmb * JMME_NSLOT * EP_REFS * EP_WAYS * sizeof(int));
