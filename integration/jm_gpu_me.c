@@ -1289,7 +1289,7 @@ static jmme_subpel_req *g_ep_spq = NULL;
 static jmme_block_res *g_ep_spo = NULL;
 static int g_ep_pcap = 0;
 static long long g_ep_hits = 0, g_ep_batches = 0, g_ep_singles = 0, g_ep_guesses = 0, g_ep_direct = 0;
-static long long g_ep_fail_bounds = 0, g_ep_fail_stale = 0, g_ep_fail_inputs = 0, g_ep_sp_hits = 0;
+static long long g_ep_fail_bounds = 0, g_ep_fail_stale = 0, g_ep_fail_inputs = 0, g_ep_sp_hits = 0, g_ep_overflow = 0;
 static double g_t_ep_build = 0;
 
 static int ep_speculating(Macroblock *currMB, int cur_list, int ref, int n_pred)
@@ -1685,12 +1685,19 @@ static distblk epzs_gpu(int variant, Macroblock *currMB, MotionVector *pred_mv, 
   q.prev_sad = (int64_t)*prevSad;
   q.medthres = (int64_t)p_EPZS->medthres[bt];
 
+  const ep_ans *a = NULL;
   if (ep_speculating(currMB, cur_list, ref, n_pred)) {
     /* the speculative path: a cached answer whose inputs are this call's, or a batch */
-    const ep_ans *a = ep_lookup(currMB, mv_block, &q, g_ep_pred, g_ep_cond, g_ep_stale, n_stale);
+    a = ep_lookup(currMB, mv_block, &q, g_ep_pred, g_ep_cond, g_ep_stale, n_stale);
     t1 = now_us();
     if (!a) a = ep_miss(currMB, mv_block, &q, g_ep_pred, g_ep_cond, g_ep_stale, n_stale);
     g_t_epzs_gpu += now_us() - t1;
+    if (a->res.n_visited > EP_MAXV) {   /* (the call itself stamped more cells than a batch keeps: searched again) */
+      ++g_ep_overflow;
+      a = NULL;
+    }
+  }
+  if (a) {
     res = a->res;
     ep_apply(p_EPZS, &a->vis[0][0], res.n_visited, cnt, side, max_x, max_y);
     g_ep_served = a;
@@ -1847,9 +1854,9 @@ static void report(void)
     if (g_epzs_calls && g_ep_spec > 0)
       fprintf(stderr, "jm_gpu_me: EPZS speculation: %lld searches answered from %lld batches (%lld guesses), "
                       "%lld searched alone; %lld not speculated; guesses refused: %lld inputs, %lld bounds, "
-                      "%lld map cells; %.1f ms building batches\n",
+                      "%lld map cells; %.1f ms building batches; %lld searched again (more stamped cells than kept)\n",
               g_ep_hits, g_ep_batches, g_ep_guesses, g_ep_singles, g_ep_direct, g_ep_fail_inputs, g_ep_fail_bounds,
-              g_ep_fail_stale, g_t_ep_build * 1e-3);
+              g_ep_fail_stale, g_t_ep_build * 1e-3, g_ep_overflow);
     if (g_epzs_sp_calls || g_epzs_sp_cpu)
       fprintf(stderr, "jm_gpu_me: %lld EPZS sub-pel refinements on the GPU (%lld chained in the search's launch), "
                       "%lld on the CPU\n", g_epzs_sp_calls, g_ep_sp_hits, g_epzs_sp_cpu);
