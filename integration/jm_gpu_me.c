@@ -1291,12 +1291,15 @@ static int g_ep_pcap = 0;
 static long long g_ep_hits = 0, g_ep_batches = 0, g_ep_singles = 0, g_ep_guesses = 0, g_ep_direct = 0;
 static long long g_ep_fail_bounds = 0, g_ep_fail_stale = 0, g_ep_fail_inputs = 0, g_ep_sp_hits = 0, g_ep_overflow = 0;
 static double g_t_ep_build = 0;
+static long long g_ep_miss_slot[JMME_NSLOT], g_ep_list_diff[JMME_NSLOT];   /* misses inside a batch, by slot */
+static int g_ep_trace = 0;   /* JMME_EPZS_TRACE=1: per-slot miss counts at exit */
 
 static int ep_speculating(Macroblock *currMB, int cur_list, int ref, int n_pred)
 {
   if (g_ep_spec < 0) {
-    const char *e = getenv("JMME_EPZS_SPECULATE"), *b = getenv("JMME_EPZS_BATCH");
+    const char *e = getenv("JMME_EPZS_SPECULATE"), *b = getenv("JMME_EPZS_BATCH"), *tr = getenv("JMME_EPZS_TRACE");
     g_ep_spec = !(e && e[0] == '0');
+    g_ep_trace = tr && tr[0] == '1';
     if (b && atoi(b) > 0) g_ep_batch = imin(atoi(b), EP_BATCH_MAX);
   }
   if (!g_n_mb) {
@@ -1373,12 +1376,17 @@ static const ep_ans *ep_lookup(Macroblock *currMB, MEBlock *mv_block, const jmme
   }
   ep_fill_in(ep_seen_at(mb, slot, ref), q, pred, cond, mb, gen);
   if (g_ep_gen != gen || mb < g_ep_mb0 || mb >= g_ep_mb1) return NULL;
+  ++g_ep_miss_slot[slot];   /* (taken back below on a hit) */
   for (w = 0; w < EP_WAYS; w++) {
     const int k = g_ep_idx[(((size_t)(mb - g_ep_mb0) * JMME_NSLOT + slot) * EP_REFS + ref) * EP_WAYS + w];
     const ep_ans *a;
     if (k < 0) break;
     a = &g_ep_ans[k];
-    if (!ep_same(&a->in, q, pred, cond)) continue;
+    if (!ep_same(&a->in, q, pred, cond)) {
+      if (g_ep_trace && a->in.q.center_x == q->center_x && a->in.q.center_y == q->center_y &&
+          a->in.q.pred_x == q->pred_x && a->in.q.pred_y == q->pred_y) ++g_ep_list_diff[slot];
+      continue;
+    }
     if (q->stop_crit < a->bnd.stop_lo || q->stop_crit > a->bnd.stop_hi || q->prev_sad < a->bnd.prev_lo ||
         q->prev_sad > a->bnd.prev_hi || a->res.n_visited > EP_MAXV) {
       ++g_ep_fail_bounds;
@@ -1395,6 +1403,7 @@ static const ep_ans *ep_lookup(Macroblock *currMB, MEBlock *mv_block, const jmme
       continue;
     }
     ++g_ep_hits;
+    --g_ep_miss_slot[slot];
     return a;
   }
   ++g_ep_fail_inputs;
@@ -1857,6 +1866,12 @@ static void report(void)
                       "%lld map cells; %.1f ms building batches; %lld searched again (more stamped cells than kept)\n",
               g_ep_hits, g_ep_batches, g_ep_guesses, g_ep_singles, g_ep_direct, g_ep_fail_inputs, g_ep_fail_bounds,
               g_ep_fail_stale, g_t_ep_build * 1e-3, g_ep_overflow);
+    if (g_ep_trace) {
+      int sl;
+      fprintf(stderr, "jm_gpu_me: EPZS misses inside batches by slot (list-only differences):");
+      for (sl = 0; sl < JMME_NSLOT; sl++) fprintf(stderr, " %d:%lld(%lld)", sl, g_ep_miss_slot[sl], g_ep_list_diff[sl]);
+      fprintf(stderr, "\n");
+    }
     if (g_epzs_sp_calls || g_epzs_sp_cpu)
       fprintf(stderr, "jm_gpu_me: %lld EPZS sub-pel refinements on the GPU (%lld chained in the search's launch), "
                       "%lld on the CPU\n", g_epzs_sp_calls, g_ep_sp_hits, g_epzs_sp_cpu);

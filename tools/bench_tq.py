@@ -35,12 +35,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--blocks", type=int, default=1 << 22)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--ops", default="", help="comma-separated subset (e.g. quant4x4,satd8x8): profiling runs")
     a = ap.parse_args()
+    want = set(a.ops.split(",")) if a.ops else None
     dev = torch.device("cuda", 0)
     st = torch.cuda.current_stream().cuda_stream
     me = MotionEstimator()
     n = a.blocks
     for op, (_, ein, eout) in TRANSFORM_OPS.items():
+        if want and op not in want:
+            continue
         x = torch.randint(-255, 256, (n, ein), dtype=torch.int32, device=dev)
         y = torch.empty((n, eout), dtype=torch.int32, device=dev)
         ms = timed(lambda: me.transform_async(op, x.data_ptr(), y.data_ptr(), n, st), a.iters)
@@ -48,6 +52,8 @@ def main():
         print(json.dumps({"op": op, "blocks": n, "ms": round(ms, 4), "GB_per_s": round(gbs, 1),
                           "hbm_frac": round(gbs / HBM, 4), "bytes_per_block": (ein + eout) * 4}))
     for size in (4, 8):
+        if want and f"satd{size}x{size}" not in want:
+            continue
         d = torch.randint(-255, 256, (n, size * size), dtype=torch.int16, device=dev)
         o = torch.empty(n, dtype=torch.int32, device=dev)
         ms = timed(lambda: me.satd_async(size, d.data_ptr(), o.data_ptr(), n, st), a.iters)
@@ -55,6 +61,9 @@ def main():
         gbs = n * b / (ms * 1e-3) / 1e9
         print(json.dumps({"op": f"satd{size}x{size}", "blocks": n, "ms": round(ms, 4), "GB_per_s": round(gbs, 1),
                           "hbm_frac": round(gbs / HBM, 4), "bytes_per_block": b}))
+    if want and "quant4x4" not in want:
+        me.close()
+        return
     p = np.zeros(1, QUANT4x4_PARAMS)
     p["scale"], p["offset"], p["inv_scale"], p["qp_per"], p["is_cavlc"] = 8192, 1 << 16, 256, 4, 1
     p["scan"] = [(k % 4, k // 4) for k in range(16)]
