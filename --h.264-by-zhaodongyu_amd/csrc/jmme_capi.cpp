@@ -108,6 +108,8 @@ struct jmme_ctx {
   jmme_block_res *h_sout = nullptr;
   size_t cap_sout = 0;
   jmme_chain_res *h_chres = nullptr;         // jmme_search_mbs_chains results (mapped pinned)
+  jmme_block_res *h_chsp = nullptr;          // jmme_search_mbs_chains_sp refinements (mapped pinned)
+  void *dv_chsp = nullptr;
   unsigned long long *h_hkeys = nullptr;    // small latency form: per-tile keys (mapped pinned)
   size_t cap_hkeys = 0;
   uint8_t *h_emap = nullptr;                 // jmme_epzs_search_ex: mapped pinned request / result block
@@ -360,6 +362,7 @@ extern "C" void jmme_destroy(jmme_ctx *ctx) {
   if (ctx->h_emap) (void)hipHostFree(ctx->h_emap);
   if (ctx->h_hkeys) (void)hipHostFree(ctx->h_hkeys);
   if (ctx->h_chres) (void)hipHostFree(ctx->h_chres);
+  if (ctx->h_chsp) (void)hipHostFree(ctx->h_chsp);
   if (ctx->chain_stream) (void)hipStreamDestroy(ctx->chain_stream);
   (void)hipFree(ctx->d_skeys);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
@@ -863,7 +866,26 @@ extern "C" int jmme_search_mbs(jmme_ctx *ctx, int mode, const jmme_mb_req *req, 
 // chained searches: validated and launched (asynchronously, on stream s)
 // before the batch of the same call, so the batch's stream sync covers them
 namespace {
-int launch_chains(jmme_ctx *ctx, int mode, const jmme_chain *chains, int n, hipStream_t s) {
+int prepare_subs(jmme_ctx *ctx, hipStream_t s);
+
+// an in-chain SubPelME template (jmme_search_mbs_chains_sp): what
+// jmme_subpel_validate checks of a request's parameters, variant 0, no test8x8
+int check_chain_sp(const jmme_ctx *ctx, int i, const jmme_subpel_req &q) {
+  if (q.variant != 0) return fail("chain %d: sub-pel variant %d (chains run sub_pel_motion_estimation)", i, q.variant);
+  if (q.flags & ~JMME_SP_CHECK0) return fail("chain %d: sub-pel flags %d (no test8x8 in chains)", i, q.flags);
+  if (q.metric_h > 2 || q.metric_q > 2) return fail("chain %d: sub-pel metric %d/%d", i, q.metric_h, q.metric_q);
+  if ((q.metric_h == 1 || q.metric_q == 1) && ctx->cfg.SourceBitDepthLuma > 11)
+    return fail("chain %d: SSE sub-pel metric at SourceBitDepthLuma %d (int sums may wrap)", i,
+                ctx->cfg.SourceBitDepthLuma);
+  if (q.start_hp > 1 || q.start_qp > 1) return fail("chain %d: start_hp/qp", i);
+  if (q.search_pos2 > 9 || q.search_pos4 > 9)
+    return fail("chain %d: search_pos2/4 %d/%d beyond JM's 9-point rings", i, q.search_pos2, q.search_pos4);
+  if (q.lambda_h < 0 || q.lambda_q < 0) return fail("chain %d: negative sub-pel lambda", i);
+  return 0;
+}
+
+int launch_chains(jmme_ctx *ctx, int mode, const jmme_chain *chains, int n, hipStream_t s,
+                  const jmme_subpel_req *sp = nullptr) {
   if (n <= 0) return 0;
   if (n > kChainInline) return fail("%d chains in one call (at most %d)", n, kChainInline);
   if (mode != JMME_FULL_SEARCH && mode != JMME_FAST_FULL_SEARCH) return fail("chains: mode %d", mode);
@@ -907,6 +929,23 @@ int launch_chains(jmme_ctx *ctx, int mode, const jmme_chain *chains, int n, hipS
   std::memset(ctx->h_chres, 0, nres * sizeof(jmme_chain_res));
   void *d_res = ctx->dv_chres;
   if (sync_ref_table(ctx, s)) return -1;
+  if (sp) {
+    for (int i = 0; i < n; ++i)
+      if (check_chain_sp(ctx, i, sp[i])) return -1;
+    if (!ctx->h_chsp) {
+      HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_chsp), kChainInline * JMME_CHAIN_MAX_STEPS *
+                                                                       sizeof(jmme_block_res), hipHostMallocMapped));
+      HIPCHK(hipHostGetDevicePointer(&ctx->dv_chsp, ctx->h_chsp, 0));
+    }
+    std::memset(ctx->h_chsp, 0, nres * sizeof(jmme_block_res));
+    if (prepare_subs(ctx, s)) return -1;
+    const SubGeom g = sub_geom(ctx->width, ctx->height);
+    p.subs = ctx->d_sub_table;
+    p.sub_pitch = g.pitch;
+    p.plane_stride = g.plane_stride;
+    p.sp_res = static_cast<jmme_block_res *>(ctx->dv_chsp);
+    std::memcpy(p.sp, sp, (size_t)n * sizeof(jmme_subpel_req));
+  }
   p.cur = ctx->d_cur;
   p.refs = ctx->d_ref_table;
   p.pitch = ctx->pitch;
@@ -924,12 +963,14 @@ int launch_chains(jmme_ctx *ctx, int mode, const jmme_chain *chains, int n, hipS
 }
 }  // namespace
 
-extern "C" int jmme_search_mbs_chains(jmme_ctx *ctx, int mode, const jmme_mb_req *req, int n, jmme_block_res *out,
-                                      const jmme_chain *chains, int n_chains, jmme_chain_res *res) {
+extern "C" int jmme_search_mbs_chains_sp(jmme_ctx *ctx, int mode, const jmme_mb_req *req, int n,
+                                         jmme_block_res *out, const jmme_chain *chains, int n_chains,
+                                         const jmme_subpel_req *sp, jmme_chain_res *res, jmme_block_res *sp_res) {
   DevGuard dg_(ctx);
   if (!ctx) return fail("null ctx");
   if (!ctx->d_cur) return fail("current picture not uploaded");
   if (n_chains < 0 || (n_chains && (!chains || !res))) return fail("null chain array");
+  if (sp && n_chains && !sp_res) return fail("null sub-pel result array");
   if (n_chains == 0) return jmme_search_mbs(ctx, mode, req, n, out);
   if (!ctx->chain_stream) HIPCHK(hipStreamCreateWithFlags(&ctx->chain_stream, hipStreamNonBlocking));
   double t_ph = ctx->phases ? now_us() : 0;
@@ -937,15 +978,21 @@ extern "C" int jmme_search_mbs_chains(jmme_ctx *ctx, int mode, const jmme_mb_req
   // the chains run on their own stream beside the batch (which syncs the null
   // stream).  On one stream, one after the other, the call took longer
   // (JMME_PHASES, 1080p drop-in: 51 us waiting, against 29 + 12 on two streams)
-  if (launch_chains(ctx, mode, chains, n_chains, ctx->chain_stream)) return -1;
+  if (launch_chains(ctx, mode, chains, n_chains, ctx->chain_stream, sp)) return -1;
   phase(ctx, 0, &t_ph);
   const int rc = n ? jmme_search_mbs(ctx, mode, req, n, out) : 0;
   if (ctx->phases) t_ph = now_us();
   HIPCHK(hipStreamSynchronize(ctx->chain_stream));
   if (rc) return rc;
   std::memcpy(res, ctx->h_chres, (size_t)n_chains * JMME_CHAIN_MAX_STEPS * sizeof(jmme_chain_res));
+  if (sp) std::memcpy(sp_res, ctx->h_chsp, (size_t)n_chains * JMME_CHAIN_MAX_STEPS * sizeof(jmme_block_res));
   phase(ctx, 5, &t_ph);
   return 0;
+}
+
+extern "C" int jmme_search_mbs_chains(jmme_ctx *ctx, int mode, const jmme_mb_req *req, int n, jmme_block_res *out,
+                                      const jmme_chain *chains, int n_chains, jmme_chain_res *res) {
+  return jmme_search_mbs_chains_sp(ctx, mode, req, n, out, chains, n_chains, nullptr, res, nullptr);
 }
 
 extern "C" int jmme_search_mbs_async(jmme_ctx *ctx, int mode, const jmme_mb_req *d_req, int n,

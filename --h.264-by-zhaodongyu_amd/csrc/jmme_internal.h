@@ -115,7 +115,13 @@ struct ChainParams {
   int mode, max_mvd, n, max_r;      // max_r: largest window range of the launch (LDS sizing)
   int hbd;                          // 16-bit planes (SourceBitDepthLuma 9..14): v_sad_u16 instantiation
   jmme_chain_res *res;              // [n][JMME_CHAIN_MAX_STEPS] (host-mapped)
+  // in-chain SubPelME (jmme_search_mbs_chains_sp); subs == nullptr: integer-pel chains
+  const uint8_t *const *subs;       // device sub-image table [list * kMaxRefs + ref]
+  int sub_pitch;
+  size_t plane_stride;
+  jmme_block_res *sp_res;           // [n][JMME_CHAIN_MAX_STEPS] (host-mapped)
   jmme_chain chains[kChainInline];
+  jmme_subpel_req sp[kChainInline]; // per chain: the SubPelME parameters
 };
 size_t chain_lds_bytes(int max_r, bool hbd = false);
 hipError_t launch_search_chains(const ChainParams &p, hipStream_t s);

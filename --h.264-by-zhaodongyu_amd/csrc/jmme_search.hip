@@ -51,6 +51,7 @@
 #include "jmme.h"
 #include "jmme_common.h"
 #include "jmme_internal.h"
+#include "jmme_subpel_dev.h"
 
 namespace jmme {
 
@@ -1880,12 +1881,85 @@ __device__ __forceinline__ void chain_sweep(const GroupCtx &g, const uint32_t *w
   }
 }
 
+// SubPelME of a chain step (sub_pel_motion_estimation, me_fullsearch.c:186-289,
+// the refinement BlockMotionSearch runs after IntPelME when DisableSubpelME is
+// 0, mv_search.c:960-976).  Per phase (half-pel ring, quarter-pel ring) one
+// thread forms one (candidate, 4x4 block) sum (jmme_subpel_dev.h job_sum: the
+// metric's block sum at UMVLine4X-clamped sub-image coordinates) and adds it
+// into the candidate's LDS slot; after the barrier every thread walks the
+// candidates in JM's order with JM's comparisons and early-exit rule (dist),
+// so the result is uniform with no broadcast.  No 8x8-transform SATD: the
+// caller refuses JMME_SP_TEST8x8 for chains.
+template <typename T>
+__device__ __forceinline__ void chain_subpel_phase(const ChainParams &p, const T *sub, const T *org, int lg_nbx,
+                                                   int lg_nb, int mx, int my, int p0, int p1, int sc, int metric,
+                                                   int *sums, int tid) {
+  const int ymax = p.height + 2 * spd::kPadY - 1 - 16 - spd::kPadY, xmax = p.width + 2 * spd::kPadX - 1 - 16 - spd::kPadX;
+  if (tid < ((p1 - p0) << lg_nb)) {
+    const int cnd = tid >> lg_nb, b = tid & ((1 << lg_nb) - 1), pos = p0 + cnd;
+    const int bxo = (b & ((1 << lg_nbx) - 1)) * 4, byo = (b >> lg_nbx) * 4;
+    const int s = spd::job_sum(sub, p.plane_stride, p.sub_pitch, org, p.pitch, ymax, xmax, metric, false,
+                               mx + sc * spd::kSpiral9[pos][0], my + sc * spd::kSpiral9[pos][1], bxo, byo);
+    atomicAdd(&sums[cnd], s);
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ jmme_block_res chain_subpel(const ChainParams &p, const jmme_chain &c,
+                                                       const jmme_subpel_req &sp, const SlotGeom &sg, int px, int py,
+                                                       const jmme_block_res &r, int (*sums)[10], int tid) {
+  const T *sub = reinterpret_cast<const T *>(p.subs[c.list * kMaxRefs + c.ref_idx]);
+  const int pos_x = c.mb_x + 4 * sg.bx, pos_y = c.mb_y + 4 * sg.by;
+  const int pxp = pos_x << 2, pyp = pos_y << 2;   // pos_x_padded (mv_search.c:685-686)
+  const int lg_nbx = sg.w == 4 ? 2 : sg.w == 2 ? 1 : 0, lg_nb = lg_nbx + (sg.h == 4 ? 2 : sg.h == 2 ? 1 : 0);
+  const T *org = reinterpret_cast<const T *>(p.cur) + (size_t)pos_y * p.pitch + pos_x;
+  int mvx = r.mv_x, mvy = r.mv_y;
+  int64_t min_mcost = sp.start_hp ? r.cost : spd::kDistMax;
+  const bool chk0 = (sp.flags & JMME_SP_CHECK0) && c.ref_idx == 0 && sg.bt == 1 && mvx == 0 && mvy == 0;
+  // half-pel ring (me_fullsearch.c:209-251)
+  {
+    const int p0 = sp.start_hp, p1 = !sp.start_hp ? max(1, (int)sp.search_pos2) : (int)sp.search_pos2;
+    chain_subpel_phase(p, sub, org, lg_nbx, lg_nb, pxp + mvx, pyp + mvy, p0, p1, 2, sp.metric_h, sums[0], tid);
+    __syncthreads();
+    int best = 0;
+    for (int pos = p0; pos < p1; ++pos) {
+      const int cx = mvx + 2 * spd::kSpiral9[pos][0], cy = mvy + 2 * spd::kSpiral9[pos][1];
+      int64_t mcost = spd::mv_cost(sp.lambda_h, cx, cy, px, py);
+      if (mcost >= min_mcost) continue;
+      mcost += spd::dist(sums[0][pos - p0], min_mcost - mcost);
+      if (pos == 0 && chk0) mcost -= (int64_t)sp.lambda_h * 16;   // weighted_cost(lambda_factor, 16)
+      if (mcost < min_mcost) { min_mcost = mcost; best = pos; }
+    }
+    if (best) { mvx += 2 * spd::kSpiral9[best][0]; mvy += 2 * spd::kSpiral9[best][1]; }
+  }
+  if (!sp.start_qp) min_mcost = spd::kDistMax;
+  // quarter-pel ring (me_fullsearch.c:252-285)
+  {
+    const int p0 = sp.start_qp, p1 = sp.search_pos4;
+    chain_subpel_phase(p, sub, org, lg_nbx, lg_nb, pxp + mvx, pyp + mvy, p0, p1, 1, sp.metric_q, sums[1], tid);
+    __syncthreads();
+    int best = 0;
+    for (int pos = p0; pos < p1; ++pos) {
+      const int cx = mvx + spd::kSpiral9[pos][0], cy = mvy + spd::kSpiral9[pos][1];
+      int64_t mcost = spd::mv_cost(sp.lambda_q, cx, cy, px, py);
+      if (mcost >= min_mcost) continue;
+      mcost += spd::dist(sums[1][pos - p0], min_mcost - mcost);
+      if (mcost < min_mcost) { min_mcost = mcost; best = pos; }
+    }
+    if (best) { mvx += spd::kSpiral9[best][0]; mvy += spd::kSpiral9[best][1]; }
+  }
+  jmme_block_res o;
+  o.mv_x = (int16_t)mvx; o.mv_y = (int16_t)mvy; o.reserved = 0; o.cost = min_mcost;
+  return o;
+}
+
 template <bool FFS, bool HBD>
 __global__ __launch_bounds__(kChainWG) void chain_kernel(ChainParams p) {
   extern __shared__ uint32_t dyn[];
   __shared__ uint32_t s_cur[HBD ? 128 : 64];
   __shared__ uint32_t s_minc[2][kChainWaves], s_minr[2][kChainWaves];   // by step parity: one barrier per step
   __shared__ jmme_chain s_chain;                                         // out of the kernel arguments once
+  __shared__ int s_sps[2][2][10];   // in-chain SubPelME: by step parity, per phase, per candidate
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 #ifdef JMME_CHAIN_PROF
   if (blockIdx.x == 0 && tid == 0) g_chain_prof[30] = __builtin_amdgcn_s_memtime();
@@ -2012,6 +2086,8 @@ __global__ __launch_bounds__(kChainWG) void chain_kernel(ChainParams p) {
       const uint32_t cmin = wave_min_u32(bc);
       const uint32_t rmin = wave_min_u32(bc == cmin ? br : ~0u);
       if (lane == 0) { s_minc[k & 1][wave] = cmin; s_minr[k & 1][wave] = rmin; }
+      // (this parity's sub-pel slots were last read in step k - 2, before step k - 1's barrier)
+      if (p.subs && tid < 20) (&s_sps[k & 1][0][0])[tid] = 0;
     }
     __syncthreads();
     CPROF(4 + 4 * k);
@@ -2023,9 +2099,16 @@ __global__ __launch_bounds__(kChainWG) void chain_kernel(ChainParams p) {
     }
     const jmme_block_res r = block_result<FFS>(g, brank != ~0u, brank, bcost);
     res[k].mv_x = r.mv_x; res[k].mv_y = r.mv_y; res[k].cost = r.cost;
-    // as BlockMotionSearch leaves it for the next partitions' predictors (mv_search.c:983)
-    mvx[k] = clampi(r.mv_x, c.mv_lim_x0, c.mv_lim_x1);
-    mvy[k] = clampi(r.mv_y, c.mv_lim_y0, c.mv_lim_y1);
+    int fx = r.mv_x, fy = r.mv_y;
+    if (p.subs) {   // SubPelME of the step's answer (mv_search.c:960-976)
+      const jmme_block_res f = chain_subpel<std::conditional_t<HBD, uint16_t, uint8_t>>(
+          p, c, p.sp[blockIdx.x], sg, in.px, in.py, r, s_sps[k & 1], tid);
+      if (tid == 0) p.sp_res[(size_t)blockIdx.x * JMME_CHAIN_MAX_STEPS + k] = f;
+      fx = f.mv_x; fy = f.mv_y;
+    }
+    // as BlockMotionSearch leaves it for the next partitions' predictors (mv_search.c:981)
+    mvx[k] = clampi(fx, c.mv_lim_x0, c.mv_lim_x1);
+    mvy[k] = clampi(fy, c.mv_lim_y0, c.mv_lim_y1);
     CPROF(5 + 4 * k);
   }
   if (tid == 0) {

@@ -121,6 +121,7 @@ def lib() -> ctypes.CDLL:
         "jmme_slot": (I, [I, I, I]),
         "jmme_search_mbs": (I, [P, I, P, I, P]),
         "jmme_search_mbs_chains": (I, [P, I, P, I, P, P, I, P]),
+        "jmme_search_mbs_chains_sp": (I, [P, I, P, I, P, P, I, P, P, P]),
         "jmme_search_mbs_async": (I, [P, I, P, I, P, P]),
         "jmme_search_mbs_planes_async": (I, [P, I, P, P, I, I, I, P, I, P, P]),
         "jmme_search_status": (I, [P, P]),

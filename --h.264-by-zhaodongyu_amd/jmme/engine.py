@@ -114,6 +114,22 @@ class MotionEstimator:
                                            len(chains), ptr(res)))
         return out, res
 
+    def search_chains_sp(self, mode: int, req: np.ndarray, chains: np.ndarray, sp: np.ndarray):
+        """jmme_search_mbs_chains_sp: chains whose steps run SubPelME too; sp is
+        one SUBPEL_REQ template per chain.  Returns (batch BLOCK_RES [n, 41],
+        CHAIN_RES [n_chains, 4] integer answers, BLOCK_RES [n_chains, 4] refined)."""
+        req = np.ascontiguousarray(req, dtype=MB_REQ)
+        chains = np.ascontiguousarray(chains, dtype=_lib.CHAIN)
+        sp = np.ascontiguousarray(sp, dtype=_lib.SUBPEL_REQ)
+        if len(sp) != len(chains):
+            raise ValueError("one sub-pel template per chain")
+        out = np.zeros((req.shape[0], NSLOT), dtype=BLOCK_RES)
+        res = np.zeros((len(chains), _lib.CHAIN_MAX_STEPS), dtype=_lib.CHAIN_RES)
+        spo = np.zeros((len(chains), _lib.CHAIN_MAX_STEPS), dtype=BLOCK_RES)
+        check(lib().jmme_search_mbs_chains_sp(self._ctx, int(mode), ptr(req), req.shape[0], ptr(out), ptr(chains),
+                                              len(chains), ptr(sp), ptr(res), ptr(spo)))
+        return out, res, spo
+
     def search_async(self, mode: int, d_req: int, n: int, d_out: int, stream: int = 0) -> None:
         """Device-resident variant: d_req/d_out are device addresses (e.g. torch data_ptr())."""
         check(lib().jmme_search_mbs_async(self._ctx, int(mode), ctypes.c_void_p(d_req), int(n),

@@ -467,6 +467,22 @@ typedef struct jmme_subpel_req {
 /* host arrays, synchronous; out[i] = (mv, cost) SubPelME returns */
 int jmme_subpel_refine(jmme_ctx *ctx, const jmme_subpel_req *req, int n, jmme_block_res *out);
 
+/* jmme_search_mbs_chains with sub_pel_motion_estimation inside the chains (FS /
+ * FFS with DisableSubpelME = 0: a partition's neighbours then hold refined
+ * vectors).  sp[i] is chain i's SubPelME template -- lambda_h / lambda_q,
+ * metric_h / metric_q, start_hp / start_qp, search_pos2 / 4 and flags
+ * (JMME_SP_CHECK0; JMME_SP_TEST8x8 is refused) as JM hands them; variant must
+ * be 0; its block, ref_slot, pred, mv, min_mcost and subthres are ignored:
+ * step k refines its own integer answer under its derived predictor with
+ * min_mcost = start_hp ? its cost : DISTBLK_MAX (mv_search.c:960-976), and
+ * the refined vector, clipped as mv_search.c:981 clips it, is what the later
+ * steps read as that partition's vector.  sp_res[i * JMME_CHAIN_MAX_STEPS + k]
+ * = the (mv, cost) SubPelME returns; res[] as jmme_search_mbs_chains (the
+ * integer answers).  sp == NULL: jmme_search_mbs_chains. */
+int jmme_search_mbs_chains_sp(jmme_ctx *ctx, int mode, const jmme_mb_req *req, int n, jmme_block_res *out,
+                              const jmme_chain *chains, int n_chains, const jmme_subpel_req *sp,
+                              jmme_chain_res *res, jmme_block_res *sp_res);
+
 /* EPZS speculative batch with its chained sub-pel refinements (jmme_epzs_bounds above). */
 /* One launch over n searches, as jmme_epzs_search_ex (host arrays, one sync),
  * plus bounds[i] and, when sp_req is not NULL, one sub-pel refinement per search

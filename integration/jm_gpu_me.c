@@ -347,6 +347,16 @@ static int spec_hyp(int list, int ref, int h, int mb0, int mb, const spec_ent *w
  * JMME_CHAINS=0 turns it off. */
 static jmme_chain g_chains[8];
 static jmme_chain_res g_chres[8 * JMME_CHAIN_MAX_STEPS];
+/* sub-pel on (DisableSubpelME = 0): the chains run SubPelME after every step
+ * (jmme_search_mbs_chains_sp), so the later steps read refined vectors as JM's
+ * do; g_chain_sp is the SubPelME template of this miss's chains and the
+ * refinements land in the sub-pel cache's chain way */
+static jmme_subpel_req g_chain_sp[8];
+static jmme_block_res g_chspres[8 * JMME_CHAIN_MAX_STEPS];
+static int g_chain_sp_on = 0;
+static long long g_chain_sp_steps = 0, g_chain_sp_hits = 0, g_chain_sp_nolam = 0;
+static int chain_subpel_template(Macroblock *currMB, MEBlock *mv_block, int list, int ref, int lambda_f);
+static void store_chain_subpel(int list, int ref, int mb, int sl, const jmme_chain_res *r, const jmme_block_res *f);
 static int g_n_chains = 0, g_chain_on = -1, g_chain_head = -1;
 static int8_t g_slot_bt[JMME_NSLOT], g_slot_bx[JMME_NSLOT], g_slot_by[JMME_NSLOT];   /* slot_geometry() */
 static void slot_geometry(void);
@@ -388,9 +398,20 @@ static int chains_on(Macroblock *currMB, int list, int ref)
     chain_groups();
     if (!g_slot_bt[0]) slot_geometry();
   }
+  (void)p_Vid;
   return g_chain_on && currSlice->slice_type == P_SLICE && currSlice->structure == FRAME &&
          currMB->list_offset == 0 && list == 0 && ref == 0 && currSlice->listXsize[0] == 1 &&
-         p_Inp->DisableSubpelME[p_Vid->view_id] && !p_Inp->Transform8x8Mode;
+         !p_Inp->Transform8x8Mode;
+}
+
+/* chains for this miss: integer-pel, or with SubPelME when it is on and its
+ * template (every step's SubPelME parameters but the step's own block,
+ * predictor and answer) is known */
+static int chains_ready(Macroblock *currMB, MEBlock *mv_block, int list, int ref, const spec_ent *want)
+{
+  if (!chains_on(currMB, list, ref)) return 0;
+  g_chain_sp_on = !currMB->p_Inp->DisableSubpelME[currMB->p_Vid->view_id];
+  return !g_chain_sp_on || chain_subpel_template(currMB, mv_block, list, ref, want->lambda);
 }
 
 /* one chain: group g's partitions from index i0, in JM's order */
@@ -467,6 +488,7 @@ static int build_chains(Macroblock *currMB, int list, int ref, int mb, int s, co
   g1 = g0 <= 2 ? 6 : 3 + 4 * ((g0 - 3) / 4) + 3;   /* through quadrant 0 / through s's quadrant */
   for (g = g0 + 1; g <= g1 && n < 8; g++)
     if (g_grp_n[g] > 1 || g0 <= 2) chain_fill(&g_chains[n++], currMB, list, ref, g, 0, want);
+  for (g = 1; g_chain_sp_on && g < n; g++) g_chain_sp[g] = g_chain_sp[0];
   return n;
 }
 
@@ -499,6 +521,7 @@ static void store_chains(int list, int ref, const spec_ent *want)
       e->mvx = r->mv_x; e->mvy = r->mv_y; e->cost = r->cost;
       e->valid = g_slot_gen[list][ref];
       ++g_chain_steps;
+      if (g_chain_sp_on) store_chain_subpel(list, ref, mb, sl, r, &g_chspres[i * JMME_CHAIN_MAX_STEPS + k]);
       /* the chain's first step is the missing call itself: its derived inputs must be the real ones */
       if (i == 0 && k == 0 && sl == g_chain_head && !spec_key_eq(e, want)) ++g_chain_head_bad;
     }
@@ -591,9 +614,9 @@ static void spec_batch(int list, int ref, int mb0, const spec_ent *want, int chk
     }
   }
   t1 = now_us();
-  if (jmme_search_mbs_chains(g_me, want->mode ? JMME_FAST_FULL_SEARCH : JMME_FULL_SEARCH, g_req, nreq, g_res,
-                             g_chains, g_n_chains, g_chres))
-    fail_jm("jmme_search_mbs_chains");
+  if (jmme_search_mbs_chains_sp(g_me, want->mode ? JMME_FAST_FULL_SEARCH : JMME_FULL_SEARCH, g_req, nreq, g_res,
+                                g_chains, g_n_chains, g_chain_sp_on ? g_chain_sp : NULL, g_chres, g_chspres))
+    fail_jm("jmme_search_mbs_chains_sp");
   t2 = now_us();
   g_t_build += t1 - t0;
   g_t_call += t2 - t1;
@@ -680,15 +703,15 @@ static const spec_ent *spec_lookup(Macroblock *currMB, MEBlock *mv_block, int li
     const char *c = getenv("JMME_CHAIN_ONLY");
     g_chain_only = !(c && c[0] == '0');
   }
-  if (g_chain_only && failed && s != 0 && chains_on(currMB, list, ref)) {
+  if (g_chain_only && failed && s != 0 && chains_ready(currMB, mv_block, list, ref, want)) {
     /* a failed guess inside a macroblock whose 16x16 search hit: the
      * macroblock's decided partitions as chains, the missing call first, and no
      * batch (the guesses for the macroblocks after this one stand).  A 16x16
      * miss says the guesses themselves are off: that one re-batches. */
     g_n_chains = build_chains(currMB, list, ref, mb, s, want, 1);
-    if (jmme_search_mbs_chains(g_me, want->mode ? JMME_FAST_FULL_SEARCH : JMME_FULL_SEARCH, g_req, 0, g_res, g_chains,
-                               g_n_chains, g_chres))
-      fail_jm("jmme_search_mbs_chains");
+    if (jmme_search_mbs_chains_sp(g_me, want->mode ? JMME_FAST_FULL_SEARCH : JMME_FULL_SEARCH, g_req, 0, g_res,
+                                  g_chains, g_n_chains, g_chain_sp_on ? g_chain_sp : NULL, g_chres, g_chspres))
+      fail_jm("jmme_search_mbs_chains_sp");
     ++g_chain_calls;
     store_chains(list, ref, want);
     e = &tab[spec_idx(mb, s, KHYP)];
@@ -696,7 +719,7 @@ static const spec_ent *spec_lookup(Macroblock *currMB, MEBlock *mv_block, int li
     ++g_chain_call_fail;   /* (the chain stopped before it: a half-way centre or an oversized range) */
   }
   if (failed) g_batch = imax(1, g_batch / 2);   /* a re-batch after a failed guess: shorter */
-  g_n_chains = chains_on(currMB, list, ref) ? build_chains(currMB, list, ref, mb, s, want, 0) : 0;
+  g_n_chains = chains_ready(currMB, mv_block, list, ref, want) ? build_chains(currMB, list, ref, mb, s, want, 0) : 0;
   spec_batch(list, ref, mb, want, chk_rule, currMB->p_Inp->rdopt);
   e = &tab[spec_idx(mb, s, 0)];
   if (!spec_same(e, want, g_slot_gen[list][ref])) error("jm_gpu_me: batch lost its own request", 500);
@@ -874,7 +897,8 @@ static void slot_geometry(void)
       }
 }
 
-#define SPK (KHYP + 1)                  /* sub-pel answers kept per (macroblock, slot) */
+#define SPK (KHYP + 2)                  /* sub-pel answers kept per (macroblock, slot): the KHYP guesses,
+                                           the real call (way KHYP), the chains' refinement (way KHYP + 1) */
 static int *g_sp_dst = NULL;
 
 static void sp_fill(jmme_subpel_req *q, int mb, int s, int list, int ref, const sp_ent *w)
@@ -980,6 +1004,80 @@ static void prefault_tables(VideoParameters *p_Vid, InputParameters *p_Inp)
   if (!p_Inp->DisableSubpelME[0]) sp_table(p_Vid, 0, 0);
 }
 
+/* lambda_factor[H_PEL] / [Q_PEL] of the F_PEL lambdas seen in sub-pel calls
+ * (the integer search receives only lambda_factor[F_PEL]; its caller's array,
+ * md_low.c:130 / mode_decision_P8x8.c:63, holds the other two) */
+#define NLAM 8
+static int g_lam[NLAM][3], g_n_lam = 0;
+
+static void note_lambdas(const int *lambda_factor)
+{
+  int i;
+  for (i = 0; i < g_n_lam; i++)
+    if (g_lam[i][0] == lambda_factor[F_PEL]) {
+      g_lam[i][1] = lambda_factor[H_PEL];
+      g_lam[i][2] = lambda_factor[Q_PEL];
+      return;
+    }
+  i = g_n_lam < NLAM ? g_n_lam++ : (int)(g_sp_calls % NLAM);
+  g_lam[i][0] = lambda_factor[F_PEL];
+  g_lam[i][1] = lambda_factor[H_PEL];
+  g_lam[i][2] = lambda_factor[Q_PEL];
+}
+
+/* the SubPelME template of the chains of this miss (g_chain_sp[0]): what
+ * __wrap_sub_pel_motion_estimation will hand the GPU for the macroblock's
+ * partitions, from the integer call's MEBlock (metrics, search_pos2 / 4 --
+ * init_mv_block, mv_search.c:700-769), p_Vid's refinement starts and the sub-pel
+ * lambdas last seen with this F_PEL lambda.  0 when JM's sub-pel calls would
+ * not be served on the GPU, or the lambdas are not known yet.  (A wrong
+ * template only costs hits: every answer is used for identical inputs only.) */
+static int chain_subpel_template(Macroblock *currMB, MEBlock *mv_block, int list, int ref, int lambda_f)
+{
+  VideoParameters *p_Vid = currMB->p_Vid;
+  Slice *currSlice = currMB->p_Slice;
+  int mode = currMB->p_Inp->SearchMode[p_Vid->view_id];
+  int mh = metric_id(mv_block->computePredHPel), mq = metric_id(mv_block->computePredQPel), i;
+  jmme_subpel_req *q = &g_chain_sp[0];
+  if ((mode != FULL_SEARCH && mode != FAST_FULL_SEARCH) || mh < 0 || mq < 0 || (g_bits > 11 && (mh == 1 || mq == 1)) ||
+      mv_block->ChromaMEEnable || mv_block->search_pos2 > 9 || mv_block->search_pos4 > 9)
+    return 0;
+  for (i = 0; i < g_n_lam && g_lam[i][0] != lambda_f; i++) {}
+  if (i == g_n_lam) {
+    ++g_chain_sp_nolam;
+    return 0;
+  }
+  memset(q, 0, sizeof *q);
+  q->lambda_h = g_lam[i][1];
+  q->lambda_q = g_lam[i][2];
+  q->metric_h = (uint8_t)mh;
+  q->metric_q = (uint8_t)mq;
+  q->start_hp = (uint8_t)(p_Vid->start_me_refinement_hp != 0);
+  q->start_qp = (uint8_t)(p_Vid->start_me_refinement_qp != 0);
+  q->search_pos2 = (uint8_t)mv_block->search_pos2;
+  q->search_pos4 = (uint8_t)mv_block->search_pos4;
+  q->flags = (uint8_t)((!currMB->p_Inp->rdopt && currSlice->slice_type != B_SLICE) ? JMME_SP_CHECK0 : 0);
+  sp_table(p_Vid, list, ref);
+  return 1;
+}
+
+/* a chain step's refinement -> way KHYP + 1 of its (macroblock, slot), keyed by
+ * the inputs BlockMotionSearch hands SubPelME after that step's answer */
+static void store_chain_subpel(int list, int ref, int mb, int sl, const jmme_chain_res *r, const jmme_block_res *f)
+{
+  const jmme_subpel_req *q = &g_chain_sp[0];
+  sp_ent *e = &g_sp[list][ref][((size_t)mb * JMME_NSLOT + sl) * SPK + KHYP + 1];
+  memset(e, 0, sizeof *e);
+  e->px = r->pred_x; e->py = r->pred_y; e->mx = r->mv_x; e->my = r->mv_y;
+  e->min_mcost = q->start_hp ? r->cost : JMME_DISTBLK_MAX;
+  e->lam_h = q->lambda_h; e->lam_q = q->lambda_q;
+  e->metric_h = q->metric_h; e->metric_q = q->metric_q; e->start_hp = q->start_hp; e->start_qp = q->start_qp;
+  e->pos2 = q->search_pos2; e->pos4 = q->search_pos4; e->flags = q->flags;
+  e->omx = f->mv_x; e->omy = f->mv_y; e->cost = f->cost;
+  e->valid = g_slot_gen[list][ref];
+  ++g_chain_sp_steps;
+}
+
 /* sub_pel_motion_estimation's contract (me_fullsearch.c:186-289) */
 distblk __wrap_sub_pel_motion_estimation(Macroblock *currMB, MotionVector *pred_mv, MEBlock *mv_block,
                                          distblk min_mcost, int *lambda_factor)
@@ -1003,6 +1101,7 @@ distblk __wrap_sub_pel_motion_estimation(Macroblock *currMB, MotionVector *pred_
     return __real_sub_pel_motion_estimation(currMB, pred_mv, mv_block, min_mcost, lambda_factor);
   }
   ensure_planes(currMB, list, ref);
+  note_lambdas(lambda_factor);
   memset(&want, 0, sizeof want);
   want.px = pred_mv->mv_x; want.py = pred_mv->mv_y;
   want.mx = mv_block->mv[list].mv_x; want.my = mv_block->mv[list].mv_y;
@@ -1022,6 +1121,7 @@ distblk __wrap_sub_pel_motion_estimation(Macroblock *currMB, MotionVector *pred_
   for (i = 0; i < SPK && !sp_same(&e[i], &want, g_slot_gen[list][ref]); i++) {}
   if (i < SPK) {
     ++g_sp_hits;
+    if (i == KHYP + 1) ++g_chain_sp_hits;
     e += i;
   } else {
     sp_batch(list, ref, mb, s, &want, currMB->p_Inp->Transform8x8Mode != 0);
@@ -1854,6 +1954,9 @@ static void report(void)
       fprintf(stderr, "jm_gpu_me: chained guesses: %lld chains, %lld steps, %lld calls answered, %lld head mismatches; "
                       "%lld chain-only calls (%lld fell back to a batch)\n",
               g_chain_sent, g_chain_steps, g_chain_hits, g_chain_head_bad, g_chain_calls, g_chain_call_fail);
+    if (g_chain_sp_steps || g_chain_sp_nolam)
+      fprintf(stderr, "jm_gpu_me: chained sub-pel: %lld refinements, %lld calls answered; %lld misses without "
+                      "known sub-pel lambdas\n", g_chain_sp_steps, g_chain_sp_hits, g_chain_sp_nolam);
     if (g_epzs_calls || g_epzs_cpu)
       fprintf(stderr, "jm_gpu_me: %lld EPZS searches on the GPU (libjmme); %lld on the CPU; "
                       "%lld predictors, %lld pre-stamped map cells, %lld switches to window scans; "

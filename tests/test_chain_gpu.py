@@ -270,3 +270,96 @@ def test_prepare_and_reserve_then_search(gpu):
             res.append((me.search(FULL_SEARCH, req), *me.search_chains(FULL_SEARCH, req[:2], chains)))
     for a, b in zip(*res):
         assert np.array_equal(a, b)
+
+
+def _sp_templates(rng, n, bits):
+    from jmme import SUBPEL_REQ
+    sp = np.zeros(n, SUBPEL_REQ)
+    sp["lambda_h"] = rng.choice([0, 40, 187, 900], n)
+    sp["lambda_q"] = rng.choice([0, 40, 187, 900], n)
+    sp["metric_h"] = rng.integers(0, 3, n)
+    sp["metric_q"] = rng.integers(0, 3, n)
+    if bits > 11:   # SSE sub-pel is refused above 11 bits
+        sp["metric_h"][sp["metric_h"] == 1] = 2
+        sp["metric_q"][sp["metric_q"] == 1] = 0
+    sp["start_hp"] = rng.integers(0, 2, n)
+    sp["start_qp"] = rng.integers(0, 2, n)
+    sp["search_pos2"] = rng.choice([9, 9, 5, 1], n)
+    sp["search_pos4"] = rng.choice([9, 9, 5, 0], n)
+    sp["flags"] = rng.choice([0, 2], n)   # JMME_SP_CHECK0
+    return sp
+
+
+@pytest.mark.parametrize("ffs,rdopt,R,bits", [(False, 0, 16, 8), (True, 1, 32, 8), (False, 1, 32, 8), (True, 0, 16, 10)])
+def test_chains_with_subpel_match_step_by_step(gpu, ffs, rdopt, R, bits):
+    """jmme_search_mbs_chains_sp: each step's integer answer equals its own
+    search under the predictor derived from the earlier steps' REFINED vectors
+    (mv_search.c:960-981), and its refinement equals a jmme_subpel_refine call
+    (sub_pel_motion_estimation, variant 0) with that answer as mv and
+    min_mcost = start_hp ? cost : DISTBLK_MAX"""
+    from jmme import FAST_FULL_SEARCH, FULL_SEARCH, MB_REQ, MotionEstimator, synth
+    dmax = (2 ** 31 - 1) << 5
+    w, h = 352, 288
+    rng = np.random.default_rng(900 + 10 * R + rdopt + 100 * ffs + bits)
+    luma = synth.luma_sequence(w, h, 2, seed=R + 7 * rdopt, gmv=(3, -2), adversarial=True, adv_range=R)
+    if bits > 8:
+        sh = bits - 8
+        luma = ((luma.astype(np.int32) << sh) + rng.integers(0, 1 << sh, size=luma.shape)).astype(np.uint16)
+    mode = FAST_FULL_SEARCH if ffs else FULL_SEARCH
+    cfg = {"SearchRange": R, "SearchMode": 0 if ffs else -1, "RDOptimization": rdopt, "SourceBitDepthLuma": bits}
+    n_steps = n_moved = 0
+    with MotionEstimator(cfg) as me:
+        me.upload_cur(luma[1])
+        me.upload_ref(0, 0, luma[0])
+        for rnd in range(3):
+            chains = _random_chains(rng, w, h, 8, R, rdopt, ffs)
+            sp = _sp_templates(rng, 8, bits)
+            _, res, spo = me.search_chains_sp(mode, np.zeros(0, MB_REQ), chains, sp)
+            for i, c in enumerate(chains):
+                prev = []
+                for k in range(int(c["n_steps"])):
+                    p, cen, rmin, rmax = derive(c, k, prev, me.max_mvd)
+                    got = res[i, k]
+                    if not ffs and (cen[0] | cen[1]) & 3:
+                        assert all(res[i, j]["cost"] == -1 for j in range(k, int(c["n_steps"]))), (i, k, res[i])
+                        break
+                    assert (got["pred_x"], got["pred_y"]) == p, (rnd, i, k, got, p)
+                    q, s = _step_req(c, k, p, cen, rmin, rmax, ffs)
+                    exp = me.search(mode, q)[0, s]
+                    assert (got["mv_x"], got["mv_y"], got["cost"]) == (exp["mv_x"], exp["mv_y"], exp["cost"]), \
+                        (rnd, i, k, got, exp)
+                    bx, by, _, _ = _geom()[s]
+                    r = sp[i:i + 1].copy()
+                    r["pos_x"], r["pos_y"] = int(c["mb_x"]) + 4 * bx, int(c["mb_y"]) + 4 * by
+                    r["blocktype"] = {0: 1, 1: 2, 3: 3, 5: 4, 9: 5, 17: 6, 25: 7}[max(v for v in (0, 1, 3, 5, 9, 17, 25)
+                                                                                  if v <= s)]
+                    r["pred_x"], r["pred_y"] = p
+                    r["mv_x"], r["mv_y"] = exp["mv_x"], exp["mv_y"]
+                    r["min_mcost"] = exp["cost"] if sp[i]["start_hp"] else dmax
+                    ref = me.subpel_refine(r)[0]
+                    assert (spo[i, k]["mv_x"], spo[i, k]["mv_y"], spo[i, k]["cost"]) == \
+                        (ref["mv_x"], ref["mv_y"], ref["cost"]), (rnd, i, k, spo[i, k], ref)
+                    n_moved += (ref["mv_x"], ref["mv_y"]) != (exp["mv_x"], exp["mv_y"])
+                    prev.append((min(max(int(ref["mv_x"]), -2048), 2047), min(max(int(ref["mv_y"]), -512), 511)))
+                    n_steps += 1
+    assert n_steps >= 24 and n_moved >= 8, (n_steps, n_moved)
+
+
+def test_chain_subpel_templates_outside_contract_are_refused(gpu):
+    from jmme import FULL_SEARCH, JmmeError, MB_REQ, SUBPEL_REQ, SP_TEST8x8, MotionEstimator
+    rng = np.random.default_rng(5)
+    plane = (rng.integers(0, 256, (64, 64))).astype(np.uint8)
+    chains = _random_chains(rng, 64, 64, 1, 4, 0, False)
+    good = np.zeros(1, SUBPEL_REQ)
+    good["search_pos2"] = good["search_pos4"] = 9
+    empty = np.zeros(0, MB_REQ)
+    with MotionEstimator({"SearchRange": 4}) as me:
+        me.upload_cur(plane)
+        me.upload_ref(0, 0, plane)
+        me.search_chains_sp(FULL_SEARCH, empty, chains, good)
+        for field, val in [("variant", 1), ("flags", SP_TEST8x8), ("metric_q", 3), ("search_pos2", 10),
+                           ("start_hp", 2), ("lambda_h", -1)]:
+            bad = good.copy()
+            bad[field] = val
+            with pytest.raises(JmmeError):
+                me.search_chains_sp(FULL_SEARCH, empty, chains, bad)
