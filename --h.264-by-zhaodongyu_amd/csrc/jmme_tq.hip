@@ -374,92 +374,104 @@ __global__ __launch_bounds__(kTB) void satd_kernel(const int16_t *__restrict__ d
 }
 
 // ---- quant_4x4_normal --------------------------------------------------------
-// A lane per scan position, 16 lanes per block, 4 blocks per wave.  JM's loop
+// A lane per scan position, 16 lanes per block, 4 blocks per wave; every wave
+// works alone (no workgroup barrier, no LDS arrays).  JM's loop
 // (quant4x4_normal.c:59-104) is sequential only through `run` and the output
 // index; both are functions of which earlier scan positions quantise to a
 // nonzero level, i.e. of the block's 16-bit slice of one ballot: the output
 // index is the popcount of the nonzero positions below, the run the distance
-// to the highest one.  The cost is a sum over the nonzero positions (a 16-lane
-// cross-lane reduction), and the level / run lists are compacted through a
-// small LDS table.  (The earlier lane-per-block form walked the scan in
-// per-lane LDS arrays: 120 VGPRs, 13 KB LDS per wave, 34 % of HBM.)
+// to the highest one.  The (level, run) lists are compacted with one
+// ds_permute each (a push: nonzero lane k to slot idx, the zero lanes behind
+// them in order -- a bijection), the 4 blocks' 17-dword level lists are then
+// pulled (ds_bpermute) into one lane-contiguous run of 68 dwords, and the cost
+// is a 16-lane DPP reduction.  kUQ rounds' loads are issued before the first
+// round's arithmetic.  With one parameter set (param_idx NULL) the lane's
+// scale / offset / inverse scale and the cost table are loaded once per wave.
+// (Round 3's form, with LDS compaction tables and three workgroup barriers per
+// round, measured 33 % of HBM: 64 % of its wave cycles parked on waits --
+// rocprofv3 SQ_WAIT_ANY -- for the barriers and a three-deep dependent load
+// chain per round.)
+template <bool UNI>   // UNI: one parameter set (param_idx NULL)
 __global__ __launch_bounds__(kWG8) void quant4x4_kernel(const jmme_quant4x4_params *__restrict__ params,
                                                         const int32_t *__restrict__ param_idx,
                                                         int32_t *__restrict__ coef, int32_t *__restrict__ levels,
                                                         int32_t *__restrict__ runs,
                                                         int32_t *__restrict__ coeff_cost,
                                                         int32_t *__restrict__ nonzero, int n) {
-  constexpr int kB = kWG8 / 16;   // blocks per workgroup per round; kUQ rounds' loads issued together
-  __shared__ int32_t s_l[kB][17], s_r[kB][16];
-  const int g = threadIdx.x >> 4, k = threadIdx.x & 15, gw = g & 3;   // block, scan position, block in the wave
-  for (int base = blockIdx.x * kB * kUQ; base < n; base += gridDim.x * kB * kUQ) {
-    int pq[kUQ], x[kUQ], sc[kUQ], of[kUQ], iv[kUQ], cc[kUQ];
-    const jmme_quant4x4_params *qp[kUQ];
+  const int lane = threadIdx.x & 63, gw = lane >> 4, k = lane & 15;
+  const int wave = (blockIdx.x * kWG8 + threadIdx.x) >> 6, nwaves = gridDim.x * (kWG8 / 64);
+  constexpr bool uni = UNI;
+  constexpr int U = UNI ? kUQ : kUQ / 2;   // rounds in flight (the per-block parameters cost registers)
+  // one parameter set: this lane's scan position and factors, once
+  // (lane k of a block also holds c_cost[k]: a level-1 lane pulls c_cost[run] from lane run of its block)
+  int pq0 = 0, sc0 = 0, of0 = 0, iv0 = 0, qper0 = 0, cavlc0 = 0, ck0 = 0;
+  if (uni) {
+    const jmme_quant4x4_params &q = params[0];
+    pq0 = q.scan[k][1] * 4 + q.scan[k][0];   // (horizontal, vertical)
+    sc0 = q.scale[pq0]; of0 = q.offset[pq0]; iv0 = q.inv_scale[pq0];
+    qper0 = q.qp_per; cavlc0 = q.is_cavlc; ck0 = q.c_cost[k];
+  }
+  // this lane's dword of the wave's 68-dword level run: block j, entry pos (16: the 0 terminator)
+  const int lj = lane / 17, lpos = lane - 17 * lj;
+  const int tj = 3, tpos = 13 + (lane & 3);   // lanes 0-3: dwords 64-67 (block 3, entries 13-16)
+  for (int b4 = wave * 4 * U; b4 < n; b4 += nwaves * 4 * U) {
+    int x[U], cc[U], pq[U], sc[U], of[U], iv[U], qper[U], cavlc[U], ck[U];
 #pragma unroll
-    for (int u = 0; u < kUQ; ++u) {
-      const int b = base + u * kB + g;
-      qp[u] = params + ((param_idx && b < n) ? param_idx[b] : 0);
-    }
-#pragma unroll
-    for (int u = 0; u < kUQ; ++u) pq[u] = qp[u]->scan[k][1] * 4 + qp[u]->scan[k][0];   // (horizontal, vertical)
-#pragma unroll
-    for (int u = 0; u < kUQ; ++u) {
-      const int b = base + u * kB + g;
-      x[u] = b < n ? coef[(size_t)b * 16 + pq[u]] : 0;
-      sc[u] = qp[u]->scale[pq[u]];
-      of[u] = qp[u]->offset[pq[u]];
-      iv[u] = qp[u]->inv_scale[pq[u]];
-      cc[u] = (k == 0 && b < n) ? coeff_cost[b] : 0;
-    }
-#pragma unroll
-    for (int u = 0; u < kUQ; ++u) {
-      const int b = base + u * kB + g;
+    for (int u = 0; u < U; ++u) {
+      const int b = b4 + 4 * u + gw;
       const bool live = b < n;
-      const jmme_quant4x4_params &q = *qp[u];
-      const int q_bits = 15 + q.qp_per;                 // Q_BITS, defines.h:311
-      const int p = pq[u], xv = x[u];
+      if (uni) {
+        pq[u] = pq0; sc[u] = sc0; of[u] = of0; iv[u] = iv0; qper[u] = qper0; cavlc[u] = cavlc0; ck[u] = ck0;
+      } else {
+        const jmme_quant4x4_params &q = params[live ? param_idx[b] : 0];
+        pq[u] = q.scan[k][1] * 4 + q.scan[k][0];
+        sc[u] = q.scale[pq[u]]; of[u] = q.offset[pq[u]]; iv[u] = q.inv_scale[pq[u]];
+        qper[u] = q.qp_per; cavlc[u] = q.is_cavlc; ck[u] = q.c_cost[k];
+      }
+      x[u] = live ? coef[(size_t)b * 16 + pq[u]] : 0;
+      cc[u] = (k == 0 && live) ? coeff_cost[b] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int b = b4 + 4 * u + gw;
+      const bool live = b < n;
+      const int q_bits = 15 + qper[u];                  // Q_BITS, defines.h:311
+      const int xv = x[u];
       int level = xv == 0 ? 0 : (abs(xv) * sc[u] + of[u]) >> q_bits;
-      if (q.is_cavlc && level > 2063) level = 2063;     // CAVLC_LEVEL_LIMIT, defines.h:99
+      if (cavlc[u] && level > 2063) level = 2063;       // CAVLC_LEVEL_LIMIT, defines.h:99
       const unsigned mg = (unsigned)(__builtin_amdgcn_ballot_w64(level != 0) >> (16 * gw)) & 0xffffu;
       const unsigned below = mg & ((1u << k) - 1u);
-      const int idx = __builtin_popcount(below);
+      const int idx = __builtin_popcount(below), nnz = __builtin_popcount(mg);
       const int run = below ? k - (32 - __builtin_clz(below)) : k;   // positions since the previous nonzero
-      s_l[g][k] = 0;
-      s_r[g][k] = 0;
-      if (k == 0) s_l[g][16] = 0;
-      __syncthreads();
+      const int sl = xv < 0 ? -level : level;
+      const int crun = __builtin_amdgcn_ds_bpermute(4 * (16 * gw + run), ck[u]);   // c_cost[run]
       int term = 0, deq = 0;
       if (level) {
-        term = level > 1 ? 999999 : (int)q.c_cost[run];   // MAX_VALUE, defines.h:123
-        const int sl = xv < 0 ? -level : level;
-        deq = ((sl * iv[u] << q.qp_per) + 8) >> 4;   // rshift_rnd_sf(., 4)
-        s_l[g][idx] = sl;
-        s_r[g][idx] = run;
+        term = level > 1 ? 999999 : crun;                     // MAX_VALUE, defines.h:123
+        deq = ((sl * iv[u] << qper[u]) + 8) >> 4;             // rshift_rnd_sf(., 4)
       }
+      // compaction: nonzero lanes to slots 0..nnz-1 in scan order, zero lanes behind
+      const int dst = 16 * gw + (level ? idx : nnz + (k - idx));
+      const int lv = __builtin_amdgcn_ds_permute(4 * dst, level ? sl : 0);
+      const int rv = __builtin_amdgcn_ds_permute(4 * dst, level ? run : 0);
       term += __shfl_xor(term, 8, 64);
       term += __shfl_xor(term, 4, 64);
       term += __shfl_xor(term, 2, 64);
       term += __shfl_xor(term, 1, 64);
-      __syncthreads();
+      // the 4 blocks' level lists (17 dwords each, the entry past the last level 0) as one run
+      const int v0 = __builtin_amdgcn_ds_bpermute(4 * (16 * lj + (lpos & 15)), lv);
+      const int v1 = __builtin_amdgcn_ds_bpermute(4 * (16 * tj + (tpos & 15)), lv);
       if (live) {
-        coef[(size_t)b * 16 + p] = deq;   // (0 where x was 0: every lane stores, whole lines)
-        runs[(size_t)b * 16 + k] = s_r[g][k];
+        coef[(size_t)b * 16 + pq[u]] = deq;   // (0 where x was 0: every lane stores, whole lines)
+        runs[(size_t)b * 16 + k] = rv;
         if (k == 0) {
           coeff_cost[b] = cc[u] + term;
           nonzero[b] = mg != 0;
         }
       }
-      {
-        // the wave's 4 blocks' level lists are one contiguous run of 68
-        // dwords: lane l stores dword l, lanes 0-3 dwords 64-67
-        const int wl = threadIdx.x & 63, w4 = g & ~3, b0 = base + u * kB + w4;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int d = h * 64 + wl, j = d / 17;
-          if (d < 68 && b0 + j < n) levels[(size_t)b0 * 17 + d] = s_l[w4 + j][d - 17 * j];
-        }
-      }
-      __syncthreads();
+      const int w0 = b4 + 4 * u;   // the wave's first block this round
+      if (w0 + lj < n) levels[(size_t)w0 * 17 + lane] = lpos == 16 ? 0 : v0;
+      if (lane < 4 && w0 + tj < n) levels[(size_t)w0 * 17 + 64 + lane] = tpos == 16 ? 0 : v1;
     }
   }
 }
@@ -502,8 +514,14 @@ hipError_t launch_satd(int size, const int16_t *diff, int32_t *out, int n, hipSt
 
 hipError_t launch_quant4x4(const jmme_quant4x4_params *params, const int32_t *param_idx, int32_t *coef, int32_t *levels,
                            int32_t *runs, int32_t *coeff_cost, int32_t *nonzero, int n, hipStream_t s) {
-  hipLaunchKernelGGL(quant4x4_kernel, dim3(grid_for(n, kWG8 / 16 * kUQ)), dim3(kWG8), 0, s, params, param_idx, coef, levels, runs,
-                     coeff_cost, nonzero, n);
+  const int per_wg = kWG8 / 16 * (param_idx ? kUQ / 2 : kUQ), g = (n + per_wg - 1) / per_wg;
+  const dim3 grid(g < 1 ? 1 : (g > 65536 ? 65536 : g));
+  if (param_idx)
+    hipLaunchKernelGGL(quant4x4_kernel<false>, grid, dim3(kWG8), 0, s, params, param_idx, coef, levels, runs,
+                       coeff_cost, nonzero, n);
+  else
+    hipLaunchKernelGGL(quant4x4_kernel<true>, grid, dim3(kWG8), 0, s, params, param_idx, coef, levels, runs,
+                       coeff_cost, nonzero, n);
   return hipGetLastError();
 }
 

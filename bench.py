@@ -52,6 +52,28 @@ HBM_PEAK_GBS = 8000.0              # MI355X_MICROARCH.md (spec)
 VSAD_LANE_OPS = 35.5e12
 VSAD_PEAK = VSAD_LANE_OPS * 4
 
+
+def plan_items(req: np.ndarray) -> tuple[int, int]:
+    """(items, abs-diffs) the plan kernel makes of a batch: per unit, the searched
+    partitions with the same predictor, lambda, range and (FS) centre share one
+    window sweep (me_plan_kernel, csrc/jmme_search.hip); an item sweeps its
+    (2 rs + 1)^2 positions x 256 pels whatever partitions it serves.  The
+    work-normalised VALU fraction divides the kernel's time by THIS work, not by
+    one window per macroblock: JM's predictors give an adversarial frame's
+    macroblocks up to 41 windows each."""
+    items = absd = 0
+    for r in req:
+        mask = int(r["slot_mask"])
+        keys = set()
+        for s in range(41):
+            if (mask >> s) & 1:
+                b = r["blk"][s]
+                keys.add((int(b["pred_x"]), int(b["pred_y"]), int(b["lambda"]), int(b["search_range"]),
+                          int(b["center_x"]), int(b["center_y"])))
+        items += len(keys)
+        absd += sum((2 * k[3] + 1) ** 2 * 256 for k in keys)
+    return items, absd
+
 JM_CFG = """# minimal JM 18.5 lencod configuration written by bench.py (unlisted keys: JM defaults)
 ProfileIDC            = 66
 LevelIDC              = 40
@@ -282,9 +304,12 @@ def case_block(dev, local: int, case: str, workload: str, iters: int = 10) -> di
     exact = int(np.sum((out["mv_x"] == expect[0]) & (out["mv_y"] == expect[1]) & (out["cost"] == expect[2])))
     me.close()
     kernel_ms = float(np.mean(kms))
+    items, absd = plan_items(req)
     return {"workload": workload, "mb_per_step": n, "ms_per_frame": round(ms, 4),
             "kernel_ms": round(kernel_ms, 4), "mb_per_s": round(n / (ms * 1e-3), 1),
             "valu_frac": round(ABSDIFF_PER_UNIT * n / (kernel_ms * 1e-3) / VSAD_PEAK, 4),
+            "items_per_step": items,
+            "valu_frac_items": round(absd / (kernel_ms * 1e-3) / VSAD_PEAK, 4),
             "hbm_frac": round(ALG_BYTES_PER_UNIT * n / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6),
             "parity": {"reference": "JM 18.5 lencod (captured)", "searches": int(len(expect[0])),
                        "bit_exact": exact},
@@ -610,6 +635,7 @@ def main():
         value = job_value(n, args.steps, ws, wall)
         ms_per_step = wall * 1e3 / args.steps
         ach = ALG_BYTES_PER_UNIT * n / (kernel_ms * 1e-3) / 1e9
+        items_step, absd_step = plan_items(req)
         cpu = None
         if not args.no_cpu_baseline and ws == 1:       # the CPU baseline is an N=1 figure
             # every host core the GPU's share allows, each running JM (the headline
@@ -648,7 +674,11 @@ def main():
             "valu": {"achieved_absdiff_per_s": round(ABSDIFF_PER_UNIT * n / (kernel_ms * 1e-3), 1),
                      "peak_absdiff_per_s": VSAD_PEAK,
                      "peak_source": "measured v_sad_u8 rate (tools/ubench_valu.hip) x 4 abs-diffs",
-                     "frac": round(ABSDIFF_PER_UNIT * n / (kernel_ms * 1e-3) / VSAD_PEAK, 4)},
+                     "frac": round(ABSDIFF_PER_UNIT * n / (kernel_ms * 1e-3) / VSAD_PEAK, 4),
+                     "items_per_step": items_step,
+                     "frac_items": round(absd_step / (kernel_ms * 1e-3) / VSAD_PEAK, 4),
+                     "note": "frac: one (2R+1)^2 window per MB (SURVEY 8(d)); frac_items: the windows the plan "
+                             "kernel really sweeps (plan_items)"},
             "event_ms_per_step": round(ev_ms / args.steps, 4),
             "per_rank": [{"rank": r, "clip_seed": sd, "searches_checked": ck, "bit_exact": ex,
                           "reference": "JM 18.5 lencod (captured)" if kind == 0 else

@@ -362,6 +362,7 @@ static int8_t g_slot_bt[JMME_NSLOT], g_slot_bx[JMME_NSLOT], g_slot_by[JMME_NSLOT
 static void slot_geometry(void);
 static long long g_chain_sent = 0, g_chain_steps = 0, g_chain_hits = 0, g_chain_head_bad = 0;
 static long long g_chain_calls = 0, g_chain_call_fail = 0;
+static double g_t_chain = 0, g_t_sp = 0;   /* ms in chain-only calls / sub-pel batches (reported at exit) */
 static int g_chain_only = -1;   /* JMME_CHAIN_ONLY=0: a failed guess always re-batches */
 static int8_t g_grp[19][4], g_grp_n[19], g_slot_grp[JMME_NSLOT], g_slot_idx[JMME_NSLOT];
 
@@ -708,12 +709,14 @@ static const spec_ent *spec_lookup(Macroblock *currMB, MEBlock *mv_block, int li
      * macroblock's decided partitions as chains, the missing call first, and no
      * batch (the guesses for the macroblocks after this one stand).  A 16x16
      * miss says the guesses themselves are off: that one re-batches. */
+    double tc = now_us();
     g_n_chains = build_chains(currMB, list, ref, mb, s, want, 1);
     if (jmme_search_mbs_chains_sp(g_me, want->mode ? JMME_FAST_FULL_SEARCH : JMME_FULL_SEARCH, g_req, 0, g_res,
                                   g_chains, g_n_chains, g_chain_sp_on ? g_chain_sp : NULL, g_chres, g_chspres))
       fail_jm("jmme_search_mbs_chains_sp");
     ++g_chain_calls;
     store_chains(list, ref, want);
+    g_t_chain += now_us() - tc;
     e = &tab[spec_idx(mb, s, KHYP)];
     if (spec_same(e, want, g_slot_gen[list][ref])) return e;
     ++g_chain_call_fail;   /* (the chain stopped before it: a half-way centre or an oversized range) */
@@ -934,6 +937,7 @@ static void sp_batch(int list, int ref, int mb0, int s0, const sp_ent *w, int t8
   sp_ent *tab = g_sp[list][ref];
   int mb1 = imax(g_spec_end[list][ref], mb0 + 1), n = 0, i, s, k, mb;
   int count = (mb1 - mb0) * JMME_NSLOT * KHYP + 1;
+  double t0 = now_us();
   if (!g_slot_bt[0]) slot_geometry();
   if (count > g_sreq_cap) {
     free(g_sreq);
@@ -975,6 +979,7 @@ static void sp_batch(int list, int ref, int mb0, int s0, const sp_ent *w, int t8
     e->valid = g_slot_gen[list][ref];
   }
   ++g_sp_batches;
+  g_t_sp += now_us() - t0;
 }
 
 static sp_ent *sp_table(VideoParameters *p_Vid, int list, int ref)
@@ -1937,8 +1942,8 @@ static void report(void)
     fprintf(stderr, "jm_gpu_me: %lld integer-pel searches on the GPU (libjmme): %lld from %lld speculative "
                     "batches, the rest one call each; %lld on the CPU (non-SAD or weighted metric)\n",
             g_calls, g_hits + g_batches + g_chain_calls - g_chain_call_fail, g_batches, g_cpu_calls);
-    fprintf(stderr, "jm_gpu_me: %lld sub-pel refinements: %lld cached, %lld batches, %lld on the CPU\n",
-            g_sp_calls, g_sp_hits, g_sp_batches, g_sp_cpu);
+    fprintf(stderr, "jm_gpu_me: %lld sub-pel refinements: %lld cached, %lld batches, %lld on the CPU; "
+                    "%.1f ms in sub-pel batches\n", g_sp_calls, g_sp_hits, g_sp_batches, g_sp_cpu, g_t_sp * 1e-3);
     if (g_batches) {
       int s;
       fprintf(stderr, "jm_gpu_me: integer batches: %lld past the batch, %lld failed guesses; %lld units; "
@@ -1952,8 +1957,9 @@ static void report(void)
     }
     if (g_chain_sent)
       fprintf(stderr, "jm_gpu_me: chained guesses: %lld chains, %lld steps, %lld calls answered, %lld head mismatches; "
-                      "%lld chain-only calls (%lld fell back to a batch)\n",
-              g_chain_sent, g_chain_steps, g_chain_hits, g_chain_head_bad, g_chain_calls, g_chain_call_fail);
+                      "%lld chain-only calls (%lld fell back to a batch); %.1f ms in chain-only calls\n",
+              g_chain_sent, g_chain_steps, g_chain_hits, g_chain_head_bad, g_chain_calls, g_chain_call_fail,
+              g_t_chain * 1e-3);
     if (g_chain_sp_steps || g_chain_sp_nolam)
       fprintf(stderr, "jm_gpu_me: chained sub-pel: %lld refinements, %lld calls answered; %lld misses without "
                       "known sub-pel lambdas\n", g_chain_sp_steps, g_chain_sp_hits, g_chain_sp_nolam);

@@ -23,6 +23,15 @@ distblk __wrap_fast_full_search_motion_estimation(Macroblock *currMB, MotionVect
   return min_mcost;
 }
 
+/* sub_pel_motion_estimation (me_fullsearch.c:186-289): no refinement either,
+ * so the sub-pel-on rows have a floor too (the vector stays the integer one) */
+distblk __wrap_sub_pel_motion_estimation(Macroblock *currMB, MotionVector *pred_mv, MEBlock *mv_block,
+                                         distblk min_mcost, int *lambda_factor)
+{
+  (void)currMB; (void)pred_mv; (void)mv_block; (void)lambda_factor;
+  return min_mcost;
+}
+
 /* the fast-full-search surface JM would build on the CPU: not built */
 void __wrap_setup_fast_full_search(Macroblock *currMB, MEBlock *mv_block, int list)
 {

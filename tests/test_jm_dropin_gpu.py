@@ -170,3 +170,7 @@ def test_lencod_720p_ffs_subpel_speculative(gpu):
         assert (gpu264, gpurec) == (ref264, refrec)
         m = re.search(r"(\d+) sub-pel refinements: (\d+) cached, (\d+) batches, (\d+) on the CPU", r.stderr)
         assert m and int(m.group(1)) == 3600 * 41 and int(m.group(4)) == 0, r.stderr[-500:]
+        # the chains carry sub-pel steps (jmme_search_mbs_chains_sp): some of JM's
+        # refinements are answered from them, and none fell back to the CPU
+        c = re.search(r"chained sub-pel: (\d+) refinements, (\d+) calls answered", r.stderr)
+        assert c and int(c.group(1)) > 0 and int(c.group(2)) > 0, r.stderr[-800:]

@@ -212,13 +212,14 @@ def _lencod(binary, d, tag, yuv, w, h, frames, params, cfg_text, env=None):
                       r.stderr)
     stats = re.search(r"integer batches: (\d+) past the batch, (\d+) failed guesses; (\d+) units; ([0-9.]+) ms building, "
                       r"([0-9.]+) ms in jmme_search_mbs", r.stderr)
-    sp = re.search(r"(\d+) sub-pel refinements: (\d+) cached, (\d+) batches, (\d+) on the CPU", r.stderr)
+    sp = re.search(r"(\d+) sub-pel refinements: (\d+) cached, (\d+) batches, (\d+) on the CPU(?:; ([\d.]+) ms)?", r.stderr)
     ep = re.search(r"(\d+) EPZS searches on the GPU \(libjmme\); (\d+) on the CPU; (\d+) predictors, "
                    r"(\d+) pre-stamped map cells, (\d+) switches to window scans; ([\d.]+) ms in the EPZS wrapper, "
                    r"([\d.]+) ms in the engine", r.stderr)
     esp = re.search(r"(\d+) EPZS sub-pel refinements on the GPU \((\d+) chained[^)]*\), (\d+) on the CPU", r.stderr)
     ch = re.search(r"chained guesses: (\d+) chains, (\d+) steps, (\d+) calls answered, (\d+) head mismatches; "
-                   r"(\d+) chain-only calls \((\d+) fell back", r.stderr)
+                   r"(\d+) chain-only calls \((\d+) fell back[^;]*(?:; ([\d.]+) ms in chain-only calls)?", r.stderr)
+    chsp = re.search(r"chained sub-pel: (\d+) refinements, (\d+) calls answered; (\d+) misses without", r.stderr)
     res = dict(wall_s=round(wall, 3), me_s=float(me.group(1)) if me else None,
                md5=(hashlib.md5(open(out, "rb").read()).hexdigest(), hashlib.md5(open(rec, "rb").read()).hexdigest()))
     if calls:
@@ -230,9 +231,15 @@ def _lencod(binary, d, tag, yuv, w, h, frames, params, cfg_text, env=None):
                    engine_call_ms=float(stats.group(5)))
     if ch:
         res["chains"] = dict(zip(("chains", "steps", "calls_answered", "head_mismatches", "chain_only_calls",
-                                  "chain_only_fallbacks"), map(int, ch.groups())))
+                                  "chain_only_fallbacks"), map(int, ch.groups()[:6])))
+        if ch.group(7):
+            res["chains"]["chain_only_ms"] = float(ch.group(7))
+        if chsp:
+            res["chains"]["subpel"] = dict(zip(("refinements", "calls_answered", "no_lambdas"), map(int, chsp.groups())))
     if sp:
-        res["subpel"] = dict(zip(("calls", "cached", "batches", "cpu"), map(int, sp.groups())))
+        res["subpel"] = dict(zip(("calls", "cached", "batches", "cpu"), map(int, sp.groups()[:4])))
+        if sp.group(5):
+            res["subpel"]["batch_ms"] = float(sp.group(5))
     if ep:
         g = ep.groups()
         res["epzs"] = dict(gpu_searches=int(g[0]), cpu_searches=int(g[1]), predictors=int(g[2]),
@@ -320,7 +327,7 @@ def dropin_block(modes=None, size=(1920, 1080), search_range=32, reps=2, host_pr
             g = gs[len(gs) // 2]
             # JM's own loop around the search (integration/jm_noop_me.c: a zero-cost IntPelME)
             fl = _lencod(floor, d, f"floor_{tag}", yuv, w, h, frames, params, CFG) \
-                if mode in (-1, 0) and params.get("DisableSubpelME", 1) and os.path.exists(floor) else None
+                if mode in (-1, 0) and os.path.exists(floor) else None
             row = {
                 "stock_me_ms_per_p_frame": round(cpu["me_s"] * 1e3 / p, 2),
                 "dropin_me_ms_per_p_frame": round(g["me_s"] * 1e3 / p, 2),
