@@ -1351,7 +1351,8 @@ static distblk real_epzs(int variant, Macroblock *currMB, MotionVector *pred_mv,
  * call per search. */
 #define EP_MAXP 128                /* predictors of a list the cache keeps (longer lists: one call each) */
 #define EP_MAXV 64                 /* stamped cells kept per cached answer */
-#define EP_WAYS 4                  /* guesses per (macroblock, partition, reference) */
+#define EP_WAYS 6                  /* guesses per (macroblock, partition, reference): the sources' inputs,
+                                      then their second-pass forms (ep_pass2) */
 #define EP_REFS 4                  /* references speculated (list 0) */
 #define EP_BATCH_MAX 512
 
@@ -1397,7 +1398,12 @@ static long long g_ep_hits = 0, g_ep_batches = 0, g_ep_singles = 0, g_ep_guesses
 static long long g_ep_fail_bounds = 0, g_ep_fail_stale = 0, g_ep_fail_inputs = 0, g_ep_sp_hits = 0, g_ep_overflow = 0;
 static double g_t_ep_build = 0;
 static long long g_ep_miss_slot[JMME_NSLOT], g_ep_list_diff[JMME_NSLOT];   /* misses inside a batch, by slot */
+/* JMME_EPZS_TRACE: misses inside a batch by kind -- [0] no way with these inputs, [1] the stop criterion
+ * outside every equal way's interval, [2] prevSad outside, [3] map cells; and the stop misses by
+ * log2 of |real - guessed| (the guess's own stop criterion) */
+static long long g_ep_miss_kind[4], g_ep_stop_off[24];
 static int g_ep_trace = 0;   /* JMME_EPZS_TRACE=1: per-slot miss counts at exit */
+static int g_ep_two_pass = 1;   /* JMME_EPZS_PASS2=0: no second pass (ep_pass2) */
 
 static int ep_speculating(Macroblock *currMB, int cur_list, int ref, int n_pred)
 {
@@ -1405,6 +1411,10 @@ static int ep_speculating(Macroblock *currMB, int cur_list, int ref, int n_pred)
     const char *e = getenv("JMME_EPZS_SPECULATE"), *b = getenv("JMME_EPZS_BATCH"), *tr = getenv("JMME_EPZS_TRACE");
     g_ep_spec = !(e && e[0] == '0');
     g_ep_trace = tr && tr[0] == '1';
+    {
+      const char *p2 = getenv("JMME_EPZS_PASS2");
+      g_ep_two_pass = !(p2 && p2[0] == '0');
+    }
     if (b && atoi(b) > 0) g_ep_batch = imin(atoi(b), EP_BATCH_MAX);
   }
   if (!g_n_mb) {
@@ -1482,6 +1492,8 @@ static const ep_ans *ep_lookup(Macroblock *currMB, MEBlock *mv_block, const jmme
   ep_fill_in(ep_seen_at(mb, slot, ref), q, pred, cond, mb, gen);
   if (g_ep_gen != gen || mb < g_ep_mb0 || mb >= g_ep_mb1) return NULL;
   ++g_ep_miss_slot[slot];   /* (taken back below on a hit) */
+  int kind = 0;
+  int64_t stop_off = -1;
   for (w = 0; w < EP_WAYS; w++) {
     const int k = g_ep_idx[(((size_t)(mb - g_ep_mb0) * JMME_NSLOT + slot) * EP_REFS + ref) * EP_WAYS + w];
     const ep_ans *a;
@@ -1495,6 +1507,14 @@ static const ep_ans *ep_lookup(Macroblock *currMB, MEBlock *mv_block, const jmme
     if (q->stop_crit < a->bnd.stop_lo || q->stop_crit > a->bnd.stop_hi || q->prev_sad < a->bnd.prev_lo ||
         q->prev_sad > a->bnd.prev_hi || a->res.n_visited > EP_MAXV) {
       ++g_ep_fail_bounds;
+      if (q->stop_crit < a->bnd.stop_lo || q->stop_crit > a->bnd.stop_hi) {
+        const int64_t d = q->stop_crit > a->in.q.stop_crit ? q->stop_crit - a->in.q.stop_crit
+                                                           : a->in.q.stop_crit - q->stop_crit;
+        if (kind < 1) kind = 1;
+        if (stop_off < 0 || d < stop_off) stop_off = d;
+      } else if (q->prev_sad < a->bnd.prev_lo || q->prev_sad > a->bnd.prev_hi) {
+        if (kind < 2) kind = 2;
+      }
       continue;
     }
     for (i = 0; i < n_stale; i++) {   /* a cell JM already holds at this BlkCount: did the guess evaluate it? */
@@ -1505,6 +1525,7 @@ static const ep_ans *ep_lookup(Macroblock *currMB, MEBlock *mv_block, const jmme
     }
     if (i < n_stale) {
       ++g_ep_fail_stale;
+      kind = 3;
       continue;
     }
     ++g_ep_hits;
@@ -1512,6 +1533,12 @@ static const ep_ans *ep_lookup(Macroblock *currMB, MEBlock *mv_block, const jmme
     return a;
   }
   ++g_ep_fail_inputs;
+  ++g_ep_miss_kind[kind];
+  if (kind == 1) {
+    int b = 0;
+    while (b < 23 && (stop_off >> b) > 0) ++b;
+    ++g_ep_stop_off[b];
+  }
   return NULL;
 }
 
@@ -1576,16 +1603,18 @@ static void ep_add(int k, const ep_in *e, int pos_x, int pos_y, EPZSParameters *
   }
 }
 
-/* search requests 0..n-1 (the real call first, with its pre-stamped cells) and keep the answers */
-static void ep_run(int n, const int16_t *stale, int n_stale, unsigned gen)
+/* search requests k0..n-1 (request 0, the real call, with its pre-stamped cells) and keep the answers */
+static void ep_run_from(int k0, int n, const int16_t *stale, int n_stale, unsigned gen)
 {
   int k;
-  g_ep_q[0].n_stale = n_stale;
-  for (k = 0; k < n; k++) g_ep_spo[k].mv_x = g_ep_spo[k].mv_y = 0, g_ep_spo[k].cost = 0, g_ep_spo[k].reserved = 0;
-  if (jmme_epzs_speculate(g_me, g_ep_q, n, g_ep_ppool, g_ep_cpool, g_ep_np, stale, n_stale, g_ep_res, g_ep_bnd,
-                          g_ep_vbuf, EP_MAXV, g_ep_spq, g_ep_spo))
+  if (k0 >= n) return;
+  g_ep_q[k0].n_stale = k0 == 0 ? n_stale : 0;
+  for (k = k0; k < n; k++) g_ep_spo[k].mv_x = g_ep_spo[k].mv_y = 0, g_ep_spo[k].cost = 0, g_ep_spo[k].reserved = 0;
+  if (jmme_epzs_speculate(g_me, g_ep_q + k0, n - k0, g_ep_ppool, g_ep_cpool, g_ep_np, stale, k0 == 0 ? n_stale : 0,
+                          g_ep_res + k0, g_ep_bnd + k0, g_ep_vbuf + 2 * (size_t)EP_MAXV * k0, EP_MAXV, g_ep_spq + k0,
+                          g_ep_spo + k0))
     fail_jm("jmme_epzs_speculate");
-  for (k = 0; k < n; k++) {
+  for (k = k0; k < n; k++) {
     ep_ans *a = &g_ep_ans[k];
     const int16_t *pp = g_ep_ppool + 2 * (size_t)g_ep_q[k].pred_off;
     ep_fill_in(&a->in, &g_ep_q[k], pp, g_ep_cpool + g_ep_q[k].pred_off, -1, gen);
@@ -1600,6 +1629,120 @@ static void ep_run(int n, const int16_t *stale, int n_stale, unsigned gen)
     }
     a->sp_res = g_ep_spo[k];
   }
+}
+
+static void ep_run(int n, const int16_t *stale, int n_stale, unsigned gen) { ep_run_from(0, n, stale, n_stale, gen); }
+
+/* ---- second pass: the stop criterion and prevSad the batch's own answers imply
+ * A guess copies its stop criterion and prevSad from the call it was taken from,
+ * but JM derives them from the distortion row of its own neighbours
+ * (EPZSDetermineStopCriterion, me_epzs_common.c:1764-1780: the left, upper and
+ * upper-right 4x4 columns of p_EPZS->distortion[list][blocktype - 1], which
+ * every search writes at its own column when it updates prevSad).  After the
+ * first launch the adapter replays the batch in JM's order on a copy of that
+ * row -- JM's row as it stands, then each partition's first guess's answer --
+ * and searches again every guess whose intervals do not hold the replayed pair
+ * (one more launch).  Single slice, one reference, no 8x8 transform (JM's
+ * order of the partitions is then the chains' order, chain_groups). */
+static int64_t *g_ep_vrow = NULL;   /* [7][columns]: the replayed distortion rows */
+static int g_ep_vcols = 0;
+static long long g_ep_pass2 = 0, g_ep_pass2_batches = 0;
+
+static int ep_avail_c(int bx, int by, int bsx)   /* get_neighbors' upper-right rule inside the MB (mv_search.c:283-301) */
+{
+  if (by > 0) {
+    if (bx < 8) {
+      if (by == 8) return bsx != 16;
+      return bx + bsx != 8;
+    }
+    return bx + bsx != 16;
+  }
+  return 1;
+}
+
+static void ep_pass2(Macroblock *currMB, int mb0, int s0, int nmb, unsigned gen, int *n_io)
+{
+  VideoParameters *p_Vid = currMB->p_Vid;
+  InputParameters *p_Inp = currMB->p_Inp;
+  Slice *currSlice = currMB->p_Slice;
+  EPZSParameters *p_EPZS = currSlice->p_EPZS;
+  const int cols = p_Vid->width >> 2, n0 = *n_io;
+  int n = n0, x, g, i, bt, started = 0;
+  if (p_Inp->slice_mode || p_Inp->Transform8x8Mode || currSlice->listXsize[0] != 1) return;
+  if (!g_grp_n[0]) chain_groups();
+  if (cols > g_ep_vcols) {
+    free(g_ep_vrow);
+    g_ep_vrow = (int64_t *)malloc((size_t)7 * cols * sizeof(int64_t));
+    if (!g_ep_vrow) error("jm_gpu_me: out of memory", 500);
+    g_ep_vcols = cols;
+  }
+  for (bt = 1; bt <= 7; bt++)
+    for (i = 0; i < cols; i++) g_ep_vrow[(size_t)(bt - 1) * cols + i] = (int64_t)p_EPZS->distortion[0][bt - 1][i];
+  for (x = mb0; x < mb0 + nmb; x++) {
+    const int mbx = (x % g_mbs_x) * 16, mby = (x / g_mbs_x) * 16;
+    for (g = 0; g < 19; g++)
+      for (i = 0; i < g_grp_n[g]; i++) {
+        const int t = g_grp[g][i];
+        int *idx = &g_ep_idx[(((size_t)(x - mb0) * JMME_NSLOT + t) * EP_REFS + 0) * EP_WAYS];
+        const int bx = g_slot_bx[t], by = g_slot_by[t];
+        const int bsx = (g_slot_bt[t] <= 2) ? 16 : (g_slot_bt[t] <= 5) ? 8 : 4;
+        const int px = mbx + bx, py = mby + by, c = px >> 2, bs4 = bsx >> 2;
+        int64_t *row, sadA, sadB, sadC, stop, ld, prev;
+        int w, nw, k;
+        if (x == mb0 && !started) {   /* the slots before the missing one are JM's by now */
+          if (t != s0) continue;
+          started = 1;
+        }
+        bt = g_slot_bt[t];
+        row = &g_ep_vrow[(size_t)(bt - 1) * cols];
+        if (idx[0] < 0) continue;
+        {
+          const jmme_epzs_req *q0 = &g_ep_ans[idx[0]].in.q;
+          const int availA = px > 0, availB = py > 0;
+          const int avail2 = (py > 0 && px + bsx < p_Vid->width && ep_avail_c(bx, by, bsx)) || (px > 0 && py > 0);
+          ld = (int64_t)q0->lambda * ((q0->variant & 1) ? 3 : 2);
+          sadA = availA ? row[c - bs4] : JMME_DISTBLK_MAX;
+          sadB = availB ? row[c] : JMME_DISTBLK_MAX;
+          sadC = avail2 && c + bs4 < cols ? row[c + bs4] : JMME_DISTBLK_MAX;
+          stop = sadA < sadB ? sadA : sadB;
+          stop = sadC < stop ? sadC : stop;
+          stop = stop > (int64_t)p_EPZS->minthres[bt] ? stop : (int64_t)p_EPZS->minthres[bt];
+          stop = stop < (int64_t)p_EPZS->maxthres[bt] + ld ? stop : (int64_t)p_EPZS->maxthres[bt] + ld;
+          stop = (9 * ((int64_t)p_EPZS->medthres[bt] + ld > stop ? (int64_t)p_EPZS->medthres[bt] + ld : stop) +
+                  2 * (int64_t)p_EPZS->medthres[bt]) >> 3;
+          stop += ld;
+          prev = row[c];
+        }
+        for (nw = 0; nw < EP_WAYS && idx[nw] >= 0; nw++) {}
+        for (w = 0; w < nw && nw < EP_WAYS; w++) {
+          const ep_ans *a = &g_ep_ans[idx[w]];
+          if (idx[w] == 0 && x == mb0 && t == s0) continue;   /* the real call */
+          if (stop >= a->bnd.stop_lo && stop <= a->bnd.stop_hi && prev >= a->bnd.prev_lo && prev <= a->bnd.prev_hi)
+            continue;
+          for (k = 0; k < nw; k++) {   /* a way with these inputs that already holds the pair */
+            const ep_ans *o = &g_ep_ans[idx[k]];
+            if (k != w && stop >= o->bnd.stop_lo && stop <= o->bnd.stop_hi && prev >= o->bnd.prev_lo &&
+                prev <= o->bnd.prev_hi && ep_same(&o->in, &a->in.q, (const int16_t *)a->in.pred, a->in.cond))
+              break;
+          }
+          if (k < nw) continue;
+          ep_add(n, &a->in, px, py, p_EPZS);
+          g_ep_q[n].stop_crit = stop;
+          g_ep_q[n].prev_sad = prev;
+          idx[nw++] = n++;
+        }
+        {   /* the row after this partition: its first guess's answer (the real call's for the missing one) */
+          const ep_ans *a = &g_ep_ans[idx[0]];
+          if (a->bnd.prev_written) row[c] = a->res.cost;
+        }
+      }
+  }
+  if (n > n0) {
+    ep_run_from(n0, n, NULL, 0, gen);
+    g_ep_pass2 += n - n0;
+    ++g_ep_pass2_batches;
+  }
+  *n_io = n;
 }
 
 /* no guess fits: search the call alone, or start the next batch when it lies past the current one */
@@ -1674,6 +1817,7 @@ static const ep_ans *ep_miss(Macroblock *currMB, MEBlock *mv_block, const jmme_e
   }
   g_t_ep_build += now_us() - t0;
   ep_run(n, stale, n_stale, gen);
+  if (g_ep_two_pass) ep_pass2(currMB, mb, ep_slot_of(q), nmb, gen, &n);
   g_ep_n = n;
   g_ep_mb0 = mb;
   g_ep_mb1 = mb + nmb;
@@ -1972,13 +2116,18 @@ static void report(void)
     if (g_epzs_calls && g_ep_spec > 0)
       fprintf(stderr, "jm_gpu_me: EPZS speculation: %lld searches answered from %lld batches (%lld guesses), "
                       "%lld searched alone; %lld not speculated; guesses refused: %lld inputs, %lld bounds, "
-                      "%lld map cells; %.1f ms building batches; %lld searched again (more stamped cells than kept)\n",
+                      "%lld map cells; %.1f ms building batches; %lld searched again (more stamped cells than kept); "
+                      "%lld second-pass guesses in %lld launches\n",
               g_ep_hits, g_ep_batches, g_ep_guesses, g_ep_singles, g_ep_direct, g_ep_fail_inputs, g_ep_fail_bounds,
-              g_ep_fail_stale, g_t_ep_build * 1e-3, g_ep_overflow);
+              g_ep_fail_stale, g_t_ep_build * 1e-3, g_ep_overflow, g_ep_pass2, g_ep_pass2_batches);
     if (g_ep_trace) {
       int sl;
       fprintf(stderr, "jm_gpu_me: EPZS misses inside batches by slot (list-only differences):");
       for (sl = 0; sl < JMME_NSLOT; sl++) fprintf(stderr, " %d:%lld(%lld)", sl, g_ep_miss_slot[sl], g_ep_list_diff[sl]);
+      fprintf(stderr, "\njm_gpu_me: EPZS misses inside batches by kind: %lld inputs, %lld stop criterion, %lld prevSad, "
+                      "%lld map cells; stop misses by bits of |real - guessed|:",
+              g_ep_miss_kind[0], g_ep_miss_kind[1], g_ep_miss_kind[2], g_ep_miss_kind[3]);
+      for (sl = 0; sl < 24; sl++) fprintf(stderr, " %lld", g_ep_stop_off[sl]);
       fprintf(stderr, "\n");
     }
     if (g_epzs_sp_calls || g_epzs_sp_cpu)
