@@ -1360,7 +1360,8 @@ int prepare_subs(jmme_ctx *ctx, hipStream_t s);   // sub-pel section below
 namespace {
 int launch_epzs_ex(jmme_ctx *ctx, const jmme_epzs_req *d_req, int n, const int16_t *d_preds, const uint8_t *d_cond,
                    const int16_t *d_stale, jmme_epzs_res *d_out, int16_t *d_vis, int max_visited, hipStream_t s,
-                   jmme_epzs_bounds *d_bounds = nullptr, jmme_block_res *d_int = nullptr) {
+                   jmme_epzs_bounds *d_bounds = nullptr, jmme_block_res *d_int = nullptr,
+                   const jmme_subpel_req *d_fused_req = nullptr, jmme_block_res *d_fused_out = nullptr) {
   if (sync_ref_table(ctx, s)) return -1;
   EpzsParams p{};
   p.cur = ctx->d_cur;
@@ -1392,6 +1393,24 @@ int launch_epzs_ex(jmme_ctx *ctx, const jmme_epzs_req *d_req, int n, const int16
   p.max_visited = max_visited;
   p.bounds = d_bounds;
   p.int_out = d_int;
+  if (d_fused_req) {   // each wave refines its own answer (jmme_epzs_speculate's small launches)
+    if (prepare_subs(ctx, s)) return -1;
+    const SubGeom g = sub_geom(ctx->width, ctx->height);
+    p.fused = 1;
+    p.fused_sp.cur = ctx->d_cur;
+    p.fused_sp.cur_pitch = ctx->pitch;
+    p.fused_sp.width = ctx->width;
+    p.fused_sp.height = ctx->height;
+    p.fused_sp.hbd = ctx->hbd ? 1 : 0;
+    p.fused_sp.subs = ctx->d_sub_table;
+    p.fused_sp.sub_pitch = g.pitch;
+    p.fused_sp.plane_stride = g.plane_stride;
+    p.fused_sp.req = d_fused_req;
+    p.fused_sp.int_res = nullptr;
+    p.fused_sp.out = d_fused_out;
+    p.fused_sp.n = n;
+    p.fused_sp.per_wave = 1;
+  }
   HIPCHK(launch_epzs(p, s));
   return 0;
 }
@@ -1533,6 +1552,7 @@ extern "C" int jmme_epzs_search_ex(jmme_ctx *ctx, const jmme_epzs_req *req, int 
 }
 
 static_assert(sizeof(jmme_epzs_bounds) == 40, "EPZS bounds ABI layout");
+constexpr int kEpzsFuseMax = 16;   // jmme_epzs_speculate launches of at most this many searches fuse the refinement
 
 extern "C" int jmme_epzs_speculate(jmme_ctx *ctx, const jmme_epzs_req *req, int n, const int16_t *preds,
                                    const uint8_t *pred_cond, int n_preds, const int16_t *stale, int n_stale,
@@ -1603,8 +1623,13 @@ extern "C" int jmme_epzs_speculate(jmme_ctx *ctx, const jmme_epzs_req *req, int 
     h_spo = reinterpret_cast<jmme_block_res *>(h + o);
   }
   hipStream_t s = nullptr;
-  if (launch_epzs_ex(ctx, d_req, n, d_preds, d_cond, d_stale, d_out, d_vis, max_visited, s, d_bnd, d_int)) return -1;
-  if (sp_req && jmme_subpel_refine_async(ctx, d_spq, n, d_int, d_spo, s)) return -1;
+  // a few searches (the drop-in's searches alone): each wave refines its own
+  // answer in the same launch; batches: the 16-refinements-per-wave kernel after it
+  const bool fuse = sp_req && n <= kEpzsFuseMax;
+  if (launch_epzs_ex(ctx, d_req, n, d_preds, d_cond, d_stale, d_out, d_vis, max_visited, s, d_bnd, d_int,
+                     fuse ? d_spq : nullptr, fuse ? d_spo : nullptr))
+    return -1;
+  if (sp_req && !fuse && jmme_subpel_refine_async(ctx, d_spq, n, d_int, d_spo, s)) return -1;
   HIPCHK(hipStreamSynchronize(s));
   std::memcpy(out, h_out, (size_t)n * sizeof(jmme_epzs_res));
   std::memcpy(bounds, h_bnd, (size_t)n * sizeof(jmme_epzs_bounds));

@@ -22,6 +22,9 @@
 #include "jmme.h"
 #include "jmme_common.h"
 #include "jmme_epzs_internal.h"
+#include "jmme_subpel_dev.h"
+
+#include <type_traits>
 
 namespace jmme {
 
@@ -298,8 +301,8 @@ __device__ __forceinline__ bool le2(int64_t pr, int64_t st, Iv &pv, Iv &sv) {
 }
 
 template <bool GRID, bool HBD>
-__device__ void search_one(const EpzsParams &p, const jmme_epzs_req &q, WaveLds &w, uint32_t *map, int lane,
-                           jmme_epzs_res *out) {
+__device__ jmme_block_res search_one(const EpzsParams &p, const jmme_epzs_req &q, WaveLds &w, uint32_t *map, int lane,
+                                     jmme_epzs_res *out) {
   Search s;
   s.ref = GRID ? p.subs[q.ref_slot] : p.refs[q.ref_slot];
   s.pitch = GRID ? p.sub_pitch : p.pitch;
@@ -645,6 +648,20 @@ __device__ void search_one(const EpzsParams &p, const jmme_epzs_req &q, WaveLds 
     }
   }
   wave_sync();
+  jmme_block_res br;   // (wave-uniform) the answer as the refinement takes it
+  br.mv_x = (int16_t)tmpx;
+  br.mv_y = (int16_t)tmpy;
+  br.reserved = 0;
+  br.cost = best;
+  return br;
+}
+
+// the fused path: this wave refines its own answer (a separate kernel
+// instance, so the batch kernel's register allocation is not touched)
+template <typename T>
+__device__ __forceinline__ void refine_fused(const SubpelParams &sp, spd::WaveLds<T> &L, int lane, int t,
+                                          jmme_block_res br) {
+  spd::refine_wave<T>(sp, L, lane, t, &br);
 }
 
 #ifndef JMME_EPZS_WAVES_PER_EU
@@ -652,10 +669,12 @@ __device__ void search_one(const EpzsParams &p, const jmme_epzs_req &q, WaveLds 
 #endif
 // the search is latency-bound (a few dependent cache-resident fetch rounds
 // per search): waves in flight matter more than a few spilled registers
-template <bool GRID, bool HBD>
+template <bool GRID, bool HBD, bool FUSED>
 __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(JMME_EPZS_WAVES_PER_EU))) void epzs_kernel(
     EpzsParams p) {
+  using SpT = std::conditional_t<HBD, uint16_t, uint8_t>;
   __shared__ WaveLds s_w[kWaves];
+  __shared__ spd::WaveLds<SpT> s_sp[FUSED ? kWaves : 1];
   extern __shared__ uint32_t s_map[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint32_t *map = s_map + (size_t)wave * p.map_words;
@@ -664,7 +683,9 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(JMME_EPZS_W
     // requests of the other grid, or with a window the map was not sized for, are refused
     const bool ok = (GRID ? q.variant >= 2 : q.variant <= 1) && q.max_x <= p.max_qpel && q.max_y <= p.max_qpel;
     if (ok) {
-      search_one<GRID, HBD>(p, q, s_w[wave], map, lane, p.out + t);
+      const jmme_block_res br = search_one<GRID, HBD>(p, q, s_w[wave], map, lane, p.out + t);
+      if (FUSED && p.fused_sp.req[t].blocktype) refine_fused<SpT>(p.fused_sp, s_sp[FUSED ? wave : 0], lane, t, br);
+      (void)br;
     } else if (lane == 0) {
       jmme_epzs_res r{};
       r.path = -1;
@@ -685,8 +706,10 @@ hipError_t launch_epzs(const EpzsParams &p, hipStream_t s) {
   if (grid > 8192) grid = 8192;
   if (grid < 1) grid = 1;
   const size_t lds = (size_t)kWaves * p.map_words * sizeof(uint32_t);
-  auto k = p.grid ? (p.hbd ? epzs_kernel<true, true> : epzs_kernel<true, false>)
-                  : (p.hbd ? epzs_kernel<false, true> : epzs_kernel<false, false>);
+  auto k = p.fused ? (p.grid ? (p.hbd ? epzs_kernel<true, true, true> : epzs_kernel<true, false, true>)
+                             : (p.hbd ? epzs_kernel<false, true, true> : epzs_kernel<false, false, true>))
+                   : (p.grid ? (p.hbd ? epzs_kernel<true, true, false> : epzs_kernel<true, false, false>)
+                             : (p.hbd ? epzs_kernel<false, true, false> : epzs_kernel<false, false, false>));
   if (lds > 65536) {   // sub-pel grid beyond R = 45: one workgroup may take up to 160 KiB
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)lds);

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "jmme.h"
+#include "jmme_subpel_internal.h"
 
 namespace jmme {
 
@@ -36,6 +37,12 @@ struct EpzsParams {
   // refinement (null: not written)
   jmme_epzs_bounds *bounds;
   jmme_block_res *int_out;
+  // fused refinement (small speculative launches): the wave that searched
+  // request t runs its EPZS sub-pel refinement fused_sp.req[t] itself, from its
+  // own answer, into fused_sp.out[t] (fused = 0: none; the caller chains the
+  // refinement kernel instead)
+  int fused;
+  SubpelParams fused_sp;
 };
 
 size_t epzs_map_words(bool grid, int max_qpel);

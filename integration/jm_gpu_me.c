@@ -1714,18 +1714,19 @@ static void ep_pass2(Macroblock *currMB, int mb0, int s0, int nmb, unsigned gen,
           prev = row[c];
         }
         for (nw = 0; nw < EP_WAYS && idx[nw] >= 0; nw++) {}
-        for (w = 0; w < nw && nw < EP_WAYS; w++) {
+        const int nw0 = nw;   /* the first pass's ways (the ones added here are searched after the loop) */
+        for (w = 0; w < nw0 && nw < EP_WAYS; w++) {
           const ep_ans *a = &g_ep_ans[idx[w]];
           if (idx[w] == 0 && x == mb0 && t == s0) continue;   /* the real call */
           if (stop >= a->bnd.stop_lo && stop <= a->bnd.stop_hi && prev >= a->bnd.prev_lo && prev <= a->bnd.prev_hi)
             continue;
-          for (k = 0; k < nw; k++) {   /* a way with these inputs that already holds the pair */
+          for (k = 0; k < nw0; k++) {   /* a way with these inputs that already holds the pair */
             const ep_ans *o = &g_ep_ans[idx[k]];
             if (k != w && stop >= o->bnd.stop_lo && stop <= o->bnd.stop_hi && prev >= o->bnd.prev_lo &&
                 prev <= o->bnd.prev_hi && ep_same(&o->in, &a->in.q, (const int16_t *)a->in.pred, a->in.cond))
               break;
           }
-          if (k < nw) continue;
+          if (k < nw0) continue;
           ep_add(n, &a->in, px, py, p_EPZS);
           g_ep_q[n].stop_crit = stop;
           g_ep_q[n].prev_sad = prev;

@@ -135,3 +135,44 @@ def test_chained_subpel_equals_separate_calls(grid, gpu):
         sep = me.subpel_refine(want[on])
     assert np.array_equal(spo[on], sep)
     assert np.array_equal(spo[~on], np.zeros((~on).sum(), BLOCK_RES))
+
+
+@pytest.mark.parametrize("grid", [False, True])
+def test_fused_refinement_of_small_launches(grid, gpu):
+    """launches of at most 16 searches refine in the searching wave itself
+    (epzs_kernel<..., FUSED>): the same answers and refinements as one big launch
+    that chains the refinement kernel"""
+    from jmme import SP_TEST8x8, SUBPEL_REQ, MotionEstimator
+    rng, cur, refs, req, preds, stale, cond = _scene(11, grid, 240)
+    n = len(req)
+    sp = np.zeros(n, SUBPEL_REQ)
+    sp["pos_x"], sp["pos_y"], sp["blocktype"] = req["pos_x"], req["pos_y"], req["blocktype"]
+    sp["ref_slot"] = req["plane"]
+    sp["pred_x"], sp["pred_y"] = req["pred_x"], req["pred_y"]
+    sp["lambda_h"] = rng.choice([0, 40, 187], n)
+    sp["lambda_q"] = rng.choice([0, 40, 187], n)
+    sp["subthres"] = rng.choice([0, 2048, 16384, DMAX], n)
+    sp["variant"] = 1
+    sp["metric_h"] = rng.integers(0, 3, n)
+    sp["metric_q"] = rng.integers(0, 3, n)
+    sp["start_hp"] = rng.integers(0, 2, n)
+    sp["start_qp"] = rng.integers(0, 2, n)
+    sp["search_pos2"] = sp["search_pos4"] = 9
+    big = (req["bsx"] >= 8) & (req["bsy"] >= 8)
+    sp["flags"] = np.where(big & (rng.random(n) < 0.5), SP_TEST8x8, 0)
+    sp["blocktype"][rng.random(n) < 0.1] = 0
+    cfg = {"EPZSSubPelGrid": 1, "SearchRange": 32, "SearchMode": 3} if grid else {}
+    q = _req_for_engine(req)
+    with MotionEstimator(cfg) as me:
+        me.upload_cur(cur)
+        for k, r in enumerate(refs):
+            me.upload_ref(0, k, r)
+        got, gb, gv, spo = me.epzs_speculate(q, preds, cond, stale, max_visited=64, sp_req=sp)
+        for size in (1, 5, 16):
+            for a in range(0, 48, size):
+                sl = slice(a, a + size)
+                g2, b2, v2, s2 = me.epzs_speculate(q[sl], preds, cond, stale, max_visited=64, sp_req=sp[sl])
+                for k in ("mv_x", "mv_y", "path", "cost", "prev_sad"):
+                    assert np.array_equal(g2[k], got[sl][k]), (size, a, k)
+                on = sp[sl]["blocktype"] != 0
+                assert np.array_equal(s2[on], spo[sl][on]), (size, a)
