@@ -493,9 +493,9 @@ int sync_ref_table(jmme_ctx *ctx, hipStream_t s) {
 int launch(jmme_ctx *ctx, int mode, const uint8_t *d_cur, const uint8_t *const *d_ref_table, int pitch,
            int w, int h, const jmme_mb_req *d_req, int n, jmme_block_res *d_out, hipStream_t s,
            uint32_t *debug_words = nullptr, bool planes_8bit = false) {
-  if (ctx->hbd && !planes_8bit)
-    return fail("SourceBitDepthLuma %d: the batched item kernel reads 8-bit planes; high bit depth is served by "
-                "jmme_search_mbs (host arrays)", ctx->cfg.SourceBitDepthLuma);
+  // high bit depth: the context's 16-bit planes go to the 64-bit-key v_sad_u16
+  // instance of the item kernel; explicitly 8-bit planes to the 8-bit one
+  const bool hbd = ctx->hbd && !planes_8bit;
   if (mode != JMME_FULL_SEARCH && mode != JMME_FAST_FULL_SEARCH)
     return fail("search mode %d not supported by the batched engine (FS=-1, FFS=0)", mode);
   if (n < 0) return fail("negative unit count");
@@ -513,7 +513,8 @@ int launch(jmme_ctx *ctx, int mode, const uint8_t *d_cur, const uint8_t *const *
   p.mode = mode;
   p.max_mvd = ctx->max_mvd;
   p.lds_range = ctx->cfg.SearchRange;
-  p.key32 = p.lds_range <= kKey32MaxRange;
+  p.key32 = !hbd && p.lds_range <= kKey32MaxRange;
+  p.hbd = hbd ? 1 : 0;
   p.items = ctx->d_items;
   p.item_cap = (unsigned)ctx->cap_items;
   p.counts = ctx->d_counts + ctx->counts_half * kCountWords;
@@ -686,7 +687,6 @@ int search_small(jmme_ctx *ctx, int mode, const jmme_mb_req *req, int n, jmme_bl
   // exactly; high bit depth has no other path, so it fails loudly.
   for (const SmallItem &it : items)
     if ((uint64_t)it.lam * 64u + ((uint64_t)256 * ctx->max_pel << 5) >= (1ull << 32)) {
-      if (ctx->hbd) return fail("lambda %d too large for the high-bit-depth search", it.lam);
       return 0;
     }
   if (items.size() > ctx->cap_sitems) {
@@ -824,8 +824,9 @@ extern "C" int jmme_search_mbs(jmme_ctx *ctx, int mode, const jmme_mb_req *req, 
   hipStream_t s = nullptr;
   // a batch of a few units: the low-latency path (one launch, no copies)
   if (mode == JMME_FULL_SEARCH || mode == JMME_FAST_FULL_SEARCH) {
-    // high bit depth: every batch on the 16-bit small kernel
-    const int r = search_small(ctx, mode, req, n, out, s, ctx->hbd);
+    // (high bit depth too: small batches on the 16-bit small kernel, the rest on
+    // the 16-bit item kernel)
+    const int r = search_small(ctx, mode, req, n, out, s);
     if (r != 0) return r < 0 ? -1 : 0;
   }
   if (ctx->phases) ++ctx->ph_big;

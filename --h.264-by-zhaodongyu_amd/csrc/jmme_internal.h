@@ -60,6 +60,7 @@ struct KParams {
                                       // (no memset launch per search)
   uint32_t *debug_words;              // debug: unit 0's first staged window (rows x wp words)
   unsigned long long *stamps;         // diagnostic builds (JMME_STAMPS): per-unit phase clocks
+  int hbd;                            // 16-bit planes (pitch in samples): the 64-bit-key v_sad_u16 instance
 };
 // status bits (counts[2]): bit 0 range > lds_range, bit 1 sub-pel centre, bit 2 refine lost a winner
 
@@ -126,7 +127,7 @@ struct ChainParams {
 size_t chain_lds_bytes(int max_r, bool hbd = false);
 hipError_t launch_search_chains(const ChainParams &p, hipStream_t s);
 
-size_t items_lds_bytes(int lds_range);
+size_t items_lds_bytes(int lds_range, bool hbd = false);
 // plan (unit requests -> items), then the persistent 32-bit and 64-bit item
 // kernels; ev0/ev1 (optional) bracket the main search kernel
 hipError_t launch_search(const KParams &p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1);

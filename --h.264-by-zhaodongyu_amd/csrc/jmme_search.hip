@@ -103,16 +103,24 @@ struct Lds {
 // the sweep (its row offsets then fold into the ds_read2 offset fields)
 constexpr int kWP32 = 80;
 __host__ __device__ inline int words_pitch(int R) { return R <= 32 ? kWP32 : 4 * ((2 * R + 13 + 3) / 4); }
+// 16-bit planes (SourceBitDepthLuma 9..14, KEY32 = false only): word[y][x] =
+// samples x, x + 1 (a 4-sample chunk is words x and x + 2), 2R + 15 words a
+// row, expanded in groups of 4 from the raw dwords of 2 samples each
+__host__ __device__ inline int groups16(int R) { return (2 * R + 15 + 3) / 4; }
+__host__ __device__ inline int words_pitch16(int R) { return R <= 32 ? kWP32 : 4 * groups16(R); }
+__host__ __device__ inline int raw_row_dwords16(int R) { return 2 * groups16(R) + 2; }
+constexpr int kRawExtra16 = 128;   // the current MB: 16 rows x 8 dwords
 
 // one layout for the kernel (carve) and the host (items_lds_bytes)
 struct LdsPlan { size_t words, raw, red, tx, ty, spec, ctr, tmax, fb, total; };
-__host__ __device__ inline LdsPlan lds_plan(int R) {
+__host__ __device__ inline LdsPlan lds_plan(int R, bool hbd = false) {
   LdsPlan q;
-  const int rows = 2 * R + 16, wp = words_pitch(R), d = 2 * R + 1;
+  const int rows = 2 * R + 16, wp = hbd ? words_pitch16(R) : words_pitch(R), d = 2 * R + 1;
   size_t off = 0;
   auto take = [&](size_t bytes) { const size_t at = off; off = (off + bytes + 15) & ~(size_t)15; return at; };
   q.words = take((size_t)rows * wp * 4);
-  q.raw = take(((size_t)rows * raw_row_dwords(R) + kRawExtra) * 4);
+  q.raw = take(hbd ? ((size_t)rows * raw_row_dwords16(R) + kRawExtra16) * 4
+                   : ((size_t)rows * raw_row_dwords(R) + kRawExtra) * 4);
   q.red = take((size_t)kWaves * kNS * 8);
   q.tx = take((size_t)d * 16);
   q.ty = take((size_t)d * 16);
@@ -124,10 +132,10 @@ __host__ __device__ inline LdsPlan lds_plan(int R) {
   return q;
 }
 
-__device__ __forceinline__ Lds carve(unsigned char *smem, int R) {
+__device__ __forceinline__ Lds carve(unsigned char *smem, int R, bool hbd = false) {
   Lds L;
-  const LdsPlan q = lds_plan(R);
-  L.wp = words_pitch(R);
+  const LdsPlan q = lds_plan(R, hbd);
+  L.wp = hbd ? words_pitch16(R) : words_pitch(R);
   L.wv = (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   L.words = reinterpret_cast<uint32_t *>(smem + q.words);
   L.raw = reinterpret_cast<uint32_t *>(smem + q.raw);
@@ -430,12 +438,21 @@ __global__ __launch_bounds__(64 * kPlanWaves) void me_plan_kernel(KParams p) {
 // ------------------------------------------------------------ item kernels --
 struct Win { int R, x0, y0, wrows, wpr, xa, sh, nd; bool inner; };
 
+template <bool HBD = false>
 __device__ __forceinline__ Win win_of(const KParams &p, const Item &it) {
   Win w;
   w.R = it.R;
   w.x0 = it.mb_x + (it.cqx >> 2) - w.R;
   w.y0 = it.mb_y + (it.cqy >> 2) - w.R;
   w.wrows = 2 * w.R + 16;
+  if (HBD) {   // two samples a dword: words 0 .. 2R+14, fetched from the even sample at or below x0
+    w.wpr = 2 * w.R + 15;
+    w.xa = w.x0 & ~1;
+    w.sh = w.x0 - w.xa;                    // 0..1
+    w.nd = raw_row_dwords16(w.R);
+    w.inner = w.xa >= 0 && w.xa + 2 * w.nd <= p.width;
+    return w;
+  }
   w.wpr = 2 * w.R + 13;                    // words per window row
   w.xa = w.x0 & ~3;                        // dword-aligned start (floor)
   w.sh = w.x0 - w.xa;                      // 0..3
@@ -460,9 +477,32 @@ __device__ __forceinline__ void lds_dma_dword(const void *gptr, uint32_t lds) {
 // picture, dword columns clamped into it -- UMVLine4X) and its current MB.  global_load_lds: per-lane global address, LDS destination
 // contiguous per wave instruction; completion is awaited (vmcnt) only at the
 // top of the next item.
+template <bool HBD = false>
 __device__ __forceinline__ void prefetch(const KParams &p, const Item &it, const Lds &L) {
   if (!it.gmask) return;
   const int tid = opaque_tid(L), lane = tid & 63, wave = ufl(tid >> 6);
+  if constexpr (HBD) {   // 16-bit: pitch in samples, dword d of a row = samples xa + 2d, +1 (clamped dwords)
+    const Win w = win_of<true>(p, it);
+    const uint16_t *ref = reinterpret_cast<const uint16_t *>(p.refs[it.ref]);
+    const int total = w.wrows * w.nd, w2 = p.width >> 1, xq = w.xa >> 1;
+    const int k = 64 / w.nd;
+    const int dr = lane / w.nd, d = lane - dr * w.nd;
+    const bool act = dr < k;
+    const uint16_t *col = ref + 2 * clampi(xq + d, 0, w2 - 1);
+    for (int r = wave * k; r < w.wrows; r += kWaves * k) {
+      const int rr = r + dr;
+      if (act && rr < w.wrows) {
+        const int gy = clampi(w.y0 + rr, 0, p.height - 1);
+        lds_dma_dword(col + (size_t)gy * p.pitch, (uint32_t)ufl((int)lds_addr(L.raw + r * w.nd)));
+      }
+    }
+    if (wave < 2) {   // the current MB: 16 rows x 8 dwords, rows 8 * wave ..
+      const int r = 8 * wave + (lane >> 3), c = lane & 7;
+      lds_dma_dword(reinterpret_cast<const uint16_t *>(p.cur) + (size_t)(it.mb_y + r) * p.pitch + it.mb_x + 2 * c,
+                    (uint32_t)ufl((int)lds_addr(L.raw + total + 64 * wave)));
+    }
+    return;
+  }
   const Win w = win_of(p, it);
   const uint8_t *ref = p.refs[it.ref];
   const int total = w.wrows * w.nd;
@@ -511,6 +551,61 @@ __device__ __forceinline__ void expand_inner(const uint32_t *src, uint32_t *dst,
     *reinterpret_cast<u32x4 *>(dst + r * wp) = v;   // ds_write_b128 (conflict-free: consecutive lanes, consecutive 16 B)
     if (rn >= wrows) break;
     r = rn; d0 = e0; d1 = e1; d2 = e2;
+  }
+}
+
+// 16-bit: word x = samples x, x+1 of the window; the 4 words of group g come
+// from raw dwords 2g .. 2g+2 (inner), or per sample through v_perm (edges)
+__device__ __forceinline__ void expand16(const KParams &p, const Item &it, const Lds &L) {
+  const int tid = opaque_tid(L);
+  const Win w = win_of<true>(p, it);
+  const uint32_t *tail = L.raw + w.wrows * w.nd;
+  if (tid < 128) L.cur[tid] = tail[tid];
+  const int ng = (w.wpr + 3) >> 2;
+  const int rstep = kWG / ng;
+  const int r0 = tid / ng, g = tid - r0 * ng;
+  if (r0 >= rstep) return;
+  uint32_t *dst = L.words + 4 * g;
+  if (w.inner) {
+    for (int r = r0; r < w.wrows; r += rstep) {
+      const uint32_t *rw = L.raw + r * w.nd + 2 * g;
+      const uint32_t d0 = rw[0], d1 = rw[1], d2 = rw[2];
+      u32x4 v;
+      if (w.sh == 0) {
+        v[0] = d0; v[1] = __builtin_amdgcn_alignbyte(d1, d0, 2); v[2] = d1; v[3] = __builtin_amdgcn_alignbyte(d2, d1, 2);
+      } else {
+        v[0] = __builtin_amdgcn_alignbyte(d1, d0, 2); v[1] = d1; v[2] = __builtin_amdgcn_alignbyte(d2, d1, 2); v[3] = d2;
+      }
+      *reinterpret_cast<u32x4 *>(dst + r * L.wp) = v;
+    }
+  } else {
+    // sample x of the window is picture column gx = clamp(x0 + x, 0, W-1) (UMVLine4X),
+    // in fetched dword clamp(gx/2 - xa/2, 0, nd-1), half gx & 1
+    const int xq = w.xa >> 1;
+    int dq[4];
+    uint32_t sel[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int c = 4 * g + k;
+      const int q0 = clampi((clampi(w.x0 + c, 0, p.width - 1) >> 1) - xq, 0, w.nd - 1);
+      dq[k] = min(q0, w.nd - 2);
+      uint32_t sl = 0;
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int gx = clampi(w.x0 + c + b, 0, p.width - 1);
+        const int q = clampi((gx >> 1) - xq, 0, w.nd - 1);
+        const uint32_t byte0 = (uint32_t)(4 * (q - dq[k]) + 2 * (gx & 1));
+        sl |= (byte0 | ((byte0 + 1) << 8)) << (16 * b);
+      }
+      sel[k] = sl;
+    }
+    for (int r = r0; r < w.wrows; r += rstep) {
+      const uint32_t *rw = L.raw + r * w.nd;
+      u32x4 v;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = __builtin_amdgcn_perm(rw[dq[k] + 1], rw[dq[k]], sel[k]);
+      *reinterpret_cast<u32x4 *>(dst + r * L.wp) = v;
+    }
   }
 }
 
@@ -1079,7 +1174,7 @@ struct ItemStamps {
 };
 
 // sweep + reduce + refine + output of one item whose window is in L.words
-template <bool KEY32, bool FFS>
+template <bool KEY32, bool FFS, bool HBD = false>
 __device__ __forceinline__ void search_item(const KParams &p, const Item &it, const Lds &L, bool fast,
                                             const uint32_t (&cs)[64], unsigned *tick, unsigned *s_tick
 #ifdef JMME_STAMPS
@@ -1130,7 +1225,59 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
       uint32_t a0[16], a1[16];
 #pragma unroll
       for (int k = 0; k < 16; ++k) { a0[k] = 0; a1[k] = 0; }
-      {
+      if constexpr (HBD) {
+        // 16-bit samples: a 4x4 block row is words 4c and 4c+2 against the current
+        // row's dwords 2c, 2c+1 (two v_sad_u16), the same one-row-ahead pipeline
+        uint32_t zero;
+        asm volatile("v_mov_b32 %0, 0" : "=v"(zero));
+        const uint32_t wrow = lds_addr(L.words) + 4u * (uint32_t)(yb * L.wp + tx);
+        const uint32_t rowb = 4u * (uint32_t)L.wp;
+        const uint32_t cb = lds_addr(curw) + zero;
+        auto rd_row = [&](uint32_t a, uint32_t (&w)[8]) {
+          const lds_u32 *q = (const lds_u32 *)(uintptr_t)a;
+#pragma unroll
+          for (int m = 0; m < 8; ++m) w[m] = q[2 * m];
+        };
+        auto rd_cur = [&](uint32_t a, uint32_t (&c)[8]) {
+          const u32x4 lo = ds_read_b128(a), hi = ds_read_b128(a + 16u);
+          c[0] = lo.x; c[1] = lo.y; c[2] = lo.z; c[3] = lo.w; c[4] = hi.x; c[5] = hi.y; c[6] = hi.z; c[7] = hi.w;
+        };
+        uint32_t nw[8], nc[8], cprev[8];
+        rd_row(wrow, nw);
+        rd_cur(cb, nc);
+#pragma unroll
+        for (int m = 0; m < 8; ++m) cprev[m] = 0;
+#pragma unroll
+        for (int r = 0; r < 17; ++r) {
+          uint32_t w[8], c[8];
+#pragma unroll
+          for (int m = 0; m < 8; ++m) { w[m] = nw[m]; c[m] = nc[m]; }
+          if (r < 16) {
+            rd_row(wrow + (uint32_t)(r + 1) * rowb, nw);
+            if (r < 15) rd_cur(cb + 32u * (uint32_t)(r + 1), nc);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          if (r < 16) {   // row r of the MB against position y
+            const int b = (r >> 2) * 4;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              a0[b + q] = __builtin_amdgcn_sad_u16(w[2 * q + 1], c[2 * q + 1],
+                                                   __builtin_amdgcn_sad_u16(w[2 * q], c[2 * q], a0[b + q]));
+          }
+          if (r > 0) {    // row r-1 of the MB against position y+1
+            const int b = ((r - 1) >> 2) * 4;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              a1[b + q] = __builtin_amdgcn_sad_u16(w[2 * q + 1], cprev[2 * q + 1],
+                                                   __builtin_amdgcn_sad_u16(w[2 * q], cprev[2 * q], a1[b + q]));
+          }
+#pragma unroll
+          for (int m = 0; m < 8; ++m) cprev[m] = c[m];
+          __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int k = 0; k < 16; ++k) asm volatile("" : "+v"(a0[k]), "+v"(a1[k]));
+      } else {
         // opaque zero: keeps the broadcast reads of the current MB inside the
         // loop instead of letting LICM pin 64 VGPRs for them
         uint32_t zero;
@@ -1401,10 +1548,11 @@ __device__ __forceinline__ Item load_item(const Item *items, unsigned j) {
 // for the item after next while it serves an item, so the index is in LDS by
 // the next item's first barrier.  Every ticket below the run's end is served by
 // the workgroup that drew it: tickets are only drawn while a next item exists.
-template <bool KEY32, bool FFS>
+template <bool KEY32, bool FFS, bool HBD = false>
 __global__ __launch_bounds__(kWG, KEY32 ? JMME_WAVES_PER_EU : 2) void me_items_kernel(KParams p) {
+  static_assert(!(HBD && KEY32), "16-bit planes take the 64-bit keys");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  __shared__ __attribute__((aligned(16))) uint32_t s_cur[64];
+  __shared__ __attribute__((aligned(16))) uint32_t s_cur[HBD ? 128 : 64];
   __shared__ unsigned s_tick;
   const unsigned cnt = (unsigned)p.n + p.counts[0];   // first groups, then the further groups
   const Item *items = p.items;
@@ -1421,7 +1569,7 @@ __global__ __launch_bounds__(kWG, KEY32 ? JMME_WAVES_PER_EU : 2) void me_items_k
   const unsigned dyn0 = 2u * (unsigned)nbx;               // ticket t serves item dyn0 + t
   unsigned *const tick = p.counts + 8 + x;
 
-  Lds L = carve(smem, p.lds_range);
+  Lds L = carve(smem, p.lds_range, HBD);
   L.cur = s_cur;
   const unsigned long long dbg_slot =
       p.debug_words ? (1ull << __builtin_ctzll((ufl64(p.req[0].slot_mask) & kAll) | (1ull << 63))) : 0ull;
@@ -1430,7 +1578,7 @@ __global__ __launch_bounds__(kWG, KEY32 ? JMME_WAVES_PER_EU : 2) void me_items_k
 #endif
 
   Item it = load_item(items, item_at(j));
-  prefetch(p, it, L);
+  prefetch<HBD>(p, it, L);
 #ifdef JMME_STAMPS
   // per-workgroup record behind the per-unit ones: start / end (s_memrealtime,
   // 100 MHz), HW_ID, XCC_ID, items served
@@ -1453,12 +1601,15 @@ __global__ __launch_bounds__(kWG, KEY32 ? JMME_WAVES_PER_EU : 2) void me_items_k
     STAMP(st.wait);
     const bool fast = it.gmask && item_fast<KEY32, FFS>(p, it);
 #ifndef JMME_ABL_NOEXPAND   // timing ablation only: the window stays as the previous item left it
-    if (it.gmask) expand(p, it, L);
+    if (it.gmask) {
+      if constexpr (HBD) expand16(p, it, L);
+      else expand(p, it, L);
+    }
 #endif
     if (fast) build_tabs<FFS>(it, L);
     __syncthreads();
     if (p.debug_words && it.u == 0 && (it.gmask & dbg_slot)) {
-      const Win w = win_of(p, it);
+      const Win w = win_of<HBD>(p, it);
       for (int i = opaque_tid(L); i < w.wrows * w.wpr; i += kWG) {
         const int r = i / w.wpr;
         p.debug_words[i] = L.words[r * L.wp + i - r * w.wpr];
@@ -1466,13 +1617,13 @@ __global__ __launch_bounds__(kWG, KEY32 ? JMME_WAVES_PER_EU : 2) void me_items_k
     }
     STAMP(st.expand);
     // the raw buffer is free: start fetching the next item behind this sweep
-    if (more) prefetch(p, nx, L);
+    if (more) prefetch<HBD>(p, nx, L);
     bool ticketed = false;
     if (it.gmask) {
       // the current MB into SGPRs: every v_sad of the v5 sweep takes it as
       // its scalar operand
       uint32_t cs[64];
-      {
+      if constexpr (!HBD) {
         // straight from the current picture (s_load_dwordx4 per MB row)
         const uint8_t *mb = p.cur + (size_t)it.mb_y * p.pitch + it.mb_x;
 #pragma unroll
@@ -1481,15 +1632,18 @@ __global__ __launch_bounds__(kWG, KEY32 ? JMME_WAVES_PER_EU : 2) void me_items_k
           cs[4 * r + 0] = (uint32_t)q.x; cs[4 * r + 1] = (uint32_t)q.y;
           cs[4 * r + 2] = (uint32_t)q.z; cs[4 * r + 3] = (uint32_t)q.w;
         }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 64; ++k) cs[k] = 0;   // (the v5 sweep's operand: 8-bit only)
       }
       if (KEY32 && (it.flags & kItemSlow64)) {
         search_item_slow64<FFS>(p, it, L);
       } else {
         ticketed = true;
 #ifdef JMME_STAMPS
-        search_item<KEY32, FFS>(p, it, L, fast, cs, more ? tick : nullptr, &s_tick, t_last, st);
+        search_item<KEY32, FFS, HBD>(p, it, L, fast, cs, more ? tick : nullptr, &s_tick, t_last, st);
 #else
-        search_item<KEY32, FFS>(p, it, L, fast, cs, more ? tick : nullptr, &s_tick);
+        search_item<KEY32, FFS, HBD>(p, it, L, fast, cs, more ? tick : nullptr, &s_tick);
 #endif
       }
     }
@@ -2126,7 +2280,7 @@ __global__ __launch_bounds__(kChainWG) void chain_kernel(ChainParams p) {
 
 struct Occupancy {
   int cus = 0;
-  int wg[4][JMME_MAX_RANGE + 1] = {};   // resident workgroups per CU, by kernel variant and lds range
+  int wg[6][JMME_MAX_RANGE + 1] = {};   // resident workgroups per CU, by kernel variant and lds range
 };
 
 template <typename K>
@@ -2144,7 +2298,7 @@ int resident_grid(Occupancy &o, int dev, int variant, K kernel, int lds_range, s
 
 }  // namespace
 
-size_t items_lds_bytes(int R) { return lds_plan(R).total; }
+size_t items_lds_bytes(int R, bool hbd) { return lds_plan(R, hbd).total; }
 
 #ifdef JMME_CHAIN_PROF
 }  // namespace jmme
@@ -2173,7 +2327,7 @@ hipError_t launch_search(const KParams &p, hipStream_t s, hipEvent_t ev0, hipEve
   (void)hipGetDevice(&dev);
   Occupancy spare;
   Occupancy &occ = (dev >= 0 && dev < kMaxDev) ? occ_tab[dev] : spare;
-  const size_t lds = items_lds_bytes(p.lds_range);
+  const size_t lds = items_lds_bytes(p.lds_range, p.hbd != 0);
   const bool ffs = p.mode == JMME_FAST_FULL_SEARCH;
   const int plan_grid = (p.n + kPlanWaves - 1) / kPlanWaves;
   if (ffs) hipLaunchKernelGGL(me_plan_kernel<true>, dim3(plan_grid), dim3(64 * kPlanWaves), 0, s, p);
@@ -2184,7 +2338,21 @@ hipError_t launch_search(const KParams &p, hipStream_t s, hipEvent_t ev0, hipEve
   auto k64 = ffs ? me_items_kernel<false, true> : me_items_kernel<false, false>;
   const int v = ffs ? 2 : 0;
   if (ev0) (void)hipEventRecord(ev0, s);
-  if (p.key32) {
+  if (p.hbd) {   // 16-bit planes: 64-bit keys, the generic sweep with v_sad_u16 (the plan routes no 32-bit items)
+    auto k16 = ffs ? me_items_kernel<false, true, true> : me_items_kernel<false, false, true>;
+    if (lds > 65536) {   // 16-bit staging above R = 36: raise the kernel's dynamic-LDS limit (once per instance)
+      static thread_local bool raised[2] = {false, false};
+      if (!raised[ffs]) {
+        if ((e = hipFuncSetAttribute(reinterpret_cast<const void *>(k16), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)lds)) != hipSuccess)
+          return e;
+        raised[ffs] = true;
+      }
+    }
+    hipLaunchKernelGGL(k16, dim3(resident_grid(occ, dev, 4 + v / 2, k16, p.lds_range, lds)), dim3(kWG), lds, s, p);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (ev1) (void)hipEventRecord(ev1, s);
+  } else if (p.key32) {
     // (units whose lambda is beyond the 32-bit keys are served in this kernel
     // too, by the exact per-partition search: no second launch)
     hipLaunchKernelGGL(k32, dim3(resident_grid(occ, dev, v, k32, p.lds_range, lds)), dim3(kWG), lds, s, p);

@@ -69,3 +69,25 @@ def read_yuv420_luma(path: str, width: int, height: int, frames: int | None = No
     for t in range(n):
         out[t] = data[t * fsize:t * fsize + width * height].reshape(height, width)
     return out
+
+
+def luma_sequence_hbd(width: int, height: int, frames: int, bits: int, seed: int = 1234,
+                      gmv: tuple[int, int] = (5, 3), adversarial: bool = False) -> np.ndarray:
+    """uint16 [frames, height, width] luma at `bits` (9..14): the 8-bit clip scaled
+    by 2^(bits-8) plus seeded low-order noise that only a high-bit-depth search sees."""
+    luma = luma_sequence(width, height, frames, seed=seed, gmv=gmv, adversarial=adversarial).astype(np.int32)
+    sh = bits - 8
+    rng = np.random.default_rng(seed + 0x10B17)
+    return np.clip((luma << sh) + rng.integers(0, 1 << sh, size=luma.shape), 0, (1 << bits) - 1).astype(np.uint16)
+
+
+def write_yuv420_16(path: str, luma: np.ndarray, bits: int) -> None:
+    """Planar I420 with 16-bit little-endian samples (JM reads two bytes per
+    sample above 8 bits); chroma mid-grey."""
+    f, h, w = luma.shape
+    grey = np.full((h // 2, w // 2), 1 << (bits - 1), np.uint16).astype("<u2").tobytes()
+    with open(path, "wb") as fp:
+        for t in range(f):
+            fp.write(luma[t].astype("<u2").tobytes())
+            fp.write(grey)
+            fp.write(grey)

@@ -269,6 +269,7 @@ def subpel_block(dev, local: int, iters: int = 20) -> dict | None:
 
 UHD_CASE = "c2_syn_4k_fs32"
 ADV_CASE = "c2_syn_1080p_adv_fs32"
+HBD_CASE = "c2_syn_1080p_fs32_10bit"
 
 
 def case_block(dev, local: int, case: str, workload: str, iters: int = 10) -> dict | None:
@@ -283,7 +284,10 @@ def case_block(dev, local: int, case: str, workload: str, iters: int = 10) -> di
         return None
     cur, ref, req, unit_of, slots, expect, meta = load_workload(case)
     n = len(req)
-    me = MotionEstimator({"SearchRange": 32, "SearchMode": -1, "RDOptimization": 0}, device=local)
+    cfg = {"SearchRange": 32, "SearchMode": -1, "RDOptimization": 0}
+    if meta.get("bits", 8) > 8:   # 16-bit planes: the 64-bit-key v_sad_u16 item kernel
+        cfg["SourceBitDepthLuma"] = meta["bits"]
+    me = MotionEstimator(cfg, device=local)
     me.upload_cur(cur)
     me.upload_ref(0, 0, ref)
     d_req = torch.from_numpy(req.view(np.uint8).copy()).to(dev)
@@ -319,6 +323,16 @@ def case_block(dev, local: int, case: str, workload: str, iters: int = 10) -> di
 def uhd_block(dev, local: int, iters: int = 10) -> dict | None:
     return case_block(dev, local, UHD_CASE, "4K (3840x2160) FS +-32 SAD integer-pel, 1 ref, 32,400 MB x ref per "
                                             "frame, JM 18.5's own requests", iters)
+
+
+def hbd_block(dev, local: int, iters: int = 10) -> dict | None:
+    """configs[1] at 10 bits (High 10: JM's uint16 planes hold 10-bit samples):
+    JM 18.5's own requests for the seeded clip at 10 bits, parity vs JM's capture.
+    HBM bytes per unit double (16-bit samples); the VALU fraction is against the
+    same v_sad_u8 ceiling, so a v_sad_u16 pass (half the samples per op) reads
+    about half of it."""
+    return case_block(dev, local, HBD_CASE, "1080p FS +-32 SAD integer-pel at 10 bits (SourceBitDepthLuma 10), "
+                                            "1 ref, 8160 MB x ref, JM 18.5's own requests", iters)
 
 
 def adversarial_block(dev, local: int, iters: int = 10) -> dict | None:
@@ -545,6 +559,7 @@ def main():
     ap.add_argument("--no-subpel", action="store_true")
     ap.add_argument("--no-uhd", action="store_true")
     ap.add_argument("--no-adversarial", action="store_true")
+    ap.add_argument("--no-hbd", action="store_true")
     ap.add_argument("--no-fractal", action="store_true", help="skip the configs[2] block (fractal full pool)")
     ap.add_argument("--no-hybrid", action="store_true", help="skip the configs[4] block (joint codec frame)")
     ap.add_argument("--no-dropin", action="store_true", help="skip the in-encoder block (lencod vs lencod_jmme)")
@@ -557,7 +572,8 @@ def main():
                          "each frame's planes over RCCL and every rank searches an MB-row band (strong)")
     args = ap.parse_args()
     if args.headline_only:
-        for k in ("no_cpu_baseline", "no_subpel", "no_uhd", "no_adversarial", "no_fractal", "no_hybrid", "no_dropin"):
+        for k in ("no_cpu_baseline", "no_subpel", "no_uhd", "no_adversarial", "no_hbd", "no_fractal", "no_hybrid",
+                  "no_dropin"):
             setattr(args, k, True)
 
     ws, rank, local = dist_env()
@@ -692,6 +708,8 @@ def main():
             line["uhd"] = uhd_block(dev, local)
         if not args.no_adversarial and ws == 1:
             line["adversarial"] = adversarial_block(dev, local)
+        if not args.no_hbd and ws == 1:
+            line["hbd"] = hbd_block(dev, local)
         if not args.no_fractal and ws == 1:
             import bench_blocks
             line["fractal"] = bench_blocks.fractal_block(dev, local)

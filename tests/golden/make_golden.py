@@ -81,6 +81,14 @@ CASES = {
                                      "RDOptimization": 0, "MDDistortion": 0, **INT_PEL},
                                   keep="compact"),
     # the same configuration at 4K (3840x2160, 32,400 MB x ref per P-frame): the bench's UHD block
+    # the headline configuration at 10 bits (High 10, SourceBitDepthLuma 10): JM's uint16
+    # imgpel planes hold 10-bit samples; the 16-bit search paths' parity fixture
+    "c2_syn_1080p_fs32_10bit": dict(src="synth", w=1920, h=1080, frames=2, seed=2024, gmv=(5, 3), bits=10,
+                                    p={"ProfileIDC": 110, "SourceBitDepthLuma": 10, "SourceBitDepthChroma": 10,
+                                       "OutputBitDepthLuma": 10, "OutputBitDepthChroma": 10,
+                                       "SearchMode": -1, "SearchRange": 32, "NumberReferenceFrames": 1,
+                                       "RDOptimization": 0, "MDDistortion": 0, **INT_PEL},
+                                    keep="compact"),
     "c2_syn_4k_fs32": dict(src="synth", w=3840, h=2160, frames=2, seed=4096, gmv=(5, 3),
                            p={"LevelIDC": 51, "SearchMode": -1, "SearchRange": 32, "NumberReferenceFrames": 1,
                               "RDOptimization": 0, "MDDistortion": 0, **INT_PEL},
@@ -100,6 +108,11 @@ def run_case(name: str, spec: dict, work: str) -> dict:
     w, h, frames = spec["w"], spec["h"], spec["frames"]
     if spec["src"] == "foreman":
         yuv = FOREMAN
+    elif spec.get("bits", 8) > 8:
+        yuv = os.path.join(work, f"{name}.yuv")
+        synth.write_yuv420_16(yuv, synth.luma_sequence_hbd(w, h, frames, spec["bits"], seed=spec["seed"],
+                                                           gmv=spec["gmv"], adversarial=spec.get("adversarial", False)),
+                              spec["bits"])
     else:
         yuv = os.path.join(work, f"{name}.yuv")
         luma = synth.luma_sequence(w, h, frames, seed=spec["seed"], gmv=spec["gmv"],
@@ -128,8 +141,12 @@ def run_case(name: str, spec: dict, work: str) -> dict:
 def coded_synth(spec: dict) -> np.ndarray:
     """The synthetic clip as JM codes it: height padded to a multiple of 16 by
     repeating the last row (JM/lencod/src/lencod.c:463-474 auto-crop)."""
-    luma = synth.luma_sequence(spec["w"], spec["h"], spec["frames"], seed=spec["seed"], gmv=spec["gmv"],
-                               adversarial=spec.get("adversarial", False))
+    if spec.get("bits", 8) > 8:
+        luma = synth.luma_sequence_hbd(spec["w"], spec["h"], spec["frames"], spec["bits"], seed=spec["seed"],
+                                       gmv=spec["gmv"], adversarial=spec.get("adversarial", False))
+    else:
+        luma = synth.luma_sequence(spec["w"], spec["h"], spec["frames"], seed=spec["seed"], gmv=spec["gmv"],
+                                   adversarial=spec.get("adversarial", False))
     hc = (spec["h"] + 15) // 16 * 16
     wc = (spec["w"] + 15) // 16 * 16
     return np.pad(luma, ((0, 0), (0, hc - spec["h"]), (0, wc - spec["w"])), mode="edge")
@@ -140,9 +157,11 @@ def save_case(name: str, spec: dict, r: dict) -> dict:
     cur_keys = sorted(k for k in planes if k[1] == 0)
     ref_keys = sorted(k for k in planes if k[1] == 1)
     allp = [planes[k] for k in cur_keys + ref_keys]
-    assert max(int(p.max()) for p in allp) <= 255, "8-bit content expected"
-    cur = np.stack([planes[k] for k in cur_keys]).astype(np.uint8)
-    ref = np.stack([planes[k] for k in ref_keys]).astype(np.uint8)
+    bits = spec.get("bits", 8)
+    assert max(int(p.max()) for p in allp) < (1 << bits), f"{bits}-bit content expected"
+    pel = np.uint8 if bits == 8 else np.uint16
+    cur = np.stack([planes[k] for k in cur_keys]).astype(pel)
+    ref = np.stack([planes[k] for k in ref_keys]).astype(pel)
     arrays = {
         "cur_frame_no": np.array([k[0] for k in cur_keys], np.int32),
         "ref_key": np.array([[k[0], k[2], k[3]] for k in ref_keys], np.int32),
@@ -154,9 +173,13 @@ def save_case(name: str, spec: dict, r: dict) -> dict:
         # are stored as an int8 residual against the generator's original.
         orig = coded_synth(spec)
         assert all(np.array_equal(cur[i], orig[f]) for i, f in enumerate(arrays["cur_frame_no"]))
-        res = ref.astype(np.int16) - orig[arrays["ref_key"][:, 0] - 1 - arrays["ref_key"][:, 2]]
-        assert res.min() >= -128 and res.max() <= 127
-        arrays["ref_residual"] = res.astype(np.int8)
+        res = ref.astype(np.int32) - orig[arrays["ref_key"][:, 0] - 1 - arrays["ref_key"][:, 2]]
+        if bits == 8:
+            assert res.min() >= -128 and res.max() <= 127
+            arrays["ref_residual"] = res.astype(np.int8)
+        else:
+            assert res.min() >= -32768 and res.max() <= 32767
+            arrays["ref_residual"] = res.astype(np.int16)
     else:
         arrays["cur"] = cur
         arrays["ref"] = ref
@@ -165,7 +188,7 @@ def save_case(name: str, spec: dict, r: dict) -> dict:
     path = os.path.join(HERE, f"{name}.npz")
     np.savez_compressed(path, **arrays)
     return dict(case=name, w=spec["w"], h=spec["h"], frames=spec["frames"], cfg_overrides=spec["p"],
-                src=spec["src"], seed=spec.get("seed"), gmv=spec.get("gmv"),
+                src=spec["src"], seed=spec.get("seed"), gmv=spec.get("gmv"), bits=spec.get("bits", 8),
                 adversarial=spec.get("adversarial", False), n_searches=int(len(recs)),
                 md5_bitstream=r["md5_264"], md5_recon=r["md5_rec"], md5_input=r["md5_input"],
                 jm_me_time=r["me_time"], jm_cmd=r["cmd"], bytes=os.path.getsize(path))

@@ -35,6 +35,7 @@ class Case:
         from jmme import synth
         self.name = name
         self.meta = manifest()[name]
+        self.bits = self.meta.get("bits", 8)
         z = np.load(os.path.join(GOLDEN, f"{name}.npz"))
         self.r = {k[2:]: z[k] for k in z.files if k.startswith("r_")}
         self.n = len(next(iter(self.r.values())))
@@ -45,13 +46,18 @@ class Case:
             ref = z["ref"]
         else:
             m = self.meta
-            luma = synth.luma_sequence(m["w"], m["h"], m["frames"], seed=m["seed"], gmv=tuple(m["gmv"]),
-                                       adversarial=m["adversarial"])
+            bits = m.get("bits", 8)
+            if bits > 8:
+                luma = synth.luma_sequence_hbd(m["w"], m["h"], m["frames"], bits, seed=m["seed"], gmv=tuple(m["gmv"]),
+                                               adversarial=m["adversarial"])
+            else:
+                luma = synth.luma_sequence(m["w"], m["h"], m["frames"], seed=m["seed"], gmv=tuple(m["gmv"]),
+                                           adversarial=m["adversarial"])
             hc, wc = (m["h"] + 15) // 16 * 16, (m["w"] + 15) // 16 * 16
             orig = np.pad(luma, ((0, 0), (0, hc - m["h"]), (0, wc - m["w"])), mode="edge")
             cur = orig[cur_fn]
-            ref = (orig[ref_key[:, 0] - 1 - ref_key[:, 2]].astype(np.int16)
-                   + z["ref_residual"].astype(np.int16)).astype(np.uint8)
+            ref = (orig[ref_key[:, 0] - 1 - ref_key[:, 2]].astype(np.int32)
+                   + z["ref_residual"].astype(np.int32)).astype(np.uint8 if bits == 8 else np.uint16)
         for c, h in zip(cur, z["cur_md5"]):
             if hashlib.md5(c.tobytes()).hexdigest() != str(h):
                 raise AssertionError(f"{name}: regenerated current frame does not match the fixture md5")

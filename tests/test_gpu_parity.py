@@ -19,7 +19,10 @@ CASES = g.cases()
 def _engine(case, gpu):
     from jmme import MotionEstimator
     ov = g.manifest()[case.name]["cfg_overrides"]
-    return MotionEstimator({"SearchRange": ov["SearchRange"], "SearchMode": ov["SearchMode"]})
+    cfg = {"SearchRange": ov["SearchRange"], "SearchMode": ov["SearchMode"]}
+    if case.bits > 8:   # a high-bit-depth capture (JM's uint16 planes hold `bits`-bit samples)
+        cfg["SourceBitDepthLuma"] = case.bits
+    return MotionEstimator(cfg)
 
 
 def _run_case(c, me, mode):

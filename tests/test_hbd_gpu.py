@@ -1,8 +1,10 @@
 """GPU: high-bit-depth luma (SourceBitDepthLuma 9..14; JM's imgpel is uint16,
 JM/lencod/inc/defines.h:37, JM/lcommon/inc/typedefs.h:30-40).  A context created
 with SourceBitDepthLuma > 8 keeps its planes 16-bit on the device and serves
-every full / fast full search batch with the v_sad_u16 small kernel
-(csrc/jmme_search.hip me_small_kernel<FFS, true>).  Checked against the oracle
+its full / fast full search batches with the v_sad_u16 kernels: small batches
+on the small kernel (csrc/jmme_search.hip me_small_kernel<FFS, true>), the rest
+on the 64-bit-key instance of the item kernel (me_items_kernel<false, FFS,
+true>); `path` forces one or the other.  Checked against the oracle
 (oracle/me_oracle.c, which reads uint16 planes as JM does) on random requests,
 against the 8-bit path on 8-bit content, at 14-bit extremes, and on the
 refusals of the 8-bit-only paths."""
@@ -33,29 +35,37 @@ def _cmp(out, keys, mv, cost):
     assert len(bad) == 0, [(keys[i], got[i].tolist(), exp[i].tolist()) for i in bad[:5]]
 
 
+def _path(me, path):
+    me.set_small_batch_limit(0 if path == "items" else 1 << 20)
+
+
+@pytest.mark.parametrize("path", ["small", "items"])
 @pytest.mark.parametrize("bits,size,R", [(10, (352, 288), 16), (10, (176, 144), 32), (12, (128, 96), 7),
                                          (14, (96, 64), 3)])
-def test_hbd_full_search_vs_oracle(bits, size, R, gpu):
+def test_hbd_full_search_vs_oracle(bits, size, R, path, gpu):
     from jmme import FULL_SEARCH, MotionEstimator
     w, h = size
     cur, ref = _planes(w, h, bits, seed=bits + R)[::-1]
     rng = np.random.default_rng(bits * 100 + R)
     req = _random_units(rng, w, h, 12, R, lam_max=4000)
     with MotionEstimator({"SearchRange": max(R, 1), "SearchMode": -1, "SourceBitDepthLuma": bits}) as me:
+        _path(me, path)
         me.upload_cur(cur)
         me.upload_ref(0, 0, ref)
         out = me.search(FULL_SEARCH, req)
     _cmp(out, *_oracle_units(cur, ref, req))
 
 
+@pytest.mark.parametrize("path", ["small", "items"])
 @pytest.mark.parametrize("R,rdopt,far", [(16, 0, 0.0), (8, 1, 0.4)])
-def test_hbd_fast_full_search_vs_oracle(R, rdopt, far, gpu):
+def test_hbd_fast_full_search_vs_oracle(R, rdopt, far, path, gpu):
     from jmme import FAST_FULL_SEARCH, MotionEstimator
     w, h = 352, 288
     cur, ref = _planes(w, h, 10, seed=R + rdopt)[::-1]
     rng = np.random.default_rng(7 * R + rdopt)
     req, mbs, blk = _ffs_random(rng, w, h, 12, R, rdopt, far)
     with MotionEstimator({"SearchRange": R, "SearchMode": 0, "RDOptimization": rdopt, "SourceBitDepthLuma": 10}) as me:
+        _path(me, path)
         me.upload_cur(cur)
         me.upload_ref(0, 0, ref)
         out = me.search(FAST_FULL_SEARCH, req)
@@ -82,16 +92,20 @@ def test_hbd_path_equals_8bit_path_on_8bit_content(gpu):
     assert np.array_equal(res[0], res[1])
 
 
-def test_hbd_extremes_14bit(gpu):
+@pytest.mark.parametrize("path,lam_max", [("small", 60000), ("items", 60000), ("items", 2000000)])
+def test_hbd_extremes_14bit(path, lam_max, gpu):
     """14-bit planes at both ends of the range (SAD of a 16x16 block near 2^22)
-    and a large lambda: the 32-bit costs of the small kernel do not wrap"""
+    and a large lambda: the 32-bit costs of the small kernel do not wrap; a
+    lambda the small kernel's 32-bit costs cannot hold goes to the item kernel's
+    64-bit keys"""
     from jmme import FULL_SEARCH, MotionEstimator
     w, h, R = 64, 64, 4
     rng = np.random.default_rng(3)
     cur = np.where(rng.random((h, w)) < 0.5, 0, 16383).astype(np.uint16)
     ref = (16383 - cur).astype(np.uint16)
-    req = _random_units(rng, w, h, 6, R, lam_max=60000)
+    req = _random_units(rng, w, h, 6, R, lam_max=lam_max)
     with MotionEstimator({"SearchRange": R, "SearchMode": -1, "SourceBitDepthLuma": 14}) as me:
+        _path(me, path)
         me.upload_cur(cur)
         me.upload_ref(0, 0, ref)
         out = me.search(FULL_SEARCH, req)

@@ -49,7 +49,9 @@ def test_fixture_inputs_are_what_jm_read():
         c = g.Case(name)
         assert c.n == g.manifest()[name]["n_searches"]
         for (f, lst, rf), p in c.ref.items():
-            assert p.dtype == np.uint8 and p.shape == c.cur[f].shape
+            # 8-bit captures as uint8; high-bit-depth ones as JM's uint16 imgpel, within the depth
+            assert p.dtype == (np.uint8 if c.bits == 8 else np.uint16) and p.shape == c.cur[f].shape
+            assert int(p.max()) < (1 << c.bits)
 
 
 def test_golden_covers_the_edge_cases():
