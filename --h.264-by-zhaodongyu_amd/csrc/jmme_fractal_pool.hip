@@ -321,7 +321,7 @@ __global__ __launch_bounds__(kPoolWG, 4) void pool_mfma44_kernel(
   __shared__ MfRange s_rg[kMfBlocks];
   __shared__ PoolBest s_best[kPoolWaves][kMfBlocks];
   __shared__ float s_thr[kPoolWaves][kMfBlocks];
-  __shared__ float4 s_dt[2][kPoolWaves][8];        // a tile's 32 sqrt(n·D), double-buffered
+  __shared__ float4 s_dt[2][kPoolWaves][8];        // a tile's 32 1/sqrt(n·D), double-buffered
   if (!flags[6]) return;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -372,8 +372,10 @@ __global__ __launch_bounds__(kPoolWG, 4) void pool_mfma44_kernel(
   }
   __syncthreads();
 
-  // the bound test compares |num'| with sqrt(thr) * sqrt(n·D): thr <= 0 prunes nothing (st = -1),
-  // thr = inf prunes everything; sqrt's <= 1 ulp errors are far inside the 2^-18 shrink
+  // the bound test compares |num'| / sqrt(n·D) with sqrt(thr): thr <= 0 prunes nothing (st = -1),
+  // thr = inf prunes everything; the <= 1 ulp errors of sqrt and rsq and the product's rounding
+  // (< 2^-21 together) are far inside the 2^-18 shrink.  A flat domain block has n·D = 1e-30 in the
+  // pool image and num' = 0 exactly, so its ratio is 0: pruned iff thr > 0, the exact rule
   auto st_of = [](float t) { return t > 0.0f ? __builtin_sqrtf(t) : -1.0f; };
   // ---- B fragments (range blocks, centred) and per-lane constants, whole stream ----
   // r~ = r - Σr/16 is a multiple of 1/16 below 256: hi = its top 8 significant
@@ -474,27 +476,33 @@ __global__ __launch_bounds__(kPoolWG, 4) void pool_mfma44_kernel(
       dt[4 * g] = r.x; dt[4 * g + 1] = r.y; dt[4 * g + 2] = r.z; dt[4 * g + 3] = r.w;
     }
     const bool tail = x0 + 31 > xb;
-    // e < 0  <=>  |num'| < sqrt(thr) * sqrt(n·D): pruned; e >= 0: the pair survives
-    // (st = sqrt(thr) per lane, sdt = sqrt(n·D) per position; the slow path recomputes e bit-identically)
+    // q < st  <=>  |num'| / sqrt(n·D) < sqrt(thr): pruned; otherwise the pair survives
+    // (st = sqrt(thr) per lane, dt = 1/sqrt(n·D) per position; the slow path recomputes q bit-identically)
     auto test = [&](const mf_f32x16 &D, float st, int v) {
-      const float e = __builtin_fmaf(-st, dt[v], __builtin_fabsf(D[v]));
-      return (tail && x0 + (v & 3) + 8 * (v >> 2) + 4 * hh > xb) ? -1.0f : e;
+      const float q = __builtin_fabsf(D[v] * dt[v]);
+      return (tail && x0 + (v & 3) + 8 * (v >> 2) + 4 * hh > xb) ? false : !(q < st);
     };
     auto num_of = [&](int cb) {
       const mf_f32x16 Dh = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, Bh[cb], mf_f32x16{}, 0, 0, 0);
       return __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, Bl[cb], Dh, 0, 0, 0);
     };
     unsigned hit = 0;
-    auto emax_of = [&](const mf_f32x16 &D, int cb) {
-      float emax = -1.0f;
+    // does any pair of the column group survive?  Products two at a time (v_pk_mul_f32), their
+    // magnitudes folded by v_max3_f32 with abs modifiers: 16 VALU per 16 pairs
+    auto any_of = [&](const mf_f32x16 &D, int cb) {
       if (!tail) {                    // the same arithmetic without the column mask
+        float qm = 0.0f;
 #pragma unroll
-        for (int v = 0; v < 16; ++v) emax = fmaxf(emax, __builtin_fmaf(-thr[cb], dt[v], __builtin_fabsf(D[v])));
-      } else {
-#pragma unroll
-        for (int v = 0; v < 16; ++v) emax = fmaxf(emax, test(D, thr[cb], v));
+        for (int v = 0; v < 16; v += 2) {
+          const mf_f32x2 pr = mf_f32x2{D[v], D[v + 1]} * mf_f32x2{dt[v], dt[v + 1]};
+          qm = fmaxf(fmaxf(qm, __builtin_fabsf(pr[0])), __builtin_fabsf(pr[1]));
+        }
+        return !(qm < thr[cb]);
       }
-      return emax;
+      bool any = false;
+#pragma unroll
+      for (int v = 0; v < 16; ++v) any |= test(D, thr[cb], v);
+      return any;
     };
     // column groups in pairs: both hi MFMAs, then both lo MFMAs (each lo finds its hi
     // done), then the two epilogues -- two accumulators live, no MFMA waits on its own chain
@@ -504,15 +512,15 @@ __global__ __launch_bounds__(kPoolWG, 4) void pool_mfma44_kernel(
       mf_f32x16 D1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, Bh[cb + 1], mf_f32x16{}, 0, 0, 0);
       D0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, Bl[cb], D0, 0, 0, 0);
       D1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, Bl[cb + 1], D1, 0, 0, 0);
-      if (__any(!(emax_of(D0, cb) < 0.0f))) hit |= 1u << cb;
-      if (__any(!(emax_of(D1, cb + 1) < 0.0f))) hit |= 2u << cb;
+      if (__any(any_of(D0, cb))) hit |= 1u << cb;
+      if (__any(any_of(D1, cb + 1))) hit |= 2u << cb;
     }
     if (hit) {                                           // rare: survivors, one at a time
       for (int cb = 0; cb < kMfCols; ++cb) {
         if (!((hit >> cb) & 1)) continue;
         const mf_f32x16 D = num_of(cb);
         for (int v = 0; v < 16; ++v) {
-          unsigned long long m = __ballot(!(test(D, thr[cb], v) < 0.0f));
+          unsigned long long m = __ballot(test(D, thr[cb], v));
           while (m) {
             const int ln = __ffsll((long long)m) - 1;
             m &= m - 1;
@@ -540,7 +548,7 @@ __global__ __launch_bounds__(kPoolWG, 4) void pool_mfma44_kernel(
       }
     }
     buf ^= 1;
-    dtl_of(buf)[col] = __builtin_sqrtf(nxt.pd.y);        // both halves store the same value: no branch,
+    dtl_of(buf)[col] = __builtin_amdgcn_rsqf(nxt.pd.y);  // both halves store the same value: no branch,
                                                          // so the waitcnt pass sees one straight path
   };
   // two register sets X, Y alternate (unrolled by two, so no register copies
@@ -552,7 +560,7 @@ __global__ __launch_bounds__(kPoolWG, 4) void pool_mfma44_kernel(
   adv(ly, lx);
   load(ly, lx, Y);
   adv(ly, lx);
-  dtl[col] = __builtin_sqrtf(X.pd.y);
+  dtl[col] = __builtin_amdgcn_rsqf(X.pd.y);
   int t = 0;
   for (; t + 1 < ntiles; t += 2) {       // both steps on every trip: exact vmcnt at the loop head
     step(cy, cx, X, Y);

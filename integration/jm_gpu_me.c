@@ -1382,7 +1382,7 @@ static ep_in *g_ep_seen = NULL;    /* [ring of macroblocks][41 slots][EP_REFS]: 
 static ep_ans *g_ep_ans = NULL;    /* the current batch's searched guesses */
 static int *g_ep_idx = NULL;       /* [batch macroblock][41][EP_REFS][EP_WAYS] -> g_ep_ans index (-1: none) */
 static int g_ep_cap = 0, g_ep_n = 0, g_ep_mb0 = 0, g_ep_mb1 = 0;
-static unsigned g_ep_gen = 0;      /* g_slot_gen the batch belongs to (0: none) */
+static unsigned g_ep_gens[EP_REFS];   /* g_slot_gen of each reference when the batch was made (0: none) */
 static const ep_ans *g_ep_served = NULL;   /* the answer the last EPZS call was served from (its refinement) */
 static ep_spp g_ep_spp;
 static jmme_epzs_req *g_ep_q = NULL;
@@ -1490,7 +1490,7 @@ static const ep_ans *ep_lookup(Macroblock *currMB, MEBlock *mv_block, const jmme
     if (!g_ep_seen) error("jm_gpu_me: out of memory", 500);
   }
   ep_fill_in(ep_seen_at(mb, slot, ref), q, pred, cond, mb, gen);
-  if (g_ep_gen != gen || mb < g_ep_mb0 || mb >= g_ep_mb1) return NULL;
+  if (!gen || g_ep_gens[ref] != gen || mb < g_ep_mb0 || mb >= g_ep_mb1) return NULL;
   ++g_ep_miss_slot[slot];   /* (taken back below on a hit) */
   int kind = 0;
   int64_t stop_off = -1;
@@ -1753,7 +1753,7 @@ static const ep_ans *ep_miss(Macroblock *currMB, MEBlock *mv_block, const jmme_e
   EPZSParameters *p_EPZS = currMB->p_Slice->p_EPZS;
   const int mb = (mv_block->pos_y >> 4) * g_mbs_x + (mv_block->pos_x >> 4), ref = q->ref_idx;
   const unsigned gen = g_slot_gen[0][ref];
-  const int inside = g_ep_gen == gen && mb >= g_ep_mb0 && mb < g_ep_mb1;
+  const int inside = gen && g_ep_gens[ref] == gen && mb >= g_ep_mb0 && mb < g_ep_mb1;
   ep_in want;
   int n = 1, x, t, r, w, nmb;
   double t0 = now_us();
@@ -1822,7 +1822,7 @@ static const ep_ans *ep_miss(Macroblock *currMB, MEBlock *mv_block, const jmme_e
   g_ep_n = n;
   g_ep_mb0 = mb;
   g_ep_mb1 = mb + nmb;
-  g_ep_gen = gen;
+  for (r = 0; r < EP_REFS; r++) g_ep_gens[r] = g_slot_gen[0][r];   /* (a call for another reference stays inside) */
   g_ep_guesses += n - 1;
   ++g_ep_batches;
   return &g_ep_ans[0];
