@@ -1626,7 +1626,8 @@ extern "C" int jmme_epzs_speculate(jmme_ctx *ctx, const jmme_epzs_req *req, int 
   hipStream_t s = nullptr;
   // a few searches (the drop-in's searches alone): each wave refines its own
   // answer in the same launch; batches: the 16-refinements-per-wave kernel after it
-  const bool fuse = sp_req && n <= kEpzsFuseMax;
+  bool fuse = sp_req && n <= kEpzsFuseMax;
+  for (int i = 0; fuse && i < n; ++i) fuse = req[i].n_pred <= kEpzsStageP && req[i].n_stale <= kEpzsStageS;
   if (launch_epzs_ex(ctx, d_req, n, d_preds, d_cond, d_stale, d_out, d_vis, max_visited, s, d_bnd, d_int,
                      fuse ? d_spq : nullptr, fuse ? d_spo : nullptr))
     return -1;

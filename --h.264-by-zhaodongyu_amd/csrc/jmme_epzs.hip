@@ -660,9 +660,21 @@ __device__ jmme_block_res search_one(const EpzsParams &p, const jmme_epzs_req &q
 // instance, so the batch kernel's register allocation is not touched)
 template <typename T>
 __device__ __forceinline__ void refine_fused(const SubpelParams &sp, spd::WaveLds<T> &L, int lane, int t,
-                                          jmme_block_res br) {
-  spd::refine_wave<T>(sp, L, lane, t, &br);
+                                          jmme_block_res br, const jmme_subpel_req *req) {
+  spd::refine_wave<T>(sp, L, lane, t, &br, req);
 }
+
+// The fused launches are the drop-in's searches alone, and their inputs sit in
+// host-mapped memory: every dependent read of them is a PCIe round trip.  Each
+// wave copies its request's predictor list, conditions, pre-stamped cells and
+// refinement request to LDS in one round first (the host fuses only launches
+// whose lists fit: kEpzsStageP predictors, kEpzsStageS pre-stamped cells).
+struct StageLds {
+  uint32_t preds[kEpzsStageP];
+  uint32_t stale[kEpzsStageS];
+  uint8_t cond[kEpzsStageP];
+  jmme_subpel_req spq;
+};
 
 #ifndef JMME_EPZS_WAVES_PER_EU
 #define JMME_EPZS_WAVES_PER_EU 4
@@ -675,16 +687,40 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(JMME_EPZS_W
   using SpT = std::conditional_t<HBD, uint16_t, uint8_t>;
   __shared__ WaveLds s_w[kWaves];
   __shared__ spd::WaveLds<SpT> s_sp[FUSED ? kWaves : 1];
+  __shared__ StageLds s_st[FUSED ? kWaves : 1];
   extern __shared__ uint32_t s_map[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint32_t *map = s_map + (size_t)wave * p.map_words;
   for (int t = blockIdx.x * kWaves + wave; t < p.n; t += gridDim.x * kWaves) {
     const jmme_epzs_req q = p.req[t];
     // requests of the other grid, or with a window the map was not sized for, are refused
-    const bool ok = (GRID ? q.variant >= 2 : q.variant <= 1) && q.max_x <= p.max_qpel && q.max_y <= p.max_qpel;
+    const bool ok = (GRID ? q.variant >= 2 : q.variant <= 1) && q.max_x <= p.max_qpel && q.max_y <= p.max_qpel &&
+                    (!FUSED || (q.n_pred <= kEpzsStageP && q.n_stale <= kEpzsStageS));
     if (ok) {
-      const jmme_block_res br = search_one<GRID, HBD>(p, q, s_w[wave], map, lane, p.out + t);
-      if (FUSED && p.fused_sp.req[t].blocktype) refine_fused<SpT>(p.fused_sp, s_sp[FUSED ? wave : 0], lane, t, br);
+      EpzsParams pl = p;
+      jmme_epzs_req ql = q;
+      StageLds &S = s_st[FUSED ? wave : 0];
+      if constexpr (FUSED) {   // (the host fuses only lists that fit the stage)
+        for (int i = lane; i < q.n_pred; i += 64) {
+          S.preds[i] = reinterpret_cast<const uint32_t *>(p.preds)[q.pred_off + i];
+          if (p.pred_cond) S.cond[i] = p.pred_cond[q.pred_off + i];
+        }
+        if (lane < q.n_stale) S.stale[lane] = reinterpret_cast<const uint32_t *>(p.stale)[q.stale_off + lane];
+        constexpr int kSpw = sizeof(jmme_subpel_req) / 4;
+        static_assert(sizeof(jmme_subpel_req) % 4 == 0 && kSpw <= 64, "staged refinement request");
+        if (lane < kSpw)
+          reinterpret_cast<uint32_t *>(&S.spq)[lane] = reinterpret_cast<const uint32_t *>(p.fused_sp.req + t)[lane];
+        wave_sync();
+        pl.preds = reinterpret_cast<const int16_t *>(S.preds);
+        pl.stale = reinterpret_cast<const int16_t *>(S.stale);
+        pl.pred_cond = p.pred_cond ? S.cond : nullptr;
+        ql.pred_off = 0;
+        ql.stale_off = 0;
+      }
+      const jmme_block_res br = search_one<GRID, HBD>(pl, ql, s_w[wave], map, lane, p.out + t);
+      if constexpr (FUSED) {
+        if (S.spq.blocktype) refine_fused<SpT>(p.fused_sp, s_sp[wave], lane, t, br, &S.spq);
+      }
       (void)br;
     } else if (lane == 0) {
       jmme_epzs_res r{};

@@ -10,6 +10,9 @@ namespace jmme {
 
 constexpr int kEpzsMaxQpel = 4 * JMME_MAX_RANGE;   // largest searchRange.max_x / max_y (qpel)
 
+// fused launches stage each request's lists in LDS (epzs_kernel): the longest they take
+constexpr int kEpzsStageP = 128, kEpzsStageS = 64;
+
 struct EpzsParams {
   const uint8_t *cur;                  // current frame: 8-bit, or 16-bit when hbd
   const uint8_t *const *refs;          // device table of reference planes (list * 32 + ref_idx)

@@ -322,16 +322,17 @@ __device__ void run_phase(const SubpelParams &p, WaveLds<T> &L, int lane, const 
 
 // One wave's refinements: lane k < p.per_wave owns request i0 + k (the body of
 // subpel_kernel; the EPZS kernel's fused single-search path calls it with
-// per_wave = 1 and its own answer as ir_one).
+// per_wave = 1, its own answer as ir_one and its request staged in LDS as req_one).
 template <typename T>
 __device__ __forceinline__ void refine_wave(const SubpelParams &p, WaveLds<T> &L, int lane, int i0,
-                                            const jmme_block_res *ir_one = nullptr) {
+                                            const jmme_block_res *ir_one = nullptr,
+                                            const jmme_subpel_req *req_one = nullptr) {
   const int i = i0 + lane;
   // owner lanes: lane k < 16 holds request i0 + k; inactive owners ask for nothing
   jmme_subpel_req q{};
   bool act = false;
   if (lane < p.per_wave && i < p.n) {
-    q = p.req[i];
+    q = req_one ? *req_one : p.req[i];
     act = q.blocktype >= 1 && q.blocktype <= 7;
   }
   int mvx = q.mv_x, mvy = q.mv_y;
