@@ -1362,7 +1362,7 @@ namespace {
 int launch_epzs_ex(jmme_ctx *ctx, const jmme_epzs_req *d_req, int n, const int16_t *d_preds, const uint8_t *d_cond,
                    const int16_t *d_stale, jmme_epzs_res *d_out, int16_t *d_vis, int max_visited, hipStream_t s,
                    jmme_epzs_bounds *d_bounds = nullptr, jmme_block_res *d_int = nullptr,
-                   const jmme_subpel_req *d_fused_req = nullptr, jmme_block_res *d_fused_out = nullptr) {
+                   const EpzsOne *one = nullptr, jmme_block_res *d_fused_out = nullptr) {
   if (sync_ref_table(ctx, s)) return -1;
   EpzsParams p{};
   p.cur = ctx->d_cur;
@@ -1394,7 +1394,7 @@ int launch_epzs_ex(jmme_ctx *ctx, const jmme_epzs_req *d_req, int n, const int16
   p.max_visited = max_visited;
   p.bounds = d_bounds;
   p.int_out = d_int;
-  if (d_fused_req) {   // each wave refines its own answer (jmme_epzs_speculate's small launches)
+  if (one) {   // a search alone, in the kernel arguments; its wave refines its own answer
     if (prepare_subs(ctx, s)) return -1;
     const SubGeom g = sub_geom(ctx->width, ctx->height);
     p.fused = 1;
@@ -1406,11 +1406,12 @@ int launch_epzs_ex(jmme_ctx *ctx, const jmme_epzs_req *d_req, int n, const int16
     p.fused_sp.subs = ctx->d_sub_table;
     p.fused_sp.sub_pitch = g.pitch;
     p.fused_sp.plane_stride = g.plane_stride;
-    p.fused_sp.req = d_fused_req;
+    p.fused_sp.req = nullptr;
     p.fused_sp.int_res = nullptr;
     p.fused_sp.out = d_fused_out;
-    p.fused_sp.n = n;
+    p.fused_sp.n = 1;
     p.fused_sp.per_wave = 1;
+    p.one = *one;
   }
   HIPCHK(launch_epzs(p, s));
   return 0;
@@ -1553,7 +1554,6 @@ extern "C" int jmme_epzs_search_ex(jmme_ctx *ctx, const jmme_epzs_req *req, int 
 }
 
 static_assert(sizeof(jmme_epzs_bounds) == 40, "EPZS bounds ABI layout");
-constexpr int kEpzsFuseMax = 16;   // jmme_epzs_speculate launches of at most this many searches fuse the refinement
 
 extern "C" int jmme_epzs_speculate(jmme_ctx *ctx, const jmme_epzs_req *req, int n, const int16_t *preds,
                                    const uint8_t *pred_cond, int n_preds, const int16_t *stale, int n_stale,
@@ -1624,12 +1624,22 @@ extern "C" int jmme_epzs_speculate(jmme_ctx *ctx, const jmme_epzs_req *req, int 
     h_spo = reinterpret_cast<jmme_block_res *>(h + o);
   }
   hipStream_t s = nullptr;
-  // a few searches (the drop-in's searches alone): each wave refines its own
-  // answer in the same launch; batches: the 16-refinements-per-wave kernel after it
-  bool fuse = sp_req && n <= kEpzsFuseMax;
-  for (int i = 0; fuse && i < n; ++i) fuse = req[i].n_pred <= kEpzsStageP && req[i].n_stale <= kEpzsStageS;
+  // a search alone (the drop-in's misses) travels in the kernel arguments and its
+  // wave refines its own answer in the same launch; batches: the
+  // 16-refinements-per-wave kernel after it
+  const bool fuse = sp_req && n == 1 && req[0].n_pred <= kEpzsStageP && req[0].n_stale <= kEpzsStageS;
+  EpzsOne one{};
+  if (fuse) {
+    one.q = req[0];
+    one.q.pred_off = 0;
+    one.q.stale_off = 0;
+    one.spq = sp_req[0];
+    if (req[0].n_pred) std::memcpy(one.preds, preds + 2 * (size_t)req[0].pred_off, (size_t)req[0].n_pred * 4);
+    if (pred_cond && req[0].n_pred) std::memcpy(one.cond, pred_cond + req[0].pred_off, (size_t)req[0].n_pred);
+    if (req[0].n_stale) std::memcpy(one.stale, stale + 2 * (size_t)req[0].stale_off, (size_t)req[0].n_stale * 4);
+  }
   if (launch_epzs_ex(ctx, d_req, n, d_preds, d_cond, d_stale, d_out, d_vis, max_visited, s, d_bnd, d_int,
-                     fuse ? d_spq : nullptr, fuse ? d_spo : nullptr))
+                     fuse ? &one : nullptr, fuse ? d_spo : nullptr))
     return -1;
   if (sp_req && !fuse && jmme_subpel_refine_async(ctx, d_spq, n, d_int, d_spo, s)) return -1;
   HIPCHK(hipStreamSynchronize(s));

@@ -337,8 +337,8 @@ __device__ jmme_block_res search_one(const EpzsParams &p, const jmme_epzs_req &q
     const int r = lane / nq, c = lane - r * nq;
     w.cur[lane] = *reinterpret_cast<const uint32_t *>(p.cur + (size_t)(q.pos_y + r) * p.pitch + q.pos_x + 4 * c);
   }
-  const int words = (s.side_x * side_y + 31) >> 5;
-  for (int i = lane; i < words; i += 64) map[i] = 0;
+  const int words = (s.side_x * side_y + 31) >> 5, quads = (words + 3) >> 2;   // map_words is a multiple of 4
+  for (int i = lane; i < quads; i += 64) reinterpret_cast<uint4 *>(map)[i] = make_uint4(0u, 0u, 0u, 0u);
   wave_sync();
   for (int i = lane; i < q.n_stale; i += 64) {   // cells already holding this BlkCount
     const int dx = p.stale[2 * (q.stale_off + i)], dy = p.stale[2 * (q.stale_off + i) + 1];
@@ -591,30 +591,42 @@ __device__ jmme_block_res search_one(const EpzsParams &p, const jmme_epzs_req &q
   // cells that already held its BlkCount), as (dx, dy) qpel from the centre
   int nv = 0;
   if (p.visited) {
+    // each lane takes a contiguous run of map quads (ds_read_b128): one popcount
+    // pass, one wave prefix sum, then every lane writes its cells (row-major order kept)
     int16_t *const vout = p.visited + 2 * (size_t)p.max_visited * (size_t)(out - p.out);
-    const int words = (s.side_x * side_y + 31) >> 5;
-    for (int base = 0; base < words; base += 64) {
-      const int wi = base + lane;
-      uint32_t bits = wi < words ? s.map[wi] : 0u;
-      int cnt = __popc(bits), pre = cnt;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {   // inclusive prefix sum over the wave
-        const int v = __shfl_up(pre, o, 64);
-        if (lane >= o) pre += v;
-      }
-      int at = nv + pre - cnt;
-      while (bits) {
-        const int b = __builtin_ctz(bits);
-        bits &= bits - 1;
-        const int c = wi * 32 + b, cyi = c / s.side_x, cxi = c - cyi * s.side_x;
-        if (at < p.max_visited) {
-          vout[2 * at] = (int16_t)(GRID ? cxi - s.max_x : 4 * cxi - s.max_x);
-          vout[2 * at + 1] = (int16_t)(GRID ? cyi - s.max_y : 4 * cyi - s.max_y);
-        }
-        ++at;
-      }
-      nv += __shfl(pre, 63, 64);
+    const uint4 *m4 = reinterpret_cast<const uint4 *>(s.map);
+    const int per = (quads + 63) >> 6, q0 = min(lane * per, quads), q1 = min(q0 + per, quads);
+    int cnt = 0;
+    for (int qi = q0; qi < q1; ++qi) {
+      const uint4 v = m4[qi];
+      cnt += __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);
     }
+    int pre = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {   // inclusive prefix sum over the wave
+      const int v = __shfl_up(pre, o, 64);
+      if (lane >= o) pre += v;
+    }
+    int at = pre - cnt;
+    for (int qi = q0; qi < q1 && at < p.max_visited; ++qi) {
+      const uint4 v = m4[qi];
+      const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        uint32_t bits = w4[e];
+        while (bits) {
+          const int b = __builtin_ctz(bits);
+          bits &= bits - 1;
+          const int c = (4 * qi + e) * 32 + b, cyi = c / s.side_x, cxi = c - cyi * s.side_x;
+          if (at < p.max_visited) {
+            vout[2 * at] = (int16_t)(GRID ? cxi - s.max_x : 4 * cxi - s.max_x);
+            vout[2 * at + 1] = (int16_t)(GRID ? cyi - s.max_y : 4 * cyi - s.max_y);
+          }
+          ++at;
+        }
+      }
+    }
+    nv = __shfl(pre, 63, 64);
   }
   if (lane == 0) {
     jmme_epzs_res r;
@@ -664,17 +676,6 @@ __device__ __forceinline__ void refine_fused(const SubpelParams &sp, spd::WaveLd
   spd::refine_wave<T>(sp, L, lane, t, &br, req);
 }
 
-// The fused launches are the drop-in's searches alone, and their inputs sit in
-// host-mapped memory: every dependent read of them is a PCIe round trip.  Each
-// wave copies its request's predictor list, conditions, pre-stamped cells and
-// refinement request to LDS in one round first (the host fuses only launches
-// whose lists fit: kEpzsStageP predictors, kEpzsStageS pre-stamped cells).
-struct StageLds {
-  uint32_t preds[kEpzsStageP];
-  uint32_t stale[kEpzsStageS];
-  uint8_t cond[kEpzsStageP];
-  jmme_subpel_req spq;
-};
 
 #ifndef JMME_EPZS_WAVES_PER_EU
 #define JMME_EPZS_WAVES_PER_EU 4
@@ -687,39 +688,25 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(JMME_EPZS_W
   using SpT = std::conditional_t<HBD, uint16_t, uint8_t>;
   __shared__ WaveLds s_w[kWaves];
   __shared__ spd::WaveLds<SpT> s_sp[FUSED ? kWaves : 1];
-  __shared__ StageLds s_st[FUSED ? kWaves : 1];
-  extern __shared__ uint32_t s_map[];
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_map[];   // quads: map_words is a multiple of 4
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint32_t *map = s_map + (size_t)wave * p.map_words;
   for (int t = blockIdx.x * kWaves + wave; t < p.n; t += gridDim.x * kWaves) {
-    const jmme_epzs_req q = p.req[t];
+    const jmme_epzs_req q = FUSED ? p.one.q : p.req[t];
     // requests of the other grid, or with a window the map was not sized for, are refused
     const bool ok = (GRID ? q.variant >= 2 : q.variant <= 1) && q.max_x <= p.max_qpel && q.max_y <= p.max_qpel &&
-                    (!FUSED || (q.n_pred <= kEpzsStageP && q.n_stale <= kEpzsStageS));
+                    (!FUSED || (t == 0 && q.n_pred <= kEpzsStageP && q.n_stale <= kEpzsStageS));
     if (ok) {
       EpzsParams pl = p;
       jmme_epzs_req ql = q;
-      StageLds &S = s_st[FUSED ? wave : 0];
-      if constexpr (FUSED) {   // (the host fuses only lists that fit the stage)
-        for (int i = lane; i < q.n_pred; i += 64) {
-          S.preds[i] = reinterpret_cast<const uint32_t *>(p.preds)[q.pred_off + i];
-          if (p.pred_cond) S.cond[i] = p.pred_cond[q.pred_off + i];
-        }
-        if (lane < q.n_stale) S.stale[lane] = reinterpret_cast<const uint32_t *>(p.stale)[q.stale_off + lane];
-        constexpr int kSpw = sizeof(jmme_subpel_req) / 4;
-        static_assert(sizeof(jmme_subpel_req) % 4 == 0 && kSpw <= 64, "staged refinement request");
-        if (lane < kSpw)
-          reinterpret_cast<uint32_t *>(&S.spq)[lane] = reinterpret_cast<const uint32_t *>(p.fused_sp.req + t)[lane];
-        wave_sync();
-        pl.preds = reinterpret_cast<const int16_t *>(S.preds);
-        pl.stale = reinterpret_cast<const int16_t *>(S.stale);
-        pl.pred_cond = p.pred_cond ? S.cond : nullptr;
-        ql.pred_off = 0;
-        ql.stale_off = 0;
+      if constexpr (FUSED) {   // the lists from the kernel arguments (the host fuses only lists that fit)
+        pl.preds = reinterpret_cast<const int16_t *>(p.one.preds);
+        pl.stale = reinterpret_cast<const int16_t *>(p.one.stale);
+        pl.pred_cond = p.pred_cond ? p.one.cond : nullptr;
       }
       const jmme_block_res br = search_one<GRID, HBD>(pl, ql, s_w[wave], map, lane, p.out + t);
       if constexpr (FUSED) {
-        if (S.spq.blocktype) refine_fused<SpT>(p.fused_sp, s_sp[wave], lane, t, br, &S.spq);
+        if (p.one.spq.blocktype) refine_fused<SpT>(p.fused_sp, s_sp[wave], lane, 0, br, &p.one.spq);
       }
       (void)br;
     } else if (lane == 0) {
@@ -732,9 +719,9 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(JMME_EPZS_W
 
 }  // namespace
 
-size_t epzs_map_words(bool grid, int max_qpel) {
+size_t epzs_map_words(bool grid, int max_qpel) {   // rounded to whole quads (the kernel clears and scans uint4s)
   const size_t side = grid ? 2 * (size_t)max_qpel + 1 : 2 * (size_t)(max_qpel >> 2) + 1;
-  return (side * side + 31) / 32;
+  return ((side * side + 31) / 32 + 3) & ~(size_t)3;
 }
 
 hipError_t launch_epzs(const EpzsParams &p, hipStream_t s) {

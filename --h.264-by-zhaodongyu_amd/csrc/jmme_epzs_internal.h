@@ -10,8 +10,16 @@ namespace jmme {
 
 constexpr int kEpzsMaxQpel = 4 * JMME_MAX_RANGE;   // largest searchRange.max_x / max_y (qpel)
 
-// fused launches stage each request's lists in LDS (epzs_kernel): the longest they take
+// a search alone (jmme_epzs_speculate with n = 1, the drop-in's misses) travels
+// whole in the kernel arguments: no host-mapped read on its path
 constexpr int kEpzsStageP = 128, kEpzsStageS = 64;
+struct EpzsOne {
+  jmme_epzs_req q;                 // pred_off = stale_off = 0
+  jmme_subpel_req spq;             // its refinement (blocktype 0: none)
+  uint32_t preds[kEpzsStageP];     // (x, y) int16 pairs
+  uint32_t stale[kEpzsStageS];
+  uint8_t cond[kEpzsStageP];
+};
 
 struct EpzsParams {
   const uint8_t *cur;                  // current frame: 8-bit, or 16-bit when hbd
@@ -40,12 +48,13 @@ struct EpzsParams {
   // refinement (null: not written)
   jmme_epzs_bounds *bounds;
   jmme_block_res *int_out;
-  // fused refinement (small speculative launches): the wave that searched
-  // request t runs its EPZS sub-pel refinement fused_sp.req[t] itself, from its
-  // own answer, into fused_sp.out[t] (fused = 0: none; the caller chains the
+  // fused refinement (a search alone): the wave that searched the request in
+  // `one` runs its EPZS sub-pel refinement one.spq itself, from its own
+  // answer, into fused_sp.out[0] (fused = 0: none; the caller chains the
   // refinement kernel instead)
   int fused;
   SubpelParams fused_sp;
+  EpzsOne one;                     // fused = 1: the one request, its lists and its refinement
 };
 
 size_t epzs_map_words(bool grid, int max_qpel);

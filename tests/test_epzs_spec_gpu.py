@@ -139,7 +139,7 @@ def test_chained_subpel_equals_separate_calls(grid, gpu):
 
 @pytest.mark.parametrize("grid", [False, True])
 def test_fused_refinement_of_small_launches(grid, gpu):
-    """launches of at most 16 searches refine in the searching wave itself
+    """a search alone travels in the kernel arguments and refines in the searching wave itself
     (epzs_kernel<..., FUSED>): the same answers and refinements as one big launch
     that chains the refinement kernel"""
     from jmme import SP_TEST8x8, SUBPEL_REQ, MotionEstimator

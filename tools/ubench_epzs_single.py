@@ -21,7 +21,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for p in (os.path.join(REPO, "tests"), os.path.join(REPO, "--h.264-by-zhaodongyu_amd")):
     sys.path.insert(0, p)
 
-CATS = ("floor", "search", "search+refine")
+CATS = ("floor", "floor/unfused", "floor/small map", "search", "search/unfused", "search+refine")
 
 
 def trace_summary(path, log):
@@ -69,8 +69,10 @@ def main():
             so, ns = int(q["stale_off"][0]), int(q["n_stale"][0])
             stale = c.stale[so:so + ns]
             q["pred_off"], q["stale_off"] = 0, 0
-            if phase == "floor":
+            if phase.startswith("floor"):
                 q["medthres"] = 1 << 40
+            if phase == "floor/small map":
+                q["max_x"] = q["max_y"] = 8
             sp = np.zeros(1, SUBPEL_REQ)
             sp["pos_x"], sp["pos_y"] = q["pos_x"], q["pos_y"]
             sp["blocktype"] = q["blocktype"] if phase == "search+refine" else 0
@@ -88,7 +90,8 @@ def main():
             t0 = time.perf_counter()
             for i in idx:
                 q, preds, stale, sp = single(i, phase)
-                me.epzs_speculate(q, preds, None, stale, max_visited=256, sp_req=sp)
+                me.epzs_speculate(q, preds, None, stale, max_visited=256,
+                                  sp_req=None if phase.endswith("unfused") else sp)
             dt = (time.perf_counter() - t0) / max(len(idx), 1)
             print(json.dumps({"phase": phase, "bt": bt, "calls": len(idx), "host_us_per_call": round(dt * 1e6, 1)}),
                   flush=True)
