@@ -117,6 +117,13 @@ struct jmme_ctx {
   unsigned long long *d_skeys = nullptr;     // per (item, tile) keys, cap_skeys * JMME_NSLOT
   size_t cap_skeys = 0;
   hipStream_t chain_stream = nullptr;        // chains run beside the batch of the same call (non-blocking)
+  // EPZS searches alone (JMME_SINGLE_MODE: 0 null stream + sync, 1 own stream + sync,
+  // 2 own stream + the kernel's completion word polled in mapped memory)
+  int single_mode = -1;
+  hipStream_t single_stream = nullptr;
+  uint32_t *h_done = nullptr;
+  void *dv_done = nullptr;
+  uint32_t done_seq = 0;
   std::vector<SmallItem> small_scratch;      // search_small's items (kept: no allocation per call)
   void *dv_hkeys = nullptr, *dv_chres = nullptr, *dv_sitems = nullptr, *dv_sout = nullptr;   // device views
   std::vector<uint8_t *> spare_planes;       // jmme_reserve: plane buffers the first uploads take
@@ -364,6 +371,11 @@ extern "C" void jmme_destroy(jmme_ctx *ctx) {
   if (ctx->h_chres) (void)hipHostFree(ctx->h_chres);
   if (ctx->h_chsp) (void)hipHostFree(ctx->h_chsp);
   if (ctx->chain_stream) (void)hipStreamDestroy(ctx->chain_stream);
+  if (ctx->single_stream) {
+    (void)hipStreamSynchronize(ctx->single_stream);
+    (void)hipStreamDestroy(ctx->single_stream);
+  }
+  if (ctx->h_done) (void)hipHostFree(ctx->h_done);
   (void)hipFree(ctx->d_skeys);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
@@ -1359,12 +1371,13 @@ int prepare_subs(jmme_ctx *ctx, hipStream_t s);   // sub-pel section below
 }  // namespace
 
 namespace {
-int launch_epzs_ex(jmme_ctx *ctx, const jmme_epzs_req *d_req, int n, const int16_t *d_preds, const uint8_t *d_cond,
-                   const int16_t *d_stale, jmme_epzs_res *d_out, int16_t *d_vis, int max_visited, hipStream_t s,
-                   jmme_epzs_bounds *d_bounds = nullptr, jmme_block_res *d_int = nullptr,
-                   const EpzsOne *one = nullptr, jmme_block_res *d_fused_out = nullptr) {
+int build_epzs_params(jmme_ctx *ctx, EpzsParams &p, const jmme_epzs_req *d_req, int n, const int16_t *d_preds,
+                      const uint8_t *d_cond, const int16_t *d_stale, jmme_epzs_res *d_out, int16_t *d_vis,
+                      int max_visited, hipStream_t s, jmme_epzs_bounds *d_bounds = nullptr,
+                      jmme_block_res *d_int = nullptr, const EpzsOne *one = nullptr,
+                      jmme_block_res *d_fused_out = nullptr, uint32_t *d_done = nullptr, uint32_t done_seq = 0) {
   if (sync_ref_table(ctx, s)) return -1;
-  EpzsParams p{};
+  std::memset(&p, 0, sizeof p);
   p.cur = ctx->d_cur;
   p.hbd = ctx->hbd ? 1 : 0;   // 16-bit planes / sub-images: the v_sad_u16 instantiation
   p.refs = ctx->d_ref_table;
@@ -1412,7 +1425,21 @@ int launch_epzs_ex(jmme_ctx *ctx, const jmme_epzs_req *d_req, int n, const int16
     p.fused_sp.n = 1;
     p.fused_sp.per_wave = 1;
     p.one = *one;
+    p.done = d_done;
+    p.done_seq = done_seq;
   }
+  return 0;
+}
+
+int launch_epzs_ex(jmme_ctx *ctx, const jmme_epzs_req *d_req, int n, const int16_t *d_preds, const uint8_t *d_cond,
+                   const int16_t *d_stale, jmme_epzs_res *d_out, int16_t *d_vis, int max_visited, hipStream_t s,
+                   jmme_epzs_bounds *d_bounds = nullptr, jmme_block_res *d_int = nullptr,
+                   const EpzsOne *one = nullptr, jmme_block_res *d_fused_out = nullptr,
+                   uint32_t *d_done = nullptr, uint32_t done_seq = 0) {
+  EpzsParams p;
+  if (build_epzs_params(ctx, p, d_req, n, d_preds, d_cond, d_stale, d_out, d_vis, max_visited, s, d_bounds, d_int, one,
+                        d_fused_out, d_done, done_seq))
+    return -1;
   HIPCHK(launch_epzs(p, s));
   return 0;
 }
@@ -1623,7 +1650,6 @@ extern "C" int jmme_epzs_speculate(jmme_ctx *ctx, const jmme_epzs_req *req, int 
     d_spo = reinterpret_cast<jmme_block_res *>(d + o);
     h_spo = reinterpret_cast<jmme_block_res *>(h + o);
   }
-  hipStream_t s = nullptr;
   // a search alone (the drop-in's misses) travels in the kernel arguments and its
   // wave refines its own answer in the same launch; batches: the
   // 16-refinements-per-wave kernel after it
@@ -1638,11 +1664,36 @@ extern "C" int jmme_epzs_speculate(jmme_ctx *ctx, const jmme_epzs_req *req, int 
     if (pred_cond && req[0].n_pred) std::memcpy(one.cond, pred_cond + req[0].pred_off, (size_t)req[0].n_pred);
     if (req[0].n_stale) std::memcpy(one.stale, stale + 2 * (size_t)req[0].stale_off, (size_t)req[0].n_stale * 4);
   }
+  if (ctx->single_mode < 0) {
+    const char *e = std::getenv("JMME_SINGLE_MODE");
+    ctx->single_mode = e ? std::max(0, std::min(2, std::atoi(e))) : 2;
+  }
+  const int mode = fuse ? ctx->single_mode : 0;
+  if (mode >= 1 && !ctx->single_stream) HIPCHK(hipStreamCreateWithFlags(&ctx->single_stream, hipStreamNonBlocking));
+  if (mode == 2 && !ctx->h_done) {
+    HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_done), 64, hipHostMallocMapped));
+    HIPCHK(hipHostGetDevicePointer(&ctx->dv_done, ctx->h_done, 0));
+    __atomic_store_n(ctx->h_done, 0u, __ATOMIC_RELEASE);
+  }
+  hipStream_t s = mode >= 1 ? ctx->single_stream : nullptr;
+  const uint32_t seq = mode == 2 ? ++ctx->done_seq : 0;
   if (launch_epzs_ex(ctx, d_req, n, d_preds, d_cond, d_stale, d_out, d_vis, max_visited, s, d_bnd, d_int,
-                     fuse ? &one : nullptr, fuse ? d_spo : nullptr))
+                     fuse ? &one : nullptr, fuse ? d_spo : nullptr,
+                     mode == 2 ? static_cast<uint32_t *>(ctx->dv_done) : nullptr, seq))
     return -1;
   if (sp_req && !fuse && jmme_subpel_refine_async(ctx, d_spq, n, d_int, d_spo, s)) return -1;
-  HIPCHK(hipStreamSynchronize(s));
+  if (mode == 2) {   // the kernel stores seq after a system-scope fence behind its last result
+    auto t0 = std::chrono::steady_clock::now();
+    for (unsigned spin = 1; __atomic_load_n(ctx->h_done, __ATOMIC_ACQUIRE) != seq; ++spin) {
+      if ((spin & 4095u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+        HIPCHK(hipStreamSynchronize(s));   // (surfaces a fault; a finished kernel has stored seq)
+        if (__atomic_load_n(ctx->h_done, __ATOMIC_ACQUIRE) != seq) return fail("EPZS search alone: no completion word");
+      }
+      __builtin_ia32_pause();
+    }
+  } else {
+    HIPCHK(hipStreamSynchronize(s));
+  }
   std::memcpy(out, h_out, (size_t)n * sizeof(jmme_epzs_res));
   std::memcpy(bounds, h_bnd, (size_t)n * sizeof(jmme_epzs_bounds));
   for (int i = 0; i < n; ++i)   // only the pairs each search wrote

@@ -715,6 +715,12 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(JMME_EPZS_W
       p.out[t] = r;
     }
   }
+  if constexpr (FUSED) {   // the host polls this word instead of synchronising the stream
+    if (p.done && blockIdx.x == 0 && wave == 0) {
+      __threadfence_system();
+      if (lane == 0) __hip_atomic_store(p.done, p.done_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
 }
 
 }  // namespace

@@ -55,6 +55,8 @@ struct EpzsParams {
   int fused;
   SubpelParams fused_sp;
   EpzsOne one;                     // fused = 1: the one request, its lists and its refinement
+  uint32_t *done;                  // fused: done_seq is stored here (mapped memory) after everything else
+  uint32_t done_seq;
 };
 
 size_t epzs_map_words(bool grid, int max_qpel);
