@@ -46,9 +46,10 @@ def main():
             args += ["-p", f"{k}={v}"]
         r = subprocess.run(args, cwd=d, capture_output=True, text=True, timeout=900, env=env)
     me = re.search(r"Total ME time for sequence\s*:\s*([0-9.]+) sec", r.stdout)
-    print("ME time", me.group(1) if me else None, "rc", r.returncode)
+    enc = re.search(r"Total encoding time for the seq\.\s*:\s*([0-9.]+) sec", r.stdout)
+    print("ME time", me.group(1) if me else None, "encoding time", enc.group(1) if enc else None, "rc", r.returncode)
     for line in r.stderr.splitlines():
-        if line.startswith("jm_gpu_me"):
+        if line.startswith("jm_gpu_me") or line.startswith("jm_f3_profile"):
             print(line)
     return r.returncode
 
