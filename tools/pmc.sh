@@ -1,7 +1,8 @@
 #!/bin/bash
 # PMC counter passes over a short bench run (one rocprofv3 pass per group;
 # --pmc never combined with sys/runtime traces).  Stops at the first failure.
-# Usage (GPU box, repo root): [JMME_LIB=...] tools/pmc.sh OUTDIR [groups...]
+# Usage (GPU box, repo root): [JMME_LIB=...] [PMC_CMD="python3 tools/bench_tq.py"] tools/pmc.sh OUTDIR [groups...]
+# (PMC_CMD: the program profiled; default the headline bench)
 set -e
 OUT=${1:-gpurun_out/pmc}; shift || true
 GROUPS_=${@:-tcc1 tcc2 sq1 sq2}
@@ -13,8 +14,9 @@ G[sq2]="SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_A
 G[sq3]="SQ_IFETCH SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_INSTS_BRANCH SQ_INST_CYCLES_SALU SQ_ACTIVE_INST_FLAT SQ_INSTS_FLAT SQ_WAVES"
 G[tcc1]="FETCH_SIZE"
 G[tcc2]="WRITE_SIZE"
+CMD=${PMC_CMD:-python3 bench.py --steps 5 --warmup 1 --headline-only}
 for g in $GROUPS_; do
   timeout -k 10 240 rocprofv3 --kernel-trace --pmc ${G[$g]} --output-format csv -d "$OUT/$g" -o p -- \
-    python3 bench.py --steps 5 --warmup 1 --headline-only > "$OUT/$g.log" 2>&1
+    $CMD > "$OUT/$g.log" 2>&1
 done
 echo pmc done
