@@ -655,6 +655,13 @@ static int speculating(void)
 }
 
 /* the cached answer for this call, batching on a miss */
+/* the sub-pel call that follows an integer answer usually finds its refinement in
+ * the matching way of the sub-pel cache (way k for integer way k, way KHYP + 1 for a
+ * chain's answer): probed first, and prefetched when the integer answer is found */
+static int g_sp_hint_mb = -1, g_sp_hint_s = -1, g_sp_hint_k = 0;
+static void sp_hint(int list, int ref, int mb, int s, int k);
+static void sp_prefetch_row(int list, int ref, int mb);
+
 static const spec_ent *spec_lookup(Macroblock *currMB, MEBlock *mv_block, int list, int ref, const spec_ent *want,
                                    int chk_rule)
 {
@@ -670,6 +677,7 @@ static const spec_ent *spec_lookup(Macroblock *currMB, MEBlock *mv_block, int li
       __builtin_prefetch(a + o, 0, 1);
       __builtin_prefetch(b + o, 1, 1);
     }
+    sp_prefetch_row(list, ref, mb + 1);
   }
   g_seen[list][ref][(size_t)mb * JMME_NSLOT + s] = *want;
   g_seen[list][ref][(size_t)mb * JMME_NSLOT + s].valid = g_slot_gen[list][ref];
@@ -678,9 +686,11 @@ static const spec_ent *spec_lookup(Macroblock *currMB, MEBlock *mv_block, int li
     if (spec_same(e, want, g_slot_gen[list][ref])) {
       ++g_hits;
       if (k == KHYP) ++g_chain_hits;
+      sp_hint(list, ref, mb, s, k);
       return e;
     }
   }
+  g_sp_hint_mb = -1;
   const int failed = mb < g_spec_end[list][ref];
   if (failed) {                                                          /* every guess failed */
     ++g_miss_guess;
@@ -903,6 +913,25 @@ static void slot_geometry(void)
 #define SPK (KHYP + 2)                  /* sub-pel answers kept per (macroblock, slot): the KHYP guesses,
                                            the real call (way KHYP), the chains' refinement (way KHYP + 1) */
 static int *g_sp_dst = NULL;
+/* way-major like the integer table: a macroblock's 41 entries of one way are contiguous */
+static inline size_t sp_idx(int mb, int s, int k) { return ((size_t)mb * SPK + k) * JMME_NSLOT + s; }
+
+static void sp_prefetch_row(int list, int ref, int mb)   /* the macroblock's way-0 sub-pel entries */
+{
+  const sp_ent *t = g_sp[list][ref];
+  size_t o;
+  if (!t) return;
+  for (o = 0; o < JMME_NSLOT * sizeof(sp_ent); o += 64) __builtin_prefetch((const char *)&t[sp_idx(mb, 0, 0)] + o, 0, 1);
+}
+
+static void sp_hint(int list, int ref, int mb, int s, int k)
+{
+  const sp_ent *t = g_sp[list][ref];
+  g_sp_hint_mb = mb;
+  g_sp_hint_s = s;
+  g_sp_hint_k = k < KHYP ? k : KHYP + 1;
+  if (t) __builtin_prefetch(&t[sp_idx(mb, s, g_sp_hint_k)], 0, 1);
+}
 
 static void sp_fill(jmme_subpel_req *q, int mb, int s, int list, int ref, const sp_ent *w)
 {
@@ -950,7 +979,7 @@ static void sp_batch(int list, int ref, int mb0, int s0, const sp_ent *w, int t8
     g_sreq_cap = count;
   }
   sp_fill(&g_sreq[n], mb0, s0, list, ref, w);
-  g_sp_dst[n++] = (mb0 * JMME_NSLOT + s0) * SPK + KHYP;
+  g_sp_dst[n++] = (int)sp_idx(mb0, s0, KHYP);
   for (mb = mb0; mb < mb1; mb++)
     for (s = 0; s < JMME_NSLOT; s++)
       for (k = 0; k < KHYP; k++) {
@@ -965,7 +994,7 @@ static void sp_batch(int list, int ref, int mb0, int s0, const sp_ent *w, int t8
         /* test8x8 as mv_search.c:1630,1770 set it: Transform8x8Mode on block types 1..4 */
         g.flags = (uint8_t)((w->flags & JMME_SP_CHECK0) | (t8 && g_slot_bt[s] <= 4 ? JMME_SP_TEST8x8 : 0));
         sp_fill(&g_sreq[n], mb, s, list, ref, &g);
-        g_sp_dst[n++] = (mb * JMME_NSLOT + s) * SPK + k;
+        g_sp_dst[n++] = (int)sp_idx(mb, s, k);
       }
   if (jmme_subpel_refine(g_me, g_sreq, n, g_sres)) fail_jm("jmme_subpel_refine");
   for (i = 0; i < n; i++) {
@@ -1071,7 +1100,7 @@ static int chain_subpel_template(Macroblock *currMB, MEBlock *mv_block, int list
 static void store_chain_subpel(int list, int ref, int mb, int sl, const jmme_chain_res *r, const jmme_block_res *f)
 {
   const jmme_subpel_req *q = &g_chain_sp[0];
-  sp_ent *e = &g_sp[list][ref][((size_t)mb * JMME_NSLOT + sl) * SPK + KHYP + 1];
+  sp_ent *e = &g_sp[list][ref][sp_idx(mb, sl, KHYP + 1)];
   memset(e, 0, sizeof *e);
   e->px = r->pred_x; e->py = r->pred_y; e->mx = r->mv_x; e->my = r->mv_y;
   e->min_mcost = q->start_hp ? r->cost : JMME_DISTBLK_MAX;
@@ -1122,15 +1151,18 @@ distblk __wrap_sub_pel_motion_estimation(Macroblock *currMB, MotionVector *pred_
   mb = (mv_block->pos_y >> 4) * g_mbs_x + (mv_block->pos_x >> 4);
   s = jmme_slot(mv_block->blocktype, (mv_block->pos_x & 15) >> 2, (mv_block->pos_y & 15) >> 2);
   if (s < 0 || mb < 0 || mb >= g_n_mb) error("jm_gpu_me: block outside the picture", 500);
-  e = &tab[((size_t)mb * JMME_NSLOT + s) * SPK];
-  for (i = 0; i < SPK && !sp_same(&e[i], &want, g_slot_gen[list][ref]); i++) {}
+  i = SPK;
+  if (mb == g_sp_hint_mb && s == g_sp_hint_s && sp_same(&tab[sp_idx(mb, s, g_sp_hint_k)], &want, g_slot_gen[list][ref]))
+    i = g_sp_hint_k;
+  else
+    for (i = 0; i < SPK && !sp_same(&tab[sp_idx(mb, s, i)], &want, g_slot_gen[list][ref]); i++) {}
   if (i < SPK) {
     ++g_sp_hits;
     if (i == KHYP + 1) ++g_chain_sp_hits;
-    e += i;
+    e = &tab[sp_idx(mb, s, i)];
   } else {
     sp_batch(list, ref, mb, s, &want, currMB->p_Inp->Transform8x8Mode != 0);
-    e += KHYP;
+    e = &tab[sp_idx(mb, s, KHYP)];
     if (!sp_same(e, &want, g_slot_gen[list][ref])) error("jm_gpu_me: sub-pel batch lost its own request", 500);
   }
   mv_block->mv[list].mv_x = e->omx;
