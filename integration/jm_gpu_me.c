@@ -981,8 +981,8 @@ static void sp_batch(int list, int ref, int mb0, int s0, const sp_ent *w, int t8
   sp_fill(&g_sreq[n], mb0, s0, list, ref, w);
   g_sp_dst[n++] = (int)sp_idx(mb0, s0, KHYP);
   for (mb = mb0; mb < mb1; mb++)
-    for (s = 0; s < JMME_NSLOT; s++)
-      for (k = 0; k < KHYP; k++) {
+    for (k = 0; k < KHYP; k++)          /* (both tables way-major: slots innermost walk memory in order) */
+      for (s = 0; s < JMME_NSLOT; s++) {
         const spec_ent *ie = &itab[spec_idx(mb, s, k)];
         sp_ent g = *w;
         if (ie->valid != g_slot_gen[list][ref]) continue;
