@@ -28,6 +28,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#include <x86intrin.h>
 
 #include "global.h"
 #include "mbuffer.h"
@@ -119,10 +120,12 @@ static void init_once(VideoParameters *p_Vid, InputParameters *p_Inp)
  * before any frame is timed, like JM's own table setup */
 static void prefault_tables(VideoParameters *p_Vid, InputParameters *p_Inp);
 static void reserve_batches(void);
+static void calibrate_clock(void);
 
 void __wrap_init_motion_search_module(VideoParameters *p_Vid, InputParameters *p_Inp)
 {
   __real_init_motion_search_module(p_Vid, p_Inp);
+  calibrate_clock();   /* (before any picture is timed) */
   if (p_Inp->SearchMode[0] == FULL_SEARCH || p_Inp->SearchMode[0] == FAST_FULL_SEARCH || p_Inp->SearchMode[0] == EPZS) {
     init_once(p_Vid, p_Inp);
     if (jmme_prepare(g_me)) fail_jm("jmme_prepare");
@@ -254,11 +257,31 @@ static int g_req_cap = 0;
 static long long g_miss_past = 0, g_miss_guess = 0, g_miss_slot[JMME_NSLOT], g_units = 0;
 static double g_t_build = 0, g_t_call = 0, g_t_wrap = 0;
 
-static double now_us(void)
+/* the adapter's timers read the TSC (a few ns; clock_gettime per EPZS call cost
+ * tens of ms per 1080p picture), scaled by a rate measured against
+ * CLOCK_MONOTONIC when the encoder starts (calibrate_clock) */
+static double g_us_per_tick = 0;
+static double mono_us(void)
 {
   struct timespec ts;
   clock_gettime(CLOCK_MONOTONIC, &ts);
   return ts.tv_sec * 1e6 + ts.tv_nsec * 1e-3;
+}
+static void calibrate_clock(void)
+{
+  double t0, t1;
+  unsigned long long c0, c1;
+  if (g_us_per_tick > 0) return;
+  t0 = mono_us();
+  c0 = __rdtsc();
+  do t1 = mono_us(); while (t1 - t0 < 2000.0);
+  c1 = __rdtsc();
+  g_us_per_tick = (t1 - t0) / (double)(c1 - c0);
+}
+static double now_us(void)
+{
+  if (g_us_per_tick <= 0) calibrate_clock();
+  return (double)__rdtsc() * g_us_per_tick;
 }
 
 static spec_ent *spec_table(VideoParameters *p_Vid, int list, int ref)
@@ -1826,12 +1849,13 @@ static const ep_ans *ep_miss(Macroblock *currMB, MEBlock *mv_block, const jmme_e
       const int px = col * 16 + g_slot_bx[t], py = (x / g_mbs_x) * 16 + g_slot_by[t];
       for (r = 0; r < EP_REFS; r++) {
         int *idx = &g_ep_idx[(((size_t)(x - mb) * JMME_NSLOT + t) * EP_REFS + r) * EP_WAYS];
+        if (!g_slot_gen[0][r]) continue;   /* a reference not in use: nothing seen for it */
         w = 0;
         while (w < EP_WAYS && idx[w] >= 0) w++;
         for (i = 0; i < ns && w < EP_WAYS; i++) {
           const ep_in *e = ep_seen_at(src[i], t, r);
           int d;
-          if (e->mb != src[i] || e->gen != g_slot_gen[0][r] || !g_slot_gen[0][r]) continue;
+          if (!g_slot_gen[0][r] || e->mb != src[i] || e->gen != g_slot_gen[0][r]) continue;
           for (d = 0; d < w; d++) {   /* a guess already made for this partition */
             const ep_in *o = idx[d] == 0 ? &want : &g_ep_ans[idx[d]].in;
             if (ep_same_moved(o, e) && o->q.pos_x == px && o->q.pos_y == py) break;
@@ -1980,9 +2004,11 @@ static distblk epzs_gpu(int variant, Macroblock *currMB, MotionVector *pred_mv, 
   if (ep_speculating(currMB, cur_list, ref, n_pred)) {
     /* the speculative path: a cached answer whose inputs are this call's, or a batch */
     a = ep_lookup(currMB, mv_block, &q, g_ep_pred, g_ep_cond, g_ep_stale, n_stale);
-    t1 = now_us();
-    if (!a) a = ep_miss(currMB, mv_block, &q, g_ep_pred, g_ep_cond, g_ep_stale, n_stale);
-    g_t_epzs_gpu += now_us() - t1;
+    if (!a) {   /* (hits are not timed: two clock reads per call were a tenth of the hits' cost) */
+      t1 = now_us();
+      a = ep_miss(currMB, mv_block, &q, g_ep_pred, g_ep_cond, g_ep_stale, n_stale);
+      g_t_epzs_gpu += now_us() - t1;
+    }
     if (a->res.n_visited > EP_MAXV) {   /* (the call itself stamped more cells than a batch keeps: searched again) */
       ++g_ep_overflow;
       a = NULL;
