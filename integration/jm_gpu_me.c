@@ -1299,6 +1299,8 @@ static void epzs_ring_sync(EPZSParameters *p_EPZS, int side)
   g_ring_count = (int)p_EPZS->BlkCount;
 }
 
+static int g_ep_bt_start = 0;   /* where the last list's block-type predictors start (EPZSBlockTypePredictors*) */
+
 /* the predictor list JM would build for this search, every conditional part
  * included and tagged; returns the count (pool: g_ep_pred / g_ep_cond) */
 static int epzs_predictors(int variant, Macroblock *currMB, MEBlock *mv_block, distblk stop)
@@ -1347,6 +1349,7 @@ static int epzs_predictors(int variant, Macroblock *currMB, MEBlock *mv_block, d
       for (i = start; i < n; i++) cond[i] = (uint8_t)(always ? JMME_EPZS_PRED_ALWAYS : JMME_EPZS_PRED_GT_3STOP);
     }
   }
+  g_ep_bt_start = n;
   if (currMB->mbAddrX != 0 && p_Inp->EPZSBlockType) {   /* ref == 0 || min_mcost > 2 * stop */
     int start = n;
     if (sub)
@@ -1417,6 +1420,7 @@ typedef struct ep_in {             /* one search's inputs */
   uint8_t cond[EP_MAXP];
   int32_t mb;                      /* the macroblock (seen ring: which one the entry holds) */
   uint32_t gen;                    /* g_slot_gen of its reference when stored (0: empty) */
+  int32_t bt_start;                /* its block-type predictors are pred[bt_start .. n_pred) (not compared) */
 } ep_in;
 
 typedef struct ep_ans {            /* a searched guess: inputs, result, validity, chained refinement */
@@ -1448,6 +1452,7 @@ static jmme_epzs_bounds *g_ep_bnd = NULL;
 static int16_t *g_ep_vbuf = NULL;
 static jmme_subpel_req *g_ep_spq = NULL;
 static jmme_block_res *g_ep_spo = NULL;
+static int32_t *g_ep_bts = NULL;   /* [g_ep_cap]: bt_start of each request's list */
 static int g_ep_pcap = 0;
 static long long g_ep_hits = 0, g_ep_batches = 0, g_ep_singles = 0, g_ep_guesses = 0, g_ep_direct = 0;
 static long long g_ep_fail_bounds = 0, g_ep_fail_stale = 0, g_ep_fail_inputs = 0, g_ep_sp_hits = 0, g_ep_overflow = 0;
@@ -1459,6 +1464,7 @@ static long long g_ep_miss_slot[JMME_NSLOT], g_ep_list_diff[JMME_NSLOT];   /* mi
 static long long g_ep_miss_kind[4], g_ep_stop_off[24];
 static int g_ep_trace = 0;   /* JMME_EPZS_TRACE=1: per-slot miss counts at exit */
 static int g_ep_two_pass = 1;   /* JMME_EPZS_PASS2=0: no second pass (ep_pass2) */
+static int g_ep_dump = 0;       /* JMME_EPZS_DUMP=n: print the first n input misses (measurement) */
 
 static int ep_speculating(Macroblock *currMB, int cur_list, int ref, int n_pred)
 {
@@ -1469,6 +1475,8 @@ static int ep_speculating(Macroblock *currMB, int cur_list, int ref, int n_pred)
     {
       const char *p2 = getenv("JMME_EPZS_PASS2");
       g_ep_two_pass = !(p2 && p2[0] == '0');
+      const char *dp = getenv("JMME_EPZS_DUMP");
+      g_ep_dump = dp ? atoi(dp) : 0;
     }
     if (b && atoi(b) > 0) g_ep_batch = imin(atoi(b), EP_BATCH_MAX);
   }
@@ -1545,6 +1553,7 @@ static const ep_ans *ep_lookup(Macroblock *currMB, MEBlock *mv_block, const jmme
     if (!g_ep_seen) error("jm_gpu_me: out of memory", 500);
   }
   ep_fill_in(ep_seen_at(mb, slot, ref), q, pred, cond, mb, gen);
+  ep_seen_at(mb, slot, ref)->bt_start = g_ep_bt_start;
   if (!gen || g_ep_gens[ref] != gen || mb < g_ep_mb0 || mb >= g_ep_mb1) return NULL;
   ++g_ep_miss_slot[slot];   /* (taken back below on a hit) */
   int kind = 0;
@@ -1589,6 +1598,28 @@ static const ep_ans *ep_lookup(Macroblock *currMB, MEBlock *mv_block, const jmme
   }
   ++g_ep_fail_inputs;
   ++g_ep_miss_kind[kind];
+  if (kind == 0 && g_ep_dump > 0 &&   /* JMME_EPZS_DUMP=n: the first n input misses that had guesses */
+      g_ep_idx[(((size_t)(mb - g_ep_mb0) * JMME_NSLOT + slot) * EP_REFS + ref) * EP_WAYS] >= 0) {
+    --g_ep_dump;
+    fprintf(stderr, "epzs-miss mb %d slot %d: c(%d,%d) p(%d,%d) n %d:", mb, slot, q->center_x, q->center_y, q->pred_x,
+            q->pred_y, q->n_pred);
+    for (i = 0; i < q->n_pred; i++) fprintf(stderr, " %d,%d/%d", pred[2 * i], pred[2 * i + 1], cond[i]);
+    fprintf(stderr, "\n");
+    for (w = 0; w < EP_WAYS; w++) {
+      const int k = g_ep_idx[(((size_t)(mb - g_ep_mb0) * JMME_NSLOT + slot) * EP_REFS + ref) * EP_WAYS + w];
+      const ep_in *a;
+      if (k < 0) break;
+      a = &g_ep_ans[k].in;
+      fprintf(stderr, "  way %d: c(%d,%d) p(%d,%d) n %d lam %d:", w, a->q.center_x, a->q.center_y, a->q.pred_x,
+              a->q.pred_y, a->q.n_pred, a->q.lambda);
+      for (i = 0; i < a->q.n_pred; i++) {
+        const int16_t *ap = (const int16_t *)a->pred;
+        const int same = i < q->n_pred && ap[2 * i] == pred[2 * i] && ap[2 * i + 1] == pred[2 * i + 1] && a->cond[i] == cond[i];
+        fprintf(stderr, same ? " ." : " %d,%d/%d", ap[2 * i], ap[2 * i + 1], a->cond[i]);
+      }
+      fprintf(stderr, "\n");
+    }
+  }
   if (kind == 1) {
     int b = 0;
     while (b < 23 && (stop_off >> b) > 0) ++b;
@@ -1602,6 +1633,8 @@ static void ep_grow(int n, int n_pred)
   if (n > g_ep_cap) {
     g_ep_cap = imax(n, 2 * g_ep_cap);
     free(g_ep_ans); free(g_ep_q); free(g_ep_res); free(g_ep_bnd); free(g_ep_vbuf); free(g_ep_spq); free(g_ep_spo);
+    free(g_ep_bts);
+    g_ep_bts = (int32_t *)malloc((size_t)g_ep_cap * sizeof(int32_t));
     g_ep_ans = (ep_ans *)malloc((size_t)g_ep_cap * sizeof(ep_ans));
     g_ep_q = (jmme_epzs_req *)malloc((size_t)g_ep_cap * sizeof(jmme_epzs_req));
     g_ep_res = (jmme_epzs_res *)malloc((size_t)g_ep_cap * sizeof(jmme_epzs_res));
@@ -1609,7 +1642,7 @@ static void ep_grow(int n, int n_pred)
     g_ep_vbuf = (int16_t *)malloc((size_t)g_ep_cap * EP_MAXV * 4);
     g_ep_spq = (jmme_subpel_req *)malloc((size_t)g_ep_cap * sizeof(jmme_subpel_req));
     g_ep_spo = (jmme_block_res *)malloc((size_t)g_ep_cap * sizeof(jmme_block_res));
-    if (!g_ep_ans || !g_ep_q || !g_ep_res || !g_ep_bnd || !g_ep_vbuf || !g_ep_spq || !g_ep_spo)
+    if (!g_ep_ans || !g_ep_q || !g_ep_res || !g_ep_bnd || !g_ep_vbuf || !g_ep_spq || !g_ep_spo || !g_ep_bts)
       error("jm_gpu_me: out of memory", 500);
   }
   if (n_pred > g_ep_pcap) {
@@ -1636,6 +1669,7 @@ static void ep_add(int k, const ep_in *e, int pos_x, int pos_y, EPZSParameters *
   memcpy(g_ep_ppool + 2 * (size_t)g_ep_np, e->pred, (size_t)e->q.n_pred * 4);
   memcpy(g_ep_cpool + g_ep_np, e->cond, (size_t)e->q.n_pred);
   g_ep_np += e->q.n_pred;
+  g_ep_bts[k] = e->bt_start;
   memset(sp, 0, sizeof *sp);
   if (g_ep_spp.valid) {   /* EPZS_sub_pel_motion_estimation of the result (mv_search.c:966-976) */
     sp->pos_x = (int16_t)pos_x;
@@ -1673,6 +1707,7 @@ static void ep_run_from(int k0, int n, const int16_t *stale, int n_stale, unsign
     ep_ans *a = &g_ep_ans[k];
     const int16_t *pp = g_ep_ppool + 2 * (size_t)g_ep_q[k].pred_off;
     ep_fill_in(&a->in, &g_ep_q[k], pp, g_ep_cpool + g_ep_q[k].pred_off, -1, gen);
+    a->in.bt_start = g_ep_bts[k];
     a->res = g_ep_res[k];
     a->bnd = g_ep_bnd[k];
     memcpy(a->vis, g_ep_vbuf + 2 * (size_t)EP_MAXV * k, (size_t)imin(a->res.n_visited, EP_MAXV) * 4);
@@ -1702,6 +1737,8 @@ static void ep_run(int n, const int16_t *stale, int n_stale, unsigned gen) { ep_
 static int64_t *g_ep_vrow = NULL;   /* [7][columns]: the replayed distortion rows */
 static int g_ep_vcols = 0;
 static long long g_ep_pass2 = 0, g_ep_pass2_batches = 0;
+static long long g_ep_tail_fixes = 0;   /* second-pass guesses whose block-type predictors were replaced */
+static ep_in g_ep_fix;                  /* (a guess's inputs with its tail replaced) */
 
 static int ep_avail_c(int bx, int by, int bsx)   /* get_neighbors' upper-right rule inside the MB (mv_search.c:283-301) */
 {
@@ -1770,19 +1807,67 @@ static void ep_pass2(Macroblock *currMB, int mb0, int s0, int nmb, unsigned gen,
         }
         for (nw = 0; nw < EP_WAYS && idx[nw] >= 0; nw++) {}
         const int nw0 = nw;   /* the first pass's ways (the ones added here are searched after the loop) */
+        /* the block-type predictors JM will append (EPZSBlockTypePredictors(MB), me_epzs_common.c:1224-1266,
+         * 1608-1645; ref 0, frame): this macroblock's final vectors of the parent block type and of the
+         * 16x16 at this position (all_mv, set after SubPelME), as the batch's first guesses answered them */
+        int16_t tail[2][2];
+        int n_tail = -1;
+        if (p_Inp->EPZSBlockType && x != 0 && bt != 1) {
+          /* BLOCK_PARENT (me_epzs_common.c:32) and each block type's size in 4x4 units */
+          static const int kParent[8] = {1, 1, 1, 1, 2, 4, 4, 5}, kW4[8] = {0, 4, 4, 2, 2, 2, 1, 1},
+                           kH4[8] = {0, 4, 2, 4, 2, 1, 2, 1};
+          const int sub = g_ep_ans[idx[0]].in.q.variant & 1, P = kParent[bt];
+          const int x4 = bx >> 2, y4 = by >> 2;
+          const int ps[2] = {jmme_slot(P, x4 - x4 % kW4[P], y4 - y4 % kH4[P]), (sub || P != 1) ? 0 : -1};
+          int j;
+          n_tail = 0;
+          for (j = 0; j < 2 && ps[j] >= 0 && n_tail >= 0; j++) {
+            const int pk = g_ep_idx[(((size_t)(x - mb0) * JMME_NSLOT + ps[j]) * EP_REFS + 0) * EP_WAYS];
+            const ep_ans *pa = pk >= 0 ? &g_ep_ans[pk] : NULL;
+            if (!pa || !pa->spq.blocktype) { n_tail = -1; break; }   /* (no chained refinement: final vector unknown) */
+            if (pa->sp_res.mv_x | pa->sp_res.mv_y) {
+              tail[n_tail][0] = pa->sp_res.mv_x;
+              tail[n_tail][1] = pa->sp_res.mv_y;
+              ++n_tail;
+            }
+          }
+        }
         for (w = 0; w < nw0 && nw < EP_WAYS; w++) {
           const ep_ans *a = &g_ep_ans[idx[w]];
+          const ep_in *in = &a->in;
           if (idx[w] == 0 && x == mb0 && t == s0) continue;   /* the real call */
-          if (stop >= a->bnd.stop_lo && stop <= a->bnd.stop_hi && prev >= a->bnd.prev_lo && prev <= a->bnd.prev_hi)
+          if (n_tail >= 0 && a->in.bt_start <= a->in.q.n_pred && a->in.bt_start + n_tail <= EP_MAXP) {
+            const int16_t *ap = (const int16_t *)a->in.pred;
+            int same = a->in.q.n_pred == a->in.bt_start + n_tail, j;
+            for (j = 0; same && j < n_tail; j++)
+              same = ap[2 * (a->in.bt_start + j)] == tail[j][0] && ap[2 * (a->in.bt_start + j) + 1] == tail[j][1] &&
+                     a->in.cond[a->in.bt_start + j] == JMME_EPZS_PRED_ALWAYS;
+            if (!same) {   /* the neighbour's block-type predictors replaced by this macroblock's */
+              int16_t *tp;
+              g_ep_fix = a->in;
+              tp = (int16_t *)g_ep_fix.pred;
+              for (j = 0; j < n_tail; j++) {
+                tp[2 * (a->in.bt_start + j)] = tail[j][0];
+                tp[2 * (a->in.bt_start + j) + 1] = tail[j][1];
+                g_ep_fix.cond[a->in.bt_start + j] = JMME_EPZS_PRED_ALWAYS;
+              }
+              g_ep_fix.q.n_pred = a->in.bt_start + n_tail;
+              in = &g_ep_fix;
+              ++g_ep_tail_fixes;
+            }
+          }
+          if (in == &a->in && stop >= a->bnd.stop_lo && stop <= a->bnd.stop_hi && prev >= a->bnd.prev_lo &&
+              prev <= a->bnd.prev_hi)
             continue;
           for (k = 0; k < nw0; k++) {   /* a way with these inputs that already holds the pair */
             const ep_ans *o = &g_ep_ans[idx[k]];
-            if (k != w && stop >= o->bnd.stop_lo && stop <= o->bnd.stop_hi && prev >= o->bnd.prev_lo &&
-                prev <= o->bnd.prev_hi && ep_same(&o->in, &a->in.q, (const int16_t *)a->in.pred, a->in.cond))
+            if ((k != w || in != &a->in) && stop >= o->bnd.stop_lo && stop <= o->bnd.stop_hi &&
+                prev >= o->bnd.prev_lo && prev <= o->bnd.prev_hi &&
+                ep_same(&o->in, &in->q, (const int16_t *)in->pred, in->cond))
               break;
           }
           if (k < nw0) continue;
-          ep_add(n, &a->in, px, py, p_EPZS);
+          ep_add(n, in, px, py, p_EPZS);
           g_ep_q[n].stop_crit = stop;
           g_ep_q[n].prev_sad = prev;
           idx[nw++] = n++;
@@ -1813,6 +1898,7 @@ static const ep_ans *ep_miss(Macroblock *currMB, MEBlock *mv_block, const jmme_e
   int n = 1, x, t, r, w, nmb;
   double t0 = now_us();
   ep_fill_in(&want, q, pred, cond, mb, gen);
+  want.bt_start = g_ep_bt_start;
   if (inside) {   /* a guess failed: this call alone; the batch's other guesses stand */
     ep_grow(1, q->n_pred);
     g_ep_np = 0;
@@ -1863,6 +1949,7 @@ static const ep_ans *ep_miss(Macroblock *currMB, MEBlock *mv_block, const jmme_e
           if (d < w) continue;
           ep_add(n, e, px, py, p_EPZS);
           g_ep_ans[n].in.q = g_ep_q[n];   /* (dedup reads the guess's inputs before the run) */
+          g_ep_ans[n].in.bt_start = e->bt_start;
           g_ep_ans[n].in.q.pos_x = (int16_t)px;
           g_ep_ans[n].in.q.pos_y = (int16_t)py;
           memcpy(g_ep_ans[n].in.pred, e->pred, (size_t)e->q.n_pred * 4);
@@ -2176,9 +2263,9 @@ static void report(void)
       fprintf(stderr, "jm_gpu_me: EPZS speculation: %lld searches answered from %lld batches (%lld guesses), "
                       "%lld searched alone; %lld not speculated; guesses refused: %lld inputs, %lld bounds, "
                       "%lld map cells; %.1f ms building batches; %lld searched again (more stamped cells than kept); "
-                      "%lld second-pass guesses in %lld launches\n",
+                      "%lld second-pass guesses in %lld launches (%lld with this macroblock's block-type predictors)\n",
               g_ep_hits, g_ep_batches, g_ep_guesses, g_ep_singles, g_ep_direct, g_ep_fail_inputs, g_ep_fail_bounds,
-              g_ep_fail_stale, g_t_ep_build * 1e-3, g_ep_overflow, g_ep_pass2, g_ep_pass2_batches);
+              g_ep_fail_stale, g_t_ep_build * 1e-3, g_ep_overflow, g_ep_pass2, g_ep_pass2_batches, g_ep_tail_fixes);
     if (g_ep_trace) {
       int sl;
       fprintf(stderr, "jm_gpu_me: EPZS misses inside batches by slot (list-only differences):");

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--frames", type=int, default=2)
     ap.add_argument("--size", default="1920x1080")
     ap.add_argument("--env", action="append", default=[])
+    ap.add_argument("--raw", action="store_true", help="print the encoder's whole stderr")
     ap.add_argument("params", nargs="*")
     a = ap.parse_args()
     from jmme import synth
@@ -49,7 +50,7 @@ def main():
     enc = re.search(r"Total encoding time for the seq\.\s*:\s*([0-9.]+) sec", r.stdout)
     print("ME time", me.group(1) if me else None, "encoding time", enc.group(1) if enc else None, "rc", r.returncode)
     for line in r.stderr.splitlines():
-        if line.startswith("jm_gpu_me") or line.startswith("jm_f3_profile"):
+        if a.raw or line.startswith("jm_gpu_me") or line.startswith("jm_f3_profile"):
             print(line)
     return r.returncode
 
