@@ -1605,6 +1605,17 @@ static const ep_ans *ep_lookup(Macroblock *currMB, MEBlock *mv_block, const jmme
             q->pred_y, q->n_pred);
     for (i = 0; i < q->n_pred; i++) fprintf(stderr, " %d,%d/%d", pred[2 * i], pred[2 * i + 1], cond[i]);
     fprintf(stderr, "\n");
+    {   /* the macroblock's first-guess answers by slot (integer / after SubPelME) */
+      int sl;
+      fprintf(stderr, "  answers:");
+      for (sl = 0; sl < JMME_NSLOT; sl++) {
+        const int k0 = g_ep_idx[(((size_t)(mb - g_ep_mb0) * JMME_NSLOT + sl) * EP_REFS + ref) * EP_WAYS];
+        if (k0 < 0) fprintf(stderr, " %d:-", sl);
+        else fprintf(stderr, " %d:%d,%d/%d,%d", sl, g_ep_ans[k0].res.mv_x, g_ep_ans[k0].res.mv_y, g_ep_ans[k0].sp_res.mv_x,
+                     g_ep_ans[k0].sp_res.mv_y);
+      }
+      fprintf(stderr, "\n");
+    }
     for (w = 0; w < EP_WAYS; w++) {
       const int k = g_ep_idx[(((size_t)(mb - g_ep_mb0) * JMME_NSLOT + slot) * EP_REFS + ref) * EP_WAYS + w];
       const ep_in *a;
@@ -1738,6 +1749,7 @@ static int64_t *g_ep_vrow = NULL;   /* [7][columns]: the replayed distortion row
 static int g_ep_vcols = 0;
 static long long g_ep_pass2 = 0, g_ep_pass2_batches = 0;
 static long long g_ep_tail_fixes = 0;   /* second-pass guesses whose block-type predictors were replaced */
+static long long g_ep_spatial_fixes = 0;   /* ... whose spatial predictors inside the macroblock were */
 static ep_in g_ep_fix;                  /* (a guess's inputs with its tail replaced) */
 
 static int ep_avail_c(int bx, int by, int bsx)   /* get_neighbors' upper-right rule inside the MB (mv_search.c:283-301) */
@@ -1832,30 +1844,68 @@ static void ep_pass2(Macroblock *currMB, int mb0, int s0, int nmb, unsigned gen,
             }
           }
         }
+        /* the spatial predictors of neighbours inside this macroblock (EPZS_spatial_predictors,
+         * me_epzs_common.c:1276-1370: left, up, up-right -- the up-left when get_neighbors,
+         * mv_search.c:283-306, makes it unavailable -- and up-left): JM reads mv_info there, which
+         * held the refined answer of the same block type's partition at that place in 95-98 % of the
+         * misses dumped (JMME_EPZS_DUMP); ref 0, so scale_mv is the identity */
+        int16_t sp[5][2] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}};
+        int sp_on[5] = {0, 0, 0, 0, 0};
+        {
+          static const int kW4[8] = {0, 4, 4, 2, 2, 2, 1, 1}, kH4[8] = {0, 4, 2, 4, 2, 1, 2, 1};
+          const int x4 = bx >> 2, y4 = by >> 2, w4 = kW4[bt], h4 = kH4[bt];
+          const int cav = ep_avail_c(bx, by, 4 * w4);
+          const int nx[5] = {0, x4 - 1, x4, cav ? x4 + w4 : x4 - 1, x4 - 1};
+          const int ny[5] = {0, y4, y4 - 1, y4 - 1, y4 - 1};
+          int j;
+          for (j = 1; j <= 4; j++) {
+            int pk;
+            const ep_ans *pa;
+            if (nx[j] < 0 || nx[j] > 3 || ny[j] < 0 || ny[j] > 3) continue;
+            pk = g_ep_idx[(((size_t)(x - mb0) * JMME_NSLOT + jmme_slot(bt, nx[j] - nx[j] % w4, ny[j] - ny[j] % h4)) *
+                           EP_REFS + 0) * EP_WAYS];
+            pa = pk >= 0 ? &g_ep_ans[pk] : NULL;
+            if (!pa || !pa->spq.blocktype) continue;
+            sp[j][0] = pa->sp_res.mv_x;
+            sp[j][1] = pa->sp_res.mv_y;
+            sp_on[j] = 1;
+          }
+        }
         for (w = 0; w < nw0 && nw < EP_WAYS; w++) {
           const ep_ans *a = &g_ep_ans[idx[w]];
           const ep_in *in = &a->in;
+          int fixed = 0, j;
           if (idx[w] == 0 && x == mb0 && t == s0) continue;   /* the real call */
+          g_ep_fix = a->in;
+          if (a->in.q.n_pred >= 5) {
+            int16_t *tp = (int16_t *)g_ep_fix.pred;
+            for (j = 1; j <= 4; j++)
+              if (sp_on[j] && (tp[2 * j] != sp[j][0] || tp[2 * j + 1] != sp[j][1])) {
+                tp[2 * j] = sp[j][0];
+                tp[2 * j + 1] = sp[j][1];
+                fixed = 1;
+              }
+            if (fixed) ++g_ep_spatial_fixes;
+          }
           if (n_tail >= 0 && a->in.bt_start <= a->in.q.n_pred && a->in.bt_start + n_tail <= EP_MAXP) {
             const int16_t *ap = (const int16_t *)a->in.pred;
-            int same = a->in.q.n_pred == a->in.bt_start + n_tail, j;
+            int same = a->in.q.n_pred == a->in.bt_start + n_tail;
             for (j = 0; same && j < n_tail; j++)
               same = ap[2 * (a->in.bt_start + j)] == tail[j][0] && ap[2 * (a->in.bt_start + j) + 1] == tail[j][1] &&
                      a->in.cond[a->in.bt_start + j] == JMME_EPZS_PRED_ALWAYS;
             if (!same) {   /* the neighbour's block-type predictors replaced by this macroblock's */
-              int16_t *tp;
-              g_ep_fix = a->in;
-              tp = (int16_t *)g_ep_fix.pred;
+              int16_t *tp = (int16_t *)g_ep_fix.pred;
               for (j = 0; j < n_tail; j++) {
                 tp[2 * (a->in.bt_start + j)] = tail[j][0];
                 tp[2 * (a->in.bt_start + j) + 1] = tail[j][1];
                 g_ep_fix.cond[a->in.bt_start + j] = JMME_EPZS_PRED_ALWAYS;
               }
               g_ep_fix.q.n_pred = a->in.bt_start + n_tail;
-              in = &g_ep_fix;
+              fixed = 1;
               ++g_ep_tail_fixes;
             }
           }
+          if (fixed) in = &g_ep_fix;
           if (in == &a->in && stop >= a->bnd.stop_lo && stop <= a->bnd.stop_hi && prev >= a->bnd.prev_lo &&
               prev <= a->bnd.prev_hi)
             continue;
@@ -2263,9 +2313,11 @@ static void report(void)
       fprintf(stderr, "jm_gpu_me: EPZS speculation: %lld searches answered from %lld batches (%lld guesses), "
                       "%lld searched alone; %lld not speculated; guesses refused: %lld inputs, %lld bounds, "
                       "%lld map cells; %.1f ms building batches; %lld searched again (more stamped cells than kept); "
-                      "%lld second-pass guesses in %lld launches (%lld with this macroblock's block-type predictors)\n",
+                      "%lld second-pass guesses in %lld launches (%lld with this macroblock's block-type predictors, "
+                      "%lld with its inner spatial predictors)\n",
               g_ep_hits, g_ep_batches, g_ep_guesses, g_ep_singles, g_ep_direct, g_ep_fail_inputs, g_ep_fail_bounds,
-              g_ep_fail_stale, g_t_ep_build * 1e-3, g_ep_overflow, g_ep_pass2, g_ep_pass2_batches, g_ep_tail_fixes);
+              g_ep_fail_stale, g_t_ep_build * 1e-3, g_ep_overflow, g_ep_pass2, g_ep_pass2_batches, g_ep_tail_fixes,
+              g_ep_spatial_fixes);
     if (g_ep_trace) {
       int sl;
       fprintf(stderr, "jm_gpu_me: EPZS misses inside batches by slot (list-only differences):");
