@@ -1299,7 +1299,9 @@ static void epzs_ring_sync(EPZSParameters *p_EPZS, int side)
   g_ring_count = (int)p_EPZS->BlkCount;
 }
 
-static int g_ep_bt_start = 0;   /* where the last list's block-type predictors start (EPZSBlockTypePredictors*) */
+/* the last list's layout: where its block-type predictors start (EPZSBlockTypePredictors*), low 16 bits,
+ * and where its spatial-memory predictors end (EPZS_spatial_memory_predictors), high 16 bits */
+static int g_ep_bt_start = 0, g_ep_mem_end = 0;
 
 /* the predictor list JM would build for this search, every conditional part
  * included and tagged; returns the count (pool: g_ep_pred / g_ep_cond) */
@@ -1321,6 +1323,7 @@ static int epzs_predictors(int variant, Macroblock *currMB, MEBlock *mv_block, d
   invalid_refs = EPZS_spatial_predictors(p_EPZS, mv_block, list, currMB->list_offset, (short)ref,
                                          p_Vid->enc_picture->mv_info);
   if (p_Inp->EPZSSpatialMem) EPZS_spatial_memory_predictors(p_EPZS, mv_block, cur_list, &n, ref_picture->size_x >> 2);
+  g_ep_mem_end = n;
   for (i = 0; i < n; i++) cond[i] = JMME_EPZS_PRED_ALWAYS;
 #if (MVC_EXTENSION_ENABLE)
   if (!sub && p_Inp->EPZSTemporal[currSlice->view_id] && (grid || bt < 5))
@@ -1349,7 +1352,7 @@ static int epzs_predictors(int variant, Macroblock *currMB, MEBlock *mv_block, d
       for (i = start; i < n; i++) cond[i] = (uint8_t)(always ? JMME_EPZS_PRED_ALWAYS : JMME_EPZS_PRED_GT_3STOP);
     }
   }
-  g_ep_bt_start = n;
+  g_ep_bt_start = n | (g_ep_mem_end << 16);
   if (currMB->mbAddrX != 0 && p_Inp->EPZSBlockType) {   /* ref == 0 || min_mcost > 2 * stop */
     int start = n;
     if (sub)
@@ -1420,7 +1423,8 @@ typedef struct ep_in {             /* one search's inputs */
   uint8_t cond[EP_MAXP];
   int32_t mb;                      /* the macroblock (seen ring: which one the entry holds) */
   uint32_t gen;                    /* g_slot_gen of its reference when stored (0: empty) */
-  int32_t bt_start;                /* its block-type predictors are pred[bt_start .. n_pred) (not compared) */
+  int32_t bt_start;                /* layout (not compared): block-type predictors from (bt_start & 0xffff),
+                                      spatial-memory predictors pred[5 .. bt_start >> 16) */
 } ep_in;
 
 typedef struct ep_ans {            /* a searched guess: inputs, result, validity, chained refinement */
@@ -1748,8 +1752,7 @@ static void ep_run(int n, const int16_t *stale, int n_stale, unsigned gen) { ep_
 static int64_t *g_ep_vrow = NULL;   /* [7][columns]: the replayed distortion rows */
 static int g_ep_vcols = 0;
 static long long g_ep_pass2 = 0, g_ep_pass2_batches = 0;
-static long long g_ep_tail_fixes = 0;   /* second-pass guesses whose block-type predictors were replaced */
-static long long g_ep_spatial_fixes = 0;   /* ... whose spatial predictors inside the macroblock were */
+static long long g_ep_list_fixes = 0;   /* second-pass guesses whose list was rebuilt from this batch's answers */
 static ep_in g_ep_fix;                  /* (a guess's inputs with its tail replaced) */
 
 static int ep_avail_c(int bx, int by, int bsx)   /* get_neighbors' upper-right rule inside the MB (mv_search.c:283-301) */
@@ -1871,41 +1874,79 @@ static void ep_pass2(Macroblock *currMB, int mb0, int s0, int nmb, unsigned gen,
             sp_on[j] = 1;
           }
         }
+        /* the spatial-memory predictors (EPZS_spatial_memory_predictors, me_epzs_common.c:1675-1718,
+         * EPZSREF): p_motion[ref][blocktype - 1][block row][picture column] at the left, up and up-right
+         * block, i.e. the `tmp` of the same block type's search there -- this batch's answer where JM
+         * will have searched it before this call (this macroblock, or one left of it in the batch),
+         * otherwise JM's memory as it stands (the row above, or macroblocks JM has done) */
+        int16_t mem[3][2];
+        int n_mem = -1;
+        if (p_Inp->EPZSSpatialMem && p_EPZS->p_motion) {
+          static const int kW4[8] = {0, 4, 4, 2, 2, 2, 1, 1}, kH4[8] = {0, 4, 2, 4, 2, 1, 2, 1};
+          const int w4 = kW4[bt], h4 = kH4[bt], x4 = bx >> 2, y4 = by >> 2, xc = x % g_mbs_x, w4pic = p_Vid->width >> 2;
+          const int pic_x = xc * 4 + x4, up = y4 > 0 ? y4 - h4 : 4 - h4;
+          const int rk_t = g_slot_grp[t] * 4 + g_slot_idx[t], rk_s0 = g_slot_grp[s0] * 4 + g_slot_idx[s0];
+          int rc[3][2], nrc = 0, j;
+          MotionVector **pm = p_EPZS->p_motion[0][0][bt - 1];
+          if (pic_x > 0) { rc[nrc][0] = y4; rc[nrc++][1] = pic_x - w4; }
+          rc[nrc][0] = up; rc[nrc++][1] = pic_x;
+          if (pic_x + w4 < w4pic) { rc[nrc][0] = up; rc[nrc++][1] = pic_x + w4; }
+          n_mem = 0;
+          for (j = 0; j < nrc && n_mem >= 0; j++) {
+            const int row = rc[j][0], col = rc[j][1], cm = col >> 2, xr = x - (xc - cm);
+            const int sl = jmme_slot(bt, (col & 3) - (col & 3) % w4, row - row % h4);
+            const int rk = g_slot_grp[sl] * 4 + g_slot_idx[sl];
+            int16_t vx, vy;
+            /* searched in this batch before this call, and not yet by JM when the batch was made */
+            const int batch = (cm == xc && rk < rk_t) || (cm < xc && xr >= mb0);
+            if (batch && !(xr == mb0 && rk < rk_s0)) {
+              const int pk = g_ep_idx[(((size_t)(xr - mb0) * JMME_NSLOT + sl) * EP_REFS + 0) * EP_WAYS];
+              if (pk < 0) { n_mem = -1; break; }
+              vx = g_ep_ans[pk].res.motion_x;
+              vy = g_ep_ans[pk].res.motion_y;
+            } else {
+              vx = pm[row][col].mv_x;
+              vy = pm[row][col].mv_y;
+            }
+            if (vx | vy) { mem[n_mem][0] = vx; mem[n_mem][1] = vy; ++n_mem; }
+          }
+        }
         for (w = 0; w < nw0 && nw < EP_WAYS; w++) {
           const ep_ans *a = &g_ep_ans[idx[w]];
           const ep_in *in = &a->in;
-          int fixed = 0, j;
+          const int np = a->in.q.n_pred, bs = a->in.bt_start & 0xffff, me = a->in.bt_start >> 16;
+          const int16_t *ap = (const int16_t *)a->in.pred;
+          int fixed = 0, j, o;
+          int16_t *tp;
           if (idx[w] == 0 && x == mb0 && t == s0) continue;   /* the real call */
-          g_ep_fix = a->in;
-          if (a->in.q.n_pred >= 5) {
-            int16_t *tp = (int16_t *)g_ep_fix.pred;
-            for (j = 1; j <= 4; j++)
-              if (sp_on[j] && (tp[2 * j] != sp[j][0] || tp[2 * j + 1] != sp[j][1])) {
-                tp[2 * j] = sp[j][0];
-                tp[2 * j + 1] = sp[j][1];
-                fixed = 1;
-              }
-            if (fixed) ++g_ep_spatial_fixes;
+          const int shaped = np >= 5 && me >= 5 && me <= bs && bs <= np;   /* (else: only the stop replay) */
+          /* rebuild: spatial [0, 5) | spatial memory [5, me) | temporal + window [me, bs) | block type [bs, np) */
+          if (shaped) g_ep_fix = a->in;
+          tp = (int16_t *)g_ep_fix.pred;
+          o = 5;
+          if (shaped) {
+          for (j = 1; j <= 4; j++)
+            if (sp_on[j]) { tp[2 * j] = sp[j][0]; tp[2 * j + 1] = sp[j][1]; }
+          if (n_mem >= 0) {
+            for (j = 0; j < n_mem; j++, o++) { tp[2 * o] = mem[j][0]; tp[2 * o + 1] = mem[j][1]; g_ep_fix.cond[o] = 0; }
+          } else {
+            for (j = 5; j < me; j++, o++) { tp[2 * o] = ap[2 * j]; tp[2 * o + 1] = ap[2 * j + 1]; g_ep_fix.cond[o] = a->in.cond[j]; }
           }
-          if (n_tail >= 0 && a->in.bt_start <= a->in.q.n_pred && a->in.bt_start + n_tail <= EP_MAXP) {
-            const int16_t *ap = (const int16_t *)a->in.pred;
-            int same = a->in.q.n_pred == a->in.bt_start + n_tail;
-            for (j = 0; same && j < n_tail; j++)
-              same = ap[2 * (a->in.bt_start + j)] == tail[j][0] && ap[2 * (a->in.bt_start + j) + 1] == tail[j][1] &&
-                     a->in.cond[a->in.bt_start + j] == JMME_EPZS_PRED_ALWAYS;
-            if (!same) {   /* the neighbour's block-type predictors replaced by this macroblock's */
-              int16_t *tp = (int16_t *)g_ep_fix.pred;
-              for (j = 0; j < n_tail; j++) {
-                tp[2 * (a->in.bt_start + j)] = tail[j][0];
-                tp[2 * (a->in.bt_start + j) + 1] = tail[j][1];
-                g_ep_fix.cond[a->in.bt_start + j] = JMME_EPZS_PRED_ALWAYS;
-              }
-              g_ep_fix.q.n_pred = a->in.bt_start + n_tail;
-              fixed = 1;
-              ++g_ep_tail_fixes;
-            }
+          if (o + (bs - me) + (n_tail >= 0 ? n_tail : np - bs) > EP_MAXP) goto no_fix;
+          for (j = me; j < bs; j++, o++) { tp[2 * o] = ap[2 * j]; tp[2 * o + 1] = ap[2 * j + 1]; g_ep_fix.cond[o] = a->in.cond[j]; }
+          if (n_tail >= 0) {
+            for (j = 0; j < n_tail; j++, o++) { tp[2 * o] = tail[j][0]; tp[2 * o + 1] = tail[j][1]; g_ep_fix.cond[o] = 0; }
+          } else {
+            for (j = bs; j < np; j++, o++) { tp[2 * o] = ap[2 * j]; tp[2 * o + 1] = ap[2 * j + 1]; g_ep_fix.cond[o] = a->in.cond[j]; }
           }
-          if (fixed) in = &g_ep_fix;
+          g_ep_fix.q.n_pred = o;
+          fixed = o != np || memcmp(g_ep_fix.pred, a->in.pred, (size_t)np * 4) || memcmp(g_ep_fix.cond, a->in.cond, (size_t)np);
+          if (fixed) {
+            ++g_ep_list_fixes;
+            in = &g_ep_fix;
+          }
+          }
+        no_fix:
           if (in == &a->in && stop >= a->bnd.stop_lo && stop <= a->bnd.stop_hi && prev >= a->bnd.prev_lo &&
               prev <= a->bnd.prev_hi)
             continue;
@@ -2313,11 +2354,9 @@ static void report(void)
       fprintf(stderr, "jm_gpu_me: EPZS speculation: %lld searches answered from %lld batches (%lld guesses), "
                       "%lld searched alone; %lld not speculated; guesses refused: %lld inputs, %lld bounds, "
                       "%lld map cells; %.1f ms building batches; %lld searched again (more stamped cells than kept); "
-                      "%lld second-pass guesses in %lld launches (%lld with this macroblock's block-type predictors, "
-                      "%lld with its inner spatial predictors)\n",
+                      "%lld second-pass guesses in %lld launches (%lld with lists rebuilt from the batch's answers)\n",
               g_ep_hits, g_ep_batches, g_ep_guesses, g_ep_singles, g_ep_direct, g_ep_fail_inputs, g_ep_fail_bounds,
-              g_ep_fail_stale, g_t_ep_build * 1e-3, g_ep_overflow, g_ep_pass2, g_ep_pass2_batches, g_ep_tail_fixes,
-              g_ep_spatial_fixes);
+              g_ep_fail_stale, g_t_ep_build * 1e-3, g_ep_overflow, g_ep_pass2, g_ep_pass2_batches, g_ep_list_fixes);
     if (g_ep_trace) {
       int sl;
       fprintf(stderr, "jm_gpu_me: EPZS misses inside batches by slot (list-only differences):");
