@@ -1856,22 +1856,39 @@ static void ep_pass2(Macroblock *currMB, int mb0, int s0, int nmb, unsigned gen,
         int sp_on[5] = {0, 0, 0, 0, 0};
         {
           static const int kW4[8] = {0, 4, 4, 2, 2, 2, 1, 1}, kH4[8] = {0, 4, 2, 4, 2, 1, 2, 1};
+          static const int16_t kNone[5][2] = {{0, 0}, {12, 0}, {0, 12}, {-12, 0}, {0, -12}};   /* unavailable */
           const int x4 = bx >> 2, y4 = by >> 2, w4 = kW4[bt], h4 = kH4[bt];
-          const int cav = ep_avail_c(bx, by, 4 * w4);
-          const int nx[5] = {0, x4 - 1, x4, cav ? x4 + w4 : x4 - 1, x4 - 1};
-          const int ny[5] = {0, y4, y4 - 1, y4 - 1, y4 - 1};
-          int j;
+          const int mbx4 = (x % g_mbs_x) * 4, mby4 = (x / g_mbs_x) * 4, W4 = p_Vid->width >> 2;
+          PicMotionParams **mvi = p_Vid->enc_picture->mv_info;
+          /* 1: value known, 0: not known here (the guess keeps its own), -1: unavailable */
+          int st[5] = {0, 0, 0, 0, 0}, j;
+          const int nx[5] = {0, x4 - 1, x4, x4 + w4, x4 - 1}, ny[5] = {0, y4, y4 - 1, y4 - 1, y4 - 1};
           for (j = 1; j <= 4; j++) {
-            int pk;
-            const ep_ans *pa;
-            if (nx[j] < 0 || nx[j] > 3 || ny[j] < 0 || ny[j] > 3) continue;
-            pk = g_ep_idx[(((size_t)(x - mb0) * JMME_NSLOT + jmme_slot(bt, nx[j] - nx[j] % w4, ny[j] - ny[j] % h4)) *
-                           EP_REFS + 0) * EP_WAYS];
-            pa = pk >= 0 ? &g_ep_ans[pk] : NULL;
-            if (!pa || !pa->spq.blocktype) continue;
-            sp[j][0] = pa->sp_res.mv_x;
-            sp[j][1] = pa->sp_res.mv_y;
-            sp_on[j] = 1;
+            const int px4 = mbx4 + nx[j], py4 = mby4 + ny[j];
+            if (px4 < 0 || py4 < 0 || px4 >= W4) { st[j] = -1; continue; }
+            if (j == 3 && !ep_avail_c(bx, by, 4 * w4)) { st[j] = -1; continue; }
+            if (nx[j] >= 0 && nx[j] <= 3 && ny[j] >= 0) {   /* inside: the same block type's refined answer */
+              const int pk = g_ep_idx[(((size_t)(x - mb0) * JMME_NSLOT +
+                                        jmme_slot(bt, nx[j] - nx[j] % w4, ny[j] - ny[j] % h4)) * EP_REFS + 0) * EP_WAYS];
+              const ep_ans *pa = pk >= 0 ? &g_ep_ans[pk] : NULL;
+              if (pa && pa->spq.blocktype) { sp[j][0] = pa->sp_res.mv_x; sp[j][1] = pa->sp_res.mv_y; st[j] = 1; }
+            } else if (ny[j] < 0 || x - 1 < mb0) {   /* a macroblock JM has decided: its mv_info */
+              const PicMotionParams *mp = &mvi[py4][px4];
+              if (mp->ref_idx[0] == 0 || (mp->mv[0].mv_x == 0 && mp->mv[0].mv_y == 0)) {
+                sp[j][0] = mp->mv[0].mv_x;
+                sp[j][1] = mp->mv[0].mv_y;
+                st[j] = 1;
+              }
+            }
+          }
+          if (st[3] < 0) {   /* get_neighbors: an unavailable up-right is the up-left (mv_search.c:303-306) */
+            st[3] = st[4];
+            sp[3][0] = sp[4][0];
+            sp[3][1] = sp[4][1];
+          }
+          for (j = 1; j <= 4; j++) {
+            if (st[j] < 0) { sp[j][0] = kNone[j][0]; sp[j][1] = kNone[j][1]; }
+            sp_on[j] = st[j] != 0;
           }
         }
         /* the spatial-memory predictors (EPZS_spatial_memory_predictors, me_epzs_common.c:1675-1718,
