@@ -1767,7 +1767,17 @@ static int ep_avail_c(int bx, int by, int bsx)   /* get_neighbors' upper-right r
   return 1;
 }
 
-static void ep_pass2(Macroblock *currMB, int mb0, int s0, int nmb, unsigned gen, int *n_io)
+/* The answer JM is assumed to get for (macroblock mb0 + xr, slot): its first guess, or, in the third
+ * pass, the second-pass rebuild of that guess (g_ep_alt) when there is one */
+static int *g_ep_alt = NULL;
+static int g_ep_alt_cap = 0, g_ep_alt_on = 0;
+static int ep_assumed(int xr, int slot)
+{
+  if (g_ep_alt_on && g_ep_alt[xr * JMME_NSLOT + slot] >= 0) return g_ep_alt[xr * JMME_NSLOT + slot];
+  return g_ep_idx[(((size_t)xr * JMME_NSLOT + slot) * EP_REFS + 0) * EP_WAYS];
+}
+
+static void ep_pass2(Macroblock *currMB, int mb0, int s0, int nmb, unsigned gen, int *n_io, int third)
 {
   VideoParameters *p_Vid = currMB->p_Vid;
   InputParameters *p_Inp = currMB->p_Inp;
@@ -1837,7 +1847,7 @@ static void ep_pass2(Macroblock *currMB, int mb0, int s0, int nmb, unsigned gen,
           int j;
           n_tail = 0;
           for (j = 0; j < 2 && ps[j] >= 0 && n_tail >= 0; j++) {
-            const int pk = g_ep_idx[(((size_t)(x - mb0) * JMME_NSLOT + ps[j]) * EP_REFS + 0) * EP_WAYS];
+            const int pk = ep_assumed(x - mb0, ps[j]);
             const ep_ans *pa = pk >= 0 ? &g_ep_ans[pk] : NULL;
             if (!pa || !pa->spq.blocktype) { n_tail = -1; break; }   /* (no chained refinement: final vector unknown) */
             if (pa->sp_res.mv_x | pa->sp_res.mv_y) {
@@ -1868,8 +1878,7 @@ static void ep_pass2(Macroblock *currMB, int mb0, int s0, int nmb, unsigned gen,
             if (px4 < 0 || py4 < 0 || px4 >= W4) { st[j] = -1; continue; }
             if (j == 3 && !ep_avail_c(bx, by, 4 * w4)) { st[j] = -1; continue; }
             if (nx[j] >= 0 && nx[j] <= 3 && ny[j] >= 0) {   /* inside: the same block type's refined answer */
-              const int pk = g_ep_idx[(((size_t)(x - mb0) * JMME_NSLOT +
-                                        jmme_slot(bt, nx[j] - nx[j] % w4, ny[j] - ny[j] % h4)) * EP_REFS + 0) * EP_WAYS];
+              const int pk = ep_assumed(x - mb0, jmme_slot(bt, nx[j] - nx[j] % w4, ny[j] - ny[j] % h4));
               const ep_ans *pa = pk >= 0 ? &g_ep_ans[pk] : NULL;
               if (pa && pa->spq.blocktype) { sp[j][0] = pa->sp_res.mv_x; sp[j][1] = pa->sp_res.mv_y; st[j] = 1; }
             } else if (ny[j] < 0 || x - 1 < mb0) {   /* a macroblock JM has decided: its mv_info */
@@ -1917,7 +1926,7 @@ static void ep_pass2(Macroblock *currMB, int mb0, int s0, int nmb, unsigned gen,
             /* searched in this batch before this call, and not yet by JM when the batch was made */
             const int batch = (cm == xc && rk < rk_t) || (cm < xc && xr >= mb0);
             if (batch && !(xr == mb0 && rk < rk_s0)) {
-              const int pk = g_ep_idx[(((size_t)(xr - mb0) * JMME_NSLOT + sl) * EP_REFS + 0) * EP_WAYS];
+              const int pk = ep_assumed(xr - mb0, sl);
               if (pk < 0) { n_mem = -1; break; }
               vx = g_ep_ans[pk].res.motion_x;
               vy = g_ep_ans[pk].res.motion_y;
@@ -1978,10 +1987,11 @@ static void ep_pass2(Macroblock *currMB, int mb0, int s0, int nmb, unsigned gen,
           ep_add(n, in, px, py, p_EPZS);
           g_ep_q[n].stop_crit = stop;
           g_ep_q[n].prev_sad = prev;
+          if (!third && w == 0 && in == &g_ep_fix) g_ep_alt[(x - mb0) * JMME_NSLOT + t] = n;   /* (for the third pass) */
           idx[nw++] = n++;
         }
         {   /* the row after this partition: its first guess's answer (the real call's for the missing one) */
-          const ep_ans *a = &g_ep_ans[idx[0]];
+          const ep_ans *a = &g_ep_ans[ep_assumed(x - mb0, t)];
           if (a->bnd.prev_written) row[c] = a->res.cost;
         }
       }
@@ -2069,7 +2079,20 @@ static const ep_ans *ep_miss(Macroblock *currMB, MEBlock *mv_block, const jmme_e
   }
   g_t_ep_build += now_us() - t0;
   ep_run(n, stale, n_stale, gen);
-  if (g_ep_two_pass) ep_pass2(currMB, mb, ep_slot_of(q), nmb, gen, &n);
+  if (g_ep_two_pass) {
+    if (nmb * JMME_NSLOT > g_ep_alt_cap) {
+      free(g_ep_alt);
+      g_ep_alt_cap = nmb * JMME_NSLOT;
+      g_ep_alt = (int *)malloc((size_t)g_ep_alt_cap * sizeof(int));
+      if (!g_ep_alt) error("jm_gpu_me: out of memory", 500);
+    }
+    memset(g_ep_alt, 0xff, (size_t)nmb * JMME_NSLOT * sizeof(int));
+    g_ep_alt_on = 0;
+    ep_pass2(currMB, mb, ep_slot_of(q), nmb, gen, &n, 0);
+    g_ep_alt_on = 1;   /* third pass: the same replay on the second pass's answers */
+    ep_pass2(currMB, mb, ep_slot_of(q), nmb, gen, &n, 1);
+    g_ep_alt_on = 0;
+  }
   g_ep_n = n;
   g_ep_mb0 = mb;
   g_ep_mb1 = mb + nmb;
