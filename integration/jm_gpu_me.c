@@ -1864,14 +1864,14 @@ static void ep_pass2(Macroblock *currMB, int mb0, int s0, int nmb, unsigned gen,
          * misses dumped (JMME_EPZS_DUMP); ref 0, so scale_mv is the identity */
         int16_t sp[5][2] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}};
         int sp_on[5] = {0, 0, 0, 0, 0};
+        int st[5] = {0, 0, 0, 0, 0}, nref[5] = {0, 0, 0, 0, 0};   /* 1 known, 0 not known, -1 unavailable; refs */
         {
           static const int kW4[8] = {0, 4, 4, 2, 2, 2, 1, 1}, kH4[8] = {0, 4, 2, 4, 2, 1, 2, 1};
           static const int16_t kNone[5][2] = {{0, 0}, {12, 0}, {0, 12}, {-12, 0}, {0, -12}};   /* unavailable */
           const int x4 = bx >> 2, y4 = by >> 2, w4 = kW4[bt], h4 = kH4[bt];
           const int mbx4 = (x % g_mbs_x) * 4, mby4 = (x / g_mbs_x) * 4, W4 = p_Vid->width >> 2;
           PicMotionParams **mvi = p_Vid->enc_picture->mv_info;
-          /* 1: value known, 0: not known here (the guess keeps its own), -1: unavailable */
-          int st[5] = {0, 0, 0, 0, 0}, j;
+          int j;
           const int nx[5] = {0, x4 - 1, x4, x4 + w4, x4 - 1}, ny[5] = {0, y4, y4 - 1, y4 - 1, y4 - 1};
           for (j = 1; j <= 4; j++) {
             const int px4 = mbx4 + nx[j], py4 = mby4 + ny[j];
@@ -1886,12 +1886,14 @@ static void ep_pass2(Macroblock *currMB, int mb0, int s0, int nmb, unsigned gen,
               if (mp->ref_idx[0] == 0 || (mp->mv[0].mv_x == 0 && mp->mv[0].mv_y == 0)) {
                 sp[j][0] = mp->mv[0].mv_x;
                 sp[j][1] = mp->mv[0].mv_y;
+                nref[j] = mp->ref_idx[0];
                 st[j] = 1;
               }
             }
           }
           if (st[3] < 0) {   /* get_neighbors: an unavailable up-right is the up-left (mv_search.c:303-306) */
             st[3] = st[4];
+            nref[3] = nref[4];
             sp[3][0] = sp[4][0];
             sp[3][1] = sp[4][1];
           }
@@ -1899,6 +1901,43 @@ static void ep_pass2(Macroblock *currMB, int mb0, int s0, int nmb, unsigned gen,
             if (st[j] < 0) { sp[j][0] = kNone[j][0]; sp[j][1] = kNone[j][1]; }
             sp_on[j] = st[j] != 0;
           }
+        }
+        /* the block's MV predictor from the same neighbours (GetMotionVectorPredictorNormal,
+         * lcommon/src/mv_prediction.c:192-300: one matching reference, the 8x16 / 16x8 directions, else
+         * the median), ref 0; unknown when a neighbour is */
+        int pv_on = 0;
+        int16_t pv[2] = {0, 0};
+        if (st[1] && st[2] && st[3]) {
+          const int aL = st[1] > 0, aU = st[2] > 0, aR = st[3] > 0;
+          const int rL = aL ? nref[1] : -1, rU = aU ? nref[2] : -1, rR = aR ? nref[3] : -1;
+          const int bsx = (g_slot_bt[t] <= 2) ? 16 : (g_slot_bt[t] <= 5) ? 8 : 4;
+          const int bsy = (bt == 1 || bt == 3) ? 16 : (bt == 2 || bt == 4 || bt == 6) ? 8 : 4;
+          int type = 0;   /* 0 median, 1 left, 2 up, 3 up-right */
+          if (rL == 0 && rU != 0 && rR != 0) type = 1;
+          else if (rL != 0 && rU == 0 && rR != 0) type = 2;
+          else if (rL != 0 && rU != 0 && rR == 0) type = 3;
+          if (bsx == 8 && bsy == 16) {
+            if (bx == 0) { if (rL == 0) type = 1; } else if (rR == 0) type = 3;
+          } else if (bsx == 16 && bsy == 8) {
+            if (by == 0) { if (rU == 0) type = 2; } else if (rL == 0) type = 1;
+          }
+          if (type == 0) {
+            if (!(aU || aR)) {
+              pv[0] = aL ? sp[1][0] : 0;
+              pv[1] = aL ? sp[1][1] : 0;
+            } else {
+              int k2;
+              for (k2 = 0; k2 < 2; k2++) {
+                const int va = aL ? sp[1][k2] : 0, vb = aU ? sp[2][k2] : 0, vc = aR ? sp[3][k2] : 0;
+                pv[k2] = (int16_t)(va + vb + vc - imin(va, imin(vb, vc)) - imax(va, imax(vb, vc)));
+              }
+            }
+          } else {
+            const int jn = type, av = jn == 1 ? aL : jn == 2 ? aU : aR;
+            pv[0] = av ? sp[jn][0] : 0;
+            pv[1] = av ? sp[jn][1] : 0;
+          }
+          pv_on = 1;
         }
         /* the spatial-memory predictors (EPZS_spatial_memory_predictors, me_epzs_common.c:1675-1718,
          * EPZSREF): p_motion[ref][blocktype - 1][block row][picture column] at the left, up and up-right
@@ -1966,7 +2005,16 @@ static void ep_pass2(Macroblock *currMB, int mb0, int s0, int nmb, unsigned gen,
             for (j = bs; j < np; j++, o++) { tp[2 * o] = ap[2 * j]; tp[2 * o + 1] = ap[2 * j + 1]; g_ep_fix.cond[o] = a->in.cond[j]; }
           }
           g_ep_fix.q.n_pred = o;
-          fixed = o != np || memcmp(g_ep_fix.pred, a->in.pred, (size_t)np * 4) || memcmp(g_ep_fix.cond, a->in.cond, (size_t)np);
+          /* the predictor, and the centre when the guess's centre was its predictor and no list part
+           * hangs on the centre (window predictors: the sub-block searches have none) */
+          if (pv_on && (pv[0] != a->in.q.pred_x || pv[1] != a->in.q.pred_y) && a->in.q.center_x == a->in.q.pred_x &&
+              a->in.q.center_y == a->in.q.pred_y && me == bs &&
+              (a->in.q.variant >= 2 || !((pv[0] | pv[1]) & 3))) {   /* (integer grid: the centre is whole-pel) */
+            g_ep_fix.q.pred_x = g_ep_fix.q.center_x = pv[0];
+            g_ep_fix.q.pred_y = g_ep_fix.q.center_y = pv[1];
+          }
+          fixed = o != np || memcmp(g_ep_fix.pred, a->in.pred, (size_t)np * 4) || memcmp(g_ep_fix.cond, a->in.cond, (size_t)np) ||
+                  g_ep_fix.q.pred_x != a->in.q.pred_x || g_ep_fix.q.pred_y != a->in.q.pred_y;
           if (fixed) {
             ++g_ep_list_fixes;
             in = &g_ep_fix;
