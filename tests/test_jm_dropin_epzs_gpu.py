@@ -128,6 +128,13 @@ def test_lencod_epzs_b_pictures_with_cpu_bipred(gpu):
 
 
 def test_lencod_epzs_1080p_frame(gpu):
-    """one 1080p P picture (8160 macroblocks, every partition of the baseline config)"""
+    """one 1080p P picture (8160 macroblocks, every partition of the baseline config); the
+    speculative batches serve the picture: few batches, most searches answered from them, a
+    small share searched alone (round trips), every refinement chained or served on the GPU"""
     st, err = _run(1920, 1080, 2, {"NumberReferenceFrames": 1}, seed=31)
     assert st["gpu"] == 8160 * 41 and st["cpu"] == 0 and st["stale"] > 0, err[-800:]
+    print({k: st[k] for k in ("hits", "batches", "alone", "direct", "sp_gpu", "sp_chained", "sp_cpu")})
+    # (round 4: 128 batches, 324,555 answered, 9,877 alone)
+    assert st["direct"] == 0 and st["batches"] <= 200, err[-800:]
+    assert st["hits"] >= 0.95 * st["gpu"] and st["alone"] <= 0.05 * st["gpu"], err[-800:]
+    assert st["sp_cpu"] == 0 and st["sp_chained"] >= 0.99 * st["sp_gpu"], err[-800:]
