@@ -38,6 +38,10 @@
 #include "jmme_subpel_internal.h"
 #include "jmme_subpel_dev.h"
 
+#ifndef JMME_INTERP_ROWS
+#define JMME_INTERP_ROWS 4   // (2: 13.7-14.2 us, 4: 12.9-13.0 us, 8: 15.2 us per 1080p reference)
+#endif
+
 namespace jmme {
 
 namespace {
@@ -54,10 +58,11 @@ __device__ __forceinline__ uint32_t pack4(int a, int b, int c, int d) {
 }
 
 // ------------------------------------------------------------ sub-images --
-// A workgroup makes a 256 x 8 tile of every sub-image; a thread makes 4 columns
-// of two consecutive rows, sharing the 7 rows of horizontal six-tap sums the two
-// need (a 4-row tile with one row a thread needed 6 per row).
-constexpr int kTileW = 256, kTileH = 8, kSW = kTileW + 16, kSH = kTileH + 6;
+// A workgroup makes a 256 x 16 tile of every sub-image; a thread makes 4 columns
+// of four consecutive rows, sharing the 9 rows of horizontal six-tap sums the four
+// need (2.25 six-tap rows per output row; two rows a thread needed 3.5, one row 6).
+constexpr int kRowsT = JMME_INTERP_ROWS;   // output rows per thread
+constexpr int kTileW = 256, kTileH = 4 * kRowsT, kSW = kTileW + 16, kSH = kTileH + 6;
 
 // four samples of one row as written to a sub-image: one dword (8-bit) or two
 // (16-bit samples, SourceBitDepthLuma 9..14)
@@ -101,24 +106,24 @@ __global__ __launch_bounds__(256) void sub_images_kernel(const T *__restrict__ s
   }
   __syncthreads();
   const int ty = threadIdx.x >> 6, tx = threadIdx.x & 63;   // a wave writes 256 contiguous samples per sub-image
-  const int row0 = Y0 + 2 * ty, col = X0 + 4 * tx;
+  const int row0 = Y0 + kRowsT * ty, col = X0 + 4 * tx;
   if (row0 >= ph || col >= pw) return;
-  int I[7][9];   // I[dr + 2][dc + 2] = sample at (row0 + dr, col + dc)
+  int I[kRowsT + 5][9];   // I[dr + 2][dc + 2] = sample at (row0 + dr, col + dc)
 #pragma unroll
-  for (int r = 0; r < 7; ++r)
+  for (int r = 0; r < kRowsT + 5; ++r)
 #pragma unroll
-    for (int c = 0; c < 9; ++c) I[r][c] = S[2 * ty + r][4 * tx + c + sh];
+    for (int c = 0; c < 9; ++c) I[r][c] = S[kRowsT * ty + r][4 * tx + c + sh];
   // horizontal six-tap (getHorSubImageSixTap) at rows -2..4, columns 0..3: the
   // unrounded sums are p_Vid->imgY_sub_tmp
-  int h[7][4];
+  int h[kRowsT + 5][4];
 #pragma unroll
-  for (int r = 0; r < 7; ++r)
+  for (int r = 0; r < kRowsT + 5; ++r)
 #pragma unroll
     for (int k = 0; k < 4; ++k)
       h[r][k] = six(I[r][k + 2], I[r][k + 3], I[r][k + 1], I[r][k + 4], I[r][k], I[r][k + 5]);
   using PK = Pack4<T>;
 #pragma unroll
-  for (int m = 0; m < 2; ++m) {   // output row row0 + m: input rows m .. m + 5
+  for (int m = 0; m < kRowsT; ++m) {   // output row row0 + m: input rows m .. m + 5
     if (row0 + m >= ph) break;
     int s00[2][5], s02[2][4], s20[5], s22[4];
 #pragma unroll
