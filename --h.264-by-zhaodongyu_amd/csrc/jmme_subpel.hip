@@ -39,7 +39,7 @@
 #include "jmme_subpel_dev.h"
 
 #ifndef JMME_INTERP_ROWS
-#define JMME_INTERP_ROWS 4   // (2: 13.7-14.2 us, 4: 12.9-13.0 us, 8: 15.2 us per 1080p reference)
+#define JMME_INTERP_ROWS 3   // (2: 13.7-14.2 us, 3: 11.6, 4: 12.8-13.0, 5: 12.0, 6: 13.0, 8: 15.2 us per 1080p reference)
 #endif
 
 namespace jmme {
@@ -58,9 +58,10 @@ __device__ __forceinline__ uint32_t pack4(int a, int b, int c, int d) {
 }
 
 // ------------------------------------------------------------ sub-images --
-// A workgroup makes a 256 x 16 tile of every sub-image; a thread makes 4 columns
-// of four consecutive rows, sharing the 9 rows of horizontal six-tap sums the four
-// need (2.25 six-tap rows per output row; two rows a thread needed 3.5, one row 6).
+// A workgroup makes a 256 x 12 tile of every sub-image; a thread makes 4 columns
+// of three consecutive rows, sharing the 8 rows of horizontal six-tap sums the three
+// need (2.67 six-tap rows per output row; two rows needed 3.5, one row 6).  Four rows
+// (2.25) issue fewer six-taps but leave 560 workgroups for 256 CUs against 746.
 constexpr int kRowsT = JMME_INTERP_ROWS;   // output rows per thread
 constexpr int kTileW = 256, kTileH = 4 * kRowsT, kSW = kTileW + 16, kSH = kTileH + 6;
 
