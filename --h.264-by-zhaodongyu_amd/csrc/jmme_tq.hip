@@ -210,7 +210,10 @@ __global__ __launch_bounds__(kTB) void transform_kernel(const int32_t *__restric
 constexpr int kT8 = 9;     // LDS row stride (dwords) of the 8x8 tiles
 constexpr int kWG8 = 256;  // 4 waves per workgroup: one-wave workgroups left too few waves per CU
 constexpr int kU8 = 4;     // 8x8 transforms: block groups per loop iteration (loads in flight)
-constexpr int kUQ = 8;     // quant: blocks per 16-lane group per loop iteration
+#ifndef JMME_QUANT_UQ
+#define JMME_QUANT_UQ 16   // (4: 0.251 ms, 8: 0.244-0.245 ms, 16: 0.240 ms per 4M blocks)
+#endif
+constexpr int kUQ = JMME_QUANT_UQ;   // quant: blocks per 16-lane group per loop iteration
 
 template <int OP>
 __global__ __launch_bounds__(kWG8) void transform8_kernel(const int32_t *__restrict__ in, int32_t *__restrict__ out,
