@@ -209,7 +209,10 @@ __global__ __launch_bounds__(kTB) void transform_kernel(const int32_t *__restric
 // integer operations in the same order as transform.c:365-506.
 constexpr int kT8 = 9;     // LDS row stride (dwords) of the 8x8 tiles
 constexpr int kWG8 = 256;  // 4 waves per workgroup: one-wave workgroups left too few waves per CU
-constexpr int kU8 = 4;     // 8x8 transforms: block groups per loop iteration (loads in flight)
+#ifndef JMME_T8_U
+#define JMME_T8_U 4
+#endif
+constexpr int kU8 = JMME_T8_U;   // 8x8 transforms: block groups per loop iteration (loads in flight)
 #ifndef JMME_QUANT_UQ
 #define JMME_QUANT_UQ 16   // (4: 0.251 ms, 8: 0.244-0.245 ms, 16: 0.240 ms per 4M blocks)
 #endif
