@@ -694,9 +694,9 @@ int search_small(jmme_ctx *ctx, int mode, const jmme_mb_req *req, int n, jmme_bl
   const int tiles = (2 * max_r + 1 + kSmallTile - 1) / kSmallTile;
   const long long wgs = (long long)items.size() * tiles * tiles;
   if (items.empty() || (wgs > ctx->small_max_wg && !force)) return items.empty() ? 1 : 0;
-  // 32-bit costs: (SAD << 5) + lambda * mvbits must not wrap.  An 8-bit batch
-  // with such a lambda goes to the item kernel, whose 64-bit keys serve it
-  // exactly; high bit depth has no other path, so it fails loudly.
+  // 32-bit costs: (SAD << 5) + lambda * mvbits must not wrap.  A batch with
+  // such a lambda (8-bit or 16-bit planes) falls through to the item kernel,
+  // whose 64-bit keys serve it exactly.
   for (const SmallItem &it : items)
     if ((uint64_t)it.lam * 64u + ((uint64_t)256 * ctx->max_pel << 5) >= (1ull << 32)) {
       return 0;

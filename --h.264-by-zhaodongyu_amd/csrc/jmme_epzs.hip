@@ -713,6 +713,17 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(JMME_EPZS_W
       jmme_epzs_res r{};
       r.path = -1;
       p.out[t] = r;
+      // a refused request leaves nothing a caller could take for a search that
+      // ran: empty intervals (stop_lo > stop_hi) and a zeroed integer result
+      if (p.bounds) {
+        jmme_epzs_bounds b{};
+        b.stop_lo = 1;
+        b.stop_hi = 0;
+        b.prev_lo = 1;
+        b.prev_hi = 0;
+        p.bounds[t] = b;
+      }
+      if (p.int_out) p.int_out[t] = jmme_block_res{};
     }
   }
   if constexpr (FUSED) {   // the host polls this word instead of synchronising the stream

@@ -485,15 +485,29 @@ __device__ __forceinline__ void prefetch(const KParams &p, const Item &it, const
     const Win w = win_of<true>(p, it);
     const uint16_t *ref = reinterpret_cast<const uint16_t *>(p.refs[it.ref]);
     const int total = w.wrows * w.nd, w2 = p.width >> 1, xq = w.xa >> 1;
-    const int k = 64 / w.nd;
-    const int dr = lane / w.nd, d = lane - dr * w.nd;
-    const bool act = dr < k;
-    const uint16_t *col = ref + 2 * clampi(xq + d, 0, w2 - 1);
-    for (int r = wave * k; r < w.wrows; r += kWaves * k) {
-      const int rr = r + dr;
-      if (act && rr < w.wrows) {
-        const int gy = clampi(w.y0 + rr, 0, p.height - 1);
-        lds_dma_dword(col + (size_t)gy * p.pitch, (uint32_t)ufl((int)lds_addr(L.raw + r * w.nd)));
+    if (w.nd > 64) {
+      // rows wider than a wave instruction (R >= 55: nd = 2R + 18 rounded):
+      // each row in 64-dword pieces, one wave instruction per piece
+      for (int r = wave; r < w.wrows; r += kWaves) {
+        const int gy = clampi(w.y0 + r, 0, p.height - 1);
+        for (int c0 = 0; c0 < w.nd; c0 += 64) {
+          const int d = c0 + lane;
+          if (d < w.nd)
+            lds_dma_dword(ref + 2 * clampi(xq + d, 0, w2 - 1) + (size_t)gy * p.pitch,
+                          (uint32_t)ufl((int)lds_addr(L.raw + r * w.nd + c0)));
+        }
+      }
+    } else {
+      const int k = 64 / w.nd;   // >= 1 here
+      const int dr = lane / w.nd, d = lane - dr * w.nd;
+      const bool act = dr < k;
+      const uint16_t *col = ref + 2 * clampi(xq + d, 0, w2 - 1);
+      for (int r = wave * k; r < w.wrows; r += kWaves * k) {
+        const int rr = r + dr;
+        if (act && rr < w.wrows) {
+          const int gy = clampi(w.y0 + rr, 0, p.height - 1);
+          lds_dma_dword(col + (size_t)gy * p.pitch, (uint32_t)ufl((int)lds_addr(L.raw + r * w.nd)));
+        }
       }
     }
     if (wave < 2) {   // the current MB: 16 rows x 8 dwords, rows 8 * wave ..
@@ -2340,13 +2354,15 @@ hipError_t launch_search(const KParams &p, hipStream_t s, hipEvent_t ev0, hipEve
   if (ev0) (void)hipEventRecord(ev0, s);
   if (p.hbd) {   // 16-bit planes: 64-bit keys, the generic sweep with v_sad_u16 (the plan routes no 32-bit items)
     auto k16 = ffs ? me_items_kernel<false, true, true> : me_items_kernel<false, false, true>;
-    if (lds > 65536) {   // 16-bit staging above R = 36: raise the kernel's dynamic-LDS limit (once per instance)
-      static thread_local bool raised[2] = {false, false};
-      if (!raised[ffs]) {
+    if (lds > 65536) {   // 16-bit staging above R = 36: raise the kernel's dynamic-LDS limit (once per instance and device)
+      static thread_local bool raised[kMaxDev][2] = {};
+      bool spare_flag = false;
+      bool &done = (dev >= 0 && dev < kMaxDev) ? raised[dev][ffs] : spare_flag;
+      if (!done) {
         if ((e = hipFuncSetAttribute(reinterpret_cast<const void *>(k16), hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)lds)) != hipSuccess)
           return e;
-        raised[ffs] = true;
+        done = true;
       }
     }
     hipLaunchKernelGGL(k16, dim3(resident_grid(occ, dev, 4 + v / 2, k16, p.lds_range, lds)), dim3(kWG), lds, s, p);
@@ -2377,13 +2393,18 @@ hipError_t launch_search_chains(const ChainParams &p, hipStream_t s) {
   const bool ffs = p.mode == JMME_FAST_FULL_SEARCH;
   auto k = p.hbd ? (ffs ? chain_kernel<true, true> : chain_kernel<false, true>)
                  : (ffs ? chain_kernel<true, false> : chain_kernel<false, false>);
-  if (lds > 65536) {   // 16-bit staging at R = 44: 65,728 B of the CU's 160 KiB (once per kernel and thread)
-    static thread_local bool raised[2] = {false, false};
-    if (!raised[ffs]) {
+  if (lds > 65536) {   // 16-bit staging at R = 44: 65,728 B of the CU's 160 KiB (once per kernel, device and thread)
+    constexpr int kMaxDev = 64;
+    static thread_local bool raised[kMaxDev][2] = {};
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    bool spare_flag = false;
+    bool &done = (dev >= 0 && dev < kMaxDev) ? raised[dev][ffs] : spare_flag;
+    if (!done) {
       const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       if (e != hipSuccess) return e;
-      raised[ffs] = true;
+      done = true;
     }
   }
   hipLaunchKernelGGL(k, dim3(p.n), dim3(kChainWG), lds, s, p);

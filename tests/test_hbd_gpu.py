@@ -41,8 +41,10 @@ def _path(me, path):
 
 @pytest.mark.parametrize("path", ["small", "items"])
 @pytest.mark.parametrize("bits,size,R", [(10, (352, 288), 16), (10, (176, 144), 32), (12, (128, 96), 7),
-                                         (14, (96, 64), 3)])
+                                         (14, (96, 64), 3), (10, (176, 144), 55), (10, (176, 144), 64)])
 def test_hbd_full_search_vs_oracle(bits, size, R, path, gpu):
+    """R 55 / 64: staged rows of more than 64 dwords (the item kernel's prefetch
+    splits each row over several wave instructions)"""
     from jmme import FULL_SEARCH, MotionEstimator
     w, h = size
     cur, ref = _planes(w, h, bits, seed=bits + R)[::-1]
