@@ -68,8 +68,20 @@ constexpr int kChunk = 16;                 // item kernel: consecutive items dea
 constexpr int kRed1 = (kNS + 3) / 4 * 2;      // reduce: registers after the permlane32 level (22)
 constexpr int kRed2 = kRed1 / 2;              //         ... after the permlane16 level (11)
 
+// v6 sweep (default): a fold reduce-scatters its keys across the wave at once
+// into 11 registers (kRed2), so no wave keeps 41 per-lane minima through the
+// sweep; the freed registers pay for 5 positions per task (13 task rows at
+// R = 32, no redundant rows).  v5 (JMME_SWEEP_V6=0): 41 per-lane minima, 3
+// positions per task.
+#ifndef JMME_SWEEP_V6
+#define JMME_SWEEP_V6 1
+#endif
 #ifndef JMME_SWEEP_P
-#define JMME_SWEEP_P 3   // positions per sweep task (vertical run)
+#if JMME_SWEEP_V6
+#define JMME_SWEEP_P 5   // positions per sweep task (vertical run)
+#else
+#define JMME_SWEEP_P 3
+#endif
 #endif
 #ifndef JMME_WAVES_PER_EU
 #define JMME_WAVES_PER_EU 4
@@ -684,7 +696,8 @@ __device__ __forceinline__ void expand(const KParams &p, const Item &it, const L
 // the window's farthest vector from the predictor passes, so all do.
 template <bool KEY32, bool FFS>
 __device__ __forceinline__ bool item_fast(const KParams &p, const Item &it) {
-  if (!KEY32 || it.rs < 1) return false;
+  // the sweep's tasks are runs of JMME_SWEEP_P positions: at least that many rows
+  if (!KEY32 || 2 * it.rs + 1 < JMME_SWEEP_P || it.rs < 1) return false;
   if (!FFS) return true;
   const int ex = max(abs(it.cqx - 4 * it.rs - it.px), abs(it.cqx + 4 * it.rs - it.px));
   const int ey = max(abs(it.cqy - 4 * it.rs - it.py), abs(it.cqy + 4 * it.rs - it.py));
@@ -812,13 +825,107 @@ __device__ __forceinline__ void centre_bounds(const GroupCtx &g, const Lds &L, i
   }
 }
 
+// ---- v6 fold: keys reduce-scattered across the wave per fold --------------
+// Four partitions m0..m3 (slots base .. base+3) per register: permlane32_swap
+// pairs (m0, m1) and (m2, m3) (lanes 0-31 keep the first, 32-63 the second),
+// permlane16_swap pairs again; row r of the result then holds the row-partial
+// minimum of slot base + perm(r), perm = (0, 2, 1, 3).  The four DPP steps that
+// finish a row run once per item (v6_write), not per fold.
+__device__ __forceinline__ uint32_t v6_sr(uint32_t m0, uint32_t m1, uint32_t m2, uint32_t m3) {
+  const auto s1 = __builtin_amdgcn_permlane32_swap(m0, m1, false, false);
+  const auto s2 = __builtin_amdgcn_permlane32_swap(m2, m3, false, false);
+  const uint32_t x = min((uint32_t)s1[0], (uint32_t)s1[1]), y = min((uint32_t)s2[0], (uint32_t)s2[1]);
+  const auto s3 = __builtin_amdgcn_permlane16_swap(x, y, false, false);
+  return min((uint32_t)s3[0], (uint32_t)s3[1]);
+}
+// slot of register q's first partition: 4x4 (25-40), 4x8 (17-24), 8x4 (9-16),
+// 8x8 (5-8), 16x8 / 8x16 (1-4), 16x16 (0, rows 1-3 padding)
+__host__ __device__ constexpr int v6_base(int q) {
+  return q < 4 ? 25 + 4 * q : q < 6 ? 17 + 4 * (q - 4) : q < 8 ? 9 + 4 * (q - 6) : q == 8 ? 5 : q == 9 ? 1 : 0;
+}
+
+// The fold of one task's P positions (their 16 4x4 keys each) into the 11
+// reduce-scattered registers.  Phase A: the 4x4 slots straight from the keys.
+// Phase B, position by position (a position's keys die with it): 8x4, 4x8,
+// then 8x8 from the 8x4s, 16x8 / 8x16 from the 8x8s and the 16x16 -- the sums
+// of partition_keys (update_full_search_large_blocks, me_fullfast.c:196-260).
+template <int P>
+__device__ __forceinline__ void fold_v6(const uint32_t (&a)[P][16], const uint32_t (&K)[P], uint32_t (&b)[kRed2]) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    uint32_t m[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      m[i] = a[0][4 * q + i];
+#pragma unroll
+      for (int j = 1; j < P; ++j) m[i] = min(m[i], a[j][4 * q + i]);
+    }
+    b[q] = min(b[q], v6_sr(m[0], m[1], m[2], m[3]));
+  }
+  // 4x8: two registers of four partitions, straight from the 4x4 keys
+#pragma unroll
+  for (int v = 0; v < 2; ++v) {
+    uint32_t m[4];
+#pragma unroll
+    for (int bx = 0; bx < 4; ++bx) {
+      m[bx] = add3(a[0][(2 * v) * 4 + bx], a[0][(2 * v + 1) * 4 + bx], 0u - K[0]);
+#pragma unroll
+      for (int j = 1; j < P; ++j) m[bx] = min(m[bx], add3(a[j][(2 * v) * 4 + bx], a[j][(2 * v + 1) * 4 + bx], 0u - K[j]));
+    }
+    b[4 + v] = min(b[4 + v], v6_sr(m[0], m[1], m[2], m[3]));
+  }
+  // 8x4 -> 8x8 -> 16x8 / 8x16 -> 16x16, position by position (its keys die with it)
+  uint32_t e8[8], g4[4], t4[4], z;   // running minima over the positions
+#pragma unroll
+  for (int j = 0; j < P; ++j) {
+    __builtin_amdgcn_sched_barrier(0);
+    const uint32_t nk = 0u - K[j];
+    uint32_t e[8], g[4], t[4];
+#pragma unroll
+    for (int by = 0; by < 4; ++by)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) e[by * 2 + h] = add3(a[j][by * 4 + 2 * h], a[j][by * 4 + 2 * h + 1], nk);   // 8x4
+#pragma unroll
+    for (int v = 0; v < 2; ++v)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) g[v * 2 + h] = add3(e[(2 * v) * 2 + h], e[(2 * v + 1) * 2 + h], nk);   // 8x8
+    t[0] = add3(g[0], g[1], nk);   // 16x8 top
+    t[1] = add3(g[2], g[3], nk);   // 16x8 bottom
+    t[2] = add3(g[0], g[2], nk);   // 8x16 left
+    t[3] = add3(g[1], g[3], nk);   // 8x16 right
+    const uint32_t zz = __builtin_elementwise_add_sat(t[0] + nk, t[1]);   // 16x16 (saturating)
+    if (j == 0) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) e8[k] = e[k];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { g4[k] = g[k]; t4[k] = t[k]; }
+      z = zz;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) e8[k] = min(e8[k], e[k]);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { g4[k] = min(g4[k], g[k]); t4[k] = min(t4[k], t[k]); }
+      z = min(z, zz);
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  b[6] = min(b[6], v6_sr(e8[0], e8[1], e8[2], e8[3]));
+  b[7] = min(b[7], v6_sr(e8[4], e8[5], e8[6], e8[7]));
+  b[8] = min(b[8], v6_sr(g4[0], g4[1], g4[2], g4[3]));
+  b[9] = min(b[9], v6_sr(t4[0], t4[1], t4[2], t4[3]));
+  b[10] = min(b[10], v6_sr(z, ~0u, ~0u, ~0u));
+}
+
 // The v5 sweep of the sub-window [-rs, rs]^2 (rs >= 1) of the staged window.
 // A task is a vertical run of P positions (x, y..y+P-1); the 15+P window rows
 // they need are read once; row r meets MB row r - j of position j.  The
 // current MB comes from SGPRs (cs), so the only LDS traffic is the window.
-template <int WP, int P>   // WP: words pitch when known at compile time (kWP32), else 0 (L.wp)
-__device__ __forceinline__ void sweep_v5(const Lds &L, const uint32_t (&cs)[64], int R, int rs,
-                                         uint32_t (&best)[kNS]) {
+// NB = kNS: per-lane minima of the 41 partition keys (v5); NB = kRed2: the
+// v6 fold's reduce-scattered registers.  Returns whether any task folded.
+template <int WP, int P, int NB>   // WP: words pitch when known at compile time (kWP32), else 0 (L.wp)
+__device__ __forceinline__ bool sweep_v5(const Lds &L, const uint32_t (&cs)[64], int R, int rs,
+                                         uint32_t (&best)[NB]) {
+  bool folded = false;
   const int tid = opaque_tid(L);
   const int D = 2 * rs + 1;
   const int DT = (D + P - 1) / P;        // tasks per column (the last one shifted up)
@@ -839,7 +946,12 @@ __device__ __forceinline__ void sweep_v5(const Lds &L, const uint32_t (&cs)[64],
   if (rows64) { tq = tid >> 6; tx = tid & 63; }
   const int wp = WP ? WP : L.wp;
   const uint32_t tb = lds_addr(L.tmax) + 32u * (uint32_t)ufl(tid >> 6);   // this wave's elimination bounds
-  for (int t = tid; t < ntask; t += kWG) {
+  // The loop runs while the wave's first lane has a task (lane 0 holds the
+  // wave's smallest t), so every lane stays active: the v6 fold's permlane swaps
+  // read every lane.  A lane past the last task recomputes a valid position --
+  // its row clamps to D - P below, its column stays inside the window -- which
+  // cannot change a minimum.
+  for (int t = tid; ufl(t) < ntask; t += kWG) {
     // a column past 63.  nrow64 is a multiple of 64, so the test is the same for
     // every lane of the wave: tested on the first lane it is a scalar branch, and
     // the division stays out of the row tasks (as a per-lane test the compiler
@@ -926,6 +1038,10 @@ __device__ __forceinline__ void sweep_v5(const Lds &L, const uint32_t (&cs)[64],
       for (int k = 0; k < 16; ++k) asm volatile("" :: "v"(a[j][k]));
 #else
     if (fold) {
+    folded = true;
+    if constexpr (NB == kRed2) {
+      fold_v6<P>(a, K, best);
+    } else {
     // positions in pairs: both keys of a partition fold with one v_min3_u32
 #pragma unroll
     for (int j = 0; j + 1 < P; j += 2) {
@@ -942,6 +1058,7 @@ __device__ __forceinline__ void sweep_v5(const Lds &L, const uint32_t (&cs)[64],
       for (int s = 0; s < kNS; ++s) best[s] = min(best[s], p0[s]);
     }
     }
+    }
 #endif
     if (rows64) {
       tq += kWaves;
@@ -950,6 +1067,26 @@ __device__ __forceinline__ void sweep_v5(const Lds &L, const uint32_t (&cs)[64],
       tq += qstep;
       if (tx >= D) { tx -= D; ++tq; }
     }
+  }
+  return folded;
+}
+
+// v6: finish the 11 reduce-scattered registers (4 DPP steps per row) and store
+// each row's slot to this wave's L.red row; a wave that never folded stores ~0
+template <bool FOLDED>
+__device__ __forceinline__ void v6_write(const Lds &L, const uint32_t (&b)[kRed2], int lane, int wave) {
+  const int row = lane >> 4;
+  const int pr = ((row & 1) << 1) | (row >> 1);
+#pragma unroll
+  for (int q = 0; q < kRed2; ++q) {
+    uint32_t v = ~0u;
+    if (FOLDED) {
+      v = dpp_min<0xB1>(b[q]);   // quad_perm [1,0,3,2]
+      v = dpp_min<0x4E>(v);      // quad_perm [2,3,0,1]
+      v = dpp_min<0x141>(v);     // row_half_mirror
+      v = dpp_min<0x140>(v);     // row_mirror
+    }
+    if ((lane & 15) == 0 && (q < kRed2 - 1 || row == 0)) L.red[wave * kNS + v6_base(q) + pr] = v;
   }
 }
 
@@ -1217,10 +1354,15 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
   const unsigned long long gmask = g.gmask;
   const int u = it.u;
 
-  // per-thread running minima of the keys
+  // per-thread running minima of the keys (v5 / generic sweep)
   Best best[kNS];
+  auto init_best = [&]() {
 #pragma unroll
-  for (int s = 0; s < kNS; ++s) best[s] = (Best)~0ull;
+    for (int s = 0; s < kNS; ++s) best[s] = (Best)~0ull;
+  };
+  // v6 fast sweep: the reduce-scattered minima
+  uint32_t b11[kRed2];
+  bool v6 = false, v6_folded = false;
 
   // ---- sweep all (2R+1)^2 positions of the window.  A task is a vertical
   // pair of positions (x, y), (x, y+1): the 17 reference rows they need are
@@ -1397,10 +1539,20 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
     if (spec && wave == kWaves - 1) special_keys<FFS>(g, L, lane);   // the wave with the fewest sweep tasks; read back after the reduce's barrier
     if constexpr (KEY32) centre_bounds<FFS>(g, L, lane, ufl(wave));
     if constexpr (KEY32) {
-      if (L.wp == kWP32) sweep_v5<kWP32, JMME_SWEEP_P>(L, cs, R, g.rs, best);
-      else sweep_v5<0, JMME_SWEEP_P>(L, cs, R, g.rs, best);
+#if JMME_SWEEP_V6
+#pragma unroll
+      for (int q = 0; q < kRed2; ++q) b11[q] = ~0u;
+      v6 = true;
+      v6_folded = L.wp == kWP32 ? sweep_v5<kWP32, JMME_SWEEP_P, kRed2>(L, cs, R, g.rs, b11)
+                                : sweep_v5<0, JMME_SWEEP_P, kRed2>(L, cs, R, g.rs, b11);
+#else
+      init_best();
+      if (L.wp == kWP32) sweep_v5<kWP32, JMME_SWEEP_P, kNS>(L, cs, R, g.rs, best);
+      else sweep_v5<0, JMME_SWEEP_P, kNS>(L, cs, R, g.rs, best);
+#endif
     }
   } else {
+    init_best();
     sweep(std::integral_constant<bool, true>{});
   }
   STAMP(st.sweep);
@@ -1416,7 +1568,11 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
 #ifdef JMME_ABL_NOREDUCE   // timing ablation only: no cross-lane reduction
   if (KEY32 && false) {
 #else
-  if (KEY32) {
+  if (KEY32 && v6) {
+    // (the fold's ballot makes v6_folded wave-uniform)
+    if (__builtin_amdgcn_ballot_w64(v6_folded)) v6_write<true>(L, b11, lane, wave);
+    else v6_write<false>(L, b11, lane, wave);
+  } else if (KEY32) {
 #endif
     // reduce-scatter through the wave: permlane32_swap pairs slots (lanes
     // 0-31 keep one, 32-63 the other), permlane16_swap pairs again (one slot

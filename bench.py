@@ -550,6 +550,68 @@ def run_fractal(args, ws: int, rank: int, local: int, dev) -> None:
                        "bit_exact": exact}}))
 
 
+def run_encoder(args, ws: int, rank: int, local: int) -> None:
+    """The product's own multi-GPU form (`--shard encoder`):
+    each rank runs JM 18.5 lencod_jmme over its own closed GOPs on its GPU
+    (integration/jmme_gop.c: one encoder process per GOP, StartFrame /
+    FramesToBeEncoded, the device fixed in the child's environment before the
+    encoder starts) -- weak scaling, no data-path collective; this process never
+    touches the GPU, so the ranks meet over gloo for the barrier and the
+    max-over-ranks time.  value = every rank's encoded macroblocks / the slowest
+    rank's wall time.  After timing, each rank's GOPs go through the stock
+    lencod with the same arguments (its host share, concurrent processes) and
+    every GOP's bitstream and reconstruction are compared byte for byte."""
+    import bench_blocks
+    if ws > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+        dist.barrier()
+    w, h = (int(x) for x in args.enc_size.split("x"))
+    t0 = time.perf_counter()
+    blk = bench_blocks.encoder_gop_block(device=local, rank=rank, gops=args.enc_gops, gop=args.enc_gop, size=(w, h),
+                                         per_gpu=args.enc_per_gpu, check_stock=False, encoder=args.enc_encoder)
+    wall = time.perf_counter() - t0
+    if blk is None:
+        raise SystemExit("--shard encoder needs integration/_build/{lencod_jmme,jmme_gop} and oracle/_ref/lencod")
+    wall = blk["wall_s"]           # the launcher's own run (clip generation excluded)
+    if ws > 1:
+        dist.barrier()
+    # parity and the host baseline, outside the timed region
+    par = bench_blocks.encoder_gop_block(device=local, rank=rank, gops=args.enc_gops, gop=args.enc_gop, size=(w, h),
+                                         per_gpu=args.enc_per_gpu, check_stock=True, encoder=args.enc_encoder)
+    ok = par["parity"]["byte_identical_gops"]
+    rec = [wall, float(ok), float(par["host_baseline"]["encoder_mb_per_s"]), float(blk["macroblocks"])]
+    if ws > 1:
+        t = torch.tensor(rec, dtype=torch.float64)
+        allr = [torch.zeros_like(t) for _ in range(ws)]
+        dist.all_gather(allr, t)
+        recs = [x.tolist() for x in allr]
+    else:
+        recs = [rec]
+    if rank == 0:
+        job_wall = max(r[0] for r in recs)
+        mbs = sum(r[3] for r in recs)
+        print(json.dumps({
+            "metric": "encoder macroblocks/sec (JM 18.5 lencod_jmme, closed GOPs, FS +-32 ME on the GPU)",
+            "value": round(mbs / job_wall, 1), "unit": "macroblocks/sec", "n_gpus": ws, "steps": 1, "warmup": 0,
+            "ms_per_step": round(job_wall * 1e3, 1), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u8",
+            "data": f"synthetic (a seeded {w}x{h} clip per rank)",
+            "config": {"workload": f"{args.enc_gops} closed GOPs x {args.enc_gop} frames per GPU through lencod_jmme, "
+                                   f"FS +-32, 1 ref, RDO off, sub-pel off", "per_gpu_encoders": args.enc_per_gpu,
+                       "parallelism": f"closed-GOP shard x{ws} (integration/jmme_gop.c per rank, no collective)"},
+            "per_rank": [{"rank": r, "wall_s": round(x[0], 3), "byte_identical_gops": int(x[1]),
+                          "macroblocks": int(x[3]), "host_encoder_mb_per_s": x[2]} for r, x in enumerate(recs)],
+            "parity": {"reference": "JM 18.5 lencod (stock, same GOP arguments)", "gops": args.enc_gops * ws,
+                       "byte_identical_gops": int(sum(x[1] for x in recs))},
+            "cpu_baseline": {"value": round(sum(x[2] for x in recs), 1), "unit": "macroblocks/sec",
+                             "cores": par["host_baseline"]["procs"] * ws, "kind": "reference",
+                             "sample": "the same GOPs through the stock lencod, concurrent processes per rank"},
+            "rank0": blk}))
+    if ws > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -567,16 +629,28 @@ def main():
                                                                   "side blocks): profiling runs")
     ap.add_argument("--workload", choices=["me", "fractal"], default="me",
                     help="me: the headline (configs[1]); fractal: configs[2] range-block bands over the ranks")
-    ap.add_argument("--shard", choices=["gop", "band"], default="gop",
+    ap.add_argument("--shard", choices=["gop", "band", "encoder"], default="gop",
                     help="gop: each rank searches its own frames (weak, default); band: rank 0 broadcasts "
-                         "each frame's planes over RCCL and every rank searches an MB-row band (strong)")
+                         "each frame's planes over RCCL and every rank searches an MB-row band (strong); encoder: "
+                         "each rank runs the drop-in encoder (lencod_jmme) over its own closed GOPs on its GPU "
+                         "(integration/jmme_gop.c, weak)")
+    ap.add_argument("--no-encoder", action="store_true", help="skip the GOP-sharded encoder block of the N=1 line")
+    ap.add_argument("--enc-gops", type=int, default=16, help="--shard encoder / encoder block: GOPs per GPU")
+    ap.add_argument("--enc-gop", type=int, default=4, help="frames per GOP (1 I + P)")
+    ap.add_argument("--enc-per-gpu", type=int, default=8, help="encoder processes at once per GPU")
+    ap.add_argument("--enc-size", default="1920x1080", help="clip size WxH")
+    ap.add_argument("--enc-encoder", default=None, help="encoder binary (default integration/_build/lencod_jmme; "
+                                                         "a CPU rehearsal passes the stock oracle/_ref/lencod)")
     args = ap.parse_args()
     if args.headline_only:
         for k in ("no_cpu_baseline", "no_subpel", "no_uhd", "no_adversarial", "no_hbd", "no_fractal", "no_hybrid",
-                  "no_dropin"):
+                  "no_dropin", "no_encoder"):
             setattr(args, k, True)
 
     ws, rank, local = dist_env()
+    if args.shard == "encoder":   # before anything touches the GPU: this process only launches encoders
+        run_encoder(args, ws, rank, local)
+        return
     if ws > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
@@ -716,6 +790,14 @@ def main():
         if not args.no_hybrid and ws == 1:
             import bench_blocks
             line["hybrid"] = bench_blocks.hybrid_block(dev, local, load_workload)
+        if not args.no_encoder and ws == 1:
+            import bench_blocks
+            # the product's multi-GPU form at N = 1: closed GOPs through lencod_jmme
+            # (the same as --shard encoder on one GPU), with the host baseline
+            w, h = (int(x) for x in args.enc_size.split("x"))
+            line["encoder_gop"] = bench_blocks.encoder_gop_block(device=local, rank=0, gops=args.enc_gops,
+                                                                 gop=args.enc_gop, size=(w, h),
+                                                                 per_gpu=args.enc_per_gpu, encoder=args.enc_encoder)
         if not args.no_dropin and ws == 1:
             import bench_blocks
             # FS / FFS (configs[1] settings), FS / FFS with encoder_baseline.cfg's

@@ -22,8 +22,10 @@
  * (each GOP carries its own parameter sets and idr_pic_id).
  *
  * Usage:
- *   jmme_gop --encoder PATH --gpus N [--per-gpu K] --gop G --frames F
+ *   jmme_gop --encoder PATH --gpus N [--per-gpu K] [--devices D0,D1,..] --gop G --frames F
  *            --prefix OUTPREFIX [--concat] -- <encoder arguments>
+ * (--devices: the HIP device index each of the N GPU slots stands for; default
+ * 0 .. N-1.  A rank-per-GPU caller passes its own device alone.)
  * Prints one JSON line: GOPs, their GPU, wall time and JM's "Total ME time".
  */
 #define _GNU_SOURCE
@@ -57,6 +59,7 @@ static void die(const char *msg)
 }
 
 static const char *g_encoder, *g_prefix;
+static int g_dev_map[64];
 static char **g_enc_args;
 static int g_n_enc_args;
 
@@ -81,7 +84,7 @@ static pid_t start_gop(gop_run *r)
   gop_path(log, sizeof log, r->gop, ".log");
   snprintf(outp, sizeof outp, "OutputFile=%s", out);
   snprintf(recp, sizeof recp, "ReconFile=%s", rec);
-  snprintf(dev, sizeof dev, "%d", r->gpu);
+  snprintf(dev, sizeof dev, "%d", r->gpu < 64 ? g_dev_map[r->gpu] : r->gpu);
   argv[k++] = (char *)g_encoder;
   for (i = 0; i < g_n_enc_args; i++) argv[k++] = g_enc_args[i];
   argv[k++] = "-p"; argv[k++] = start;
@@ -141,6 +144,8 @@ int main(int argc, char **argv)
   int *busy;
   gop_run *runs;
   double t_start;
+  const char *devices = NULL;
+  for (i = 0; i < 64; i++) g_dev_map[i] = i;
   for (i = 1; i < argc; i++) {
     if (!strcmp(argv[i], "--")) { i++; break; }
     if (!strcmp(argv[i], "--concat")) { concat = 1; continue; }
@@ -151,10 +156,23 @@ int main(int argc, char **argv)
     else if (!strcmp(argv[i], "--gop")) gop = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--frames")) frames = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--prefix")) g_prefix = argv[++i];
+    else if (!strcmp(argv[i], "--devices")) devices = argv[++i];
     else die("unknown option (see the usage in jmme_gop.c)");
   }
   if (!g_encoder || !g_prefix || gpus < 1 || per_gpu < 1 || gop < 1 || frames < 1)
     die("need --encoder, --prefix, --gpus >= 1, --gop >= 1, --frames >= 1");
+  if (devices) {   /* "3" or "0,2,5": slot g runs on device devices[g] */
+    const char *q = devices;
+    int g = 0;
+    while (*q && g < 64) {
+      char *end;
+      long v = strtol(q, &end, 10);
+      if (end == q || v < 0 || (*end && *end != ',')) die("bad --devices list");
+      g_dev_map[g++] = (int)v;
+      q = *end == ',' ? end + 1 : end;
+    }
+    if (g < gpus) die("--devices names fewer devices than --gpus");
+  }
   g_enc_args = argv + i;
   g_n_enc_args = argc - i;
   n_gops = (frames + gop - 1) / gop;
@@ -214,9 +232,10 @@ int main(int argc, char **argv)
   printf("{\"gops\": %d, \"gop\": %d, \"frames\": %d, \"gpus\": %d, \"per_gpu\": %d, \"wall_s\": %.3f, \"failed\": %d, "
          "\"runs\": [", n_gops, gop, frames, gpus, per_gpu, now_s() - t_start, failed);
   for (i = 0; i < n_gops; i++)
-    printf("%s{\"gop\": %d, \"gpu\": %d, \"first\": %d, \"frames\": %d, \"wall_s\": %.3f, \"me_s\": %.3f, "
-           "\"status\": %d}", i ? ", " : "", i, runs[i].gpu, runs[i].first, runs[i].count, runs[i].t1 - runs[i].t0,
-           runs[i].me_s, runs[i].status);
+    printf("%s{\"gop\": %d, \"gpu\": %d, \"device\": %d, \"first\": %d, \"frames\": %d, \"wall_s\": %.3f, "
+           "\"me_s\": %.3f, \"status\": %d}", i ? ", " : "", i, runs[i].gpu,
+           runs[i].gpu < 64 ? g_dev_map[runs[i].gpu] : runs[i].gpu, runs[i].first, runs[i].count,
+           runs[i].t1 - runs[i].t0, runs[i].me_s, runs[i].status);
   printf("]}\n");
   free(runs);
   free(busy);

@@ -346,3 +346,104 @@ def dropin_block(modes=None, size=(1920, 1080), search_range=32, reps=2, host_pr
                            me_speedup_vs_host=round(row["dropin_mb_per_s"] / host_rate, 3) if g["me_s"] else None)
             out[tag] = row
     return out
+
+
+# ---- the encoder itself sharded by closed GOPs ----------
+# JM's ME is sequential inside a GOP (frame t searches the reconstruction of t-1,
+# store_picture_in_dpb, JM/lencod/src/mbuffer.c:1905), so the product scales by
+# closed GOPs: integration/jmme_gop.c starts one encoder per GOP (StartFrame /
+# FramesToBeEncoded, JM/lencod/inc/configfile.h:39,47), its GPU fixed in the
+# child's environment before the encoder starts.  These settings are configs[1]'s
+# (FS +-32, 1 ref, RDO off, sub-pel off).
+ENCODER_PARAMS = {"SearchMode": -1, "SearchRange": 32, "NumberReferenceFrames": 1, "RDOptimization": 0}
+
+
+def _gop_launch(launcher, encoder, d, tag, yuv, w, h, frames, gop, slots, per_slot, devices, cfg_text, params,
+                timeout=1200):
+    """One jmme_gop run over the clip: returns (report, per-GOP md5 pairs)."""
+    import hashlib
+    import json
+    import os
+    import subprocess
+    wd = os.path.join(d, tag)
+    os.makedirs(wd, exist_ok=True)
+    cfg = os.path.join(wd, "enc.cfg")
+    open(cfg, "w").write(cfg_text)
+    enc_args = ["-d", cfg, "-p", f"InputFile={yuv}", "-p", f"SourceWidth={w}", "-p", f"SourceHeight={h}",
+                "-p", f"OutputWidth={w}", "-p", f"OutputHeight={h}"]
+    for k, v in params.items():
+        enc_args += ["-p", f"{k}={v}"]
+    prefix = os.path.join(wd, "g")
+    cmd = [launcher, "--encoder", encoder, "--gpus", str(slots), "--per-gpu", str(per_slot), "--gop", str(gop),
+           "--frames", str(frames), "--prefix", prefix]
+    if devices is not None:
+        cmd += ["--devices", ",".join(str(x) for x in devices)]
+    t0 = time.time()
+    r = subprocess.run(cmd + ["--"] + enc_args, cwd=wd, capture_output=True, text=True, timeout=timeout)
+    wall = time.time() - t0
+    if r.returncode != 0:
+        raise RuntimeError(f"jmme_gop ({tag}) failed: " + r.stdout[-800:] + r.stderr[-800:])
+    rep = json.loads(r.stdout.strip().splitlines()[-1])
+    rep["python_wall_s"] = round(wall, 3)
+    md5 = []
+    for g in range(rep["gops"]):
+        md5.append(tuple(hashlib.md5(open(f"{prefix}_gop{g:03d}{sfx}", "rb").read()).hexdigest()
+                         for sfx in (".264", "_rec.yuv")))
+    return rep, md5
+
+
+def encoder_gop_block(device: int = 0, rank: int = 0, gops: int = 16, gop: int = 4, size=(1920, 1080),
+                      per_gpu: int = 8, host_procs=None, check_stock: bool = True, encoder=None) -> dict | None:
+    """One rank's share of the GOP-sharded encoder: `gops` closed GOPs of `gop`
+    frames of a seeded 1080p clip (its own seed per rank) through lencod_jmme on
+    HIP device `device` (`per_gpu` encoders at once), timed wall to wall, then --
+    outside the timed region -- the same GOPs through the stock lencod as
+    concurrent CPU processes (the host baseline: `host_procs` at once), and every
+    GOP's bitstream and reconstruction compared byte for byte.  The caller
+    (this process) never touches the GPU."""
+    import os
+    import tempfile
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    stock = os.path.join(repo, "oracle", "_ref", "lencod")
+    gpu = encoder or os.path.join(repo, "integration", "_build", "lencod_jmme")   # (a CPU rehearsal passes the stock one)
+    launcher = os.path.join(repo, "integration", "_build", "jmme_gop")
+    if not all(os.path.exists(p) for p in (stock, gpu, launcher)):
+        return None
+    if host_procs is None:
+        from bench import host_cores
+        host_procs = host_cores()
+    from jmme import synth
+    from test_jm_dropin_gpu import CFG
+    w, h = size
+    frames = gops * gop
+    mbs = (w // 16) * ((h + 15) // 16)
+    seed = 3000 + rank
+    with tempfile.TemporaryDirectory() as d:
+        yuv = os.path.join(d, "in.yuv")
+        synth.write_yuv420(yuv, synth.luma_sequence(w, h, frames, seed=seed, gmv=(5, 3)))
+        _progress(f"encoder gop block rank {rank}: {gops} GOPs x {gop} frames on device {device}")
+        g_rep, g_md5 = _gop_launch(launcher, gpu, d, "gpu", yuv, w, h, frames, gop, 1, per_gpu, [device], CFG,
+                                   ENCODER_PARAMS)
+        out = {"encoder": os.path.basename(gpu),
+               "workload": f"JM 18.5 lencod_jmme (ME on the GPU) encoding {gops} closed GOPs of {gop} frames "
+                           f"(1 I + {gop - 1} P) of a seeded {w}x{h} clip, FS +-32, 1 ref, RDO off, sub-pel off; "
+                           f"one encoder process per GOP (integration/jmme_gop.c), {per_gpu} at once on the GPU",
+               "device": device, "clip_seed": seed, "gops": gops, "gop": gop, "frames": frames,
+               "macroblocks": frames * mbs, "wall_s": g_rep["python_wall_s"],
+               "encoder_mb_per_s": round(frames * mbs / g_rep["python_wall_s"], 1),
+               "me_s_per_gop": [r["me_s"] for r in g_rep["runs"]],
+               "me_mb_per_s": round(gops * (gop - 1) * mbs / max(1e-9, sum(r["me_s"] for r in g_rep["runs"])), 1)}
+        if check_stock:
+            _progress(f"encoder gop block rank {rank}: the same GOPs through the stock encoder, {host_procs} at once")
+            s_rep, s_md5 = _gop_launch(launcher, stock, d, "stock", yuv, w, h, frames, gop, min(host_procs, gops), 1,
+                                       None, CFG, ENCODER_PARAMS)
+            same = [a == b for a, b in zip(g_md5, s_md5)]
+            out["parity"] = {"reference": "JM 18.5 lencod (stock, same GOP arguments)", "gops": gops,
+                             "byte_identical_gops": int(sum(same))}
+            out["host_baseline"] = {"procs": min(host_procs, gops), "wall_s": s_rep["python_wall_s"],
+                                    "encoder_mb_per_s": round(frames * mbs / s_rep["python_wall_s"], 1),
+                                    "me_mb_per_s": round(gops * (gop - 1) * mbs /
+                                                         max(1e-9, sum(r["me_s"] for r in s_rep["runs"])), 1),
+                                    "kind": "reference"}
+            out["encoder_speedup_vs_host"] = round(s_rep["python_wall_s"] / g_rep["python_wall_s"], 2)
+    return out
