@@ -567,20 +567,16 @@ def run_encoder(args, ws: int, rank: int, local: int) -> None:
         dist.init_process_group("gloo")
         dist.barrier()
     w, h = (int(x) for x in args.enc_size.split("x"))
-    t0 = time.perf_counter()
+    # the timed region is the launcher's own run (clip generation excluded); the
+    # stock encodes (parity, host baseline) follow once every rank's run is done
     blk = bench_blocks.encoder_gop_block(device=local, rank=rank, gops=args.enc_gops, gop=args.enc_gop, size=(w, h),
-                                         per_gpu=args.enc_per_gpu, check_stock=False, encoder=args.enc_encoder)
-    wall = time.perf_counter() - t0
+                                         per_gpu=args.enc_per_gpu, check_stock=True, encoder=args.enc_encoder,
+                                         between=(lambda: dist.barrier()) if ws > 1 else None)
     if blk is None:
         raise SystemExit("--shard encoder needs integration/_build/{lencod_jmme,jmme_gop} and oracle/_ref/lencod")
-    wall = blk["wall_s"]           # the launcher's own run (clip generation excluded)
-    if ws > 1:
-        dist.barrier()
-    # parity and the host baseline, outside the timed region
-    par = bench_blocks.encoder_gop_block(device=local, rank=rank, gops=args.enc_gops, gop=args.enc_gop, size=(w, h),
-                                         per_gpu=args.enc_per_gpu, check_stock=True, encoder=args.enc_encoder)
-    ok = par["parity"]["byte_identical_gops"]
-    rec = [wall, float(ok), float(par["host_baseline"]["encoder_mb_per_s"]), float(blk["macroblocks"])]
+    wall = blk["wall_s"]
+    ok = blk["parity"]["byte_identical_gops"]
+    rec = [wall, float(ok), float(blk["host_baseline"]["encoder_mb_per_s"]), float(blk["macroblocks"])]
     if ws > 1:
         t = torch.tensor(rec, dtype=torch.float64)
         allr = [torch.zeros_like(t) for _ in range(ws)]
@@ -605,7 +601,7 @@ def run_encoder(args, ws: int, rank: int, local: int) -> None:
             "parity": {"reference": "JM 18.5 lencod (stock, same GOP arguments)", "gops": args.enc_gops * ws,
                        "byte_identical_gops": int(sum(x[1] for x in recs))},
             "cpu_baseline": {"value": round(sum(x[2] for x in recs), 1), "unit": "macroblocks/sec",
-                             "cores": par["host_baseline"]["procs"] * ws, "kind": "reference",
+                             "cores": blk["host_baseline"]["procs"] * ws, "kind": "reference",
                              "sample": "the same GOPs through the stock lencod, concurrent processes per rank"},
             "rank0": blk}))
     if ws > 1:

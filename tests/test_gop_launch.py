@@ -79,3 +79,31 @@ def test_gop_launcher_gpu_dropin_matches_single_cpu_run(gpu):
         for r in rep["runs"]:
             log = open(os.path.join(d, f"shard_gop{r['gop']:03d}.log")).read()
             assert "Total ME time" in log
+
+
+@pytest.mark.skipif(not (os.path.exists(STOCK) and os.path.exists(LAUNCHER)), reason="JM build / launcher absent")
+def test_bench_shard_encoder_two_ranks_cpu_rehearsal():
+    """bench.py --shard encoder under torch.distributed.run at world size 2 (gloo,
+    no GPU: the stock encoder stands in for lencod_jmme): each rank encodes its
+    own closed GOPs through the launcher, the job time is the slowest rank's, and
+    every GOP is checked against the stock encoder byte for byte."""
+    import socket
+    import sys
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(REPO, "bench.py"),
+                        "--gpus", "2", "--shard", "encoder", "--enc-encoder", STOCK, "--enc-size", "176x144",
+                        "--enc-gops", "2", "--enc-gop", "2", "--enc-per-gpu", "1"],
+                       cwd=REPO, capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, (r.stdout[-1500:], r.stderr[-2500:])
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["scaling"] == "weak"
+    assert line["parity"] == {"reference": "JM 18.5 lencod (stock, same GOP arguments)", "gops": 4,
+                              "byte_identical_gops": 4}
+    assert [p["rank"] for p in line["per_rank"]] == [0, 1]
+    mbs = sum(p["macroblocks"] for p in line["per_rank"])
+    assert mbs == 2 * 2 * 2 * (176 // 16) * (144 // 16)
+    assert abs(line["value"] - mbs / max(p["wall_s"] for p in line["per_rank"])) < 0.01 * line["value"] + 1

@@ -393,7 +393,8 @@ def _gop_launch(launcher, encoder, d, tag, yuv, w, h, frames, gop, slots, per_sl
 
 
 def encoder_gop_block(device: int = 0, rank: int = 0, gops: int = 16, gop: int = 4, size=(1920, 1080),
-                      per_gpu: int = 8, host_procs=None, check_stock: bool = True, encoder=None) -> dict | None:
+                      per_gpu: int = 8, host_procs=None, check_stock: bool = True, encoder=None,
+                      between=None) -> dict | None:
     """One rank's share of the GOP-sharded encoder: `gops` closed GOPs of `gop`
     frames of a seeded 1080p clip (its own seed per rank) through lencod_jmme on
     HIP device `device` (`per_gpu` encoders at once), timed wall to wall, then --
@@ -405,7 +406,8 @@ def encoder_gop_block(device: int = 0, rank: int = 0, gops: int = 16, gop: int =
     import tempfile
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     stock = os.path.join(repo, "oracle", "_ref", "lencod")
-    gpu = encoder or os.path.join(repo, "integration", "_build", "lencod_jmme")   # (a CPU rehearsal passes the stock one)
+    gpu = os.path.abspath(encoder) if encoder else os.path.join(repo, "integration", "_build", "lencod_jmme")
+    # (a CPU rehearsal passes the stock encoder here)
     launcher = os.path.join(repo, "integration", "_build", "jmme_gop")
     if not all(os.path.exists(p) for p in (stock, gpu, launcher)):
         return None
@@ -433,6 +435,8 @@ def encoder_gop_block(device: int = 0, rank: int = 0, gops: int = 16, gop: int =
                "encoder_mb_per_s": round(frames * mbs / g_rep["python_wall_s"], 1),
                "me_s_per_gop": [r["me_s"] for r in g_rep["runs"]],
                "me_mb_per_s": round(gops * (gop - 1) * mbs / max(1e-9, sum(r["me_s"] for r in g_rep["runs"])), 1)}
+        if between is not None:   # (ranks meet here: no rank's stock encodes overlap another's timed run)
+            between()
         if check_stock:
             _progress(f"encoder gop block rank {rank}: the same GOPs through the stock encoder, {host_procs} at once")
             s_rep, s_md5 = _gop_launch(launcher, stock, d, "stock", yuv, w, h, frames, gop, min(host_procs, gops), 1,
