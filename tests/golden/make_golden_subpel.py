@@ -69,6 +69,11 @@ CASES = {
     "subpel_syn_1080p_fs32": dict(src="synth", w=1920, h=1080, frames=2, seed=2024, gmv=(5, 3),
                                   p={"SearchMode": -1, "SearchRange": 32, "NumberReferenceFrames": 1,
                                      "RDOptimization": 0, "MDDistortion": 2, **SUB}, keep="compact"),
+    # BASELINE configs[3]'s algorithm at size: one 4K P-frame, EPZS (encoder_baseline.cfg's EPZS section,
+    # RDO on, SATD) on the integer grid + EPZS_sub_pel_motion_estimation, level 5.1 (the clip of c2_syn_4k_fs32)
+    "subpel_syn_4k_epzs32": dict(src="synth", w=3840, h=2160, frames=2, seed=4096, gmv=(5, 3),
+                                 p={"LevelIDC": 51, "SearchMode": 3, "SearchRange": 32, "NumberReferenceFrames": 1,
+                                    **SUB}, keep="compact"),
 }
 
 KEEP_FIELDS = ["kind", "frame_no", "blocktype", "pos_x", "pos_y", "bsx", "bsy", "list", "ref",

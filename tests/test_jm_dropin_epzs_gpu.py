@@ -138,3 +138,28 @@ def test_lencod_epzs_1080p_frame(gpu):
     assert st["direct"] == 0 and st["batches"] <= 200, err[-800:]
     assert st["hits"] >= 0.95 * st["gpu"] and st["alone"] <= 0.05 * st["gpu"], err[-800:]
     assert st["sp_cpu"] == 0 and st["sp_chained"] >= 0.99 * st["sp_gpu"], err[-800:]
+
+
+def test_lencod_epzs_4k_frame_matches_stock_golden(gpu):
+    """BASELINE configs[3] in the encoder at size: one 3840x2160 P picture (32,400
+    macroblocks, level 5.1) with encoder_baseline.cfg's EPZS keys -- quarter-pel
+    grid, SATD, RDO on, adaptive rounding -- through lencod_jmme.  The stock
+    encoder's md5s were recorded in this container by
+    tests/golden/make_golden_encodes.py (the stock 4K encode takes a minute; it is
+    not repeated here); the drop-in must reproduce bitstream and reconstruction
+    byte for byte with every EPZS search on the GPU."""
+    from golden_io import manifest
+    from jmme import synth
+    from test_jm_dropin_gpu import _md5
+    m = manifest()["enc_4k_epzs_baseline"]
+    w, h, frames = m["w"], m["h"], m["frames"]
+    with tempfile.TemporaryDirectory() as d:
+        yuv = os.path.join(d, "in.yuv")
+        synth.write_yuv420(yuv, synth.luma_sequence(w, h, frames, seed=m["seed"], gmv=tuple(m["gmv"])))
+        assert _md5(yuv) == m["md5_input"], "the seeded clip does not regenerate identically"
+        b, r, res = _encode(GPU, d, "gpu", yuv, w, h, frames, m["params"])
+        st = epzs_stats(res.stderr)
+        assert (b, r) == (m["md5_bitstream"], m["md5_recon"]), res.stderr[-800:]
+    assert st["gpu"] == 32400 * 41 and st["cpu"] == 0 and st["stale"] > 0, res.stderr[-800:]
+    print({k: st.get(k) for k in ("hits", "batches", "alone", "direct", "wrap_ms", "call_ms")})
+    assert st["direct"] == 0 and st["hits"] >= 0.9 * st["gpu"], res.stderr[-800:]
