@@ -525,7 +525,11 @@ int launch(jmme_ctx *ctx, int mode, const uint8_t *d_cur, const uint8_t *const *
   p.mode = mode;
   p.max_mvd = ctx->max_mvd;
   p.lds_range = ctx->cfg.SearchRange;
-  p.key32 = !hbd && p.lds_range <= kKey32MaxRange;
+  // 32-bit keys: 8-bit planes, or 16-bit ones up to 10 bits (a 4x4 SAD < 2^14: its
+  // key SAD << 16 + K stays exact; larger partitions saturate into the exact
+  // re-search); JMME_HBD_KEY32=0 keeps 16-bit planes on the 64-bit keys (A/B)
+  static const bool hbd_key32 = [] { const char *e = getenv("JMME_HBD_KEY32"); return !(e && e[0] == '0'); }();
+  p.key32 = (!hbd || (hbd_key32 && ctx->cfg.SourceBitDepthLuma <= 10)) && p.lds_range <= kKey32MaxRange;
   p.hbd = hbd ? 1 : 0;
   p.items = ctx->d_items;
   p.item_cap = (unsigned)ctx->cap_items;

@@ -309,10 +309,21 @@ __device__ __forceinline__ bool pos_eligible(const GroupCtx &g, bool gate_ok, in
   return gate_ok && (lring <= g.rs || (g.preseed && is00));
 }
 
-template <bool KEY32, bool FFS, bool ALL, typename Best>
+template <bool KEY32, bool FFS, bool ALL, typename Best, bool HBD = false>
 __device__ __forceinline__ void update_slots(const uint32_t (&ps)[kNS], const GroupCtx &g, const PosCtx &c,
                                              Best (&best)[kNS]) {
-  if (KEY32) {
+  if (KEY32 && HBD) {   // 16-bit samples: a partition SAD may pass 2^16, its key saturates (exact re-search)
+    const uint32_t k32 = (c.mvc << kCostShift) | (c.rank >> kRankDrop);
+    const uint32_t k32_0 = (c.mvc0 << kCostShift) | (c.rank >> kRankDrop);
+#pragma unroll
+    for (int s = 0; s < kNS; ++s) {
+      if (!ALL && !((g.gmask >> s) & 1)) continue;
+      const uint32_t k = ps[s] > 0xffffu ? ~0u : __builtin_elementwise_add_sat(ps[s] << (5 + kCostShift),
+                                                                               s == 0 ? k32_0 : k32);
+      const uint32_t kk = FFS ? (c.ok ? k : ~0u) : k;
+      best[s] = min((uint32_t)best[s], kk);
+    }
+  } else if (KEY32) {
     const uint32_t k32 = (c.mvc << kCostShift) | (c.rank >> kRankDrop);
     const uint32_t k32_0 = (c.mvc0 << kCostShift) | (c.rank >> kRankDrop);
 #pragma unroll
@@ -347,6 +358,17 @@ __device__ __forceinline__ uint32_t partition_sad_at(const Lds &L, const uint32_
     for (int c = 0; c < gm.w; ++c) sad = __builtin_amdgcn_sad_u8(w[4 * c], cur[row * 4 + gm.bx + c], sad);
   }
   return sad;
+}
+
+// One 4-pel row of a 4x4 block against the current MB: the window word at
+// the block's column (w[0]; 16-bit planes: words x and x + 2 hold the 4
+// samples) and the MB row (8-bit: one dword a block; 16-bit: two).
+constexpr int cur_words(bool hbd) { return hbd ? 8 : 4; }   // L.cur dwords per MB row
+template <bool HBD>
+__device__ __forceinline__ uint32_t sad4(const uint32_t *w, const uint32_t *cur_row, int bx, uint32_t acc) {
+  if constexpr (HBD)
+    return __builtin_amdgcn_sad_u16(w[2], cur_row[2 * bx + 1], __builtin_amdgcn_sad_u16(w[0], cur_row[2 * bx], acc));
+  return __builtin_amdgcn_sad_u8(w[0], cur_row[bx], acc);
 }
 
 template <int CTRL>
@@ -777,12 +799,12 @@ __device__ __forceinline__ void partition_keys(const uint32_t (&a)[16], uint32_t
 // keeps, per size n in {1, 2, 4, 8, 16}, the largest centre key of that size
 // plus n-1 (for a rounded-up division) in its 8-word L.tmax slot.
 // On the bench clip 92 % of the 64-lane tasks skip the keys and minima.
-template <bool FFS>
+template <bool FFS, bool HBD = false>
 __device__ __forceinline__ void centre_bounds(const GroupCtx &g, const Lds &L, int lane, int wave) {
   const int b = lane & 15, i = lane >> 4;   // 4x4 block, row in it
   const int bx = b & 3, by = b >> 2;
-  uint32_t sad = __builtin_amdgcn_sad_u8(L.words[(g.R + 4 * by + i) * L.wp + g.R + 4 * bx],
-                                         L.cur[(4 * by + i) * 4 + bx], 0u);
+  uint32_t sad = sad4<HBD>(&L.words[(g.R + 4 * by + i) * L.wp + g.R + 4 * bx], L.cur + (4 * by + i) * cur_words(HBD),
+                           bx, 0u);
   sad += __shfl_xor(sad, 16, 64);
   sad += __shfl_xor(sad, 32, 64);           // every lane: the SAD of its block
   uint32_t S[16];
@@ -849,7 +871,16 @@ __host__ __device__ constexpr int v6_base(int q) {
 // Phase B, position by position (a position's keys die with it): 8x4, 4x8,
 // then 8x8 from the 8x4s, 16x8 / 8x16 from the 8x8s and the 16x16 -- the sums
 // of partition_keys (update_full_search_large_blocks, me_fullfast.c:196-260).
-template <int P>
+// the key of the union of two partitions from theirs (each SAD << 16 + K):
+// a + b - K, or for 16-bit samples (SAT) saturating -- a sum past 2^32 becomes
+// ~0u, which the reduce sends to the exact re-search when it is the minimum
+template <bool SAT>
+__device__ __forceinline__ uint32_t ukey(uint32_t a, uint32_t b, uint32_t K) {
+  if constexpr (SAT) return __builtin_elementwise_add_sat(a, b - K);
+  return add3(a, b, 0u - K);
+}
+
+template <int P, bool SAT = false>
 __device__ __forceinline__ void fold_v6(const uint32_t (&a)[P][16], const uint32_t (&K)[P], uint32_t (&b)[kRed2]) {
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -868,9 +899,9 @@ __device__ __forceinline__ void fold_v6(const uint32_t (&a)[P][16], const uint32
     uint32_t m[4];
 #pragma unroll
     for (int bx = 0; bx < 4; ++bx) {
-      m[bx] = add3(a[0][(2 * v) * 4 + bx], a[0][(2 * v + 1) * 4 + bx], 0u - K[0]);
+      m[bx] = ukey<SAT>(a[0][(2 * v) * 4 + bx], a[0][(2 * v + 1) * 4 + bx], K[0]);
 #pragma unroll
-      for (int j = 1; j < P; ++j) m[bx] = min(m[bx], add3(a[j][(2 * v) * 4 + bx], a[j][(2 * v + 1) * 4 + bx], 0u - K[j]));
+      for (int j = 1; j < P; ++j) m[bx] = min(m[bx], ukey<SAT>(a[j][(2 * v) * 4 + bx], a[j][(2 * v + 1) * 4 + bx], K[j]));
     }
     b[4 + v] = min(b[4 + v], v6_sr(m[0], m[1], m[2], m[3]));
   }
@@ -884,15 +915,15 @@ __device__ __forceinline__ void fold_v6(const uint32_t (&a)[P][16], const uint32
 #pragma unroll
     for (int by = 0; by < 4; ++by)
 #pragma unroll
-      for (int h = 0; h < 2; ++h) e[by * 2 + h] = add3(a[j][by * 4 + 2 * h], a[j][by * 4 + 2 * h + 1], nk);   // 8x4
+      for (int h = 0; h < 2; ++h) e[by * 2 + h] = ukey<SAT>(a[j][by * 4 + 2 * h], a[j][by * 4 + 2 * h + 1], K[j]);   // 8x4
 #pragma unroll
     for (int v = 0; v < 2; ++v)
 #pragma unroll
-      for (int h = 0; h < 2; ++h) g[v * 2 + h] = add3(e[(2 * v) * 2 + h], e[(2 * v + 1) * 2 + h], nk);   // 8x8
-    t[0] = add3(g[0], g[1], nk);   // 16x8 top
-    t[1] = add3(g[2], g[3], nk);   // 16x8 bottom
-    t[2] = add3(g[0], g[2], nk);   // 8x16 left
-    t[3] = add3(g[1], g[3], nk);   // 8x16 right
+      for (int h = 0; h < 2; ++h) g[v * 2 + h] = ukey<SAT>(e[(2 * v) * 2 + h], e[(2 * v + 1) * 2 + h], K[j]);   // 8x8
+    t[0] = ukey<SAT>(g[0], g[1], K[j]);   // 16x8 top
+    t[1] = ukey<SAT>(g[2], g[3], K[j]);   // 16x8 bottom
+    t[2] = ukey<SAT>(g[0], g[2], K[j]);   // 8x16 left
+    t[3] = ukey<SAT>(g[1], g[3], K[j]);   // 8x16 right
     const uint32_t zz = __builtin_elementwise_add_sat(t[0] + nk, t[1]);   // 16x16 (saturating)
     if (j == 0) {
 #pragma unroll
@@ -922,7 +953,11 @@ __device__ __forceinline__ void fold_v6(const uint32_t (&a)[P][16], const uint32
 // current MB comes from SGPRs (cs), so the only LDS traffic is the window.
 // NB = kNS: per-lane minima of the 41 partition keys (v5); NB = kRed2: the
 // v6 fold's reduce-scattered registers.  Returns whether any task folded.
-template <int WP, int P, int NB>   // WP: words pitch when known at compile time (kWP32), else 0 (L.wp)
+// HBD: 16-bit samples (SourceBitDepthLuma <= 10): words x, x + 2 hold a block
+// row's 4 samples, the MB rows come from LDS (128 dwords: no room in SGPRs), a
+// block's SAD is accumulated plain and made a key (SAD << 16 + K) at the end,
+// and partition keys saturate (fold_v6<P, true>).
+template <int WP, int P, int NB, bool HBD = false>   // WP: words pitch when known at compile time (kWP32), else 0 (L.wp)
 __device__ __forceinline__ bool sweep_v5(const Lds &L, const uint32_t (&cs)[64], int R, int rs,
                                          uint32_t (&best)[NB]) {
   bool folded = false;
@@ -978,6 +1013,42 @@ __device__ __forceinline__ bool sweep_v5(const Lds &L, const uint32_t (&cs)[64],
     // pitch the row offsets then ride in the ds_read2 offset fields
     const uint32_t wbase = (lds_addr(L.words) + 4u * (uint32_t)((off + y0) * wp + off + tx)) & 0x7fffffffu;
     const lds_u32 *wrow = reinterpret_cast<const lds_u32 *>((uintptr_t)wbase);
+    if constexpr (HBD) {
+      const uint32_t cb = lds_addr(L.cur);
+      uint32_t cm[16][8];   // MB rows as loaded (fully unrolled: P rows live at a time)
+#pragma unroll
+      for (int j = 0; j < P; ++j)
+#pragma unroll
+        for (int k = 0; k < 16; ++k) a[j][k] = 0u;
+#pragma unroll
+      for (int r = 0; r < 15 + P; ++r) {
+        const lds_u32 *ad = wrow + r * wp;
+        const u32x2 w0 = u32x2{ad[0], ad[2]}, w1 = u32x2{ad[4], ad[6]};
+        const u32x2 w2 = u32x2{ad[8], ad[10]}, w3 = u32x2{ad[12], ad[14]};
+        if (r < 16) {
+          const u32x4 lo = ds_read_b128(cb + 32u * (uint32_t)r), hi = ds_read_b128(cb + 32u * (uint32_t)r + 16u);
+          cm[r][0] = lo.x; cm[r][1] = lo.y; cm[r][2] = lo.z; cm[r][3] = lo.w;
+          cm[r][4] = hi.x; cm[r][5] = hi.y; cm[r][6] = hi.z; cm[r][7] = hi.w;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+          const int mr = r - j;
+          if (mr < 0 || mr > 15) continue;
+          const int b = (mr >> 2) * 4;
+          a[j][b + 0] = __builtin_amdgcn_sad_u16(w0.y, cm[mr][1], __builtin_amdgcn_sad_u16(w0.x, cm[mr][0], a[j][b + 0]));
+          a[j][b + 1] = __builtin_amdgcn_sad_u16(w1.y, cm[mr][3], __builtin_amdgcn_sad_u16(w1.x, cm[mr][2], a[j][b + 1]));
+          a[j][b + 2] = __builtin_amdgcn_sad_u16(w2.y, cm[mr][5], __builtin_amdgcn_sad_u16(w2.x, cm[mr][4], a[j][b + 2]));
+          a[j][b + 3] = __builtin_amdgcn_sad_u16(w3.y, cm[mr][7], __builtin_amdgcn_sad_u16(w3.x, cm[mr][6], a[j][b + 3]));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // the 4x4 keys: exact for SAD < 2^14 (<= 10 bits) and lambda <= kMaxLambda32
+#pragma unroll
+      for (int j = 0; j < P; ++j)
+#pragma unroll
+        for (int k = 0; k < 16; ++k) a[j][k] = (a[j][k] << 16) + K[j];
+    } else {
     u32x2 n01 = u32x2{wrow[0], wrow[4]}, n23 = u32x2{wrow[8], wrow[12]};
 #pragma unroll
     for (int r = 0; r < 15 + P; ++r) {
@@ -1000,6 +1071,7 @@ __device__ __forceinline__ bool sweep_v5(const Lds &L, const uint32_t (&cs)[64],
         a[j][b + 3] = __builtin_amdgcn_sad_hi_u8(w23.y, cs[mr * 4 + 3], first ? K[j] : a[j][b + 3]);
       }
       __builtin_amdgcn_sched_barrier(0);
+    }
     }
     // exact elimination (centre_bounds): skip the keys and minima when no lane's
     // task can beat the centre in any partition
@@ -1040,7 +1112,7 @@ __device__ __forceinline__ bool sweep_v5(const Lds &L, const uint32_t (&cs)[64],
     if (fold) {
     folded = true;
     if constexpr (NB == kRed2) {
-      fold_v6<P>(a, K, best);
+      fold_v6<P, HBD>(a, K, best);
     } else {
     // positions in pairs: both keys of a partition fold with one v_min3_u32
 #pragma unroll
@@ -1129,7 +1201,7 @@ __device__ __forceinline__ uint32_t special_key(const GroupCtx &g, const Lds &L,
 // barrier): the special candidate's 16 4x4 SADs, then its key
 // for every slot into L.spec[16 + s] (one wave: its LDS writes land before its
 // own later reads, no barrier); read back after the reduce's barrier.
-template <bool FFS>
+template <bool FFS, bool HBD = false>
 __device__ __forceinline__ void special_keys(const GroupCtx &g, const Lds &L, int lane) {
   if (lane < 16) {
     const int ox = -(g.cqx >> 2), oy = -(g.cqy >> 2);
@@ -1137,7 +1209,7 @@ __device__ __forceinline__ void special_keys(const GroupCtx &g, const Lds &L, in
     const uint32_t *w = L.words + (oy + g.R + 4 * by) * L.wp + ox + g.R + 4 * bx;
     uint32_t sad = 0;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) sad = __builtin_amdgcn_sad_u8(w[r * L.wp], L.cur[(4 * by + r) * 4 + bx], sad);
+    for (int r = 0; r < 4; ++r) sad = sad4<HBD>(w + r * L.wp, L.cur + (4 * by + r) * cur_words(HBD), bx, sad);
     L.spec[lane] = sad;
   }
   if (lane < kNS) L.spec[16 + lane] = special_key<FFS>(g, L, lane);
@@ -1151,7 +1223,7 @@ __device__ __forceinline__ void special_keys(const GroupCtx &g, const Lds &L, in
 // result is the min over this call's half of L.fb.  Successive calls of one
 // item must pass alternating halves (a call counter, not the slot: the slots of
 // a sparse group mask need not alternate), so one barrier per call suffices.
-template <bool FFS>
+template <bool FFS, bool HBD = false>
 __device__ __forceinline__ unsigned long long exact_slot(const GroupCtx &g, const Lds &L, int s, int half) {
   const int tid = opaque_tid(L), lane = tid & 63, wave = tid >> 6;
   const int R = g.R, D = 2 * R + 1;
@@ -1166,8 +1238,8 @@ __device__ __forceinline__ unsigned long long exact_slot(const GroupCtx &g, cons
     uint32_t sad = 0;
     for (int r = 0; r < 4 * gm.h; ++r)
       for (int c = 0; c < gm.w; ++c)
-        sad = __builtin_amdgcn_sad_u8(L.words[(oyw + 4 * gm.by + r) * L.wp + oxw + 4 * (gm.bx + c)],
-                                      L.cur[(4 * gm.by + r) * 4 + gm.bx + c], sad);
+        sad = sad4<HBD>(&L.words[(oyw + 4 * gm.by + r) * L.wp + oxw + 4 * (gm.bx + c)],
+                        L.cur + (4 * gm.by + r) * cur_words(HBD), gm.bx + c, sad);
     const int sidx = spiral_index_bl(ox, oy);
     const uint32_t rank = FFS ? ((g.preseed && is00) ? 0u : (uint32_t)sidx + 1u) : (uint32_t)sidx;
     const uint32_t mvc = (!FFS && g.chk00 && s == 0) ? check00_adjust(mc.mvc, g.lam, is00) : mc.mvc;
@@ -1219,9 +1291,9 @@ __device__ __forceinline__ jmme_block_res block_result(const GroupCtx &g, bool f
 // candidates consecutive groups (the winner found by one ballot).  Every lane
 // forms its slot's key from the per-wave minima itself, so nothing else needs
 // the LDS combine.  skip0: slot 0 is served by the exact fallback instead.
-template <bool FFS>
+template <bool FFS, bool HBD = false>
 __device__ __forceinline__ void refine_output32(const KParams &p, const GroupCtx &g, const Lds &L, bool spec,
-                                                bool fast, bool skip0, int u) {
+                                                bool fast, unsigned long long skip, int u) {
   const int tid = opaque_tid(L), lane = tid & 63, wave = ufl(tid >> 6);
   int s, j, q, nq;
   if (wave == 0) { s = 25 + (lane >> 2); j = lane & 3; q = 0; nq = 1; }
@@ -1230,7 +1302,7 @@ __device__ __forceinline__ void refine_output32(const KParams &p, const GroupCtx
     if (lane < 32) { s = 5 + (lane >> 3); j = (lane >> 1) & 3; q = lane & 1; nq = 2; }
     else { s = 0; j = (lane >> 3) & 3; q = lane & 7; nq = 8; }
   } else { s = 1 + (lane >> 4); j = (lane >> 2) & 3; q = lane & 3; nq = 4; }
-  const bool mine = ((g.gmask >> s) & 1) && !(skip0 && s == 0);
+  const bool mine = ((g.gmask >> s) & 1) && !((skip >> s) & 1);
   uint32_t key = ~0u;
   if (mine) {
 #pragma unroll
@@ -1262,7 +1334,7 @@ __device__ __forceinline__ void refine_output32(const KParams &p, const GroupCtx
       const int bx = gm.bx + k % gm.w, by = gm.by + k / gm.w;
       const uint32_t *w = L.words + (oy + R + 4 * by) * L.wp + ox + R + 4 * bx;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) sad = __builtin_amdgcn_sad_u8(w[r * L.wp], L.cur[(4 * by + r) * 4 + bx], sad);
+      for (int r = 0; r < 4; ++r) sad = sad4<HBD>(w + r * L.wp, L.cur + (4 * by + r) * cur_words(HBD), bx, sad);
     }
   }
   // sum the parts (groups of nq aligned lanes; every lane active here)
@@ -1508,7 +1580,7 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
       auto eval_position = [&](const uint32_t (&acc)[16], int oyw) {
         uint32_t ps[kNS];
         partition_sads(acc, ps);
-        update_slots<KEY32, FFS, decltype(all_tag)::value>(ps, g, pos_ctx(oyw), best);
+        update_slots<KEY32, FFS, decltype(all_tag)::value, Best, HBD>(ps, g, pos_ctx(oyw), best);
       };
 
 #ifdef JMME_ABL_NOCOST   // timing ablation only: keep the SADs live, skip the cost/minimum work
@@ -1536,9 +1608,15 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
   // per-partition masks in the loop)
   const bool spec = KEY32 && fast && special_on<FFS>(g);
   if (KEY32 && fast) {
-    if (spec && wave == kWaves - 1) special_keys<FFS>(g, L, lane);   // the wave with the fewest sweep tasks; read back after the reduce's barrier
-    if constexpr (KEY32) centre_bounds<FFS>(g, L, lane, ufl(wave));
-    if constexpr (KEY32) {
+    if (spec && wave == kWaves - 1) special_keys<FFS, HBD>(g, L, lane);   // the wave with the fewest sweep tasks; read back after the reduce's barrier
+    if constexpr (KEY32) centre_bounds<FFS, HBD>(g, L, lane, ufl(wave));
+    if constexpr (KEY32 && HBD) {   // 16-bit samples (<= 10 bits): 3 positions a task (the MB rows take VGPRs)
+#pragma unroll
+      for (int q = 0; q < kRed2; ++q) b11[q] = ~0u;
+      v6 = true;
+      v6_folded = L.wp == kWP32 ? sweep_v5<kWP32, 3, kRed2, true>(L, cs, R, g.rs, b11)
+                                : sweep_v5<0, 3, kRed2, true>(L, cs, R, g.rs, b11);
+    } else if constexpr (KEY32) {
 #if JMME_SWEEP_V6
 #pragma unroll
       for (int q = 0; q < kRed2; ++q) b11[q] = ~0u;
@@ -1616,27 +1694,43 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
   }
   __syncthreads();
   if constexpr (KEY32) {
-    // every 32-bit 16x16 key saturated (uniform: every thread forms slot 0's key)
-    bool fb16 = false;
-    if (gmask & 1) {
+    // partitions whose every key saturated go to the exact 64-bit search: at
+    // 8 bits only the 16x16 can (uniform: every thread forms slot 0's key); with
+    // 16-bit samples any partition of 8x8 or more (each wave finds them itself:
+    // lane s forms slot s's key)
+    unsigned long long satm = 0;
+    if constexpr (HBD) {
+      bool m = false;
+      if (lane < kNS && ((gmask >> lane) & 1)) {
+        uint32_t k0 = ~0u;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) k0 = min(k0, (uint32_t)L.red[w * kNS + lane]);
+        if (spec) k0 = min(k0, L.spec[16 + lane]);
+        if (fast) k0 = min(k0, L.ctr[lane]);
+        m = k0 == ~0u;
+      }
+      satm = __builtin_amdgcn_ballot_w64(m);
+    } else if (gmask & 1) {
       uint32_t k0 = ~0u;
 #pragma unroll
       for (int w = 0; w < kWaves; ++w) k0 = min(k0, (uint32_t)L.red[w * kNS]);
       if (spec) k0 = min(k0, L.spec[16]);
       if (fast) k0 = min(k0, L.ctr[0]);
-      fb16 = k0 == ~0u;
+      satm = k0 == ~0u ? 1ull : 0ull;
     }
     STAMP(st.reduce);
 #ifndef JMME_ABL_NOREFINE   // timing ablation only: no refine / output
-    refine_output32<FFS>(p, g, L, spec, fast, fb16, u);
+    refine_output32<FFS, HBD>(p, g, L, spec, fast, satm, u);
 #endif
     if (tick && opaque_tid(L) == 0) *s_tick = tk;
     STAMP(st.refine);
-    if (fb16) {   // search the 16x16 again with exact keys
-      const unsigned long long k16 = exact_slot<FFS>(g, L, 0, 0);
+    int call = 0;
+    for (unsigned long long m = satm; m; m &= m - 1) {   // search those again with exact keys
+      const int sl = __builtin_ctzll(m);
+      const unsigned long long k = exact_slot<FFS, HBD>(g, L, sl, call++);
       if (opaque_tid(L) == 0)
-        p.out[(size_t)u * kNS] =
-            block_result<FFS>(g, k16 != ~0ull, (uint32_t)(k16 & 0x7fffffffu), (uint32_t)(k16 >> 32));
+        p.out[(size_t)u * kNS + sl] =
+            block_result<FFS>(g, k != ~0ull, (uint32_t)(k & 0x7fffffffu), (uint32_t)(k >> 32));
     }
     STAMP(st.out);
     return;
@@ -1666,7 +1760,7 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
 
 // A unit whose lambda exceeds the 32-bit keys' range (kItemSlow64): every
 // partition of the item by the exact 64-bit search, one after the other.
-template <bool FFS>
+template <bool FFS, bool HBD = false>
 __device__ __forceinline__ void search_item_slow64(const KParams &p, const Item &it, const Lds &L) {
   GroupCtx g;
   g.cqx = it.cqx; g.cqy = it.cqy; g.R = it.R; g.px = it.px; g.py = it.py; g.lam = it.lam;
@@ -1678,7 +1772,7 @@ __device__ __forceinline__ void search_item_slow64(const KParams &p, const Item 
   int call = 0;
   for (int s = 0; s < kNS; ++s) {
     if (!((g.gmask >> s) & 1)) continue;
-    const unsigned long long k = exact_slot<FFS>(g, L, s, call++);
+    const unsigned long long k = exact_slot<FFS, HBD>(g, L, s, call++);
     if (opaque_tid(L) == 0)
       p.out[(size_t)it.u * kNS + s] =
           block_result<FFS>(g, k != ~0ull, (uint32_t)(k & 0x7fffffffu), (uint32_t)(k >> 32));
@@ -1720,7 +1814,6 @@ __device__ __forceinline__ Item load_item(const Item *items, unsigned j) {
 // the workgroup that drew it: tickets are only drawn while a next item exists.
 template <bool KEY32, bool FFS, bool HBD = false>
 __global__ __launch_bounds__(kWG, KEY32 ? JMME_WAVES_PER_EU : 2) void me_items_kernel(KParams p) {
-  static_assert(!(HBD && KEY32), "16-bit planes take the 64-bit keys");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ __attribute__((aligned(16))) uint32_t s_cur[HBD ? 128 : 64];
   __shared__ unsigned s_tick;
@@ -1807,7 +1900,7 @@ __global__ __launch_bounds__(kWG, KEY32 ? JMME_WAVES_PER_EU : 2) void me_items_k
         for (int k = 0; k < 64; ++k) cs[k] = 0;   // (the v5 sweep's operand: 8-bit only)
       }
       if (KEY32 && (it.flags & kItemSlow64)) {
-        search_item_slow64<FFS>(p, it, L);
+        search_item_slow64<FFS, HBD>(p, it, L);
       } else {
         ticketed = true;
 #ifdef JMME_STAMPS
@@ -2450,7 +2543,7 @@ __global__ __launch_bounds__(kChainWG) void chain_kernel(ChainParams p) {
 
 struct Occupancy {
   int cus = 0;
-  int wg[6][JMME_MAX_RANGE + 1] = {};   // resident workgroups per CU, by kernel variant and lds range
+  int wg[8][JMME_MAX_RANGE + 1] = {};   // resident workgroups per CU, by kernel variant and lds range
 };
 
 template <typename K>
@@ -2508,12 +2601,13 @@ hipError_t launch_search(const KParams &p, hipStream_t s, hipEvent_t ev0, hipEve
   auto k64 = ffs ? me_items_kernel<false, true> : me_items_kernel<false, false>;
   const int v = ffs ? 2 : 0;
   if (ev0) (void)hipEventRecord(ev0, s);
-  if (p.hbd) {   // 16-bit planes: 64-bit keys, the generic sweep with v_sad_u16 (the plan routes no 32-bit items)
-    auto k16 = ffs ? me_items_kernel<false, true, true> : me_items_kernel<false, false, true>;
+  if (p.hbd) {   // 16-bit planes: v_sad_u16; 32-bit keys up to 10 bits (p.key32), else 64-bit keys and the generic sweep
+    auto k16 = p.key32 ? (ffs ? me_items_kernel<true, true, true> : me_items_kernel<true, false, true>)
+                       : (ffs ? me_items_kernel<false, true, true> : me_items_kernel<false, false, true>);
     if (lds > 65536) {   // 16-bit staging above R = 36: raise the kernel's dynamic-LDS limit (once per instance and device)
-      static thread_local bool raised[kMaxDev][2] = {};
+      static thread_local bool raised[kMaxDev][4] = {};
       bool spare_flag = false;
-      bool &done = (dev >= 0 && dev < kMaxDev) ? raised[dev][ffs] : spare_flag;
+      bool &done = (dev >= 0 && dev < kMaxDev) ? raised[dev][ffs + 2 * (p.key32 != 0)] : spare_flag;
       if (!done) {
         if ((e = hipFuncSetAttribute(reinterpret_cast<const void *>(k16), hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)lds)) != hipSuccess)
@@ -2521,7 +2615,8 @@ hipError_t launch_search(const KParams &p, hipStream_t s, hipEvent_t ev0, hipEve
         done = true;
       }
     }
-    hipLaunchKernelGGL(k16, dim3(resident_grid(occ, dev, 4 + v / 2, k16, p.lds_range, lds)), dim3(kWG), lds, s, p);
+    hipLaunchKernelGGL(k16, dim3(resident_grid(occ, dev, (p.key32 ? 6 : 4) + v / 2, k16, p.lds_range, lds)), dim3(kWG),
+                       lds, s, p);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (ev1) (void)hipEventRecord(ev1, s);
   } else if (p.key32) {

@@ -114,6 +114,37 @@ def test_hbd_extremes_14bit(path, lam_max, gpu):
     _cmp(out, *_oracle_units(cur, ref, req))
 
 
+@pytest.mark.parametrize("ffs", [0, 1])
+def test_hbd_10bit_saturated_keys(ffs, gpu):
+    """10-bit planes at both ends of the range: the 32-bit keys of the 10-bit item
+    kernel stay exact for 4x4 blocks (SAD < 2^14) while every larger partition's
+    key saturates, so those partitions go through the exact 64-bit re-search --
+    the results must equal the oracle's everywhere (FS and FFS, RDO off)"""
+    from jmme import FAST_FULL_SEARCH, FULL_SEARCH, MotionEstimator
+    w, h, R = 96, 64, 8
+    rng = np.random.default_rng(11 + ffs)
+    cur = np.where(rng.random((h, w)) < 0.5, 0, 1023).astype(np.uint16)
+    ref = (1023 - cur).astype(np.uint16)
+    ref[::7] = cur[::7]                       # a few rows that match: mixed saturated / exact keys
+    with MotionEstimator({"SearchRange": R, "SearchMode": 0 if ffs else -1, "RDOptimization": 0,
+                          "SourceBitDepthLuma": 10}) as me:
+        _path(me, "items")
+        me.upload_cur(cur)
+        me.upload_ref(0, 0, ref)
+        if ffs:
+            req, mbs, blk = _ffs_random(rng, w, h, 12, R, 0, 0.0)
+            out = me.search(FAST_FULL_SEARCH, req)
+            max_mvd = me.max_mvd
+        else:
+            req = _random_units(rng, w, h, 12, R, lam_max=4000)
+            out = me.search(FULL_SEARCH, req)
+    if ffs:
+        mv, cost = ol.ffs_batch(cur, ref, R, max_mvd, 0, mbs, blk)
+        _cmp(out, [(u, s) for u in range(len(req)) for s in range(41)], mv, cost)
+    else:
+        _cmp(out, *_oracle_units(cur, ref, req))
+
+
 def test_hbd_refusals(gpu):
     """samples above the declared depth are refused at upload; SSE sub-pel
     refinement is refused above 11 bits (JM's int sum can wrap there)"""

@@ -60,9 +60,14 @@ def test_small_kernels_read_inline_items_without_scratch(tmp_path):
 
 
 def test_16bit_item_kernels_without_scratch(tmp_path):
-    """the 64-bit-key v_sad_u16 instances (SourceBitDepthLuma 9..14) exist and do not spill"""
+    """the v_sad_u16 instances (SourceBitDepthLuma 9..14) exist and do not spill: the
+    64-bit-key ones (11..14 bits) and the 32-bit-key ones (9..10 bits), which are
+    written for 4 waves/SIMD like the 8-bit kernels"""
     kernels = _kernel_metadata(tmp_path)
     for ffs in (0, 1):
-        name = f"_ZN4jmme12_GLOBAL__N_115me_items_kernelILb0ELb{ffs}ELb1EEEvNS_7KParamsE"
-        assert name in kernels, name
-        assert kernels[name][".private_segment_fixed_size"] == 0, name
+        for key32 in (0, 1):
+            name = f"_ZN4jmme12_GLOBAL__N_115me_items_kernelILb{key32}ELb{ffs}ELb1EEEvNS_7KParamsE"
+            assert name in kernels, name
+            assert kernels[name][".private_segment_fixed_size"] == 0, name
+            if key32:
+                assert kernels[name][".vgpr_count"] <= 128, (name, kernels[name][".vgpr_count"])
