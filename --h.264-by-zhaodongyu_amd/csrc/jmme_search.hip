@@ -372,6 +372,11 @@ __device__ __forceinline__ uint32_t sad4(const uint32_t *w, const uint32_t *cur_
 }
 
 template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_mov(uint32_t v) {   // full row / bank masks: every lane reads a valid source
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, true);
+}
+
+template <int CTRL>
 __device__ __forceinline__ uint32_t dpp_min(uint32_t v) {
   // full row/bank masks and in-row patterns: every lane reads a valid source,
   // so the mov folds into v_min_u32_dpp (GCNDPPCombine)
@@ -806,44 +811,47 @@ __device__ __forceinline__ void centre_bounds(const GroupCtx &g, const Lds &L, i
   uint32_t sad = sad4<HBD>(&L.words[(g.R + 4 * by + i) * L.wp + g.R + 4 * bx], L.cur + (4 * by + i) * cur_words(HBD),
                            bx, 0u);
   sad += __shfl_xor(sad, 16, 64);
-  sad += __shfl_xor(sad, 32, 64);           // every lane: the SAD of its block
-  uint32_t S[16];
-#pragma unroll
-  for (int k = 0; k < 16; ++k) S[k] = __builtin_amdgcn_readlane(sad, k);
+  sad += __shfl_xor(sad, 32, 64);           // every lane: the SAD of its block b
   // K at the centre: mvcost << 11 | rank >> 2, rank 0 (FFS 1: still 0 after >> 2)
-  const uint64_t Kc =
-      (uint64_t)(((uint32_t)g.lam * (uint32_t)(mvbits(g.cqx - g.px) + mvbits(g.cqy - g.py))) << kCostShift);
-  uint32_t m1 = 0, m2 = 0;
-#pragma unroll
-  for (int k = 0; k < 16; ++k) m1 = max(m1, S[k]);
-#pragma unroll
-  for (int y = 0; y < 4; ++y) m2 = max(m2, max(S[4 * y] + S[4 * y + 1], S[4 * y + 2] + S[4 * y + 3]));   // 8x4
-#pragma unroll
-  for (int x = 0; x < 4; ++x) m2 = max(m2, max(S[x] + S[4 + x], S[8 + x] + S[12 + x]));                 // 4x8
-  const uint32_t q00 = S[0] + S[1] + S[4] + S[5], q10 = S[2] + S[3] + S[6] + S[7];
-  const uint32_t q01 = S[8] + S[9] + S[12] + S[13], q11 = S[10] + S[11] + S[14] + S[15];
-  const uint32_t m4 = max(max(q00, q10), max(q01, q11));
-  const uint32_t m8 = max(max(q00 + q10, q01 + q11), max(q00 + q01, q10 + q11));
-  const uint32_t m16 = q00 + q10 + q01 + q11;
-  auto bound = [&](uint32_t m, uint32_t n) -> uint32_t {
-    const uint64_t v = Kc + ((uint64_t)m << 16) + (n - 1);
-    return v > 0xffffffffull ? 0xffffffffu : (uint32_t)v;
+  const uint32_t Kc = ((uint32_t)g.lam * (uint32_t)(mvbits(g.cqx - g.px) + mvbits(g.cqy - g.py))) << kCostShift;
+  // every partition's SAD at lane b from its neighbours' (in VGPRs: as scalars the
+  // sums spilled SGPRs, the MB holding 64 of them): lane b ^ 1 is the block to
+  // the right / left (DPP quad_perm), b ^ 4 below / above, b ^ 2 two columns
+  // over, b ^ 8 two rows over (ds_swizzle xor within 32 lanes)
+  auto xs4 = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x101F); };   // lane ^ 4
+  auto xs8 = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x201F); };   // lane ^ 8
+  const uint32_t p2h = sad + dpp_mov<0xB1>(sad);   // 8x4 with block b
+  const uint32_t p2v = sad + xs4(sad);        // 4x8
+  const uint32_t p4 = p2h + xs4(p2h);         // 8x8
+  const uint32_t p8h = p4 + dpp_mov<0x4E>(p4);     // 16x8
+  const uint32_t p8v = p4 + xs8(p4);          // 8x16
+  const uint32_t p16 = p8h + xs8(p8h);        // 16x16
+  // the largest of each size over the row of 16 lanes (every lane of the row holds it)
+  auto rmax = [&](uint32_t v) {
+    v = max(v, dpp_mov<0xB1>(v));
+    v = max(v, dpp_mov<0x4E>(v));
+    v = max(v, dpp_mov<0x141>(v));
+    return max(v, dpp_mov<0x140>(v));
   };
-  if (lane < 5) {
-    const uint32_t v = lane == 0 ? bound(m1, 1) : lane == 1 ? bound(m2, 2) : lane == 2 ? bound(m4, 4)
-                                                : lane == 3 ? bound(m8, 8) : bound(m16, 16);
-    L.tmax[wave * 8 + lane] = v;
+  // a key Kc + (SAD << 16), saturating (16-bit samples: a SAD may pass 2^16)
+  auto key = [&](uint32_t m) { return m > 0xffffu ? ~0u : __builtin_elementwise_add_sat(Kc, m << 16); };
+  const uint32_t m1 = rmax(sad), m2 = rmax(max(p2h, p2v)), m4 = rmax(p4), m8 = rmax(max(p8h, p8v));
+  if (lane == 0) {   // per size n: the largest centre key plus n - 1 (a rounded-up division)
+    uint32_t *t = L.tmax + wave * 8;
+    t[0] = key(m1);
+    t[1] = __builtin_elementwise_add_sat(key(m2), 1u);
+    t[2] = __builtin_elementwise_add_sat(key(m4), 3u);
+    t[3] = __builtin_elementwise_add_sat(key(m8), 7u);
+    t[4] = __builtin_elementwise_add_sat(key(p16), 15u);
   }
-  if (wave == kWaves - 1) {   // the centre's keys for the combine (same form as the sweep's, 16x16 saturating)
-    if (lane < 16) L.ctr[kNS + lane] = sad;
-    if (lane < kNS) {
-      const SlotGeom gm = slot_geom(lane);
-      uint32_t sum = 0;
-      for (int j = 0; j < gm.h; ++j)
-        for (int k = 0; k < gm.w; ++k) sum += L.ctr[kNS + (gm.by + j) * 4 + gm.bx + k];
-      const uint64_t v = Kc + ((uint64_t)sum << 16);
-      L.ctr[lane] = v > 0xffffffffull ? 0xffffffffu : (uint32_t)v;
-    }
+  if (wave == kWaves - 1 && lane < 16) {   // the centre's keys for the combine (same form as the sweep's)
+    L.ctr[25 + b] = key(sad);
+    if (!(bx & 1)) L.ctr[9 + by * 2 + (bx >> 1)] = key(p2h);
+    if (!(by & 1)) L.ctr[17 + (by >> 1) * 4 + bx] = key(p2v);
+    if (!((bx | by) & 1)) L.ctr[5 + (by >> 1) * 2 + (bx >> 1)] = key(p4);
+    if (bx == 0 && !(by & 1)) L.ctr[1 + (by >> 1)] = key(p8h);
+    if (by == 0 && !(bx & 1)) L.ctr[3 + (bx >> 1)] = key(p8v);
+    if (b == 0) L.ctr[0] = key(p16);
   }
 }
 
@@ -1291,9 +1299,10 @@ __device__ __forceinline__ jmme_block_res block_result(const GroupCtx &g, bool f
 // candidates consecutive groups (the winner found by one ballot).  Every lane
 // forms its slot's key from the per-wave minima itself, so nothing else needs
 // the LDS combine.  skip0: slot 0 is served by the exact fallback instead.
-template <bool FFS, bool HBD = false>
+template <bool FFS, bool HBD = false, int WP = 0>   // WP: words pitch when known at compile time (kWP32), else 0
 __device__ __forceinline__ void refine_output32(const KParams &p, const GroupCtx &g, const Lds &L, bool spec,
                                                 bool fast, unsigned long long skip, int u) {
+  const int wp = WP ? WP : L.wp;
   const int tid = opaque_tid(L), lane = tid & 63, wave = ufl(tid >> 6);
   int s, j, q, nq;
   if (wave == 0) { s = 25 + (lane >> 2); j = lane & 3; q = 0; nq = 1; }
@@ -1325,16 +1334,26 @@ __device__ __forceinline__ void refine_output32(const KParams &p, const GroupCtx
       if (exists) spiral_offset_fast(sidx, &ox, &oy);
     }
   }
-  // this lane's blocks of the candidate
+  // this lane's blocks of the candidate: block q * per of the partition and,
+  // when per = 2, the next one -- to its right, or below it for a 4x8 (w = 1);
+  // partition widths are 1, 2, 4 blocks, so k / w is a shift by w >> 1
   uint32_t sad = 0;
   if (exists) {
     const SlotGeom gm = slot_geom(s);
     const int per = (gm.w * gm.h) / nq;   // 1 or 2, uniform per wave
-    for (int k = q * per; k < (q + 1) * per; ++k) {
-      const int bx = gm.bx + k % gm.w, by = gm.by + k / gm.w;
-      const uint32_t *w = L.words + (oy + R + 4 * by) * L.wp + ox + R + 4 * bx;
+    const int k0 = q * per;
+    const int bx = gm.bx + (k0 & (gm.w - 1)), by = gm.by + (k0 >> (gm.w >> 1));
+    const uint32_t *w = L.words + (oy + R + 4 * by) * wp + ox + R + 4 * bx;
+    const uint32_t *c = L.cur + 4 * by * cur_words(HBD);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) sad = sad4<HBD>(w + r * L.wp, L.cur + (4 * by + r) * cur_words(HBD), bx, sad);
+    for (int r = 0; r < 4; ++r) sad = sad4<HBD>(w + r * wp, c + r * cur_words(HBD), bx, sad);
+    if (per == 2) {
+      const bool vert = gm.w == 1;
+      const uint32_t *w2 = vert ? w + 4 * wp : w + 4;
+      const uint32_t *c2 = vert ? c + 4 * cur_words(HBD) : c;
+      const int bx2 = vert ? bx : bx + 1;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sad = sad4<HBD>(w2 + r * wp, c2 + r * cur_words(HBD), bx2, sad);
     }
   }
   // sum the parts (groups of nq aligned lanes; every lane active here)
@@ -1360,18 +1379,16 @@ __device__ __forceinline__ void refine_output32(const KParams &p, const GroupCtx
     m = rank_ok && (sad << 5) + mv == (key >> kCostShift) && ok;
   }
   const unsigned long long M = __builtin_amdgcn_ballot_w64(m);
+  // only leader lanes (q = 0) can match: bit jj * nq of M >> base is candidate jj
+  // of this slot, the bits below j * nq its candidates before this one
   const int base = lane - q - j * nq;   // leader lane of (s, candidate 0)
-  unsigned long long lower = 0, all = 0;
-#pragma unroll
-  for (int jj = 0; jj < kCand; ++jj) {
-    const unsigned long long b = 1ull << (base + jj * nq);
-    all |= b;
-    lower |= jj < j ? b : 0ull;
-  }
+  const unsigned long long grp = M >> base;
+  const bool lower_hit = (grp & ((1ull << (j * nq)) - 1)) != 0;
+  const bool any_hit = (grp & ((1ull << (kCand * nq)) - 1)) != 0;
   if (!mine || q != 0) return;
   jmme_block_res res;
   res.reserved = 0;
-  if (m && !(M & lower)) {
+  if (m && !lower_hit) {
     res.mv_x = (int16_t)(g.cqx + 4 * ox);
     res.mv_y = (int16_t)(g.cqy + 4 * oy);
     res.cost = (int64_t)(key >> kCostShift);
@@ -1385,7 +1402,7 @@ __device__ __forceinline__ void refine_output32(const KParams &p, const GroupCtx
     const int64_t dmax = (int64_t)(((uint64_t)dhi << 32) | dlo);
     res.mv_x = (int16_t)g.cqx; res.mv_y = (int16_t)g.cqy; res.cost = dmax;
   } else {
-    if (j == 0 && !(M & all)) atomicOr(&p.counts[2], 4u);   // cannot happen: refine lost the winner
+    if (j == 0 && !any_hit) atomicOr(&p.counts[2], 4u);   // cannot happen: refine lost the winner
     return;
   }
   p.out[(size_t)u * kNS + s] = res;
@@ -1720,7 +1737,8 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
     }
     STAMP(st.reduce);
 #ifndef JMME_ABL_NOREFINE   // timing ablation only: no refine / output
-    refine_output32<FFS, HBD>(p, g, L, spec, fast, satm, u);
+    if (L.wp == kWP32) refine_output32<FFS, HBD, kWP32>(p, g, L, spec, fast, satm, u);
+    else refine_output32<FFS, HBD, 0>(p, g, L, spec, fast, satm, u);
 #endif
     if (tick && opaque_tid(L) == 0) *s_tick = tk;
     STAMP(st.refine);

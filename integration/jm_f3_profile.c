@@ -29,6 +29,8 @@ static rq8_fn g_rq8;
 static dist_fn g_d4, g_d8;
 static long long g_n[4];
 static unsigned long long g_c[4];
+static long long g_n_inter4, g_n_islice4;   /* 4x4 calls with intra == 0; calls made in I slices */
+static unsigned long long g_c_inter4;
 static unsigned long long g_tsc0;
 static struct timespec g_ts0;
 
@@ -49,8 +51,14 @@ static int t_rq4(Macroblock *m, ColorPlane pl, int bx, int by, int *cc, int intr
 {
   unsigned long long t = __rdtsc();
   int r = g_rq4(m, pl, bx, by, cc, intra);
-  g_c[0] += __rdtsc() - t;
+  unsigned long long dt = __rdtsc() - t;
+  g_c[0] += dt;
   ++g_n[0];
+  if (!intra) {   /* an inter residual: the prediction is a motion-compensated block */
+    ++g_n_inter4;
+    g_c_inter4 += dt;
+  }
+  if (m->p_Slice->slice_type == I_SLICE) ++g_n_islice4;
   return r;
 }
 
@@ -123,4 +131,6 @@ static void report(void)
   for (i = 0; i < 4; i++)
     fprintf(stderr, "jm_f3_profile: %s: %lld calls, %.1f ms, %.1f ns per call\n", name[i], g_n[i],
             (double)g_c[i] / ghz * 1e-6, g_n[i] ? (double)g_c[i] / ghz / (double)g_n[i] : 0.0);
+  fprintf(stderr, "jm_f3_profile: residual_transform_quant_luma_4x4 inter (intra == 0): %lld calls, %.1f ms; "
+          "in I slices: %lld calls\n", g_n_inter4, (double)g_c_inter4 / ghz * 1e-6, g_n_islice4);
 }
