@@ -965,10 +965,13 @@ __device__ __forceinline__ void fold_v6(const uint32_t (&a)[P][16], const uint32
 // row's 4 samples, the MB rows come from LDS (128 dwords: no room in SGPRs), a
 // block's SAD is accumulated plain and made a key (SAD << 16 + K) at the end,
 // and partition keys saturate (fold_v6<P, true>).
-template <int WP, int P, int NB, bool HBD = false>   // WP: words pitch when known at compile time (kWP32), else 0 (L.wp)
-__device__ __forceinline__ bool sweep_v5(const Lds &L, const uint32_t (&cs)[64], int R, int rs,
+// RS: the sub-window's range when known at compile time (32, the common +-32
+// search: the task geometry folds to constants), else 0 (rs_in)
+template <int WP, int P, int NB, bool HBD = false, int RS = 0>   // WP: words pitch when known at compile time (kWP32), else 0 (L.wp)
+__device__ __forceinline__ bool sweep_v5(const Lds &L, const uint32_t (&cs)[64], int R, int rs_in,
                                          uint32_t (&best)[NB]) {
   bool folded = false;
+  const int rs = RS ? RS : rs_in;
   const int tid = opaque_tid(L);
   const int D = 2 * rs + 1;
   const int DT = (D + P - 1) / P;        // tasks per column (the last one shifted up)
@@ -1638,8 +1641,9 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
 #pragma unroll
       for (int q = 0; q < kRed2; ++q) b11[q] = ~0u;
       v6 = true;
-      v6_folded = L.wp == kWP32 ? sweep_v5<kWP32, JMME_SWEEP_P, kRed2>(L, cs, R, g.rs, b11)
-                                : sweep_v5<0, JMME_SWEEP_P, kRed2>(L, cs, R, g.rs, b11);
+      v6_folded = (L.wp == kWP32 && g.rs == 32) ? sweep_v5<kWP32, JMME_SWEEP_P, kRed2, false, 32>(L, cs, R, g.rs, b11)
+                  : L.wp == kWP32                 ? sweep_v5<kWP32, JMME_SWEEP_P, kRed2>(L, cs, R, g.rs, b11)
+                                                  : sweep_v5<0, JMME_SWEEP_P, kRed2>(L, cs, R, g.rs, b11);
 #else
       init_best();
       if (L.wp == kWP32) sweep_v5<kWP32, JMME_SWEEP_P, kNS>(L, cs, R, g.rs, best);
