@@ -123,6 +123,22 @@ __global__ __launch_bounds__(256) void sub_images_kernel(const T *__restrict__ s
     for (int k = 0; k < 4; ++k)
       h[r][k] = six(I[r][k + 2], I[r][k + 3], I[r][k + 1], I[r][k + 4], I[r][k], I[r][k + 5]);
   using PK = Pack4<T>;
+  // stores: a wave-uniform plane base (SGPRs) plus a 32-bit per-lane offset, so
+  // each of the 16 stores per row is one global_store with a scalar base instead
+  // of 64-bit address arithmetic per plane (a plane is < 4 GiB)
+  // (a raw buffer over the 16 planes: the plane is the scalar soffset, the sample
+  // the per-lane voffset; the 16 planes of one reference span < 4 GiB)
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, -1, 0x00020000);
+  const uint32_t off0 = ((uint32_t)row0 * (uint32_t)dst_pitch + (uint32_t)col) * (uint32_t)sizeof(T);
+  auto store = [&](int k, int m, typename Pack4<T>::V v) {
+    const int vo = (int)(off0 + (uint32_t)m * (uint32_t)dst_pitch * (uint32_t)sizeof(T));
+    const int so = (int)((uint32_t)k * (uint32_t)plane_stride * (uint32_t)sizeof(T));
+    if constexpr (sizeof(T) == 1) __builtin_amdgcn_raw_buffer_store_b32(v, rsrc, vo, so, 0);
+    else {
+      typedef unsigned u32x2v __attribute__((ext_vector_type(2)));
+      __builtin_amdgcn_raw_buffer_store_b64(u32x2v{v.x, v.y}, rsrc, vo, so, 0);
+    }
+  };
 #pragma unroll
   for (int m = 0; m < kRowsT; ++m) {   // output row row0 + m: input rows m .. m + 5
     if (row0 + m >= ph) break;
@@ -168,9 +184,8 @@ __global__ __launch_bounds__(256) void sub_images_kernel(const T *__restrict__ s
       o[13] = L(P20, Q02);    // [3][1]
       o[14] = L(P22, Q02);    // [3][2]
       o[15] = L(Q02, P20n);   // [3][3] getDiagSubImageBiLinear
-      T *d = dst + (size_t)(row0 + m) * dst_pitch + col;
 #pragma unroll
-      for (int k = 0; k < 16; ++k) *reinterpret_cast<typename PK::V *>(d + (size_t)k * plane_stride) = o[k];
+      for (int k = 0; k < 16; ++k) store(k, m, o[k]);
       continue;
     }
     int q[12][4];
@@ -192,9 +207,8 @@ __global__ __launch_bounds__(256) void sub_images_kernel(const T *__restrict__ s
     const int qi[12] = {1, 4, 5, 6, 9, 3, 7, 11, 12, 13, 14, 15};
 #pragma unroll
     for (int j = 0; j < 12; ++j) o[qi[j]] = PK::make(q[j][0], q[j][1], q[j][2], q[j][3]);
-    T *d = dst + (size_t)(row0 + m) * dst_pitch + col;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) *reinterpret_cast<typename PK::V *>(d + (size_t)k * plane_stride) = o[k];
+    for (int k = 0; k < 16; ++k) store(k, m, o[k]);
   }
 }
 
