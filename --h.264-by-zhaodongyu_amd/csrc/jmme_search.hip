@@ -1834,7 +1834,9 @@ __device__ __forceinline__ Item load_item(const Item *items, unsigned j) {
 // for the item after next while it serves an item, so the index is in LDS by
 // the next item's first barrier.  Every ticket below the run's end is served by
 // the workgroup that drew it: tickets are only drawn while a next item exists.
-template <bool KEY32, bool FFS, bool HBD = false>
+// LR: the launch's LDS range when fixed at compile time (32: every LDS offset
+// and the window pitch are constants, no SGPRs hold them), else 0 (p.lds_range)
+template <bool KEY32, bool FFS, bool HBD = false, int LR = 0>
 __global__ __launch_bounds__(kWG, KEY32 ? JMME_WAVES_PER_EU : 2) void me_items_kernel(KParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ __attribute__((aligned(16))) uint32_t s_cur[HBD ? 128 : 64];
@@ -1854,7 +1856,7 @@ __global__ __launch_bounds__(kWG, KEY32 ? JMME_WAVES_PER_EU : 2) void me_items_k
   const unsigned dyn0 = 2u * (unsigned)nbx;               // ticket t serves item dyn0 + t
   unsigned *const tick = p.counts + 8 + x;
 
-  Lds L = carve(smem, p.lds_range, HBD);
+  Lds L = carve(smem, LR ? LR : p.lds_range, HBD);
   L.cur = s_cur;
   const unsigned long long dbg_slot =
       p.debug_words ? (1ull << __builtin_ctzll((ufl64(p.req[0].slot_mask) & kAll) | (1ull << 63))) : 0ull;
@@ -2619,7 +2621,9 @@ hipError_t launch_search(const KParams &p, hipStream_t s, hipEvent_t ev0, hipEve
   else hipLaunchKernelGGL(me_plan_kernel<false>, dim3(plan_grid), dim3(64 * kPlanWaves), 0, s, p);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  auto k32 = ffs ? me_items_kernel<true, true> : me_items_kernel<true, false>;
+  // the common +-32 launch: the instance with its LDS layout fixed at compile time
+  auto k32 = p.lds_range == 32 ? (ffs ? me_items_kernel<true, true, false, 32> : me_items_kernel<true, false, false, 32>)
+                               : (ffs ? me_items_kernel<true, true> : me_items_kernel<true, false>);
   auto k64 = ffs ? me_items_kernel<false, true> : me_items_kernel<false, false>;
   const int v = ffs ? 2 : 0;
   if (ev0) (void)hipEventRecord(ev0, s);

@@ -79,6 +79,114 @@ template <> struct Pack4<uint16_t> {
   }
 };
 
+// ---- 8-bit: the six-taps two columns at a time in packed 16-bit lanes ------
+// Every six-tap of 8-bit samples lies in [-2550, 10710] and fits an int16 lane,
+// so the horizontal sums of columns (0, 1) and (2, 3), the vertical sums of
+// raw samples and the (+16) >> 5 clips run as v_pk_* on pairs; only the centre
+// plane's second pass (six-tap of the horizontal sums, up to ~4.3e5) needs 32
+// bits.  The same values as the scalar form below, in the same order of the
+// same integer operations (img_luma.c:151-431 getHor/Ver/VerTmp six-taps).
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ s16x2 as_s16x2(uint32_t v) { return __builtin_bit_cast(s16x2, v); }
+__device__ __forceinline__ uint32_t as_u32(s16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+__device__ __forceinline__ s16x2 six2(s16x2 a, s16x2 b, s16x2 c, s16x2 d, s16x2 e, s16x2 f) {
+  // 20 (c + d) - 5 (b + e) + (a + f), per 16-bit lane
+  const s16x2 k20 = {20, 20}, k5 = {5, 5};
+  return (c + d) * k20 - (b + e) * k5 + (a + f);
+}
+__device__ __forceinline__ s16x2 clip5(s16x2 x) {   // iClip1(255, (x + 16) >> 5) per lane
+  const s16x2 k16 = {16, 16}, k0 = {0, 0}, k255 = {255, 255};
+  const s16x2 y = (x + k16) >> 5;
+  return __builtin_elementwise_min(__builtin_elementwise_max(y, k0), k255);
+}
+// bytes 0 and 2 of two packed pairs -> 4 samples (lo pair first)
+__device__ __forceinline__ uint32_t pack_pairs(s16x2 lo, s16x2 hi) {
+  return __builtin_amdgcn_perm(as_u32(hi), as_u32(lo), 0x06040200u);
+}
+
+// rows: the thread's staged rows (row 0 = picture row row0 - 2), pitch in bytes;
+// a thread makes 4 columns of kRowsT output rows
+// (8-bit rows are staged from the dword boundary 2 bytes below the tile's first
+// sample: X0 - kPadX - 2 is 2 mod 4 for every tile)
+static_assert(kTileW % 4 == 0 && ((-(kPadX + 2)) & 3) == 2, "8-bit staging offset");
+__device__ __forceinline__ void interp_rows8(const uint8_t *rows, int pitch, int tx, int row0, int ph, uint8_t *dst,
+                                             int dst_pitch, size_t plane_stride, int col) {
+  constexpr int NR = kRowsT + 5;
+  // the 12 bytes at the thread's dword: sample I[c] of the scalar form is byte c + 2
+  uint32_t D1[NR], D2[NR];
+  s16x2 h01[NR], h23[NR], r23[NR], r45[NR], r67[NR];
+#pragma unroll
+  for (int r = 0; r < NR; ++r) {
+    const uint32_t *q = reinterpret_cast<const uint32_t *>(rows + (size_t)r * pitch) + tx;
+    const uint32_t d0 = q[0], d1 = q[1], d2 = q[2];
+    D1[r] = d1;
+    D2[r] = d2;
+    // P_j = (I_j, I_j+1) as two 16-bit lanes, I_j = byte j + 2 of d0:d1:d2
+    const s16x2 P0 = as_s16x2(__builtin_amdgcn_perm(d1, d0, 0x0c030c02u));
+    const s16x2 P1 = as_s16x2(__builtin_amdgcn_perm(d1, d0, 0x0c040c03u));
+    const s16x2 P2 = as_s16x2(__builtin_amdgcn_perm(d1, d0, 0x0c050c04u));
+    const s16x2 P3 = as_s16x2(__builtin_amdgcn_perm(d1, d0, 0x0c060c05u));
+    const s16x2 P4 = as_s16x2(__builtin_amdgcn_perm(d1, d0, 0x0c070c06u));
+    const s16x2 P5 = as_s16x2(__builtin_amdgcn_perm(d2, d1, 0x0c040c03u));
+    const s16x2 P6 = as_s16x2(__builtin_amdgcn_perm(d2, d1, 0x0c050c04u));
+    const s16x2 P7 = as_s16x2(__builtin_amdgcn_perm(d2, d1, 0x0c060c05u));
+    h01[r] = six2(P0, P1, P2, P3, P4, P5);   // getHorSubImageSixTap, columns 0, 1 (imgY_sub_tmp)
+    h23[r] = six2(P2, P3, P4, P5, P6, P7);   // columns 2, 3
+    r23[r] = P2;                             // raw samples of columns 0..5 for the vertical taps
+    r45[r] = P4;
+    r67[r] = P6;
+  }
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, -1, 0x00020000);
+  const uint32_t off0 = (uint32_t)row0 * (uint32_t)dst_pitch + (uint32_t)col;
+#pragma unroll
+  for (int m = 0; m < kRowsT; ++m) {   // output row row0 + m: staged rows m .. m + 5
+    if (row0 + m >= ph) break;
+    auto sixv = [&](const s16x2 (&v)[NR]) { return six2(v[m], v[m + 1], v[m + 2], v[m + 3], v[m + 4], v[m + 5]); };
+    const s16x2 v23 = clip5(sixv(r23)), v45 = clip5(sixv(r45)), v67 = clip5(sixv(r67));   // getVerSubImageSixTap
+    const uint32_t P20 = pack_pairs(v23, v45);                                              // columns 0..3
+    // columns 1..4: (v23.y, v45.x, v45.y) then v67.x
+    const uint32_t P20n = __builtin_amdgcn_perm(as_u32(v67), __builtin_amdgcn_perm(as_u32(v45), as_u32(v23),
+                                                                                  0x0c060402u), 0x04020100u);
+    const uint32_t P02 = pack_pairs(clip5(h01[m + 2]), clip5(h23[m + 2]));                  // getHorSubImageSixTap, rounded
+    const uint32_t Q02 = pack_pairs(clip5(h01[m + 3]), clip5(h23[m + 3]));
+    // getVerSubImageSixTapTmp: the six-tap of the horizontal sums, 32-bit
+    int s22[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      int t[6];
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        const s16x2 hv = k < 2 ? h01[m + j] : h23[m + j];
+        t[j] = (k & 1) ? (int)hv.y : (int)hv.x;
+      }
+      s22[k] = clipv((six(t[2], t[3], t[1], t[4], t[0], t[5]) + 512) >> 10, 255);
+    }
+    const uint32_t P00 = D1[m + 2];                                           // integer samples, columns 0..3
+    const uint32_t P00n = __builtin_amdgcn_alignbyte(D2[m + 2], D1[m + 2], 1);   // columns 1..4
+    const uint32_t Q00 = D1[m + 3];
+    const uint32_t P22 = pack4(s22[0], s22[1], s22[2], s22[3]);
+    auto L = [](uint32_t a, uint32_t b) { return __builtin_amdgcn_lerp(a, b, 0x01010101u); };
+    uint32_t o[16];
+    o[0] = P00; o[2] = P02; o[8] = P20; o[10] = P22;
+    o[1] = L(P00, P02);     // [0][1] getSubImageBiLinear
+    o[4] = L(P00, P20);     // [1][0]
+    o[5] = L(P02, P20);     // [1][1]
+    o[6] = L(P02, P22);     // [1][2]
+    o[9] = L(P20, P22);     // [2][1]
+    o[3] = L(P02, P00n);    // [0][3] getHorSubImageBiLinear
+    o[7] = L(P02, P20n);    // [1][3]
+    o[11] = L(P22, P20n);   // [2][3]
+    o[12] = L(P20, Q00);    // [3][0] getVerSubImageBiLinear
+    o[13] = L(P20, Q02);    // [3][1]
+    o[14] = L(P22, Q02);    // [3][2]
+    o[15] = L(Q02, P20n);   // [3][3] getDiagSubImageBiLinear
+    const int vo = (int)(off0 + (uint32_t)m * (uint32_t)dst_pitch);
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      __builtin_amdgcn_raw_buffer_store_b32(o[k], rsrc, vo, (int)((uint32_t)k * (uint32_t)plane_stride), 0);
+  }
+}
+
 // T = sample type; pitches and the plane stride in samples; maxv = max_imgpel_value
 template <typename T>
 __global__ __launch_bounds__(256) void sub_images_kernel(const T *__restrict__ src, int src_pitch, int W, int H,
@@ -109,6 +217,10 @@ __global__ __launch_bounds__(256) void sub_images_kernel(const T *__restrict__ s
   const int ty = threadIdx.x >> 6, tx = threadIdx.x & 63;   // a wave writes 256 contiguous samples per sub-image
   const int row0 = Y0 + kRowsT * ty, col = X0 + 4 * tx;
   if (row0 >= ph || col >= pw) return;
+  if constexpr (sizeof(T) == 1) {
+    interp_rows8(&S[kRowsT * ty][0], kRowW, tx, row0, ph, dst, dst_pitch, plane_stride, col);
+    return;
+  }
   int I[kRowsT + 5][9];   // I[dr + 2][dc + 2] = sample at (row0 + dr, col + dc)
 #pragma unroll
   for (int r = 0; r < kRowsT + 5; ++r)

@@ -8,7 +8,7 @@ import collections, csv, glob, json, os, sys
 import argparse
 ap = argparse.ArgumentParser()
 ap.add_argument("root")
-ap.add_argument("kernel", nargs="?", default="me_items_kernel<true, false, false>")
+ap.add_argument("kernel", nargs="?", default="me_items_kernel<true, false, false")
 ap.add_argument("--traffic-json")
 a_ = ap.parse_args()
 root, kern, out_json = a_.root, a_.kernel, a_.traffic_json
