@@ -107,3 +107,31 @@ def test_bench_shard_encoder_two_ranks_cpu_rehearsal():
     mbs = sum(p["macroblocks"] for p in line["per_rank"])
     assert mbs == 2 * 2 * 2 * (176 // 16) * (144 // 16)
     assert abs(line["value"] - mbs / max(p["wall_s"] for p in line["per_rank"])) < 0.01 * line["value"] + 1
+
+
+@pytest.mark.skipif(not os.path.exists(LAUNCHER), reason="launcher absent")
+def test_gop_launcher_device_map(tmp_path):
+    """--devices maps the launcher's GPU slots to HIP device indices (a rank-per-GPU
+    caller passes its own device alone); each encoder sees its device in
+    HIP_VISIBLE_DEVICES, set before it starts.  A stand-in encoder script reports
+    its environment and arguments into the GOP's log."""
+    enc = tmp_path / "fake_enc.sh"
+    enc.write_text("#!/bin/sh\necho \"dev=$HIP_VISIBLE_DEVICES args=$*\"\n"
+                   "echo 'Total ME time for sequence        :   0.125 sec'\n")
+    enc.chmod(0o755)
+    prefix = str(tmp_path / "g")
+    r = subprocess.run([LAUNCHER, "--encoder", str(enc), "--gpus", "2", "--devices", "5,7", "--gop", "2",
+                        "--frames", "5", "--prefix", prefix, "--", "-d", "x.cfg"],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    rep = json.loads(r.stdout.strip().splitlines()[-1])
+    assert rep["gops"] == 3 and rep["failed"] == 0
+    assert [g["frames"] for g in rep["runs"]] == [2, 2, 1]
+    for g in rep["runs"]:
+        log = open(f"{prefix}_gop{g['gop']:03d}.log").read()
+        assert f"dev={g['device']}" in log and g["device"] == (5, 7)[g["gpu"]], (g, log)
+        assert f"StartFrame={g['first']}" in log and f"FramesToBeEncoded={g['frames']}" in log
+        assert g["me_s"] == 0.125
+    bad = subprocess.run([LAUNCHER, "--encoder", str(enc), "--gpus", "2", "--devices", "5", "--gop", "2",
+                          "--frames", "4", "--prefix", prefix, "--"], capture_output=True, text=True, timeout=60)
+    assert bad.returncode == 2 and "fewer devices" in bad.stderr
