@@ -50,7 +50,9 @@ int fail(const char *fmt, ...) {
 // (or a caller such as torch that switches devices) never mix pointers.
 struct DevGuard {
   int prev = -1;
-  explicit DevGuard(const jmme_ctx *c);
+  // keep_server: the caller may hand a request to a running EPZS server; every
+  // other entry point stops it first (it may write what the server reads)
+  explicit DevGuard(const jmme_ctx *c, bool keep_server = false);
   ~DevGuard() { if (prev >= 0) (void)hipSetDevice(prev); }
   DevGuard(const DevGuard &) = delete;
   DevGuard &operator=(const DevGuard &) = delete;
@@ -124,6 +126,19 @@ struct jmme_ctx {
   uint32_t *h_done = nullptr;
   void *dv_done = nullptr;
   uint32_t done_seq = 0;
+  // JMME_SINGLE_MODE 3: the resident EPZS server (jmme_epzs.hip
+  // epzs_server_kernel) and its mailbox in mapped pinned memory
+  EpzsBox *h_box = nullptr;
+  EpzsBox *d_box = nullptr;
+  hipStream_t srv_stream = nullptr;
+  bool srv_running = false;
+  int srv_grid = -1, srv_hbd = -1, srv_map_words = 0;
+  uint32_t srv_seq = 0;
+  uint32_t srv_idle_ticks = 200000;          // 2 ms at s_memrealtime's 100 MHz (JMME_EPZS_SERVER_IDLE_US)
+  long long srv_launches = 0, srv_served = 0;
+  bool srv_check = false;                    // JMME_EPZS_SERVER_CHECK: every served search again by the fused kernel
+  uint8_t *h_chk = nullptr;                  // (its outputs, mapped pinned)
+  long long srv_mismatch = 0;
   std::vector<SmallItem> small_scratch;      // search_small's items (kept: no allocation per call)
   void *dv_hkeys = nullptr, *dv_chres = nullptr, *dv_sitems = nullptr, *dv_sout = nullptr;   // device views
   std::vector<uint8_t *> spare_planes;       // jmme_reserve: plane buffers the first uploads take
@@ -145,11 +160,23 @@ inline void phase(jmme_ctx *ctx, int i, double *t) {
   ctx->ph_us[i] += n - *t;
   *t = n;
 }
+
+// the resident EPZS server exits at its next poll; returns once its stream is idle
+int server_stop(jmme_ctx *ctx) {
+  if (!ctx->srv_running) return 0;
+  ctx->srv_running = false;
+  __atomic_store_n(&ctx->h_box->quit, 1u, __ATOMIC_RELEASE);
+  const hipError_t e = hipStreamSynchronize(ctx->srv_stream);
+  __atomic_store_n(&ctx->h_box->quit, 0u, __ATOMIC_RELEASE);
+  if (e != hipSuccess) return fail("EPZS server: %s", hipGetErrorString(e));
+  return 0;
+}
 }  // namespace
 
-DevGuard::DevGuard(const jmme_ctx *c) {
+DevGuard::DevGuard(const jmme_ctx *c, bool keep_server) {
   int cur = 0;
   if (c && hipGetDevice(&cur) == hipSuccess && cur != c->device && hipSetDevice(c->device) == hipSuccess) prev = cur;
+  if (c && !keep_server) (void)server_stop(const_cast<jmme_ctx *>(c));
 }
 
 // ----------------------------------------------------------------- config --
@@ -376,6 +403,13 @@ extern "C" void jmme_destroy(jmme_ctx *ctx) {
     (void)hipStreamDestroy(ctx->single_stream);
   }
   if (ctx->h_done) (void)hipHostFree(ctx->h_done);
+  if (ctx->phases && ctx->srv_launches)
+    fprintf(stderr, "jmme EPZS server: %lld searches over %lld launches\n", ctx->srv_served, ctx->srv_launches);
+  if (ctx->srv_check) fprintf(stderr, "jmme EPZS server check: %lld mismatches\n", ctx->srv_mismatch);
+  if (ctx->h_chk) (void)hipHostFree(ctx->h_chk);
+  (void)server_stop(ctx);   // (the guard above has stopped it already)
+  if (ctx->srv_stream) (void)hipStreamDestroy(ctx->srv_stream);
+  if (ctx->h_box) (void)hipHostFree(ctx->h_box);
   (void)hipFree(ctx->d_skeys);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
@@ -1435,6 +1469,111 @@ int build_epzs_params(jmme_ctx *ctx, EpzsParams &p, const jmme_epzs_req *d_req, 
   return 0;
 }
 
+// JMME_SINGLE_MODE 3: a fused search alone handed to the resident server.
+// (Re)launches it when it is not running -- first use, stopped by another
+// entry point, or gone after its idle time -- and waits for the request's
+// number in the completion word.
+int epzs_serve(jmme_ctx *ctx, const jmme_epzs_req *d_req, const int16_t *d_preds, const uint8_t *d_cond,
+               const int16_t *d_stale, jmme_epzs_res *d_out, int16_t *d_vis, int max_visited,
+               jmme_epzs_bounds *d_bnd, jmme_block_res *d_int, const EpzsOne &one, jmme_block_res *d_spo) {
+  if (!ctx->h_box) {
+    HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_box), sizeof(EpzsBox), hipHostMallocMapped));
+    std::memset(static_cast<void *>(ctx->h_box), 0, sizeof(EpzsBox));
+    void *dv = nullptr;
+    HIPCHK(hipHostGetDevicePointer(&dv, ctx->h_box, 0));
+    ctx->d_box = static_cast<EpzsBox *>(dv);
+  }
+  if (!ctx->srv_stream) HIPCHK(hipStreamCreateWithFlags(&ctx->srv_stream, hipStreamNonBlocking));
+  // a reference table or sub-images still to build are writes the server would not see: stop it first
+  bool prep = ctx->ref_table_dirty || ctx->sub_table_dirty;
+  for (int k = 0; k < kMaxLists * kMaxRefs && !prep; ++k) prep = ctx->d_refs[k] && (ctx->sub_stale[k] || !ctx->d_subs[k]);
+  if (prep && server_stop(ctx)) return -1;
+  EpzsBox *box = ctx->h_box;
+  // the server is idle between requests (the last one's number is in `done`), so
+  // the request is built in place
+  if (build_epzs_params(ctx, box->p, d_req, 1, d_preds, d_cond, d_stale, d_out, d_vis, max_visited, ctx->srv_stream,
+                        d_bnd, d_int, &one, d_spo, nullptr, 0))
+    return -1;
+  const EpzsParams &p = box->p;
+  if (ctx->srv_running && (ctx->srv_grid != p.grid || ctx->srv_hbd != p.hbd || ctx->srv_map_words < p.map_words) &&
+      server_stop(ctx))
+    return -1;
+  const uint32_t seq = ++ctx->srv_seq;
+  auto start = [&]() -> int {
+    __atomic_store_n(&box->alive, 1u, __ATOMIC_RELEASE);
+    HIPCHK(launch_epzs_server(ctx->d_box, p.grid != 0, p.hbd != 0, p.map_words, seq - 1, ctx->srv_idle_ticks,
+                              1000000000ull /* 10 s */, ctx->srv_stream));
+    ctx->srv_running = true;
+    ctx->srv_grid = p.grid;
+    ctx->srv_hbd = p.hbd;
+    ctx->srv_map_words = p.map_words;
+    ++ctx->srv_launches;
+    return 0;
+  };
+  if (!ctx->srv_running && start()) return -1;
+  __atomic_store_n(&box->seq, seq, __ATOMIC_RELEASE);
+  auto t0 = std::chrono::steady_clock::now();
+  for (unsigned spin = 1; __atomic_load_n(&box->done, __ATOMIC_ACQUIRE) != seq; ++spin) {
+    if ((spin & 63u) == 0 && __atomic_load_n(&box->alive, __ATOMIC_ACQUIRE) == 0) {
+      // it left (idle or life time) without this request, or served it just before
+      if (__atomic_load_n(&box->done, __ATOMIC_ACQUIRE) == seq) break;
+      ctx->srv_running = false;
+      HIPCHK(hipStreamSynchronize(ctx->srv_stream));
+      if (start()) return -1;
+    }
+    if ((spin & 4095u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+      const int r = server_stop(ctx);   // (surfaces a fault)
+      if (__atomic_load_n(&box->done, __ATOMIC_ACQUIRE) == seq && r == 0) break;
+      return fail("EPZS server: no completion word for request %u", seq);
+    }
+    __builtin_ia32_pause();
+  }
+  ++ctx->srv_served;
+  return 0;
+}
+
+// JMME_EPZS_SERVER_CHECK (diagnostic): the request the server just served, run
+// again by the fused launch into a block of its own; any difference is printed
+int epzs_serve_check(jmme_ctx *ctx, const jmme_epzs_res *h_out, const jmme_epzs_bounds *h_bnd, const int16_t *h_vis,
+                     const jmme_block_res *h_spo, jmme_block_res spo0, int max_visited) {
+  const size_t b_out = 64, b_bnd = 64, b_int = 64, b_spo = 64, b_vis = align64((size_t)max_visited * 4);
+  if (!ctx->h_chk) HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_chk), 256 + 4 * 65536, hipHostMallocMapped));
+  if (b_vis > 4 * 65536) return fail("server check: max_visited %d", max_visited);
+  void *dv = nullptr;
+  HIPCHK(hipHostGetDevicePointer(&dv, ctx->h_chk, 0));
+  uint8_t *h = ctx->h_chk, *d = static_cast<uint8_t *>(dv);
+  std::memset(h, 0, 256 + b_vis);
+  std::memcpy(h + b_out + b_bnd + b_int, &spo0, sizeof spo0);
+  EpzsParams pc = ctx->h_box->p;
+  pc.out = reinterpret_cast<jmme_epzs_res *>(d);
+  pc.bounds = reinterpret_cast<jmme_epzs_bounds *>(d + b_out);
+  pc.int_out = pc.int_out ? reinterpret_cast<jmme_block_res *>(d + b_out + b_bnd) : nullptr;
+  pc.fused_sp.out = reinterpret_cast<jmme_block_res *>(d + b_out + b_bnd + b_int);
+  pc.visited = reinterpret_cast<int16_t *>(d + b_out + b_bnd + b_int + b_spo);
+  pc.done = nullptr;
+  if (!ctx->single_stream) HIPCHK(hipStreamCreateWithFlags(&ctx->single_stream, hipStreamNonBlocking));
+  HIPCHK(launch_epzs(pc, ctx->single_stream));
+  HIPCHK(hipStreamSynchronize(ctx->single_stream));
+  const jmme_epzs_res *o = reinterpret_cast<const jmme_epzs_res *>(h);
+  const jmme_epzs_bounds *b = reinterpret_cast<const jmme_epzs_bounds *>(h + b_out);
+  const jmme_block_res *sp = reinterpret_cast<const jmme_block_res *>(h + b_out + b_bnd + b_int);
+  const int16_t *v = reinterpret_cast<const int16_t *>(h + b_out + b_bnd + b_int + b_spo);
+  const int nv = std::min(o->n_visited, max_visited);
+  const bool same = !std::memcmp(o, h_out, sizeof *o) && !std::memcmp(b, h_bnd, sizeof *b) &&
+                    !std::memcmp(sp, h_spo, sizeof *sp) && !std::memcmp(v, h_vis, (size_t)nv * 4);
+  if (!same && ctx->srv_mismatch++ < 20) {
+    const jmme_epzs_req &q = pc.one.q;
+    fprintf(stderr, "jmme EPZS server check: request %u (%d,%d) %dx%d bt %d var %d n_pred %d n_stale %d | server mv (%d,%d) "
+            "cost %lld path %d nv %d sp (%d,%d) %lld | fused mv (%d,%d) cost %lld path %d nv %d sp (%d,%d) %lld | bounds %s "
+            "visited %s\n", ctx->srv_seq, q.pos_x, q.pos_y, q.bsx, q.bsy, q.blocktype, q.variant, q.n_pred, q.n_stale,
+            h_out->mv_x, h_out->mv_y, (long long)h_out->cost, h_out->path, h_out->n_visited, h_spo->mv_x, h_spo->mv_y,
+            (long long)h_spo->cost, o->mv_x, o->mv_y, (long long)o->cost, o->path, o->n_visited, sp->mv_x, sp->mv_y,
+            (long long)sp->cost, std::memcmp(b, h_bnd, sizeof *b) ? "differ" : "same",
+            std::memcmp(v, h_vis, (size_t)nv * 4) ? "differ" : "same");
+  }
+  return 0;
+}
+
 int launch_epzs_ex(jmme_ctx *ctx, const jmme_epzs_req *d_req, int n, const int16_t *d_preds, const uint8_t *d_cond,
                    const int16_t *d_stale, jmme_epzs_res *d_out, int16_t *d_vis, int max_visited, hipStream_t s,
                    jmme_epzs_bounds *d_bounds = nullptr, jmme_block_res *d_int = nullptr,
@@ -1590,7 +1729,7 @@ extern "C" int jmme_epzs_speculate(jmme_ctx *ctx, const jmme_epzs_req *req, int 
                                    const uint8_t *pred_cond, int n_preds, const int16_t *stale, int n_stale,
                                    jmme_epzs_res *out, jmme_epzs_bounds *bounds, int16_t *visited, int max_visited,
                                    const jmme_subpel_req *sp_req, jmme_block_res *sp_out) {
-  DevGuard dg_(ctx);
+  DevGuard dg_(ctx, true);   // a search alone may go to the running server (below)
   if (!ctx) return fail("null ctx");
   if (n <= 0) return n < 0 ? fail("negative request count") : 0;
   if (!req || !out || !bounds || !visited || (n_preds && !preds) || (n_stale && !stale)) return fail("null array");
@@ -1611,6 +1750,7 @@ extern "C" int jmme_epzs_speculate(jmme_ctx *ctx, const jmme_epzs_req *req, int 
   const size_t b_res = sp_req ? align64((size_t)n * sizeof(jmme_block_res)) : 0;
   const size_t need = b_req + b_pred + b_stale + b_cond + b_out + b_bnd + b_vis + b_sp + 2 * b_res;
   if (need > ctx->cap_emap) {
+    if (server_stop(ctx)) return -1;   // (its next request lands in the new block)
     if (ctx->h_emap) (void)hipHostFree(ctx->h_emap);
     ctx->h_emap = nullptr;
     ctx->cap_emap = 0;
@@ -1670,9 +1810,23 @@ extern "C" int jmme_epzs_speculate(jmme_ctx *ctx, const jmme_epzs_req *req, int 
   }
   if (ctx->single_mode < 0) {
     const char *e = std::getenv("JMME_SINGLE_MODE");
-    ctx->single_mode = e ? std::max(0, std::min(2, std::atoi(e))) : 2;
+    ctx->single_mode = e ? std::max(0, std::min(3, std::atoi(e))) : 2;
+    ctx->srv_check = std::getenv("JMME_EPZS_SERVER_CHECK") != nullptr;
+    const char *ie = std::getenv("JMME_EPZS_SERVER_IDLE_US");
+    if (ie) ctx->srv_idle_ticks = (uint32_t)std::max(1, std::min(1000000, std::atoi(ie))) * 100u;
   }
   const int mode = fuse ? ctx->single_mode : 0;
+  if (mode != 3 && server_stop(ctx)) return -1;
+  if (mode == 3) {   // the resident server: no launch on the search's path
+    const jmme_block_res spo0 = *h_spo;
+    if (epzs_serve(ctx, d_req, d_preds, d_cond, d_stale, d_out, d_vis, max_visited, d_bnd, d_int, one, d_spo)) return -1;
+    if (ctx->srv_check && epzs_serve_check(ctx, h_out, h_bnd, h_vis, h_spo, spo0, max_visited)) return -1;
+    std::memcpy(out, h_out, sizeof(jmme_epzs_res));
+    std::memcpy(bounds, h_bnd, sizeof(jmme_epzs_bounds));
+    std::memcpy(visited, h_vis, (size_t)std::min(out[0].n_visited, max_visited) * 4);
+    std::memcpy(sp_out, h_spo, sizeof(jmme_block_res));
+    return 0;
+  }
   if (mode >= 1 && !ctx->single_stream) HIPCHK(hipStreamCreateWithFlags(&ctx->single_stream, hipStreamNonBlocking));
   if (mode == 2 && !ctx->h_done) {
     HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_done), 64, hipHostMallocMapped));
@@ -2054,7 +2208,7 @@ extern "C" int jmme_sub_images_async(jmme_ctx *ctx, const uint8_t *d_src, int sr
 }
 
 extern "C" int jmme_subpel_validate(jmme_ctx *ctx, const jmme_subpel_req *req, int n) {
-  DevGuard dg_(ctx);
+  DevGuard dg_(ctx, true);   // (host-side checks only: a running EPZS server may stay)
   if (!ctx) return fail("null ctx");
   if (n < 0) return fail("negative request count");
   if (n && !req) return fail("null request array");

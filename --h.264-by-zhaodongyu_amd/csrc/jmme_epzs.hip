@@ -734,7 +734,97 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(JMME_EPZS_W
   }
 }
 
+// A resident server for the searches alone (JMME_SINGLE_MODE 3): one wave
+// polls the request number in mapped host memory, copies each request (the
+// EpzsParams of a fused search, lists included) into LDS and serves it as the
+// fused kernel does, then stores the number it served after a system-scope
+// fence.  No launch per search.  Every exit is reached by the one wave: the
+// host's quit word, idle_ticks without a request, or life_ticks in all
+// (s_memrealtime, 100 MHz); its last store clears `alive`.  The data the
+// searches read (planes, sub-images, tables) must not change while it runs:
+// the host stops it before any such write (a kernel boundary is what makes
+// another launch's writes visible to this one's caches).
+template <bool GRID, bool HBD>
+__global__ __launch_bounds__(64) void epzs_server_kernel(EpzsBox *box, uint32_t last, uint32_t idle_ticks,
+                                                          unsigned long long life_ticks) {
+  using SpT = std::conditional_t<HBD, uint16_t, uint8_t>;
+  __shared__ WaveLds s_w;
+  __shared__ spd::WaveLds<SpT> s_sp;
+  __shared__ __attribute__((aligned(16))) EpzsParams s_p;
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_map[];
+  static_assert(sizeof(EpzsParams) % 16 == 0, "the request is copied as uint4s");
+  const int lane = threadIdx.x;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  unsigned long long t_idle = t0;
+  for (;;) {
+    const uint32_t s = (uint32_t)__builtin_amdgcn_readfirstlane(
+        (int)__hip_atomic_load(&box->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM));
+    if (s == last) {
+      const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+      const uint32_t quit = (uint32_t)__builtin_amdgcn_readfirstlane(
+          (int)__hip_atomic_load(&box->quit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+      if (quit || now - t_idle > idle_ticks || now - t0 > life_ticks) break;
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    last = s;
+    {   // the request, behind the acquire of its number
+      const uint4 *src = reinterpret_cast<const uint4 *>(&box->p);
+      uint4 *dst = reinterpret_cast<uint4 *>(&s_p);
+      for (int i = lane; i < (int)(sizeof(EpzsParams) / 16); i += 64) dst[i] = src[i];
+    }
+    __syncthreads();
+    if (lane == 0) {   // the lists from the LDS copy
+      s_p.preds = reinterpret_cast<const int16_t *>(s_p.one.preds);
+      s_p.stale = reinterpret_cast<const int16_t *>(s_p.one.stale);
+      s_p.pred_cond = s_p.pred_cond ? s_p.one.cond : nullptr;
+    }
+    __syncthreads();
+    const EpzsParams &p = s_p;
+    const jmme_epzs_req &q = p.one.q;
+    const bool ok = (GRID ? q.variant >= 2 : q.variant <= 1) && q.max_x <= p.max_qpel && q.max_y <= p.max_qpel &&
+                    q.n_pred <= kEpzsStageP && q.n_stale <= kEpzsStageS;
+    if (ok) {
+      const jmme_block_res br = search_one<GRID, HBD>(p, q, s_w, s_map, lane, p.out);
+      if (p.one.spq.blocktype) refine_fused<SpT>(p.fused_sp, s_sp, lane, 0, br, &p.one.spq);
+    } else if (lane == 0) {   // as the batch kernel refuses one
+      jmme_epzs_res r{};
+      r.path = -1;
+      p.out[0] = r;
+      if (p.bounds) {
+        jmme_epzs_bounds b{};
+        b.stop_lo = 1;
+        b.stop_hi = 0;
+        b.prev_lo = 1;
+        b.prev_hi = 0;
+        p.bounds[0] = b;
+      }
+      if (p.int_out) p.int_out[0] = jmme_block_res{};
+    }
+    __threadfence_system();
+    if (lane == 0) __hip_atomic_store(&box->done, s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    __syncthreads();
+    t_idle = __builtin_amdgcn_s_memrealtime();
+  }
+  __threadfence_system();
+  if (lane == 0) __hip_atomic_store(&box->alive, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 }  // namespace
+
+hipError_t launch_epzs_server(EpzsBox *d_box, bool grid, bool hbd, int map_words, uint32_t last, uint32_t idle_ticks,
+                              unsigned long long life_ticks, hipStream_t s) {
+  auto k = grid ? (hbd ? epzs_server_kernel<true, true> : epzs_server_kernel<true, false>)
+                : (hbd ? epzs_server_kernel<false, true> : epzs_server_kernel<false, false>);
+  const size_t lds = (size_t)map_words * sizeof(uint32_t);
+  if (lds > 65536) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(k, dim3(1), dim3(64), lds, s, d_box, last, idle_ticks, life_ticks);
+  return hipGetLastError();
+}
 
 size_t epzs_map_words(bool grid, int max_qpel) {   // rounded to whole quads (the kernel clears and scans uint4s)
   const size_t side = grid ? 2 * (size_t)max_qpel + 1 : 2 * (size_t)(max_qpel >> 2) + 1;

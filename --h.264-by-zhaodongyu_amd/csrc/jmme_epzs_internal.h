@@ -21,7 +21,7 @@ struct EpzsOne {
   uint8_t cond[kEpzsStageP];
 };
 
-struct EpzsParams {
+struct alignas(16) EpzsParams {   // (whole uint4s: the server copies it so)
   const uint8_t *cur;                  // current frame: 8-bit, or 16-bit when hbd
   const uint8_t *const *refs;          // device table of reference planes (list * 32 + ref_idx)
   int pitch, width, height;            // pitch in samples
@@ -61,5 +61,16 @@ struct EpzsParams {
 
 size_t epzs_map_words(bool grid, int max_qpel);
 hipError_t launch_epzs(const EpzsParams &p, hipStream_t s);
+// The resident server's mailbox (JMME_SINGLE_MODE 3), in mapped pinned host
+// memory; each word the two sides exchange has a cache line to itself
+struct alignas(64) EpzsBox {
+  uint32_t seq, pad0[15];     // host: the request number, stored (release) after p
+  uint32_t quit, pad1[15];    // host: 1 = the server exits at its next poll
+  uint32_t done, pad2[15];    // server: the number it served, after its results and a system fence
+  uint32_t alive, pad3[15];   // host: 1 before a launch; server: 0 as its last store
+  EpzsParams p;               // the request: a fused search alone (fused = 1, one = its lists)
+};
+hipError_t launch_epzs_server(EpzsBox *d_box, bool grid, bool hbd, int map_words, uint32_t last, uint32_t idle_ticks,
+                              unsigned long long life_ticks, hipStream_t s);
 
 }  // namespace jmme

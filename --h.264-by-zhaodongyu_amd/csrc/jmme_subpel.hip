@@ -160,6 +160,10 @@ __device__ __forceinline__ void interp_rows8(const uint8_t *rows, int pitch, int
         t[j] = (k & 1) ? (int)hv.y : (int)hv.x;
       }
       s22[k] = clipv((six(t[2], t[3], t[1], t[4], t[0], t[5]) + 512) >> 10, 255);
+      // (kept out of a fused v_ashr_pk_u8_i32: packed with the next column's value
+      // by that instruction, the upper half of its destination came out wrong --
+      // sub-images 6, 9, 10, 11 and 14 differed from JM's)
+      asm volatile("" : "+v"(s22[k]));
     }
     const uint32_t P00 = D1[m + 2];                                           // integer samples, columns 0..3
     const uint32_t P00n = __builtin_amdgcn_alignbyte(D2[m + 2], D1[m + 2], 1);   // columns 1..4

@@ -163,3 +163,31 @@ def test_lencod_epzs_4k_frame_matches_stock_golden(gpu):
     assert st["gpu"] == 32400 * 41 and st["cpu"] == 0 and st["stale"] > 0, res.stderr[-800:]
     print({k: st.get(k) for k in ("hits", "batches", "alone", "direct", "wrap_ms", "call_ms")})
     assert st["direct"] == 0 and st["hits"] >= 0.9 * st["gpu"], res.stderr[-800:]
+
+
+_SRV_LINE = re.compile(r"jmme EPZS server: (\d+) searches over (\d+) launches")
+
+
+@pytest.mark.parametrize("w,h,frames,over,idle_us", [
+    (352, 288, 3, {"NumberReferenceFrames": 2}, 2000),
+    # an idle time shorter than the gap between two misses: the server leaves
+    # between most requests and the host relaunches it (the exit / relaunch race)
+    (352, 288, 3, {"NumberReferenceFrames": 2}, 3),
+    (176, 144, 4, {"NumberReferenceFrames": 2, "EPZSSubPelGrid": 0}, 2000),
+    (1920, 1080, 2, {"NumberReferenceFrames": 1}, 2000),
+])
+def test_lencod_epzs_resident_server(gpu, w, h, frames, over, idle_us):
+    """JMME_SINGLE_MODE=3: the searches alone go to a resident server kernel that
+    polls a mailbox in mapped memory (no launch per search); every other entry
+    point stops it first.  Byte-identical, and the server served them."""
+    st, err = _run(w, h, frames, over, seed=w + frames,
+                   env={"JMME_SINGLE_MODE": "3", "JMME_EPZS_SERVER_IDLE_US": str(idle_us), "JMME_PHASES": "1"})
+    assert st["gpu"] > 0 and st["cpu"] == 0, err[-800:]
+    m = _SRV_LINE.search(err)
+    assert m, err[-800:]
+    served, launches = int(m.group(1)), int(m.group(2))
+    print({"alone": st.get("alone"), "served": served, "launches": launches, "wrap_ms": st["wrap_ms"]})
+    # (the searches alone, plus those searched again when a search stamped more cells than kept)
+    assert 0.9 * st["alone"] <= served <= st["alone"] + 64 and 1 <= launches <= served, err[-800:]
+    if idle_us >= 2000:   # the server stays up between misses (stopped by the batches and uploads only)
+        assert launches <= 0.2 * served, err[-800:]

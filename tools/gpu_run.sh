@@ -10,6 +10,7 @@
 #   bench[:ARGS]        python bench.py (ARGS: comma-separated extra arguments)
 #   dropin:MODE[:ARGS]  tools/bench_dropin.py --mode MODE (ARGS: comma-separated extra arguments)
 #   py:SCRIPT[:ARGS]    python3 SCRIPT (a tools/ benchmark) with comma-separated arguments
+#   env:NAME=VALUE      export NAME=VALUE for the steps after it (env:NAME= unsets)
 set -e
 cd "$(dirname "$0")/.."
 R=$(pwd)
@@ -51,6 +52,9 @@ for step in "$@"; do
       extra=""
       [ "$script" != "$arg" ] && extra=$(echo "${arg#*:}" | tr ',' ' ')
       timeout -k 10 600 python3 "$script" $extra > "$O/py_$n.out" 2> "$O/py_$n.err" ;;
+    env)
+      name=${arg%%=*}
+      if [ -n "${arg#*=}" ]; then export "$arg"; else unset "$name"; fi ;;
     *)
       echo "unknown step $step" >&2
       exit 2 ;;
