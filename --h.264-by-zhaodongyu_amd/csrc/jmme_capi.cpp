@@ -120,7 +120,8 @@ struct jmme_ctx {
   size_t cap_skeys = 0;
   hipStream_t chain_stream = nullptr;        // chains run beside the batch of the same call (non-blocking)
   // EPZS searches alone (JMME_SINGLE_MODE: 0 null stream + sync, 1 own stream + sync,
-  // 2 own stream + the kernel's completion word polled in mapped memory)
+  // 2 own stream + the kernel's completion word polled in mapped memory, 3 (default)
+  // the resident server below)
   int single_mode = -1;
   hipStream_t single_stream = nullptr;
   uint32_t *h_done = nullptr;
@@ -136,6 +137,8 @@ struct jmme_ctx {
   uint32_t srv_seq = 0;
   uint32_t srv_idle_ticks = 200000;          // 2 ms at s_memrealtime's 100 MHz (JMME_EPZS_SERVER_IDLE_US)
   long long srv_launches = 0, srv_served = 0;
+  double srv_service_us = 0;                 // JMME_PHASES: the server's own time per request, summed
+  double srv_copy_us = 0, srv_search_us = 0; // (to the request's copy in LDS, to the search's end)
   bool srv_check = false;                    // JMME_EPZS_SERVER_CHECK: every served search again by the fused kernel
   uint8_t *h_chk = nullptr;                  // (its outputs, mapped pinned)
   long long srv_mismatch = 0;
@@ -146,6 +149,8 @@ struct jmme_ctx {
   // JMME_PHASES=1: host-side phase times of the latency calls, printed at jmme_destroy
   bool phases = false;
   double ph_us[12] = {};
+  double ep_us[2] = {};                      // JMME_PHASES: jmme_epzs_speculate time, searches alone / batches
+  long long ep_n[2] = {};
   long long ph_calls = 0, ph_big = 0;
 };
 
@@ -404,8 +409,14 @@ extern "C" void jmme_destroy(jmme_ctx *ctx) {
   }
   if (ctx->h_done) (void)hipHostFree(ctx->h_done);
   if (ctx->phases && ctx->srv_launches)
-    fprintf(stderr, "jmme EPZS server: %lld searches over %lld launches\n", ctx->srv_served, ctx->srv_launches);
+    fprintf(stderr, "jmme EPZS server: %lld searches over %lld launches; %.2f us per search in the server "
+            "(request copy %.2f, search to %.2f)\n", ctx->srv_served, ctx->srv_launches,
+            ctx->srv_service_us / std::max(1ll, ctx->srv_served), ctx->srv_copy_us / std::max(1ll, ctx->srv_served),
+            ctx->srv_search_us / std::max(1ll, ctx->srv_served));
   if (ctx->srv_check) fprintf(stderr, "jmme EPZS server check: %lld mismatches\n", ctx->srv_mismatch);
+  if (ctx->phases && (ctx->ep_n[0] || ctx->ep_n[1]))
+    fprintf(stderr, "jmme EPZS calls: %lld alone, %.1f ms (%.2f us each); %lld batches, %.1f ms\n", ctx->ep_n[0],
+            ctx->ep_us[0] / 1e3, ctx->ep_us[0] / std::max(1ll, ctx->ep_n[0]), ctx->ep_n[1], ctx->ep_us[1] / 1e3);
   if (ctx->h_chk) (void)hipHostFree(ctx->h_chk);
   (void)server_stop(ctx);   // (the guard above has stopped it already)
   if (ctx->srv_stream) (void)hipStreamDestroy(ctx->srv_stream);
@@ -1529,6 +1540,11 @@ int epzs_serve(jmme_ctx *ctx, const jmme_epzs_req *d_req, const int16_t *d_preds
     __builtin_ia32_pause();
   }
   ++ctx->srv_served;
+  if (ctx->phases) {
+    ctx->srv_service_us += 0.01 * box->service;
+    ctx->srv_copy_us += 0.01 * box->copy;
+    ctx->srv_search_us += 0.01 * box->search;
+  }
   return 0;
 }
 
@@ -1731,6 +1747,10 @@ extern "C" int jmme_epzs_speculate(jmme_ctx *ctx, const jmme_epzs_req *req, int 
                                    const jmme_subpel_req *sp_req, jmme_block_res *sp_out) {
   DevGuard dg_(ctx, true);   // a search alone may go to the running server (below)
   if (!ctx) return fail("null ctx");
+  struct EpTimer {   // JMME_PHASES: the call's time, by kind
+    jmme_ctx *c; int k; double t0;
+    ~EpTimer() { if (c->phases) { c->ep_us[k] += now_us() - t0; ++c->ep_n[k]; } }
+  } ep_timer_{ctx, n > 1, ctx->phases ? now_us() : 0.0};
   if (n <= 0) return n < 0 ? fail("negative request count") : 0;
   if (!req || !out || !bounds || !visited || (n_preds && !preds) || (n_stale && !stale)) return fail("null array");
   if (sp_req && !sp_out) return fail("sub-pel requests without an output array");
@@ -1810,7 +1830,7 @@ extern "C" int jmme_epzs_speculate(jmme_ctx *ctx, const jmme_epzs_req *req, int 
   }
   if (ctx->single_mode < 0) {
     const char *e = std::getenv("JMME_SINGLE_MODE");
-    ctx->single_mode = e ? std::max(0, std::min(3, std::atoi(e))) : 2;
+    ctx->single_mode = e ? std::max(0, std::min(3, std::atoi(e))) : 3;
     ctx->srv_check = std::getenv("JMME_EPZS_SERVER_CHECK") != nullptr;
     const char *ie = std::getenv("JMME_EPZS_SERVER_IDLE_US");
     if (ie) ctx->srv_idle_ticks = (uint32_t)std::max(1, std::min(1000000, std::atoi(ie))) * 100u;

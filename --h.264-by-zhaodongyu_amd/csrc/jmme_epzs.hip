@@ -768,6 +768,7 @@ __global__ __launch_bounds__(64) void epzs_server_kernel(EpzsBox *box, uint32_t 
       continue;
     }
     last = s;
+    const unsigned long long t_seen = __builtin_amdgcn_s_memrealtime();
     {   // the request, behind the acquire of its number
       const uint4 *src = reinterpret_cast<const uint4 *>(&box->p);
       uint4 *dst = reinterpret_cast<uint4 *>(&s_p);
@@ -780,12 +781,14 @@ __global__ __launch_bounds__(64) void epzs_server_kernel(EpzsBox *box, uint32_t 
       s_p.pred_cond = s_p.pred_cond ? s_p.one.cond : nullptr;
     }
     __syncthreads();
+    const unsigned long long t_copy = __builtin_amdgcn_s_memrealtime();
     const EpzsParams &p = s_p;
     const jmme_epzs_req &q = p.one.q;
     const bool ok = (GRID ? q.variant >= 2 : q.variant <= 1) && q.max_x <= p.max_qpel && q.max_y <= p.max_qpel &&
                     q.n_pred <= kEpzsStageP && q.n_stale <= kEpzsStageS;
     if (ok) {
       const jmme_block_res br = search_one<GRID, HBD>(p, q, s_w, s_map, lane, p.out);
+      if (lane == 0) box->search = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_seen);
       if (p.one.spq.blocktype) refine_fused<SpT>(p.fused_sp, s_sp, lane, 0, br, &p.one.spq);
     } else if (lane == 0) {   // as the batch kernel refuses one
       jmme_epzs_res r{};
@@ -800,6 +803,10 @@ __global__ __launch_bounds__(64) void epzs_server_kernel(EpzsBox *box, uint32_t 
         p.bounds[0] = b;
       }
       if (p.int_out) p.int_out[0] = jmme_block_res{};
+    }
+    if (lane == 0) {
+      box->service = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_seen);
+      box->copy = (uint32_t)(t_copy - t_seen);
     }
     __threadfence_system();
     if (lane == 0) __hip_atomic_store(&box->done, s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -68,6 +68,8 @@ struct alignas(64) EpzsBox {
   uint32_t quit, pad1[15];    // host: 1 = the server exits at its next poll
   uint32_t done, pad2[15];    // server: the number it served, after its results and a system fence
   uint32_t alive, pad3[15];   // host: 1 before a launch; server: 0 as its last store
+  uint32_t service, copy, search, pad4[13];   // server: the request's time from its number seen to its results
+                                              // stored, to its copy in LDS, to the search's end (10 ns ticks)
   EpzsParams p;               // the request: a fused search alone (fused = 1, one = its lists)
 };
 hipError_t launch_epzs_server(EpzsBox *d_box, bool grid, bool hbd, int map_words, uint32_t last, uint32_t idle_ticks,

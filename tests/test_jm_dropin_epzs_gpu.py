@@ -191,3 +191,13 @@ def test_lencod_epzs_resident_server(gpu, w, h, frames, over, idle_us):
     assert 0.9 * st["alone"] <= served <= st["alone"] + 64 and 1 <= launches <= served, err[-800:]
     if idle_us >= 2000:   # the server stays up between misses (stopped by the batches and uploads only)
         assert launches <= 0.2 * served, err[-800:]
+
+
+@pytest.mark.parametrize("mode", ["2", "0"])
+def test_lencod_epzs_launch_per_search_modes(gpu, mode):
+    """the searches alone as one launch each (JMME_SINGLE_MODE 2: own stream and a
+    polled completion word; 0: the null stream and a stream sync) -- the forms the
+    resident server replaced as the default -- stay byte-identical"""
+    st, err = _run(352, 288, 3, {"NumberReferenceFrames": 2}, seed=11, env={"JMME_SINGLE_MODE": mode, "JMME_PHASES": "1"})
+    assert st["gpu"] > 0 and st["cpu"] == 0 and st["alone"] > 0, err[-800:]
+    assert not _SRV_LINE.search(err), err[-800:]
