@@ -631,6 +631,8 @@ int ensure_sp(jmme_ctx *ctx, size_t bytes) {
 constexpr size_t align64(size_t v) { return (v + 63) & ~size_t(63); }
 
 int status_words(const unsigned *st, const jmme_ctx *ctx) {
+  if (st[2] & 8u) return fail("internal (JMME_DBG_CHECKS): the waves of a workgroup computed different saturated-slot masks");
+  if (st[2] & 16u) return fail("internal (JMME_DBG_CHECKS): the waves of a workgroup disagree on the item");
   if (st[2] & 4u) return fail("internal: the refine pass lost a winner");
   if (st[2] & 1u) return fail("a request's search range exceeds the configured SearchRange %d (or an FFS block range its surface's)", ctx->cfg.SearchRange);
   if (st[2] & 2u) return fail("a full-search centre is not on the integer grid (EPZSSubPelGrid sub-pel centres are not supported)");

@@ -1630,6 +1630,9 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
   if (KEY32 && fast) {
     if (spec && wave == kWaves - 1) special_keys<FFS, HBD>(g, L, lane);   // the wave with the fewest sweep tasks; read back after the reduce's barrier
     if constexpr (KEY32) centre_bounds<FFS, HBD>(g, L, lane, ufl(wave));
+#ifdef JMME_DBG_SYNC_TMAX   // diagnostic: the centre bounds stored before the sweep reads them
+    __syncthreads();
+#endif
     if constexpr (KEY32 && HBD) {   // 16-bit samples (<= 10 bits): 3 positions a task (the MB rows take VGPRs)
 #pragma unroll
       for (int q = 0; q < kRed2; ++q) b11[q] = ~0u;
@@ -1739,6 +1742,16 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
       if (fast) k0 = min(k0, L.ctr[0]);
       satm = k0 == ~0u ? 1ull : 0ull;
     }
+#ifdef JMME_DBG_CHECKS   // diagnostic: every wave computed the same saturated-slot mask
+    {
+      __shared__ unsigned long long s_dbg_satm[kWaves];
+      if (lane == 0) s_dbg_satm[ufl(wave)] = satm;
+      __syncthreads();
+      for (int w = 0; w < kWaves; ++w)
+        if (s_dbg_satm[w] != satm && lane == 0) atomicOr(&p.counts[2], 8u);
+      __syncthreads();
+    }
+#endif
     STAMP(st.reduce);
 #ifndef JMME_ABL_NOREFINE   // timing ablation only: no refine / output
     if (L.wp == kWP32) refine_output32<FFS, HBD, kWP32>(p, g, L, spec, fast, satm, u);
@@ -1879,9 +1892,27 @@ __global__ __launch_bounds__(kWG, KEY32 ? JMME_WAVES_PER_EU : 2) void me_items_k
     // this item's fetch has landed (every wave waits for its own loads, the
     // barrier for everyone's); the previous item is completely done with LDS,
     // and the ticket it drew is visible
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // lgkmcnt(0) too: the ticket wave 0 stored to s_tick (and every other LDS
+    // store of the previous item) must have landed before any wave passes the
+    // barrier.  With vmcnt(0) alone here the compiler dropped the barrier's own
+    // LDS wait, and waves on the other SIMDs now and then read the old ticket:
+    // the workgroup's waves then served different items (wrong results for
+    // whole refine waves, ~1 launch in 5 at 10 bits)
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __syncthreads();
     if (!first) jn = dyn0 + (unsigned)ufl((int)s_tick);
+#ifdef JMME_DBG_CHECKS   // diagnostic: every wave serves the same item and draws the same next one
+    {
+      __shared__ unsigned s_dbg_it[2 * kWaves];
+      const int wv = (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+      if ((threadIdx.x & 63) == 0) { s_dbg_it[2 * wv] = (unsigned)it.u; s_dbg_it[2 * wv + 1] = jn; }
+      __syncthreads();
+      for (int w = 0; w < kWaves; ++w)
+        if ((s_dbg_it[2 * w] != (unsigned)it.u || s_dbg_it[2 * w + 1] != jn) && (threadIdx.x & 63) == 0)
+          atomicOr(&p.counts[2], 16u);
+      __syncthreads();
+    }
+#endif
     const bool more = jn < end;
     Item nx;
     if (more) nx = load_item(items, item_at(jn));
@@ -1905,6 +1936,10 @@ __global__ __launch_bounds__(kWG, KEY32 ? JMME_WAVES_PER_EU : 2) void me_items_k
     STAMP(st.expand);
     // the raw buffer is free: start fetching the next item behind this sweep
     if (more) prefetch<HBD>(p, nx, L);
+#ifdef JMME_DBG_SYNC_PREFETCH   // diagnostic: no LDS DMA in flight during the item
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+#endif
     bool ticketed = false;
     if (it.gmask) {
       // the current MB into SGPRs: every v_sad of the v5 sweep takes it as
