@@ -139,6 +139,7 @@ struct jmme_ctx {
   long long srv_launches = 0, srv_served = 0;
   double srv_service_us = 0;                 // JMME_PHASES: the server's own time per request, summed
   double srv_copy_us = 0, srv_search_us = 0; // (to the request's copy in LDS, to the search's end)
+  double srv_ph_us[5] = {};                  // (the search's phases: set-up, centre, predictors, walk, visited)
   bool srv_check = false;                    // JMME_EPZS_SERVER_CHECK: every served search again by the fused kernel
   uint8_t *h_chk = nullptr;                  // (its outputs, mapped pinned)
   long long srv_mismatch = 0;
@@ -413,6 +414,11 @@ extern "C" void jmme_destroy(jmme_ctx *ctx) {
             "(request copy %.2f, search to %.2f)\n", ctx->srv_served, ctx->srv_launches,
             ctx->srv_service_us / std::max(1ll, ctx->srv_served), ctx->srv_copy_us / std::max(1ll, ctx->srv_served),
             ctx->srv_search_us / std::max(1ll, ctx->srv_served));
+  if (ctx->phases && ctx->srv_served)
+    fprintf(stderr, "jmme EPZS server search phases (us): set-up %.2f, centre %.2f, predictors %.2f, walk %.2f, "
+            "visited %.2f\n", ctx->srv_ph_us[0] / ctx->srv_served, ctx->srv_ph_us[1] / ctx->srv_served,
+            ctx->srv_ph_us[2] / ctx->srv_served, ctx->srv_ph_us[3] / ctx->srv_served,
+            ctx->srv_ph_us[4] / ctx->srv_served);
   if (ctx->srv_check) fprintf(stderr, "jmme EPZS server check: %lld mismatches\n", ctx->srv_mismatch);
   if (ctx->phases && (ctx->ep_n[0] || ctx->ep_n[1]))
     fprintf(stderr, "jmme EPZS calls: %lld alone, %.1f ms (%.2f us each); %lld batches, %.1f ms\n", ctx->ep_n[0],
@@ -1546,6 +1552,7 @@ int epzs_serve(jmme_ctx *ctx, const jmme_epzs_req *d_req, const int16_t *d_preds
     ctx->srv_service_us += 0.01 * box->service;
     ctx->srv_copy_us += 0.01 * box->copy;
     ctx->srv_search_us += 0.01 * box->search;
+    for (int i = 0; i < 5; ++i) ctx->srv_ph_us[i] += 0.01 * box->ph[i];
   }
   return 0;
 }

@@ -89,6 +89,7 @@ struct Search {
   int lambda;
   const uint32_t *cur;   // LDS, bsx/4 (16-bit: bsx/2) dwords per row
   uint32_t *map;
+  uint32_t *flags;       // one bit per map word this search stamped (after the bitmap)
 };
 
 // SAD of row r of the block at (ox, oy) against the current block's row r
@@ -181,23 +182,34 @@ __device__ __forceinline__ unsigned row_sad_grid(const Search &s, int cx, int cy
 // Costs (mv_cost + SAD << 5) of the candidates held by lanes 0..K-1 (qpel
 // (mx, my)), returned in the same lanes.  One lane per (candidate, row):
 // 64/bsy candidates per pass, row sums reduced inside aligned lane groups.
+// Passes of C candidates go B at a time (the sub-pel grid's clamped reads have
+// no branch, so the B passes' loads issue back to back and their latencies
+// overlap: a search is a chain of such rounds, one wave, latency-bound).
 template <int NQ, int LOGR, bool GRID, bool HBD>
 __device__ __forceinline__ int64_t eval_t(const Search &s, int lane, int K, int mx, int my) {
   constexpr int R = 1 << LOGR, C = 64 >> LOGR;
+  constexpr int B = GRID ? (C >= 16 ? 1 : 16 / C) : 1;   // up to 16 candidates in flight
   const int grp = lane >> LOGR, r = lane & (R - 1);
   unsigned mine = 0;
-  for (int base = 0; base < K; base += C) {
-    const int c = base + grp;
-    const int cmx = __shfl(mx, c & 63, 64), cmy = __shfl(my, c & 63, 64);
-    unsigned sad = 0u;
-    if (c < K)
-      sad = GRID ? row_sad_grid<NQ, HBD>(s, (s.pos_x << 2) + cmx, (s.pos_y << 2) + cmy, r)
-                 : row_sad<NQ, HBD>(s, s.pos_x + (cmx >> 2), s.pos_y + (cmy >> 2), r);
+  for (int base = 0; base < K; base += B * C) {
+    unsigned sad[B];
 #pragma unroll
-    for (int m = 1; m < R; m <<= 1) sad += __shfl_xor(sad, m, 64);
-    const int j = lane - base;
-    const unsigned v = __shfl(sad, (j & (C - 1)) << LOGR, 64);
-    if (j >= 0 && j < C) mine = v;
+    for (int b = 0; b < B; ++b) {
+      const int c = base + b * C + grp;
+      const int cmx = __shfl(mx, c & 63, 64), cmy = __shfl(my, c & 63, 64);
+      sad[b] = 0u;
+      if (c < K)
+        sad[b] = GRID ? row_sad_grid<NQ, HBD>(s, (s.pos_x << 2) + cmx, (s.pos_y << 2) + cmy, r)
+                      : row_sad<NQ, HBD>(s, s.pos_x + (cmx >> 2), s.pos_y + (cmy >> 2), r);
+    }
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+#pragma unroll
+      for (int m = 1; m < R; m <<= 1) sad[b] += __shfl_xor(sad[b], m, 64);
+      const int j = lane - base - b * C;
+      const unsigned v = __shfl(sad[b], (j & (C - 1)) << LOGR, 64);
+      if (j >= 0 && j < C) mine = v;
+    }
   }
   const int64_t mvc = (int64_t)s.lambda * (mvbits(mx - s.pred_x) + mvbits(my - s.pred_y));
   return mvc + ((int64_t)mine << 5);
@@ -259,7 +271,15 @@ __device__ __forceinline__ int cell_of(const Search &s, int mx, int my) {
               : ((my - s.cy + s.max_y) >> 2) * s.side_x + ((mx - s.cx + s.max_x) >> 2);
 }
 __device__ __forceinline__ bool test_cell(const Search &s, int c) { return (s.map[c >> 5] >> (c & 31)) & 1u; }
-__device__ __forceinline__ void set_cell(const Search &s, int c) { atomicOr(&s.map[c >> 5], 1u << (c & 31)); }
+__device__ __forceinline__ void set_cell(const Search &s, int c) {
+  atomicOr(&s.map[c >> 5], 1u << (c & 31));
+  atomicOr(&s.flags[c >> 10], 1u << ((c >> 5) & 31));
+}
+// a wave's map area at the start of a kernel (garbage LDS): all zero, so that
+// each search need clear only the words the previous one flagged
+__device__ __forceinline__ void map_init(uint32_t *area, int map_words, int lane) {
+  for (int i = lane; i < (map_words >> 2); i += 64) reinterpret_cast<uint4 *>(area)[i] = make_uint4(0u, 0u, 0u, 0u);
+}
 
 // value of lane j (j wave-uniform) as a scalar
 __device__ __forceinline__ int rl(int v, int j) { return __builtin_amdgcn_readlane(v, j); }
@@ -300,9 +320,11 @@ __device__ __forceinline__ bool le2(int64_t pr, int64_t st, Iv &pv, Iv &sv) {
   return false;
 }
 
+// stamps (the server's JMME_PHASES clocks, else null): s_memrealtime after the
+// set-up, the centre, the predictors, the pattern walk and the visited cells
 template <bool GRID, bool HBD>
 __device__ jmme_block_res search_one(const EpzsParams &p, const jmme_epzs_req &q, WaveLds &w, uint32_t *map, int lane,
-                                     jmme_epzs_res *out) {
+                                     jmme_epzs_res *out, unsigned long long *stamps = nullptr) {
   Search s;
   s.ref = GRID ? p.subs[q.ref_slot] : p.refs[q.ref_slot];
   s.pitch = GRID ? p.sub_pitch : p.pitch;
@@ -323,6 +345,8 @@ __device__ jmme_block_res search_one(const EpzsParams &p, const jmme_epzs_req &q
   s.lambda = q.lambda;
   s.cur = w.cur;
   s.map = map;
+  const int bw = epzs_bitmap_words(GRID, p.max_qpel), nfl = (bw + 31) >> 5;
+  s.flags = map + bw;
   const int side_y = GRID ? 2 * q.max_y + 1 : (2 * q.max_y >> 2) + 1;
   const int nq = q.bsx >> 2;
 
@@ -337,8 +361,17 @@ __device__ jmme_block_res search_one(const EpzsParams &p, const jmme_epzs_req &q
     const int r = lane / nq, c = lane - r * nq;
     w.cur[lane] = *reinterpret_cast<const uint32_t *>(p.cur + (size_t)(q.pos_y + r) * p.pitch + q.pos_x + 4 * c);
   }
-  const int words = (s.side_x * side_y + 31) >> 5, quads = (words + 3) >> 2;   // map_words is a multiple of 4
-  for (int i = lane; i < quads; i += 64) reinterpret_cast<uint4 *>(map)[i] = make_uint4(0u, 0u, 0u, 0u);
+  (void)side_y;
+  // the words the previous search on this map stamped (the rest is zero)
+  for (int i = lane; i < nfl; i += 64) {
+    uint32_t f = s.flags[i];
+    while (f) {
+      const int b = __builtin_ctz(f);
+      f &= f - 1;
+      map[32 * i + b] = 0u;
+    }
+    s.flags[i] = 0u;
+  }
   wave_sync();
   for (int i = lane; i < q.n_stale; i += 64) {   // cells already holding this BlkCount
     const int dx = p.stale[2 * (q.stale_off + i)], dy = p.stale[2 * (q.stale_off + i) + 1];
@@ -354,7 +387,9 @@ __device__ jmme_block_res search_one(const EpzsParams &p, const jmme_epzs_req &q
   const int64_t lambda_dist = (int64_t)q.lambda * (variant ? 3 : 2);
   const int mv_range = variant ? 12 : 10;
   int64_t stop = q.medthres + lambda_dist, prev = q.prev_sad;
+  if (stamps) stamps[0] = __builtin_amdgcn_s_memrealtime();
   int64_t best = rl64(eval_costs<GRID, HBD>(s, lane, 1, s.cx, s.cy), 0);
+  if (stamps) stamps[1] = stamps[2] = __builtin_amdgcn_s_memrealtime();   // ([2]: no predictor round)
   int tmpx = s.cx, tmpy = s.cy, path = 5;
   bool update = true;
   Iv sv{INT64_MIN, INT64_MAX}, pv{INT64_MIN, INT64_MAX};
@@ -482,6 +517,7 @@ __device__ jmme_block_res search_one(const EpzsParams &p, const jmme_epzs_req &q
         wave_sync();
       }
     }
+    if (stamps) stamps[2] = __builtin_amdgcn_s_memrealtime();
     // me_epzs_int.c:249-265: prev * 3 < best
     if (GRID && !done && !variant && refi > 0 && frame && !ge(prev, fdiv(best - 1, 3) + 1, pv)) {
       path = 7;
@@ -576,6 +612,7 @@ __device__ jmme_block_res search_one(const EpzsParams &p, const jmme_epzs_req &q
       }
     }
   }
+  if (stamps) stamps[3] = __builtin_amdgcn_s_memrealtime();
   bool written = false;
   if (update && (refi == 0 || ge(prev, best + 1, pv))) {   // prev > best
     prev = best;
@@ -591,15 +628,19 @@ __device__ jmme_block_res search_one(const EpzsParams &p, const jmme_epzs_req &q
   // cells that already held its BlkCount), as (dx, dy) qpel from the centre
   int nv = 0;
   if (p.visited) {
-    // each lane takes a contiguous run of map quads (ds_read_b128): one popcount
-    // pass, one wave prefix sum, then every lane writes its cells (row-major order kept)
+    // each lane takes a contiguous run of flag words, i.e. the stamped map words
+    // in order: one popcount pass, one wave prefix sum, then every lane writes
+    // its cells (row-major order kept)
     int16_t *const vout = p.visited + 2 * (size_t)p.max_visited * (size_t)(out - p.out);
-    const uint4 *m4 = reinterpret_cast<const uint4 *>(s.map);
-    const int per = (quads + 63) >> 6, q0 = min(lane * per, quads), q1 = min(q0 + per, quads);
+    const int per = (nfl + 63) >> 6, f0 = min(lane * per, nfl), f1 = min(f0 + per, nfl);
     int cnt = 0;
-    for (int qi = q0; qi < q1; ++qi) {
-      const uint4 v = m4[qi];
-      cnt += __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);
+    for (int fi = f0; fi < f1; ++fi) {
+      uint32_t f = s.flags[fi];
+      while (f) {
+        const int b = __builtin_ctz(f);
+        f &= f - 1;
+        cnt += __popc(s.map[32 * fi + b]);
+      }
     }
     int pre = cnt;
 #pragma unroll
@@ -608,16 +649,17 @@ __device__ jmme_block_res search_one(const EpzsParams &p, const jmme_epzs_req &q
       if (lane >= o) pre += v;
     }
     int at = pre - cnt;
-    for (int qi = q0; qi < q1 && at < p.max_visited; ++qi) {
-      const uint4 v = m4[qi];
-      const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        uint32_t bits = w4[e];
+    for (int fi = f0; fi < f1 && at < p.max_visited; ++fi) {
+      uint32_t f = s.flags[fi];
+      while (f) {
+        const int fb = __builtin_ctz(f);
+        f &= f - 1;
+        const int wi = 32 * fi + fb;
+        uint32_t bits = s.map[wi];
         while (bits) {
           const int b = __builtin_ctz(bits);
           bits &= bits - 1;
-          const int c = (4 * qi + e) * 32 + b, cyi = c / s.side_x, cxi = c - cyi * s.side_x;
+          const int c = wi * 32 + b, cyi = c / s.side_x, cxi = c - cyi * s.side_x;
           if (at < p.max_visited) {
             vout[2 * at] = (int16_t)(GRID ? cxi - s.max_x : 4 * cxi - s.max_x);
             vout[2 * at + 1] = (int16_t)(GRID ? cyi - s.max_y : 4 * cyi - s.max_y);
@@ -628,6 +670,7 @@ __device__ jmme_block_res search_one(const EpzsParams &p, const jmme_epzs_req &q
     }
     nv = __shfl(pre, 63, 64);
   }
+  if (stamps) stamps[4] = __builtin_amdgcn_s_memrealtime();
   if (lane == 0) {
     jmme_epzs_res r;
     r.mv_x = (int16_t)tmpx;
@@ -691,6 +734,8 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(JMME_EPZS_W
   extern __shared__ __attribute__((aligned(16))) uint32_t s_map[];   // quads: map_words is a multiple of 4
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint32_t *map = s_map + (size_t)wave * p.map_words;
+  map_init(map, p.map_words, lane);
+  wave_sync();
   for (int t = blockIdx.x * kWaves + wave; t < p.n; t += gridDim.x * kWaves) {
     const jmme_epzs_req q = FUSED ? p.one.q : p.req[t];
     // requests of the other grid, or with a window the map was not sized for, are refused
@@ -756,6 +801,7 @@ __global__ __launch_bounds__(64) void epzs_server_kernel(EpzsBox *box, uint32_t 
   const int lane = threadIdx.x;
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   unsigned long long t_idle = t0;
+  int map_area = -1;   // (the map area's layout the flags describe; -1: not initialised)
   for (;;) {
     const uint32_t s = (uint32_t)__builtin_amdgcn_readfirstlane(
         (int)__hip_atomic_load(&box->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM));
@@ -784,11 +830,24 @@ __global__ __launch_bounds__(64) void epzs_server_kernel(EpzsBox *box, uint32_t 
     const unsigned long long t_copy = __builtin_amdgcn_s_memrealtime();
     const EpzsParams &p = s_p;
     const jmme_epzs_req &q = p.one.q;
+    if (map_area != p.max_qpel) {   // first request, or another window size: the whole area once
+      map_init(s_map, p.map_words, lane);
+      wave_sync();
+      map_area = p.max_qpel;
+    }
     const bool ok = (GRID ? q.variant >= 2 : q.variant <= 1) && q.max_x <= p.max_qpel && q.max_y <= p.max_qpel &&
                     q.n_pred <= kEpzsStageP && q.n_stale <= kEpzsStageS;
     if (ok) {
-      const jmme_block_res br = search_one<GRID, HBD>(p, q, s_w, s_map, lane, p.out);
-      if (lane == 0) box->search = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_seen);
+      unsigned long long st[5] = {t_copy, t_copy, t_copy, t_copy, t_copy};
+      const jmme_block_res br = search_one<GRID, HBD>(p, q, s_w, s_map, lane, p.out, st);
+      if (lane == 0) {
+        box->search = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_seen);
+        box->ph[0] = (uint32_t)(st[0] - t_copy);   // set-up: current block, map, stale cells
+        box->ph[1] = (uint32_t)(st[1] - st[0]);    // the centre
+        box->ph[2] = (uint32_t)(st[2] - st[1]);    // predictors (0 on the early exits)
+        box->ph[3] = (uint32_t)(st[3] - st[2]);    // pattern walk and dual refinement
+        box->ph[4] = (uint32_t)(st[4] - st[3]);    // visited cells
+      }
       if (p.one.spq.blocktype) refine_fused<SpT>(p.fused_sp, s_sp, lane, 0, br, &p.one.spq);
     } else if (lane == 0) {   // as the batch kernel refuses one
       jmme_epzs_res r{};
@@ -833,9 +892,9 @@ hipError_t launch_epzs_server(EpzsBox *d_box, bool grid, bool hbd, int map_words
   return hipGetLastError();
 }
 
-size_t epzs_map_words(bool grid, int max_qpel) {   // rounded to whole quads (the kernel clears and scans uint4s)
-  const size_t side = grid ? 2 * (size_t)max_qpel + 1 : 2 * (size_t)(max_qpel >> 2) + 1;
-  return ((side * side + 31) / 32 + 3) & ~(size_t)3;
+size_t epzs_map_words(bool grid, int max_qpel) {   // bitmap + flags, whole quads
+  const int bw = epzs_bitmap_words(grid, max_qpel);
+  return (size_t)bw + (size_t)epzs_flag_words(bw);
 }
 
 hipError_t launch_epzs(const EpzsParams &p, hipStream_t s) {

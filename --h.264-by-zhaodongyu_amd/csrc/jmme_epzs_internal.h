@@ -59,7 +59,16 @@ struct alignas(16) EpzsParams {   // (whole uint4s: the server copies it so)
   uint32_t done_seq;
 };
 
-size_t epzs_map_words(bool grid, int max_qpel);
+// A wave's EPZSMap area: the bitmap (one bit per cell of the largest window,
+// whole quads), then one flag bit per bitmap word that a search stamped (whole
+// quads): the next search clears only the flagged words, and the visited cells
+// are read back from them, not from a scan of the whole bitmap
+__host__ __device__ inline int epzs_bitmap_words(bool grid, int max_qpel) {
+  const int side = grid ? 2 * max_qpel + 1 : 2 * (max_qpel >> 2) + 1;
+  return ((side * side + 31) / 32 + 3) & ~3;
+}
+__host__ __device__ inline int epzs_flag_words(int bitmap_words) { return ((bitmap_words + 31) / 32 + 3) & ~3; }
+size_t epzs_map_words(bool grid, int max_qpel);   // bitmap + flags
 hipError_t launch_epzs(const EpzsParams &p, hipStream_t s);
 // The resident server's mailbox (JMME_SINGLE_MODE 3), in mapped pinned host
 // memory; each word the two sides exchange has a cache line to itself
@@ -68,8 +77,9 @@ struct alignas(64) EpzsBox {
   uint32_t quit, pad1[15];    // host: 1 = the server exits at its next poll
   uint32_t done, pad2[15];    // server: the number it served, after its results and a system fence
   uint32_t alive, pad3[15];   // host: 1 before a launch; server: 0 as its last store
-  uint32_t service, copy, search, pad4[13];   // server: the request's time from its number seen to its results
-                                              // stored, to its copy in LDS, to the search's end (10 ns ticks)
+  uint32_t service, copy, search, ph[5], pad4[8];   // server: the request's time from its number seen to its
+                                              // results stored, to its copy in LDS, to the search's end, and
+                                              // the search's phases (10 ns ticks)
   EpzsParams p;               // the request: a fused search alone (fused = 1, one = its lists)
 };
 hipError_t launch_epzs_server(EpzsBox *d_box, bool grid, bool hbd, int map_words, uint32_t last, uint32_t idle_ticks,
