@@ -2286,7 +2286,7 @@ extern "C" int jmme_subpel_refine_async(jmme_ctx *ctx, const jmme_subpel_req *d_
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (prepare_subs(ctx, s)) return -1;
   const SubGeom g = sub_geom(ctx->width, ctx->height);
-  SubpelParams p;
+  SubpelParams p{};
   p.cur = ctx->d_cur;
   p.cur_pitch = ctx->pitch;
   p.width = ctx->width;

@@ -444,7 +444,7 @@ __device__ jmme_block_res search_one(const EpzsParams &p, const jmme_epzs_req &q
       bool dup = inr && test_cell(s, cell);
       const int cnt = min(64, q.n_pred - base);
       for (int j = 0; j < cnt - 1; ++j) {   // an earlier predictor of this chunk on the same cell
-        const int cj = __shfl(cell, j, 64);
+        const int cj = __builtin_amdgcn_readlane(cell, j);   // (j is uniform: a scalar read, no LDS round trip)
         dup |= j < lane && cj == cell;
       }
       const bool eval = inr && !dup;
