@@ -139,7 +139,8 @@ struct jmme_ctx {
   long long srv_launches = 0, srv_served = 0;
   double srv_service_us = 0;                 // JMME_PHASES: the server's own time per request, summed
   double srv_copy_us = 0, srv_search_us = 0; // (to the request's copy in LDS, to the search's end)
-  double srv_ph_us[5] = {};                  // (the search's phases: set-up, centre, predictors, walk, visited)
+  double srv_ph_us[8] = {};                  // (the search's phases: set-up, centre, predictors, walk, visited
+                                             //  (its word list); the refinement's window and phases)
   bool srv_check = false;                    // JMME_EPZS_SERVER_CHECK: every served search again by the fused kernel
   uint8_t *h_chk = nullptr;                  // (its outputs, mapped pinned)
   long long srv_mismatch = 0;
@@ -416,9 +417,11 @@ extern "C" void jmme_destroy(jmme_ctx *ctx) {
             ctx->srv_search_us / std::max(1ll, ctx->srv_served));
   if (ctx->phases && ctx->srv_served)
     fprintf(stderr, "jmme EPZS server search phases (us): set-up %.2f, centre %.2f, predictors %.2f, walk %.2f, "
-            "visited %.2f\n", ctx->srv_ph_us[0] / ctx->srv_served, ctx->srv_ph_us[1] / ctx->srv_served,
+            "visited %.2f (word list %.2f); refinement: window %.2f, phases %.2f\n",
+            ctx->srv_ph_us[0] / ctx->srv_served, ctx->srv_ph_us[1] / ctx->srv_served,
             ctx->srv_ph_us[2] / ctx->srv_served, ctx->srv_ph_us[3] / ctx->srv_served,
-            ctx->srv_ph_us[4] / ctx->srv_served);
+            ctx->srv_ph_us[4] / ctx->srv_served, ctx->srv_ph_us[5] / ctx->srv_served,
+            ctx->srv_ph_us[6] / ctx->srv_served, ctx->srv_ph_us[7] / ctx->srv_served);
   if (ctx->srv_check) fprintf(stderr, "jmme EPZS server check: %lld mismatches\n", ctx->srv_mismatch);
   if (ctx->phases && (ctx->ep_n[0] || ctx->ep_n[1]))
     fprintf(stderr, "jmme EPZS calls: %lld alone, %.1f ms (%.2f us each); %lld batches, %.1f ms\n", ctx->ep_n[0],
@@ -1488,6 +1491,22 @@ int build_epzs_params(jmme_ctx *ctx, EpzsParams &p, const jmme_epzs_req *d_req, 
   return 0;
 }
 
+// the request built in box->p, posted as box->req's chunks: three dwords of it
+// and the request number in each 16-byte store (one x86 store each), so a chunk
+// the server reads is never half old, half new
+static void post_request(EpzsBox *box, uint32_t seq) {
+  typedef uint32_t v4u __attribute__((vector_size(16)));
+  const uint32_t *src = reinterpret_cast<const uint32_t *>(&box->p);
+  constexpr int kDw = (int)(sizeof(EpzsParams) / 4);
+  for (int i = 0; i < kEpzsReqChunks; ++i) {
+    v4u c;
+    for (int k = 0; k < 3; ++k) c[k] = 3 * i + k < kDw ? src[3 * i + k] : 0u;
+    c[3] = seq;
+    *reinterpret_cast<volatile v4u *>(&box->req[i]) = c;
+  }
+  __atomic_store_n(&box->seq, seq, __ATOMIC_RELEASE);
+}
+
 // JMME_SINGLE_MODE 3: a fused search alone handed to the resident server.
 // (Re)launches it when it is not running -- first use, stopped by another
 // entry point, or gone after its idle time -- and waits for the request's
@@ -1530,7 +1549,7 @@ int epzs_serve(jmme_ctx *ctx, const jmme_epzs_req *d_req, const int16_t *d_preds
     return 0;
   };
   if (!ctx->srv_running && start()) return -1;
-  __atomic_store_n(&box->seq, seq, __ATOMIC_RELEASE);
+  post_request(box, seq);
   auto t0 = std::chrono::steady_clock::now();
   for (unsigned spin = 1; __atomic_load_n(&box->done, __ATOMIC_ACQUIRE) != seq; ++spin) {
     if ((spin & 63u) == 0 && __atomic_load_n(&box->alive, __ATOMIC_ACQUIRE) == 0) {
@@ -1552,7 +1571,7 @@ int epzs_serve(jmme_ctx *ctx, const jmme_epzs_req *d_req, const int16_t *d_preds
     ctx->srv_service_us += 0.01 * box->service;
     ctx->srv_copy_us += 0.01 * box->copy;
     ctx->srv_search_us += 0.01 * box->search;
-    for (int i = 0; i < 5; ++i) ctx->srv_ph_us[i] += 0.01 * box->ph[i];
+    for (int i = 0; i < 8; ++i) ctx->srv_ph_us[i] += 0.01 * box->ph[i];
   }
   return 0;
 }

@@ -73,15 +73,19 @@ hipError_t launch_epzs(const EpzsParams &p, hipStream_t s);
 // The resident server's mailbox (JMME_SINGLE_MODE 3), in mapped pinned host
 // memory; each word the two sides exchange has a cache line to itself
 struct alignas(64) EpzsBox {
-  uint32_t seq, pad0[15];     // host: the request number, stored (release) after p
+  uint32_t seq, pad0[15];     // host: the request number (the server reads it from req[])
   uint32_t quit, pad1[15];    // host: 1 = the server exits at its next poll
   uint32_t done, pad2[15];    // server: the number it served, after its results and a system fence
   uint32_t alive, pad3[15];   // host: 1 before a launch; server: 0 as its last store
-  uint32_t service, copy, search, ph[5], pad4[8];   // server: the request's time from its number seen to its
+  uint32_t service, copy, search, ph[8], pad4[5];   // server: the request's time from its number seen to its
                                               // results stored, to its copy in LDS, to the search's end, and
-                                              // the search's phases (10 ns ticks)
-  EpzsParams p;               // the request: a fused search alone (fused = 1, one = its lists)
+                                              // the search's phases and the refinement's window
+                                              // load and phases (10 ns ticks)
+  EpzsParams p;               // host: the request is built here (a fused search alone: fused = 1, one = its
+                              // lists), then written to req[] -- the server reads req[] only
+  uint4 req[(sizeof(EpzsParams) / 4 + 2) / 3];   // host: p as chunks (three dwords of p, then the request number)
 };
+constexpr int kEpzsReqChunks = (int)((sizeof(EpzsParams) / 4 + 2) / 3);
 hipError_t launch_epzs_server(EpzsBox *d_box, bool grid, bool hbd, int map_words, uint32_t last, uint32_t idle_ticks,
                               unsigned long long life_ticks, hipStream_t s);
 

@@ -2375,7 +2375,7 @@ __device__ __forceinline__ void chain_subpel_phase(const ChainParams &p, const T
     const int cnd = tid >> lg_nb, b = tid & ((1 << lg_nb) - 1), pos = p0 + cnd;
     const int bxo = (b & ((1 << lg_nbx) - 1)) * 4, byo = (b >> lg_nbx) * 4;
     const int s = spd::job_sum(sub, p.plane_stride, p.sub_pitch, org, p.pitch, ymax, xmax, metric, false,
-                               mx + sc * spd::kSpiral9[pos][0], my + sc * spd::kSpiral9[pos][1], bxo, byo);
+                               mx + sc * spd::spiral_x(pos), my + sc * spd::spiral_y(pos), bxo, byo);
     atomicAdd(&sums[cnd], s);
   }
 }
@@ -2399,14 +2399,14 @@ __device__ __forceinline__ jmme_block_res chain_subpel(const ChainParams &p, con
     __syncthreads();
     int best = 0;
     for (int pos = p0; pos < p1; ++pos) {
-      const int cx = mvx + 2 * spd::kSpiral9[pos][0], cy = mvy + 2 * spd::kSpiral9[pos][1];
+      const int cx = mvx + 2 * spd::spiral_x(pos), cy = mvy + 2 * spd::spiral_y(pos);
       int64_t mcost = spd::mv_cost(sp.lambda_h, cx, cy, px, py);
       if (mcost >= min_mcost) continue;
       mcost += spd::dist(sums[0][pos - p0], min_mcost - mcost);
       if (pos == 0 && chk0) mcost -= (int64_t)sp.lambda_h * 16;   // weighted_cost(lambda_factor, 16)
       if (mcost < min_mcost) { min_mcost = mcost; best = pos; }
     }
-    if (best) { mvx += 2 * spd::kSpiral9[best][0]; mvy += 2 * spd::kSpiral9[best][1]; }
+    if (best) { mvx += 2 * spd::spiral_x(best); mvy += 2 * spd::spiral_y(best); }
   }
   if (!sp.start_qp) min_mcost = spd::kDistMax;
   // quarter-pel ring (me_fullsearch.c:252-285)
@@ -2416,13 +2416,13 @@ __device__ __forceinline__ jmme_block_res chain_subpel(const ChainParams &p, con
     __syncthreads();
     int best = 0;
     for (int pos = p0; pos < p1; ++pos) {
-      const int cx = mvx + spd::kSpiral9[pos][0], cy = mvy + spd::kSpiral9[pos][1];
+      const int cx = mvx + spd::spiral_x(pos), cy = mvy + spd::spiral_y(pos);
       int64_t mcost = spd::mv_cost(sp.lambda_q, cx, cy, px, py);
       if (mcost >= min_mcost) continue;
       mcost += spd::dist(sums[1][pos - p0], min_mcost - mcost);
       if (mcost < min_mcost) { min_mcost = mcost; best = pos; }
     }
-    if (best) { mvx += spd::kSpiral9[best][0]; mvy += spd::kSpiral9[best][1]; }
+    if (best) { mvx += spd::spiral_x(best); mvy += spd::spiral_y(best); }
   }
   jmme_block_res o;
   o.mv_x = (int16_t)mvx; o.mv_y = (int16_t)mvy; o.reserved = 0; o.cost = min_mcost;

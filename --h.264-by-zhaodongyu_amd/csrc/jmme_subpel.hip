@@ -36,7 +36,7 @@
 #include "jmme.h"
 #include "jmme_common.h"
 #include "jmme_subpel_internal.h"
-#include "jmme_subpel_dev.h"
+#include "jmme_refine_dev.h"
 
 #ifndef JMME_INTERP_ROWS
 #define JMME_INTERP_ROWS 3   // (2: 13.7-14.2 us, 3: 11.6, 4: 12.8-13.0, 5: 12.0, 6: 13.0, 8: 15.2 us per 1080p reference)
@@ -46,7 +46,7 @@ namespace jmme {
 
 namespace {
 
-using namespace spd;   // kDistMax, kPad*, kSpiral9, mv_cost, job_sum, dist, blk_size (jmme_subpel_dev.h)
+using namespace spd;   // kDistMax, kPad*, spiral_x/y, mv_cost, job_sum, dist, blk_size (jmme_subpel_dev.h)
 
 __device__ __forceinline__ int clipv(int v, int maxv) { return min(max(v, 0), maxv); }   // iClip1(max_imgpel_value)
 __device__ __forceinline__ int avg2(int a, int b) { return (a + b + 1) >> 1; }   // rshift_rnd_sf(a + b, 1)

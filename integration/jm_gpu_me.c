@@ -1461,6 +1461,8 @@ static int g_ep_pcap = 0;
 static long long g_ep_hits = 0, g_ep_batches = 0, g_ep_singles = 0, g_ep_guesses = 0, g_ep_direct = 0;
 static long long g_ep_fail_bounds = 0, g_ep_fail_stale = 0, g_ep_fail_inputs = 0, g_ep_sp_hits = 0, g_ep_overflow = 0;
 static double g_t_ep_build = 0;
+static double g_t_ep_run = 0, g_t_ep_runlib = 0, g_t_ep_p2 = 0, g_t_ep_lookup = 0;   /* host clocks (reported at exit) */
+static long long g_ep_lookups = 0;
 static long long g_ep_miss_slot[JMME_NSLOT], g_ep_list_diff[JMME_NSLOT];   /* misses inside a batch, by slot */
 /* JMME_EPZS_TRACE: misses inside a batch by kind -- [0] no way with these inputs, [1] the stop criterion
  * outside every equal way's interval, [2] prevSad outside, [3] map cells; and the stop misses by
@@ -1711,6 +1713,7 @@ static void ep_add(int k, const ep_in *e, int pos_x, int pos_y, EPZSParameters *
 static void ep_run_from(int k0, int n, const int16_t *stale, int n_stale, unsigned gen)
 {
   int k;
+  double t0 = now_us(), t1;
   if (k0 >= n) return;
   g_ep_q[k0].n_stale = k0 == 0 ? n_stale : 0;
   for (k = k0; k < n; k++) g_ep_spo[k].mv_x = g_ep_spo[k].mv_y = 0, g_ep_spo[k].cost = 0, g_ep_spo[k].reserved = 0;
@@ -1718,6 +1721,8 @@ static void ep_run_from(int k0, int n, const int16_t *stale, int n_stale, unsign
                           g_ep_res + k0, g_ep_bnd + k0, g_ep_vbuf + 2 * (size_t)EP_MAXV * k0, EP_MAXV, g_ep_spq + k0,
                           g_ep_spo + k0))
     fail_jm("jmme_epzs_speculate");
+  t1 = now_us();
+  g_t_ep_runlib += t1 - t0;
   for (k = k0; k < n; k++) {
     ep_ans *a = &g_ep_ans[k];
     const int16_t *pp = g_ep_ppool + 2 * (size_t)g_ep_q[k].pred_off;
@@ -1734,6 +1739,7 @@ static void ep_run_from(int k0, int n, const int16_t *stale, int n_stale, unsign
     }
     a->sp_res = g_ep_spo[k];
   }
+  g_t_ep_run += now_us() - t0;
 }
 
 static void ep_run(int n, const int16_t *stale, int n_stale, unsigned gen) { ep_run_from(0, n, stale, n_stale, gen); }
@@ -1754,6 +1760,17 @@ static int g_ep_vcols = 0;
 static long long g_ep_pass2 = 0, g_ep_pass2_batches = 0;
 static long long g_ep_list_fixes = 0;   /* second-pass guesses whose list was rebuilt from this batch's answers */
 static ep_in g_ep_fix;                  /* (a guess's inputs with its tail replaced) */
+
+/* *d = *e, the list only as far as it goes (a whole ep_in is ~0.7 KB: the passes copy one per way) */
+static void ep_copy_in(ep_in *d, const ep_in *e)
+{
+  d->q = e->q;
+  memcpy(d->pred, e->pred, (size_t)e->q.n_pred * 4);
+  memcpy(d->cond, e->cond, (size_t)e->q.n_pred);
+  d->mb = e->mb;
+  d->gen = e->gen;
+  d->bt_start = e->bt_start;
+}
 
 static int ep_avail_c(int bx, int by, int bsx)   /* get_neighbors' upper-right rule inside the MB (mv_search.c:283-301) */
 {
@@ -1986,7 +2003,7 @@ static void ep_pass2(Macroblock *currMB, int mb0, int s0, int nmb, unsigned gen,
           if (idx[w] == 0 && x == mb0 && t == s0) continue;   /* the real call */
           const int shaped = np >= 5 && me >= 5 && me <= bs && bs <= np;   /* (else: only the stop replay) */
           /* rebuild: spatial [0, 5) | spatial memory [5, me) | temporal + window [me, bs) | block type [bs, np) */
-          if (shaped) g_ep_fix = a->in;
+          if (shaped) ep_copy_in(&g_ep_fix, &a->in);
           tp = (int16_t *)g_ep_fix.pred;
           o = 5;
           if (shaped) {
@@ -2136,10 +2153,12 @@ static const ep_ans *ep_miss(Macroblock *currMB, MEBlock *mv_block, const jmme_e
     }
     memset(g_ep_alt, 0xff, (size_t)nmb * JMME_NSLOT * sizeof(int));
     g_ep_alt_on = 0;
+    t0 = now_us();
     ep_pass2(currMB, mb, ep_slot_of(q), nmb, gen, &n, 0);
     g_ep_alt_on = 1;   /* third pass: the same replay on the second pass's answers */
     ep_pass2(currMB, mb, ep_slot_of(q), nmb, gen, &n, 1);
     g_ep_alt_on = 0;
+    g_t_ep_p2 += now_us() - t0;
   }
   g_ep_n = n;
   g_ep_mb0 = mb;
@@ -2269,7 +2288,9 @@ static distblk epzs_gpu(int variant, Macroblock *currMB, MotionVector *pred_mv, 
   const ep_ans *a = NULL;
   if (ep_speculating(currMB, cur_list, ref, n_pred)) {
     /* the speculative path: a cached answer whose inputs are this call's, or a batch */
+    t1 = g_ep_trace ? now_us() : 0.0;
     a = ep_lookup(currMB, mv_block, &q, g_ep_pred, g_ep_cond, g_ep_stale, n_stale);
+    if (g_ep_trace) { g_t_ep_lookup += now_us() - t1; ++g_ep_lookups; }
     if (!a) {   /* (hits are not timed: two clock reads per call were a tenth of the hits' cost) */
       t1 = now_us();
       a = ep_miss(currMB, mv_block, &q, g_ep_pred, g_ep_cond, g_ep_stale, n_stale);
@@ -2445,6 +2466,10 @@ static void report(void)
                       "%lld second-pass guesses in %lld launches (%lld with lists rebuilt from the batch's answers)\n",
               g_ep_hits, g_ep_batches, g_ep_guesses, g_ep_singles, g_ep_direct, g_ep_fail_inputs, g_ep_fail_bounds,
               g_ep_fail_stale, g_t_ep_build * 1e-3, g_ep_overflow, g_ep_pass2, g_ep_pass2_batches, g_ep_list_fixes);
+    if (g_epzs_calls && g_ep_batches)
+      fprintf(stderr, "jm_gpu_me: EPZS host clocks: %.1f ms running guesses (%.1f ms of it in the library), %.1f ms in the "
+                      "second and third passes (with their runs), %.1f ms in %lld lookups (JMME_EPZS_TRACE=1 only)\n",
+              g_t_ep_run * 1e-3, g_t_ep_runlib * 1e-3, g_t_ep_p2 * 1e-3, g_t_ep_lookup * 1e-3, g_ep_lookups);
     if (g_ep_trace) {
       int sl;
       fprintf(stderr, "jm_gpu_me: EPZS misses inside batches by slot (list-only differences):");

@@ -44,7 +44,7 @@ def main():
                 ok = g["md5"] == cpu["md5"]
                 res[mode].append(round(g["me_s"] * 1e3, 1))
                 print(json.dumps({"mode": mode, "rep": r, "me_ms": res[mode][-1], "byte_identical": ok,
-                                  "epzs": g.get("epzs"), "spec": g.get("epzs_speculation")}), flush=True)
+                                  "epzs": g.get("epzs"), "spec": g.get("epzs_speculation"), "lib": g.get("lib_clocks")}), flush=True)
                 if not ok:
                     sys.exit(1)
     print(json.dumps({"stock_me_ms": round(cpu["me_s"] * 1e3, 1), "mode2_me_ms": res["2"], "mode3_me_ms": res["3"]}))

@@ -255,6 +255,10 @@ def _lencod(binary, d, tag, yuv, w, h, frames, params, cfg_text, env=None):
         res["epzs_speculation"] = dict(zip(("answered_from_batches", "batches", "guesses", "searched_alone",
                                             "not_speculated", "refused_inputs", "refused_bounds", "refused_cells"),
                                            map(int, spec.groups()[:8])), build_ms=float(spec.group(9)))
+    # JMME_PHASES=1: the library's own clocks (server phases, calls by kind), as printed
+    lib_lines = [ln for ln in r.stderr.splitlines() if ln.startswith(("jmme EPZS", "jm_gpu_me: EPZS misses", "jm_gpu_me: EPZS host"))]
+    if lib_lines:
+        res["lib_clocks"] = lib_lines
     return res
 
 
