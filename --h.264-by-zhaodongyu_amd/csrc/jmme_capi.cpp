@@ -139,7 +139,7 @@ struct jmme_ctx {
   long long srv_launches = 0, srv_served = 0;
   double srv_service_us = 0;                 // JMME_PHASES: the server's own time per request, summed
   double srv_copy_us = 0, srv_search_us = 0; // (to the request's copy in LDS, to the search's end)
-  double srv_ph_us[8] = {};                  // (the search's phases: set-up, centre, predictors, walk, visited
+  double srv_ph_us[10] = {};                  // (the search's phases: set-up, centre, predictors, walk, visited
                                              //  (its word list); the refinement's window and phases)
   bool srv_check = false;                    // JMME_EPZS_SERVER_CHECK: every served search again by the fused kernel
   uint8_t *h_chk = nullptr;                  // (its outputs, mapped pinned)
@@ -417,11 +417,13 @@ extern "C" void jmme_destroy(jmme_ctx *ctx) {
             ctx->srv_search_us / std::max(1ll, ctx->srv_served));
   if (ctx->phases && ctx->srv_served)
     fprintf(stderr, "jmme EPZS server search phases (us): set-up %.2f, centre %.2f, predictors %.2f, walk %.2f, "
-            "visited %.2f (word list %.2f); refinement: window %.2f, phases %.2f\n",
+            "visited %.2f (word list %.2f); refinement: window %.2f, phases %.2f; predictor rounds (summed over all "
+            "searches / searches): set-up %.2f, costs %.2f\n",
             ctx->srv_ph_us[0] / ctx->srv_served, ctx->srv_ph_us[1] / ctx->srv_served,
             ctx->srv_ph_us[2] / ctx->srv_served, ctx->srv_ph_us[3] / ctx->srv_served,
             ctx->srv_ph_us[4] / ctx->srv_served, ctx->srv_ph_us[5] / ctx->srv_served,
-            ctx->srv_ph_us[6] / ctx->srv_served, ctx->srv_ph_us[7] / ctx->srv_served);
+            ctx->srv_ph_us[6] / ctx->srv_served, ctx->srv_ph_us[7] / ctx->srv_served, ctx->srv_ph_us[8] / ctx->srv_served,
+            ctx->srv_ph_us[9] / ctx->srv_served);
   if (ctx->srv_check) fprintf(stderr, "jmme EPZS server check: %lld mismatches\n", ctx->srv_mismatch);
   if (ctx->phases && (ctx->ep_n[0] || ctx->ep_n[1]))
     fprintf(stderr, "jmme EPZS calls: %lld alone, %.1f ms (%.2f us each); %lld batches, %.1f ms\n", ctx->ep_n[0],
@@ -1571,7 +1573,7 @@ int epzs_serve(jmme_ctx *ctx, const jmme_epzs_req *d_req, const int16_t *d_preds
     ctx->srv_service_us += 0.01 * box->service;
     ctx->srv_copy_us += 0.01 * box->copy;
     ctx->srv_search_us += 0.01 * box->search;
-    for (int i = 0; i < 8; ++i) ctx->srv_ph_us[i] += 0.01 * box->ph[i];
+    for (int i = 0; i < 10; ++i) ctx->srv_ph_us[i] += 0.01 * box->ph[i];
   }
   return 0;
 }

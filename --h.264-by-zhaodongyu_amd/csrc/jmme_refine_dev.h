@@ -380,6 +380,19 @@ __device__ void tile_phase(const SubpelParams &p, TileLds<T> &W, int lane, int b
   wave_sync();
 }
 
+// a wave-uniform copy of v (lane 0's), dword by dword into SGPRs
+template <typename S>
+__device__ __forceinline__ S uni(const S &v) {
+  static_assert(sizeof(S) % 4 == 0, "whole dwords");
+  uint32_t w[sizeof(S) / 4];
+  __builtin_memcpy(w, &v, sizeof(S));
+#pragma unroll
+  for (int k = 0; k < (int)(sizeof(S) / 4); ++k) w[k] = (uint32_t)__builtin_amdgcn_readfirstlane((int)w[k]);
+  S r;
+  __builtin_memcpy(&r, w, sizeof(S));
+  return r;
+}
+
 // One wave's refinements: lane k < p.per_wave owns request i0 + k (the body of
 // subpel_kernel; the EPZS kernel's fused single-search path calls it with
 // per_wave = 1, its own answer as ir_one and its request staged in LDS as req_one).
@@ -390,17 +403,22 @@ __device__ __forceinline__ void refine_wave(const SubpelParams &p, WaveLds<T> &L
                                             const jmme_block_res *ir_one = nullptr,
                                             const jmme_subpel_req *req_one = nullptr, TileLds<T> *W = nullptr) {
   const int i = i0 + lane;
-  // owner lanes: lane k < 16 holds request i0 + k; inactive owners ask for nothing
+  // owner lanes: lane k < 16 holds request i0 + k; inactive owners ask for nothing.
+  // With a window (one request), every lane holds it, read into SGPRs: the folds
+  // below are then scalar code with scalar branches, not one lane's VALU chain
   jmme_subpel_req q{};
   bool act = false;
-  if (lane < p.per_wave && i < p.n) {
+  if constexpr (TILE) {
+    q = uni(*req_one);
+    act = i0 < p.n && q.blocktype >= 1 && q.blocktype <= 7;
+  } else if (lane < p.per_wave && i < p.n) {
     q = req_one ? *req_one : p.req[i];
     act = q.blocktype >= 1 && q.blocktype <= 7;
   }
   int mvx = q.mv_x, mvy = q.mv_y;
   int64_t min_mcost = q.min_mcost;
   if (act && (ir_one || p.int_res)) {
-    const jmme_block_res ir = ir_one ? *ir_one : p.int_res[i];
+    const jmme_block_res ir = TILE ? uni(*ir_one) : ir_one ? *ir_one : p.int_res[i];
     mvx = ir.mv_x;
     mvy = ir.mv_y;
     min_mcost = q.start_hp ? (int64_t)ir.cost : kDistMax;
@@ -417,7 +435,11 @@ __device__ __forceinline__ void refine_wave(const SubpelParams &p, WaveLds<T> &L
   const int pxp = q.pos_x << 2, pyp = q.pos_y << 2;   // pos_x_padded (mv_search.c:685-686)
   const int px = q.pred_x, py = q.pred_y;
   const bool epzs = q.variant == 1;
-  const int *sums = TILE ? W->sums : L.sums[lane < kK ? lane : 0];
+  const int *sums_p = TILE ? W->sums : L.sums[lane < kK ? lane : 0];
+  auto sums = [&](int k) -> int {   // a phase's sum of candidate k (a scalar with a window)
+    if constexpr (TILE) return __builtin_amdgcn_readfirstlane(sums_p[k]);
+    else return sums_p[k];
+  };
   // a phase: the 16-per-wave form, or lane 0's request from its window
   auto phase = [&](int a0, int a1, int metric, bool t8v, int sc, int tab, int mx, int my) {
     if constexpr (TILE) {
@@ -446,7 +468,7 @@ __device__ __forceinline__ void refine_wave(const SubpelParams &p, WaveLds<T> &L
         const int ox = tab_x(epzs, pos), oy = tab_y(epzs, pos);
         const int cx = mvx + 2 * ox, cy = mvy + 2 * oy;
         int64_t mcost = mv_cost(lambda, cx, cy, px, py);
-        const int sm = sums[pos - q.start_hp];
+        const int sm = sums(pos - q.start_hp);
         if (!epzs) {
           if (mcost >= min_mcost) continue;
           mcost += dist(sm, min_mcost - mcost);
@@ -481,7 +503,7 @@ __device__ __forceinline__ void refine_wave(const SubpelParams &p, WaveLds<T> &L
         const int cx = mvx + 2 * ept_x(pos), cy = mvy + 2 * ept_y(pos);
         int64_t mcost = mv_cost(lambda, cx, cy, px, py);
         if (mcost < min_mcost) {
-          mcost += dist(sums[pos - s0], min_mcost - mcost);
+          mcost += dist(sums(pos - s0), min_mcost - mcost);
           if (mcost < min_mcost) { min_mcost = mcost; best_pos = pos; }
         }
       }
@@ -509,7 +531,7 @@ __device__ __forceinline__ void refine_wave(const SubpelParams &p, WaveLds<T> &L
         const int ox = tab_x(epzs, pos), oy = tab_y(epzs, pos);
         const int cx = mvx + ox, cy = mvy + oy;
         int64_t mcost = mv_cost(lambda, cx, cy, px, py);
-        const int sm = sums[pos - q.start_qp];
+        const int sm = sums(pos - q.start_qp);
         if (!epzs) {
           if (mcost >= min_mcost) continue;
           mcost += dist(sm, min_mcost - mcost);
@@ -545,14 +567,14 @@ __device__ __forceinline__ void refine_wave(const SubpelParams &p, WaveLds<T> &L
         const int cx = mvx + ept_x(pos), cy = mvy + ept_y(pos);
         int64_t mcost = mv_cost(lambda, cx, cy, px, py);
         if (mcost < min_mcost) {
-          mcost += dist(sums[pos - s0], min_mcost - mcost);
+          mcost += dist(sums(pos - s0), min_mcost - mcost);
           if (mcost < min_mcost) { min_mcost = mcost; best_pos = pos; }
         }
       }
     }
     if (act && epzs && !early && best_pos > 0) { mvx += ept_x(best_pos); mvy += ept_y(best_pos); }
   }
-  if (act) {
+  if (act && (!TILE || lane == 0)) {
     jmme_block_res r;
     r.mv_x = (int16_t)mvx;
     r.mv_y = (int16_t)mvy;

@@ -1470,6 +1470,7 @@ static long long g_ep_miss_slot[JMME_NSLOT], g_ep_list_diff[JMME_NSLOT];   /* mi
 static long long g_ep_miss_kind[4], g_ep_stop_off[24];
 static int g_ep_trace = 0;   /* JMME_EPZS_TRACE=1: per-slot miss counts at exit */
 static int g_ep_two_pass = 1;   /* JMME_EPZS_PASS2=0: no second pass (ep_pass2) */
+static int g_ep_third = 1;      /* JMME_EPZS_PASS3=0: no third pass (the rebuild repeated on the second pass's answers) */
 static int g_ep_dump = 0;       /* JMME_EPZS_DUMP=n: print the first n input misses (measurement) */
 
 static int ep_speculating(Macroblock *currMB, int cur_list, int ref, int n_pred)
@@ -1479,8 +1480,9 @@ static int ep_speculating(Macroblock *currMB, int cur_list, int ref, int n_pred)
     g_ep_spec = !(e && e[0] == '0');
     g_ep_trace = tr && tr[0] == '1';
     {
-      const char *p2 = getenv("JMME_EPZS_PASS2");
+      const char *p2 = getenv("JMME_EPZS_PASS2"), *p3 = getenv("JMME_EPZS_PASS3");
       g_ep_two_pass = !(p2 && p2[0] == '0');
+      g_ep_third = !(p3 && p3[0] == '0');
       const char *dp = getenv("JMME_EPZS_DUMP");
       g_ep_dump = dp ? atoi(dp) : 0;
     }
@@ -2155,9 +2157,11 @@ static const ep_ans *ep_miss(Macroblock *currMB, MEBlock *mv_block, const jmme_e
     g_ep_alt_on = 0;
     t0 = now_us();
     ep_pass2(currMB, mb, ep_slot_of(q), nmb, gen, &n, 0);
-    g_ep_alt_on = 1;   /* third pass: the same replay on the second pass's answers */
-    ep_pass2(currMB, mb, ep_slot_of(q), nmb, gen, &n, 1);
-    g_ep_alt_on = 0;
+    if (g_ep_third) {
+      g_ep_alt_on = 1;   /* third pass: the same replay on the second pass's answers */
+      ep_pass2(currMB, mb, ep_slot_of(q), nmb, gen, &n, 1);
+      g_ep_alt_on = 0;
+    }
     g_t_ep_p2 += now_us() - t0;
   }
   g_ep_n = n;

@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--idle-us", type=int, default=2000)
     ap.add_argument("--size", default="1920x1080")
+    ap.add_argument("--b-env", default=None, help="NAME=VALUE: compare the server (mode 3) without and with this "
+                                                   "variable instead of mode 2 against mode 3")
     a = ap.parse_args()
     from bench_blocks import _lencod, dropin_modes
     from jmme import synth
@@ -40,6 +42,11 @@ def main():
         for r in range(a.reps):
             for mode in ("2", "3"):
                 env = {"JMME_SINGLE_MODE": mode, "JMME_EPZS_SERVER_IDLE_US": str(a.idle_us)}
+                if a.b_env:   # arm "2" becomes: the server with the extra variable
+                    env["JMME_SINGLE_MODE"] = "3"
+                    if mode == "2":
+                        k, v = a.b_env.split("=", 1)
+                        env[k] = v
                 g = _lencod(gpu, d, f"gpu_{mode}_{r}", yuv, w, h, frames, params, CFG, env)
                 ok = g["md5"] == cpu["md5"]
                 res[mode].append(round(g["me_s"] * 1e3, 1))
