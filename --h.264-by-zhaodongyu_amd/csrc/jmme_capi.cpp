@@ -138,6 +138,10 @@ struct jmme_ctx {
   uint32_t srv_idle_ticks = 200000;          // 2 ms at s_memrealtime's 100 MHz (JMME_EPZS_SERVER_IDLE_US)
   long long srv_launches = 0, srv_served = 0;
   double srv_service_us = 0;                 // JMME_PHASES: the server's own time per request, summed
+  double srv_host_us[4] = {};                // JMME_PHASES: a search alone on the host -- call entry to the
+                                             // server hand-off, hand-off to posted, posted to done, done to return
+  double srv_t_call = 0, srv_t_post = 0, srv_t_done = 0;
+  double srv_cycles = 0;                     // JMME_PHASES: s_memtime ticks over the requests' service, summed
   double srv_copy_us = 0, srv_search_us = 0; // (to the request's copy in LDS, to the search's end)
   double srv_ph_us[10] = {};                  // (the search's phases: set-up, centre, predictors, walk, visited
                                              //  (its word list); the refinement's window and phases)
@@ -424,6 +428,12 @@ extern "C" void jmme_destroy(jmme_ctx *ctx) {
             ctx->srv_ph_us[4] / ctx->srv_served, ctx->srv_ph_us[5] / ctx->srv_served,
             ctx->srv_ph_us[6] / ctx->srv_served, ctx->srv_ph_us[7] / ctx->srv_served, ctx->srv_ph_us[8] / ctx->srv_served,
             ctx->srv_ph_us[9] / ctx->srv_served);
+  if (ctx->phases && ctx->srv_served)
+    fprintf(stderr, "jmme EPZS server host side (us per search): call to hand-off %.2f, hand-off to posted %.2f, "
+            "posted to done %.2f, done to return %.2f; shader clock while serving %.0f MHz\n",
+            ctx->srv_host_us[0] / ctx->srv_served,
+            ctx->srv_host_us[1] / ctx->srv_served, ctx->srv_host_us[2] / ctx->srv_served,
+            ctx->srv_host_us[3] / ctx->srv_served, ctx->srv_cycles / std::max(1e-9, ctx->srv_service_us));
   if (ctx->srv_check) fprintf(stderr, "jmme EPZS server check: %lld mismatches\n", ctx->srv_mismatch);
   if (ctx->phases && (ctx->ep_n[0] || ctx->ep_n[1]))
     fprintf(stderr, "jmme EPZS calls: %lld alone, %.1f ms (%.2f us each); %lld batches, %.1f ms\n", ctx->ep_n[0],
@@ -1516,6 +1526,7 @@ static void post_request(EpzsBox *box, uint32_t seq) {
 int epzs_serve(jmme_ctx *ctx, const jmme_epzs_req *d_req, const int16_t *d_preds, const uint8_t *d_cond,
                const int16_t *d_stale, jmme_epzs_res *d_out, int16_t *d_vis, int max_visited,
                jmme_epzs_bounds *d_bnd, jmme_block_res *d_int, const EpzsOne &one, jmme_block_res *d_spo) {
+  const double t_in = ctx->phases ? now_us() : 0.0;
   if (!ctx->h_box) {
     HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_box), sizeof(EpzsBox), hipHostMallocMapped));
     std::memset(static_cast<void *>(ctx->h_box), 0, sizeof(EpzsBox));
@@ -1552,6 +1563,7 @@ int epzs_serve(jmme_ctx *ctx, const jmme_epzs_req *d_req, const int16_t *d_preds
   };
   if (!ctx->srv_running && start()) return -1;
   post_request(box, seq);
+  const double t_post = ctx->phases ? now_us() : 0.0;
   auto t0 = std::chrono::steady_clock::now();
   for (unsigned spin = 1; __atomic_load_n(&box->done, __ATOMIC_ACQUIRE) != seq; ++spin) {
     if ((spin & 63u) == 0 && __atomic_load_n(&box->alive, __ATOMIC_ACQUIRE) == 0) {
@@ -1570,7 +1582,12 @@ int epzs_serve(jmme_ctx *ctx, const jmme_epzs_req *d_req, const int16_t *d_preds
   }
   ++ctx->srv_served;
   if (ctx->phases) {
+    ctx->srv_t_done = now_us();
+    ctx->srv_host_us[0] += t_in - ctx->srv_t_call;
+    ctx->srv_host_us[1] += t_post - t_in;
+    ctx->srv_host_us[2] += ctx->srv_t_done - t_post;
     ctx->srv_service_us += 0.01 * box->service;
+    ctx->srv_cycles += box->cycles;
     ctx->srv_copy_us += 0.01 * box->copy;
     ctx->srv_search_us += 0.01 * box->search;
     for (int i = 0; i < 10; ++i) ctx->srv_ph_us[i] += 0.01 * box->ph[i];
@@ -1868,6 +1885,7 @@ extern "C" int jmme_epzs_speculate(jmme_ctx *ctx, const jmme_epzs_req *req, int 
   const int mode = fuse ? ctx->single_mode : 0;
   if (mode != 3 && server_stop(ctx)) return -1;
   if (mode == 3) {   // the resident server: no launch on the search's path
+    ctx->srv_t_call = ep_timer_.t0;
     const jmme_block_res spo0 = *h_spo;
     if (epzs_serve(ctx, d_req, d_preds, d_cond, d_stale, d_out, d_vis, max_visited, d_bnd, d_int, one, d_spo)) return -1;
     if (ctx->srv_check && epzs_serve_check(ctx, h_out, h_bnd, h_vis, h_spo, spo0, max_visited)) return -1;
@@ -1875,6 +1893,7 @@ extern "C" int jmme_epzs_speculate(jmme_ctx *ctx, const jmme_epzs_req *req, int 
     std::memcpy(bounds, h_bnd, sizeof(jmme_epzs_bounds));
     std::memcpy(visited, h_vis, (size_t)std::min(out[0].n_visited, max_visited) * 4);
     std::memcpy(sp_out, h_spo, sizeof(jmme_block_res));
+    if (ctx->phases) ctx->srv_host_us[3] += now_us() - ctx->srv_t_done;
     return 0;
   }
   if (mode >= 1 && !ctx->single_stream) HIPCHK(hipStreamCreateWithFlags(&ctx->single_stream, hipStreamNonBlocking));
