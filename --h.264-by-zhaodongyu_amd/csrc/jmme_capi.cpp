@@ -141,7 +141,8 @@ struct jmme_ctx {
   double srv_host_us[4] = {};                // JMME_PHASES: a search alone on the host -- call entry to the
                                              // server hand-off, hand-off to posted, posted to done, done to return
   double srv_t_call = 0, srv_t_post = 0, srv_t_done = 0;
-  double srv_cycles = 0;                     // JMME_PHASES: s_memtime ticks over the requests' service, summed
+  double srv_cycles = 0;
+  double srv_rph_us[6] = {};                 // JMME_PHASES: the refinement's phase ends and passes (from its window)                     // JMME_PHASES: s_memtime ticks over the requests' service, summed
   double srv_copy_us = 0, srv_search_us = 0; // (to the request's copy in LDS, to the search's end)
   double srv_ph_us[10] = {};                  // (the search's phases: set-up, centre, predictors, walk, visited
                                              //  (its word list); the refinement's window and phases)
@@ -434,6 +435,12 @@ extern "C" void jmme_destroy(jmme_ctx *ctx) {
             ctx->srv_host_us[0] / ctx->srv_served,
             ctx->srv_host_us[1] / ctx->srv_served, ctx->srv_host_us[2] / ctx->srv_served,
             ctx->srv_host_us[3] / ctx->srv_served, ctx->srv_cycles / std::max(1e-9, ctx->srv_service_us));
+  if (ctx->phases && ctx->srv_served)
+    fprintf(stderr, "jmme EPZS server refinement (us from its window, mean): phase A ends %.2f, B %.2f, C %.2f, D %.2f; "
+            "first pass ends %.2f, second %.2f\n", ctx->srv_rph_us[0] / ctx->srv_served,
+            ctx->srv_rph_us[1] / ctx->srv_served, ctx->srv_rph_us[2] / ctx->srv_served,
+            ctx->srv_rph_us[3] / ctx->srv_served, ctx->srv_rph_us[4] / ctx->srv_served,
+            ctx->srv_rph_us[5] / ctx->srv_served);
   if (ctx->srv_check) fprintf(stderr, "jmme EPZS server check: %lld mismatches\n", ctx->srv_mismatch);
   if (ctx->phases && (ctx->ep_n[0] || ctx->ep_n[1]))
     fprintf(stderr, "jmme EPZS calls: %lld alone, %.1f ms (%.2f us each); %lld batches, %.1f ms\n", ctx->ep_n[0],
@@ -1588,6 +1595,7 @@ int epzs_serve(jmme_ctx *ctx, const jmme_epzs_req *d_req, const int16_t *d_preds
     ctx->srv_host_us[2] += ctx->srv_t_done - t_post;
     ctx->srv_service_us += 0.01 * box->service;
     ctx->srv_cycles += box->cycles;
+    for (int i = 0; i < 6; ++i) ctx->srv_rph_us[i] += 0.01 * box->rph[i];
     ctx->srv_copy_us += 0.01 * box->copy;
     ctx->srv_search_us += 0.01 * box->search;
     for (int i = 0; i < 10; ++i) ctx->srv_ph_us[i] += 0.01 * box->ph[i];

@@ -77,7 +77,8 @@ struct alignas(64) EpzsBox {
   uint32_t quit, pad1[15];    // host: 1 = the server exits at its next poll
   uint32_t done, pad2[15];    // server: the number it served, after its results and a system fence
   uint32_t alive, pad3[15];   // host: 1 before a launch; server: 0 as its last store
-  uint32_t service, copy, search, ph[10], cycles, pad4[2];   // server: the request's time from its number seen to its
+  uint32_t service, copy, search, ph[10], cycles, pad4[2];
+  uint32_t rph[6], pad5[10];  // server: the refinement's phase ends A, B, C, D and its two passes (from its window)   // server: the request's time from its number seen to its
                                               // results stored, to its copy in LDS, to the search's end, and
                                               // the search's phases and the refinement's window
                                               // load and phases (10 ns ticks)

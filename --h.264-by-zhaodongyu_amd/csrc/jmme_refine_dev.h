@@ -401,7 +401,8 @@ __device__ __forceinline__ S uni(const S &v) {
 template <typename T, bool TILE = false>
 __device__ __forceinline__ void refine_wave(const SubpelParams &p, WaveLds<T> &L, int lane, int i0,
                                             const jmme_block_res *ir_one = nullptr,
-                                            const jmme_subpel_req *req_one = nullptr, TileLds<T> *W = nullptr) {
+                                            const jmme_subpel_req *req_one = nullptr, TileLds<T> *W = nullptr,
+                                            unsigned long long *stamps = nullptr) {
   const int i = i0 + lane;
   // owner lanes: lane k < 16 holds request i0 + k; inactive owners ask for nothing.
   // With a window (one request), every lane holds it, read into SGPRs: the folds
@@ -436,15 +437,43 @@ __device__ __forceinline__ void refine_wave(const SubpelParams &p, WaveLds<T> &L
   const int px = q.pred_x, py = q.pred_y;
   const bool epzs = q.variant == 1;
   const int *sums_p = TILE ? W->sums : L.sums[lane < kK ? lane : 0];
+  int sums_off = 0;   // (window: where this phase's candidates start in the sums computed)
+  int sv = 0;         // (window: lane k holds the pass's sum of position c_p0 + k, read once per pass)
   auto sums = [&](int k) -> int {   // a phase's sum of candidate k (a scalar with a window)
-    if constexpr (TILE) return __builtin_amdgcn_readfirstlane(sums_p[k]);
+    if constexpr (TILE) return __builtin_amdgcn_readlane(sv, k + sums_off);
     else return sums_p[k];
   };
-  // a phase: the 16-per-wave form, or lane 0's request from its window
+  // what the window's sums hold: positions [c_p0, kMaxCand) of table 1 around (c_mx, c_my) with metric
+  // c_metric and scale c_sc (c_p0 < 0: nothing kept)
+  int c_p0 = -1, c_metric = -1, c_sc = -1, c_mx = 0, c_my = 0, npass = 0;
+  // a phase: the 16-per-wave form, or the request from its window.  With a window,
+  // a phase on EPZS's search_point table costs every later position of the table
+  // too (the same centre, metric and scale), so the follow-up phase after it
+  // (me_epzs_sub.c:96-127, 175-210: positions next_start..next_end around the
+  // same centre) reads sums already made: two passes instead of four
   auto phase = [&](int a0, int a1, int metric, bool t8v, int sc, int tab, int mx, int my) {
     if constexpr (TILE) {
-      auto u = [](int v) { return __builtin_amdgcn_readlane(v, 0); };
-      tile_phase(p, *W, lane, u(bsx), u(o.bsy), u(a0), u(a1), u(metric), u((int)t8v) != 0, sc, u(tab), u(mx), u(my));
+      if (a1 <= a0) return;   // (no candidates: the fold below reads nothing)
+      if (tab == 1 && c_p0 >= 0 && a0 >= c_p0 && a1 <= kMaxCand && metric == c_metric && sc == c_sc && mx == c_mx &&
+          my == c_my) {
+        sums_off = a0 - c_p0;
+        return;
+      }
+      const int e1 = tab == 1 ? kMaxCand : a1;
+      tile_phase(p, *W, lane, bsx, o.bsy, a0, e1, metric, t8v, sc, tab, mx, my);
+      sv = sums_p[lane < kMaxCand ? lane : 0];   // (the fold reads them by readlane, not one LDS trip each)
+      if (stamps) {   // (pass ends; constant indices: a computed one puts the array in scratch)
+        const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+        if (npass == 0) stamps[4] = t;
+        else stamps[5] = t;
+      }
+      ++npass;
+      sums_off = 0;
+      c_p0 = tab == 1 ? a0 : -1;
+      c_metric = metric;
+      c_sc = sc;
+      c_mx = mx;
+      c_my = my;
     } else {
       run_phase(p, L, lane, o, a0, a1, metric, t8v, sc, tab, mx, my);
     }
@@ -490,6 +519,7 @@ __device__ __forceinline__ void refine_wave(const SubpelParams &p, WaveLds<T> &L
       }
     }
   }
+  if (TILE && stamps) stamps[0] = __builtin_amdgcn_s_memrealtime();   // (server clocks: phase ends)
   // ---- phase B: EPZS half-pel follow-up (me_epzs_sub.c:96-127)
   {
     int s0 = 0, s1 = 0;
@@ -510,6 +540,7 @@ __device__ __forceinline__ void refine_wave(const SubpelParams &p, WaveLds<T> &L
       if (best_pos) { mvx += 2 * ept_x(best_pos); mvy += 2 * ept_y(best_pos); }
     }
   }
+  if (TILE && stamps) stamps[1] = __builtin_amdgcn_s_memrealtime();   // (server clocks: phase ends)
   // ---- phase C: quarter-pel ring (me_fullsearch.c:252-282 | me_epzs_sub.c:135-172)
   lambda = q.lambda_q;
   {
@@ -548,6 +579,7 @@ __device__ __forceinline__ void refine_wave(const SubpelParams &p, WaveLds<T> &L
       if (!epzs && best_pos) { mvx += spiral_x(best_pos); mvy += spiral_y(best_pos); }
     }
   }
+  if (TILE && stamps) stamps[2] = __builtin_amdgcn_s_memrealtime();   // (server clocks: phase ends)
   // ---- phase D: EPZS quarter-pel follow-up (me_epzs_sub.c:175-210)
   {
     int s0 = 0, s1 = 0;
@@ -574,6 +606,7 @@ __device__ __forceinline__ void refine_wave(const SubpelParams &p, WaveLds<T> &L
     }
     if (act && epzs && !early && best_pos > 0) { mvx += ept_x(best_pos); mvy += ept_y(best_pos); }
   }
+  if (TILE && stamps) stamps[3] = __builtin_amdgcn_s_memrealtime();   // (server clocks: phase ends)
   if (act && (!TILE || lane == 0)) {
     jmme_block_res r;
     r.mv_x = (int16_t)mvx;
