@@ -38,6 +38,15 @@
 #include "jmme_subpel_internal.h"
 #include "jmme_refine_dev.h"
 
+// Cache policy of the sub-image stores: sc0 | sc1 (system scope, written through
+// rather than left dirty in L2).  A/B on the 1080p reference (tools/ab_interp.sh,
+// two interleaved rounds, sub-image parity green in each, profiles/round5/interp/):
+// default policy 9.9-10.0 us (47.5 % of 8 TB/s), nt 9.2 (51.5 %), sc1 8.9 (53 %),
+// sc1 | nt 9.3-9.9, sc0 | nt 9.3, sc0 | sc1 8.8 us (53.7 %); the refinement that
+// reads the sub-images after them is unchanged (0.200-0.202 ms per frame either way).
+#ifndef JMME_INTERP_AUX
+#define JMME_INTERP_AUX 17
+#endif
 #ifndef JMME_INTERP_ROWS
 #define JMME_INTERP_ROWS 3   // (2: 13.7-14.2 us, 3: 11.6, 4: 12.8-13.0, 5: 12.0, 6: 13.0, 8: 15.2 us per 1080p reference)
 #endif
@@ -187,7 +196,7 @@ __device__ __forceinline__ void interp_rows8(const uint8_t *rows, int pitch, int
     const int vo = (int)(off0 + (uint32_t)m * (uint32_t)dst_pitch);
 #pragma unroll
     for (int k = 0; k < 16; ++k)
-      __builtin_amdgcn_raw_buffer_store_b32(o[k], rsrc, vo, (int)((uint32_t)k * (uint32_t)plane_stride), 0);
+      __builtin_amdgcn_raw_buffer_store_b32(o[k], rsrc, vo, (int)((uint32_t)k * (uint32_t)plane_stride), JMME_INTERP_AUX);
   }
 }
 
@@ -249,10 +258,10 @@ __global__ __launch_bounds__(256) void sub_images_kernel(const T *__restrict__ s
   auto store = [&](int k, int m, typename Pack4<T>::V v) {
     const int vo = (int)(off0 + (uint32_t)m * (uint32_t)dst_pitch * (uint32_t)sizeof(T));
     const int so = (int)((uint32_t)k * (uint32_t)plane_stride * (uint32_t)sizeof(T));
-    if constexpr (sizeof(T) == 1) __builtin_amdgcn_raw_buffer_store_b32(v, rsrc, vo, so, 0);
+    if constexpr (sizeof(T) == 1) __builtin_amdgcn_raw_buffer_store_b32(v, rsrc, vo, so, JMME_INTERP_AUX);
     else {
       typedef unsigned u32x2v __attribute__((ext_vector_type(2)));
-      __builtin_amdgcn_raw_buffer_store_b64(u32x2v{v.x, v.y}, rsrc, vo, so, 0);
+      __builtin_amdgcn_raw_buffer_store_b64(u32x2v{v.x, v.y}, rsrc, vo, so, JMME_INTERP_AUX);
     }
   };
 #pragma unroll
