@@ -45,7 +45,10 @@
 // sc1 | nt 9.3-9.9, sc0 | nt 9.3, sc0 | sc1 8.8 us (53.7 %); the refinement that
 // reads the sub-images after them is unchanged (0.200-0.202 ms per frame either way).
 #ifndef JMME_INTERP_T16
-#define JMME_INTERP_T16 0    // A/B knob: 8-bit outputs transposed through LDS and stored 16 bytes a lane
+// A/B knob: 8-bit outputs transposed through a 48 KB LDS tile and stored 16 bytes a lane.
+// Measured slower (12.8 vs 8.8 us per 1080p reference, profiles/round5/interp/): the
+// tile limits the workgroups a CU holds and adds an LDS round trip; off.
+#define JMME_INTERP_T16 0
 #endif
 #ifndef JMME_INTERP_AUX
 #define JMME_INTERP_AUX 17
