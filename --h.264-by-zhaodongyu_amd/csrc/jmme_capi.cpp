@@ -142,6 +142,7 @@ struct jmme_ctx {
                                              // server hand-off, hand-off to posted, posted to done, done to return
   double srv_t_call = 0, srv_t_post = 0, srv_t_done = 0;
   double srv_cycles = 0;
+  double ep_batch_us[3] = {};                // JMME_PHASES: batches -- copies in, launches + wait, copies out
   double srv_rph_us[6] = {};                 // JMME_PHASES: the refinement's phase ends and passes (from its window)                     // JMME_PHASES: s_memtime ticks over the requests' service, summed
   double srv_copy_us = 0, srv_search_us = 0; // (to the request's copy in LDS, to the search's end)
   double srv_ph_us[10] = {};                  // (the search's phases: set-up, centre, predictors, walk, visited
@@ -442,6 +443,9 @@ extern "C" void jmme_destroy(jmme_ctx *ctx) {
             ctx->srv_rph_us[3] / ctx->srv_served, ctx->srv_rph_us[4] / ctx->srv_served,
             ctx->srv_rph_us[5] / ctx->srv_served);
   if (ctx->srv_check) fprintf(stderr, "jmme EPZS server check: %lld mismatches\n", ctx->srv_mismatch);
+  if (ctx->phases && ctx->ep_n[1])
+    fprintf(stderr, "jmme EPZS batches (ms in all): validation and copies in %.1f, launches and wait %.1f, copies "
+            "out %.1f\n", ctx->ep_batch_us[0] * 1e-3, ctx->ep_batch_us[1] * 1e-3, ctx->ep_batch_us[2] * 1e-3);
   if (ctx->phases && (ctx->ep_n[0] || ctx->ep_n[1]))
     fprintf(stderr, "jmme EPZS calls: %lld alone, %.1f ms (%.2f us each); %lld batches, %.1f ms\n", ctx->ep_n[0],
             ctx->ep_us[0] / 1e3, ctx->ep_us[0] / std::max(1ll, ctx->ep_n[0]), ctx->ep_n[1], ctx->ep_us[1] / 1e3);
@@ -1891,6 +1895,7 @@ extern "C" int jmme_epzs_speculate(jmme_ctx *ctx, const jmme_epzs_req *req, int 
     if (ie) ctx->srv_idle_ticks = (uint32_t)std::max(1, std::min(1000000, std::atoi(ie))) * 100u;
   }
   const int mode = fuse ? ctx->single_mode : 0;
+  const double t_staged = ctx->phases && n > 1 ? now_us() : 0.0;   // (batches: the copies in are done)
   if (mode != 3 && server_stop(ctx)) return -1;
   if (mode == 3) {   // the resident server: no launch on the search's path
     ctx->srv_t_call = ep_timer_.t0;
@@ -1929,12 +1934,18 @@ extern "C" int jmme_epzs_speculate(jmme_ctx *ctx, const jmme_epzs_req *req, int 
   } else {
     HIPCHK(hipStreamSynchronize(s));
   }
+  const double t_synced = ctx->phases && n > 1 ? now_us() : 0.0;
   std::memcpy(out, h_out, (size_t)n * sizeof(jmme_epzs_res));
   std::memcpy(bounds, h_bnd, (size_t)n * sizeof(jmme_epzs_bounds));
   for (int i = 0; i < n; ++i)   // only the pairs each search wrote
     std::memcpy(visited + 2 * (size_t)max_visited * i, h_vis + 2 * (size_t)max_visited * i,
                 (size_t)std::min(out[i].n_visited, max_visited) * 4);
   if (sp_req) std::memcpy(sp_out, h_spo, (size_t)n * sizeof(jmme_block_res));
+  if (ctx->phases && n > 1) {
+    ctx->ep_batch_us[0] += t_staged - ep_timer_.t0;   // validation and copies in
+    ctx->ep_batch_us[1] += t_synced - t_staged;       // launches and the wait
+    ctx->ep_batch_us[2] += now_us() - t_synced;       // copies out
+  }
   return 0;
 }
 
