@@ -1539,7 +1539,7 @@ int epzs_serve(jmme_ctx *ctx, const jmme_epzs_req *d_req, const int16_t *d_preds
                jmme_epzs_bounds *d_bnd, jmme_block_res *d_int, const EpzsOne &one, jmme_block_res *d_spo) {
   const double t_in = ctx->phases ? now_us() : 0.0;
   if (!ctx->h_box) {
-    HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_box), sizeof(EpzsBox), hipHostMallocMapped));
+    HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_box), sizeof(EpzsBox), hipHostMallocMapped | hipHostMallocCoherent));
     std::memset(static_cast<void *>(ctx->h_box), 0, sizeof(EpzsBox));
     void *dv = nullptr;
     HIPCHK(hipHostGetDevicePointer(&dv, ctx->h_box, 0));
@@ -1911,7 +1911,7 @@ extern "C" int jmme_epzs_speculate(jmme_ctx *ctx, const jmme_epzs_req *req, int 
   }
   if (mode >= 1 && !ctx->single_stream) HIPCHK(hipStreamCreateWithFlags(&ctx->single_stream, hipStreamNonBlocking));
   if (mode == 2 && !ctx->h_done) {
-    HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_done), 64, hipHostMallocMapped));
+    HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_done), 64, hipHostMallocMapped | hipHostMallocCoherent));
     HIPCHK(hipHostGetDevicePointer(&ctx->dv_done, ctx->h_done, 0));
     __atomic_store_n(ctx->h_done, 0u, __ATOMIC_RELEASE);
   }
@@ -2290,6 +2290,8 @@ extern "C" int jmme_sub_images_async(jmme_ctx *ctx, const uint8_t *d_src, int sr
   if (dst_pitch < ((pw + 3) & ~3) || (dst_pitch & 3) || (reinterpret_cast<uintptr_t>(d_dst) & 3))
     return fail("sub-image pitch %d: need a multiple of 4 >= %d and a 4-byte aligned buffer", dst_pitch, pw);
   if (plane_stride < (size_t)ph * dst_pitch || (plane_stride & 3)) return fail("sub-image plane stride too small");
+  if (15 * plane_stride + (size_t)ph * dst_pitch >= ((size_t)1 << 32))
+    return fail("sub-image planes span %zu bytes: the 16 planes must lie within 4 GiB", 16 * plane_stride);
   HIPCHK(launch_sub_images(d_src, src_pitch, width, height, d_dst, dst_pitch, plane_stride,
                            reinterpret_cast<hipStream_t>(stream)));
   return 0;

@@ -71,17 +71,9 @@ constexpr int kRed2 = kRed1 / 2;              //         ... after the permlane1
 // v6 sweep (default): a fold reduce-scatters its keys across the wave at once
 // into 11 registers (kRed2), so no wave keeps 41 per-lane minima through the
 // sweep; the freed registers pay for 5 positions per task (13 task rows at
-// R = 32, no redundant rows).  v5 (JMME_SWEEP_V6=0): 41 per-lane minima, 3
-// positions per task.
-#ifndef JMME_SWEEP_V6
-#define JMME_SWEEP_V6 1
-#endif
+// R = 32, no redundant rows).
 #ifndef JMME_SWEEP_P
-#if JMME_SWEEP_V6
 #define JMME_SWEEP_P 5   // positions per sweep task (vertical run)
-#else
-#define JMME_SWEEP_P 3
-#endif
 #endif
 #ifndef JMME_WAVES_PER_EU
 #define JMME_WAVES_PER_EU 4
@@ -171,9 +163,6 @@ __device__ __forceinline__ Lds carve(unsigned char *smem, int R, bool hbd = fals
 #endif
 
 __device__ __forceinline__ int ufl(int v) { return __builtin_amdgcn_readfirstlane(v); }
-#ifdef JMME_ELIM_COUNT
-__device__ unsigned long long g_elim_tasks[2];   // diagnostic: wave-tasks tested, skipped
-#endif
 __device__ __forceinline__ unsigned long long ufl64(unsigned long long v) {
   unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
   unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
@@ -1105,21 +1094,8 @@ __device__ __forceinline__ bool sweep_v5(const Lds &L, const uint32_t (&cs)[64],
       need = max(need, __builtin_elementwise_sub_sat(t.z, kmin) >> 2);
       need = max(need, __builtin_elementwise_sub_sat(t.w, kmin) >> 3);
       need = max(need, __builtin_elementwise_sub_sat(t16, kmin) >> 4);
-#ifndef JMME_NO_ELIM
       fold = __builtin_amdgcn_ballot_w64(e < need) != 0;
-#else
-      fold = __builtin_amdgcn_ballot_w64(e < need) != 0 || true;
-#endif
-#ifdef JMME_ELIM_COUNT   // diagnostic (contended atomics: distorts timing)
-      if ((tid & 63) == 0) { atomicAdd(&g_elim_tasks[0], 1ull); if (!fold) atomicAdd(&g_elim_tasks[1], 1ull); }
-#endif
     }
-#ifdef JMME_ABL_NOFOLD   // timing ablation only: keep the 4x4 keys live, no partition keys / minima
-#pragma unroll
-    for (int j = 0; j < P; ++j)
-#pragma unroll
-      for (int k = 0; k < 16; ++k) asm volatile("" :: "v"(a[j][k]));
-#else
     if (fold) {
     folded = true;
     if constexpr (NB == kRed2) {
@@ -1142,7 +1118,6 @@ __device__ __forceinline__ bool sweep_v5(const Lds &L, const uint32_t (&cs)[64],
     }
     }
     }
-#endif
     if (rows64) {
       tq += kWaves;
     } else {
@@ -1538,11 +1513,7 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
         // hides behind a row of arithmetic (and the other waves of the SIMD)
         u32x2 n01, n23;
         u32x4 cn;
-#ifdef JMME_ABL_NOLDS    // timing ablation only: no window reads
-        n01 = u32x2{(uint32_t)tx, (uint32_t)tx ^ 1u}; n23 = u32x2{(uint32_t)tx ^ 2u, (uint32_t)tx ^ 3u};
-#else
         n01 = ds_read2_0_4(wrow); n23 = ds_read2_8_12(wrow);
-#endif
         cn = ds_read_b128(cb);
         u32x4 cprev = u32x4{0u, 0u, 0u, 0u};
 #pragma unroll
@@ -1551,11 +1522,7 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
           const u32x4 c = cn;
           if (r < 16) {
             const uint32_t a = wrow + (uint32_t)(r + 1) * rowb;
-#ifdef JMME_ABL_NOLDS
-            n01 = u32x2{(r + 1) * 0x01010101u + tx, a}; n23 = u32x2{a ^ 2u, a ^ 3u};
-#else
             n01 = ds_read2_0_4(a); n23 = ds_read2_8_12(a);
-#endif
             if (r < 15) cn = ds_read_b128(cb + 16u * (uint32_t)(r + 1));
           }
           __builtin_amdgcn_sched_barrier(0);
@@ -1603,11 +1570,6 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
         update_slots<KEY32, FFS, decltype(all_tag)::value, Best, HBD>(ps, g, pos_ctx(oyw), best);
       };
 
-#ifdef JMME_ABL_NOCOST   // timing ablation only: keep the SADs live, skip the cost/minimum work
-#pragma unroll
-      for (int k = 0; k < 16; ++k) asm volatile("" :: "v"(a0[k]), "v"(a1[k]));
-      (void)eval_position;
-#else
       // range 0 (D == 1): one position -- the second is made a copy of it
       if (D == 1) {
 #pragma unroll
@@ -1617,7 +1579,6 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
       // partition fold into one v_min3_u32
       eval_position(a0, yb);
       eval_position(a1, min(yb + 1, D - 1));
-#endif
       tx += rstep;
       ty += qstep;
       if (tx >= D) { tx -= D; ++ty; }
@@ -1630,9 +1591,6 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
   if (KEY32 && fast) {
     if (spec && wave == kWaves - 1) special_keys<FFS, HBD>(g, L, lane);   // the wave with the fewest sweep tasks; read back after the reduce's barrier
     if constexpr (KEY32) centre_bounds<FFS, HBD>(g, L, lane, ufl(wave));
-#ifdef JMME_DBG_SYNC_TMAX   // diagnostic: the centre bounds stored before the sweep reads them
-    __syncthreads();
-#endif
     if constexpr (KEY32 && HBD) {   // 16-bit samples (<= 10 bits): 3 positions a task (the MB rows take VGPRs)
 #pragma unroll
       for (int q = 0; q < kRed2; ++q) b11[q] = ~0u;
@@ -1640,18 +1598,12 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
       v6_folded = L.wp == kWP32 ? sweep_v5<kWP32, 3, kRed2, true>(L, cs, R, g.rs, b11)
                                 : sweep_v5<0, 3, kRed2, true>(L, cs, R, g.rs, b11);
     } else if constexpr (KEY32) {
-#if JMME_SWEEP_V6
 #pragma unroll
       for (int q = 0; q < kRed2; ++q) b11[q] = ~0u;
       v6 = true;
       v6_folded = (L.wp == kWP32 && g.rs == 32) ? sweep_v5<kWP32, JMME_SWEEP_P, kRed2, false, 32>(L, cs, R, g.rs, b11)
                   : L.wp == kWP32                 ? sweep_v5<kWP32, JMME_SWEEP_P, kRed2>(L, cs, R, g.rs, b11)
                                                   : sweep_v5<0, JMME_SWEEP_P, kRed2>(L, cs, R, g.rs, b11);
-#else
-      init_best();
-      if (L.wp == kWP32) sweep_v5<kWP32, JMME_SWEEP_P, kNS>(L, cs, R, g.rs, best);
-      else sweep_v5<0, JMME_SWEEP_P, kNS>(L, cs, R, g.rs, best);
-#endif
     }
   } else {
     init_best();
@@ -1667,15 +1619,11 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
   // LDS once the reduce and refine have hidden the atomic's round trip
   unsigned tk = 0;
   if (tick && tid == 0) tk = atomicAdd(tick, 1u);
-#ifdef JMME_ABL_NOREDUCE   // timing ablation only: no cross-lane reduction
-  if (KEY32 && false) {
-#else
   if (KEY32 && v6) {
     // (the fold's ballot makes v6_folded wave-uniform)
     if (__builtin_amdgcn_ballot_w64(v6_folded)) v6_write<true>(L, b11, lane, wave);
     else v6_write<false>(L, b11, lane, wave);
   } else if (KEY32) {
-#endif
     // reduce-scatter through the wave: permlane32_swap pairs slots (lanes
     // 0-31 keep one, 32-63 the other), permlane16_swap pairs again (one slot
     // per row of 16), four DPP steps finish each row -- 11 registers carry
@@ -1753,10 +1701,8 @@ __device__ __forceinline__ void search_item(const KParams &p, const Item &it, co
     }
 #endif
     STAMP(st.reduce);
-#ifndef JMME_ABL_NOREFINE   // timing ablation only: no refine / output
     if (L.wp == kWP32) refine_output32<FFS, HBD, kWP32>(p, g, L, spec, fast, satm, u);
     else refine_output32<FFS, HBD, 0>(p, g, L, spec, fast, satm, u);
-#endif
     if (tick && opaque_tid(L) == 0) *s_tick = tk;
     STAMP(st.refine);
     int call = 0;
@@ -1918,12 +1864,10 @@ __global__ __launch_bounds__(kWG, KEY32 ? JMME_WAVES_PER_EU : 2) void me_items_k
     if (more) nx = load_item(items, item_at(jn));
     STAMP(st.wait);
     const bool fast = it.gmask && item_fast<KEY32, FFS>(p, it);
-#ifndef JMME_ABL_NOEXPAND   // timing ablation only: the window stays as the previous item left it
     if (it.gmask) {
       if constexpr (HBD) expand16(p, it, L);
       else expand(p, it, L);
     }
-#endif
     if (fast) build_tabs<FFS>(it, L);
     __syncthreads();
     if (p.debug_words && it.u == 0 && (it.gmask & dbg_slot)) {
@@ -1936,10 +1880,6 @@ __global__ __launch_bounds__(kWG, KEY32 ? JMME_WAVES_PER_EU : 2) void me_items_k
     STAMP(st.expand);
     // the raw buffer is free: start fetching the next item behind this sweep
     if (more) prefetch<HBD>(p, nx, L);
-#ifdef JMME_DBG_SYNC_PREFETCH   // diagnostic: no LDS DMA in flight during the item
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-#endif
     bool ticketed = false;
     if (it.gmask) {
       // the current MB into SGPRs: every v_sad of the v5 sweep takes it as
@@ -2630,16 +2570,6 @@ extern "C" int jmme_debug_chain_prof(unsigned long long *out) {
 namespace jmme {
 #endif
 
-#ifdef JMME_ELIM_COUNT
-}  // namespace jmme
-// diagnostic builds: wave-tasks the elimination test saw / skipped since the last call
-extern "C" int jmme_debug_elim(unsigned long long *out) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(jmme::g_elim_tasks), 2 * sizeof(unsigned long long)) != hipSuccess) return -1;
-  const unsigned long long z[2] = {0, 0};
-  return hipMemcpyToSymbol(HIP_SYMBOL(jmme::g_elim_tasks), z, sizeof z) == hipSuccess ? 0 : -1;
-}
-namespace jmme {
-#endif
 
 hipError_t launch_search(const KParams &p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
   // occupancy per device: the caller (jmme_capi) has made the context's device current

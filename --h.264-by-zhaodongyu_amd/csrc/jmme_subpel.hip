@@ -44,12 +44,6 @@
 // default policy 9.9-10.0 us (47.5 % of 8 TB/s), nt 9.2 (51.5 %), sc1 8.9 (53 %),
 // sc1 | nt 9.3-9.9, sc0 | nt 9.3, sc0 | sc1 8.8 us (53.7 %); the refinement that
 // reads the sub-images after them is unchanged (0.200-0.202 ms per frame either way).
-#ifndef JMME_INTERP_T16
-// A/B knob: 8-bit outputs transposed through a 48 KB LDS tile and stored 16 bytes a lane.
-// Measured slower (12.8 vs 8.8 us per 1080p reference, profiles/round5/interp/): the
-// tile limits the workgroups a CU holds and adds an LDS round trip; off.
-#define JMME_INTERP_T16 0
-#endif
 #ifndef JMME_INTERP_AUX
 #define JMME_INTERP_AUX 17
 #endif
@@ -124,11 +118,8 @@ __device__ __forceinline__ uint32_t pack_pairs(s16x2 lo, s16x2 hi) {
 // (8-bit rows are staged from the dword boundary 2 bytes below the tile's first
 // sample: X0 - kPadX - 2 is 2 mod 4 for every tile)
 static_assert(kTileW % 4 == 0 && ((-(kPadX + 2)) & 3) == 2, "8-bit staging offset");
-// ot (JMME_INTERP_T16): the outputs go to the workgroup's LDS tile ot[plane][tile row][dword]
-// (tile row lr0 + m) instead of to memory, for 16-byte stores after a barrier
 __device__ __forceinline__ void interp_rows8(const uint8_t *rows, int pitch, int tx, int row0, int ph, uint8_t *dst,
-                                             int dst_pitch, size_t plane_stride, int col, uint32_t *ot = nullptr,
-                                             int lr0 = 0) {
+                                             int dst_pitch, size_t plane_stride, int col) {
   constexpr int NR = kRowsT + 5;
   // the 12 bytes at the thread's dword: sample I[c] of the scalar form is byte c + 2
   uint32_t D1[NR], D2[NR];
@@ -202,11 +193,6 @@ __device__ __forceinline__ void interp_rows8(const uint8_t *rows, int pitch, int
     o[13] = L(P20, Q02);    // [3][1]
     o[14] = L(P22, Q02);    // [3][2]
     o[15] = L(Q02, P20n);   // [3][3] getDiagSubImageBiLinear
-    if (ot) {
-#pragma unroll
-      for (int k = 0; k < 16; ++k) ot[(k * kTileH + lr0 + m) * (kTileW / 4) + tx] = o[k];
-      continue;
-    }
     const int vo = (int)(off0 + (uint32_t)m * (uint32_t)dst_pitch);
 #pragma unroll
     for (int k = 0; k < 16; ++k)
@@ -243,27 +229,6 @@ __global__ __launch_bounds__(256) void sub_images_kernel(const T *__restrict__ s
   __syncthreads();
   const int ty = threadIdx.x >> 6, tx = threadIdx.x & 63;   // a wave writes 256 contiguous samples per sub-image
   const int row0 = Y0 + kRowsT * ty, col = X0 + 4 * tx;
-#if JMME_INTERP_T16
-  if constexpr (sizeof(T) == 1) {   // the tile through LDS, stored as 16-byte chunks (pw is a multiple of 16)
-    __shared__ __attribute__((aligned(16))) uint32_t OT[16 * kTileH * (kTileW / 4)];
-    if (row0 < ph && col < pw)
-      interp_rows8(&S[kRowsT * ty][0], kRowW, tx, row0, ph, dst, dst_pitch, plane_stride, col, OT, kRowsT * ty);
-    __syncthreads();
-    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, -1, 0x00020000);
-    constexpr int kQ = kTileW / 16;   // chunks a tile row
-    for (int c = threadIdx.x; c < 16 * kTileH * kQ; c += 256) {
-      const int k = c / (kTileH * kQ), rem = c - k * (kTileH * kQ), r = rem / kQ, q = rem - r * kQ;
-      if (Y0 + r < ph && X0 + 16 * q < pw) {
-        typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
-        const uint4 v = *reinterpret_cast<const uint4 *>(&OT[(k * kTileH + r) * (kTileW / 4) + 4 * q]);
-        __builtin_amdgcn_raw_buffer_store_b128(u32x4v{v.x, v.y, v.z, v.w}, rsrc,
-                                               (int)((uint32_t)(Y0 + r) * (uint32_t)dst_pitch + (uint32_t)(X0 + 16 * q)),
-                                               (int)((uint32_t)k * (uint32_t)plane_stride), JMME_INTERP_AUX);
-      }
-    }
-    return;
-  }
-#endif
   if (row0 >= ph || col >= pw) return;
   if constexpr (sizeof(T) == 1) {
     interp_rows8(&S[kRowsT * ty][0], kRowW, tx, row0, ph, dst, dst_pitch, plane_stride, col);
@@ -387,6 +352,10 @@ __global__ __launch_bounds__(256) void subpel_kernel(SubpelParams p) {
 hipError_t launch_sub_images(const uint8_t *src, int src_pitch, int w, int h, uint8_t *dst, int dst_pitch,
                              size_t plane_stride, hipStream_t s, int bits) {
   const int pw = w + 2 * kPadX, ph = h + 2 * kPadY;
+  // the stores address the 16 planes through one buffer resource with a 32-bit
+  // voffset + soffset: the last plane's last row must lie below 4 GiB
+  if ((15 * plane_stride + (size_t)ph * dst_pitch) * (bits > 8 ? 2 : 1) >= ((size_t)1 << 32))
+    return hipErrorInvalidValue;
   dim3 grid((pw + kTileW - 1) / kTileW, (ph + kTileH - 1) / kTileH);
   if (bits > 8)
     hipLaunchKernelGGL(sub_images_kernel<uint16_t>, grid, dim3(256), 0, s, reinterpret_cast<const uint16_t *>(src),

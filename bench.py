@@ -295,17 +295,20 @@ def case_block(dev, local: int, case: str, workload: str, iters: int = 10) -> di
     st = torch.cuda.current_stream(dev)
     me.search_async(FULL_SEARCH, d_req.data_ptr(), n, d_out.data_ptr(), st.cuda_stream)
     torch.cuda.synchronize(dev)
+    out = d_out.cpu().numpy().view(BLOCK_RES).reshape(n, NSLOT)[unit_of, slots]
+    exact = int(np.sum((out["mv_x"] == expect[0]) & (out["mv_y"] == expect[1]) & (out["cost"] == expect[2])))
+    outs = timed_buffers(d_out, iters)
+    torch.cuda.synchronize(dev)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     kms = []
     e0.record(st)
-    for _ in range(iters):
-        me.search_async(FULL_SEARCH, d_req.data_ptr(), n, d_out.data_ptr(), st.cuda_stream)
+    for i in range(iters):
+        me.search_async(FULL_SEARCH, d_req.data_ptr(), n, outs[i % len(outs)].data_ptr(), st.cuda_stream)
         kms.append(me.last_kernel_ms())
     e1.record(st)
     torch.cuda.synchronize(dev)
     ms = e0.elapsed_time(e1) / iters
-    out = d_out.cpu().numpy().view(BLOCK_RES).reshape(n, NSLOT)[unit_of, slots]
-    exact = int(np.sum((out["mv_x"] == expect[0]) & (out["mv_y"] == expect[1]) & (out["cost"] == expect[2])))
+    timed = timed_parity(outs, min(iters, len(outs)), n, unit_of, slots, expect, "JM 18.5 lencod (captured)")
     me.close()
     kernel_ms = float(np.mean(kms))
     items, absd = plan_items(req)
@@ -317,6 +320,7 @@ def case_block(dev, local: int, case: str, workload: str, iters: int = 10) -> di
             "hbm_frac": round(ALG_BYTES_PER_UNIT * n / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6),
             "parity": {"reference": "JM 18.5 lencod (captured)", "searches": int(len(expect[0])),
                        "bit_exact": exact},
+            "parity_timed": timed,
             "jm_me_time_at_capture": meta.get("jm_me_time")}
 
 
@@ -393,6 +397,30 @@ def oracle_parity(cur, ref, req, out, sample: int = 96, seed: int = 5) -> tuple[
     got = np.array(got, np.int64).reshape(-1, 3)
     exp = np.column_stack([mv[:, 0], mv[:, 1], cost]).astype(np.int64)
     return len(exp), int(np.sum(np.all(got == exp, axis=1)))
+
+
+def timed_buffers(d_out, steps: int, cap_bytes: int = 2 << 30) -> list:
+    """One output buffer per timed launch (up to cap_bytes in all, then reused
+    round-robin), filled with 0xFF -- no valid result record -- so a launch that
+    skipped or half-wrote a partition cannot pass for the one before it."""
+    k = max(1, min(steps, cap_bytes // max(1, d_out.numel())))
+    return [torch.full_like(d_out, 0xFF) for _ in range(k)]
+
+
+def timed_parity(outs, launches: int, n: int, unit_of, slots, expect, reference: str) -> dict:
+    """Bit-exactness of every timed launch's output, per partition search:
+    (mv, cost) against `expect` -- JM 18.5's captured results on rank 0, the
+    post-warm-up output (itself checked against the oracle) on the other ranks."""
+    from jmme import BLOCK_RES, NSLOT
+    ok = wrong = 0
+    for d_o in outs[:launches]:
+        g = d_o.cpu().numpy().view(BLOCK_RES).reshape(n, NSLOT)[unit_of, slots]
+        bad = int(np.sum((g["mv_x"] != expect[0]) | (g["mv_y"] != expect[1]) | (g["cost"] != expect[2])))
+        ok += bad == 0
+        wrong += bad
+    return {"reference": reference, "launches": launches, "launches_exact": ok,
+            "searches_per_launch": int(len(expect[0])), "wrong_searches": wrong,
+            "note": "every timed launch wrote its own 0xFF-poisoned output buffer"}
 
 
 def job_value(units_per_rank_step: int, steps: int, ws: int, wall: float) -> float:
@@ -566,38 +594,56 @@ def run_encoder(args, ws: int, rank: int, local: int) -> None:
         import torch.distributed as dist
         dist.init_process_group("gloo")
         dist.barrier()
-    w, h = (int(x) for x in args.enc_size.split("x"))
+    params, psize, ptext = bench_blocks.encoder_preset(args.enc_preset)
+    w, h = (int(x) for x in args.enc_size.split("x")) if args.enc_size else psize
+    # host placement: each rank's encoders on its GPU's NUMA-local cores (its share
+    # of them when GPUs share a node), one core per running encoder
+    local_ws = int(os.environ.get("LOCAL_WORLD_SIZE", ws))
+    cpus, source = bench_blocks.gpu_local_cpus(local, local_ws) if (ws > 1 or args.enc_pin) else (None, "unpinned")
     # the timed region is the launcher's own run (clip generation excluded); the
     # stock encodes (parity, host baseline) follow once every rank's run is done
     blk = bench_blocks.encoder_gop_block(device=local, rank=rank, gops=args.enc_gops, gop=args.enc_gop, size=(w, h),
                                          per_gpu=args.enc_per_gpu, check_stock=True, encoder=args.enc_encoder,
-                                         between=(lambda: dist.barrier()) if ws > 1 else None)
+                                         between=(lambda: dist.barrier()) if ws > 1 else None,
+                                         preset=args.enc_preset, cpus=cpus)
     if blk is None:
         raise SystemExit("--shard encoder needs integration/_build/{lencod_jmme,jmme_gop} and oracle/_ref/lencod")
+    blk["host_placement"]["source"] = source
     wall = blk["wall_s"]
     ok = blk["parity"]["byte_identical_gops"]
     rec = [wall, float(ok), float(blk["host_baseline"]["encoder_mb_per_s"]), float(blk["macroblocks"])]
+    cores = cpus or []
+    core_rec = torch.zeros(256, dtype=torch.int64)   # this rank's cores (-1 padded), gathered for the report
+    core_rec.fill_(-1)
+    core_rec[:min(256, len(cores))] = torch.tensor(cores[:256], dtype=torch.int64)
     if ws > 1:
         t = torch.tensor(rec, dtype=torch.float64)
         allr = [torch.zeros_like(t) for _ in range(ws)]
         dist.all_gather(allr, t)
         recs = [x.tolist() for x in allr]
+        allc = [torch.zeros_like(core_rec) for _ in range(ws)]
+        dist.all_gather(allc, core_rec)
+        core_sets = [[int(c) for c in x.tolist() if c >= 0] for x in allc]
     else:
         recs = [rec]
+        core_sets = [list(cores)]
     if rank == 0:
         job_wall = max(r[0] for r in recs)
         mbs = sum(r[3] for r in recs)
         print(json.dumps({
-            "metric": "encoder macroblocks/sec (JM 18.5 lencod_jmme, closed GOPs, FS +-32 ME on the GPU)",
+            "metric": f"encoder macroblocks/sec (JM 18.5 lencod_jmme, closed GOPs, ME on the GPU; preset "
+                      f"{args.enc_preset})",
             "value": round(mbs / job_wall, 1), "unit": "macroblocks/sec", "n_gpus": ws, "steps": 1, "warmup": 0,
             "ms_per_step": round(job_wall * 1e3, 1), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "u8",
             "data": f"synthetic (a seeded {w}x{h} clip per rank)",
             "config": {"workload": f"{args.enc_gops} closed GOPs x {args.enc_gop} frames per GPU through lencod_jmme, "
-                                   f"FS +-32, 1 ref, RDO off, sub-pel off", "per_gpu_encoders": args.enc_per_gpu,
+                                   f"{w}x{h}, {ptext}", "preset": args.enc_preset, "per_gpu_encoders": args.enc_per_gpu,
                        "parallelism": f"closed-GOP shard x{ws} (integration/jmme_gop.c per rank, no collective)"},
             "per_rank": [{"rank": r, "wall_s": round(x[0], 3), "byte_identical_gops": int(x[1]),
-                          "macroblocks": int(x[3]), "host_encoder_mb_per_s": x[2]} for r, x in enumerate(recs)],
+                          "macroblocks": int(x[3]), "host_encoder_mb_per_s": x[2],
+                          "cpus": bench_blocks._cpulist_text(core_sets[r]) if core_sets[r] else "unpinned"}
+                         for r, x in enumerate(recs)],
             "parity": {"reference": "JM 18.5 lencod (stock, same GOP arguments)", "gops": args.enc_gops * ws,
                        "byte_identical_gops": int(sum(x[1] for x in recs))},
             "cpu_baseline": {"value": round(sum(x[2] for x in recs), 1), "unit": "macroblocks/sec",
@@ -634,13 +680,19 @@ def main():
     ap.add_argument("--enc-gops", type=int, default=16, help="--shard encoder / encoder block: GOPs per GPU")
     ap.add_argument("--enc-gop", type=int, default=4, help="frames per GOP (1 I + P)")
     ap.add_argument("--enc-per-gpu", type=int, default=8, help="encoder processes at once per GPU")
-    ap.add_argument("--enc-size", default="1920x1080", help="clip size WxH")
+    ap.add_argument("--enc-size", default=None, help="clip size WxH (default: the preset's)")
+    ap.add_argument("--enc-preset", choices=["fs", "epzs4k"], default="fs",
+                    help="fs: configs[1]'s settings at 1080p; epzs4k: configs[3] as configured (4K, "
+                         "encoder_baseline.cfg's EPZS keys, RDO on)")
+    ap.add_argument("--enc-pin", action="store_true", help="pin the encoders at N=1 too (N>1 always pins)")
+    ap.add_argument("--no-encoder-4k", action="store_true", help="skip the configs[3] GOP-encoder block of the N=1 line")
+    ap.add_argument("--enc4k-gops", type=int, default=8, help="encoder_gop_epzs4k block: GOPs (of 2 frames)")
     ap.add_argument("--enc-encoder", default=None, help="encoder binary (default integration/_build/lencod_jmme; "
                                                          "a CPU rehearsal passes the stock oracle/_ref/lencod)")
     args = ap.parse_args()
     if args.headline_only:
         for k in ("no_cpu_baseline", "no_subpel", "no_uhd", "no_adversarial", "no_hbd", "no_fractal", "no_hybrid",
-                  "no_dropin", "no_encoder"):
+                  "no_dropin", "no_encoder", "no_encoder_4k"):
             setattr(args, k, True)
 
     ws, rank, local = dist_env()
@@ -676,8 +728,8 @@ def main():
     d_out = torch.zeros(n * NSLOT * BLOCK_RES.itemsize, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
 
-    def step():
-        me.search_async(FULL_SEARCH, d_req.data_ptr(), n, d_out.data_ptr(), stream.cuda_stream)
+    def step(d_o=d_out):
+        me.search_async(FULL_SEARCH, d_req.data_ptr(), n, d_o.data_ptr(), stream.cuda_stream)
 
     for _ in range(args.warmup):
         step()
@@ -701,14 +753,18 @@ def main():
         kms.append(me.last_kernel_ms())
     kernel_ms = float(np.mean(kms))
 
+    # every timed launch writes its own output buffer, poisoned beforehand, so the
+    # work inside the timed region is checked too (parity_timed), not only the
+    # post-warm-up launch above
+    timed_outs = timed_buffers(d_out, args.steps)
     if ws > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize(dev)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record(stream)
-    for _ in range(args.steps):
-        step()
+    for i in range(args.steps):
+        step(timed_outs[i % len(timed_outs)])
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     if ws > 1:
@@ -716,6 +772,11 @@ def main():
     wall = time.perf_counter() - t0
     ev_ms = ev0.elapsed_time(ev1)
     wall, _ = reduce_over_ranks(wall, exact, ws, dev)
+    own = full[unit_of, slots]
+    timed = timed_parity(timed_outs, min(args.steps, len(timed_outs)), n, unit_of, slots,
+                         expect if rank == 0 else (own["mv_x"], own["mv_y"], own["cost"]),
+                         "JM 18.5 lencod (captured)" if rank == 0 else "post-warm-up output (oracle-checked)")
+    timed_worst = reduce_over_ranks(0.0, timed["launches_exact"] - timed["launches"], ws, dev)[1]
 
     if rank == 0:
         value = job_value(n, args.steps, ws, wall)
@@ -753,6 +814,7 @@ def main():
                                                                   ": rank r searches the P-frame of its own GOP")},
             "parity": {"reference": "JM 18.5 lencod (captured)", "searches": int(len(expect[0])),
                        "bit_exact": exact},
+            "parity_timed": dict(timed, all_ranks_exact=timed_worst == 0),
             "roofline": {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(ach / HBM_PEAK_GBS, 6), "traffic": pmc_traffic(),
                          "kernel_ms": round(kernel_ms, 4),
@@ -790,10 +852,18 @@ def main():
             import bench_blocks
             # the product's multi-GPU form at N = 1: closed GOPs through lencod_jmme
             # (the same as --shard encoder on one GPU), with the host baseline
-            w, h = (int(x) for x in args.enc_size.split("x"))
+            size = tuple(int(x) for x in args.enc_size.split("x")) if args.enc_size else None
             line["encoder_gop"] = bench_blocks.encoder_gop_block(device=local, rank=0, gops=args.enc_gops,
-                                                                 gop=args.enc_gop, size=(w, h),
-                                                                 per_gpu=args.enc_per_gpu, encoder=args.enc_encoder)
+                                                                 gop=args.enc_gop, size=size,
+                                                                 per_gpu=args.enc_per_gpu, encoder=args.enc_encoder,
+                                                                 preset=args.enc_preset)
+        if not args.no_encoder_4k and ws == 1:
+            import bench_blocks
+            # configs[3] as configured: 4K, encoder_baseline.cfg's EPZS keys, RDO on
+            # (--shard encoder --enc-preset epzs4k is the same over N GPUs)
+            line["encoder_gop_epzs4k"] = bench_blocks.encoder_gop_block(device=local, rank=0, gops=args.enc4k_gops,
+                                                                        gop=2, per_gpu=min(8, args.enc4k_gops),
+                                                                        encoder=args.enc_encoder, preset="epzs4k")
         if not args.no_dropin and ws == 1:
             import bench_blocks
             # FS / FFS (configs[1] settings), FS / FFS with encoder_baseline.cfg's

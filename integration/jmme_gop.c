@@ -21,15 +21,25 @@
  * on the GPU with lencod_jmme); the bitstreams differ only in their headers
  * (each GOP carries its own parameter sets and idr_pic_id).
  *
+ * Host placement: the encoders are host-bound (JM's mode decision, entropy
+ * coding and the adapter stay on the CPU), so each child is pinned to host cores
+ * with sched_setaffinity between fork and exec when a core list is given
+ * (--cpus; without it the scheduler places them).  The list is cut into one
+ * contiguous share per GPU slot -- a rank-per-GPU caller passes its GPU's
+ * NUMA-local cores -- and each running child of a slot takes a core of its
+ * share to itself while there are enough (the whole share otherwise).
+ *
  * Usage:
- *   jmme_gop --encoder PATH --gpus N [--per-gpu K] [--devices D0,D1,..] --gop G --frames F
- *            --prefix OUTPREFIX [--concat] -- <encoder arguments>
+ *   jmme_gop --encoder PATH --gpus N [--per-gpu K] [--devices D0,D1,..] [--cpus LIST]
+ *            --gop G --frames F --prefix OUTPREFIX [--concat] -- <encoder arguments>
  * (--devices: the HIP device index each of the N GPU slots stands for; default
- * 0 .. N-1.  A rank-per-GPU caller passes its own device alone.)
+ * 0 .. N-1.  A rank-per-GPU caller passes its own device alone.  --cpus: a
+ * Linux cpulist, e.g. "0-15,64-79".)
  * Prints one JSON line: GOPs, their GPU, wall time and JM's "Total ME time".
  */
 #define _GNU_SOURCE
 #include <errno.h>
+#include <sched.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -40,6 +50,7 @@
 
 typedef struct gop_run {
   int gop, gpu, first, count;
+  int core;        /* the core the child has to itself (index into g_cpus), -1: its slot's whole share */
   pid_t pid;
   double t0, t1, me_s;
   int status;
@@ -62,6 +73,72 @@ static const char *g_encoder, *g_prefix;
 static int g_dev_map[64];
 static char **g_enc_args;
 static int g_n_enc_args;
+static int g_pin;
+static int *g_cpus, g_n_cpus;      /* host cores the children run on */
+static unsigned char *g_core_busy;  /* per entry of g_cpus: held by a running child */
+static int g_gpus;
+
+/* "0-3,8,10-11" -> cores; returns the count (-1: malformed) */
+static int parse_cpulist(const char *q, int **out)
+{
+  int n = 0, cap = 64;
+  int *v = (int *)malloc(sizeof(int) * (size_t)cap);
+  if (!v) die("out of memory");
+  while (*q) {
+    char *end;
+    long a = strtol(q, &end, 10), b;
+    if (end == q || a < 0) { free(v); return -1; }
+    b = a;
+    if (*end == '-') {
+      q = end + 1;
+      b = strtol(q, &end, 10);
+      if (end == q || b < a) { free(v); return -1; }
+    }
+    for (; a <= b; a++) {
+      if (n == cap) {
+        cap *= 2;
+        v = (int *)realloc(v, sizeof(int) * (size_t)cap);
+        if (!v) die("out of memory");
+      }
+      v[n++] = (int)a;
+    }
+    if (*end && *end != ',') { free(v); return -1; }
+    q = *end == ',' ? end + 1 : end;
+  }
+  *out = v;
+  return n;
+}
+
+/* slot g's share of g_cpus: [lo, hi) */
+static void slot_share(int g, int *lo, int *hi)
+{
+  *lo = (int)((long)g * g_n_cpus / g_gpus);
+  *hi = (int)((long)(g + 1) * g_n_cpus / g_gpus);
+  if (*hi <= *lo) {   /* fewer cores than slots: slots share cores round-robin */
+    *lo = g % g_n_cpus;
+    *hi = *lo + 1;
+  }
+}
+
+/* a free core of slot g's share for a new child (-1: none free, the child takes the share) */
+static int take_core(int g)
+{
+  int lo, hi, c;
+  slot_share(g, &lo, &hi);
+  for (c = lo; c < hi; c++)
+    if (!g_core_busy[c]) { g_core_busy[c] = 1; return c; }
+  return -1;
+}
+
+/* the child's cpulist as text (for the report) */
+static void placement_text(const gop_run *r, char *buf, size_t n)
+{
+  int lo, hi;
+  if (!g_pin) { snprintf(buf, n, "unpinned"); return; }
+  if (r->core >= 0) { snprintf(buf, n, "%d", g_cpus[r->core]); return; }
+  slot_share(r->gpu, &lo, &hi);
+  snprintf(buf, n, hi - lo == 1 ? "%d" : "%d-%d", g_cpus[lo], g_cpus[hi - 1]);  /* (shares are listed in order) */
+}
 
 static void gop_path(char *buf, size_t n, int gop, const char *suffix)
 {
@@ -97,6 +174,21 @@ static pid_t start_gop(gop_run *r)
   if (pid == 0) {
     FILE *f = freopen(log, "w", stdout);
     if (!f) _exit(127);
+    if (g_pin) {   /* the host cores are fixed before the encoder starts, like the device */
+      cpu_set_t set;
+      int lo, hi, c;
+      CPU_ZERO(&set);
+      if (r->core >= 0) {
+        CPU_SET(g_cpus[r->core], &set);
+      } else {
+        slot_share(r->gpu, &lo, &hi);
+        for (c = lo; c < hi; c++) CPU_SET(g_cpus[c], &set);
+      }
+      if (sched_setaffinity(0, sizeof set, &set)) {
+        fprintf(stderr, "jmme_gop: sched_setaffinity: %s\n", strerror(errno));
+        _exit(127);
+      }
+    }
     /* the device is fixed before the encoder (and the HIP runtime in it) starts */
     setenv("HIP_VISIBLE_DEVICES", dev, 1);
     execv(g_encoder, argv);
@@ -144,7 +236,7 @@ int main(int argc, char **argv)
   int *busy;
   gop_run *runs;
   double t_start;
-  const char *devices = NULL;
+  const char *devices = NULL, *cpus = NULL;
   for (i = 0; i < 64; i++) g_dev_map[i] = i;
   for (i = 1; i < argc; i++) {
     if (!strcmp(argv[i], "--")) { i++; break; }
@@ -157,6 +249,7 @@ int main(int argc, char **argv)
     else if (!strcmp(argv[i], "--frames")) frames = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--prefix")) g_prefix = argv[++i];
     else if (!strcmp(argv[i], "--devices")) devices = argv[++i];
+    else if (!strcmp(argv[i], "--cpus")) cpus = argv[++i];
     else die("unknown option (see the usage in jmme_gop.c)");
   }
   if (!g_encoder || !g_prefix || gpus < 1 || per_gpu < 1 || gop < 1 || frames < 1)
@@ -173,6 +266,23 @@ int main(int argc, char **argv)
     }
     if (g < gpus) die("--devices names fewer devices than --gpus");
   }
+  g_gpus = gpus;
+  g_pin = cpus != NULL;
+  if (cpus) {
+    g_n_cpus = parse_cpulist(cpus, &g_cpus);
+    if (g_n_cpus <= 0) die("bad --cpus list");
+  } else {   /* the launcher's own affinity */
+    cpu_set_t set;
+    int c;
+    if (sched_getaffinity(0, sizeof set, &set)) die("sched_getaffinity failed");
+    g_cpus = (int *)malloc(sizeof(int) * CPU_SETSIZE);
+    if (!g_cpus) die("out of memory");
+    for (c = 0; c < CPU_SETSIZE; c++)
+      if (CPU_ISSET(c, &set)) g_cpus[g_n_cpus++] = c;
+    if (!g_n_cpus) die("empty affinity");
+  }
+  g_core_busy = (unsigned char *)calloc((size_t)g_n_cpus, 1);
+  if (!g_core_busy) die("out of memory");
   g_enc_args = argv + i;
   g_n_enc_args = argc - i;
   n_gops = (frames + gop - 1) / gop;
@@ -192,6 +302,7 @@ int main(int argc, char **argv)
     for (g = 0; g < gpus && next < n_gops; g++)
       while (busy[g] < per_gpu && next < n_gops) {
         runs[next].gpu = g;
+        runs[next].core = g_pin ? take_core(g) : -1;
         start_gop(&runs[next]);
         busy[g]++;
         next++;
@@ -206,6 +317,7 @@ int main(int argc, char **argv)
           runs[i].status = WIFEXITED(st) ? WEXITSTATUS(st) : 128 + (WIFSIGNALED(st) ? WTERMSIG(st) : 0);
           runs[i].me_s = me_time(i);
           busy[runs[i].gpu]--;
+          if (runs[i].core >= 0) g_core_busy[runs[i].core] = 0;
           if (runs[i].status) failed++;
           done++;
           break;
@@ -230,14 +342,20 @@ int main(int argc, char **argv)
     fclose(fr);
   }
   printf("{\"gops\": %d, \"gop\": %d, \"frames\": %d, \"gpus\": %d, \"per_gpu\": %d, \"wall_s\": %.3f, \"failed\": %d, "
-         "\"runs\": [", n_gops, gop, frames, gpus, per_gpu, now_s() - t_start, failed);
-  for (i = 0; i < n_gops; i++)
-    printf("%s{\"gop\": %d, \"gpu\": %d, \"device\": %d, \"first\": %d, \"frames\": %d, \"wall_s\": %.3f, "
-           "\"me_s\": %.3f, \"status\": %d}", i ? ", " : "", i, runs[i].gpu,
-           runs[i].gpu < 64 ? g_dev_map[runs[i].gpu] : runs[i].gpu, runs[i].first, runs[i].count,
+         "\"host_cores\": %d, \"pinned\": %d, \"runs\": [", n_gops, gop, frames, gpus, per_gpu, now_s() - t_start, failed,
+         g_n_cpus, g_pin);
+  for (i = 0; i < n_gops; i++) {
+    char place[64];
+    placement_text(&runs[i], place, sizeof place);
+    printf("%s{\"gop\": %d, \"gpu\": %d, \"device\": %d, \"cpus\": \"%s\", \"first\": %d, \"frames\": %d, "
+           "\"wall_s\": %.3f, \"me_s\": %.3f, \"status\": %d}", i ? ", " : "", i, runs[i].gpu,
+           runs[i].gpu < 64 ? g_dev_map[runs[i].gpu] : runs[i].gpu, place, runs[i].first, runs[i].count,
            runs[i].t1 - runs[i].t0, runs[i].me_s, runs[i].status);
+  }
   printf("]}\n");
   free(runs);
   free(busy);
+  free(g_cpus);
+  free(g_core_busy);
   return failed ? 1 : 0;
 }

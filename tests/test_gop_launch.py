@@ -34,6 +34,14 @@ def _clip(d):
             "-p", "NumberReferenceFrames=2", "-p", "RDOptimization=0"]
 
 
+def _cpulist(text):
+    out = []
+    for part in text.split(","):
+        a, _, b = part.partition("-")
+        out += list(range(int(a), int(b or a) + 1))
+    return out
+
+
 def _md5(p):
     return hashlib.md5(open(p, "rb").read()).hexdigest()
 
@@ -104,6 +112,14 @@ def test_bench_shard_encoder_two_ranks_cpu_rehearsal():
     assert line["parity"] == {"reference": "JM 18.5 lencod (stock, same GOP arguments)", "gops": 4,
                               "byte_identical_gops": 4}
     assert [p["rank"] for p in line["per_rank"]] == [0, 1]
+    # host placement: each rank's encoders on its own cores (its GPU's NUMA-local
+    # share, or its share of the affinity here), disjoint between the ranks
+    sets = [set(_cpulist(p["cpus"])) for p in line["per_rank"]]
+    assert all(sets) and not (sets[0] & sets[1]), line["per_rank"]
+    assert sets[0] | sets[1] <= set(os.sched_getaffinity(0))
+    placed = line["rank0"]["host_placement"]
+    assert placed["source"] in ("numa", "affinity")
+    assert all(set(_cpulist(c)) <= sets[0] for c in placed["per_gop"]), placed
     mbs = sum(p["macroblocks"] for p in line["per_rank"])
     assert mbs == 2 * 2 * 2 * (176 // 16) * (144 // 16)
     assert abs(line["value"] - mbs / max(p["wall_s"] for p in line["per_rank"])) < 0.01 * line["value"] + 1
@@ -135,3 +151,36 @@ def test_gop_launcher_device_map(tmp_path):
     bad = subprocess.run([LAUNCHER, "--encoder", str(enc), "--gpus", "2", "--devices", "5", "--gop", "2",
                           "--frames", "4", "--prefix", prefix, "--"], capture_output=True, text=True, timeout=60)
     assert bad.returncode == 2 and "fewer devices" in bad.stderr
+
+
+@pytest.mark.skipif(not os.path.exists(LAUNCHER), reason="launcher absent")
+def test_gop_launcher_pins_host_cores(tmp_path):
+    """--cpus: the list is cut into one contiguous share per GPU slot and every
+    running encoder holds a core of its slot's share to itself (set with
+    sched_setaffinity between fork and exec); a freed core goes to the next GOP.
+    The stand-in encoder reports the cores it was allowed to run on."""
+    cores = sorted(os.sched_getaffinity(0))
+    if len(cores) < 4:
+        pytest.skip("needs 4 host cores")
+    use = cores[:4]
+    enc = tmp_path / "fake_enc.sh"
+    enc.write_text("#!/bin/sh\ngrep Cpus_allowed_list /proc/self/status\nsleep 0.2\n")
+    enc.chmod(0o755)
+    prefix = str(tmp_path / "g")
+    r = subprocess.run([LAUNCHER, "--encoder", str(enc), "--gpus", "2", "--per-gpu", "2", "--cpus",
+                        ",".join(map(str, use)), "--gop", "1", "--frames", "6", "--prefix", prefix, "--"],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    rep = json.loads(r.stdout.strip().splitlines()[-1])
+    assert rep["pinned"] == 1 and rep["host_cores"] == 4 and rep["failed"] == 0
+    share = {0: set(use[:2]), 1: set(use[2:])}
+    for g in rep["runs"]:
+        log = open(f"{prefix}_gop{g['gop']:03d}.log").read()
+        allowed = log.split(":", 1)[1].strip()
+        assert allowed == g["cpus"] and int(allowed) in share[g["gpu"]], (g, log)
+    # two encoders of a slot run at once: never on the same core
+    first = [g for g in rep["runs"] if g["gop"] < 4]
+    assert len({g["cpus"] for g in first}) == 4, first
+    unpinned = subprocess.run([LAUNCHER, "--encoder", str(enc), "--gpus", "1", "--gop", "1", "--frames", "1",
+                               "--prefix", prefix, "--"], capture_output=True, text=True, timeout=60)
+    assert json.loads(unpinned.stdout.strip().splitlines()[-1])["pinned"] == 0

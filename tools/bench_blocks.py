@@ -357,13 +357,97 @@ def dropin_block(modes=None, size=(1920, 1080), search_range=32, reps=2, host_pr
 # store_picture_in_dpb, JM/lencod/src/mbuffer.c:1905), so the product scales by
 # closed GOPs: integration/jmme_gop.c starts one encoder per GOP (StartFrame /
 # FramesToBeEncoded, JM/lencod/inc/configfile.h:39,47), its GPU fixed in the
-# child's environment before the encoder starts.  These settings are configs[1]'s
-# (FS +-32, 1 ref, RDO off, sub-pel off).
+# child's environment before the encoder starts and, when given a core list, its
+# host cores too.  Two presets:
+#   fs     -- configs[1]'s settings (FS +-32, 1 ref, RDO off, sub-pel off), 1080p;
+#   epzs4k -- configs[3] as configured: 3840x2160, JM/bin/encoder_baseline.cfg's
+#             EPZS keys (quarter-pel grid, SATD sub-pel, RDO on, adaptive
+#             rounding; the file's EPZS section, tests/test_jm_dropin_epzs_gpu.py
+#             BASELINE_EPZS) at level 5.1.
 ENCODER_PARAMS = {"SearchMode": -1, "SearchRange": 32, "NumberReferenceFrames": 1, "RDOptimization": 0}
 
 
+def encoder_preset(name: str):
+    """(JM parameters, (w, h), text for the report) of a GOP-encoder preset"""
+    if name == "fs":
+        return ENCODER_PARAMS, (1920, 1080), "FS +-32, 1 ref, RDO off, sub-pel off (configs[1]'s settings)"
+    if name == "epzs4k":
+        from test_jm_dropin_epzs_gpu import BASELINE_EPZS
+        return (dict(BASELINE_EPZS, NumberReferenceFrames=1, LevelIDC=51), (3840, 2160),
+                "EPZS +-32 (encoder_baseline.cfg's EPZS keys: quarter-pel grid, SATD sub-pel, RDO on, adaptive "
+                "rounding), 1 ref, level 5.1 (configs[3])")
+    raise ValueError(f"unknown encoder preset {name!r}")
+
+
+def _cpulist(text: str) -> list[int]:
+    out = []
+    for part in text.strip().split(","):
+        if not part:
+            continue
+        a, _, b = part.partition("-")
+        out += list(range(int(a), int(b or a) + 1))
+    return out
+
+
+def _kfd_gpu_cpus(index: int) -> list[int] | None:
+    """The host cores local to HIP device `index` (its PCI device's NUMA node),
+    read from sysfs -- the KFD topology's GPU nodes in order, their PCI address,
+    then the device's local_cpulist -- without initialising the GPU.  None when
+    the topology is not readable (CPU containers)."""
+    import os
+    root = "/sys/class/kfd/kfd/topology/nodes"
+    try:
+        nodes = sorted((int(n) for n in os.listdir(root)), key=int)
+        gpus = []
+        for n in nodes:
+            props = dict(ln.split() for ln in open(f"{root}/{n}/properties") if len(ln.split()) == 2)
+            if int(props.get("simd_count", 0)) > 0:
+                gpus.append(props)
+        vis = os.environ.get("ROCR_VISIBLE_DEVICES") or os.environ.get("HIP_VISIBLE_DEVICES")
+        if vis:
+            gpus = [gpus[int(v)] for v in vis.split(",") if v.strip()]
+        props = gpus[index]
+        loc, dom = int(props["location_id"]), int(props.get("domain", 0))
+        bdf = f"{dom:04x}:{loc >> 8:02x}:{(loc >> 3) & 0x1f:02x}.{loc & 7}"
+        return _cpulist(open(f"/sys/bus/pci/devices/{bdf}/local_cpulist").read())
+    except (OSError, ValueError, KeyError, IndexError):
+        return None
+
+
+def gpu_local_cpus(local: int, local_ws: int) -> tuple[list[int], str]:
+    """The host cores rank `local` of `local_ws` runs its encoders on: its GPU's
+    NUMA-local cores that this process may use, split evenly among the local
+    ranks whose GPUs share that NUMA node; without a readable topology, an even
+    split of this process's affinity by local rank.  Returns (cores, source)."""
+    import os
+    allowed = sorted(os.sched_getaffinity(0))
+    mine = _kfd_gpu_cpus(local)
+    if mine:
+        node = [c for c in allowed if c in set(mine)]
+        peers = [r for r in range(local_ws) if _kfd_gpu_cpus(r) == mine]
+        if node and local in peers:
+            k, i = len(peers), peers.index(local)
+            share = node[i * len(node) // k:(i + 1) * len(node) // k] or node
+            return share, "numa"
+    k = max(1, local_ws)
+    share = allowed[local * len(allowed) // k:(local + 1) * len(allowed) // k] or allowed
+    return share, "affinity"
+
+
+def _cpulist_text(cores) -> str:
+    cores = sorted(cores)
+    runs, i = [], 0
+    while i < len(cores):
+        j = i
+        while j + 1 < len(cores) and cores[j + 1] == cores[j] + 1:
+            j += 1
+        runs.append(str(cores[i]) if i == j else f"{cores[i]}-{cores[j]}")
+        i = j + 1
+    return ",".join(runs)
+
+
 def _gop_launch(launcher, encoder, d, tag, yuv, w, h, frames, gop, slots, per_slot, devices, cfg_text, params,
-                timeout=1200):
+                timeout=1200, cpus=None):
     """One jmme_gop run over the clip: returns (report, per-GOP md5 pairs)."""
     import hashlib
     import json
@@ -382,6 +466,8 @@ def _gop_launch(launcher, encoder, d, tag, yuv, w, h, frames, gop, slots, per_sl
            "--frames", str(frames), "--prefix", prefix]
     if devices is not None:
         cmd += ["--devices", ",".join(str(x) for x in devices)]
+    if cpus:
+        cmd += ["--cpus", _cpulist_text(cpus)]
     t0 = time.time()
     r = subprocess.run(cmd + ["--"] + enc_args, cwd=wd, capture_output=True, text=True, timeout=timeout)
     wall = time.time() - t0
@@ -396,16 +482,18 @@ def _gop_launch(launcher, encoder, d, tag, yuv, w, h, frames, gop, slots, per_sl
     return rep, md5
 
 
-def encoder_gop_block(device: int = 0, rank: int = 0, gops: int = 16, gop: int = 4, size=(1920, 1080),
+def encoder_gop_block(device: int = 0, rank: int = 0, gops: int = 16, gop: int = 4, size=None,
                       per_gpu: int = 8, host_procs=None, check_stock: bool = True, encoder=None,
-                      between=None) -> dict | None:
+                      between=None, preset: str = "fs", cpus=None) -> dict | None:
     """One rank's share of the GOP-sharded encoder: `gops` closed GOPs of `gop`
-    frames of a seeded 1080p clip (its own seed per rank) through lencod_jmme on
-    HIP device `device` (`per_gpu` encoders at once), timed wall to wall, then --
-    outside the timed region -- the same GOPs through the stock lencod as
-    concurrent CPU processes (the host baseline: `host_procs` at once), and every
-    GOP's bitstream and reconstruction compared byte for byte.  The caller
-    (this process) never touches the GPU."""
+    frames of a seeded clip (its own seed per rank; the preset's size unless
+    `size` is given) through lencod_jmme on HIP device `device` (`per_gpu`
+    encoders at once; pinned one to a core of `cpus` when given), timed wall to
+    wall, then -- outside the timed region -- the same GOPs through the stock
+    lencod as concurrent CPU processes (the host baseline: `host_procs` at once,
+    on the same cores when `cpus` is given), and every GOP's bitstream and
+    reconstruction compared byte for byte.  The caller (this process) never
+    touches the GPU."""
     import os
     import tempfile
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -417,34 +505,38 @@ def encoder_gop_block(device: int = 0, rank: int = 0, gops: int = 16, gop: int =
         return None
     if host_procs is None:
         from bench import host_cores
-        host_procs = host_cores()
+        host_procs = host_cores() if not cpus else len(cpus)
     from jmme import synth
     from test_jm_dropin_gpu import CFG
-    w, h = size
+    params, psize, ptext = encoder_preset(preset)
+    w, h = size or psize
     frames = gops * gop
     mbs = (w // 16) * ((h + 15) // 16)
     seed = 3000 + rank
     with tempfile.TemporaryDirectory() as d:
         yuv = os.path.join(d, "in.yuv")
         synth.write_yuv420(yuv, synth.luma_sequence(w, h, frames, seed=seed, gmv=(5, 3)))
-        _progress(f"encoder gop block rank {rank}: {gops} GOPs x {gop} frames on device {device}")
+        _progress(f"encoder gop block ({preset}) rank {rank}: {gops} GOPs x {gop} frames on device {device}")
         g_rep, g_md5 = _gop_launch(launcher, gpu, d, "gpu", yuv, w, h, frames, gop, 1, per_gpu, [device], CFG,
-                                   ENCODER_PARAMS)
-        out = {"encoder": os.path.basename(gpu),
+                                   params, cpus=cpus)
+        out = {"encoder": os.path.basename(gpu), "preset": preset,
                "workload": f"JM 18.5 lencod_jmme (ME on the GPU) encoding {gops} closed GOPs of {gop} frames "
-                           f"(1 I + {gop - 1} P) of a seeded {w}x{h} clip, FS +-32, 1 ref, RDO off, sub-pel off; "
-                           f"one encoder process per GOP (integration/jmme_gop.c), {per_gpu} at once on the GPU",
+                           f"(1 I + {gop - 1} P) of a seeded {w}x{h} clip, {ptext}; one encoder process per GOP "
+                           f"(integration/jmme_gop.c), {per_gpu} at once on the GPU",
                "device": device, "clip_seed": seed, "gops": gops, "gop": gop, "frames": frames,
                "macroblocks": frames * mbs, "wall_s": g_rep["python_wall_s"],
                "encoder_mb_per_s": round(frames * mbs / g_rep["python_wall_s"], 1),
                "me_s_per_gop": [r["me_s"] for r in g_rep["runs"]],
-               "me_mb_per_s": round(gops * (gop - 1) * mbs / max(1e-9, sum(r["me_s"] for r in g_rep["runs"])), 1)}
+               "me_mb_per_s": round(gops * (gop - 1) * mbs / max(1e-9, sum(r["me_s"] for r in g_rep["runs"])), 1),
+               "host_placement": {"cpus": _cpulist_text(cpus) if cpus else "unpinned (scheduler)",
+                                  "per_gop": [r.get("cpus") for r in g_rep["runs"]]}}
         if between is not None:   # (ranks meet here: no rank's stock encodes overlap another's timed run)
             between()
         if check_stock:
-            _progress(f"encoder gop block rank {rank}: the same GOPs through the stock encoder, {host_procs} at once")
+            _progress(f"encoder gop block ({preset}) rank {rank}: the same GOPs through the stock encoder, "
+                      f"{min(host_procs, gops)} at once")
             s_rep, s_md5 = _gop_launch(launcher, stock, d, "stock", yuv, w, h, frames, gop, min(host_procs, gops), 1,
-                                       None, CFG, ENCODER_PARAMS)
+                                       None, CFG, params, cpus=cpus)
             same = [a == b for a, b in zip(g_md5, s_md5)]
             out["parity"] = {"reference": "JM 18.5 lencod (stock, same GOP arguments)", "gops": gops,
                              "byte_identical_gops": int(sum(same))}
@@ -452,6 +544,9 @@ def encoder_gop_block(device: int = 0, rank: int = 0, gops: int = 16, gop: int =
                                     "encoder_mb_per_s": round(frames * mbs / s_rep["python_wall_s"], 1),
                                     "me_mb_per_s": round(gops * (gop - 1) * mbs /
                                                          max(1e-9, sum(r["me_s"] for r in s_rep["runs"])), 1),
+                                    "me_s_per_gop": [r["me_s"] for r in s_rep["runs"]],
                                     "kind": "reference"}
             out["encoder_speedup_vs_host"] = round(s_rep["python_wall_s"] / g_rep["python_wall_s"], 2)
+            out["me_speedup_vs_host"] = round(sum(r["me_s"] for r in s_rep["runs"]) /
+                                              max(1e-9, sum(r["me_s"] for r in g_rep["runs"])), 2)
     return out

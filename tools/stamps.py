@@ -54,14 +54,3 @@ if len(wg):
         print(f"  CUs with {k} items: {sel.sum()}  last end ns mean {per_cu_end[sel].mean():.0f} max {per_cu_end[sel].max():.0f}")
     np.save(os.path.join(REPO, "gpurun_out", "stamps_wg.npy"), raw[len(req):n])
 
-try:
-    import ctypes
-    e = (ctypes.c_ulonglong * 2)()
-    lib_ = _lib.lib()
-    lib_.jmme_debug_elim(e)            # reset (counts of the earlier runs)
-    me.search(FULL_SEARCH, req)
-    torch.cuda.synchronize()
-    lib_.jmme_debug_elim(e)
-    print("elimination: wave-tasks %d skipped %d (%.1f %%)" % (e[0], e[1], 100.0 * e[1] / max(1, e[0])))
-except AttributeError:
-    pass
