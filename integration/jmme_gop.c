@@ -29,8 +29,17 @@
  * NUMA-local cores -- and each running child of a slot takes a core of its
  * share to itself while there are enough (the whole share otherwise).
  *
+ * GPU queues: the HIP runtime gives each process up to GPU_MAX_HW_QUEUES (4)
+ * hardware queues, one per stream it uses.  With 8 encoders on one GPU that is
+ * more user queues than the GPU's scheduler keeps mapped at once, and it then
+ * time-slices them: measured on MI355X with 8 concurrent 4K EPZS encodes (whose
+ * searches alone are round trips), JM's ME time per GOP went from 1.3 s to 5.4 s
+ * (tools/exp_gop_queues.py).  So each child gets GPU_MAX_HW_QUEUES =
+ * 16 / per_gpu, clamped to [1, 4] (--hw-queues N overrides, 0 leaves the
+ * environment alone).
+ *
  * Usage:
- *   jmme_gop --encoder PATH --gpus N [--per-gpu K] [--devices D0,D1,..] [--cpus LIST]
+ *   jmme_gop --encoder PATH --gpus N [--per-gpu K] [--devices D0,D1,..] [--cpus LIST] [--hw-queues N]
  *            --gop G --frames F --prefix OUTPREFIX [--concat] -- <encoder arguments>
  * (--devices: the HIP device index each of the N GPU slots stands for; default
  * 0 .. N-1.  A rank-per-GPU caller passes its own device alone.  --cpus: a
@@ -77,6 +86,7 @@ static int g_pin;
 static int *g_cpus, g_n_cpus;      /* host cores the children run on */
 static unsigned char *g_core_busy;  /* per entry of g_cpus: held by a running child */
 static int g_gpus;
+static int g_hw_queues;            /* GPU_MAX_HW_QUEUES for the children (0: inherited) */
 
 /* "0-3,8,10-11" -> cores; returns the count (-1: malformed) */
 static int parse_cpulist(const char *q, int **out)
@@ -191,6 +201,11 @@ static pid_t start_gop(gop_run *r)
     }
     /* the device is fixed before the encoder (and the HIP runtime in it) starts */
     setenv("HIP_VISIBLE_DEVICES", dev, 1);
+    if (g_hw_queues > 0) {
+      char hq[16];
+      snprintf(hq, sizeof hq, "%d", g_hw_queues);
+      setenv("GPU_MAX_HW_QUEUES", hq, 1);
+    }
     execv(g_encoder, argv);
     fprintf(stderr, "jmme_gop: exec %s: %s\n", g_encoder, strerror(errno));
     _exit(127);
@@ -237,6 +252,7 @@ int main(int argc, char **argv)
   gop_run *runs;
   double t_start;
   const char *devices = NULL, *cpus = NULL;
+  int hw_queues = -1;
   for (i = 0; i < 64; i++) g_dev_map[i] = i;
   for (i = 1; i < argc; i++) {
     if (!strcmp(argv[i], "--")) { i++; break; }
@@ -250,6 +266,7 @@ int main(int argc, char **argv)
     else if (!strcmp(argv[i], "--prefix")) g_prefix = argv[++i];
     else if (!strcmp(argv[i], "--devices")) devices = argv[++i];
     else if (!strcmp(argv[i], "--cpus")) cpus = argv[++i];
+    else if (!strcmp(argv[i], "--hw-queues")) hw_queues = atoi(argv[++i]);
     else die("unknown option (see the usage in jmme_gop.c)");
   }
   if (!g_encoder || !g_prefix || gpus < 1 || per_gpu < 1 || gop < 1 || frames < 1)
@@ -267,6 +284,9 @@ int main(int argc, char **argv)
     if (g < gpus) die("--devices names fewer devices than --gpus");
   }
   g_gpus = gpus;
+  if (hw_queues < 0) hw_queues = per_gpu > 4 ? (16 / per_gpu < 1 ? 1 : 16 / per_gpu) : 4;
+  if (hw_queues > 4) hw_queues = 4;
+  g_hw_queues = hw_queues;
   g_pin = cpus != NULL;
   if (cpus) {
     g_n_cpus = parse_cpulist(cpus, &g_cpus);
@@ -342,8 +362,8 @@ int main(int argc, char **argv)
     fclose(fr);
   }
   printf("{\"gops\": %d, \"gop\": %d, \"frames\": %d, \"gpus\": %d, \"per_gpu\": %d, \"wall_s\": %.3f, \"failed\": %d, "
-         "\"host_cores\": %d, \"pinned\": %d, \"runs\": [", n_gops, gop, frames, gpus, per_gpu, now_s() - t_start, failed,
-         g_n_cpus, g_pin);
+         "\"host_cores\": %d, \"pinned\": %d, \"hw_queues\": %d, \"runs\": [", n_gops, gop, frames, gpus, per_gpu,
+         now_s() - t_start, failed, g_n_cpus, g_pin, g_hw_queues);
   for (i = 0; i < n_gops; i++) {
     char place[64];
     placement_text(&runs[i], place, sizeof place);

@@ -132,7 +132,7 @@ def test_gop_launcher_device_map(tmp_path):
     HIP_VISIBLE_DEVICES, set before it starts.  A stand-in encoder script reports
     its environment and arguments into the GOP's log."""
     enc = tmp_path / "fake_enc.sh"
-    enc.write_text("#!/bin/sh\necho \"dev=$HIP_VISIBLE_DEVICES args=$*\"\n"
+    enc.write_text("#!/bin/sh\necho \"dev=$HIP_VISIBLE_DEVICES hq=$GPU_MAX_HW_QUEUES args=$*\"\n"
                    "echo 'Total ME time for sequence        :   0.125 sec'\n")
     enc.chmod(0o755)
     prefix = str(tmp_path / "g")
@@ -146,6 +146,7 @@ def test_gop_launcher_device_map(tmp_path):
     for g in rep["runs"]:
         log = open(f"{prefix}_gop{g['gop']:03d}.log").read()
         assert f"dev={g['device']}" in log and g["device"] == (5, 7)[g["gpu"]], (g, log)
+        assert "hq=4" in log, log   # (one encoder per GPU: the runtime's default queue count, set explicitly)
         assert f"StartFrame={g['first']}" in log and f"FramesToBeEncoded={g['frames']}" in log
         assert g["me_s"] == 0.125
     bad = subprocess.run([LAUNCHER, "--encoder", str(enc), "--gpus", "2", "--devices", "5", "--gop", "2",
@@ -184,3 +185,8 @@ def test_gop_launcher_pins_host_cores(tmp_path):
     unpinned = subprocess.run([LAUNCHER, "--encoder", str(enc), "--gpus", "1", "--gop", "1", "--frames", "1",
                                "--prefix", prefix, "--"], capture_output=True, text=True, timeout=60)
     assert json.loads(unpinned.stdout.strip().splitlines()[-1])["pinned"] == 0
+    # 8 encoders on one GPU: 2 hardware queues each (16 in all), so the GPU's scheduler
+    # keeps every encoder's queues mapped (tools/exp_gop_queues.py)
+    eight = subprocess.run([LAUNCHER, "--encoder", str(enc), "--gpus", "1", "--per-gpu", "8", "--gop", "1",
+                            "--frames", "1", "--prefix", prefix, "--"], capture_output=True, text=True, timeout=60)
+    assert json.loads(eight.stdout.strip().splitlines()[-1])["hw_queues"] == 2

@@ -528,6 +528,7 @@ def encoder_gop_block(device: int = 0, rank: int = 0, gops: int = 16, gop: int =
                "encoder_mb_per_s": round(frames * mbs / g_rep["python_wall_s"], 1),
                "me_s_per_gop": [r["me_s"] for r in g_rep["runs"]],
                "me_mb_per_s": round(gops * (gop - 1) * mbs / max(1e-9, sum(r["me_s"] for r in g_rep["runs"])), 1),
+               "hw_queues_per_encoder": g_rep.get("hw_queues"),
                "host_placement": {"cpus": _cpulist_text(cpus) if cpus else "unpinned (scheduler)",
                                   "per_gop": [r.get("cpus") for r in g_rep["runs"]]}}
         if between is not None:   # (ranks meet here: no rank's stock encodes overlap another's timed run)

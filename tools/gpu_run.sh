@@ -11,6 +11,7 @@
 #   dropin:MODE[:ARGS]  tools/bench_dropin.py --mode MODE (ARGS: comma-separated extra arguments)
 #   py:SCRIPT[:ARGS]    python3 SCRIPT (a tools/ benchmark) with comma-separated arguments
 #   env:NAME=VALUE      export NAME=VALUE for the steps after it (env:NAME= unsets)
+#   info                the box's host placement facts (CPUs, affinity, cgroup limits, the GPU's NUMA cores)
 set -e
 cd "$(dirname "$0")/.."
 R=$(pwd)
@@ -40,7 +41,12 @@ for step in "$@"; do
       bash tools/pmc.sh "$O/pmc" tcc1 tcc2 sq1 sq2
       python3 tools/pmc_summary.py "$O/pmc" --traffic-json "$O/pmc_traffic.json" > "$O/pmc_summary.txt" ;;
     bench)
-      timeout -k 10 600 python3 bench.py $(echo "$arg" | tr ',' ' ') > "$O/bench_$n.json" 2> "$O/bench_$n.err" ;;
+      timeout -k 10 1100 python3 bench.py $(echo "$arg" | tr ',' ' ') > "$O/bench_$n.json" 2> "$O/bench_$n.err" ;;
+    info)
+      { nproc; python3 -c "import os; print('affinity', len(os.sched_getaffinity(0)))";
+        cat /sys/fs/cgroup/cpu.max /sys/fs/cgroup/cpuset.cpus.effective 2>/dev/null || true;
+        python3 -c "import sys; sys.path.insert(0, 'tools'); sys.path.insert(0, 'tests'); import bench_blocks as b; print('gpu0 local cpus', b._kfd_gpu_cpus(0)); print('placement', b.gpu_local_cpus(0, 1))";
+        lscpu | head -30; } > "$O/info.txt" 2>&1 ;;
     dropin)
       mode=${arg%%:*}
       extra=""
