@@ -1412,7 +1412,7 @@ static distblk real_epzs(int variant, Macroblock *currMB, MotionVector *pred_mv,
  * call per search. */
 #define EP_MAXP 128                /* predictors of a list the cache keeps (longer lists: one call each) */
 #define EP_MAXV 64                 /* stamped cells kept per cached answer */
-#define EP_WAYS 6                  /* guesses per (macroblock, partition, reference): the sources' inputs,
+#define EP_WAYS 10                 /* guesses per (macroblock, partition, reference): the sources' inputs,
                                       then their second-pass forms (ep_pass2) */
 #define EP_REFS 4                  /* references speculated (list 0) */
 #define EP_BATCH_MAX 512
@@ -1797,6 +1797,122 @@ static int ep_assumed(int xr, int slot)
   return g_ep_idx[(((size_t)xr * JMME_NSLOT + slot) * EP_REFS + 0) * EP_WAYS];
 }
 
+/* One hypothesis about the rate-distortion decisions a partition's spatial neighbours depend on:
+ * the spatial predictors 1..4 it implies (sp_on 0: keep the guess's own) and the MV predictor */
+#define EP_HYP 9
+typedef struct ep_hyp {
+  int16_t sp[5][2];
+  int sp_on[5], pv_on;
+  int16_t pv[2];
+} ep_hyp;
+static long long g_ep_hyp_guesses = 0;   /* second-pass guesses made for hypotheses 1..8 */
+
+static const int kEpW4[8] = {0, 4, 4, 2, 2, 2, 1, 1}, kEpH4[8] = {0, 4, 2, 4, 2, 1, 2, 1};
+
+/* the refined answer the batch assumes for (macroblock mb0 + xr, block type m at 4x4 position (x4, y4)),
+ * or 0 when it has none */
+static int ep_refined_at(int xr, int m, int x4, int y4, int16_t v[2])
+{
+  const int pk = ep_assumed(xr, jmme_slot(m, x4 - x4 % kEpW4[m], y4 - y4 % kEpH4[m]));
+  const ep_ans *pa = pk >= 0 ? &g_ep_ans[pk] : NULL;
+  if (!pa || !pa->spq.blocktype) return 0;
+  v[0] = pa->sp_res.mv_x;
+  v[1] = pa->sp_res.mv_y;
+  return 1;
+}
+
+/* hypothesis h's neighbours of slot t (block type bt at (bx, by)) of macroblock x; returns whether any
+ * neighbour was decided under it (else hypothesis h is hypothesis 0) */
+static int ep_neighbours(ep_hyp *H, int h, int x, int mb0, int bt, int bx, int by, VideoParameters *p_Vid)
+{
+  static const int16_t kNone[5][2] = {{0, 0}, {12, 0}, {0, 12}, {-12, 0}, {0, -12}};   /* unavailable */
+  const int x4 = bx >> 2, y4 = by >> 2, w4 = kEpW4[bt];
+  const int mbx4 = (x % g_mbs_x) * 4, mby4 = (x / g_mbs_x) * 4, W4 = p_Vid->width >> 2;
+  PicMotionParams **mvi = p_Vid->enc_picture->mv_info;
+  const int nx[5] = {0, x4 - 1, x4, x4 + w4, x4 - 1}, ny[5] = {0, y4, y4 - 1, y4 - 1, y4 - 1};
+  int st[5] = {0, 0, 0, 0, 0}, nref[5] = {0, 0, 0, 0, 0};   /* 1 known, 0 not known, -1 unavailable; refs */
+  int j, dep = 0;
+  memset(H, 0, sizeof *H);
+  for (j = 1; j <= 4; j++) {
+    const int px4 = mbx4 + nx[j], py4 = mby4 + ny[j];
+    if (px4 < 0 || py4 < 0 || px4 >= W4) { st[j] = -1; continue; }
+    if (j == 3 && !ep_avail_c(bx, by, 4 * w4)) { st[j] = -1; continue; }
+    if (nx[j] >= 0 && nx[j] <= 3 && ny[j] >= 0) {   /* inside this macroblock */
+      const int decided = bt >= 4 && ((nx[j] >> 1) != (x4 >> 1) || (ny[j] >> 1) != (y4 >> 1));
+      const int m = decided && h >= 4 && h <= 7 ? h : bt;
+      if (decided && m != bt) dep = 1;
+      if (ep_refined_at(x - mb0, m, nx[j], ny[j], H->sp[j])) st[j] = 1;
+    } else if (ny[j] >= 0 && nx[j] < 0 && x - 1 >= mb0) {   /* the left macroblock, in this batch */
+      if (h >= 1 && h <= 7) {
+        if (ep_refined_at(x - 1 - mb0, h, 3, ny[j], H->sp[j])) { st[j] = 1; dep = 1; }
+      } else if (h == 8) {   /* P_Skip: the 16x16 MV predictor (FindSkipModeMotionVector) */
+        const int pk = ep_assumed(x - 1 - mb0, 0);
+        if (pk >= 0) {
+          H->sp[j][0] = g_ep_ans[pk].in.q.pred_x;
+          H->sp[j][1] = g_ep_ans[pk].in.q.pred_y;
+          st[j] = 1;
+          dep = 1;
+        }
+      }
+    } else if (ny[j] < 0 || x - 1 < mb0) {   /* a macroblock JM has decided: its mv_info */
+      const PicMotionParams *mp = &mvi[py4][px4];
+      if (mp->ref_idx[0] == 0 || (mp->mv[0].mv_x == 0 && mp->mv[0].mv_y == 0)) {
+        H->sp[j][0] = mp->mv[0].mv_x;
+        H->sp[j][1] = mp->mv[0].mv_y;
+        nref[j] = mp->ref_idx[0];
+        st[j] = 1;
+      }
+    }
+  }
+  if (st[3] < 0) {   /* get_neighbors: an unavailable up-right is the up-left (mv_search.c:303-306) */
+    st[3] = st[4];
+    nref[3] = nref[4];
+    H->sp[3][0] = H->sp[4][0];
+    H->sp[3][1] = H->sp[4][1];
+  }
+  for (j = 1; j <= 4; j++) {
+    if (st[j] < 0) { H->sp[j][0] = kNone[j][0]; H->sp[j][1] = kNone[j][1]; }
+    if (st[j] == 0) { H->sp[j][0] = H->sp[j][1] = 0; }
+    H->sp_on[j] = st[j] != 0;
+  }
+  /* the block's MV predictor from the same neighbours (GetMotionVectorPredictorNormal,
+   * lcommon/src/mv_prediction.c:192-300: one matching reference, the 8x16 / 16x8 directions, else
+   * the median), ref 0; unknown when a neighbour is */
+  if (st[1] && st[2] && st[3]) {
+    const int aL = st[1] > 0, aU = st[2] > 0, aR = st[3] > 0;
+    const int rL = aL ? nref[1] : -1, rU = aU ? nref[2] : -1, rR = aR ? nref[3] : -1;
+    const int bsx = (bt <= 2) ? 16 : (bt <= 5) ? 8 : 4;
+    const int bsy = (bt == 1 || bt == 3) ? 16 : (bt == 2 || bt == 4 || bt == 6) ? 8 : 4;
+    int type = 0;   /* 0 median, 1 left, 2 up, 3 up-right */
+    if (rL == 0 && rU != 0 && rR != 0) type = 1;
+    else if (rL != 0 && rU == 0 && rR != 0) type = 2;
+    else if (rL != 0 && rU != 0 && rR == 0) type = 3;
+    if (bsx == 8 && bsy == 16) {
+      if (bx == 0) { if (rL == 0) type = 1; } else if (rR == 0) type = 3;
+    } else if (bsx == 16 && bsy == 8) {
+      if (by == 0) { if (rU == 0) type = 2; } else if (rL == 0) type = 1;
+    }
+    if (type == 0) {
+      if (!(aU || aR)) {
+        H->pv[0] = aL ? H->sp[1][0] : 0;
+        H->pv[1] = aL ? H->sp[1][1] : 0;
+      } else {
+        int k2;
+        for (k2 = 0; k2 < 2; k2++) {
+          const int va = aL ? H->sp[1][k2] : 0, vb = aU ? H->sp[2][k2] : 0, vc = aR ? H->sp[3][k2] : 0;
+          H->pv[k2] = (int16_t)(va + vb + vc - imin(va, imin(vb, vc)) - imax(va, imax(vb, vc)));
+        }
+      }
+    } else {
+      const int jn = type, av = jn == 1 ? aL : jn == 2 ? aU : aR;
+      H->pv[0] = av ? H->sp[jn][0] : 0;
+      H->pv[1] = av ? H->sp[jn][1] : 0;
+    }
+    H->pv_on = 1;
+  }
+  return dep;
+}
+
 static void ep_pass2(Macroblock *currMB, int mb0, int s0, int nmb, unsigned gen, int *n_io, int third)
 {
   VideoParameters *p_Vid = currMB->p_Vid;
@@ -1880,84 +1996,23 @@ static void ep_pass2(Macroblock *currMB, int mb0, int s0, int nmb, unsigned gen,
         /* the spatial predictors of neighbours inside this macroblock (EPZS_spatial_predictors,
          * me_epzs_common.c:1276-1370: left, up, up-right -- the up-left when get_neighbors,
          * mv_search.c:283-306, makes it unavailable -- and up-left): JM reads mv_info there, which
-         * held the refined answer of the same block type's partition at that place in 95-98 % of the
-         * misses dumped (JMME_EPZS_DUMP); ref 0, so scale_mv is the identity */
-        int16_t sp[5][2] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}};
-        int sp_on[5] = {0, 0, 0, 0, 0};
-        int st[5] = {0, 0, 0, 0, 0}, nref[5] = {0, 0, 0, 0, 0};   /* 1 known, 0 not known, -1 unavailable; refs */
-        {
-          static const int kW4[8] = {0, 4, 4, 2, 2, 2, 1, 1}, kH4[8] = {0, 4, 2, 4, 2, 1, 2, 1};
-          static const int16_t kNone[5][2] = {{0, 0}, {12, 0}, {0, 12}, {-12, 0}, {0, -12}};   /* unavailable */
-          const int x4 = bx >> 2, y4 = by >> 2, w4 = kW4[bt], h4 = kH4[bt];
-          const int mbx4 = (x % g_mbs_x) * 4, mby4 = (x / g_mbs_x) * 4, W4 = p_Vid->width >> 2;
-          PicMotionParams **mvi = p_Vid->enc_picture->mv_info;
-          int j;
-          const int nx[5] = {0, x4 - 1, x4, x4 + w4, x4 - 1}, ny[5] = {0, y4, y4 - 1, y4 - 1, y4 - 1};
-          for (j = 1; j <= 4; j++) {
-            const int px4 = mbx4 + nx[j], py4 = mby4 + ny[j];
-            if (px4 < 0 || py4 < 0 || px4 >= W4) { st[j] = -1; continue; }
-            if (j == 3 && !ep_avail_c(bx, by, 4 * w4)) { st[j] = -1; continue; }
-            if (nx[j] >= 0 && nx[j] <= 3 && ny[j] >= 0) {   /* inside: the same block type's refined answer */
-              const int pk = ep_assumed(x - mb0, jmme_slot(bt, nx[j] - nx[j] % w4, ny[j] - ny[j] % h4));
-              const ep_ans *pa = pk >= 0 ? &g_ep_ans[pk] : NULL;
-              if (pa && pa->spq.blocktype) { sp[j][0] = pa->sp_res.mv_x; sp[j][1] = pa->sp_res.mv_y; st[j] = 1; }
-            } else if (ny[j] < 0 || x - 1 < mb0) {   /* a macroblock JM has decided: its mv_info */
-              const PicMotionParams *mp = &mvi[py4][px4];
-              if (mp->ref_idx[0] == 0 || (mp->mv[0].mv_x == 0 && mp->mv[0].mv_y == 0)) {
-                sp[j][0] = mp->mv[0].mv_x;
-                sp[j][1] = mp->mv[0].mv_y;
-                nref[j] = mp->ref_idx[0];
-                st[j] = 1;
-              }
-            }
-          }
-          if (st[3] < 0) {   /* get_neighbors: an unavailable up-right is the up-left (mv_search.c:303-306) */
-            st[3] = st[4];
-            nref[3] = nref[4];
-            sp[3][0] = sp[4][0];
-            sp[3][1] = sp[4][1];
-          }
-          for (j = 1; j <= 4; j++) {
-            if (st[j] < 0) { sp[j][0] = kNone[j][0]; sp[j][1] = kNone[j][1]; }
-            sp_on[j] = st[j] != 0;
-          }
-        }
-        /* the block's MV predictor from the same neighbours (GetMotionVectorPredictorNormal,
-         * lcommon/src/mv_prediction.c:192-300: one matching reference, the 8x16 / 16x8 directions, else
-         * the median), ref 0; unknown when a neighbour is */
-        int pv_on = 0;
-        int16_t pv[2] = {0, 0};
-        if (st[1] && st[2] && st[3]) {
-          const int aL = st[1] > 0, aU = st[2] > 0, aR = st[3] > 0;
-          const int rL = aL ? nref[1] : -1, rU = aU ? nref[2] : -1, rR = aR ? nref[3] : -1;
-          const int bsx = (g_slot_bt[t] <= 2) ? 16 : (g_slot_bt[t] <= 5) ? 8 : 4;
-          const int bsy = (bt == 1 || bt == 3) ? 16 : (bt == 2 || bt == 4 || bt == 6) ? 8 : 4;
-          int type = 0;   /* 0 median, 1 left, 2 up, 3 up-right */
-          if (rL == 0 && rU != 0 && rR != 0) type = 1;
-          else if (rL != 0 && rU == 0 && rR != 0) type = 2;
-          else if (rL != 0 && rU != 0 && rR == 0) type = 3;
-          if (bsx == 8 && bsy == 16) {
-            if (bx == 0) { if (rL == 0) type = 1; } else if (rR == 0) type = 3;
-          } else if (bsx == 16 && bsy == 8) {
-            if (by == 0) { if (rU == 0) type = 2; } else if (rL == 0) type = 1;
-          }
-          if (type == 0) {
-            if (!(aU || aR)) {
-              pv[0] = aL ? sp[1][0] : 0;
-              pv[1] = aL ? sp[1][1] : 0;
-            } else {
-              int k2;
-              for (k2 = 0; k2 < 2; k2++) {
-                const int va = aL ? sp[1][k2] : 0, vb = aU ? sp[2][k2] : 0, vc = aR ? sp[3][k2] : 0;
-                pv[k2] = (int16_t)(va + vb + vc - imin(va, imin(vb, vc)) - imax(va, imax(vb, vc)));
-              }
-            }
-          } else {
-            const int jn = type, av = jn == 1 ? aL : jn == 2 ? aU : aR;
-            pv[0] = av ? sp[jn][0] : 0;
-            pv[1] = av ? sp[jn][1] : 0;
-          }
-          pv_on = 1;
+         * holds the refined answer of the same block type's partition at that place (set_me_parameters
+         * after each search) -- except where rate-distortion decisions wrote it: an 8x8 block of this
+         * macroblock already decided holds its chosen sub-mode's vectors (set_ref_and_motion_vectors,
+         * mode_decision_P8x8.c:40-320), and the macroblock to the left, when it lies in this batch, its
+         * final mode's.  Those are branched over (ep_hyp): hypothesis 0 as above (the same block type
+         * inside, the left macroblock unknown), 1..7 that mode decided there (inside: sub-modes 4..7),
+         * 8 a skipped left macroblock (its 16x16 predictor).  ref 0, so scale_mv is the identity */
+        ep_hyp hyp[EP_HYP];
+        int n_hyp = 0, hh;
+        for (hh = 0; hh < EP_HYP; hh++) {
+          ep_hyp *H = &hyp[n_hyp];
+          int dep = ep_neighbours(H, hh, x, mb0, bt, bx, by, p_Vid);
+          int e;
+          if (hh > 0 && !dep) continue;       /* no decided neighbour: the same as hypothesis 0 */
+          for (e = 0; e < n_hyp; e++)
+            if (!memcmp(&hyp[e], H, sizeof *H)) break;
+          if (e == n_hyp) ++n_hyp;
         }
         /* the spatial-memory predictors (EPZS_spatial_memory_predictors, me_epzs_common.c:1675-1718,
          * EPZSREF): p_motion[ref][blocktype - 1][block row][picture column] at the left, up and up-right
@@ -1996,9 +2051,13 @@ static void ep_pass2(Macroblock *currMB, int mb0, int s0, int nmb, unsigned gen,
             if (vx | vy) { mem[n_mem][0] = vx; mem[n_mem][1] = vy; ++n_mem; }
           }
         }
-        for (w = 0; w < nw0 && nw < EP_WAYS; w++) {
+        for (w = 0; w < nw0 && nw < EP_WAYS; w++)
+        for (hh = 0; hh < (w == 0 ? n_hyp : 1) && nw < EP_WAYS; hh++) {
           const ep_ans *a = &g_ep_ans[idx[w]];
           const ep_in *in = &a->in;
+          const int16_t (*sp)[2] = hyp[hh].sp;
+          const int *sp_on = hyp[hh].sp_on, pv_on = hyp[hh].pv_on;
+          const int16_t *pv = hyp[hh].pv;
           const int np = a->in.q.n_pred, bs = a->in.bt_start & 0xffff, me = a->in.bt_start >> 16;
           const int16_t *ap = (const int16_t *)a->in.pred;
           int fixed = 0, j, o;
@@ -2052,9 +2111,14 @@ static void ep_pass2(Macroblock *currMB, int mb0, int s0, int nmb, unsigned gen,
               break;
           }
           if (k < nw0) continue;
+          for (k = nw0; k < nw; k++)     /* one added by this pass already (another hypothesis, the same list) */
+            if (ep_same(&g_ep_ans[idx[k]].in, &in->q, (const int16_t *)in->pred, in->cond)) break;
+          if (k < nw) continue;
           ep_add(n, in, px, py, p_EPZS);
           g_ep_q[n].stop_crit = stop;
           g_ep_q[n].prev_sad = prev;
+          ep_fill_in(&g_ep_ans[n].in, &g_ep_q[n], (const int16_t *)in->pred, in->cond, -1, gen);   /* (dedup above) */
+          if (hh > 0) ++g_ep_hyp_guesses;
           if (!third && w == 0 && in == &g_ep_fix) g_ep_alt[(x - mb0) * JMME_NSLOT + t] = n;   /* (for the third pass) */
           idx[nw++] = n++;
         }
@@ -2468,9 +2532,11 @@ static void report(void)
       fprintf(stderr, "jm_gpu_me: EPZS speculation: %lld searches answered from %lld batches (%lld guesses), "
                       "%lld searched alone; %lld not speculated; guesses refused: %lld inputs, %lld bounds, "
                       "%lld map cells; %.1f ms building batches; %lld searched again (more stamped cells than kept); "
-                      "%lld second-pass guesses in %lld launches (%lld with lists rebuilt from the batch's answers)\n",
+                      "%lld second-pass guesses in %lld launches (%lld with lists rebuilt from the batch's answers, %lld for "
+                      "decided-neighbour hypotheses)\n",
               g_ep_hits, g_ep_batches, g_ep_guesses, g_ep_singles, g_ep_direct, g_ep_fail_inputs, g_ep_fail_bounds,
-              g_ep_fail_stale, g_t_ep_build * 1e-3, g_ep_overflow, g_ep_pass2, g_ep_pass2_batches, g_ep_list_fixes);
+              g_ep_fail_stale, g_t_ep_build * 1e-3, g_ep_overflow, g_ep_pass2, g_ep_pass2_batches, g_ep_list_fixes,
+              g_ep_hyp_guesses);
     if (g_epzs_calls && g_ep_batches)
       fprintf(stderr, "jm_gpu_me: EPZS host clocks: %.1f ms running guesses (%.1f ms of it in the library), %.1f ms in the "
                       "second and third passes (with their runs), %.1f ms in %lld lookups (JMME_EPZS_TRACE=1 only)\n",
