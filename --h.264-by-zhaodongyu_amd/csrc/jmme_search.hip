@@ -104,8 +104,17 @@ struct Lds {
 // words per window row in LDS: the 2R+13 words a row needs, rounded up to the
 // expand's groups of 4 (it writes whole groups, 16-B aligned: one ds_write_b128);
 // every launch up to R = 32 uses the R = 32 pitch, a compile-time constant of
-// the sweep (its row offsets then fold into the ds_read2 offset fields)
-constexpr int kWP32 = 80;
+// the sweep (its row offsets then fold into the ds_read2 offset fields).
+// 84, not the 80 a row needs: the sweep's last wave-task (window column 64 at
+// R = 32) has its 13 lanes 5 rows apart, and ds_read2_b32 banks are (a/4) mod 32
+// -- with 80 they fell on 2 banks (up to 7-way conflicts), with 84 on 8 (at most
+// 2-way): SQ_LDS_BANK_CONFLICT 9.0e6 -> 4.4e6 cycles per 1080p launch
+// (profiles/round6/lds_pitch/)
+#ifndef JMME_WP32
+#define JMME_WP32 84
+#endif
+constexpr int kWP32 = JMME_WP32;
+static_assert(kWP32 % 4 == 0 && kWP32 >= 80, "window pitch: whole 16-B groups of the 80 words a row needs at R = 32");
 __host__ __device__ inline int words_pitch(int R) { return R <= 32 ? kWP32 : 4 * ((2 * R + 13 + 3) / 4); }
 // 16-bit planes (SourceBitDepthLuma 9..14, KEY32 = false only): word[y][x] =
 // samples x, x + 1 (a 4-sample chunk is words x and x + 2), 2R + 15 words a
