@@ -160,6 +160,12 @@ struct jmme_ctx {
   double ep_us[2] = {};                      // JMME_PHASES: jmme_epzs_speculate time, searches alone / batches
   long long ep_n[2] = {};
   long long ph_calls = 0, ph_big = 0;
+  // jmme_residual4x4: parameter sets, requests and results in one mapped pinned
+  // block the kernel reads and writes across PCIe (a few blocks per call)
+  uint8_t *h_rq = nullptr;
+  void *dv_rq = nullptr;
+  size_t cap_rq = 0;
+  hipStream_t rq_stream = nullptr;
 };
 
 namespace {
@@ -450,6 +456,8 @@ extern "C" void jmme_destroy(jmme_ctx *ctx) {
     fprintf(stderr, "jmme EPZS calls: %lld alone, %.1f ms (%.2f us each); %lld batches, %.1f ms\n", ctx->ep_n[0],
             ctx->ep_us[0] / 1e3, ctx->ep_us[0] / std::max(1ll, ctx->ep_n[0]), ctx->ep_n[1], ctx->ep_us[1] / 1e3);
   if (ctx->h_chk) (void)hipHostFree(ctx->h_chk);
+  if (ctx->rq_stream) (void)hipStreamDestroy(ctx->rq_stream);
+  if (ctx->h_rq) (void)hipHostFree(ctx->h_rq);
   (void)server_stop(ctx);   // (the guard above has stopped it already)
   if (ctx->srv_stream) (void)hipStreamDestroy(ctx->srv_stream);
   if (ctx->h_box) (void)hipHostFree(ctx->h_box);
@@ -1280,6 +1288,43 @@ extern "C" int jmme_quant4x4(jmme_ctx *ctx, const jmme_quant4x4_params *params, 
   HIPCHK(hipMemcpy(runs, dr.p, (size_t)n * 64, hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(coeff_cost, dk.p, (size_t)n * 4, hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(nonzero, dn.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+extern "C" int jmme_residual4x4(jmme_ctx *ctx, const jmme_quant4x4_params *params, int n_params,
+                                const jmme_resid4x4_req *req, jmme_resid4x4_res *res, int n) {
+  DevGuard dg_(ctx);
+  if (!ctx) return fail("null ctx");
+  if (n <= 0) return n < 0 ? fail("negative block count") : 0;
+  if (!params || n_params <= 0 || !req || !res) return fail("null array");
+  for (int p = 0; p < n_params; ++p) {
+    const jmme_quant4x4_params &q = params[p];
+    if (q.qp_per < 0 || q.qp_per > 16) return fail("quant set %d: qp_per %d out of range", p, q.qp_per);
+    for (int k = 0; k < 16; ++k)
+      if (q.scan[k][0] > 3 || q.scan[k][1] > 3) return fail("quant set %d: scan entry %d outside 4x4", p, k);
+  }
+  for (int b = 0; b < n; ++b) {
+    if (req[b].param < 0 || req[b].param >= n_params) return fail("block %d: parameter set %d of %d", b, req[b].param, n_params);
+    if (req[b].max_pel <= 0 || req[b].max_pel > 0xffff) return fail("block %d: max_pel %d", b, req[b].max_pel);
+  }
+  const size_t pb = (sizeof(jmme_quant4x4_params) * n_params + 255) & ~(size_t)255;
+  const size_t qb = (sizeof(jmme_resid4x4_req) * n + 255) & ~(size_t)255, rb = sizeof(jmme_resid4x4_res) * n;
+  if (pb + qb + rb > ctx->cap_rq) {
+    if (ctx->h_rq) HIPCHK(hipHostFree(ctx->h_rq));
+    ctx->h_rq = nullptr;
+    ctx->cap_rq = std::max(pb + qb + rb, (size_t)1 << 16);
+    HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_rq), ctx->cap_rq, hipHostMallocMapped | hipHostMallocCoherent));
+    HIPCHK(hipHostGetDevicePointer(&ctx->dv_rq, ctx->h_rq, 0));
+  }
+  if (!ctx->rq_stream) HIPCHK(hipStreamCreateWithFlags(&ctx->rq_stream, hipStreamNonBlocking));
+  std::memcpy(ctx->h_rq, params, sizeof(jmme_quant4x4_params) * n_params);
+  std::memcpy(ctx->h_rq + pb, req, sizeof(jmme_resid4x4_req) * n);
+  uint8_t *dv = static_cast<uint8_t *>(ctx->dv_rq);
+  HIPCHK(launch_residual4x4(reinterpret_cast<const jmme_quant4x4_params *>(dv),
+                            reinterpret_cast<const jmme_resid4x4_req *>(dv + pb),
+                            reinterpret_cast<jmme_resid4x4_res *>(dv + pb + qb), n, ctx->rq_stream));
+  HIPCHK(hipStreamSynchronize(ctx->rq_stream));
+  std::memcpy(res, ctx->h_rq + pb + qb, rb);
   return 0;
 }
 

@@ -482,6 +482,79 @@ __global__ __launch_bounds__(kWG8) void quant4x4_kernel(const jmme_quant4x4_para
   }
 }
 
+// residual_transform_quant_luma_4x4 (JM/lencod/src/block.c:660-724) of inter
+// blocks, whole: check_zero, forward4x4, quant_4x4_normal, and -- when a level
+// survives -- inverse4x4 and sample_reconstruct (lcommon/src/blk_prediction.c:48-62,
+// dq_bits = DQ_BITS = 6), else the prediction copied.  One lane per block: the
+// drop-in hands over the four 4x4 blocks of an 8x8 prediction at a time, so this
+// is a latency path (a handful of blocks per launch), and the quantisation walks
+// the scan in JM's order with JM's run counting.
+__global__ __launch_bounds__(64) void residual4x4_kernel(const jmme_quant4x4_params *__restrict__ params,
+                                                         const jmme_resid4x4_req *__restrict__ req,
+                                                         jmme_resid4x4_res *__restrict__ res, int n) {
+  const int b = blockIdx.x * 64 + threadIdx.x;
+  if (b >= n) return;
+  const jmme_resid4x4_req &q = req[b];
+  jmme_resid4x4_res &o = res[b];
+  int ores[16], coef[16];
+  int any = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) { ores[k] = q.ores[k]; any |= ores[k]; }
+  o.zero = any == 0;
+  o.nonzero = 0;
+  o.cost = 0;
+  if (!any) {   // check_zero: no coefficients; JM stores ACLevel[0] = 0 and copies the prediction
+    o.levels[0] = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) o.recon[k] = q.pred[k];
+    return;
+  }
+  const jmme_quant4x4_params &P = params[q.param];
+  transform_one<JMME_TF_FORWARD4x4>(ores, coef);
+  const int qp_per = P.qp_per, q_bits = 15 + qp_per;   // Q_BITS, defines.h:311
+  int run = 0, nl = 0, cost = 0, nonzero = 0;
+  for (int c = 0; c < 16; ++c) {   // quant_4x4_normal, quant4x4_normal.c:68-106
+    const int i = P.scan[c][0], j = P.scan[c][1], pos = 4 * j + i;
+    const int v = coef[pos];
+    if (v != 0) {
+      int level = (abs(v) * P.scale[pos] + P.offset[pos]) >> q_bits;
+      if (level != 0) {
+        if (P.is_cavlc) level = min(level, 2063);   // CAVLC_LEVEL_LIMIT, defines.h:99
+        cost += level > 1 ? 999999 : P.c_cost[run];   // MAX_VALUE, defines.h:123
+        level = v < 0 ? -level : level;
+        coef[pos] = ((level * P.inv_scale[pos] << qp_per) + 8) >> 4;   // rshift_rnd_sf(., 4)
+        o.levels[nl] = level;
+        o.runs[nl] = run;
+        ++nl;
+        run = 0;
+        nonzero = 1;
+      } else {
+        coef[pos] = 0;
+        ++run;
+      }
+    } else {
+      ++run;
+    }
+  }
+  o.levels[nl] = 0;
+  o.cost = cost;
+  o.nonzero = nonzero;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) o.coef[k] = coef[k];
+  if (nonzero) {
+    int rres[16];
+    transform_one<JMME_TF_INVERSE4x4>(coef, rres);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      o.rres[k] = rres[k];
+      o.recon[k] = (jmme_imgpel)min(max(((rres[k] + 32) >> 6) + (int)q.pred[k], 0), q.max_pel);
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) o.recon[k] = q.pred[k];
+  }
+}
+
 int grid_for(int n, int per_wg = 64) {
   const int g = (n + per_wg - 1) / per_wg;
   return g < 1 ? 1 : (g > 8192 ? 8192 : g);
@@ -528,6 +601,12 @@ hipError_t launch_quant4x4(const jmme_quant4x4_params *params, const int32_t *pa
   else
     hipLaunchKernelGGL(quant4x4_kernel<true>, grid, dim3(kWG8), 0, s, params, param_idx, coef, levels, runs,
                        coeff_cost, nonzero, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_residual4x4(const jmme_quant4x4_params *params, const jmme_resid4x4_req *req,
+                              jmme_resid4x4_res *res, int n, hipStream_t s) {
+  hipLaunchKernelGGL(residual4x4_kernel, dim3((n + 63) / 64), dim3(64), 0, s, params, req, res, n);
   return hipGetLastError();
 }
 

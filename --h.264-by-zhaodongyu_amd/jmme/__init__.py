@@ -6,6 +6,7 @@ buffers, the IntPelME search contract) over the C ABI of libjmme.so
 """
 from ._lib import (BLK_CHECK00, BLOCK_REQ, BLOCK_RES, DISTBLK_MAX, EPZS_BOUNDS, EPZS_REQ, EPZS_RES,  # noqa: F401
                    FAST_FULL_SEARCH,
-                   FRACTAL_MB, FRACTAL_NODE, FRACTAL_REQ, FRACTAL_RES, FULL_SEARCH, MB_REQ, NSLOT, QUANT4x4_PARAMS,
+                   FRACTAL_MB, FRACTAL_NODE, FRACTAL_REQ, FRACTAL_RES, FULL_SEARCH, MB_REQ, NSLOT, QUANT4x4_PARAMS, RESID4x4_REQ,
+                   RESID4x4_RES,
                    SP_CHECK0, SP_TEST8x8, SUBPEL_REQ, TRANSFORM_OPS, JmmeError)
 from .engine import MotionEstimator, config_from_cfg, slot_of, spiral  # noqa: F401

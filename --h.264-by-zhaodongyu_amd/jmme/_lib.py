@@ -66,11 +66,16 @@ SP_TEST8x8, SP_CHECK0 = 1, 2
 SUBPEL_PAD_Y, SUBPEL_PAD_X = 20, 32
 QUANT4x4_PARAMS = np.dtype([("scale", "<i4", (16,)), ("offset", "<i4", (16,)), ("inv_scale", "<i4", (16,)),
                             ("qp_per", "<i4"), ("is_cavlc", "<i4"), ("scan", "u1", (16, 2)), ("c_cost", "u1", (16,))])
+RESID4x4_REQ = np.dtype([("ores", "<i4", (16,)), ("pred", "<u2", (16,)), ("param", "<i4"), ("max_pel", "<i4")])
+RESID4x4_RES = np.dtype([("coef", "<i4", (16,)), ("rres", "<i4", (16,)), ("levels", "<i4", (17,)),
+                         ("runs", "<i4", (16,)), ("cost", "<i4"), ("nonzero", "<i4"), ("zero", "<i4"),
+                         ("recon", "<u2", (16,))])
 TRANSFORM_OPS = {"forward4x4": (0, 16, 16), "inverse4x4": (1, 16, 16), "hadamard4x4": (2, 16, 16),
                  "ihadamard4x4": (3, 16, 16), "hadamard4x2": (4, 8, 8), "ihadamard4x2": (5, 8, 8),
                  "hadamard2x2": (6, 4, 4), "ihadamard2x2": (7, 4, 4), "forward8x8": (8, 64, 64),
                  "inverse8x8": (9, 64, 64)}   # name -> (jmme_transform_op, in elems, out elems)
 assert BLOCK_REQ.itemsize == 16 and MB_REQ.itemsize == 688 and BLOCK_RES.itemsize == 16
+assert RESID4x4_REQ.itemsize == 104 and RESID4x4_RES.itemsize == 304
 assert QUANT4x4_PARAMS.itemsize == 248 and FRACTAL_REQ.itemsize == 8 and FRACTAL_RES.itemsize == 32
 assert FRACTAL_NODE.itemsize == 40 and FRACTAL_MB.itemsize == 848
 assert EPZS_REQ.itemsize == 80 and EPZS_RES.itemsize == 32 and SUBPEL_REQ.itemsize == 48
@@ -136,6 +141,7 @@ def lib() -> ctypes.CDLL:
         "jmme_satd": (I, [P, I, P, P, I]),
         "jmme_satd_async": (I, [P, I, P, P, I, P]),
         "jmme_quant4x4": (I, [P, P, I, P, P, P, P, P, P, I]),
+        "jmme_residual4x4": (I, [P, P, I, P, P, I]),
         "jmme_fractal_search": (I, [P, P, P, I, I, I, I, P, I, P]),
         "jmme_fractal_words_async": (I, [P, P, I, I, I, P, P]),
         "jmme_fractal_search_async": (I, [P, P, I, P, I, I, I, P, I, P, P]),

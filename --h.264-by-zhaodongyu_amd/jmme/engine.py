@@ -207,6 +207,23 @@ class MotionEstimator:
                                   ptr(coef), ptr(levels), ptr(runs), ptr(cost), ptr(nz), n))
         return coef, levels, runs, cost, nz
 
+    def residual4x4(self, params: np.ndarray, ores: np.ndarray, pred: np.ndarray, param_idx=None,
+                    max_pel: int = 255) -> np.ndarray:
+        """residual_transform_quant_luma_4x4 of n inter blocks (JM/lencod/src/block.c:660-724):
+        ores / pred [n, 16] -> RESID4x4_RES records (what JM leaves: levels, runs, cost,
+        nonzero, the dequantised block, mb_rres and the reconstruction)."""
+        params = np.ascontiguousarray(params, _lib.QUANT4x4_PARAMS).reshape(-1)
+        ores = np.asarray(ores, np.int32).reshape(-1, 16)
+        n = ores.shape[0]
+        req = np.zeros(n, _lib.RESID4x4_REQ)
+        req["ores"] = ores
+        req["pred"] = np.asarray(pred).reshape(n, 16)
+        req["param"] = 0 if param_idx is None else np.asarray(param_idx, np.int32).reshape(n)
+        req["max_pel"] = max_pel
+        res = np.zeros(n, _lib.RESID4x4_RES)
+        check(lib().jmme_residual4x4(self._ctx, ptr(params), params.shape[0], ptr(req), ptr(res), n))
+        return res
+
     def quant4x4_async(self, d_params: int, d_param_idx: int, d_coef: int, d_levels: int, d_runs: int,
                        d_coeff_cost: int, d_nonzero: int, n: int, stream: int = 0) -> None:
         check(lib().jmme_quant4x4_async(self._ctx, d_params, d_param_idx or None, d_coef, d_levels, d_runs,

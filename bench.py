@@ -677,6 +677,7 @@ def main():
                          "each rank runs the drop-in encoder (lencod_jmme) over its own closed GOPs on its GPU "
                          "(integration/jmme_gop.c, weak)")
     ap.add_argument("--no-encoder", action="store_true", help="skip the GOP-sharded encoder block of the N=1 line")
+    ap.add_argument("--no-f3", action="store_true", help="skip the (f)3 block (inter residual coding on the GPU)")
     ap.add_argument("--enc-gops", type=int, default=16, help="--shard encoder / encoder block: GOPs per GPU")
     ap.add_argument("--enc-gop", type=int, default=4, help="frames per GOP (1 I + P)")
     ap.add_argument("--enc-per-gpu", type=int, default=8, help="encoder processes at once per GPU")
@@ -692,7 +693,7 @@ def main():
     args = ap.parse_args()
     if args.headline_only:
         for k in ("no_cpu_baseline", "no_subpel", "no_uhd", "no_adversarial", "no_hbd", "no_fractal", "no_hybrid",
-                  "no_dropin", "no_encoder", "no_encoder_4k"):
+                  "no_dropin", "no_encoder", "no_encoder_4k", "no_f3"):
             setattr(args, k, True)
 
     ws, rank, local = dist_env()
@@ -864,6 +865,10 @@ def main():
             line["encoder_gop_epzs4k"] = bench_blocks.encoder_gop_block(device=local, rank=0, gops=args.enc4k_gops,
                                                                         gop=2, per_gpu=min(8, args.enc4k_gops),
                                                                         encoder=args.enc_encoder, preset="epzs4k")
+        if not args.no_f3 and ws == 1:
+            import bench_blocks
+            # mode decision's inter residual coding from the GPU (off by default in the product)
+            line["f3"] = bench_blocks.f3_block()
         if not args.no_dropin and ws == 1:
             import bench_blocks
             # FS / FFS (configs[1] settings), FS / FFS with encoder_baseline.cfg's

@@ -309,6 +309,38 @@ int jmme_quant4x4_async(jmme_ctx *ctx, const jmme_quant4x4_params *d_params, con
                         int32_t *d_coef, int32_t *d_levels, int32_t *d_runs, int32_t *d_coeff_cost,
                         int32_t *d_nonzero, int n, void *stream);
 
+/* residual_transform_quant_luma_4x4 (JM/lencod/src/block.c:660-724) of inter
+ * blocks -- the mode-decision call SURVEY.md §8(f)3 names: check_zero,
+ * forward4x4, quant_4x4_normal, then inverse4x4 + sample_reconstruct
+ * (lcommon/src/blk_prediction.c:48-62) when a level survives, else the
+ * prediction.  Per block: ores = mb_ores[block_y + r][block_x + c] (original -
+ * prediction), pred = mb_pred[...], param = index of its jmme_quant4x4_params
+ * (q_params_4x4[pl][0][qp], qp_per, CAVLC, scan, COEFF_COST4x4[disthres]),
+ * max_pel = max_imgpel_value.  Results: what JM leaves -- zero (check_zero
+ * found no coefficient: JM sets ACLevel[0] = 0 and copies the prediction),
+ * nonzero (the return value), cost (added to *coeff_cost), levels / runs
+ * (cofAC[b8][b4][0/1], levels 0-terminated), coef (tblk16x16 after the
+ * quantiser: the dequantised block; not touched when zero), rres (mb_rres,
+ * only when nonzero), recon (enc_picture rows). */
+typedef struct jmme_resid4x4_req {
+  int32_t ores[16];
+  jmme_imgpel pred[16];
+  int32_t param;
+  int32_t max_pel;
+} jmme_resid4x4_req;   /* 104 bytes */
+
+typedef struct jmme_resid4x4_res {
+  int32_t coef[16];
+  int32_t rres[16];
+  int32_t levels[17];
+  int32_t runs[16];
+  int32_t cost, nonzero, zero;
+  jmme_imgpel recon[16];
+} jmme_resid4x4_res;   /* 304 bytes */
+
+int jmme_residual4x4(jmme_ctx *ctx, const jmme_quant4x4_params *params, int n_params,
+                     const jmme_resid4x4_req *req, jmme_resid4x4_res *res, int n);
+
 /* ---- EPZS integer-pel search --------------------------
  * EPZS_motion_estimation (variant 0) and EPZS_subMB_motion_estimation
  * (variant 1), JM/lencod/src/me_epzs.c:54-407 / 417-780 (EPZSSubPelGrid = 0),

@@ -90,9 +90,16 @@ static distblk t_d8(short *d, distblk m)
 }
 
 extern void __real_select_transform(Macroblock *currMB);
+/* (weak: the CPU-only profiling build, lencod_f3prof, links no GPU server) */
+extern int jm_f3_gpu_on(void) __attribute__((weak));
+extern int jm_f3_gpu_rq4(Macroblock *m, ColorPlane pl, int bx, int by, int *cc, int intra) __attribute__((weak));
+extern int residual_transform_quant_luma_4x4(Macroblock *, ColorPlane, int, int, int *, int);
 void __wrap_select_transform(Macroblock *currMB)
 {
   __real_select_transform(currMB);
+  /* JMME_F3=1: the plain 4x4 residual coding goes through the GPU server (jm_f3_gpu.c) */
+  if (jm_f3_gpu_on && jm_f3_gpu_on() && currMB->residual_transform_quant_luma_4x4 == residual_transform_quant_luma_4x4)
+    currMB->residual_transform_quant_luma_4x4 = jm_f3_gpu_rq4;
   if (!on()) return;
   if (currMB->residual_transform_quant_luma_4x4 != t_rq4) {
     g_rq4 = currMB->residual_transform_quant_luma_4x4;

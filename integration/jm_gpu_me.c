@@ -114,6 +114,13 @@ static void init_once(VideoParameters *p_Vid, InputParameters *p_Inp)
   if (!g_me) fail_jm("jmme_create");
 }
 
+/* the encoder's GPU engine (created on first use): jm_f3_gpu.c's residual coding shares it */
+jmme_ctx *jm_gpu_me_engine(VideoParameters *p_Vid, InputParameters *p_Inp)
+{
+  init_once(p_Vid, p_Inp);
+  return g_me;
+}
+
 /* init_motion_search_module (mv_search.c:315, called once from init_encoder,
  * lencod.c:606) builds JM's ME tables; the GPU engine is created there too, and
  * its one-time start-up (code-object loading, first-launch setup) is paid
@@ -1470,8 +1477,6 @@ static long long g_ep_miss_slot[JMME_NSLOT], g_ep_list_diff[JMME_NSLOT];   /* mi
 static long long g_ep_miss_kind[4], g_ep_stop_off[24];
 static int g_ep_trace = 0;   /* JMME_EPZS_TRACE=1: per-slot miss counts at exit */
 static int g_ep_two_pass = 1;   /* JMME_EPZS_PASS2=0: no second pass (ep_pass2) */
-static int g_ep_third = 0;      /* JMME_EPZS_PASS3=1: a third pass (the rebuild repeated on the second pass's answers):
-                                   ~600 fewer searches alone per 1080p P picture for ~36 ms of host work, off */
 static int g_ep_dump = 0;       /* JMME_EPZS_DUMP=n: print the first n input misses (measurement) */
 
 static int ep_speculating(Macroblock *currMB, int cur_list, int ref, int n_pred)
@@ -1481,9 +1486,8 @@ static int ep_speculating(Macroblock *currMB, int cur_list, int ref, int n_pred)
     g_ep_spec = !(e && e[0] == '0');
     g_ep_trace = tr && tr[0] == '1';
     {
-      const char *p2 = getenv("JMME_EPZS_PASS2"), *p3 = getenv("JMME_EPZS_PASS3");
+      const char *p2 = getenv("JMME_EPZS_PASS2");
       g_ep_two_pass = !(p2 && p2[0] == '0');
-      g_ep_third = p3 && p3[0] == '1';
       const char *dp = getenv("JMME_EPZS_DUMP");
       g_ep_dump = dp ? atoi(dp) : 0;
     }
@@ -1787,13 +1791,11 @@ static int ep_avail_c(int bx, int by, int bsx)   /* get_neighbors' upper-right r
   return 1;
 }
 
-/* The answer JM is assumed to get for (macroblock mb0 + xr, slot): its first guess, or, in the third
- * pass, the second-pass rebuild of that guess (g_ep_alt) when there is one */
-static int *g_ep_alt = NULL;
-static int g_ep_alt_cap = 0, g_ep_alt_on = 0;
+/* The answer JM is assumed to get for (macroblock mb0 + xr, slot): its first guess.  (A third pass
+ * repeating the rebuild on the second pass's answers saved ~600 searches alone per 1080p P picture
+ * for ~36 ms more host work: measured slower, removed.) */
 static int ep_assumed(int xr, int slot)
 {
-  if (g_ep_alt_on && g_ep_alt[xr * JMME_NSLOT + slot] >= 0) return g_ep_alt[xr * JMME_NSLOT + slot];
   return g_ep_idx[(((size_t)xr * JMME_NSLOT + slot) * EP_REFS + 0) * EP_WAYS];
 }
 
@@ -1913,7 +1915,7 @@ static int ep_neighbours(ep_hyp *H, int h, int x, int mb0, int bt, int bx, int b
   return dep;
 }
 
-static void ep_pass2(Macroblock *currMB, int mb0, int s0, int nmb, unsigned gen, int *n_io, int third)
+static void ep_pass2(Macroblock *currMB, int mb0, int s0, int nmb, unsigned gen, int *n_io)
 {
   VideoParameters *p_Vid = currMB->p_Vid;
   InputParameters *p_Inp = currMB->p_Inp;
@@ -2119,7 +2121,6 @@ static void ep_pass2(Macroblock *currMB, int mb0, int s0, int nmb, unsigned gen,
           g_ep_q[n].prev_sad = prev;
           ep_fill_in(&g_ep_ans[n].in, &g_ep_q[n], (const int16_t *)in->pred, in->cond, -1, gen);   /* (dedup above) */
           if (hh > 0) ++g_ep_hyp_guesses;
-          if (!third && w == 0 && in == &g_ep_fix) g_ep_alt[(x - mb0) * JMME_NSLOT + t] = n;   /* (for the third pass) */
           idx[nw++] = n++;
         }
         {   /* the row after this partition: its first guess's answer (the real call's for the missing one) */
@@ -2212,21 +2213,8 @@ static const ep_ans *ep_miss(Macroblock *currMB, MEBlock *mv_block, const jmme_e
   g_t_ep_build += now_us() - t0;
   ep_run(n, stale, n_stale, gen);
   if (g_ep_two_pass) {
-    if (nmb * JMME_NSLOT > g_ep_alt_cap) {
-      free(g_ep_alt);
-      g_ep_alt_cap = nmb * JMME_NSLOT;
-      g_ep_alt = (int *)malloc((size_t)g_ep_alt_cap * sizeof(int));
-      if (!g_ep_alt) error("jm_gpu_me: out of memory", 500);
-    }
-    memset(g_ep_alt, 0xff, (size_t)nmb * JMME_NSLOT * sizeof(int));
-    g_ep_alt_on = 0;
     t0 = now_us();
-    ep_pass2(currMB, mb, ep_slot_of(q), nmb, gen, &n, 0);
-    if (g_ep_third) {
-      g_ep_alt_on = 1;   /* third pass: the same replay on the second pass's answers */
-      ep_pass2(currMB, mb, ep_slot_of(q), nmb, gen, &n, 1);
-      g_ep_alt_on = 0;
-    }
+    ep_pass2(currMB, mb, ep_slot_of(q), nmb, gen, &n);
     g_t_ep_p2 += now_us() - t0;
   }
   g_ep_n = n;
@@ -2539,7 +2527,7 @@ static void report(void)
               g_ep_hyp_guesses);
     if (g_epzs_calls && g_ep_batches)
       fprintf(stderr, "jm_gpu_me: EPZS host clocks: %.1f ms running guesses (%.1f ms of it in the library), %.1f ms in the "
-                      "second and third passes (with their runs), %.1f ms in %lld lookups (JMME_EPZS_TRACE=1 only)\n",
+                      "second pass (with its runs), %.1f ms in %lld lookups (JMME_EPZS_TRACE=1 only)\n",
               g_t_ep_run * 1e-3, g_t_ep_runlib * 1e-3, g_t_ep_p2 * 1e-3, g_t_ep_lookup * 1e-3, g_ep_lookups);
     if (g_ep_trace) {
       int sl;

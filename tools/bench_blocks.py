@@ -220,7 +220,7 @@ def _lencod(binary, d, tag, yuv, w, h, frames, params, cfg_text, env=None):
     ch = re.search(r"chained guesses: (\d+) chains, (\d+) steps, (\d+) calls answered, (\d+) head mismatches; "
                    r"(\d+) chain-only calls \((\d+) fell back[^;]*(?:; ([\d.]+) ms in chain-only calls)?", r.stderr)
     chsp = re.search(r"chained sub-pel: (\d+) refinements, (\d+) calls answered; (\d+) misses without", r.stderr)
-    res = dict(wall_s=round(wall, 3), me_s=float(me.group(1)) if me else None,
+    res = dict(wall_s=round(wall, 3), me_s=float(me.group(1)) if me else None, stderr=r.stderr[-4000:],
                md5=(hashlib.md5(open(out, "rb").read()).hexdigest(), hashlib.md5(open(rec, "rb").read()).hexdigest()))
     if calls:
         res.update(gpu_searches=int(calls.group(1)), batches=int(calls.group(3)),
@@ -341,7 +341,7 @@ def dropin_block(modes=None, size=(1920, 1080), search_range=32, reps=2, host_pr
                 "dropin_me_ms_per_p_frame_runs": [round(x["me_s"] * 1e3 / p, 2) for x in gs],
                 "jm_loop_floor_ms_per_p_frame": round(fl["me_s"] * 1e3 / p, 2) if fl and fl["me_s"] else None,
                 "stock_wall_s": cpu["wall_s"], "dropin_wall_s": g["wall_s"],
-                "dropin": {k: v for k, v in g.items() if k not in ("md5", "me_s", "wall_s")}}
+                "dropin": {k: v for k, v in g.items() if k not in ("md5", "me_s", "wall_s", "stderr")}}
             if host:
                 # the host's rate: every encoder's P-frame macroblocks over the slowest one's ME time
                 host_rate = host_procs * mbs * p / max(host)
@@ -349,6 +349,52 @@ def dropin_block(modes=None, size=(1920, 1080), search_range=32, reps=2, host_pr
                            host_me_ms_per_p_frame_slowest=round(max(host) * 1e3 / p, 2),
                            me_speedup_vs_host=round(row["dropin_mb_per_s"] / host_rate, 3) if g["me_s"] else None)
             out[tag] = row
+    return out
+
+
+# ---- mode decision's inter residual coding on the GPU --------------
+F3_PARAMS = {"SearchMode": -1, "SearchRange": 16, "NumberReferenceFrames": 1, "RDOptimization": 1,
+             "DisableSubpelME": 0, "MEDistortionHPel": 2, "MEDistortionQPel": 2, "MDDistortion": 2,
+             "AdaptiveRounding": 0}
+_F3_RE = r"jm_f3_gpu: (\d+) 4x4 residual calls: (\d+) served from (\d+) GPU batches; on JM's code: (\d+) intra, " \
+         r"(\d+) other forms, (\d+) input mismatches"
+
+
+def f3_block(size=(352, 288), frames=3) -> dict | None:
+    """lencod_jmme with and without JMME_F3=1 (integration/jm_f3_gpu.c: every inter
+    residual_transform_quant_luma_4x4 call of mode decision answered from one GPU
+    launch per macroblock and mode) against the stock encoder on the same clip:
+    byte identity, the served share and the encode-time delta.  The plain
+    quantiser (adaptive rounding off) is the one served."""
+    import os
+    import re
+    import tempfile
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    stock = os.path.join(repo, "oracle", "_ref", "lencod")
+    gpu = os.path.join(repo, "integration", "_build", "lencod_jmme")
+    if not (os.path.exists(stock) and os.path.exists(gpu)):
+        return None
+    from jmme import synth
+    from test_jm_dropin_gpu import CFG
+    w, h = size
+    with tempfile.TemporaryDirectory() as d:
+        yuv = os.path.join(d, "in.yuv")
+        synth.write_yuv420(yuv, synth.luma_sequence(w, h, frames, seed=77, gmv=(2, -1)))
+        ref = _lencod(stock, d, "cpu", yuv, w, h, frames, F3_PARAMS, CFG)
+        off = _lencod(gpu, d, "off", yuv, w, h, frames, F3_PARAMS, CFG)
+        on = _lencod(gpu, d, "on", yuv, w, h, frames, F3_PARAMS, CFG, env={"JMME_F3": "1"})
+        _progress(f"f3 block: encode {off['wall_s']:.2f} s without, {on['wall_s']:.2f} s with the GPU residuals")
+    out = {"workload": f"JM 18.5 lencod_jmme, seeded {w}x{h} clip, 1 I + {frames - 1} P, FS +-16 + sub-pel, RDO on, "
+                       f"adaptive rounding off: inter 4x4 residual coding of mode decision from the GPU (JMME_F3=1)",
+           "params": F3_PARAMS, "byte_identical": ref["md5"] == off["md5"] == on["md5"],
+           "encode_wall_s": {"stock": ref["wall_s"], "dropin": off["wall_s"], "dropin_f3": on["wall_s"]},
+           "f3_delta_s": round(on["wall_s"] - off["wall_s"], 3)}
+    m = re.search(_F3_RE, on.get("stderr", ""))
+    if m:
+        calls, served, batches, intra, other, mism = map(int, m.groups())
+        out.update(calls=calls, served=served, batches=batches, intra_on_cpu=intra, other_on_cpu=other,
+                   input_mismatches=mism, us_per_batch_delta=round((on["wall_s"] - off["wall_s"]) * 1e6 /
+                                                                   max(1, batches), 1))
     return out
 
 
