@@ -1419,7 +1419,7 @@ static distblk real_epzs(int variant, Macroblock *currMB, MotionVector *pred_mv,
  * call per search. */
 #define EP_MAXP 128                /* predictors of a list the cache keeps (longer lists: one call each) */
 #define EP_MAXV 64                 /* stamped cells kept per cached answer */
-#define EP_WAYS 10                 /* guesses per (macroblock, partition, reference): the sources' inputs,
+#define EP_WAYS 6                  /* guesses per (macroblock, partition, reference): the sources' inputs,
                                       then their second-pass forms (ep_pass2) */
 #define EP_REFS 4                  /* references speculated (list 0) */
 #define EP_BATCH_MAX 512
@@ -1799,15 +1799,13 @@ static int ep_assumed(int xr, int slot)
   return g_ep_idx[(((size_t)xr * JMME_NSLOT + slot) * EP_REFS + 0) * EP_WAYS];
 }
 
-/* One hypothesis about the rate-distortion decisions a partition's spatial neighbours depend on:
- * the spatial predictors 1..4 it implies (sp_on 0: keep the guess's own) and the MV predictor */
-#define EP_HYP 9
+/* A partition's spatial predictors 1..4 as the batch assumes them (sp_on 0: keep the guess's own)
+ * and the MV predictor they imply */
 typedef struct ep_hyp {
   int16_t sp[5][2];
   int sp_on[5], pv_on;
   int16_t pv[2];
 } ep_hyp;
-static long long g_ep_hyp_guesses = 0;   /* second-pass guesses made for hypotheses 1..8 */
 
 static const int kEpW4[8] = {0, 4, 4, 2, 2, 2, 1, 1}, kEpH4[8] = {0, 4, 2, 4, 2, 1, 2, 1};
 
@@ -1823,9 +1821,10 @@ static int ep_refined_at(int xr, int m, int x4, int y4, int16_t v[2])
   return 1;
 }
 
-/* hypothesis h's neighbours of slot t (block type bt at (bx, by)) of macroblock x; returns whether any
- * neighbour was decided under it (else hypothesis h is hypothesis 0) */
-static int ep_neighbours(ep_hyp *H, int h, int x, int mb0, int bt, int bx, int by, VideoParameters *p_Vid)
+/* the neighbours of the partition of block type bt at (bx, by) of macroblock x: inside this macroblock
+ * the refined answer of the same block type's partition there (set_me_parameters after each search),
+ * in a macroblock JM has decided its mv_info, in the left macroblock when it lies in this batch unknown */
+static void ep_neighbours(ep_hyp *H, int x, int mb0, int bt, int bx, int by, VideoParameters *p_Vid)
 {
   static const int16_t kNone[5][2] = {{0, 0}, {12, 0}, {0, 12}, {-12, 0}, {0, -12}};   /* unavailable */
   const int x4 = bx >> 2, y4 = by >> 2, w4 = kEpW4[bt];
@@ -1833,29 +1832,14 @@ static int ep_neighbours(ep_hyp *H, int h, int x, int mb0, int bt, int bx, int b
   PicMotionParams **mvi = p_Vid->enc_picture->mv_info;
   const int nx[5] = {0, x4 - 1, x4, x4 + w4, x4 - 1}, ny[5] = {0, y4, y4 - 1, y4 - 1, y4 - 1};
   int st[5] = {0, 0, 0, 0, 0}, nref[5] = {0, 0, 0, 0, 0};   /* 1 known, 0 not known, -1 unavailable; refs */
-  int j, dep = 0;
+  int j;
   memset(H, 0, sizeof *H);
   for (j = 1; j <= 4; j++) {
     const int px4 = mbx4 + nx[j], py4 = mby4 + ny[j];
     if (px4 < 0 || py4 < 0 || px4 >= W4) { st[j] = -1; continue; }
     if (j == 3 && !ep_avail_c(bx, by, 4 * w4)) { st[j] = -1; continue; }
     if (nx[j] >= 0 && nx[j] <= 3 && ny[j] >= 0) {   /* inside this macroblock */
-      const int decided = bt >= 4 && ((nx[j] >> 1) != (x4 >> 1) || (ny[j] >> 1) != (y4 >> 1));
-      const int m = decided && h >= 4 && h <= 7 ? h : bt;
-      if (decided && m != bt) dep = 1;
-      if (ep_refined_at(x - mb0, m, nx[j], ny[j], H->sp[j])) st[j] = 1;
-    } else if (ny[j] >= 0 && nx[j] < 0 && x - 1 >= mb0) {   /* the left macroblock, in this batch */
-      if (h >= 1 && h <= 7) {
-        if (ep_refined_at(x - 1 - mb0, h, 3, ny[j], H->sp[j])) { st[j] = 1; dep = 1; }
-      } else if (h == 8) {   /* P_Skip: the 16x16 MV predictor (FindSkipModeMotionVector) */
-        const int pk = ep_assumed(x - 1 - mb0, 0);
-        if (pk >= 0) {
-          H->sp[j][0] = g_ep_ans[pk].in.q.pred_x;
-          H->sp[j][1] = g_ep_ans[pk].in.q.pred_y;
-          st[j] = 1;
-          dep = 1;
-        }
-      }
+      if (ep_refined_at(x - mb0, bt, nx[j], ny[j], H->sp[j])) st[j] = 1;
     } else if (ny[j] < 0 || x - 1 < mb0) {   /* a macroblock JM has decided: its mv_info */
       const PicMotionParams *mp = &mvi[py4][px4];
       if (mp->ref_idx[0] == 0 || (mp->mv[0].mv_x == 0 && mp->mv[0].mv_y == 0)) {
@@ -1912,7 +1896,6 @@ static int ep_neighbours(ep_hyp *H, int h, int x, int mb0, int bt, int bx, int b
     }
     H->pv_on = 1;
   }
-  return dep;
 }
 
 static void ep_pass2(Macroblock *currMB, int mb0, int s0, int nmb, unsigned gen, int *n_io)
@@ -1996,26 +1979,13 @@ static void ep_pass2(Macroblock *currMB, int mb0, int s0, int nmb, unsigned gen,
           }
         }
         /* the spatial predictors of neighbours inside this macroblock (EPZS_spatial_predictors,
-         * me_epzs_common.c:1276-1370: left, up, up-right -- the up-left when get_neighbors,
-         * mv_search.c:283-306, makes it unavailable -- and up-left): JM reads mv_info there, which
-         * holds the refined answer of the same block type's partition at that place (set_me_parameters
-         * after each search) -- except where rate-distortion decisions wrote it: an 8x8 block of this
-         * macroblock already decided holds its chosen sub-mode's vectors (set_ref_and_motion_vectors,
-         * mode_decision_P8x8.c:40-320), and the macroblock to the left, when it lies in this batch, its
-         * final mode's.  Those are branched over (ep_hyp): hypothesis 0 as above (the same block type
-         * inside, the left macroblock unknown), 1..7 that mode decided there (inside: sub-modes 4..7),
-         * 8 a skipped left macroblock (its 16x16 predictor).  ref 0, so scale_mv is the identity */
-        ep_hyp hyp[EP_HYP];
-        int n_hyp = 0, hh;
-        for (hh = 0; hh < EP_HYP; hh++) {
-          ep_hyp *H = &hyp[n_hyp];
-          int dep = ep_neighbours(H, hh, x, mb0, bt, bx, by, p_Vid);
-          int e;
-          if (hh > 0 && !dep) continue;       /* no decided neighbour: the same as hypothesis 0 */
-          for (e = 0; e < n_hyp; e++)
-            if (!memcmp(&hyp[e], H, sizeof *H)) break;
-          if (e == n_hyp) ++n_hyp;
-        }
+         * me_epzs_common.c:1276-1370) and the MV predictor they imply: ep_neighbours.  (Round 6 also
+         * branched the guesses over the rate-distortion decisions those neighbours hang on -- the
+         * sub-mode chosen for an earlier 8x8 block, the left macroblock's final mode: 1,115 fewer
+         * searches alone per 1080p P picture for 28,928 more guesses, and the second pass's added
+         * host time ate the gain (JM ME 0.449 vs 0.456 s); not kept: profiles/round6/epzs_hyp/.) */
+        ep_hyp hyp0;
+        ep_neighbours(&hyp0, x, mb0, bt, bx, by, p_Vid);
         /* the spatial-memory predictors (EPZS_spatial_memory_predictors, me_epzs_common.c:1675-1718,
          * EPZSREF): p_motion[ref][blocktype - 1][block row][picture column] at the left, up and up-right
          * block, i.e. the `tmp` of the same block type's search there -- this batch's answer where JM
@@ -2053,13 +2023,12 @@ static void ep_pass2(Macroblock *currMB, int mb0, int s0, int nmb, unsigned gen,
             if (vx | vy) { mem[n_mem][0] = vx; mem[n_mem][1] = vy; ++n_mem; }
           }
         }
-        for (w = 0; w < nw0 && nw < EP_WAYS; w++)
-        for (hh = 0; hh < (w == 0 ? n_hyp : 1) && nw < EP_WAYS; hh++) {
+        for (w = 0; w < nw0 && nw < EP_WAYS; w++) {
           const ep_ans *a = &g_ep_ans[idx[w]];
           const ep_in *in = &a->in;
-          const int16_t (*sp)[2] = hyp[hh].sp;
-          const int *sp_on = hyp[hh].sp_on, pv_on = hyp[hh].pv_on;
-          const int16_t *pv = hyp[hh].pv;
+          const int16_t (*sp)[2] = hyp0.sp;
+          const int *sp_on = hyp0.sp_on, pv_on = hyp0.pv_on;
+          const int16_t *pv = hyp0.pv;
           const int np = a->in.q.n_pred, bs = a->in.bt_start & 0xffff, me = a->in.bt_start >> 16;
           const int16_t *ap = (const int16_t *)a->in.pred;
           int fixed = 0, j, o;
@@ -2113,14 +2082,9 @@ static void ep_pass2(Macroblock *currMB, int mb0, int s0, int nmb, unsigned gen,
               break;
           }
           if (k < nw0) continue;
-          for (k = nw0; k < nw; k++)     /* one added by this pass already (another hypothesis, the same list) */
-            if (ep_same(&g_ep_ans[idx[k]].in, &in->q, (const int16_t *)in->pred, in->cond)) break;
-          if (k < nw) continue;
           ep_add(n, in, px, py, p_EPZS);
           g_ep_q[n].stop_crit = stop;
           g_ep_q[n].prev_sad = prev;
-          ep_fill_in(&g_ep_ans[n].in, &g_ep_q[n], (const int16_t *)in->pred, in->cond, -1, gen);   /* (dedup above) */
-          if (hh > 0) ++g_ep_hyp_guesses;
           idx[nw++] = n++;
         }
         {   /* the row after this partition: its first guess's answer (the real call's for the missing one) */
@@ -2520,11 +2484,9 @@ static void report(void)
       fprintf(stderr, "jm_gpu_me: EPZS speculation: %lld searches answered from %lld batches (%lld guesses), "
                       "%lld searched alone; %lld not speculated; guesses refused: %lld inputs, %lld bounds, "
                       "%lld map cells; %.1f ms building batches; %lld searched again (more stamped cells than kept); "
-                      "%lld second-pass guesses in %lld launches (%lld with lists rebuilt from the batch's answers, %lld for "
-                      "decided-neighbour hypotheses)\n",
+                      "%lld second-pass guesses in %lld launches (%lld with lists rebuilt from the batch's answers)\n",
               g_ep_hits, g_ep_batches, g_ep_guesses, g_ep_singles, g_ep_direct, g_ep_fail_inputs, g_ep_fail_bounds,
-              g_ep_fail_stale, g_t_ep_build * 1e-3, g_ep_overflow, g_ep_pass2, g_ep_pass2_batches, g_ep_list_fixes,
-              g_ep_hyp_guesses);
+              g_ep_fail_stale, g_t_ep_build * 1e-3, g_ep_overflow, g_ep_pass2, g_ep_pass2_batches, g_ep_list_fixes);
     if (g_epzs_calls && g_ep_batches)
       fprintf(stderr, "jm_gpu_me: EPZS host clocks: %.1f ms running guesses (%.1f ms of it in the library), %.1f ms in the "
                       "second pass (with its runs), %.1f ms in %lld lookups (JMME_EPZS_TRACE=1 only)\n",
