@@ -380,6 +380,39 @@ __device__ void tile_phase(const SubpelParams &p, TileLds<T> &W, int lane, int b
   wave_sync();
 }
 
+// The first (cost, lane) minimum over lanes 0..15 of the wave (lanes >= n, and
+// lanes whose `live` is false, hold no candidate): every lane gets the cost and
+// the lane.  A fold of JM's refinement walks its candidates in order with strict
+// `<` and an early-exit distortion that returns the running bound exactly when the
+// full cost exceeds it (dist(), jmme_subpel_dev.h), so its minimum is this
+// lexicographic one over the full costs (me_epzs_sub.c:66-88, 96-127, 150-172,
+// 175-210).  Four butterfly steps instead of a dependent compare per candidate.
+template <int CTRL>
+__device__ __forceinline__ void argmin_step(int64_t &v, int &k) {
+  const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)v, CTRL, 0xf, 0xf, true);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)((uint64_t)v >> 32), CTRL, 0xf, 0xf, true);
+  const int ok = __builtin_amdgcn_mov_dpp(k, CTRL, 0xf, 0xf, true);
+  const int64_t ov = (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+  const bool take = ov < v || (ov == v && ok < k);
+  v = take ? ov : v;
+  k = take ? ok : k;
+}
+
+__device__ __forceinline__ void wave_argmin16(int64_t c, bool live, int lane, int64_t &cmin, int &kmin) {
+  int64_t v = live ? c : INT64_MAX;
+  int k = live ? lane : 64;
+  // DPP within each row of 16 lanes: lane ^ 1, lane ^ 2 (quad_perm), then the
+  // half-row mirror (i <-> 7 - i) and the row mirror (i <-> 15 - i) pair the
+  // quads and the halves: after the four steps every lane of row 0 holds its minimum
+  argmin_step<0xB1>(v, k);
+  argmin_step<0x4E>(v, k);
+  argmin_step<0x141>(v, k);
+  argmin_step<0x140>(v, k);
+  cmin = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)v >> 32)) << 32) |
+                   (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v));
+  kmin = __builtin_amdgcn_readfirstlane(k);
+}
+
 // a wave-uniform copy of v (lane 0's), dword by dword into SGPRs
 template <typename S>
 __device__ __forceinline__ S uni(const S &v) {
@@ -487,12 +520,58 @@ __device__ __forceinline__ void refine_wave(const SubpelParams &p, WaveLds<T> &L
   const int64_t sub_threshold = q.subthres + (int64_t)q.lambda_h * 2;
   bool early = false;
   const bool chk0 = (q.flags & JMME_SP_CHECK0) && (q.ref_slot & 31) == 0 && q.blocktype == 1 && mvx == 0 && mvy == 0;
+  // (window, EPZS) a phase's candidates pos in [a0, a1) of the search_point table, lane k = pos - a0:
+  // their full costs, mv cost + sum << 5, with the vectors at scale sc around (mvx, mvy)
+  auto cand_cost = [&](int a0, int a1, int sc, int lam, bool &live) -> int64_t {
+    const int pos = a0 + lane;
+    live = lane < 16 && pos < a1;
+    const int sm = __shfl(sv, (lane + sums_off) & 63, 64);   // the pass's sum of candidate lane
+    const int cx = mvx + sc * ept_x(live ? pos : 0), cy = mvy + sc * ept_y(live ? pos : 0);
+    return mv_cost(lam, cx, cy, px, py) + ((int64_t)sm << 5);
+  };
+  // JM's top-2 fold (strict <, best / second tracking): the first minimum over the running best
+  // (its cost and position, ahead of every candidate) and the candidates; the second is the first
+  // minimum over the rest, with the running best ahead when a candidate took its place, else the
+  // running second (cost DISTBLK_MAX) ahead.  (sc, lamsc unused here: scale of the vectors; kept
+  // explicit at the call sites.)
+  auto top2 = [&](int a0, int a1, int sc, int, int lam, int64_t &mn, int &bp, int64_t &sec, int &sp) {
+    if (a1 <= a0) return;
+    bool live;
+    const int64_t c = cand_cost(a0, a1, sc, lam, live);
+    int64_t c1;
+    int k1;
+    wave_argmin16(c, live, lane, c1, k1);
+    if (k1 >= 64 || mn <= c1) {        // the running best stays
+      if (k1 < 64 && c1 < sec) { sec = c1; sp = a0 + k1; }
+      return;
+    }
+    int64_t c2;
+    int k2;
+    wave_argmin16(c, live && lane != k1, lane, c2, k2);
+    // the running best becomes the second unless a later candidate is strictly below it
+    if (k2 < 64 && c2 < mn) { sec = c2; sp = a0 + k2; } else { sec = mn; sp = bp; }
+    mn = c1;
+    bp = a0 + k1;
+  };
+  // JM's follow-up fold (strict <, minimum only)
+  auto min1 = [&](int a0, int a1, int sc, int lam, int64_t &mn, int &bp) {
+    if (a1 <= a0) return;
+    bool live;
+    const int64_t c = cand_cost(a0, a1, sc, lam, live);
+    int64_t c1;
+    int k1;
+    wave_argmin16(c, live, lane, c1, k1);
+    if (k1 < 64 && c1 < mn) { mn = c1; bp = a0 + k1; }
+  };
 
   // ---- phase A: half-pel ring (me_fullsearch.c:221-250 | me_epzs_sub.c:66-88)
   {
     const int p1 = epzs ? min(5, max_pos2) : max_pos2;
     phase(q.start_hp, act ? p1 : 0, q.metric_h, t8, 2, epzs, mvx + pxp, mvy + pyp);
-    if (act) {
+    if (TILE && act && epzs) {   // the top-2 fold as two wave minima (wave_argmin16)
+      top2(q.start_hp, p1, 2, 2, lambda, min_mcost, best_pos, second_mcost, second_pos);
+      early = best_pos == 0 && px == mvx && py == mvy && min_mcost < sub_threshold;   // :90-93
+    } else if (act) {
       for (int pos = q.start_hp; pos < p1; ++pos) {
         const int ox = tab_x(epzs, pos), oy = tab_y(epzs, pos);
         const int cx = mvx + 2 * ox, cy = mvy + 2 * oy;
@@ -528,7 +607,10 @@ __device__ __forceinline__ void refine_wave(const SubpelParams &p, WaveLds<T> &L
       s1 = next_end(best_pos * 5 + second_pos);
     }
     phase(s0, s1, q.metric_h, t8, 2, 1, mvx + pxp, mvy + pyp);
-    if (act && epzs && !early) {
+    if (TILE && act && epzs && !early) {
+      min1(s0, s1, 2, lambda, min_mcost, best_pos);
+      if (best_pos) { mvx += 2 * ept_x(best_pos); mvy += 2 * ept_y(best_pos); }
+    } else if (act && epzs && !early) {
       for (int pos = s0; pos < s1; ++pos) {
         const int cx = mvx + 2 * ept_x(pos), cy = mvy + 2 * ept_y(pos);
         int64_t mcost = mv_cost(lambda, cx, cy, px, py);
@@ -557,7 +639,9 @@ __device__ __forceinline__ void refine_wave(const SubpelParams &p, WaveLds<T> &L
       }
     }
     phase(q.start_qp, p1, q.metric_q, t8, 1, epzs, mvx + pxp, mvy + pyp);
-    if (act && !early) {
+    if (TILE && act && !early && epzs) {
+      top2(q.start_qp, p1, 1, 1, lambda, min_mcost, best_pos, second_mcost, second_pos);
+    } else if (act && !early) {
       for (int pos = q.start_qp; pos < p1; ++pos) {
         const int ox = tab_x(epzs, pos), oy = tab_y(epzs, pos);
         const int cx = mvx + ox, cy = mvy + oy;
@@ -594,7 +678,9 @@ __device__ __forceinline__ void refine_wave(const SubpelParams &p, WaveLds<T> &L
       s1 = k >= 0 ? next_end(k) : 0;
     }
     phase(s0, s1, q.metric_q, t8, 1, 1, mvx + pxp, mvy + pyp);
-    if (go) {
+    if (TILE && go) {
+      min1(s0, s1, 1, lambda, min_mcost, best_pos);
+    } else if (go) {
       for (int pos = s0; pos < s1; ++pos) {
         const int cx = mvx + ept_x(pos), cy = mvy + ept_y(pos);
         int64_t mcost = mv_cost(lambda, cx, cy, px, py);
