@@ -1451,6 +1451,7 @@ static int g_ep_spec = -1, g_ep_batch = 64, g_ep_ring_n = 0;
 static ep_in *g_ep_seen = NULL;    /* [ring of macroblocks][41 slots][EP_REFS]: the inputs JM really searched with */
 static ep_ans *g_ep_ans = NULL;    /* the current batch's searched guesses */
 static int *g_ep_idx = NULL;       /* [batch macroblock][41][EP_REFS][EP_WAYS] -> g_ep_ans index (-1: none) */
+static int g_ep_idx_mbs = 0;       /* macroblocks g_ep_idx holds room for */
 static int g_ep_cap = 0, g_ep_n = 0, g_ep_mb0 = 0, g_ep_mb1 = 0;
 static unsigned g_ep_gens[EP_REFS];   /* g_slot_gen of each reference when the batch was made (0: none) */
 static const ep_ans *g_ep_served = NULL;   /* the answer the last EPZS call was served from (its refinement) */
@@ -1478,6 +1479,7 @@ static long long g_ep_miss_kind[4], g_ep_stop_off[24];
 static int g_ep_trace = 0;   /* JMME_EPZS_TRACE=1: per-slot miss counts at exit */
 static int g_ep_two_pass = 1;   /* JMME_EPZS_PASS2=0: no second pass (ep_pass2) */
 static int g_ep_dump = 0;       /* JMME_EPZS_DUMP=n: print the first n input misses (measurement) */
+static int g_ep_clk = -1;       /* the wrapper's per-call clock (JMME_PHASES=1 or JMME_EPZS_TRACE=1) */
 
 static int ep_speculating(Macroblock *currMB, int cur_list, int ref, int n_pred)
 {
@@ -2131,9 +2133,12 @@ static const ep_ans *ep_miss(Macroblock *currMB, MEBlock *mv_block, const jmme_e
   {
     int need = 1 + nmb * JMME_NSLOT * EP_REFS * EP_WAYS;   /* at most EP_WAYS guesses per partition and reference */
     ep_grow(need + 1, (need + 1) * EP_MAXP);
-    free(g_ep_idx);
-    g_ep_idx = (int *)malloc((size_t)nmb * JMME_NSLOT * EP_REFS * EP_WAYS * sizeof(int));
-    if (!g_ep_idx) error("jm_gpu_me: out of memory", 500);
+    if (nmb > g_ep_idx_mbs) {   /* (kept across batches: a fresh 250 KB block per batch was malloc / page churn) */
+      free(g_ep_idx);
+      g_ep_idx_mbs = nmb;
+      g_ep_idx = (int *)malloc((size_t)nmb * JMME_NSLOT * EP_REFS * EP_WAYS * sizeof(int));
+      if (!g_ep_idx) error("jm_gpu_me: out of memory", 500);
+    }
     memset(g_ep_idx, 0xff, (size_t)nmb * JMME_NSLOT * EP_REFS * EP_WAYS * sizeof(int));
   }
   g_ep_np = 0;
@@ -2225,7 +2230,11 @@ static distblk epzs_gpu(int variant, Macroblock *currMB, MotionVector *pred_mv, 
     ++g_epzs_cpu;
     return real_epzs(variant, currMB, pred_mv, mv_block, min_mcost, lambda_factor);
   }
-  t0 = now_us();
+  if (g_ep_clk < 0) {   /* per-call clocks only when asked for (two TSC reads a call were ~13 ms per 1080p picture) */
+    const char *ph = getenv("JMME_PHASES"), *tr = getenv("JMME_EPZS_TRACE");
+    g_ep_clk = (ph && ph[0] == '1') || (tr && tr[0] == '1');
+  }
+  t0 = g_ep_clk ? now_us() : 0.0;
   ensure_planes(currMB, list, ref);
   ++g_epzs_calls;
   epzs_ring_sync(p_EPZS, side);
@@ -2350,7 +2359,7 @@ static distblk epzs_gpu(int variant, Macroblock *currMB, MotionVector *pred_mv, 
   }
   mv->mv_x = res.mv_x;
   mv->mv_y = res.mv_y;
-  g_t_epzs += now_us() - t0;
+  if (g_ep_clk) g_t_epzs += now_us() - t0;
   return (distblk)res.cost;
 }
 

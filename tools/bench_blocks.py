@@ -245,7 +245,9 @@ def _lencod(binary, d, tag, yuv, w, h, frames, params, cfg_text, env=None):
         res["epzs"] = dict(gpu_searches=int(g[0]), cpu_searches=int(g[1]), predictors=int(g[2]),
                            pre_stamped_cells=int(g[3]), window_scan_switches=int(g[4]), wrapper_ms=float(g[5]),
                            engine_call_ms=float(g[6]),
-                           us_per_search=round(float(g[5]) * 1e3 / max(1, int(g[0])), 2))
+                           us_per_search=round(float(g[5]) * 1e3 / max(1, int(g[0])), 2) if float(g[5]) > 0 else None)
+        if float(g[5]) == 0:   # (the adapter's per-call clock runs only under JMME_PHASES / JMME_EPZS_TRACE)
+            del res["epzs"]["wrapper_ms"], res["epzs"]["us_per_search"]
     if esp:
         res["epzs_subpel"] = dict(gpu=int(esp.group(1)), chained=int(esp.group(2)), cpu=int(esp.group(3)))
     spec = re.search(r"EPZS speculation: (\d+) searches answered from (\d+) batches \((\d+) guesses\), (\d+) searched "
