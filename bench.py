@@ -259,10 +259,25 @@ def subpel_block(dev, local: int, iters: int = 20) -> dict | None:
     me.close()
     h, w = c.cur[f].shape
     ibytes = w * h + 16 * (w + 64) * (h + 40)
+    # the same kernel on a 2160p reference: with the 1080p point, the launch's
+    # fixed cost and the marginal streaming rate (t = fixed + bytes / rate)
+    h4, w4 = 2160, 3840
+    pic4 = np.random.default_rng(4).integers(0, 256, (h4, w4)).astype(np.uint16)
+    with MotionEstimator({"SourceWidth": w4, "SourceHeight": h4}, device=local) as me4:
+        me4.upload_cur(pic4)
+        me4.upload_ref(0, 0, pic4)
+        ms_i4 = timed(lambda: _lib.check(_lib.lib().jmme_interpolate_ref(me4._ctx, 0, 0, st.cuda_stream)))
+    ibytes4 = w4 * h4 + 16 * (w4 + 64) * (h4 + 40)
+    marginal = (ibytes4 - ibytes) / max((ms_i4 - ms_i) * 1e-3, 1e-9)   # bytes/s
+    fixed_us = (ms_i - ibytes / marginal * 1e3) * 1e3
     return {"workload": "JM 18.5 sub_pel_motion_estimation for one 1080p P-frame (FS +-32, SATD half/quarter-pel)",
             "refinements": int(len(q)), "refine_ms": round(ms_r, 4), "interpolate_ms": round(ms_i, 4),
             "mb_per_s": round((w // 16) * (h // 16) / ((ms_r + ms_i) * 1e-3), 1),
             "interpolate_hbm_frac": round(ibytes / (ms_i * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "interpolate_2160p_ms": round(ms_i4, 4),
+            "interpolate_2160p_hbm_frac": round(ibytes4 / (ms_i4 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "interpolate_marginal_hbm_frac": round(marginal / 1e9 / HBM_PEAK_GBS, 4),
+            "interpolate_fixed_us": round(fixed_us, 2),
             "parity": {"reference": "JM 18.5 lencod (captured)", "refinements": int(len(q)), "bit_exact": exact},
             "jm_me_time_with_subpel": c.meta.get("jm_me_time")}
 
