@@ -1476,6 +1476,7 @@ static long long g_ep_miss_slot[JMME_NSLOT], g_ep_list_diff[JMME_NSLOT];   /* mi
  * outside every equal way's interval, [2] prevSad outside, [3] map cells; and the stop misses by
  * log2 of |real - guessed| (the guess's own stop criterion) */
 static long long g_ep_miss_kind[4], g_ep_stop_off[24];
+static long long g_ep_stop_side[8][2];   /* stop misses by the nearest way's return path, real below / above */
 static int g_ep_trace = 0;   /* JMME_EPZS_TRACE=1: per-slot miss counts at exit */
 static int g_ep_two_pass = 1;   /* JMME_EPZS_PASS2=0: no second pass (ep_pass2) */
 static int g_ep_dump = 0;       /* JMME_EPZS_DUMP=n: print the first n input misses (measurement) */
@@ -1571,7 +1572,7 @@ static const ep_ans *ep_lookup(Macroblock *currMB, MEBlock *mv_block, const jmme
   ep_seen_at(mb, slot, ref)->bt_start = g_ep_bt_start;
   if (!gen || g_ep_gens[ref] != gen || mb < g_ep_mb0 || mb >= g_ep_mb1) return NULL;
   ++g_ep_miss_slot[slot];   /* (taken back below on a hit) */
-  int kind = 0;
+  int kind = 0, stop_path = 0, stop_above = 0;
   int64_t stop_off = -1;
   for (w = 0; w < EP_WAYS; w++) {
     const int k = g_ep_idx[(((size_t)(mb - g_ep_mb0) * JMME_NSLOT + slot) * EP_REFS + ref) * EP_WAYS + w];
@@ -1590,7 +1591,11 @@ static const ep_ans *ep_lookup(Macroblock *currMB, MEBlock *mv_block, const jmme
         const int64_t d = q->stop_crit > a->in.q.stop_crit ? q->stop_crit - a->in.q.stop_crit
                                                            : a->in.q.stop_crit - q->stop_crit;
         if (kind < 1) kind = 1;
-        if (stop_off < 0 || d < stop_off) stop_off = d;
+        if (stop_off < 0 || d < stop_off) {
+          stop_off = d;
+          stop_path = a->res.path;
+          stop_above = q->stop_crit > a->bnd.stop_hi;
+        }
       } else if (q->prev_sad < a->bnd.prev_lo || q->prev_sad > a->bnd.prev_hi) {
         if (kind < 2) kind = 2;
       }
@@ -1650,6 +1655,7 @@ static const ep_ans *ep_lookup(Macroblock *currMB, MEBlock *mv_block, const jmme
     int b = 0;
     while (b < 23 && (stop_off >> b) > 0) ++b;
     ++g_ep_stop_off[b];
+    ++g_ep_stop_side[stop_path >= 0 && stop_path < 8 ? stop_path : 0][stop_above];
   }
   return NULL;
 }
@@ -2508,6 +2514,8 @@ static void report(void)
                       "%lld map cells; stop misses by bits of |real - guessed|:",
               g_ep_miss_kind[0], g_ep_miss_kind[1], g_ep_miss_kind[2], g_ep_miss_kind[3]);
       for (sl = 0; sl < 24; sl++) fprintf(stderr, " %lld", g_ep_stop_off[sl]);
+      fprintf(stderr, "\njm_gpu_me: EPZS stop misses by the nearest way's return path (real below / above its interval):");
+      for (sl = 0; sl < 8; sl++) fprintf(stderr, " %d:%lld/%lld", sl, g_ep_stop_side[sl][0], g_ep_stop_side[sl][1]);
       fprintf(stderr, "\n");
     }
     if (g_epzs_sp_calls || g_epzs_sp_cpu)
