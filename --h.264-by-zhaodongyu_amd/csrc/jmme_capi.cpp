@@ -60,6 +60,22 @@ struct DevGuard {
 
 }  // namespace
 
+#ifndef JMME_CHUNK_STRIPES
+#define JMME_CHUNK_STRIPES 8
+#endif
+// Items dealt to an XCD at a time (the item kernel's chunks, c % 8 -> XCD c).
+// JMME_CHUNK_STRIPES=1: a picture row of macroblocks / 8 when that divides, so
+// that a full frame's chunk c is column stripe c % 8 of its row -- each XCD
+// then serves one stripe of columns top to bottom and its L2 holds the windows
+// of vertical as well as horizontal neighbours; else 16.
+inline int item_chunk(int width, int *rot) {
+  static const int stripes = [] { const char *e = getenv("JMME_CHUNK_STRIPES"); return e ? atoi(e) : JMME_CHUNK_STRIPES; }();
+  const int mbs_x = width / 16;
+  const bool on = stripes && mbs_x >= 8 && mbs_x % 8 == 0;
+  *rot = on && stripes > 1 ? stripes : 0;
+  return on ? mbs_x / 8 : 16;
+}
+
 struct jmme_ctx {
   jmme_config cfg;
   int device = 0;
@@ -621,6 +637,7 @@ int launch(jmme_ctx *ctx, int mode, const uint8_t *d_cur, const uint8_t *const *
   p.counts = ctx->d_counts + ctx->counts_half * kCountWords;
   p.counts_next = ctx->d_counts + (ctx->counts_half ^ 1) * kCountWords;
   p.debug_words = debug_words;
+  p.chunk = item_chunk(w, &p.rot);
 #ifdef JMME_STAMPS
   // n units x 8 words, then 4 words per workgroup (up to kStampWGs)
   const size_t words = (size_t)n * 8 + (size_t)kStampWGs * 4;

@@ -61,6 +61,8 @@ struct KParams {
   uint32_t *debug_words;              // debug: unit 0's first staged window (rows x wp words)
   unsigned long long *stamps;         // diagnostic builds (JMME_STAMPS): per-unit phase clocks
   int hbd;                            // 16-bit planes (pitch in samples): the 64-bit-key v_sad_u16 instance
+  int chunk;                          // item kernel: consecutive items dealt to one XCD (>= 1)
+  int rot;                            // ... the XCD of chunk (8 r + s) is (s - r / rot) mod 8 (0: s)
 };
 // status bits (counts[2]): bit 0 range > lds_range, bit 1 sub-pel centre, bit 2 refine lost a winner
 

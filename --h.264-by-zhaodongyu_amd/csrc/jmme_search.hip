@@ -64,7 +64,6 @@ constexpr int kCostShift = 11;             // key32 = cost << 11 | rank >> 2
 constexpr int kRankDrop = 2;
 constexpr int kCand = 1 << kRankDrop;      // refine candidates per partition
 constexpr int kPlanWaves = 16;             // plan kernel: units per workgroup
-constexpr int kChunk = 16;                 // item kernel: consecutive items dealt to one XCD
 constexpr int kRed1 = (kNS + 3) / 4 * 2;      // reduce: registers after the permlane32 level (22)
 constexpr int kRed2 = kRed1 / 2;              //         ... after the permlane16 level (11)
 
@@ -1812,12 +1811,15 @@ __global__ __launch_bounds__(kWG, KEY32 ? JMME_WAVES_PER_EU : 2) void me_items_k
   const unsigned cnt = (unsigned)p.n + p.counts[0];   // first groups, then the further groups
   const Item *items = p.items;
   const int x = blockIdx.x & 7, lb = blockIdx.x >> 3, nbx = (gridDim.x - x + 7) >> 3;
-  // XCD x's list: the chunks of kChunk consecutive items c with c % 8 == x
+  // XCD x's list: the chunks of p.chunk consecutive items c with c % 8 == x
   // (a chunk's macroblocks are neighbours: their windows overlap in the XCD's
-  // L2); k-th item of the list = list index (k / kChunk * 8 + x) * kChunk + k % kChunk
-  const unsigned rounds = cnt / (8u * kChunk), rest = cnt - rounds * 8u * kChunk;
-  const unsigned end = rounds * kChunk + (unsigned)min(max((int)rest - x * kChunk, 0), kChunk);
-  auto item_at = [&](unsigned k) { return (k / kChunk * 8u + (unsigned)x) * kChunk + k % kChunk; };
+  // L2); k-th item of the list = list index (k / ch * 8 + x) * ch + k % ch
+  const unsigned ch = (unsigned)ufl(p.chunk), rot = (unsigned)ufl(p.rot);
+  // the stripe XCD x serves in round r
+  auto stripe = [&](unsigned r) { return rot ? ((unsigned)x + r / rot) & 7u : (unsigned)x; };
+  const unsigned rounds = cnt / (8u * ch), rest = cnt - rounds * 8u * ch;
+  const unsigned end = rounds * ch + (unsigned)min(max((int)rest - (int)stripe(rounds) * (int)ch, 0), (int)ch);
+  auto item_at = [&](unsigned k) { const unsigned r = k / ch; return (r * 8u + stripe(r)) * ch + k % ch; };
   const unsigned j = (unsigned)lb;
   if (j >= end) return;
   unsigned jn = j + nbx;                                  // the second item (static)
