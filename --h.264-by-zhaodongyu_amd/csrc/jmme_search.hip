@@ -1786,8 +1786,10 @@ __device__ __forceinline__ Item load_item(const Item *items, unsigned j) {
 }
 
 // Persistent item kernel.  The KEY32 instance drains the 32-bit list, the
-// other the 64-bit list.  XCD x (= blockIdx % 8) serves every 8th chunk of 16
-// consecutive items (neighbouring macroblocks' windows overlap in its L2; with
+// other the 64-bit list.  XCD x (= blockIdx % 8) serves every 8th chunk of
+// p.chunk consecutive items -- one eighth of a macroblock row when that
+// divides, the stripes rotating every p.rot rows, else 16 items (neighbouring
+// macroblocks' windows overlap in its L2; with
 // whole eighths of the list instead, the last eighth -- the bottom rows, whose
 // padded, flat blocks defeat the elimination, and all further groups, which
 // the bottom row holds -- made one XCD end 30 us after the others).  Inside
