@@ -282,7 +282,7 @@ def dropin_modes():
             ("EPZS", dict(BASELINE_EPZS), 2))
 
 
-def dropin_block(modes=None, size=(1920, 1080), search_range=32, reps=2, host_procs=None) -> dict | None:
+def dropin_block(modes=None, size=(1920, 1080), search_range=32, reps=3, host_procs=None) -> dict | None:
     """JM 18.5 lencod, stock (CPU) and lencod_jmme (the same JM objects, the ME
     through libjmme) on the same seeded clip: JM's own 'Total ME time' per
     P-frame, and byte identity of bitstream and reconstruction.  The GPU engine is
