@@ -153,6 +153,7 @@ struct jmme_ctx {
   uint32_t srv_seq = 0;
   uint32_t srv_idle_ticks = 200000;          // 2 ms at s_memrealtime's 100 MHz (JMME_EPZS_SERVER_IDLE_US)
   long long srv_launches = 0, srv_served = 0;
+  long long srv_fallbacks = 0;   // requests the server left unserved (2 s without it), launched instead
   double srv_service_us = 0;                 // JMME_PHASES: the server's own time per request, summed
   double srv_host_us[4] = {};                // JMME_PHASES: a search alone on the host -- call entry to the
                                              // server hand-off, hand-off to posted, posted to done, done to return
@@ -438,6 +439,8 @@ extern "C" void jmme_destroy(jmme_ctx *ctx) {
     (void)hipStreamDestroy(ctx->single_stream);
   }
   if (ctx->h_done) (void)hipHostFree(ctx->h_done);
+  if (ctx->srv_fallbacks)   // (always reported: it says the GPU's queues were oversubscribed)
+    fprintf(stderr, "jmme EPZS server: %lld requests not taken within 2 s, launched on their own\n", ctx->srv_fallbacks);
   if (ctx->phases && ctx->srv_launches)
     fprintf(stderr, "jmme EPZS server: %lld searches over %lld launches; %.2f us per search in the server "
             "(request copy %.2f, search to %.2f)\n", ctx->srv_served, ctx->srv_launches,
@@ -1647,9 +1650,15 @@ int epzs_serve(jmme_ctx *ctx, const jmme_epzs_req *d_req, const int16_t *d_preds
       if (start()) return -1;
     }
     if ((spin & 4095u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
-      const int r = server_stop(ctx);   // (surfaces a fault)
-      if (__atomic_load_n(&box->done, __ATOMIC_ACQUIRE) == seq && r == 0) break;
-      return fail("EPZS server: no completion word for request %u", seq);
+      // 2 s without it: on a GPU whose mapped queues are oversubscribed (more
+      // processes' queues than the hardware maps) the server's queue can stay
+      // unmapped that long.  Stop it (surfacing a fault) and, when it left
+      // without the request, hand the request back for an ordinary launch.
+      const int r = server_stop(ctx);
+      if (r) return -1;
+      if (__atomic_load_n(&box->done, __ATOMIC_ACQUIRE) == seq) break;
+      ++ctx->srv_fallbacks;
+      return 1;
     }
     __builtin_ia32_pause();
   }
@@ -1956,13 +1965,19 @@ extern "C" int jmme_epzs_speculate(jmme_ctx *ctx, const jmme_epzs_req *req, int 
     const char *ie = std::getenv("JMME_EPZS_SERVER_IDLE_US");
     if (ie) ctx->srv_idle_ticks = (uint32_t)std::max(1, std::min(1000000, std::atoi(ie))) * 100u;
   }
-  const int mode = fuse ? ctx->single_mode : 0;
+  int mode = fuse ? ctx->single_mode : 0;
   const double t_staged = ctx->phases && n > 1 ? now_us() : 0.0;   // (batches: the copies in are done)
   if (mode != 3 && server_stop(ctx)) return -1;
+  int served = 1;
+  const jmme_block_res spo0 = h_spo ? *h_spo : jmme_block_res{};   // (the server check's input)
   if (mode == 3) {   // the resident server: no launch on the search's path
     ctx->srv_t_call = ep_timer_.t0;
-    const jmme_block_res spo0 = *h_spo;
-    if (epzs_serve(ctx, d_req, d_preds, d_cond, d_stale, d_out, d_vis, max_visited, d_bnd, d_int, one, d_spo)) return -1;
+    const int r = epzs_serve(ctx, d_req, d_preds, d_cond, d_stale, d_out, d_vis, max_visited, d_bnd, d_int, one, d_spo);
+    if (r < 0) return -1;
+    served = r == 0;
+    if (!served) mode = 1;   // (not taken: the fused launch below)
+  }
+  if (mode == 3 && served) {
     if (ctx->srv_check && epzs_serve_check(ctx, h_out, h_bnd, h_vis, h_spo, spo0, max_visited)) return -1;
     std::memcpy(out, h_out, sizeof(jmme_epzs_res));
     std::memcpy(bounds, h_bnd, sizeof(jmme_epzs_bounds));

@@ -715,6 +715,28 @@ def main():
     if args.shard == "encoder":   # before anything touches the GPU: this process only launches encoders
         run_encoder(args, ws, rank, local)
         return
+    # N = 1: the GOP-encoder blocks run first, before this process touches the
+    # GPU.  Its own hardware queues would otherwise join the encoders' (8 x 2)
+    # on the device and oversubscribe the queues the hardware maps: the
+    # encoders' queues are then time-sliced and their resident EPZS servers wait
+    # seconds (profiles/round6/gop_queues/).
+    pre = {}
+    if ws == 1 and args.workload == "me" and args.shard == "gop":
+        import bench_blocks
+        if not args.no_encoder:
+            # the product's multi-GPU form at N = 1: closed GOPs through lencod_jmme
+            # (the same as --shard encoder on one GPU), with the host baseline
+            size = tuple(int(x) for x in args.enc_size.split("x")) if args.enc_size else None
+            pre["encoder_gop"] = bench_blocks.encoder_gop_block(device=local, rank=0, gops=args.enc_gops,
+                                                                gop=args.enc_gop, size=size,
+                                                                per_gpu=args.enc_per_gpu, encoder=args.enc_encoder,
+                                                                preset=args.enc_preset)
+        if not args.no_encoder_4k:
+            # configs[3] as configured: 4K, encoder_baseline.cfg's EPZS keys, RDO on
+            # (--shard encoder --enc-preset epzs4k is the same over N GPUs)
+            pre["encoder_gop_epzs4k"] = bench_blocks.encoder_gop_block(device=local, rank=0, gops=args.enc4k_gops,
+                                                                       gop=2, per_gpu=min(8, args.enc4k_gops),
+                                                                       encoder=args.enc_encoder, preset="epzs4k")
     if ws > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
@@ -864,22 +886,9 @@ def main():
         if not args.no_hybrid and ws == 1:
             import bench_blocks
             line["hybrid"] = bench_blocks.hybrid_block(dev, local, load_workload)
-        if not args.no_encoder and ws == 1:
-            import bench_blocks
-            # the product's multi-GPU form at N = 1: closed GOPs through lencod_jmme
-            # (the same as --shard encoder on one GPU), with the host baseline
-            size = tuple(int(x) for x in args.enc_size.split("x")) if args.enc_size else None
-            line["encoder_gop"] = bench_blocks.encoder_gop_block(device=local, rank=0, gops=args.enc_gops,
-                                                                 gop=args.enc_gop, size=size,
-                                                                 per_gpu=args.enc_per_gpu, encoder=args.enc_encoder,
-                                                                 preset=args.enc_preset)
-        if not args.no_encoder_4k and ws == 1:
-            import bench_blocks
-            # configs[3] as configured: 4K, encoder_baseline.cfg's EPZS keys, RDO on
-            # (--shard encoder --enc-preset epzs4k is the same over N GPUs)
-            line["encoder_gop_epzs4k"] = bench_blocks.encoder_gop_block(device=local, rank=0, gops=args.enc4k_gops,
-                                                                        gop=2, per_gpu=min(8, args.enc4k_gops),
-                                                                        encoder=args.enc_encoder, preset="epzs4k")
+        for k in ("encoder_gop", "encoder_gop_epzs4k"):   # (measured before the GPU was touched, above)
+            if k in pre:
+                line[k] = pre[k]
         if not args.no_f3 and ws == 1:
             import bench_blocks
             # mode decision's inter residual coding from the GPU (off by default in the product)

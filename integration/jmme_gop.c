@@ -158,7 +158,7 @@ static void gop_path(char *buf, size_t n, int gop, const char *suffix)
 /* fork + exec one GOP's encoder on `gpu`; the child's stdout goes to its log */
 static pid_t start_gop(gop_run *r)
 {
-  char start[64], count[64], out[4096], rec[4096], log[4096], dev[32];
+  char start[64], count[64], out[4096], rec[4096], log[4096], errp[4096], dev[32];
   char outp[4200], recp[4200];
   pid_t pid;
   int i, k = 0;
@@ -169,6 +169,7 @@ static pid_t start_gop(gop_run *r)
   gop_path(out, sizeof out, r->gop, ".264");
   gop_path(rec, sizeof rec, r->gop, "_rec.yuv");
   gop_path(log, sizeof log, r->gop, ".log");
+  gop_path(errp, sizeof errp, r->gop, ".err");
   snprintf(outp, sizeof outp, "OutputFile=%s", out);
   snprintf(recp, sizeof recp, "ReconFile=%s", rec);
   snprintf(dev, sizeof dev, "%d", r->gpu < 64 ? g_dev_map[r->gpu] : r->gpu);
@@ -184,6 +185,7 @@ static pid_t start_gop(gop_run *r)
   if (pid == 0) {
     FILE *f = freopen(log, "w", stdout);
     if (!f) _exit(127);
+    if (!freopen(errp, "w", stderr)) _exit(127);   /* the encoder's (and libjmme's) reports, per GOP */
     if (g_pin) {   /* the host cores are fixed before the encoder starts, like the device */
       cpu_set_t set;
       int lo, hi, c;
