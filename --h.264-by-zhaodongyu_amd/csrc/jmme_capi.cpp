@@ -127,6 +127,9 @@ struct jmme_ctx {
   size_t cap_sout = 0;
   jmme_chain_res *h_chres = nullptr;         // jmme_search_mbs_chains results (mapped pinned)
   jmme_block_res *h_chsp = nullptr;          // jmme_search_mbs_chains_sp refinements (mapped pinned)
+  uint32_t *h_chdone = nullptr;              // per chain: the launch's number behind its results (mapped, coherent)
+  void *dv_chdone = nullptr;
+  uint32_t chain_seq = 0;
   void *dv_chsp = nullptr;
   unsigned long long *h_hkeys = nullptr;    // small latency form: per-tile keys (mapped pinned)
   size_t cap_hkeys = 0;
@@ -439,6 +442,7 @@ extern "C" void jmme_destroy(jmme_ctx *ctx) {
     (void)hipStreamDestroy(ctx->single_stream);
   }
   if (ctx->h_done) (void)hipHostFree(ctx->h_done);
+  if (ctx->h_chdone) (void)hipHostFree(ctx->h_chdone);
   if (ctx->srv_fallbacks)   // (always reported: it says the GPU's queues were oversubscribed)
     fprintf(stderr, "jmme EPZS server: %lld requests not taken within 2 s, launched on their own\n", ctx->srv_fallbacks);
   if (ctx->phases && ctx->srv_launches)
@@ -1081,8 +1085,33 @@ int launch_chains(jmme_ctx *ctx, int mode, const jmme_chain *chains, int n, hipS
   p.max_r = max_r;
   p.hbd = ctx->hbd ? 1 : 0;
   p.res = static_cast<jmme_chain_res *>(d_res);
+  if (!ctx->h_chdone) {
+    HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_chdone), kChainInline * sizeof(uint32_t),
+                         hipHostMallocMapped | hipHostMallocCoherent));
+    HIPCHK(hipHostGetDevicePointer(&ctx->dv_chdone, ctx->h_chdone, 0));
+    std::memset(ctx->h_chdone, 0, kChainInline * sizeof(uint32_t));
+  }
+  p.done = static_cast<uint32_t *>(ctx->dv_chdone);
+  p.seq = ++ctx->chain_seq;
   std::memcpy(p.chains, chains, (size_t)n * sizeof(jmme_chain));
   HIPCHK(launch_search_chains(p, s));
+  return 0;
+}
+
+// the chains of the last launch have stored their completion words (polled:
+// a stream synchronisation costs more than the words' PCIe write); 2 s
+// without them, the stream is synchronised instead (surfacing a fault)
+int wait_chains(jmme_ctx *ctx, int n, hipStream_t s) {
+  const uint32_t seq = ctx->chain_seq;
+  auto t0 = std::chrono::steady_clock::now();
+  for (int i = 0; i < n; ++i)
+    for (unsigned spin = 1; __atomic_load_n(&ctx->h_chdone[i], __ATOMIC_ACQUIRE) != seq; ++spin) {
+      if ((spin & 4095u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+        HIPCHK(hipStreamSynchronize(s));
+        if (__atomic_load_n(&ctx->h_chdone[i], __ATOMIC_ACQUIRE) != seq) return fail("chains: no completion word");
+      }
+      __builtin_ia32_pause();
+    }
   return 0;
 }
 }  // namespace
@@ -1106,8 +1135,11 @@ extern "C" int jmme_search_mbs_chains_sp(jmme_ctx *ctx, int mode, const jmme_mb_
   phase(ctx, 0, &t_ph);
   const int rc = n ? jmme_search_mbs(ctx, mode, req, n, out) : 0;
   if (ctx->phases) t_ph = now_us();
-  HIPCHK(hipStreamSynchronize(ctx->chain_stream));
-  if (rc) return rc;
+  if (rc) {
+    (void)hipStreamSynchronize(ctx->chain_stream);
+    return rc;
+  }
+  if (wait_chains(ctx, n_chains, ctx->chain_stream)) return -1;
   std::memcpy(res, ctx->h_chres, (size_t)n_chains * JMME_CHAIN_MAX_STEPS * sizeof(jmme_chain_res));
   if (sp) std::memcpy(sp_res, ctx->h_chsp, (size_t)n_chains * JMME_CHAIN_MAX_STEPS * sizeof(jmme_block_res));
   phase(ctx, 5, &t_ph);

@@ -123,6 +123,8 @@ struct ChainParams {
   int sub_pitch;
   size_t plane_stride;
   jmme_block_res *sp_res;           // [n][JMME_CHAIN_MAX_STEPS] (host-mapped)
+  uint32_t *done;                   // [n] (host-mapped): chain i stores seq behind its last result (or nullptr)
+  uint32_t seq;
   jmme_chain chains[kChainInline];
   jmme_subpel_req sp[kChainInline]; // per chain: the SubPelME parameters
 };

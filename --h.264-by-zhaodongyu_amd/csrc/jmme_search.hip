@@ -2545,6 +2545,12 @@ __global__ __launch_bounds__(kChainWG) void chain_kernel(ChainParams p) {
 #pragma unroll
     for (int k = 0; k < JMME_CHAIN_MAX_STEPS; ++k)
       if (k < n_steps) out[k] = res[k];
+    // the host polls this word instead of synchronising the stream: every
+    // result of this chain (written by this thread) is visible before it
+    if (p.done) {
+      __threadfence_system();
+      __hip_atomic_store(p.done + blockIdx.x, p.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
   }
   CPROF(18);
 #ifdef JMME_CHAIN_PROF
