@@ -74,3 +74,24 @@ def test_16bit_item_kernels_without_scratch(tmp_path):
             assert kernels[name][".private_segment_fixed_size"] == 0, name
             if key32:
                 assert kernels[name][".vgpr_count"] <= 128, (name, kernels[name][".vgpr_count"])
+
+
+def test_headline_kernel_sgpr_spills_pinned(tmp_path):
+    """the headline instance's SGPR spills (lane spills: the current macroblock's 64
+    SGPRs beside the item loop's state, restored by v_readlane after each item's
+    sweep) stay at today's count and never become VGPR spills"""
+    k = _kernel_metadata(tmp_path)["_ZN4jmme12_GLOBAL__N_115me_items_kernelILb1ELb0ELb0ELi32EEEvNS_7KParamsE"]
+    assert k[".vgpr_spill_count"] == 0, k[".vgpr_spill_count"]
+    assert k[".sgpr_spill_count"] <= 72, k[".sgpr_spill_count"]   # (66 before the stripe dealing's state)
+
+
+def test_interpolation_kernel_budget(tmp_path, monkeypatch):
+    """getSubImagesLuma's 8-bit kernel: no spills, no scratch, <= 64 VGPRs (8 waves/SIMD possible)"""
+    global OBJ
+    monkeypatch.setattr(__import__(__name__), "OBJ", os.path.join(os.path.dirname(OBJ), "jmme_subpel.o"))
+    kernels = _kernel_metadata(tmp_path)
+    hits = [v for n, v in kernels.items() if "sub_images_kernel" in n and "IhE" in n]
+    assert len(hits) == 1, sorted(kernels)
+    k = hits[0]
+    assert k[".private_segment_fixed_size"] == 0 and k[".vgpr_spill_count"] == 0 and k[".sgpr_spill_count"] == 0, k
+    assert k[".vgpr_count"] <= 64, k[".vgpr_count"]
