@@ -393,6 +393,7 @@ static void slot_geometry(void);
 static long long g_chain_sent = 0, g_chain_steps = 0, g_chain_hits = 0, g_chain_head_bad = 0;
 static long long g_chain_calls = 0, g_chain_call_fail = 0;
 static double g_t_chain = 0, g_t_sp = 0;   /* ms in chain-only calls / sub-pel batches (reported at exit) */
+static double g_t_sp_part[3];               /* sub-pel batches: building, the library call, storing (us) */
 static int g_chain_only = -1;   /* JMME_CHAIN_ONLY=0: a failed guess always re-batches */
 static int8_t g_grp[19][4], g_grp_n[19], g_slot_grp[JMME_NSLOT], g_slot_idx[JMME_NSLOT];
 
@@ -990,6 +991,23 @@ static void sp_fill(jmme_subpel_req *q, int mb, int s, int list, int ref, const 
 /* one batched refinement: the calling block with its real inputs (answer kept
  * in way KHYP) and, for the macroblocks the integer cache covers, every cached
  * integer answer of every slot (way k for integer way k) */
+/* the batch buffers for `count` requests (touched: the pages are faulted in here) */
+static void sp_reserve(int count)
+{
+  if (count <= g_sreq_cap) return;
+  free(g_sreq);
+  free(g_sres);
+  free(g_sp_dst);
+  g_sreq = (jmme_subpel_req *)malloc((size_t)count * sizeof(jmme_subpel_req));
+  g_sres = (jmme_block_res *)malloc((size_t)count * sizeof(jmme_block_res));
+  g_sp_dst = (int *)malloc((size_t)count * sizeof(int));
+  if (!g_sreq || !g_sres || !g_sp_dst) error("jm_gpu_me: out of memory", 500);
+  memset(g_sreq, 0, (size_t)count * sizeof(jmme_subpel_req));
+  memset(g_sres, 0, (size_t)count * sizeof(jmme_block_res));
+  memset(g_sp_dst, 0, (size_t)count * sizeof(int));
+  g_sreq_cap = count;
+}
+
 static void sp_batch(int list, int ref, int mb0, int s0, const sp_ent *w, int t8)
 {
   const spec_ent *itab = g_spec[list][ref];
@@ -998,46 +1016,63 @@ static void sp_batch(int list, int ref, int mb0, int s0, const sp_ent *w, int t8
   int count = (mb1 - mb0) * JMME_NSLOT * KHYP + 1;
   double t0 = now_us();
   if (!g_slot_bt[0]) slot_geometry();
-  if (count > g_sreq_cap) {
-    free(g_sreq);
-    free(g_sres);
-    free(g_sp_dst);
-    g_sreq = (jmme_subpel_req *)malloc((size_t)count * sizeof(jmme_subpel_req));
-    g_sres = (jmme_block_res *)malloc((size_t)count * sizeof(jmme_block_res));
-    g_sp_dst = (int *)malloc((size_t)count * sizeof(int));
-    if (!g_sreq || !g_sres || !g_sp_dst) error("jm_gpu_me: out of memory", 500);
-    g_sreq_cap = count;
-  }
+  sp_reserve(count);
   sp_fill(&g_sreq[n], mb0, s0, list, ref, w);
   g_sp_dst[n++] = (int)sp_idx(mb0, s0, KHYP);
-  for (mb = mb0; mb < mb1; mb++)
-    for (k = 0; k < KHYP; k++)          /* (both tables way-major: slots innermost walk memory in order) */
-      for (s = 0; s < JMME_NSLOT; s++) {
-        const spec_ent *ie = &itab[spec_idx(mb, s, k)];
-        sp_ent g = *w;
-        if (ie->valid != g_slot_gen[list][ref]) continue;
-        g.px = ie->px;
-        g.py = ie->py;
-        g.mx = ie->mvx;
-        g.my = ie->mvy;
-        g.min_mcost = w->start_hp ? ie->cost : JMME_DISTBLK_MAX;
-        /* test8x8 as mv_search.c:1630,1770 set it: Transform8x8Mode on block types 1..4 */
-        g.flags = (uint8_t)((w->flags & JMME_SP_CHECK0) | (t8 && g_slot_bt[s] <= 4 ? JMME_SP_TEST8x8 : 0));
-        sp_fill(&g_sreq[n], mb, s, list, ref, &g);
-        g_sp_dst[n++] = (int)sp_idx(mb, s, k);
+  {
+    /* the guesses: this call's request with each cached integer answer's block,
+     * predictor, vector and cost (the fields every guess shares filled once) */
+    const unsigned gen = g_slot_gen[list][ref];
+    jmme_subpel_req tq;
+    uint8_t sflags[JMME_NSLOT];
+    sp_fill(&tq, mb0, 0, list, ref, w);
+    for (s = 0; s < JMME_NSLOT; s++)   /* test8x8 as mv_search.c:1630,1770 set it: Transform8x8Mode on types 1..4 */
+      sflags[s] = (uint8_t)((w->flags & JMME_SP_CHECK0) | (t8 && g_slot_bt[s] <= 4 ? JMME_SP_TEST8x8 : 0));
+    for (mb = mb0; mb < mb1; mb++) {
+      const int16_t bx0 = (int16_t)((mb % g_mbs_x) * 16), by0 = (int16_t)((mb / g_mbs_x) * 16);
+      for (k = 0; k < KHYP; k++) {      /* (both tables way-major: slots innermost walk memory in order) */
+        const spec_ent *ie = &itab[spec_idx(mb, 0, k)];
+        for (s = 0; s < JMME_NSLOT; s++, ie++) {
+          jmme_subpel_req *q;
+          if (ie->valid != gen) continue;
+          q = &g_sreq[n];
+          *q = tq;
+          q->pos_x = (int16_t)(bx0 + g_slot_bx[s]);
+          q->pos_y = (int16_t)(by0 + g_slot_by[s]);
+          q->blocktype = (int16_t)g_slot_bt[s];
+          q->pred_x = ie->px;
+          q->pred_y = ie->py;
+          q->mv_x = ie->mvx;
+          q->mv_y = ie->mvy;
+          q->min_mcost = w->start_hp ? ie->cost : JMME_DISTBLK_MAX;
+          q->flags = sflags[s];
+          g_sp_dst[n++] = (int)sp_idx(mb, s, k);
+        }
       }
-  if (jmme_subpel_refine(g_me, g_sreq, n, g_sres)) fail_jm("jmme_subpel_refine");
-  for (i = 0; i < n; i++) {
-    const jmme_subpel_req *q = &g_sreq[i];
-    sp_ent *e = &tab[g_sp_dst[i]];
-    e->px = q->pred_x; e->py = q->pred_y; e->mx = q->mv_x; e->my = q->mv_y;
-    e->min_mcost = q->min_mcost; e->lam_h = q->lambda_h; e->lam_q = q->lambda_q;
-    e->metric_h = q->metric_h; e->metric_q = q->metric_q; e->start_hp = q->start_hp; e->start_qp = q->start_qp;
-    e->pos2 = q->search_pos2; e->pos4 = q->search_pos4; e->flags = q->flags;
-    e->omx = g_sres[i].mv_x; e->omy = g_sres[i].mv_y; e->cost = g_sres[i].cost;
-    e->valid = g_slot_gen[list][ref];
+    }
+  }
+  {
+    const double t1 = now_us();
+    g_t_sp_part[0] += t1 - t0;
+    if (jmme_subpel_refine(g_me, g_sreq, n, g_sres)) fail_jm("jmme_subpel_refine");
+    g_t_sp_part[1] += now_us() - t1;
+  }
+  const double t2 = now_us();
+  {
+    /* every request of the batch shares the call's lambdas, metrics and switches */
+    sp_ent te = *w;
+    te.valid = g_slot_gen[list][ref];
+    for (i = 0; i < n; i++) {
+      const jmme_subpel_req *q = &g_sreq[i];
+      sp_ent *e = &tab[g_sp_dst[i]];
+      *e = te;
+      e->px = q->pred_x; e->py = q->pred_y; e->mx = q->mv_x; e->my = q->mv_y;
+      e->min_mcost = q->min_mcost; e->flags = q->flags;
+      e->omx = g_sres[i].mv_x; e->omy = g_sres[i].mv_y; e->cost = g_sres[i].cost;
+    }
   }
   ++g_sp_batches;
+  g_t_sp_part[2] += now_us() - t2;
   g_t_sp += now_us() - t0;
 }
 
@@ -1065,7 +1100,10 @@ static void prefault_tables(VideoParameters *p_Vid, InputParameters *p_Inp)
   spec_table(p_Vid, 0, 0);
   memset(g_spec[0][0], 0, (size_t)g_n_mb * JMME_NSLOT * KWAYS * sizeof(spec_ent));
   memset(g_seen[0][0], 0, (size_t)g_n_mb * JMME_NSLOT * sizeof(spec_ent));
-  if (!p_Inp->DisableSubpelME[0]) sp_table(p_Vid, 0, 0);
+  if (!p_Inp->DisableSubpelME[0]) {
+    sp_table(p_Vid, 0, 0);
+    sp_reserve(g_n_mb * JMME_NSLOT * KHYP + 1);   /* a sub-pel batch over the whole picture at most */
+  }
 }
 
 /* lambda_factor[H_PEL] / [Q_PEL] of the F_PEL lambdas seen in sub-pel calls
@@ -2469,7 +2507,9 @@ static void report(void)
                     "batches, the rest one call each; %lld on the CPU (non-SAD or weighted metric)\n",
             g_calls, g_hits + g_batches + g_chain_calls - g_chain_call_fail, g_batches, g_cpu_calls);
     fprintf(stderr, "jm_gpu_me: %lld sub-pel refinements: %lld cached, %lld batches, %lld on the CPU; "
-                    "%.1f ms in sub-pel batches\n", g_sp_calls, g_sp_hits, g_sp_batches, g_sp_cpu, g_t_sp * 1e-3);
+                    "%.1f ms in sub-pel batches (building %.1f, in the library %.1f, storing %.1f)\n", g_sp_calls,
+              g_sp_hits, g_sp_batches, g_sp_cpu, g_t_sp * 1e-3, g_t_sp_part[0] * 1e-3, g_t_sp_part[1] * 1e-3,
+              g_t_sp_part[2] * 1e-3);
     if (g_batches) {
       int s;
       fprintf(stderr, "jm_gpu_me: integer batches: %lld past the batch, %lld failed guesses; %lld units; "
