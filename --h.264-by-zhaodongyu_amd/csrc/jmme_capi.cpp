@@ -2579,7 +2579,13 @@ extern "C" int jmme_reserve(jmme_ctx *ctx, int max_units) {
   const size_t n = (size_t)max_units;
   if (ensure_units(ctx, n) || ensure_items(ctx, n * JMME_NSLOT)) return -1;
   const size_t rq = align64(n * sizeof(jmme_mb_req)), rs = align64(n * JMME_NSLOT * sizeof(jmme_block_res));
-  if (ensure_pin(ctx, rq + rs + 64)) return -1;
+  size_t pin = rq + rs + 64;
+  if (!ctx->cfg.DisableSubpelME) {   // jmme_subpel_refine's [requests | outputs] for n * JMME_NSLOT refinements
+    const size_t nsp = n * JMME_NSLOT, sp = align64(nsp * sizeof(jmme_subpel_req)) + nsp * sizeof(jmme_block_res);
+    if (ensure_sp(ctx, sp)) return -1;
+    pin = std::max(pin, sp);
+  }
+  if (ensure_pin(ctx, pin)) return -1;
   // the configured picture's planes: the staging buffer and device planes for
   // the current picture and every reference of list 0, taken by the first uploads
   const int w = ctx->cfg.SourceWidth, h = ctx->cfg.SourceHeight;

@@ -212,7 +212,9 @@ int jmme_set_small_batch_limit(jmme_ctx *ctx, int max_workgroups);
 int jmme_prepare(jmme_ctx *ctx);
 /* Size the synchronous batch path's device and pinned host buffers for batches
  * of up to `max_units` units now (they otherwise grow on demand, each growth a
- * device allocation inside some search call).  Optional. */
+ * device allocation inside some search call) -- and, unless the configuration
+ * has DisableSubpelME, jmme_subpel_refine's for batches of max_units *
+ * JMME_NSLOT refinements.  Optional. */
 int jmme_reserve(jmme_ctx *ctx, int max_units);
 
 /* Device-resident variant for pipelines and the benchmark: d_req/d_out are
