@@ -184,17 +184,21 @@ def _oracle_units(cur, ref, req):
     return keys, mv, cost
 
 
-@pytest.mark.parametrize("size,R", [((3840, 2160), 32), ((1920, 1088), 16), ((352, 288), 44), ((176, 144), 0)])
-def test_random_requests_vs_oracle(size, R, gpu):
+@pytest.mark.parametrize("size,R,n", [((3840, 2160), 32, 24), ((1920, 1088), 16, 24), ((352, 288), 44, 24),
+                                      ((176, 144), 0, 24), ((256, 64), 16, 200), ((128, 48), 8, 150)])
+def test_random_requests_vs_oracle(size, R, n, gpu):
     """Inputs no JM run produced (4K, unusual ranges, centres far outside the
-    picture, mixed windows per MB): HIP == oracle on every partition."""
+    picture, mixed windows per MB): HIP == oracle on every partition.  The
+    narrow pictures (16 and 8 macroblocks a row) deal items to the XCDs in
+    column stripes of 2 and 1 items rotating every 8 rounds, over many rounds
+    and a partial last one: every unit must still be served exactly once."""
     from jmme import FULL_SEARCH, MotionEstimator
     from jmme import synth
     w, h = size
     rng = np.random.default_rng(R + w)
     luma = synth.luma_sequence(w, h, 2, seed=w + R, gmv=(3, -2))
     cur, ref = luma[1], luma[0]
-    req = _random_units(rng, w, h, 24, R)
+    req = _random_units(rng, w, h, n, R)
     with MotionEstimator({"SearchRange": max(R, 1), "SearchMode": -1}) as me:
         me.upload_cur(cur)
         me.upload_ref(0, 0, ref)
